@@ -1,0 +1,267 @@
+/*
+ * trajopt_hip.h — C-ABI of the MI355X batched SQP trajectory optimizer.
+ *
+ * This is the drop-in boundary between the host layer that mirrors trajopt's
+ * plugin surface (ProblemConstructionInfo / TermInfo::hatch / sco::Model /
+ * BasicTrustRegionSQP) and the HIP kernels that run the sequential convex
+ * optimisation inner loop for a whole batch of structurally identical problems.
+ *
+ * Plain C: fixed-size structs, plain pointers and sizes, no torch / HIP types
+ * in any signature (the stream is passed as an opaque void*).  Every entry point
+ * returns 0 on success and a negative THIP_E* code on failure; no exception
+ * crosses the ABI.  thip_last_error() gives the message.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference tree):
+ *   thip_create / thip_upload   <- trajopt::ConstructProblem(pci) + TrajOptProb ctor
+ *                                   (trajopt/src/problem_description.cpp:414-598) and
+ *                                   OptProb::createVariables (trajopt_sco/src/modeling.cpp:181-198):
+ *                                   the batch of problems is lowered once into SoA device buffers.
+ *   thip_sqp_run                <- sco::BasicTrustRegionSQP::optimize
+ *                                   (trajopt_sco/src/optimizers.cpp:699-991), the whole penalty /
+ *                                   SQP / trust-region loop, device-resident, one workgroup per problem.
+ *   thip_linearize              <- the convexify step of that loop for CartPose + JointVel terms:
+ *                                   CartPoseErrCalculator / CartPoseJacCalculator
+ *                                   (trajopt/src/kinematic_terms.cpp:252-370) and
+ *                                   JointVelEqCost::convex (trajopt/src/trajectory_costs.cpp:296-301).
+ *   thip_qp_solve               <- sco::OSQPModel::optimize (trajopt_sco/src/osqp_interface.cpp:440-615):
+ *                                   one OSQP-1.0-semantics solve (Ruiz scaling, ADMM, adaptive rho,
+ *                                   polish) of the convexified QP of every problem at a given x.
+ *   thip_download               <- OptResults (trajopt_sco/include/trajopt_sco/optimizers.hpp:40-59).
+ *
+ * Data layout: every per-problem array is problem-major and row-major inside a
+ * problem: trajectories are [batch][n_steps][n_dof] (the reference's
+ * x[t*D + j] layout, problem_description.cpp:557-598), poses are 3x4 row-major
+ * [R | t] blocks of 12 doubles.
+ */
+#ifndef TRAJOPT_HIP_H
+#define TRAJOPT_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define THIP_MAX_DOF 8
+#define THIP_MAX_LINKS 24
+#define THIP_MAX_STEPS 64
+#define THIP_MAX_CART 64
+#define THIP_MAX_SPHERES 32
+#define THIP_MAX_PRIMS 16
+
+/* error codes */
+#define THIP_OK 0
+#define THIP_E_INVALID (-1)
+#define THIP_E_HIP (-2)
+#define THIP_E_NOMEM (-3)
+#define THIP_E_STATE (-4)
+
+/* joint types (URDF) */
+#define THIP_JOINT_FIXED 0
+#define THIP_JOINT_REVOLUTE 1
+#define THIP_JOINT_CONTINUOUS 2
+#define THIP_JOINT_PRISMATIC 3
+
+/* sco::OptStatus (trajopt_sco/include/trajopt_sco/optimizers.hpp:25-33) */
+#define THIP_OPT_CONVERGED 0
+#define THIP_OPT_SCO_ITERATION_LIMIT 1
+#define THIP_OPT_PENALTY_ITERATION_LIMIT 2
+#define THIP_OPT_TIME_LIMIT 3
+#define THIP_OPT_FAILED 4
+#define THIP_OPT_INVALID 5
+
+/* sco::CvxOptStatus (trajopt_sco/include/trajopt_sco/solver_interface.hpp:40-45) */
+#define THIP_CVX_SOLVED 0
+#define THIP_CVX_INFEASIBLE 1
+#define THIP_CVX_FAILED 2
+
+/* scene primitive types (collision, config C) */
+#define THIP_PRIM_SPHERE 0
+#define THIP_PRIM_BOX 1
+#define THIP_PRIM_CAPSULE 2
+
+/* Serial kinematic chain (the tesseract JointGroup of the reference, restated):
+ * link 0 is the chain root (static, world pose = base_pose); link k >= 1 hangs
+ * off link k-1 through joint k with a fixed origin transform followed by the
+ * joint motion about/along `joint_axis` (expressed in the joint frame). */
+typedef struct thip_chain {
+  int n_links;
+  int n_dof;
+  double base_pose[12];
+  int joint_type[THIP_MAX_LINKS];
+  int joint_dof[THIP_MAX_LINKS];          /* dof index for movable joints, -1 for fixed */
+  double joint_origin[THIP_MAX_LINKS][12];
+  double joint_axis[THIP_MAX_LINKS][3];
+  double lower[THIP_MAX_DOF];             /* joint limits -> variable bounds */
+  double upper[THIP_MAX_DOF];
+} thip_chain;
+
+/* sco::BasicTrustRegionSQPParameters (optimizers.hpp:92-135), numeric members only */
+typedef struct thip_sqp_params {
+  double improve_ratio_threshold;   /* 0.25 */
+  double min_trust_box_size;        /* 1e-4 */
+  double min_approx_improve;        /* 1e-4 */
+  double min_approx_improve_frac;   /* -DBL_MAX */
+  int max_iter;                     /* 50 */
+  double trust_shrink_ratio;        /* 0.1 */
+  double trust_expand_ratio;        /* 1.5 */
+  double cnt_tolerance;             /* 1e-4 */
+  double max_merit_coeff_increases; /* 5 */
+  int max_qp_solver_failures;       /* 3 */
+  double merit_coeff_increase_ratio;/* 10 */
+  double initial_merit_error_coeff; /* 10 */
+  int inflate_constraints_individually; /* 1 */
+  double trust_box_size;            /* 0.1 */
+} thip_sqp_params;
+
+/* OSQP settings as configured by OSQPModelConfig::setDefaultOSQPSettings
+ * (trajopt_sco/src/osqp_interface.cpp:78-90) on top of OSQP 1.0 defaults. */
+typedef struct thip_osqp_settings {
+  double rho;            /* 0.1 */
+  double sigma;          /* 1e-6 */
+  double alpha;          /* 1.6 */
+  int scaling;           /* 10 */
+  int adaptive_rho;      /* 1 (iteration based) */
+  int adaptive_rho_interval; /* 0 -> 4 * check_termination */
+  double adaptive_rho_tolerance; /* 5 */
+  int max_iter;          /* 8192 */
+  double eps_abs;        /* 1e-4 */
+  double eps_rel;        /* 1e-6 */
+  double eps_prim_inf;   /* 1e-4 */
+  double eps_dual_inf;   /* 1e-4 */
+  int check_termination; /* 25 */
+  int warm_starting;     /* 1 */
+  int polishing;         /* 1 */
+  double delta;          /* 1e-6 */
+  int polish_refine_iter;/* 3 */
+} thip_osqp_settings;
+
+/* The structure shared by every problem of a batch: chain, horizon, term
+ * tables (the lowered TermInfo list), solver parameters.  Per-problem data
+ * (initial trajectory, CartPose target poses, scene primitives) is uploaded
+ * separately, batched. */
+typedef struct thip_problem_desc {
+  int n_steps;
+  thip_chain chain;
+
+  /* fixed_timesteps: x[t, :] == init[t, :] as persistent model equalities
+   * (problem_description.cpp:489-510) */
+  int n_fixed;
+  int fixed_steps[THIP_MAX_STEPS];
+
+  /* JointVelTermInfo as a cost, zero tolerances -> JointVelEqCost
+   * (problem_description.cpp:1216-1391, trajectory_costs.cpp:257-301) */
+  int jv_enabled;
+  int jv_first_step;
+  int jv_last_step;
+  double jv_coeffs[THIP_MAX_DOF];
+  double jv_targets[THIP_MAX_DOF];
+
+  /* CartPoseTermInfo (problem_description.cpp:919-1005): source = chain link
+   * (active) with source offset, target = static chain root frame with a
+   * per-problem target offset pose. is_cnt: 0 = ABS cost, 1 = EQ constraint. */
+  int n_cart;
+  int cart_step[THIP_MAX_CART];
+  int cart_is_cnt[THIP_MAX_CART];
+  int cart_source_link[THIP_MAX_CART];
+  double cart_source_offset[THIP_MAX_CART][12];
+  double cart_pos_coeffs[THIP_MAX_CART][3];
+  double cart_rot_coeffs[THIP_MAX_CART][3];
+
+  /* CollisionTermInfo, LVS_DISCRETE cost (collision_terms.cpp:737-906,1267-1306):
+   * robot collision model = spheres rigidly attached to chain links; the scene
+   * is per problem (n_prims primitives of 16 doubles each, see THIP_PRIM_*). */
+  int coll_enabled;
+  int coll_is_cnt;
+  int coll_first_step;
+  int coll_last_step;
+  int coll_n_fixed;
+  int coll_fixed_steps[THIP_MAX_STEPS];
+  double coll_margin;      /* dist_pen */
+  double coll_coeff;       /* coeffs */
+  double coll_buffer;      /* collision_margin_buffer */
+  double coll_lvs;         /* longest_valid_segment_length */
+  int n_spheres;
+  int sphere_link[THIP_MAX_SPHERES];
+  double sphere_center[THIP_MAX_SPHERES][3];  /* in link frame */
+  double sphere_radius[THIP_MAX_SPHERES];
+  int n_prims;
+
+  thip_sqp_params sqp;
+  thip_osqp_settings osqp;
+} thip_problem_desc;
+
+/* Per-problem results (sco::OptResults + counters the build adds). */
+typedef struct thip_result {
+  int status;         /* THIP_OPT_* */
+  int n_sqp_iters;    /* executed SQP iterations (outer-loop bodies, all penalty rounds) */
+  int n_qp_solves;    /* OptResults::n_qp_solves */
+  int n_func_evals;   /* OptResults::n_func_evals */
+  long long n_admm_iters; /* ADMM iterations summed over QP solves */
+  int n_merit_increases;
+  double total_cost;  /* OptResults::total_cost */
+  double max_cnt_viol;/* max over constraints of the violation (0 if none) */
+  double final_trust_box;
+  int n_costs;
+  int n_cnts;
+} thip_result;
+
+typedef struct thip_ctx thip_ctx;
+
+/* Fill defaults (reference default parameters). */
+void thip_default_sqp_params(thip_sqp_params* p);
+void thip_default_osqp_settings(thip_osqp_settings* s);
+
+/* Validate the descriptor and allocate device buffers for `batch` problems on
+ * HIP device `device`. */
+int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx** out);
+
+/* Use this HIP stream (hipStream_t passed as void*; NULL = the ctx's own). */
+int thip_set_stream(thip_ctx* ctx, void* stream);
+
+/* H2D copy of per-problem inputs:
+ *   init_traj    [batch][n_steps][n_dof]
+ *   cart_targets [batch][n_cart][12]     target-frame offset poses (may be NULL if n_cart == 0)
+ *   scene        [batch][n_prims][16]    primitive records (may be NULL if n_prims == 0)  */
+int thip_upload(thip_ctx* ctx, const double* init_traj, const double* cart_targets, const double* scene);
+
+/* Device-to-device variant: pointers are device pointers (e.g. torch tensors). */
+int thip_upload_device(thip_ctx* ctx, const double* d_init_traj, const double* d_cart_targets,
+                       const double* d_scene);
+
+/* Run BasicTrustRegionSQP::optimize for every problem (asynchronous on the
+ * ctx stream). */
+int thip_sqp_run(thip_ctx* ctx);
+
+/* Convexify at trajectory x [batch][n_steps][n_dof] (host pointer): CartPose
+ * error rows and forward-difference Jacobians, exactly as the SQP loop does.
+ *   err [batch][n_cart][6]   (rows of indices with zero coeff are 0)
+ *   jac [batch][n_cart][6][n_dof]
+ * Synchronous. */
+int thip_linearize(thip_ctx* ctx, const double* x, double* err, double* jac);
+
+/* Forward kinematics of every chain link at x: poses [batch][n_steps][n_links][12]. Synchronous. */
+int thip_fwd_kin(thip_ctx* ctx, const double* x, double* poses);
+
+/* Copy results back (synchronises the stream):
+ *   x       [batch][n_steps][n_dof]  final trajectory
+ *   results [batch]                  (may be NULL) */
+int thip_download(thip_ctx* ctx, double* x, thip_result* results);
+
+/* Device pointer of the final trajectories (valid until destroy). */
+const double* thip_device_x(thip_ctx* ctx);
+
+/* Per-launch timing of the last thip_sqp_run, measured with HIP events on the
+ * ctx stream around the fused kernel (milliseconds). */
+double thip_last_kernel_ms(thip_ctx* ctx);
+
+void thip_destroy(thip_ctx* ctx);
+const char* thip_last_error(thip_ctx* ctx);
+
+/* Version / build info string. */
+const char* thip_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TRAJOPT_HIP_H */

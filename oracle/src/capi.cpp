@@ -1,0 +1,165 @@
+// ORACLE — test infrastructure only (see sco_expr.hpp header).
+//
+// C entry points of the CPU oracle, loaded (ctypes) only by tests/,
+// __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+#include <atomic>
+#include <cstring>
+#include <exception>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "terms.hpp"
+
+using namespace orc;
+
+namespace
+{
+thread_local std::string g_err;
+
+void solveOne(const thip_problem_desc* d, const double* init, const double* targets, const double* scene,
+              double* out_x, thip_result* res)
+{
+  const int N = d->n_steps, D = d->chain.n_dof;
+  TrajProblem tp = constructProblem(*d, init, targets, scene);
+  BasicTrustRegionSQP opt(tp.prob);
+  opt.getParameters() = toSqpParams(d->sqp);
+  opt.initialize(tp.init);
+  opt.optimize();
+  const OptResults& r = opt.results();
+  std::memcpy(out_x, r.x.data(), sizeof(double) * static_cast<std::size_t>(N * D));
+  if (res)
+  {
+    std::memset(res, 0, sizeof(*res));
+    res->status = static_cast<int>(r.status);
+    res->n_sqp_iters = r.n_sqp_iters;
+    res->n_qp_solves = r.n_qp_solves;
+    res->n_func_evals = r.n_func_evals;
+    res->n_admm_iters = r.n_admm_iters;
+    res->n_merit_increases = r.n_merit_increases;
+    res->total_cost = r.total_cost;
+    res->max_cnt_viol = r.cnt_viols.empty() ? 0.0 : vecMax(r.cnt_viols);
+    res->final_trust_box = opt.getParameters().trust_box_size;
+    res->n_costs = static_cast<int>(r.cost_vals.size());
+    res->n_cnts = static_cast<int>(r.cnt_viols.size());
+  }
+}
+}  // namespace
+
+extern "C" {
+
+const char* oracle_last_error() { return g_err.c_str(); }
+
+// BasicTrustRegionSQP::optimize over a batch, problems spread over n_threads.
+int oracle_solve_batch(const thip_problem_desc* d, int batch, const double* init, const double* targets,
+                       const double* scene, double* out_x, thip_result* res, int n_threads)
+{
+  const int N = d->n_steps, D = d->chain.n_dof;
+  std::atomic<int> next{ 0 };
+  std::atomic<int> failed{ 0 };
+  std::string first_err;
+  std::mutex err_mu;
+  auto worker = [&]() {
+    for (;;)
+    {
+      const int b = next.fetch_add(1);
+      if (b >= batch)
+        break;
+      try
+      {
+        solveOne(d, init + static_cast<std::size_t>(b) * N * D,
+                 targets ? targets + static_cast<std::size_t>(b) * d->n_cart * 12 : nullptr,
+                 scene ? scene + static_cast<std::size_t>(b) * d->n_prims * 16 : nullptr,
+                 out_x + static_cast<std::size_t>(b) * N * D, res ? res + b : nullptr);
+      }
+      catch (const std::exception& e)
+      {
+        failed.fetch_add(1);
+        std::lock_guard<std::mutex> lk(err_mu);
+        if (first_err.empty())
+          first_err = e.what();
+      }
+    }
+  };
+  if (n_threads <= 1)
+    worker();
+  else
+  {
+    std::vector<std::thread> th;
+    for (int i = 0; i < n_threads; ++i)
+      th.emplace_back(worker);
+    for (auto& t : th)
+      t.join();
+  }
+  if (failed.load())
+  {
+    g_err = first_err;
+    return -1;
+  }
+  return 0;
+}
+
+// CartPose error rows + FD jacobians at x for every CartPose term:
+//   err [batch][n_cart][6], jac [batch][n_cart][6][n_dof]; rows in hatch order
+//   (indices with |coeff| > 1e-5), unused rows zero.
+int oracle_linearize(const thip_problem_desc* d, int batch, const double* x, const double* targets, double* err,
+                     double* jac)
+{
+  const int N = d->n_steps, D = d->chain.n_dof;
+  for (int b = 0; b < batch; ++b)
+    for (int k = 0; k < d->n_cart; ++k)
+    {
+      CartPoseCalc c;
+      c.chain = &d->chain;
+      c.source_link = d->cart_source_link[k];
+      c.source_offset = Iso3::from12(d->cart_source_offset[k]);
+      c.target_offset = Iso3::from12(targets + (static_cast<std::size_t>(b) * d->n_cart + k) * 12);
+      DblVec coeffs;
+      cartPoseIndices(*d, k, c.indices, coeffs);
+      const int t = d->cart_step[k];
+      DblVec q(x + (static_cast<std::size_t>(b) * N + t) * D, x + (static_cast<std::size_t>(b) * N + t + 1) * D);
+      const DblVec e = c(q);
+      const Mat J = c.jac(q);
+      double* eo = err + (static_cast<std::size_t>(b) * d->n_cart + k) * 6;
+      double* jo = jac + (static_cast<std::size_t>(b) * d->n_cart + k) * 6 * D;
+      std::memset(eo, 0, sizeof(double) * 6);
+      std::memset(jo, 0, sizeof(double) * 6 * static_cast<std::size_t>(D));
+      for (std::size_t r = 0; r < c.indices.size(); ++r)
+      {
+        eo[r] = e[r];
+        for (int j = 0; j < D; ++j)
+          jo[r * static_cast<std::size_t>(D) + static_cast<std::size_t>(j)] = J(static_cast<int>(r), j);
+      }
+    }
+  return 0;
+}
+
+// link poses at n configurations: poses [n][n_links][12]
+int oracle_fwd_kin(const thip_chain* chain, int n, const double* q, double* poses)
+{
+  std::vector<Iso3> fk;
+  for (int i = 0; i < n; ++i)
+  {
+    chainFwdKin(*chain, q + static_cast<std::size_t>(i) * chain->n_dof, fk);
+    for (int l = 0; l < chain->n_links; ++l)
+      fk[static_cast<std::size_t>(l)].to12(poses + (static_cast<std::size_t>(i) * chain->n_links + l) * 12);
+  }
+  return 0;
+}
+
+// tesseract calcTransformError restated (for the pose-error KATs)
+void oracle_transform_error(const double* t1, const double* t2, double* err6)
+{
+  calcTransformError(Iso3::from12(t1), Iso3::from12(t2), err6);
+}
+
+void oracle_jacobian_transform_error_diff(const double* target, const double* source, const double* source_pert,
+                                          double* err6)
+{
+  calcJacobianTransformErrorDiff(Iso3::from12(target), Iso3::from12(source), Iso3::from12(source_pert), err6);
+}
+
+int oracle_sizeof_desc() { return static_cast<int>(sizeof(thip_problem_desc)); }
+int oracle_sizeof_result() { return static_cast<int>(sizeof(thip_result)); }
+
+}  // extern "C"
