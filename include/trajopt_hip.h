@@ -24,9 +24,11 @@
  *                                   CartPoseErrCalculator / CartPoseJacCalculator
  *                                   (trajopt/src/kinematic_terms.cpp:252-370) and
  *                                   JointVelEqCost::convex (trajopt/src/trajectory_costs.cpp:296-301).
- *   thip_qp_solve               <- sco::OSQPModel::optimize (trajopt_sco/src/osqp_interface.cpp:440-615):
- *                                   one OSQP-1.0-semantics solve (Ruiz scaling, ADMM, adaptive rho,
- *                                   polish) of the convexified QP of every problem at a given x.
+ *   (inside thip_sqp_run)       <- sco::OSQPModel::optimize (trajopt_sco/src/osqp_interface.cpp:440-615):
+ *                                   every QP solve with OSQP-1.0 semantics (Ruiz scaling, ADMM, adaptive
+ *                                   rho, polish, warm start) on the structured convexified QP.
+ *   thip_fwd_kin                <- tesseract JointGroup::calcFwdKin as called at
+ *                                   trajopt/src/kinematic_terms.cpp:255,355 (all chain links).
  *   thip_download               <- OptResults (trajopt_sco/include/trajopt_sco/optimizers.hpp:40-59).
  *
  * Data layout: every per-problem array is problem-major and row-major inside a
@@ -259,6 +261,9 @@ const char* thip_last_error(thip_ctx* ctx);
 
 /* Version / build info string. */
 const char* thip_build_info(void);
+
+/* sizeof(thip_problem_desc) as compiled into the library (ABI check). */
+int thip_sizeof_desc(void);
 
 #ifdef __cplusplus
 }

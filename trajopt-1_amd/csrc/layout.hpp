@@ -1,0 +1,131 @@
+// Device-side problem layout of the batched SQP (host + device).
+//
+// One HIP workgroup owns one problem for the whole BasicTrustRegionSQP run.
+// The convexified QP is kept in structured (waypoint-blocked) form instead of
+// CSC: columns are [x (N*D traj vars) | aux (neg, pos per CartPose row)], rows
+// are [fixed-timestep rows | CartPose "abs" rows | one bound row per column],
+// the same row/column sets OSQPModel builds from the model
+// (trajopt_sco/src/osqp_interface.cpp:170-281), so every OSQP quantity
+// (scaling, rho vector, residuals, polish active set) has a 1:1 counterpart.
+#pragma once
+#include "../../include/trajopt_hip.h"
+
+namespace thip
+{
+constexpr int kBlock = 256;  // threads per problem workgroup
+constexpr int kWaves = kBlock / 64;
+
+// per-problem double workspace arrays
+enum DArr : int
+{
+  A_X = 0,   // current SQP iterate (nx)
+  A_XN,      // candidate iterate new_x (nx)
+  A_INIT,    // initial trajectory (nx)
+  A_TGT,     // CartPose target offsets (n_cart*12)
+  A_G,       // CartPose rows, weighted, cleaned jacobian (n_abs*D)
+  A_GC,      // CartPose rows, weighted constant (n_abs)
+  A_COST,    // cost values at X (n_costs)
+  A_VIOL,    // constraint violations at X (n_cnts)
+  A_NCOST,   // cost values at XN
+  A_NVIOL,   // violations at XN
+  A_MU,      // merit coefficients (n_cnts)
+  A_PD,      // scaled P diagonal (nx)
+  A_PO,      // scaled P (t,j)-(t+1,j) coupling (nx)
+  A_Q,       // scaled q (n_cols)
+  A_DS,      // D scaling (n_cols)
+  A_BS,      // scaled bound-row entry (n_cols)
+  A_GS,      // scaled CartPose x coefficients (n_abs*D)
+  A_WS,      // scaled aux coefficients (n_abs*2)
+  A_FS,      // scaled fixed-row coefficient (n_fixed_rows)
+  A_E,       // row scaling (m)
+  A_L,       // scaled lower bounds (m)
+  A_U,       // scaled upper bounds (m)
+  A_RHO,     // rho per row (m)
+  A_XA0,     // ADMM x, double buffered (n_cols)
+  A_XA1,
+  A_Z0,      // ADMM z, double buffered (m)
+  A_Z1,
+  A_Y,       // ADMM y (m)
+  A_XT,      // x tilde (n_cols)
+  A_ZT,      // z tilde (m)
+  A_DX,      // delta x (n_cols)
+  A_DY,      // delta y (m)
+  A_BA,      // aux right-hand sides (n_cols, aux part used)
+  A_MR,      // row multipliers (n_rows)
+  A_AX,      // A x (m)
+  A_PX,      // P x (n_cols)
+  A_ATY,     // A' y (n_cols)
+  A_PRV,     // primal residual vector (m)
+  A_DRV,     // dual residual vector (n_cols)
+  A_DG,      // diagonal of the aux block / x-col diagonal (n_cols)
+  A_RE,      // effective rho of CartPose rows after aux elimination (n_rows)
+  A_LINV,    // inverse Cholesky factor of the diagonal blocks (N*D*D)
+  A_KB,      // assembled diagonal blocks (N*D*D)
+  A_CV,      // block solve vectors (nx)
+  A_YV,      // (nx)
+  A_SOLX,    // warm-start solution x, unscaled (n_cols)
+  A_SOLY,    // warm-start solution y, unscaled (m)
+  A_PB,      // polish rhs (n_cols + m)
+  A_PS,      // polish solution (n_cols + m)
+  A_PR,      // polish residual (n_cols + m)
+  A_PZ,      // polish z (m)
+  A_BXW,     // column rhs work (n_cols)
+  A_COUNT
+};
+
+enum IArr : int
+{
+  I_MASK = 0,  // jacobian drop mask per CartPose row (n_abs)
+  I_PMASK,     // mask of the previous QP setup (n_abs)
+  I_TYPE,      // constraint type per row: -1 loose, 0 ineq, 1 eq (m)
+  I_ACT,       // polish active flags (m)
+  I_COUNT
+};
+
+struct Layout
+{
+  int N, D, nx;
+  int n_links;
+  int n_fixed, n_fixed_rows;
+  int n_cart;
+  int n_abs;      // CartPose rows (cost rows first, then constraint rows)
+  int n_abs_cost; // rows belonging to cost terms
+  int n_cols;     // nx + 2*n_abs
+  int n_rows;     // n_fixed_rows + n_abs
+  int m;          // n_rows + n_cols
+  int n_costs;    // JointVel (0/1) + CartPose cost terms
+  int n_cnts;     // CartPose constraint terms
+  int jv_first, jv_last;
+  long long dstride;  // doubles per problem
+  long long istride;  // ints per problem
+  long long doff[A_COUNT];
+  long long ioff[I_COUNT];
+};
+
+// shared (batch-wide) tables, device resident
+struct Tables
+{
+  int* row_term;   // CartPose term of each abs row (n_abs)
+  int* row_comp;   // error component 0..5 (n_abs)
+  int* row_step;   // waypoint (n_abs)
+  double* row_w;   // coefficient (n_abs)
+  int* step_ptr;   // CSR waypoint -> abs rows (N+1)
+  int* step_rows;  // (n_abs)
+  int* term_row0;  // first abs row of each CartPose term (n_cart)
+  int* term_nrow;  // rows of each term (n_cart)
+  int* term_slot;  // cost index or constraint index of each term (n_cart)
+  int* fixed_of_step;  // fixed-step slot of each waypoint or -1 (N)
+};
+
+struct KernelArgs
+{
+  Layout L;
+  Tables T;
+  const thip_problem_desc* desc;  // device copy
+  double* ws;
+  int* iws;
+  thip_result* res;
+  int batch;
+};
+
+}  // namespace thip

@@ -1,0 +1,1821 @@
+// Batched BasicTrustRegionSQP on MI355X (gfx950): one 256-thread workgroup per
+// problem runs the whole penalty / SQP / trust-region loop of
+// trajopt_sco/src/optimizers.cpp:699-991, including
+//   * convexification: CartPose error + forward-difference jacobian (one
+//     thread per perturbed FK, unperturbed poses staged in LDS) and the
+//     constant JointVel quadratic (kinematic_terms.cpp:252-370,
+//     trajectory_costs.cpp:257-301, modeling_utils.cpp:168-269)
+//   * the QP solve with OSQP 1.0 semantics (osqp_interface.cpp:283-615): Ruiz
+//     scaling, vector rho, ADMM with the linear system solved as a
+//     waypoint-block-tridiagonal Cholesky after closed-form elimination of the
+//     abs/hinge auxiliary variables, termination / infeasibility checks,
+//     iteration-based adaptive rho, polishing with iterative refinement and the
+//     reference's warm-start policy.
+// All arithmetic is fp64. The path is latency / LDS bound, not a dense
+// contraction, so there is no MFMA.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "kin_device.hpp"
+#include "layout.hpp"
+
+namespace thip
+{
+// ------------------------------------------------------------------ constants
+constexpr double kInf = 1e30;  // OSQP_INFTY
+constexpr double kRhoMin = 1e-6, kRhoMax = 1e6, kRhoTol = 1e-4, kRhoEq = 1e3;
+constexpr double kMinScal = 1e-4, kMaxScal = 1e4;
+constexpr double kDivTol = 1.0 / kInf;
+
+enum
+{
+  ST_SOLVED = 1,
+  ST_SOLVED_INACC = 2,
+  ST_PINF = 3,
+  ST_PINF_INACC = 4,
+  ST_DINF = 5,
+  ST_DINF_INACC = 6,
+  ST_MAXIT = 7,
+  ST_NONCVX = 9,
+  ST_UNSOLVED = 11
+};
+
+// ----------------------------------------------------------- shared control
+struct Ctl
+{
+  // reductions
+  double red[kWaves * 16];
+  double bc[16];
+  // SQP state
+  double trust;
+  int status;
+  int n_sqp, n_qp, n_fev, n_merit;
+  long long n_admm;
+  // OSQP state
+  double c, cinv;
+  double rho;       // current rho of the active workspace
+  double prev_rho;  // rho of the previous workspace
+  int prev_status;  // status of the previous workspace (0 = none)
+  int cur;          // double-buffer parity
+  int qp_status, polish_status, iter;
+  double prim_res, dual_res;
+  int flag;
+  int can_check;
+};
+
+struct Ctx
+{
+  const Layout& L;
+  const Tables& T;
+  const thip_problem_desc* d;
+  double* w;
+  int* iw;
+  double* big;
+  Ctl* s;
+  int tid, lane, wave;
+  __device__ Ctx(const Layout& l, const Tables& t, const thip_problem_desc* dd, double* ww, int* ii, double* bb,
+                 Ctl* ss)
+    : L(l), T(t), d(dd), w(ww), iw(ii), big(bb), s(ss)
+  {
+    tid = threadIdx.x;
+    lane = tid & 63;
+    wave = tid >> 6;
+  }
+  __device__ __forceinline__ double* a(int k) const { return w + L.doff[k]; }
+  __device__ __forceinline__ int* ia(int k) const { return iw + L.ioff[k]; }
+};
+
+#define FOR(i, n) for (int i = c.tid; i < (n); i += kBlock)
+#define BSYNC() __syncthreads()
+
+__device__ __forceinline__ double wave_max(double v)
+{
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    v += __shfl_xor(v, o);
+  return v;
+}
+
+// K simultaneous block max-reductions; results in c.s->bc[0..K)
+template <int K>
+__device__ void block_max(Ctx& c, double (&v)[K])
+{
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+  {
+    const double r = wave_max(v[k]);
+    if (c.lane == 0)
+      c.s->red[c.wave * 16 + k] = r;
+  }
+  BSYNC();
+  if (c.tid < K)
+  {
+    double r = c.s->red[c.tid];
+    for (int wv = 1; wv < kWaves; ++wv)
+      r = fmax(r, c.s->red[wv * 16 + c.tid]);
+    c.s->bc[c.tid] = r;
+  }
+  BSYNC();
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    v[k] = c.s->bc[k];
+  BSYNC();
+}
+
+__device__ double block_sum(Ctx& c, double v)
+{
+  const double r = wave_sum(v);
+  if (c.lane == 0)
+    c.s->red[c.wave * 16] = r;
+  BSYNC();
+  double s = 0;
+  for (int wv = 0; wv < kWaves; ++wv)
+    s += c.s->red[wv * 16];
+  BSYNC();
+  return s;
+}
+
+__device__ __forceinline__ double limit_scaling(double a)
+{
+  a = a < kMinScal ? 1.0 : a;
+  a = a > kMaxScal ? kMaxScal : a;
+  return a;
+}
+
+// ======================================================================
+// Convexification of CartPose terms at trajectory x (nx):
+//   A_G [n_abs][D]: weight * cleanupAff(J row), A_GC: weight * (y - J.x),
+//   I_MASK: kept-entry bit mask (|J| > 1e-7)
+// ======================================================================
+__device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
+{
+  const Layout& L = c.L;
+  const int D = L.D;
+  const thip_chain& ch = c.d->chain;
+  double* stage = c.big;  // [n_cart][30]: source pose (12), target^-1 (12), err (6)
+  const double* tgt = c.a(A_TGT);
+  FOR(k, L.n_cart)
+  {
+    const int t = c.d->cart_step[k];
+    Pose S, So, Tb, To, Tt, Ti;
+    chain_fk(ch, x + t * D, c.d->cart_source_link[k], S);
+    pose_load(So, c.d->cart_source_offset[k]);
+    Pose Ss;
+    pose_mul(S, So, Ss);
+    pose_load(Tb, ch.base_pose);
+    pose_load(To, tgt + 12 * k);
+    pose_mul(Tb, To, Tt);
+    pose_inv(Tt, Ti);
+    double* st = stage + 30 * k;
+    for (int i = 0; i < 9; ++i)
+    {
+      st[i] = Ss.r[i];
+      st[12 + i] = Ti.r[i];
+    }
+    for (int i = 0; i < 3; ++i)
+    {
+      st[9 + i] = Ss.t[i];
+      st[21 + i] = Ti.t[i];
+    }
+    transform_error(Ti, Ss, st + 24);
+  }
+  BSYNC();
+  // perturbed FKs: item (k, p)
+  const double eps = 1e-5;
+  double* G = c.a(A_G);
+  FOR(item, L.n_cart * D)
+  {
+    const int k = item / D, p = item % D;
+    const int t = c.d->cart_step[k];
+    double q[THIP_MAX_DOF];
+    for (int j = 0; j < D; ++j)
+      q[j] = x[t * D + j];
+    q[p] = q[p] + eps;
+    Pose S, So, Sp;
+    chain_fk(ch, q, c.d->cart_source_link[k], S);
+    pose_load(So, c.d->cart_source_offset[k]);
+    pose_mul(S, So, Sp);
+    const double* st = stage + 30 * k;
+    Pose Ss, Ti;
+    for (int i = 0; i < 9; ++i)
+    {
+      Ss.r[i] = st[i];
+      Ti.r[i] = st[12 + i];
+    }
+    for (int i = 0; i < 3; ++i)
+    {
+      Ss.t[i] = st[9 + i];
+      Ti.t[i] = st[21 + i];
+    }
+    // calcJacobianTransformErrorDiff(target, source, source_perturbed)
+    Pose pe, ppe;
+    pose_mul(Ti, Ss, pe);
+    pose_mul(Ti, Sp, ppe);
+    double diff[6], r0[3], r1[3];
+    for (int i = 0; i < 3; ++i)
+      diff[i] = ppe.t[i] - pe.t[i];
+    rot_error(pe.r, r0, true);
+    rot_error(ppe.r, r1, true);
+    for (int i = 0; i < 3; ++i)
+      diff[3 + i] = r1[i] - r0[i];
+    const int r0w = c.T.term_row0[k], nr = c.T.term_nrow[k];
+    for (int rr = 0; rr < nr; ++rr)
+    {
+      const int row = r0w + rr;
+      G[row * D + p] = diff[c.T.row_comp[row]] / eps;
+    }
+  }
+  BSYNC();
+  // affFromValGrad + cleanupAff + exprScale(weight)
+  double* GC = c.a(A_GC);
+  int* mask = c.ia(I_MASK);
+  FOR(row, L.n_abs)
+  {
+    const int k = c.T.row_term[row];
+    const int t = c.d->cart_step[k];
+    const double y = stage[30 * k + 24 + c.T.row_comp[row]];
+    double dot = 0;
+    for (int j = 0; j < D; ++j)
+      dot += G[row * D + j] * x[t * D + j];
+    const double wgt = c.T.row_w[row];
+    if (raw_jac)
+      for (int j = 0; j < D; ++j)
+        raw_jac[row * D + j] = G[row * D + j];
+    int m = 0;
+    for (int j = 0; j < D; ++j)
+    {
+      const double g = G[row * D + j];
+      const bool keep = fabs(g) > 1e-7;
+      m |= keep ? (1 << j) : 0;
+      G[row * D + j] = keep ? g * wgt : 0.0;
+    }
+    mask[row] = m;
+    GC[row] = (y - dot) * wgt;
+  }
+  BSYNC();
+}
+
+// ======================================================================
+// Exact cost values / constraint violations at x (Cost::value,
+// Constraint::violation).  costs[n_costs], viols[n_cnts]
+// ======================================================================
+__device__ void evaluate(Ctx& c, const double* x, double* costs, double* viols)
+{
+  const Layout& L = c.L;
+  const int D = L.D;
+  const thip_chain& ch = c.d->chain;
+  // JointVel: sum_{t,j} c_j (x_{t+1,j} - x_{t,j} - targ_j)^2
+  double jv = 0;
+  if (c.d->jv_enabled)
+  {
+    const int nv = (L.jv_last - L.jv_first) * D;
+    FOR(i, nv)
+    {
+      const int t = L.jv_first + i / D, j = i % D;
+      const double dd = (x[(t + 1) * D + j] - x[t * D + j]) - c.d->jv_targets[j];
+      jv += (dd * dd) * c.d->jv_coeffs[j];
+    }
+  }
+  jv = block_sum(c, jv);
+  if (c.tid == 0 && c.d->jv_enabled)
+    costs[0] = jv;
+  const double* tgt = c.a(A_TGT);
+  FOR(k, L.n_cart)
+  {
+    const int t = c.d->cart_step[k];
+    Pose S, So, Ss, Tb, To, Tt, Ti;
+    chain_fk(ch, x + t * D, c.d->cart_source_link[k], S);
+    pose_load(So, c.d->cart_source_offset[k]);
+    pose_mul(S, So, Ss);
+    pose_load(Tb, ch.base_pose);
+    pose_load(To, tgt + 12 * k);
+    pose_mul(Tb, To, Tt);
+    pose_inv(Tt, Ti);
+    double err[6];
+    transform_error(Ti, Ss, err);
+    const int r0 = c.T.term_row0[k], nr = c.T.term_nrow[k];
+    double v = 0;
+    if (c.d->cart_is_cnt[k])
+    {
+      for (int rr = 0; rr < nr; ++rr)
+        v += fabs(err[c.T.row_comp[r0 + rr]] * c.T.row_w[r0 + rr]);
+      viols[c.T.term_slot[k]] = v;
+    }
+    else
+    {
+      for (int rr = 0; rr < nr; ++rr)
+        v += fabs(err[c.T.row_comp[r0 + rr]]) * c.T.row_w[r0 + rr];
+      costs[c.T.term_slot[k]] = v;
+    }
+  }
+  BSYNC();
+}
+
+// ======================================================================
+// QP assembly + Ruiz scaling (osqp scale_data) on the structured QP.
+// Rows: [fixed rows | abs rows | bound rows(n_cols)].
+// ======================================================================
+__device__ __forceinline__ int bound_row(const Layout& L, int col) { return L.n_rows + col; }
+
+__device__ void build_and_scale(Ctx& c)
+{
+  const Layout& L = c.L;
+  const int D = L.D, nx = L.nx;
+  const thip_osqp_settings& os = c.d->osqp;
+  double *PD = c.a(A_PD), *PO = c.a(A_PO), *Q = c.a(A_Q), *DS = c.a(A_DS), *BS = c.a(A_BS);
+  double *GS = c.a(A_GS), *WS = c.a(A_WS), *FS = c.a(A_FS), *E = c.a(A_E);
+  const double *G = c.a(A_G), *MU = c.a(A_MU);
+  // ---- unscaled data
+  FOR(col, nx)
+  {
+    const int t = col / D, j = col % D;
+    double pd = 0, po = 0, q = 0;
+    if (c.d->jv_enabled)
+    {
+      const double cj = c.d->jv_coeffs[j], tg = c.d->jv_targets[j];
+      const bool prev = (t - 1 >= L.jv_first) && (t - 1 <= L.jv_last - 1);
+      const bool here = (t >= L.jv_first) && (t <= L.jv_last - 1);
+      double dsum = 0;
+      if (prev)
+        dsum += cj;
+      if (here)
+        dsum += cj;
+      pd = dsum + dsum;
+      po = here ? cj * -2.0 : 0.0;
+      // q: term t-1 contributes (2*(-tg)*1)*c, term t (2*(-tg)*(-1))*c; zero coefficients skipped
+      double qa = 0;
+      if (prev)
+      {
+        const double v = (2 * (-tg) * 1.0) * cj;
+        if (v != 0.)
+          qa += v;
+      }
+      if (here)
+      {
+        const double v = (2 * (-tg) * -1.0) * cj;
+        if (v != 0.)
+          qa += v;
+      }
+      q = qa;
+    }
+    PD[col] = pd;
+    PO[col] = po;
+    Q[col] = q;
+    DS[col] = 1.0;
+    BS[col] = 1.0;
+  }
+  FOR(r, L.n_abs)
+  {
+    const int ca = nx + 2 * r;
+    const int k = c.T.row_term[r];
+    const double qv = c.d->cart_is_cnt[k] ? MU[c.T.term_slot[k]] : 1.0;
+    Q[ca] = qv;
+    Q[ca + 1] = qv;
+    DS[ca] = DS[ca + 1] = 1.0;
+    BS[ca] = BS[ca + 1] = 1.0;
+    WS[2 * r] = 1.0;
+    WS[2 * r + 1] = -1.0;
+    for (int j = 0; j < D; ++j)
+      GS[r * D + j] = G[r * D + j];
+  }
+  FOR(f, L.n_fixed_rows) FS[f] = 1.0;
+  FOR(r, L.m) E[r] = 1.0;
+  if (c.tid == 0)
+    c.s->c = 1.0;
+  BSYNC();
+  double* Dt = c.a(A_DG);
+  double* Et = c.a(A_PRV);
+  for (int it = 0; it < os.scaling; ++it)
+  {
+    // column norms of [P; A]
+    FOR(col, L.n_cols)
+    {
+      double v;
+      if (col < nx)
+      {
+        const int t = col / D, j = col % D;
+        v = fabs(PD[col]);
+        if (t < L.N - 1)
+          v = fmax(v, fabs(PO[col]));
+        if (t > 0)
+          v = fmax(v, fabs(PO[col - D]));
+        const int f = c.T.fixed_of_step[t];
+        if (f >= 0)
+          v = fmax(v, fabs(FS[f * D + j]));
+        for (int p = c.T.step_ptr[t]; p < c.T.step_ptr[t + 1]; ++p)
+          v = fmax(v, fabs(GS[c.T.step_rows[p] * D + j]));
+        v = fmax(v, fabs(BS[col]));
+      }
+      else
+      {
+        const int r = (col - nx) >> 1, sd = (col - nx) & 1;
+        v = fmax(fabs(WS[2 * r + sd]), fabs(BS[col]));
+      }
+      Dt[col] = 1.0 / sqrt(limit_scaling(v));
+    }
+    FOR(r, L.m)
+    {
+      double v;
+      if (r < L.n_fixed_rows)
+        v = fabs(FS[r]);
+      else if (r < L.n_rows)
+      {
+        const int a = r - L.n_fixed_rows;
+        v = 0;
+        for (int j = 0; j < D; ++j)
+          v = fmax(v, fabs(GS[a * D + j]));
+        v = fmax(v, fabs(WS[2 * a]));
+        v = fmax(v, fabs(WS[2 * a + 1]));
+      }
+      else
+        v = fabs(BS[r - L.n_rows]);
+      Et[r] = 1.0 / sqrt(limit_scaling(v));
+    }
+    BSYNC();
+    FOR(col, L.n_cols)
+    {
+      if (col < nx)
+      {
+        const int t = col / D;
+        PD[col] = (PD[col] * Dt[col]) * Dt[col];
+        if (t < L.N - 1)
+          PO[col] = (PO[col] * Dt[col]) * Dt[col + D];
+      }
+      BS[col] = (BS[col] * Et[bound_row(L, col)]) * Dt[col];
+      Q[col] *= Dt[col];
+      DS[col] *= Dt[col];
+    }
+    FOR(r, L.n_abs)
+    {
+      const int t = c.T.row_step[r];
+      const int er = L.n_fixed_rows + r;
+      for (int j = 0; j < D; ++j)
+        GS[r * D + j] = (GS[r * D + j] * Et[er]) * Dt[t * D + j];
+      WS[2 * r] = (WS[2 * r] * Et[er]) * Dt[nx + 2 * r];
+      WS[2 * r + 1] = (WS[2 * r + 1] * Et[er]) * Dt[nx + 2 * r + 1];
+    }
+    FOR(f, L.n_fixed_rows)
+    {
+      const int slot = f / D, j = f % D;
+      const int col = c.d->fixed_steps[slot] * D + j;
+      FS[f] = (FS[f] * Et[f]) * Dt[col];
+    }
+    FOR(r, L.m) E[r] *= Et[r];
+    BSYNC();
+    // cost normalisation
+    double colsum = 0, qn = 0;
+    FOR(col, L.n_cols)
+    {
+      if (col < nx)
+      {
+        const int t = col / D;
+        double v = fabs(PD[col]);
+        if (t < L.N - 1)
+          v = fmax(v, fabs(PO[col]));
+        if (t > 0)
+          v = fmax(v, fabs(PO[col - D]));
+        colsum += v;
+      }
+      qn = fmax(qn, fabs(Q[col]));
+    }
+    colsum = block_sum(c, colsum);
+    double qq[1] = { qn };
+    block_max<1>(c, qq);
+    double ct = colsum / (double)L.n_cols;
+    const double iq = limit_scaling(qq[0]);
+    ct = fmax(ct, iq);
+    ct = limit_scaling(ct);
+    ct = 1.0 / ct;
+    FOR(col, L.n_cols)
+    {
+      if (col < nx)
+      {
+        PD[col] *= ct;
+        PO[col] *= ct;
+      }
+      Q[col] *= ct;
+    }
+    if (c.tid == 0)
+      c.s->c *= ct;
+    BSYNC();
+  }
+  if (c.tid == 0)
+    c.s->cinv = 1.0 / c.s->c;
+  BSYNC();
+}
+
+// ======================================================================
+// Linear system: K = P + sig I + A' diag(rK) A, aux variables eliminated,
+// block tridiagonal Cholesky over waypoints.  rK per row in A_RHO (ADMM) or
+// given by the polish active set.
+// ======================================================================
+struct Solver
+{
+  double* M;   // LDS [N][D][D] forward chain matrices
+  double* Nb;  // LDS [N][D][D] backward chain matrices
+};
+
+// row rho for the factor: ADMM uses A_RHO, polish 1/delta on active rows
+__device__ __forceinline__ double rho_k(const Ctx& c, int r, bool polish, double delta)
+{
+  if (!polish)
+    return c.a(A_RHO)[r];
+  return c.ia(I_ACT)[r] != 0 ? 1.0 / delta : 0.0;
+}
+
+// returns false if the reduced matrix is not positive definite
+__device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delta)
+{
+  const Layout& L = c.L;
+  const int D = L.D, nx = L.nx, N = L.N;
+  const double *PD = c.a(A_PD), *PO = c.a(A_PO), *BS = c.a(A_BS), *GS = c.a(A_GS), *WS = c.a(A_WS),
+               *FS = c.a(A_FS);
+  double *DG = c.a(A_DG), *RE = c.a(A_RE), *KB = c.a(A_KB), *LI = c.a(A_LINV);
+  FOR(col, L.n_cols)
+  {
+    const double rb = rho_k(c, bound_row(L, col), polish, delta);
+    DG[col] = sigK + rb * (BS[col] * BS[col]);
+  }
+  BSYNC();
+  FOR(r, L.n_abs)
+  {
+    const int ca = nx + 2 * r;
+    const double rr = rho_k(c, L.n_fixed_rows + r, polish, delta);
+    const double phi = WS[2 * r] * WS[2 * r] / DG[ca] + WS[2 * r + 1] * WS[2 * r + 1] / DG[ca + 1];
+    RE[r] = rr / (1.0 + rr * phi);
+  }
+  BSYNC();
+  // diagonal blocks
+  FOR(e, N * D * D)
+  {
+    const int t = e / (D * D), i = (e / D) % D, j = e % D;
+    double v = 0;
+    if (i == j)
+    {
+      v = PD[t * D + i] + DG[t * D + i];
+      const int f = c.T.fixed_of_step[t];
+      if (f >= 0)
+      {
+        const int fr = f * D + i;
+        v += rho_k(c, fr, polish, delta) * (FS[fr] * FS[fr]);
+      }
+    }
+    for (int p = c.T.step_ptr[t]; p < c.T.step_ptr[t + 1]; ++p)
+    {
+      const int r = c.T.step_rows[p];
+      v += RE[r] * (GS[r * D + i] * GS[r * D + j]);
+    }
+    KB[e] = v;
+  }
+  BSYNC();
+  // sequential block Cholesky by wave 0; lanes own rows of the 7x7 blocks
+  __shared__ double Sblk[THIP_MAX_DOF * THIP_MAX_DOF];
+  __shared__ double Lsub[THIP_MAX_DOF * THIP_MAX_DOF];
+  __shared__ int bad;
+  if (c.tid == 0)
+    bad = 0;
+  BSYNC();
+  if (c.wave == 0)
+  {
+    const int DD = D * D;
+    for (int t = 0; t < N; ++t)
+    {
+      // S = KB_t - Lsub Lsub^T   (Lsub = L_{t,t-1})
+      for (int e = c.lane; e < DD; e += 64)
+      {
+        const int i = e / D, j = e % D;
+        double v = KB[t * DD + e];
+        if (t > 0)
+          for (int k = 0; k < D; ++k)
+            v -= Lsub[i * D + k] * Lsub[j * D + k];
+        Sblk[e] = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // in-place Cholesky (lower) of Sblk: lane i owns row i
+      for (int j = 0; j < D; ++j)
+      {
+        if (c.lane == j)
+        {
+          double v = Sblk[j * D + j];
+          for (int k = 0; k < j; ++k)
+            v -= Sblk[j * D + k] * Sblk[j * D + k];
+          if (!(v > 0))
+          {
+            bad = 1;
+            v = 1.0;
+          }
+          Sblk[j * D + j] = sqrt(v);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (c.lane > j && c.lane < D)
+        {
+          const int i = c.lane;
+          double v = Sblk[i * D + j];
+          for (int k = 0; k < j; ++k)
+            v -= Sblk[i * D + k] * Sblk[j * D + k];
+          Sblk[i * D + j] = v / Sblk[j * D + j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      // Linv_t: lane j solves L x = e_j (column j of the inverse)
+      double* Li = LI + t * DD;
+      if (c.lane < D)
+      {
+        const int j = c.lane;
+        double xcol[THIP_MAX_DOF];
+        for (int i = 0; i < D; ++i)
+        {
+          double v = (i == j) ? 1.0 : 0.0;
+          for (int k = 0; k < i; ++k)
+            v -= Sblk[i * D + k] * xcol[k];
+          xcol[i] = (i < j) ? 0.0 : v / Sblk[i * D + i];
+        }
+        for (int i = 0; i < D; ++i)
+          Li[i * D + j] = xcol[i];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // M_t = Linv_t * L_{t,t-1}
+      if (t > 0)
+        for (int e = c.lane; e < DD; e += 64)
+        {
+          const int i = e / D, j = e % D;
+          double v = 0;
+          for (int k = 0; k <= i; ++k)
+            v += Li[i * D + k] * Lsub[k * D + j];
+          sv.M[t * DD + e] = v;
+        }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (t < N - 1)
+      {
+        // L_{t+1,t} = O_t Linv_t^T, O_t = diag(PO[t*D + i])
+        for (int e = c.lane; e < DD; e += 64)
+        {
+          const int i = e / D, k = e % D;
+          Lsub[e] = PO[t * D + i] * Li[k * D + i];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // N_t = Linv_t^T L_{t+1,t}^T : N[i][j] = sum_k Linv[k][i] Lsub[j][k]
+        for (int e = c.lane; e < DD; e += 64)
+        {
+          const int i = e / D, j = e % D;
+          double v = 0;
+          for (int k = i; k < D; ++k)
+            v += Li[k * D + i] * Lsub[j * D + k];
+          sv.Nb[t * DD + e] = v;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  BSYNC();
+  const bool ok = (bad == 0);
+  BSYNC();
+  return ok;
+}
+
+// Solve K [x; aux] = b (b over all n_cols, given in A_BXW for x cols and
+// A_BA for aux cols).  Result in out (n_cols).
+// Aux elimination per CartPose row (Sherman-Morrison on the 2x2 aux block).
+__device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, double* out)
+{
+  const Layout& L = c.L;
+  const int D = L.D, nx = L.nx, N = L.N, DD = D * D;
+  const double *GS = c.a(A_GS), *WS = c.a(A_WS), *DG = c.a(A_DG), *RE = c.a(A_RE), *LI = c.a(A_LINV);
+  double *BX = c.a(A_BXW), *BA = c.a(A_BA), *MR = c.a(A_MR), *CV = c.a(A_CV), *YV = c.a(A_YV);
+  // beta_r = RE_r * sum_a w_a b_a / Dg_a
+  FOR(r, L.n_abs)
+  {
+    const int ca = nx + 2 * r;
+    MR[r] = RE[r] * (WS[2 * r] * BA[ca] / DG[ca] + WS[2 * r + 1] * BA[ca + 1] / DG[ca + 1]);
+  }
+  BSYNC();
+  FOR(col, nx)
+  {
+    const int t = col / D, j = col % D;
+    double b = BX[col];
+    for (int p = c.T.step_ptr[t]; p < c.T.step_ptr[t + 1]; ++p)
+    {
+      const int r = c.T.step_rows[p];
+      b -= GS[r * D + j] * MR[r];
+    }
+    BX[col] = b;
+  }
+  BSYNC();
+  FOR(col, nx)
+  {
+    const int t = col / D, i = col % D;
+    double v = 0;
+    for (int k = 0; k <= i; ++k)
+      v += LI[t * DD + i * D + k] * BX[t * D + k];
+    CV[col] = v;
+  }
+  BSYNC();
+  // forward chain y_t = c_t - M_t y_{t-1}
+  if (c.wave == 0)
+  {
+    const int i = c.lane >> 3, k = c.lane & 7;
+    const bool act = (i < D) && (k < D);
+    double yk = (k < D) ? CV[k] : 0.0;
+    if (c.lane < D)
+      YV[c.lane] = CV[c.lane];
+    for (int t = 1; t < N; ++t)
+    {
+      double pr = act ? sv.M[t * DD + i * D + k] * yk : 0.0;
+      pr += __shfl_xor(pr, 1);
+      pr += __shfl_xor(pr, 2);
+      pr += __shfl_xor(pr, 4);
+      const double yi = (i < D) ? CV[t * D + i] - pr : 0.0;
+      yk = __shfl(yi, (k < D ? k : 0) * 8);
+      if (i == 0 && k < D)
+        YV[t * D + k] = yk;
+    }
+  }
+  BSYNC();
+  FOR(col, nx)
+  {
+    const int t = col / D, i = col % D;
+    double v = 0;
+    for (int k = i; k < D; ++k)
+      v += LI[t * DD + k * D + i] * YV[t * D + k];
+    CV[col] = v;
+  }
+  BSYNC();
+  // backward chain x_t = d_t - N_t x_{t+1}
+  if (c.wave == 0)
+  {
+    const int i = c.lane >> 3, k = c.lane & 7;
+    const bool act = (i < D) && (k < D);
+    double xk = (k < D) ? CV[(N - 1) * D + k] : 0.0;
+    if (c.lane < D)
+      out[(N - 1) * D + c.lane] = CV[(N - 1) * D + c.lane];
+    for (int t = N - 2; t >= 0; --t)
+    {
+      double pr = act ? sv.Nb[t * DD + i * D + k] * xk : 0.0;
+      pr += __shfl_xor(pr, 1);
+      pr += __shfl_xor(pr, 2);
+      pr += __shfl_xor(pr, 4);
+      const double xi = (i < D) ? CV[t * D + i] - pr : 0.0;
+      xk = __shfl(xi, (k < D ? k : 0) * 8);
+      if (i == 0 && k < D)
+        out[t * D + k] = xk;
+    }
+  }
+  BSYNC();
+  // aux back-substitution
+  FOR(r, L.n_abs)
+  {
+    const int t = c.T.row_step[r];
+    const int ca = nx + 2 * r;
+    double g = 0;
+    for (int j = 0; j < D; ++j)
+      g += GS[r * D + j] * out[t * D + j];
+    const double rr = rho_k(c, L.n_fixed_rows + r, polish, delta);
+    const double v0 = BA[ca] - rr * WS[2 * r] * g;
+    const double v1 = BA[ca + 1] - rr * WS[2 * r + 1] * g;
+    const double psi = WS[2 * r] * v0 / DG[ca] + WS[2 * r + 1] * v1 / DG[ca + 1];
+    out[ca] = v0 / DG[ca] - (WS[2 * r] / DG[ca]) * RE[r] * psi;
+    out[ca + 1] = v1 / DG[ca + 1] - (WS[2 * r + 1] / DG[ca + 1]) * RE[r] * psi;
+  }
+  BSYNC();
+}
+
+// A x for one row (scaled); x over n_cols
+__device__ __forceinline__ double row_ax(const Ctx& c, int r, const double* x)
+{
+  const Layout& L = c.L;
+  const int D = L.D;
+  if (r < L.n_fixed_rows)
+  {
+    const int slot = r / D, j = r % D;
+    return c.a(A_FS)[r] * x[c.d->fixed_steps[slot] * D + j];
+  }
+  if (r < L.n_rows)
+  {
+    const int a = r - L.n_fixed_rows;
+    const int t = c.T.row_step[a];
+    const double* GS = c.a(A_GS);
+    double v = 0;
+    for (int j = 0; j < D; ++j)
+      v += GS[a * D + j] * x[t * D + j];
+    const int ca = L.nx + 2 * a;
+    v += c.a(A_WS)[2 * a] * x[ca] + c.a(A_WS)[2 * a + 1] * x[ca + 1];
+    return v;
+  }
+  const int col = r - L.n_rows;
+  return c.a(A_BS)[col] * x[col];
+}
+
+// (P x)_col and (A' y)_col (scaled)
+__device__ __forceinline__ double col_px(const Ctx& c, int col, const double* x)
+{
+  const Layout& L = c.L;
+  if (col >= L.nx)
+    return 0.0;
+  const int D = L.D, t = col / D;
+  const double *PD = c.a(A_PD), *PO = c.a(A_PO);
+  double v = PD[col] * x[col];
+  if (t < L.N - 1)
+    v += PO[col] * x[col + D];
+  if (t > 0)
+    v += PO[col - D] * x[col - D];
+  return v;
+}
+__device__ __forceinline__ double col_aty(const Ctx& c, int col, const double* y)
+{
+  const Layout& L = c.L;
+  const int D = L.D;
+  double v = c.a(A_BS)[col] * y[bound_row(L, col)];
+  if (col < L.nx)
+  {
+    const int t = col / D, j = col % D;
+    const int f = c.T.fixed_of_step[t];
+    if (f >= 0)
+      v += c.a(A_FS)[f * D + j] * y[f * D + j];
+    const double* GS = c.a(A_GS);
+    for (int p = c.T.step_ptr[t]; p < c.T.step_ptr[t + 1]; ++p)
+    {
+      const int a = c.T.step_rows[p];
+      v += GS[a * D + j] * y[L.n_fixed_rows + a];
+    }
+  }
+  else
+  {
+    const int a = (col - L.nx) >> 1, sd = (col - L.nx) & 1;
+    v += c.a(A_WS)[2 * a + sd] * y[L.n_fixed_rows + a];
+  }
+  return v;
+}
+
+// ======================================================================
+// OSQP solve on the structured QP (one workgroup)
+// ======================================================================
+__device__ void set_rho_vec(Ctx& c)
+{
+  const Layout& L = c.L;
+  const double *Lo = c.a(A_L), *Up = c.a(A_U);
+  double* RH = c.a(A_RHO);
+  int* TY = c.ia(I_TYPE);
+  const double rho = c.s->rho;
+  FOR(r, L.m)
+  {
+    int ty;
+    double rv;
+    if (Lo[r] < -kInf * kMinScal && Up[r] > kInf * kMinScal)
+    {
+      ty = -1;
+      rv = kRhoMin;
+    }
+    else if (Up[r] - Lo[r] < kRhoTol)
+    {
+      ty = 1;
+      rv = kRhoEq * rho;
+    }
+    else
+    {
+      ty = 0;
+      rv = rho;
+    }
+    TY[r] = ty;
+    RH[r] = rv;
+  }
+  BSYNC();
+}
+
+// residuals at (x, z, y); stores prim/dual residuals and the tolerance /
+// rho-estimate norms in bc[]: returns via c.s
+struct Norms
+{
+  double prim_res, dual_res;
+  double zE, axE, qD, atyD, pxD;  // scaled-for-termination norms
+  double pr, dr, z, ax, q, aty, px;  // raw (scaled-space) norms for rho estimate
+};
+
+__device__ void compute_residuals(Ctx& c, const double* x, const double* z, const double* y, Norms& nm)
+{
+  const Layout& L = c.L;
+  double *AX = c.a(A_AX), *PX = c.a(A_PX), *ATY = c.a(A_ATY), *PRV = c.a(A_PRV), *DRV = c.a(A_DRV);
+  const double *E = c.a(A_E), *DS = c.a(A_DS), *Q = c.a(A_Q);
+  double v[12] = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
+  FOR(r, L.m)
+  {
+    const double ax = row_ax(c, r, x);
+    const double pr = ax - z[r];
+    AX[r] = ax;
+    PRV[r] = pr;
+    const double einv = 1.0 / E[r];
+    v[0] = fmax(v[0], fabs(einv * pr));
+    v[1] = fmax(v[1], fabs(einv * z[r]));
+    v[2] = fmax(v[2], fabs(einv * ax));
+    v[3] = fmax(v[3], fabs(pr));
+    v[4] = fmax(v[4], fabs(z[r]));
+    v[5] = fmax(v[5], fabs(ax));
+  }
+  FOR(col, L.n_cols)
+  {
+    const double px = col_px(c, col, x);
+    const double aty = col_aty(c, col, y);
+    PX[col] = px;
+    ATY[col] = aty;
+    const double dr = Q[col] + px + aty;
+    DRV[col] = dr;
+    const double dinv = 1.0 / DS[col];
+    v[6] = fmax(v[6], fabs(dinv * dr));
+    v[7] = fmax(v[7], fabs(dinv * Q[col]));
+    v[8] = fmax(v[8], fabs(dinv * aty));
+    v[9] = fmax(v[9], fabs(dinv * px));
+    v[10] = fmax(v[10], fabs(dr));
+    v[11] = fmax(v[11], fmax(fabs(Q[col]), fmax(fabs(aty), fabs(px))));
+  }
+  block_max<12>(c, v);
+  nm.prim_res = (L.m > 0) ? v[0] : 0.0;
+  nm.zE = v[1];
+  nm.axE = v[2];
+  nm.pr = v[3];
+  nm.z = v[4];
+  nm.ax = v[5];
+  nm.dual_res = c.s->cinv * v[6];
+  nm.qD = v[7];
+  nm.atyD = v[8];
+  nm.pxD = v[9];
+  nm.dr = v[10];
+  nm.q = v[11];  // max(|q|,|A'y|,|Px|) combined (used only inside max())
+}
+
+__device__ bool is_primal_infeasible(Ctx& c, double eps)
+{
+  const Layout& L = c.L;
+  double* DY = c.a(A_DY);
+  const double *Lo = c.a(A_L), *Up = c.a(A_U), *E = c.a(A_E), *DS = c.a(A_DS);
+  double nv[1] = { 0 };
+  FOR(r, L.m)
+  {
+    double dy = DY[r];
+    if (Up[r] > kInf * kMinScal)
+      dy = (Lo[r] < -kInf * kMinScal) ? 0.0 : fmin(dy, 0.0);
+    else if (Lo[r] < -kInf * kMinScal)
+      dy = fmax(dy, 0.0);
+    DY[r] = dy;
+    nv[0] = fmax(nv[0], fabs(E[r] * dy));
+  }
+  block_max<1>(c, nv);
+  const double ndy = nv[0];
+  if (!(ndy > kDivTol))
+    return false;
+  double lhs = 0;
+  FOR(r, L.m) lhs += Up[r] * fmax(DY[r], 0.0) + Lo[r] * fmin(DY[r], 0.0);
+  lhs = block_sum(c, lhs);
+  if (!(lhs < eps * ndy))
+    return false;
+  double av[1] = { 0 };
+  FOR(col, L.n_cols) av[0] = fmax(av[0], fabs((1.0 / DS[col]) * col_aty(c, col, DY)));
+  block_max<1>(c, av);
+  return av[0] < eps * ndy;
+}
+
+__device__ bool is_dual_infeasible(Ctx& c, double eps)
+{
+  const Layout& L = c.L;
+  const double *DX = c.a(A_DX), *DS = c.a(A_DS), *Q = c.a(A_Q), *E = c.a(A_E), *Lo = c.a(A_L), *Up = c.a(A_U);
+  double nv[1] = { 0 };
+  FOR(col, L.n_cols) nv[0] = fmax(nv[0], fabs(DS[col] * DX[col]));
+  block_max<1>(c, nv);
+  const double ndx = nv[0];
+  const double cs = c.s->c;
+  if (!(ndx > kDivTol))
+    return false;
+  double qdx = 0;
+  FOR(col, L.n_cols) qdx += Q[col] * DX[col];
+  qdx = block_sum(c, qdx);
+  if (!(qdx < cs * eps * ndx))
+    return false;
+  double pv[1] = { 0 };
+  FOR(col, L.n_cols) pv[0] = fmax(pv[0], fabs((1.0 / DS[col]) * col_px(c, col, DX)));
+  block_max<1>(c, pv);
+  if (!(pv[0] < cs * eps * ndx))
+    return false;
+  double bad[1] = { 0 };
+  FOR(r, L.m)
+  {
+    const double adx = (1.0 / E[r]) * row_ax(c, r, DX);
+    if (((Up[r] < kInf * kMinScal) && (adx > eps * ndx)) || ((Lo[r] > -kInf * kMinScal) && (adx < -eps * ndx)))
+      bad[0] = 1.0;
+  }
+  block_max<1>(c, bad);
+  return bad[0] == 0.0;
+}
+
+// check_termination; sets c.s->qp_status when it fires
+__device__ bool check_termination(Ctx& c, const Norms& nm, bool approx)
+{
+  const thip_osqp_settings& os = c.d->osqp;
+  double ea = os.eps_abs, er = os.eps_rel, epi = os.eps_prim_inf, edi = os.eps_dual_inf;
+  if (approx)
+  {
+    ea *= 10;
+    er *= 10;
+    epi *= 10;
+    edi *= 10;
+  }
+  bool prim_ok = false, dual_ok = false, pinf = false, dinf = false;
+  if (c.L.m == 0)
+    prim_ok = true;
+  else
+  {
+    const double eps_prim = ea + er * fmax(nm.zE, nm.axE);
+    if (nm.prim_res < eps_prim)
+      prim_ok = true;
+    else
+      pinf = is_primal_infeasible(c, epi);
+  }
+  const double eps_dual = ea + er * (c.s->cinv * fmax(fmax(nm.qD, nm.atyD), nm.pxD));
+  if (nm.dual_res < eps_dual)
+    dual_ok = true;
+  else
+    dinf = is_dual_infeasible(c, edi);
+  int st = 0;
+  if (prim_ok && dual_ok)
+    st = approx ? ST_SOLVED_INACC : ST_SOLVED;
+  else if (pinf)
+    st = approx ? ST_PINF_INACC : ST_PINF;
+  else if (dinf)
+    st = approx ? ST_DINF_INACC : ST_DINF;
+  if (c.tid == 0 && st != 0)
+    c.s->qp_status = st;
+  BSYNC();
+  return st != 0;
+}
+
+__device__ void admm_step(Ctx& c, Solver& sv)
+{
+  const Layout& L = c.L;
+  const int D = L.D, nx = L.nx;
+  const thip_osqp_settings& os = c.d->osqp;
+  const double sig = os.sigma, al = os.alpha;
+  // swap buffers
+  const int cur = c.s->cur ^ 1;
+  BSYNC();
+  if (c.tid == 0)
+    c.s->cur = cur;
+  double* x = c.a(cur ? A_XA1 : A_XA0);
+  const double* xp = c.a(cur ? A_XA0 : A_XA1);
+  double* z = c.a(cur ? A_Z1 : A_Z0);
+  const double* zp = c.a(cur ? A_Z0 : A_Z1);
+  double *Y = c.a(A_Y), *XT = c.a(A_XT), *ZT = c.a(A_ZT), *DX = c.a(A_DX), *DY = c.a(A_DY);
+  double *BX = c.a(A_BXW), *BA = c.a(A_BA);
+  const double *Q = c.a(A_Q), *BS = c.a(A_BS), *RH = c.a(A_RHO), *Lo = c.a(A_L), *Up = c.a(A_U);
+  const double *FS = c.a(A_FS), *GS = c.a(A_GS), *WS = c.a(A_WS);
+  double* MRt = c.a(A_PZ);  // eta of structural rows (scratch)
+  // eta_r = rho_r zp_r - y_r for structural rows, and aux right-hand sides
+  FOR(r, L.n_rows)
+  {
+    const double eta = RH[r] * zp[r] - Y[r];
+    MRt[r] = eta;
+    if (r >= L.n_fixed_rows)
+    {
+      const int a = r - L.n_fixed_rows, ca = nx + 2 * a;
+      for (int sd = 0; sd < 2; ++sd)
+      {
+        const int col = ca + sd, br = bound_row(L, col);
+        const double etab = RH[br] * zp[br] - Y[br];
+        BA[col] = sig * xp[col] - Q[col] + BS[col] * etab + WS[2 * a + sd] * eta;
+      }
+    }
+  }
+  BSYNC();
+  FOR(col, nx)
+  {
+    const int t = col / D, j = col % D, br = bound_row(L, col);
+    const double etab = RH[br] * zp[br] - Y[br];
+    double b = sig * xp[col] - Q[col] + BS[col] * etab;
+    const int f = c.T.fixed_of_step[t];
+    if (f >= 0)
+      b += FS[f * D + j] * MRt[f * D + j];
+    for (int p = c.T.step_ptr[t]; p < c.T.step_ptr[t + 1]; ++p)
+    {
+      const int a = c.T.step_rows[p];
+      b += GS[a * D + j] * MRt[L.n_fixed_rows + a];
+    }
+    BX[col] = b;
+  }
+  BSYNC();
+  reduced_solve(c, sv, false, 0.0, XT);
+  // z tilde = A x tilde; updates
+  FOR(r, L.m)
+  {
+    const double zt = row_ax(c, r, XT);
+    ZT[r] = zt;
+    const double rho = RH[r];
+    double zr = (1.0 / rho) * Y[r];
+    zr = zr + al * zt;
+    zr = zr + (1.0 - al) * zp[r];
+    zr = fmin(fmax(zr, Lo[r]), Up[r]);
+    z[r] = zr;
+    const double dy = rho * (al * zt + (1.0 - al) * zp[r] - zr);
+    DY[r] = dy;
+    Y[r] += dy;
+  }
+  FOR(col, L.n_cols)
+  {
+    const double xv = al * XT[col] + (1.0 - al) * xp[col];
+    x[col] = xv;
+    DX[col] = xv - xp[col];
+  }
+  BSYNC();
+}
+
+__device__ double rho_estimate(Ctx& c, const Norms& nm)
+{
+  double pr = nm.pr, dr = nm.dr;
+  const double prn = fmax(nm.z, nm.ax);
+  pr /= (prn + kDivTol);
+  const double drn = nm.q;
+  dr /= (drn + kDivTol);
+  double est = c.s->rho * sqrt(pr / (dr + kDivTol));
+  return fmin(fmax(est, kRhoMin), kRhoMax);
+}
+
+// polish: returns nothing; updates x/z/y buffers on success
+__device__ void polish(Ctx& c, Solver& sv, Norms& nm)
+{
+  const Layout& L = c.L;
+  const thip_osqp_settings& os = c.d->osqp;
+  const double delta = os.delta;
+  const int cur = c.s->cur;
+  double* x = c.a(cur ? A_XA1 : A_XA0);
+  double* z = c.a(cur ? A_Z1 : A_Z0);
+  double* Y = c.a(A_Y);
+  const double *Lo = c.a(A_L), *Up = c.a(A_U), *Q = c.a(A_Q);
+  int* ACT = c.ia(I_ACT);
+  FOR(r, L.m)
+  {
+    int f = 0;
+    if (z[r] - Lo[r] < -Y[r])
+      f = -1;
+    else if (Up[r] - z[r] < Y[r])
+      f = 1;
+    ACT[r] = f;
+  }
+  BSYNC();
+  if (!factor(c, sv, delta, true, delta))
+  {
+    if (c.tid == 0)
+      c.s->polish_status = -1;
+    BSYNC();
+    return;
+  }
+  // PB = [b_x (n_cols); b_y (m)], PS = solution [x; y], PR = residual
+  double *PB = c.a(A_PB), *PS = c.a(A_PS), *PR = c.a(A_PR), *PZ = c.a(A_PZ);
+  double *BX = c.a(A_BXW), *BA = c.a(A_BA), *XT = c.a(A_XT);
+  const int nc = L.n_cols, nx = L.nx, D = L.D;
+  FOR(col, nc) PB[col] = -Q[col];
+  FOR(r, L.m) PB[nc + r] = (ACT[r] < 0) ? Lo[r] : ((ACT[r] > 0) ? Up[r] : 0.0);
+  FOR(k, nc + L.m) PR[k] = PB[k];
+  FOR(k, nc + L.m) PS[k] = 0.0;
+  BSYNC();
+  const double *BS = c.a(A_BS), *FS = c.a(A_FS), *GS = c.a(A_GS), *WS = c.a(A_WS);
+  for (int it = 0; it <= os.polish_refine_iter; ++it)
+  {
+    // solve K_delta d = PR  (rhs_x + A_act' r_y / delta), d_y = (A_act d_x - r_y) / delta
+    double* eta = PZ;  // r_y / delta on active rows (structural part used for the gather)
+    FOR(r, L.m) eta[r] = (ACT[r] != 0) ? PR[nc + r] / delta : 0.0;
+    BSYNC();
+    FOR(col, nc)
+    {
+      double b = PR[col] + BS[col] * eta[bound_row(L, col)];
+      if (col < nx)
+      {
+        const int t = col / D, j = col % D;
+        const int f = c.T.fixed_of_step[t];
+        if (f >= 0)
+          b += FS[f * D + j] * eta[f * D + j];
+        for (int p = c.T.step_ptr[t]; p < c.T.step_ptr[t + 1]; ++p)
+        {
+          const int a = c.T.step_rows[p];
+          b += GS[a * D + j] * eta[L.n_fixed_rows + a];
+        }
+        BX[col] = b;
+      }
+      else
+      {
+        const int a = (col - nx) >> 1, sd = (col - nx) & 1;
+        b += WS[2 * a + sd] * eta[L.n_fixed_rows + a];
+        BA[col] = b;
+      }
+    }
+    BSYNC();
+    reduced_solve(c, sv, true, delta, XT);
+    FOR(col, nc) PS[col] += XT[col];
+    FOR(r, L.m)
+    {
+      if (ACT[r] != 0)
+        PS[nc + r] += (row_ax(c, r, XT) - PR[nc + r]) / delta;
+    }
+    BSYNC();
+    if (it == os.polish_refine_iter)
+      break;
+    // residual of the unregularised KKT: PR = PB - K [x; y]
+    FOR(col, nc) PR[col] = PB[col] - col_px(c, col, PS) - col_aty(c, col, PS + nc);
+    FOR(r, L.m) PR[nc + r] = (ACT[r] != 0) ? PB[nc + r] - row_ax(c, r, PS) : 0.0;
+    BSYNC();
+  }
+  // polished point: x, z = A x, y (active) -> normal cone projection
+  double* pz = PZ;
+  double* py = PR + nc;  // reuse
+  FOR(r, L.m)
+  {
+    const double zr = row_ax(c, r, PS);
+    const double yr = (ACT[r] != 0) ? PS[nc + r] : 0.0;
+    const double tv = zr + yr;
+    const double zc = fmin(fmax(tv, Lo[r]), Up[r]);
+    pz[r] = zc;
+    py[r] = tv - zc;
+  }
+  BSYNC();
+  Norms pn;
+  compute_residuals(c, PS, pz, py, pn);
+  const bool ok = (pn.prim_res < nm.prim_res && pn.dual_res < nm.dual_res) ||
+                  (pn.prim_res < nm.prim_res && nm.dual_res < 1e-10) ||
+                  (pn.dual_res < nm.dual_res && nm.prim_res < 1e-10);
+  if (ok)
+  {
+    FOR(col, nc) x[col] = PS[col];
+    FOR(r, L.m)
+    {
+      z[r] = pz[r];
+      Y[r] = py[r];
+    }
+    nm.prim_res = pn.prim_res;
+    nm.dual_res = pn.dual_res;
+  }
+  if (c.tid == 0)
+    c.s->polish_status = ok ? 1 : -1;
+  BSYNC();
+}
+
+// One OSQPModel::optimize(): setup (bounds, rho, warm start, factor) + solve.
+// Scaled P/A/q must be current (build_and_scale).  Trust-box bounds from X.
+// Returns the CvxOptStatus.
+__device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
+{
+  const Layout& L = c.L;
+  const int nx = L.nx, D = L.D;
+  const thip_osqp_settings& os = c.d->osqp;
+  const thip_chain& ch = c.d->chain;
+  const double* X = c.a(A_X);
+  double *Lo = c.a(A_L), *Up = c.a(A_U);
+  const double *E = c.a(A_E), *GC = c.a(A_GC), *INIT = c.a(A_INIT), *DS = c.a(A_DS);
+  // bounds (unscaled -> scaled by E)
+  const double tb = c.s->trust;
+  FOR(r, L.m)
+  {
+    double lo, up;
+    if (r < L.n_fixed_rows)
+    {
+      const int slot = r / D, j = r % D;
+      lo = up = INIT[c.d->fixed_steps[slot] * D + j];
+    }
+    else if (r < L.n_rows)
+    {
+      lo = up = -GC[r - L.n_fixed_rows];
+    }
+    else
+    {
+      const int col = r - L.n_rows;
+      if (col < nx)
+      {
+        const int j = col % D;
+        const double lb = ch.lower[j], ub = ch.upper[j];
+        const double xi = fmin(fmax(X[col], lb), ub);  // std::clamp
+        lo = fmax(xi - tb, lb);
+        up = fmin(xi + tb, ub);
+        lo = fmax(lo, -kInf);
+        up = fmin(up, kInf);
+      }
+      else
+      {
+        lo = 0.0;
+        up = kInf;
+      }
+    }
+    Lo[r] = lo * E[r];
+    Up[r] = up * E[r];
+  }
+  // warm start policy (osqp_interface.cpp:283-370)
+  const bool warm = (c.s->prev_status == ST_SOLVED || c.s->prev_status == ST_SOLVED_INACC) && os.warm_starting &&
+                    pattern_equal;
+  if (c.tid == 0)
+  {
+    c.s->rho = fmin(fmax(warm ? c.s->prev_rho : os.rho, kRhoMin), kRhoMax);
+    c.s->cur = 0;
+    c.s->qp_status = ST_UNSOLVED;
+    c.s->polish_status = 0;
+  }
+  BSYNC();
+  set_rho_vec(c);
+  double* x = c.a(A_XA0);
+  double* z = c.a(A_Z0);
+  double* Y = c.a(A_Y);
+  const double *SX = c.a(A_SOLX), *SY = c.a(A_SOLY);
+  if (warm)
+  {
+    FOR(col, L.n_cols) x[col] = SX[col] * (1.0 / DS[col]);
+    FOR(r, L.m) Y[r] = (SY[r] * (1.0 / E[r])) * c.s->c;
+    BSYNC();
+    FOR(r, L.m) z[r] = row_ax(c, r, x);
+  }
+  else
+  {
+    FOR(col, L.n_cols) x[col] = 0.0;
+    FOR(r, L.m)
+    {
+      z[r] = 0.0;
+      Y[r] = 0.0;
+    }
+  }
+  BSYNC();
+  if (!factor(c, sv, os.sigma, false, 0.0))
+  {
+    // setup failure: CVX_FAILED, no workspace for the next warm start
+    if (c.tid == 0)
+      c.s->prev_status = 0;
+    BSYNC();
+    return THIP_CVX_FAILED;
+  }
+  const int interval = (os.adaptive_rho == 1 && os.adaptive_rho_interval == 0) ?
+                           (os.check_termination ? 4 * os.check_termination : 100) :
+                           os.adaptive_rho_interval;
+  Norms nm{};
+  bool can_check = false;
+  int it;
+  bool fail = false;
+  for (it = 1; it <= os.max_iter; ++it)
+  {
+    admm_step(c, sv);
+    can_check = os.check_termination && (it % os.check_termination == 0);
+    const int cur = c.s->cur;
+    const double* xc = c.a(cur ? A_XA1 : A_XA0);
+    const double* zc = c.a(cur ? A_Z1 : A_Z0);
+    if (can_check)
+    {
+      compute_residuals(c, xc, zc, Y, nm);
+      if (check_termination(c, nm, false))
+        break;
+    }
+    if (os.adaptive_rho && interval && (it % interval == 0))
+    {
+      if (!can_check)
+        compute_residuals(c, xc, zc, Y, nm);
+      const double rn = rho_estimate(c, nm);
+      const double rho = c.s->rho;
+      if (rn > rho * os.adaptive_rho_tolerance || rn < rho / os.adaptive_rho_tolerance)
+      {
+        BSYNC();
+        if (c.tid == 0)
+          c.s->rho = fmin(fmax(rn, kRhoMin), kRhoMax);
+        BSYNC();
+        const double nr = c.s->rho;
+        double* RH = c.a(A_RHO);
+        const int* TY = c.ia(I_TYPE);
+        FOR(r, L.m)
+        {
+          if (TY[r] == 0)
+            RH[r] = nr;
+          else if (TY[r] == 1)
+            RH[r] = kRhoEq * nr;
+        }
+        BSYNC();
+        if (!factor(c, sv, os.sigma, false, 0.0))
+        {
+          fail = true;
+          break;
+        }
+      }
+    }
+  }
+  if (fail)
+  {
+    if (c.tid == 0)
+    {
+      c.s->qp_status = ST_NONCVX;
+      c.s->prev_status = ST_NONCVX;
+      c.s->iter = it;
+    }
+    BSYNC();
+    return THIP_CVX_FAILED;
+  }
+  const int cur = c.s->cur;
+  double* xc = c.a(cur ? A_XA1 : A_XA0);
+  double* zc = c.a(cur ? A_Z1 : A_Z0);
+  int iters = it;
+  if (!can_check)
+  {
+    iters = it - 1;
+    compute_residuals(c, xc, zc, Y, nm);
+    check_termination(c, nm, false);
+  }
+  if (c.s->qp_status == ST_UNSOLVED)
+  {
+    if (!check_termination(c, nm, true))
+    {
+      if (c.tid == 0)
+        c.s->qp_status = ST_MAXIT;
+      BSYNC();
+    }
+  }
+  if (os.polishing && c.s->qp_status == ST_SOLVED)
+    polish(c, sv, nm);
+  // store_solution (unscaled) -> warm-start memory
+  const int st = c.s->qp_status;
+  const bool inf = (st == ST_PINF || st == ST_PINF_INACC || st == ST_DINF || st == ST_DINF_INACC);
+  double *SXw = c.a(A_SOLX), *SYw = c.a(A_SOLY);
+  FOR(col, L.n_cols) SXw[col] = inf ? NAN : DS[col] * xc[col];
+  FOR(r, L.m) SYw[r] = inf ? NAN : c.s->cinv * (E[r] * Y[r]);
+  BSYNC();
+  if (c.tid == 0)
+  {
+    c.s->prev_status = st;
+    c.s->prev_rho = c.s->rho;
+    c.s->iter = iters;
+    c.s->n_admm += iters;
+  }
+  BSYNC();
+  if (st == ST_SOLVED || st == ST_SOLVED_INACC)
+    return THIP_CVX_SOLVED;
+  if (inf)
+    return THIP_CVX_INFEASIBLE;
+  return THIP_CVX_FAILED;
+}
+
+// ======================================================================
+// The SQP driver kernel: BasicTrustRegionSQP::optimize per workgroup
+// ======================================================================
+__device__ void sqp_optimize(Ctx& c, Solver& sv)
+{
+  const Layout& L = c.L;
+  const int nx = L.nx, D = L.D;
+  const thip_sqp_params& P = c.d->sqp;
+  double *X = c.a(A_X), *XN = c.a(A_XN);
+  double *COST = c.a(A_COST), *VIOL = c.a(A_VIOL), *NCOST = c.a(A_NCOST), *NVIOL = c.a(A_NVIOL), *MU = c.a(A_MU);
+  const thip_chain& ch = c.d->chain;
+  // getClosestFeasiblePoint(x, 1e-3)
+  FOR(col, nx)
+  {
+    const int j = col % D;
+    const double lb = ch.lower[j], ub = ch.upper[j];
+    const double inset = fmin(1e-3, (ub - lb) / 2);
+    X[col] = fmin(fmax(X[col], lb + inset), ub - inset);
+  }
+  FOR(i, L.n_cnts) MU[i] = P.initial_merit_error_coeff;
+  if (c.tid == 0)
+  {
+    c.s->trust = P.trust_box_size;
+    c.s->status = THIP_OPT_INVALID;
+    c.s->n_sqp = c.s->n_qp = c.s->n_fev = c.s->n_merit = 0;
+    c.s->n_admm = 0;
+    c.s->prev_status = 0;
+    c.s->prev_rho = c.d->osqp.rho;
+  }
+  BSYNC();
+  int* mask = c.ia(I_MASK);
+  int* pmask = c.ia(I_PMASK);
+  bool have_prev_setup = false;
+  bool first_eval = true;
+  int retval = THIP_OPT_INVALID;
+  for (int mi = 0; mi < P.max_merit_coeff_increases; ++mi)
+  {
+    bool goto_penalty = false, goto_cleanup = false;
+    for (int iter = 1;; ++iter)
+    {
+      if (c.tid == 0)
+        c.s->n_sqp++;
+      if (first_eval)
+      {
+        evaluate(c, X, COST, VIOL);
+        if (c.tid == 0)
+          c.s->n_fev++;
+        first_eval = false;
+      }
+      // convexify
+      linearize(c, X);
+      build_and_scale(c);
+      // pattern of A (jacobian drops) vs previous QP setup
+      double diff[1] = { 0 };
+      FOR(r, L.n_abs) if (mask[r] != pmask[r]) diff[0] = 1.0;
+      block_max<1>(c, diff);
+      bool pattern_equal = have_prev_setup && diff[0] == 0.0;
+      FOR(r, L.n_abs) pmask[r] = mask[r];
+      have_prev_setup = true;
+      BSYNC();
+      int qp_failures = 0;
+      bool converged_inner = false, failed = false;
+      while (c.s->trust >= P.min_trust_box_size)
+      {
+        const int st = qp_solve(c, sv, pattern_equal);
+        pattern_equal = true;  // same P/A within this SQP iteration
+        if (c.tid == 0)
+          c.s->n_qp++;
+        BSYNC();
+        if (st != THIP_CVX_SOLVED)
+        {
+          if (qp_failures < P.max_qp_solver_failures - 1)
+          {
+            if (c.tid == 0)
+              c.s->trust *= P.trust_shrink_ratio;
+            BSYNC();
+            ++qp_failures;
+            continue;
+          }
+          if (qp_failures == P.max_qp_solver_failures - 1)
+          {
+            if (c.tid == 0)
+              c.s->trust = P.min_trust_box_size;
+            BSYNC();
+            ++qp_failures;
+            continue;
+          }
+          failed = true;
+          break;
+        }
+        // model values at the QP solution (unscaled solution in A_SOLX)
+        const double* SX = c.a(A_SOLX);
+        FOR(col, nx) XN[col] = SX[col];
+        BSYNC();
+        // JointVel model value (quadratic, exact), CartPose model values
+        double jvm = 0;
+        if (c.d->jv_enabled)
+        {
+          const int nv = (L.jv_last - L.jv_first) * D;
+          FOR(i, nv)
+          {
+            const int t = L.jv_first + i / D, j = i % D;
+            const double dd = (XN[(t + 1) * D + j] - XN[t * D + j]) - c.d->jv_targets[j];
+            jvm += (dd * dd) * c.d->jv_coeffs[j];
+          }
+        }
+        jvm = block_sum(c, jvm);
+        double* mcost = c.big;                 // [n_costs]
+        double* mviol = c.big + L.n_costs;     // [n_cnts]
+        if (c.tid == 0 && c.d->jv_enabled)
+          mcost[0] = jvm;
+        const double *G = c.a(A_G), *GC = c.a(A_GC);
+        FOR(k, L.n_cart)
+        {
+          const int r0 = c.T.term_row0[k], nr = c.T.term_nrow[k];
+          double v = 0;
+          if (c.d->cart_is_cnt[k])
+          {
+            const int t = c.d->cart_step[k];
+            for (int rr = 0; rr < nr; ++rr)
+            {
+              const int row = r0 + rr;
+              double a = GC[row];
+              for (int j = 0; j < D; ++j)
+                if (mask[row] & (1 << j))
+                  a += G[row * D + j] * XN[t * D + j];
+              v += fabs(a);
+            }
+            mviol[c.T.term_slot[k]] = v;
+          }
+          else
+          {
+            for (int rr = 0; rr < nr; ++rr)
+            {
+              const int ca = nx + 2 * (r0 + rr);
+              v += SX[ca];
+              v += SX[ca + 1];
+            }
+            mcost[c.T.term_slot[k]] = v;
+          }
+        }
+        BSYNC();
+        evaluate(c, XN, NCOST, NVIOL);
+        int decision = 0;  // 1 converged, 2 shrink, 3 accept
+        if (c.tid == 0)
+        {
+          double oc = 0, mc = 0, nc = 0, ov = 0, mv = 0, nvv = 0;
+          for (int i = 0; i < L.n_costs; ++i)
+          {
+            oc += COST[i];
+            mc += mcost[i];
+            nc += NCOST[i];
+          }
+          for (int i = 0; i < L.n_cnts; ++i)
+          {
+            ov += VIOL[i] * MU[i];
+            mv += mviol[i] * MU[i];
+            nvv += NVIOL[i] * MU[i];
+          }
+          const double old_merit = oc + ov, model_merit = mc + mv, new_merit = nc + nvv;
+          const double approx = old_merit - model_merit;
+          const double exact = old_merit - new_merit;
+          const double ratio = exact / approx;
+          c.s->n_fev++;
+          if (approx < P.min_approx_improve)
+            decision = 1;
+          else if (approx / old_merit < P.min_approx_improve_frac)
+            decision = 1;
+          else if (exact < 0 || ratio < P.improve_ratio_threshold)
+          {
+            decision = 2;
+            c.s->trust *= P.trust_shrink_ratio;
+          }
+          else
+          {
+            decision = 3;
+            c.s->trust *= P.trust_expand_ratio;
+          }
+          c.s->flag = decision;
+        }
+        BSYNC();
+        decision = c.s->flag;
+        BSYNC();
+        if (decision == 1)
+        {
+          converged_inner = true;
+          break;
+        }
+        if (decision == 3)
+        {
+          FOR(col, nx) X[col] = XN[col];
+          FOR(i, L.n_costs) COST[i] = NCOST[i];
+          FOR(i, L.n_cnts) VIOL[i] = NVIOL[i];
+          BSYNC();
+          break;
+        }
+      }
+      if (failed)
+      {
+        retval = THIP_OPT_FAILED;
+        goto_cleanup = true;
+        break;
+      }
+      if (converged_inner)
+      {
+        retval = THIP_OPT_CONVERGED;
+        goto_penalty = true;
+        break;
+      }
+      if (c.s->trust < P.min_trust_box_size)
+      {
+        retval = THIP_OPT_CONVERGED;
+        goto_penalty = true;
+        break;
+      }
+      else if (iter >= P.max_iter)
+      {
+        retval = THIP_OPT_SCO_ITERATION_LIMIT;
+        double vm = -INFINITY;
+        for (int i = 0; i < L.n_cnts; ++i)
+          vm = fmax(vm, VIOL[i]);
+        if (L.n_cnts == 0 || vm < P.cnt_tolerance)
+          retval = THIP_OPT_CONVERGED;
+        goto_cleanup = true;
+        break;
+      }
+    }
+    if (goto_cleanup)
+      break;
+    // penalty adjustment
+    (void)goto_penalty;
+    double vm = -INFINITY;
+    for (int i = 0; i < L.n_cnts; ++i)
+      vm = fmax(vm, VIOL[i]);
+    if (L.n_cnts == 0 || vm < P.cnt_tolerance)
+      goto done;
+    BSYNC();
+    if (c.tid == 0)
+    {
+      for (int i = 0; i < L.n_cnts; ++i)
+        if (!P.inflate_constraints_individually || VIOL[i] > P.cnt_tolerance)
+          MU[i] *= P.merit_coeff_increase_ratio;
+      c.s->trust = fmax(c.s->trust, P.min_trust_box_size / P.trust_shrink_ratio * 1.5);
+      c.s->n_merit++;
+    }
+    BSYNC();
+    if (mi + 1 >= P.max_merit_coeff_increases)
+    {
+      retval = THIP_OPT_PENALTY_ITERATION_LIMIT;
+      goto done;
+    }
+  }
+done:
+  if (c.tid == 0)
+    c.s->status = retval;
+  BSYNC();
+}
+
+__global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
+{
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  __shared__ Ctl ctl;
+  const int b = blockIdx.x;
+  if (b >= args.batch)
+    return;
+  const Layout& L = args.L;
+  Ctx c(L, args.T, args.desc, args.ws + (long long)b * L.dstride, args.iws + (long long)b * L.istride, dyn, &ctl);
+  Solver sv;
+  sv.M = dyn;
+  sv.Nb = dyn + L.N * L.D * L.D;
+  sqp_optimize(c, sv);
+  if (c.tid == 0)
+  {
+    thip_result r{};
+    r.status = ctl.status;
+    r.n_sqp_iters = ctl.n_sqp;
+    r.n_qp_solves = ctl.n_qp;
+    r.n_func_evals = ctl.n_fev;
+    r.n_admm_iters = ctl.n_admm;
+    r.n_merit_increases = ctl.n_merit;
+    double tc = 0;
+    const double* COST = c.a(A_COST);
+    for (int i = 0; i < L.n_costs; ++i)
+      tc += COST[i];
+    r.total_cost = tc;
+    double vm = 0;
+    const double* VIOL = c.a(A_VIOL);
+    for (int i = 0; i < L.n_cnts; ++i)
+      vm = (i == 0) ? VIOL[i] : fmax(vm, VIOL[i]);
+    r.max_cnt_viol = vm;
+    r.final_trust_box = ctl.trust;
+    r.n_costs = L.n_costs;
+    r.n_cnts = L.n_cnts;
+    args.res[b] = r;
+  }
+}
+
+// standalone convexification (thip_linearize): writes rows into err/jac layout
+__global__ __launch_bounds__(kBlock) void linearize_kernel(KernelArgs args, const double* xin, double* err,
+                                                           double* jac)
+{
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  __shared__ Ctl ctl;
+  const int b = blockIdx.x;
+  if (b >= args.batch)
+    return;
+  const Layout& L = args.L;
+  Ctx c(L, args.T, args.desc, args.ws + (long long)b * L.dstride, args.iws + (long long)b * L.istride, dyn, &ctl);
+  const int D = L.D;
+  double* X = c.a(A_XN);
+  FOR(i, L.nx) X[i] = xin[(long long)b * L.nx + i];
+  BSYNC();
+  double* raw = c.a(A_PB);  // scratch (n_cols + m >= n_abs * D)
+  linearize(c, X, raw);
+  FOR(k, L.n_cart)
+  {
+    const int r0 = c.T.term_row0[k], nr = c.T.term_nrow[k];
+    double* eo = err + ((long long)b * L.n_cart + k) * 6;
+    double* jo = jac + ((long long)b * L.n_cart + k) * 6 * D;
+    for (int i = 0; i < 6; ++i)
+    {
+      eo[i] = 0;
+      for (int j = 0; j < D; ++j)
+        jo[i * D + j] = 0;
+    }
+    for (int rr = 0; rr < nr; ++rr)
+    {
+      const int row = r0 + rr;
+      eo[rr] = c.big[30 * k + 24 + c.T.row_comp[row]];
+      for (int j = 0; j < D; ++j)
+        jo[rr * D + j] = raw[row * D + j];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void fwd_kin_kernel(KernelArgs args, const double* xin, double* poses)
+{
+  const int b = blockIdx.x;
+  if (b >= args.batch)
+    return;
+  const Layout& L = args.L;
+  const thip_chain& ch = args.desc->chain;
+  for (int i = threadIdx.x; i < L.N * L.n_links; i += kBlock)
+  {
+    const int t = i / L.n_links, l = i % L.n_links;
+    Pose P;
+    chain_fk(ch, xin + ((long long)b * L.N + t) * L.D, l, P);
+    double* o = poses + (((long long)b * L.N + t) * L.n_links + l) * 12;
+    for (int r = 0; r < 3; ++r)
+    {
+      for (int k = 0; k < 3; ++k)
+        o[r * 4 + k] = P.r[r * 3 + k];
+      o[r * 4 + 3] = P.t[r];
+    }
+  }
+}
+
+}  // namespace thip

@@ -1,0 +1,255 @@
+"""ctypes mirror of include/trajopt_hip.h and the loader of the HIP library.
+
+The HIP library (libtrajopt_hip.so, built in-tree by __graft_entry__.build())
+is the only compute path. `load_hip()` raises if it is missing: there is no
+CPU fallback anywhere in the product.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+MAX_DOF = 8
+MAX_LINKS = 24
+MAX_STEPS = 64
+MAX_CART = 64
+MAX_SPHERES = 32
+MAX_PRIMS = 16
+
+JOINT_FIXED, JOINT_REVOLUTE, JOINT_CONTINUOUS, JOINT_PRISMATIC = 0, 1, 2, 3
+PRIM_SPHERE, PRIM_BOX, PRIM_CAPSULE = 0, 1, 2
+
+OPT_STATUS = {
+    0: "OPT_CONVERGED",
+    1: "OPT_SCO_ITERATION_LIMIT",
+    2: "OPT_PENALTY_ITERATION_LIMIT",
+    3: "OPT_TIME_LIMIT",
+    4: "OPT_FAILED",
+    5: "INVALID",
+}
+
+_D12 = C.c_double * 12
+_D3 = C.c_double * 3
+
+
+class Chain(C.Structure):
+    _fields_ = [
+        ("n_links", C.c_int),
+        ("n_dof", C.c_int),
+        ("base_pose", C.c_double * 12),
+        ("joint_type", C.c_int * MAX_LINKS),
+        ("joint_dof", C.c_int * MAX_LINKS),
+        ("joint_origin", _D12 * MAX_LINKS),
+        ("joint_axis", _D3 * MAX_LINKS),
+        ("lower", C.c_double * MAX_DOF),
+        ("upper", C.c_double * MAX_DOF),
+    ]
+
+
+class SqpParams(C.Structure):
+    _fields_ = [
+        ("improve_ratio_threshold", C.c_double),
+        ("min_trust_box_size", C.c_double),
+        ("min_approx_improve", C.c_double),
+        ("min_approx_improve_frac", C.c_double),
+        ("max_iter", C.c_int),
+        ("trust_shrink_ratio", C.c_double),
+        ("trust_expand_ratio", C.c_double),
+        ("cnt_tolerance", C.c_double),
+        ("max_merit_coeff_increases", C.c_double),
+        ("max_qp_solver_failures", C.c_int),
+        ("merit_coeff_increase_ratio", C.c_double),
+        ("initial_merit_error_coeff", C.c_double),
+        ("inflate_constraints_individually", C.c_int),
+        ("trust_box_size", C.c_double),
+    ]
+
+
+class OsqpSettings(C.Structure):
+    _fields_ = [
+        ("rho", C.c_double),
+        ("sigma", C.c_double),
+        ("alpha", C.c_double),
+        ("scaling", C.c_int),
+        ("adaptive_rho", C.c_int),
+        ("adaptive_rho_interval", C.c_int),
+        ("adaptive_rho_tolerance", C.c_double),
+        ("max_iter", C.c_int),
+        ("eps_abs", C.c_double),
+        ("eps_rel", C.c_double),
+        ("eps_prim_inf", C.c_double),
+        ("eps_dual_inf", C.c_double),
+        ("check_termination", C.c_int),
+        ("warm_starting", C.c_int),
+        ("polishing", C.c_int),
+        ("delta", C.c_double),
+        ("polish_refine_iter", C.c_int),
+    ]
+
+
+class ProblemDesc(C.Structure):
+    _fields_ = [
+        ("n_steps", C.c_int),
+        ("chain", Chain),
+        ("n_fixed", C.c_int),
+        ("fixed_steps", C.c_int * MAX_STEPS),
+        ("jv_enabled", C.c_int),
+        ("jv_first_step", C.c_int),
+        ("jv_last_step", C.c_int),
+        ("jv_coeffs", C.c_double * MAX_DOF),
+        ("jv_targets", C.c_double * MAX_DOF),
+        ("n_cart", C.c_int),
+        ("cart_step", C.c_int * MAX_CART),
+        ("cart_is_cnt", C.c_int * MAX_CART),
+        ("cart_source_link", C.c_int * MAX_CART),
+        ("cart_source_offset", _D12 * MAX_CART),
+        ("cart_pos_coeffs", _D3 * MAX_CART),
+        ("cart_rot_coeffs", _D3 * MAX_CART),
+        ("coll_enabled", C.c_int),
+        ("coll_is_cnt", C.c_int),
+        ("coll_first_step", C.c_int),
+        ("coll_last_step", C.c_int),
+        ("coll_n_fixed", C.c_int),
+        ("coll_fixed_steps", C.c_int * MAX_STEPS),
+        ("coll_margin", C.c_double),
+        ("coll_coeff", C.c_double),
+        ("coll_buffer", C.c_double),
+        ("coll_lvs", C.c_double),
+        ("n_spheres", C.c_int),
+        ("sphere_link", C.c_int * MAX_SPHERES),
+        ("sphere_center", _D3 * MAX_SPHERES),
+        ("sphere_radius", C.c_double * MAX_SPHERES),
+        ("n_prims", C.c_int),
+        ("sqp", SqpParams),
+        ("osqp", OsqpSettings),
+    ]
+
+
+class Result(C.Structure):
+    _fields_ = [
+        ("status", C.c_int),
+        ("n_sqp_iters", C.c_int),
+        ("n_qp_solves", C.c_int),
+        ("n_func_evals", C.c_int),
+        ("n_admm_iters", C.c_longlong),
+        ("n_merit_increases", C.c_int),
+        ("total_cost", C.c_double),
+        ("max_cnt_viol", C.c_double),
+        ("final_trust_box", C.c_double),
+        ("n_costs", C.c_int),
+        ("n_cnts", C.c_int),
+    ]
+
+
+def default_sqp_params() -> SqpParams:
+    """sco::BasicTrustRegionSQPParameters defaults (optimizers.hpp:92-135)."""
+    p = SqpParams()
+    p.improve_ratio_threshold = 0.25
+    p.min_trust_box_size = 1e-4
+    p.min_approx_improve = 1e-4
+    p.min_approx_improve_frac = -1.7976931348623157e308
+    p.max_iter = 50
+    p.trust_shrink_ratio = 0.1
+    p.trust_expand_ratio = 1.5
+    p.cnt_tolerance = 1e-4
+    p.max_merit_coeff_increases = 5
+    p.max_qp_solver_failures = 3
+    p.merit_coeff_increase_ratio = 10
+    p.initial_merit_error_coeff = 10
+    p.inflate_constraints_individually = 1
+    p.trust_box_size = 1e-1
+    return p
+
+
+def default_osqp_settings() -> OsqpSettings:
+    """OSQP 1.0 defaults + OSQPModelConfig::setDefaultOSQPSettings overrides
+    (trajopt_sco/src/osqp_interface.cpp:78-90)."""
+    s = OsqpSettings()
+    s.rho = 0.1
+    s.sigma = 1e-6
+    s.alpha = 1.6
+    s.scaling = 10
+    s.adaptive_rho = 1
+    s.adaptive_rho_interval = 0
+    s.adaptive_rho_tolerance = 5.0
+    s.max_iter = 8192
+    s.eps_abs = 1e-4
+    s.eps_rel = 1e-6
+    s.eps_prim_inf = 1e-4
+    s.eps_dual_inf = 1e-4
+    s.check_termination = 25
+    s.warm_starting = 1
+    s.polishing = 1
+    s.delta = 1e-6
+    s.polish_refine_iter = 3
+    return s
+
+
+PKG_DIR = Path(__file__).resolve().parent.parent          # trajopt-1_amd/
+LIB_DIR = PKG_DIR / "lib"
+HIP_LIB = LIB_DIR / "libtrajopt_hip.so"
+
+_hip = None
+
+
+def _declare(lib):
+    P = C.POINTER
+    vp = C.c_void_p
+    dp = P(C.c_double)
+    lib.thip_create.argtypes = [C.c_int, P(ProblemDesc), C.c_int, P(vp)]
+    lib.thip_create.restype = C.c_int
+    lib.thip_set_stream.argtypes = [vp, vp]
+    lib.thip_set_stream.restype = C.c_int
+    lib.thip_upload.argtypes = [vp, dp, dp, dp]
+    lib.thip_upload.restype = C.c_int
+    lib.thip_upload_device.argtypes = [vp, vp, vp, vp]
+    lib.thip_upload_device.restype = C.c_int
+    lib.thip_sqp_run.argtypes = [vp]
+    lib.thip_sqp_run.restype = C.c_int
+    lib.thip_linearize.argtypes = [vp, dp, dp, dp]
+    lib.thip_linearize.restype = C.c_int
+    lib.thip_fwd_kin.argtypes = [vp, dp, dp]
+    lib.thip_fwd_kin.restype = C.c_int
+    lib.thip_download.argtypes = [vp, dp, P(Result)]
+    lib.thip_download.restype = C.c_int
+    lib.thip_device_x.argtypes = [vp]
+    lib.thip_device_x.restype = vp
+    lib.thip_last_kernel_ms.argtypes = [vp]
+    lib.thip_last_kernel_ms.restype = C.c_double
+    lib.thip_destroy.argtypes = [vp]
+    lib.thip_destroy.restype = None
+    lib.thip_last_error.argtypes = [vp]
+    lib.thip_last_error.restype = C.c_char_p
+    lib.thip_build_info.argtypes = []
+    lib.thip_build_info.restype = C.c_char_p
+    lib.thip_default_sqp_params.argtypes = [P(SqpParams)]
+    lib.thip_default_sqp_params.restype = None
+    lib.thip_default_osqp_settings.argtypes = [P(OsqpSettings)]
+    lib.thip_default_osqp_settings.restype = None
+    lib.thip_sizeof_desc.argtypes = []
+    lib.thip_sizeof_desc.restype = C.c_int
+    return lib
+
+
+def load_hip():
+    """Load the in-tree HIP library. Raises if it has not been built: the
+    product has no fallback path."""
+    global _hip
+    if _hip is None:
+        if not HIP_LIB.exists():
+            raise RuntimeError(
+                f"{HIP_LIB} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)"
+            )
+        _hip = _declare(C.CDLL(str(HIP_LIB)))
+        if _hip.thip_sizeof_desc() != C.sizeof(ProblemDesc):
+            raise RuntimeError("thip_problem_desc layout mismatch between Python and the HIP library")
+    return _hip
+
+
+def exported_symbols():
+    """Function names declared in include/trajopt_hip.h."""
+    import re
+
+    hdr = (PKG_DIR.parent / "include" / "trajopt_hip.h").read_text()
+    return sorted(set(re.findall(r"\b(thip_[a-z_]+)\s*\(", hdr)))

@@ -1,0 +1,172 @@
+"""Synthetic batched workloads, deterministic per problem.
+
+Each problem b draws from splitmix64 seeded with 20261015 + b:
+  * a reference joint path q_ref(t) = q_mid + a * sin(2 pi t / (N-1) + phi),
+    a ~ U(0.1, 0.4) * range, phi ~ U(0, 2 pi), clipped 0.05 inside the limits
+    (continuous joints use [-pi, pi] as their range);
+  * CartPose targets = FK(q_ref(t)) of the tool frame expressed in the chain
+    root (torso_lift_link, static), i.e. the target-frame offset pose;
+  * the initial trajectory: joint-interpolated q_ref(0) -> q_ref(N-1) plus
+    N(0, 0.02) noise on interior steps; fixed_timesteps = [0].
+
+Configs (BASELINE.json):
+  A  7-DoF PR2 right arm, 10 steps, JointVel cost + one CartPose EQ constraint
+     at the last step (target = FK(q_ref(mid-horizon)), a reaching problem).
+  B  30 steps, JointVel cost + CartPose ABS costs at t = 1..29 (tracking).
+  C  B + 10-primitive scene + LVS-discrete collision cost.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import abi
+from .robots import PR2_TOOL_LINK, chain_limits, fwd_kin, pr2_right_arm
+
+SEED_BASE = 20261015
+_MASK = (1 << 64) - 1
+
+
+class SplitMix64:
+    def __init__(self, seed: int):
+        self.s = seed & _MASK
+
+    def next(self) -> int:
+        self.s = (self.s + 0x9E3779B97F4A7C15) & _MASK
+        z = self.s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _MASK
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _MASK
+        return z ^ (z >> 31)
+
+    def uniform(self, lo=0.0, hi=1.0) -> float:
+        return lo + (hi - lo) * ((self.next() >> 11) * (1.0 / 9007199254740992.0))
+
+    def normal(self, sigma=1.0) -> float:
+        u1 = self.uniform()
+        u2 = self.uniform()
+        u1 = max(u1, 1e-300)
+        return sigma * math.sqrt(-2.0 * math.log(u1)) * math.cos(2.0 * math.pi * u2)
+
+
+@dataclass
+class Workload:
+    name: str
+    desc: abi.ProblemDesc
+    init: np.ndarray      # [B, N, D]
+    targets: np.ndarray   # [B, n_cart, 12]
+    scene: np.ndarray     # [B, n_prims, 16]
+    q_ref: np.ndarray     # [B, N, D]
+
+    @property
+    def batch(self):
+        return self.init.shape[0]
+
+    @property
+    def n_steps(self):
+        return self.init.shape[1]
+
+    @property
+    def n_dof(self):
+        return self.init.shape[2]
+
+    def slice(self, lo, hi):
+        return Workload(self.name, self.desc, self.init[lo:hi].copy(), self.targets[lo:hi].copy(),
+                        self.scene[lo:hi].copy(), self.q_ref[lo:hi].copy())
+
+
+def _ref_path(rng: SplitMix64, lo, hi, types, n_steps):
+    D = len(lo)
+    q_lo = np.where(types == abi.JOINT_CONTINUOUS, -math.pi, lo)
+    q_hi = np.where(types == abi.JOINT_CONTINUOUS, math.pi, hi)
+    mid = 0.5 * (q_lo + q_hi)
+    rng_ = q_hi - q_lo
+    a = np.array([rng.uniform(0.1, 0.4) for _ in range(D)]) * rng_
+    phi = np.array([rng.uniform(0.0, 2 * math.pi) for _ in range(D)])
+    t = np.arange(n_steps)[:, None]
+    q = mid[None, :] + a[None, :] * np.sin(2 * math.pi * t / (n_steps - 1) + phi[None, :])
+    return np.clip(q, q_lo + 0.05, q_hi - 0.05)
+
+
+def _pose12_in_root(chain, q, link):
+    T = fwd_kin(chain, q)
+    rel = np.linalg.inv(T[0]) @ T[link]
+    return rel[:3, :].reshape(12)
+
+
+def base_desc(n_steps: int) -> abi.ProblemDesc:
+    d = abi.ProblemDesc()
+    d.n_steps = n_steps
+    d.chain = pr2_right_arm()
+    d.n_fixed = 1
+    d.fixed_steps[0] = 0
+    d.jv_enabled = 1
+    d.jv_first_step = 0
+    d.jv_last_step = -1
+    for j in range(d.chain.n_dof):
+        d.jv_coeffs[j] = 1.0
+        d.jv_targets[j] = 0.0
+    d.sqp = abi.default_sqp_params()
+    d.osqp = abi.default_osqp_settings()
+    return d
+
+
+def _add_cart(d, k, step, is_cnt):
+    d.cart_step[k] = step
+    d.cart_is_cnt[k] = 1 if is_cnt else 0
+    d.cart_source_link[k] = PR2_TOOL_LINK
+    eye = [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0]
+    for i in range(12):
+        d.cart_source_offset[k][i] = eye[i]
+    for i in range(3):
+        d.cart_pos_coeffs[k][i] = 1.0
+        d.cart_rot_coeffs[k][i] = 1.0
+
+
+def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int | None = None) -> Workload:
+    config = config.upper()
+    if config == "A":
+        N = n_steps or 10
+    elif config in ("B", "C"):
+        N = n_steps or 30
+    else:
+        raise ValueError(f"unknown config {config}")
+    d = base_desc(N)
+    chain = d.chain
+    lo, hi, types = chain_limits(chain)
+    D = chain.n_dof
+    if config == "A":
+        d.n_cart = 1
+        _add_cart(d, 0, N - 1, True)
+    else:
+        d.n_cart = N - 1
+        for k, t in enumerate(range(1, N)):
+            _add_cart(d, k, t, False)
+    if config == "C":
+        from .scene import add_collision_model
+        add_collision_model(d)
+
+    init = np.zeros((batch, N, D))
+    targets = np.zeros((batch, d.n_cart, 12))
+    q_refs = np.zeros((batch, N, D))
+    scene = np.zeros((batch, max(d.n_prims, 0), 16))
+    for b in range(batch):
+        rng = SplitMix64(SEED_BASE + first_problem + b)
+        q_ref = _ref_path(rng, lo, hi, types, N)
+        q_refs[b] = q_ref
+        start, end = q_ref[0], q_ref[N - 1]
+        for t in range(N):
+            init[b, t] = start + (end - start) * (t / (N - 1))
+        for t in range(1, N - 1):
+            for j in range(D):
+                init[b, t, j] += rng.normal(0.02)
+        if config == "A":
+            targets[b, 0] = _pose12_in_root(chain, q_ref[(N - 1) // 2], PR2_TOOL_LINK)
+        else:
+            for k in range(d.n_cart):
+                targets[b, k] = _pose12_in_root(chain, q_ref[d.cart_step[k]], PR2_TOOL_LINK)
+        if config == "C":
+            from .scene import make_scene
+            scene[b] = make_scene(rng, chain, q_ref, d)
+    return Workload(config, d, init, targets, scene, q_refs)

@@ -1,0 +1,126 @@
+"""Robot kinematic chains used by the synthetic workloads.
+
+PR2 right arm: the reference's `right_arm` group (chain torso_lift_link ->
+r_gripper_tool_frame, trajopt_common/data/pr2.srdf:15-17) with the joint data
+of trajopt_common/data/arm_around_table.urdf (shoulder_pan 1479-1485,
+shoulder_lift 1513-1523, upper_arm_roll 1545-1550, elbow_flex 1702-1712,
+forearm_roll 1655-1664, wrist_flex 1779-1788, wrist_roll 1811-1820, tool
+1908-1911; base chain base_footprint->base_link 121-124, torso 735-744 with
+the torso joint at 0).  Continuous joints get +-4 pi variable bounds.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from .abi import JOINT_CONTINUOUS, JOINT_FIXED, JOINT_REVOLUTE, Chain
+
+
+def _pose(xyz=(0.0, 0.0, 0.0)):
+    p = np.zeros(12)
+    p[0] = p[5] = p[10] = 1.0
+    p[3], p[7], p[11] = xyz
+    return p
+
+
+# (name, type, origin xyz, axis, (lower, upper))
+PR2_RIGHT_ARM = [
+    ("r_shoulder_pan_joint", JOINT_REVOLUTE, (0.0, -0.188, 0.0), (0, 0, 1), (-2.2853981634, 0.714601836603)),
+    ("r_shoulder_lift_joint", JOINT_REVOLUTE, (0.1, 0.0, 0.0), (0, 1, 0), (-0.5236, 1.3963)),
+    ("r_upper_arm_roll_joint", JOINT_REVOLUTE, (0.0, 0.0, 0.0), (1, 0, 0), (-3.9, 0.8)),
+    ("r_upper_arm_joint", JOINT_FIXED, (0.0, 0.0, 0.0), None, None),
+    ("r_elbow_flex_joint", JOINT_REVOLUTE, (0.4, 0.0, 0.0), (0, 1, 0), (-2.3213, 0.0)),
+    ("r_forearm_roll_joint", JOINT_CONTINUOUS, (0.0, 0.0, 0.0), (1, 0, 0), (-4 * math.pi, 4 * math.pi)),
+    ("r_forearm_joint", JOINT_FIXED, (0.0, 0.0, 0.0), None, None),
+    ("r_wrist_flex_joint", JOINT_REVOLUTE, (0.321, 0.0, 0.0), (0, 1, 0), (-2.18, 0.0)),
+    ("r_wrist_roll_joint", JOINT_CONTINUOUS, (0.0, 0.0, 0.0), (1, 0, 0), (-4 * math.pi, 4 * math.pi)),
+    ("r_gripper_palm_joint", JOINT_FIXED, (0.0, 0.0, 0.0), None, None),
+    ("r_gripper_tool_joint", JOINT_FIXED, (0.18, 0.0, 0.0), None, None),
+]
+# world pose of torso_lift_link: base_footprint -> base_link (0,0,0.051) -> torso (-0.05,0,0.739675), q_torso = 0
+PR2_TORSO_WORLD = (-0.05, 0.0, 0.051 + 0.739675)
+PR2_TOOL_LINK = 11  # r_gripper_tool_frame
+
+
+def pr2_right_arm() -> Chain:
+    c = Chain()
+    c.n_links = len(PR2_RIGHT_ARM) + 1
+    base = _pose(PR2_TORSO_WORLD)
+    for i in range(12):
+        c.base_pose[i] = base[i]
+    dof = 0
+    for k, (_, jtype, xyz, axis, lim) in enumerate(PR2_RIGHT_ARM, start=1):
+        c.joint_type[k] = jtype
+        o = _pose(xyz)
+        for i in range(12):
+            c.joint_origin[k][i] = o[i]
+        if jtype == JOINT_FIXED:
+            c.joint_dof[k] = -1
+        else:
+            c.joint_dof[k] = dof
+            for i in range(3):
+                c.joint_axis[k][i] = axis[i]
+            c.lower[dof], c.upper[dof] = lim
+            dof += 1
+    c.n_dof = dof
+    c.joint_dof[0] = -1
+    return c
+
+
+def chain_limits(c: Chain):
+    lo = np.array([c.lower[i] for i in range(c.n_dof)])
+    hi = np.array([c.upper[i] for i in range(c.n_dof)])
+    types = []
+    for k in range(1, c.n_links):
+        if c.joint_type[k] != JOINT_FIXED:
+            types.append(c.joint_type[k])
+    return lo, hi, np.array(types)
+
+
+# ---------------------------------------------------------------- numpy FK
+def _axis_angle(axis, angle):
+    """Eigen AngleAxis::toRotationMatrix."""
+    ax = np.asarray(axis, dtype=float)
+    s, c = math.sin(angle), math.cos(angle)
+    sa = s * ax
+    ca = (1 - c) * ax
+    R = np.zeros((3, 3))
+    t = ca[0] * ax[1]
+    R[0, 1] = t - sa[2]
+    R[1, 0] = t + sa[2]
+    t = ca[0] * ax[2]
+    R[0, 2] = t + sa[1]
+    R[2, 0] = t - sa[1]
+    t = ca[1] * ax[2]
+    R[1, 2] = t - sa[0]
+    R[2, 1] = t + sa[0]
+    R[0, 0] = ca[0] * ax[0] + c
+    R[1, 1] = ca[1] * ax[1] + c
+    R[2, 2] = ca[2] * ax[2] + c
+    return R
+
+
+def _to44(p12):
+    T = np.eye(4)
+    T[:3, :] = np.asarray(p12, dtype=float).reshape(3, 4)
+    return T
+
+
+def fwd_kin(c: Chain, q):
+    """World pose (4x4) of every link at joint values q (host-side helper for
+    data generation only)."""
+    T = [_to44(list(c.base_pose))]
+    for k in range(1, c.n_links):
+        t = T[-1] @ _to44(list(c.joint_origin[k]))
+        jt = c.joint_type[k]
+        if jt in (JOINT_REVOLUTE, JOINT_CONTINUOUS):
+            M = np.eye(4)
+            M[:3, :3] = _axis_angle(list(c.joint_axis[k]), q[c.joint_dof[k]])
+            t = t @ M
+        elif jt != JOINT_FIXED:
+            M = np.eye(4)
+            M[:3, 3] = np.asarray(list(c.joint_axis[k])) * q[c.joint_dof[k]]
+            t = t @ M
+        T.append(t)
+    return T

@@ -1,0 +1,99 @@
+"""BatchTrustRegionSQP over the C-ABI (the batched tier of SURVEY.md §8b).
+
+Lowers a Workload (one shared thip_problem_desc + per-problem arrays) onto one
+HIP device and runs sco::BasicTrustRegionSQP::optimize for every problem in
+one fused launch.  No CPU fallback: every method raises if the HIP library or
+the device call fails.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class HipError(RuntimeError):
+    pass
+
+
+class BatchTrustRegionSQP:
+    def __init__(self, workload, device: int = 0, stream=None):
+        self.lib = abi.load_hip()
+        self.wl = workload
+        self.batch = workload.batch
+        self.ctx = C.c_void_p()
+        rc = self.lib.thip_create(device, C.byref(workload.desc), self.batch, C.byref(self.ctx))
+        if rc != 0:
+            raise HipError(f"thip_create: {self.lib.thip_last_error(None).decode()}")
+        if stream is not None:
+            self._check(self.lib.thip_set_stream(self.ctx, C.c_void_p(stream)), "thip_set_stream")
+        self.uploaded = False
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise HipError(f"{what}: {self.lib.thip_last_error(self.ctx).decode()}")
+
+    def upload(self):
+        wl = self.wl
+        self._init = np.ascontiguousarray(wl.init, dtype=np.float64)
+        self._tgt = np.ascontiguousarray(wl.targets, dtype=np.float64) if wl.targets.size else None
+        self._scene = np.ascontiguousarray(wl.scene, dtype=np.float64) if wl.scene.size else None
+        self._check(
+            self.lib.thip_upload(self.ctx, _dp(self._init), _dp(self._tgt) if self._tgt is not None else None,
+                                 _dp(self._scene) if self._scene is not None else None),
+            "thip_upload",
+        )
+        self.uploaded = True
+
+    def run(self):
+        if not self.uploaded:
+            self.upload()
+        self._check(self.lib.thip_sqp_run(self.ctx), "thip_sqp_run")
+
+    def kernel_ms(self) -> float:
+        return float(self.lib.thip_last_kernel_ms(self.ctx))
+
+    def download(self):
+        x = np.zeros((self.batch, self.wl.n_steps, self.wl.n_dof))
+        res = (abi.Result * self.batch)()
+        self._check(self.lib.thip_download(self.ctx, _dp(x), res), "thip_download")
+        return x, list(res)
+
+    def optimize(self):
+        self.run()
+        return self.download()
+
+    def linearize(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        D = self.wl.n_dof
+        n_cart = self.wl.desc.n_cart
+        err = np.zeros((self.batch, n_cart, 6))
+        jac = np.zeros((self.batch, n_cart, 6, D))
+        if not self.uploaded:
+            self.upload()
+        self._check(self.lib.thip_linearize(self.ctx, _dp(x), _dp(err), _dp(jac)), "thip_linearize")
+        return err, jac
+
+    def fwd_kin(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        n_links = self.wl.desc.chain.n_links
+        poses = np.zeros((self.batch, self.wl.n_steps, n_links, 12))
+        self._check(self.lib.thip_fwd_kin(self.ctx, _dp(x), _dp(poses)), "thip_fwd_kin")
+        return poses
+
+    def close(self):
+        if self.ctx:
+            self.lib.thip_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
