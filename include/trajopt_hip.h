@@ -265,6 +265,19 @@ const char* thip_build_info(void);
 /* sizeof(thip_problem_desc) as compiled into the library (ABI check). */
 int thip_sizeof_desc(void);
 
+/* Diagnostics: record one 10-double entry per QP solve of every problem
+ * (warm_started, rho_initial, admm_iters, osqp_status, polish_status,
+ * rho_final, prim_res, dual_res, sum|x*|, trust_box) during thip_sqp_run,
+ * up to `capacity` entries per problem (0 disables). */
+int thip_debug_trace(thip_ctx* ctx, int capacity);
+/* records [batch][capacity][10], counts [batch] */
+int thip_debug_get_trace(thip_ctx* ctx, double* records, int* counts);
+/* Diagnostics: workspace layout (array offsets in doubles / ints, and
+ * dims = {N, D, nx, n_fixed_rows, n_abs, n_cols, n_rows, m, dstride, istride,
+ * n_double_arrays, n_int_arrays}) and a copy of the device workspace. */
+int thip_debug_layout(thip_ctx* ctx, long long* doff, long long* ioff, long long* dims);
+int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws);
+
 #ifdef __cplusplus
 }
 #endif

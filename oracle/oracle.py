@@ -80,6 +80,25 @@ def solve(wl, n_threads=1):
     return x, list(res)
 
 
+def solve_trace(wl, b, cap=2048):
+    """Problem b with its per-QP trace records (see oracle_solve_trace)."""
+    L = lib()
+    L.oracle_solve_trace.argtypes = [C.POINTER(abi.ProblemDesc), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                     C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(abi.Result),
+                                     C.POINTER(C.c_double), C.c_int]
+    L.oracle_solve_trace.restype = C.c_int
+    init = np.ascontiguousarray(wl.init[b], dtype=np.float64)
+    tg = np.ascontiguousarray(wl.targets[b], dtype=np.float64) if wl.targets.size else None
+    sc = np.ascontiguousarray(wl.scene[b], dtype=np.float64) if wl.scene.size else None
+    x = np.zeros_like(init)
+    res = abi.Result()
+    rec = np.zeros((cap, 10))
+    n = L.oracle_solve_trace(C.byref(wl.desc), _dp(init), _dp(tg), _dp(sc), _dp(x), C.byref(res), _dp(rec), cap)
+    if n < 0:
+        raise RuntimeError(L.oracle_last_error().decode())
+    return x, res, rec[:n]
+
+
 def linearize(wl, x):
     L = lib()
     B = wl.batch

@@ -134,6 +134,42 @@ int oracle_linearize(const thip_problem_desc* d, int batch, const double* x, con
   return 0;
 }
 
+// one problem with a per-QP trace: rec[cap][10] =
+// (warm, rho0, iters, status, polish, rho1, prim_res, dual_res, sum|x|, trust_box); returns #records
+int oracle_solve_trace(const thip_problem_desc* d, const double* init, const double* targets, const double* scene,
+                       double* out_x, thip_result* res, double* rec, int cap)
+{
+  try
+  {
+    const int N = d->n_steps, D = d->chain.n_dof;
+    TrajProblem tp = constructProblem(*d, init, targets, scene);
+    auto* om = dynamic_cast<OSQPModel*>(tp.prob->getModel().get());
+    std::vector<OSQPModel::Trace> tr;
+    om->trace = &tr;
+    BasicTrustRegionSQP opt(tp.prob);
+    opt.getParameters() = toSqpParams(d->sqp);
+    opt.initialize(tp.init);
+    opt.optimize();
+    om->trace = nullptr;
+    std::memcpy(out_x, opt.results().x.data(), sizeof(double) * static_cast<std::size_t>(N * D));
+    if (res)
+    {
+      res->status = opt.results().status;
+      res->n_sqp_iters = opt.results().n_sqp_iters;
+      res->n_qp_solves = opt.results().n_qp_solves;
+      res->n_admm_iters = opt.results().n_admm_iters;
+    }
+    const int n = std::min<int>(cap, static_cast<int>(tr.size()));
+    std::memcpy(rec, tr.data(), sizeof(double) * 10 * static_cast<std::size_t>(n));
+    return n;
+  }
+  catch (const std::exception& e)
+  {
+    g_err = e.what();
+    return -1;
+  }
+}
+
 // link poses at n configurations: poses [n][n_links][12]
 int oracle_fwd_kin(const thip_chain* chain, int n, const double* q, double* poses)
 {

@@ -369,10 +369,22 @@ CvxOptStatus OSQPModel::optimize()
   }
   catch (const std::exception&)
   {
+    if (trace)
+      trace->push_back({ 0, 0, 0, -1, 0, 0, 0, 0, 0, trace_trust });
     return CVX_FAILED;
   }
+  const double rho0 = ws_->settings().rho;
   const int ret = ws_->solve();
   admm_iters_total += ws_->iter;
+  if (trace)
+  {
+    double xs = 0;
+    for (double v : ws_->sol_x)
+      xs += std::fabs(v);
+    trace->push_back({ last_warm_started ? 1.0 : 0.0, rho0, static_cast<double>(ws_->iter),
+                       static_cast<double>(ws_->status_val), static_cast<double>(ws_->status_polish),
+                       ws_->settings().rho, ws_->prim_res, ws_->dual_res, xs, trace_trust });
+  }
   last_osqp_status = ws_->status_val;
   last_polish_status = ws_->status_polish;
   if (ret == 0)
@@ -985,6 +997,8 @@ OptStatus BasicTrustRegionSQP::optimize()
         while (param_.trust_box_size >= param_.min_trust_box_size)
         {
           setTrustBoxConstraints(results_.x);
+          if (osqp_model)
+            osqp_model->trace_trust = param_.trust_box_size;
           const CvxOptStatus status = model_->optimize();
           ++results_.n_qp_solves;
           if (osqp_model)

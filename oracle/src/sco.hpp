@@ -114,6 +114,12 @@ public:
   VarVector getVars() const override { return vars_; }
 
   // counters the build adds (not in the reference)
+  struct Trace
+  {
+    double warm, rho0, iters, status, polish, rho1, prim, dual, xsum, trust;
+  };
+  std::vector<Trace>* trace = nullptr;
+  double trace_trust = 0;
   long long admm_iters_total = 0;
   int last_osqp_status = 0;
   int last_polish_status = 0;

@@ -126,6 +126,10 @@ struct KernelArgs
   int* iws;
   thip_result* res;
   int batch;
+  // diagnostics: per-QP trace records [batch][trace_cap][10] (null = off)
+  double* trace;
+  int* trace_n;
+  int trace_cap;
 };
 
 }  // namespace thip

@@ -62,6 +62,10 @@ struct Ctl
   double prim_res, dual_res;
   int flag;
   int can_check;
+  // diagnostics
+  double* trace;
+  int trace_cap, trace_n;
+  double rho0;
 };
 
 struct Ctx
@@ -549,8 +553,11 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
   {
     const int ca = nx + 2 * r;
     const double rr = rho_k(c, L.n_fixed_rows + r, polish, delta);
-    const double phi = WS[2 * r] * WS[2 * r] / DG[ca] + WS[2 * r + 1] * WS[2 * r + 1] / DG[ca + 1];
-    RE[r] = rr / (1.0 + rr * phi);
+    // rho_eff = rho dn dp / det(K_aa), det = dn dp + rho (dn wp^2 + dp wn^2):
+    // every term positive, no cancellation even when dn or dp ~ delta
+    const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
+    const double det = dn * dp + rr * (dn * wp * wp + dp * wn * wn);
+    RE[r] = rr * dn * dp / det;
   }
   BSYNC();
   // diagonal blocks
@@ -688,30 +695,43 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
   return ok;
 }
 
-// Solve K [x; aux] = b (b over all n_cols, given in A_BXW for x cols and
-// A_BA for aux cols).  Result in out (n_cols).
-// Aux elimination per CartPose row (Sherman-Morrison on the 2x2 aux block).
-__device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, double* out)
+// Solve K [x; aux] = r + A' eta, with r (n_cols) in A_BXW (overwritten) and
+// eta over all m rows; K = P + diag(sigK) + A' diag(rho) A as in factor().
+// The 2x2 aux block of each CartPose row is eliminated with its explicit
+// inverse, expanded so that the rho^2 and eta_r terms cancel analytically:
+// with polish rho = 1/delta the textbook Sherman-Morrison form subtracts
+// O(1/delta^2) quantities and loses ~12 digits.
+__device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, const double* eta, double* out)
 {
   const Layout& L = c.L;
-  const int D = L.D, nx = L.nx, N = L.N, DD = D * D;
-  const double *GS = c.a(A_GS), *WS = c.a(A_WS), *DG = c.a(A_DG), *RE = c.a(A_RE), *LI = c.a(A_LINV);
+  const int D = L.D, nx = L.nx, N = L.N, DD = D * D, nfr = L.n_fixed_rows;
+  const double *GS = c.a(A_GS), *WS = c.a(A_WS), *DG = c.a(A_DG), *LI = c.a(A_LINV), *BS = c.a(A_BS),
+               *FS = c.a(A_FS);
   double *BX = c.a(A_BXW), *BA = c.a(A_BA), *MR = c.a(A_MR), *CV = c.a(A_CV), *YV = c.a(A_YV);
-  // beta_r = RE_r * sum_a w_a b_a / Dg_a
   FOR(r, L.n_abs)
   {
     const int ca = nx + 2 * r;
-    MR[r] = RE[r] * (WS[2 * r] * BA[ca] / DG[ca] + WS[2 * r + 1] * BA[ca + 1] / DG[ca + 1]);
+    const double rr = rho_k(c, nfr + r, polish, delta);
+    const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
+    const double rn = BX[ca] + BS[ca] * eta[bound_row(L, ca)];
+    const double rp = BX[ca + 1] + BS[ca + 1] * eta[bound_row(L, ca + 1)];
+    const double det = dn * dp + rr * (dn * wp * wp + dp * wn * wn);
+    MR[r] = (eta[nfr + r] * dn * dp - rr * (wn * dp * rn + wp * dn * rp)) / det;
+    BA[ca] = rn;
+    BA[ca + 1] = rp;
   }
   BSYNC();
   FOR(col, nx)
   {
     const int t = col / D, j = col % D;
-    double b = BX[col];
+    double b = BX[col] + BS[col] * eta[bound_row(L, col)];
+    const int f = c.T.fixed_of_step[t];
+    if (f >= 0)
+      b += FS[f * D + j] * eta[f * D + j];
     for (int p = c.T.step_ptr[t]; p < c.T.step_ptr[t + 1]; ++p)
     {
       const int r = c.T.step_rows[p];
-      b -= GS[r * D + j] * MR[r];
+      b += GS[r * D + j] * MR[r];
     }
     BX[col] = b;
   }
@@ -784,12 +804,14 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, dou
     double g = 0;
     for (int j = 0; j < D; ++j)
       g += GS[r * D + j] * out[t * D + j];
-    const double rr = rho_k(c, L.n_fixed_rows + r, polish, delta);
-    const double v0 = BA[ca] - rr * WS[2 * r] * g;
-    const double v1 = BA[ca + 1] - rr * WS[2 * r + 1] * g;
-    const double psi = WS[2 * r] * v0 / DG[ca] + WS[2 * r + 1] * v1 / DG[ca + 1];
-    out[ca] = v0 / DG[ca] - (WS[2 * r] / DG[ca]) * RE[r] * psi;
-    out[ca + 1] = v1 / DG[ca + 1] - (WS[2 * r + 1] / DG[ca + 1]) * RE[r] * psi;
+    const double rr = rho_k(c, nfr + r, polish, delta);
+    const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
+    const double rn = BA[ca], rp = BA[ca + 1];
+    const double det = dn * dp + rr * (dn * wp * wp + dp * wn * wn);
+    const double cross = wp * rn - wn * rp;
+    const double h = eta[nfr + r] - rr * g;
+    out[ca] = (dp * rn + rr * wp * cross + wn * dp * h) / det;
+    out[ca + 1] = (dn * rp - rr * wn * cross + wp * dn * h) / det;
   }
   BSYNC();
 }
@@ -1063,7 +1085,6 @@ __device__ bool check_termination(Ctx& c, const Norms& nm, bool approx)
 __device__ void admm_step(Ctx& c, Solver& sv)
 {
   const Layout& L = c.L;
-  const int D = L.D, nx = L.nx;
   const thip_osqp_settings& os = c.d->osqp;
   const double sig = os.sigma, al = os.alpha;
   // swap buffers
@@ -1076,44 +1097,13 @@ __device__ void admm_step(Ctx& c, Solver& sv)
   double* z = c.a(cur ? A_Z1 : A_Z0);
   const double* zp = c.a(cur ? A_Z0 : A_Z1);
   double *Y = c.a(A_Y), *XT = c.a(A_XT), *ZT = c.a(A_ZT), *DX = c.a(A_DX), *DY = c.a(A_DY);
-  double *BX = c.a(A_BXW), *BA = c.a(A_BA);
-  const double *Q = c.a(A_Q), *BS = c.a(A_BS), *RH = c.a(A_RHO), *Lo = c.a(A_L), *Up = c.a(A_U);
-  const double *FS = c.a(A_FS), *GS = c.a(A_GS), *WS = c.a(A_WS);
-  double* MRt = c.a(A_PZ);  // eta of structural rows (scratch)
-  // eta_r = rho_r zp_r - y_r for structural rows, and aux right-hand sides
-  FOR(r, L.n_rows)
-  {
-    const double eta = RH[r] * zp[r] - Y[r];
-    MRt[r] = eta;
-    if (r >= L.n_fixed_rows)
-    {
-      const int a = r - L.n_fixed_rows, ca = nx + 2 * a;
-      for (int sd = 0; sd < 2; ++sd)
-      {
-        const int col = ca + sd, br = bound_row(L, col);
-        const double etab = RH[br] * zp[br] - Y[br];
-        BA[col] = sig * xp[col] - Q[col] + BS[col] * etab + WS[2 * a + sd] * eta;
-      }
-    }
-  }
+  double* BX = c.a(A_BXW);
+  const double *Q = c.a(A_Q), *RH = c.a(A_RHO), *Lo = c.a(A_L), *Up = c.a(A_U);
+  double* ETA = c.a(A_PZ);  // eta = rho zp - y over all rows (scratch)
+  FOR(r, L.m) ETA[r] = RH[r] * zp[r] - Y[r];
+  FOR(col, L.n_cols) BX[col] = sig * xp[col] - Q[col];
   BSYNC();
-  FOR(col, nx)
-  {
-    const int t = col / D, j = col % D, br = bound_row(L, col);
-    const double etab = RH[br] * zp[br] - Y[br];
-    double b = sig * xp[col] - Q[col] + BS[col] * etab;
-    const int f = c.T.fixed_of_step[t];
-    if (f >= 0)
-      b += FS[f * D + j] * MRt[f * D + j];
-    for (int p = c.T.step_ptr[t]; p < c.T.step_ptr[t + 1]; ++p)
-    {
-      const int a = c.T.step_rows[p];
-      b += GS[a * D + j] * MRt[L.n_fixed_rows + a];
-    }
-    BX[col] = b;
-  }
-  BSYNC();
-  reduced_solve(c, sv, false, 0.0, XT);
+  reduced_solve(c, sv, false, 0.0, ETA, XT);
   // z tilde = A x tilde; updates
   FOR(r, L.m)
   {
@@ -1180,45 +1170,40 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
   }
   // PB = [b_x (n_cols); b_y (m)], PS = solution [x; y], PR = residual
   double *PB = c.a(A_PB), *PS = c.a(A_PS), *PR = c.a(A_PR), *PZ = c.a(A_PZ);
-  double *BX = c.a(A_BXW), *BA = c.a(A_BA), *XT = c.a(A_XT);
-  const int nc = L.n_cols, nx = L.nx, D = L.D;
-  FOR(col, nc) PB[col] = -Q[col];
-  FOR(r, L.m) PB[nc + r] = (ACT[r] < 0) ? Lo[r] : ((ACT[r] > 0) ? Up[r] : 0.0);
-  FOR(k, nc + L.m) PR[k] = PB[k];
-  FOR(k, nc + L.m) PS[k] = 0.0;
+  double *BX = c.a(A_BXW), *XT = c.a(A_XT);
+  const int nc = L.n_cols;
+  FOR(col, nc)
+  {
+    PB[col] = -Q[col];
+    PR[col] = -Q[col];
+    PS[col] = 0.0;
+  }
+  FOR(r, L.m)
+  {
+    const double b = (ACT[r] < 0) ? Lo[r] : ((ACT[r] > 0) ? Up[r] : 0.0);
+    PB[nc + r] = b;
+    PR[nc + r] = b;
+    PS[nc + r] = 0.0;
+  }
   BSYNC();
-  const double *BS = c.a(A_BS), *FS = c.a(A_FS), *GS = c.a(A_GS), *WS = c.a(A_WS);
-  for (int it = 0; it <= os.polish_refine_iter; ++it)
+  // OSQP refines polish_refine_iter times with an LDL factor of the
+  // quasi-definite KKT.  The waypoint-block normal-equation solve used here is
+  // a weaker preconditioner for the same iteration (its dual part is formed as
+  // (A dx - r_y) / delta), so refinement continues until the unregularised KKT
+  // residual stops decreasing: both converge to the same polished KKT point.
+  double rnorm_prev = INFINITY;
+  double bscale[1] = { 0 };
+  FOR(k, nc + L.m) bscale[0] = fmax(bscale[0], fabs(PB[k]));
+  block_max<1>(c, bscale);
+  const int max_refine = os.polish_refine_iter + 24;
+  for (int it = 0; it <= max_refine; ++it)
   {
     // solve K_delta d = PR  (rhs_x + A_act' r_y / delta), d_y = (A_act d_x - r_y) / delta
-    double* eta = PZ;  // r_y / delta on active rows (structural part used for the gather)
+    double* eta = PZ;  // r_y / delta on active rows
     FOR(r, L.m) eta[r] = (ACT[r] != 0) ? PR[nc + r] / delta : 0.0;
+    FOR(col, nc) BX[col] = PR[col];
     BSYNC();
-    FOR(col, nc)
-    {
-      double b = PR[col] + BS[col] * eta[bound_row(L, col)];
-      if (col < nx)
-      {
-        const int t = col / D, j = col % D;
-        const int f = c.T.fixed_of_step[t];
-        if (f >= 0)
-          b += FS[f * D + j] * eta[f * D + j];
-        for (int p = c.T.step_ptr[t]; p < c.T.step_ptr[t + 1]; ++p)
-        {
-          const int a = c.T.step_rows[p];
-          b += GS[a * D + j] * eta[L.n_fixed_rows + a];
-        }
-        BX[col] = b;
-      }
-      else
-      {
-        const int a = (col - nx) >> 1, sd = (col - nx) & 1;
-        b += WS[2 * a + sd] * eta[L.n_fixed_rows + a];
-        BA[col] = b;
-      }
-    }
-    BSYNC();
-    reduced_solve(c, sv, true, delta, XT);
+    reduced_solve(c, sv, true, delta, eta, XT);
     FOR(col, nc) PS[col] += XT[col];
     FOR(r, L.m)
     {
@@ -1226,12 +1211,26 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
         PS[nc + r] += (row_ax(c, r, XT) - PR[nc + r]) / delta;
     }
     BSYNC();
-    if (it == os.polish_refine_iter)
+    if (it == max_refine)
       break;
     // residual of the unregularised KKT: PR = PB - K [x; y]
-    FOR(col, nc) PR[col] = PB[col] - col_px(c, col, PS) - col_aty(c, col, PS + nc);
-    FOR(r, L.m) PR[nc + r] = (ACT[r] != 0) ? PB[nc + r] - row_ax(c, r, PS) : 0.0;
-    BSYNC();
+    double rn[1] = { 0 };
+    FOR(col, nc)
+    {
+      const double v = PB[col] - col_px(c, col, PS) - col_aty(c, col, PS + nc);
+      PR[col] = v;
+      rn[0] = fmax(rn[0], fabs(v));
+    }
+    FOR(r, L.m)
+    {
+      const double v = (ACT[r] != 0) ? PB[nc + r] - row_ax(c, r, PS) : 0.0;
+      PR[nc + r] = v;
+      rn[0] = fmax(rn[0], fabs(v));
+    }
+    block_max<1>(c, rn);
+    if (it >= os.polish_refine_iter && (rn[0] <= 1e-15 * (1.0 + bscale[0]) || rn[0] >= 0.5 * rnorm_prev))
+      break;
+    rnorm_prev = rn[0];
   }
   // polished point: x, z = A x, y (active) -> normal cone projection
   double* pz = PZ;
@@ -1321,6 +1320,7 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   if (c.tid == 0)
   {
     c.s->rho = fmin(fmax(warm ? c.s->prev_rho : os.rho, kRhoMin), kRhoMax);
+    c.s->rho0 = c.s->rho;
     c.s->cur = 0;
     c.s->qp_status = ST_UNSOLVED;
     c.s->polish_status = 0;
@@ -1352,7 +1352,17 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   {
     // setup failure: CVX_FAILED, no workspace for the next warm start
     if (c.tid == 0)
+    {
       c.s->prev_status = 0;
+      if (c.s->trace && c.s->trace_n < c.s->trace_cap)
+      {
+        double* rec = c.s->trace + 10 * c.s->trace_n++;
+        for (int i = 0; i < 10; ++i)
+          rec[i] = 0;
+        rec[3] = -1;
+        rec[9] = c.s->trust;
+      }
+    }
     BSYNC();
     return THIP_CVX_FAILED;
   }
@@ -1454,6 +1464,28 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
     c.s->n_admm += iters;
   }
   BSYNC();
+  if (c.s->trace)
+  {
+    double xs = 0;
+    FOR(col, L.n_cols) xs += fabs(SXw[col]);
+    xs = block_sum(c, xs);
+    if (c.tid == 0 && c.s->trace_n < c.s->trace_cap)
+    {
+      double* rec = c.s->trace + 10 * c.s->trace_n;
+      rec[0] = warm ? 1.0 : 0.0;
+      rec[1] = c.s->rho0;
+      rec[2] = iters;
+      rec[3] = st;
+      rec[4] = c.s->polish_status;
+      rec[5] = c.s->rho;
+      rec[6] = nm.prim_res;
+      rec[7] = nm.dual_res;
+      rec[8] = xs;
+      rec[9] = c.s->trust;
+      c.s->trace_n++;
+    }
+    BSYNC();
+  }
   if (st == ST_SOLVED || st == ST_SOLVED_INACC)
     return THIP_CVX_SOLVED;
   if (inf)
@@ -1731,7 +1763,16 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
   Solver sv;
   sv.M = dyn;
   sv.Nb = dyn + L.N * L.D * L.D;
+  if (threadIdx.x == 0)
+  {
+    ctl.trace = args.trace ? args.trace + (long long)b * args.trace_cap * 10 : nullptr;
+    ctl.trace_cap = args.trace_cap;
+    ctl.trace_n = 0;
+  }
+  __syncthreads();
   sqp_optimize(c, sv);
+  if (threadIdx.x == 0 && args.trace_n)
+    args.trace_n[b] = ctl.trace_n;
   if (c.tid == 0)
   {
     thip_result r{};

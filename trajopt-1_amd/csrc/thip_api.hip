@@ -44,6 +44,9 @@ struct thip_ctx
   hipStream_t stream = nullptr;
   bool own_stream = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double* d_trace = nullptr;
+  int* d_trace_n = nullptr;
+  int trace_cap = 0;
   bool uploaded = false;
   bool ran = false;
   size_t lds_bytes = 0;
@@ -362,6 +365,9 @@ static KernelArgs make_args(thip_ctx* ctx)
   a.iws = ctx->d_iws;
   a.res = ctx->d_res;
   a.batch = ctx->batch;
+  a.trace = ctx->d_trace;
+  a.trace_n = ctx->d_trace_n;
+  a.trace_cap = ctx->trace_cap;
   return a;
 }
 
@@ -516,6 +522,68 @@ int thip_fwd_kin(thip_ctx* ctx, const double* x, double* poses)
   return THIP_OK;
 }
 
+int thip_debug_trace(thip_ctx* ctx, int capacity)
+{
+  if (!ctx || capacity < 0)
+    return THIP_E_INVALID;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  if (ctx->d_trace)
+    hipFree(ctx->d_trace);
+  if (ctx->d_trace_n)
+    hipFree(ctx->d_trace_n);
+  ctx->d_trace = nullptr;
+  ctx->d_trace_n = nullptr;
+  ctx->trace_cap = capacity;
+  if (capacity == 0)
+    return THIP_OK;
+  const size_t B = static_cast<size_t>(ctx->batch);
+  HIPCHK(ctx, hipMalloc(&ctx->d_trace, B * static_cast<size_t>(capacity) * 10 * sizeof(double)));
+  HIPCHK(ctx, hipMalloc(&ctx->d_trace_n, B * sizeof(int)));
+  HIPCHK(ctx, hipMemset(ctx->d_trace_n, 0, B * sizeof(int)));
+  return THIP_OK;
+}
+
+int thip_debug_layout(thip_ctx* ctx, long long* doff, long long* ioff, long long* dims)
+{
+  if (!ctx)
+    return THIP_E_INVALID;
+  const Layout& L = ctx->L;
+  for (int k = 0; k < A_COUNT; ++k)
+    doff[k] = L.doff[k];
+  for (int k = 0; k < I_COUNT; ++k)
+    ioff[k] = L.ioff[k];
+  const long long d[] = { L.N, L.D, L.nx, L.n_fixed_rows, L.n_abs, L.n_cols, L.n_rows, L.m, L.dstride, L.istride,
+                          A_COUNT, I_COUNT };
+  for (int k = 0; k < 12; ++k)
+    dims[k] = d[k];
+  return THIP_OK;
+}
+
+int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws)
+{
+  if (!ctx)
+    return THIP_E_INVALID;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  const size_t B = static_cast<size_t>(ctx->batch);
+  HIPCHK(ctx, hipMemcpy(dws, ctx->d_ws, B * static_cast<size_t>(ctx->L.dstride) * sizeof(double),
+                        hipMemcpyDeviceToHost));
+  HIPCHK(ctx, hipMemcpy(iws, ctx->d_iws, B * static_cast<size_t>(ctx->L.istride) * sizeof(int),
+                        hipMemcpyDeviceToHost));
+  return THIP_OK;
+}
+
+int thip_debug_get_trace(thip_ctx* ctx, double* records, int* counts)
+{
+  if (!ctx || !ctx->d_trace || !records || !counts)
+    return THIP_E_INVALID;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  const size_t B = static_cast<size_t>(ctx->batch);
+  HIPCHK(ctx, hipMemcpy(records, ctx->d_trace, B * static_cast<size_t>(ctx->trace_cap) * 10 * sizeof(double),
+                        hipMemcpyDeviceToHost));
+  HIPCHK(ctx, hipMemcpy(counts, ctx->d_trace_n, B * sizeof(int), hipMemcpyDeviceToHost));
+  return THIP_OK;
+}
+
 void thip_destroy(thip_ctx* ctx)
 {
   if (!ctx)
@@ -533,6 +601,8 @@ void thip_destroy(thip_ctx* ctx)
   hipFree(ctx->d_tgt);
   hipFree(ctx->d_scene);
   hipFree(ctx->d_x);
+  hipFree(ctx->d_trace);
+  hipFree(ctx->d_trace_n);
   if (ctx->ev0)
     hipEventDestroy(ctx->ev0);
   if (ctx->ev1)

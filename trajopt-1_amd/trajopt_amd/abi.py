@@ -227,6 +227,10 @@ def _declare(lib):
     lib.thip_default_sqp_params.restype = None
     lib.thip_default_osqp_settings.argtypes = [P(OsqpSettings)]
     lib.thip_default_osqp_settings.restype = None
+    lib.thip_debug_trace.argtypes = [vp, C.c_int]
+    lib.thip_debug_trace.restype = C.c_int
+    lib.thip_debug_get_trace.argtypes = [vp, dp, P(C.c_int)]
+    lib.thip_debug_get_trace.restype = C.c_int
     lib.thip_sizeof_desc.argtypes = []
     lib.thip_sizeof_desc.restype = C.c_int
     return lib

@@ -87,6 +87,16 @@ class BatchTrustRegionSQP:
         self._check(self.lib.thip_fwd_kin(self.ctx, _dp(x), _dp(poses)), "thip_fwd_kin")
         return poses
 
+    def enable_trace(self, capacity=512):
+        self._trace_cap = capacity
+        self._check(self.lib.thip_debug_trace(self.ctx, capacity), "thip_debug_trace")
+
+    def get_trace(self):
+        rec = np.zeros((self.batch, self._trace_cap, 10))
+        cnt = (C.c_int * self.batch)()
+        self._check(self.lib.thip_debug_get_trace(self.ctx, _dp(rec), cnt), "thip_debug_get_trace")
+        return [rec[b, : cnt[b]] for b in range(self.batch)]
+
     def close(self):
         if self.ctx:
             self.lib.thip_destroy(self.ctx)
