@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Batched trust-region SQP benchmark (BASELINE.json metric).
+
+A "step" is one sco::BasicTrustRegionSQP::optimize of every problem in the
+per-GPU batch (1024 problems of 7-DoF x 30 waypoints), run by one fused HIP
+launch from inputs already resident in HBM.  `value` is SQP (outer) iterations
+per second summed over all problems of all ranks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 1024]
+
+Multi-GPU: one process per GPU (torchrun); every rank solves its own
+contiguous shard of problem seeds (weak scaling, no data-path collective); a
+gloo barrier brackets the timed region and the max elapsed time over ranks is
+reported.
+
+Extra JSON objects:
+  roofline      algorithmic HBM bytes of sqp_kernel (SURVEY.md §8d B_iter
+                model, counters read back from the device) / its HIP-event
+                duration, against the 8 TB/s HBM3E peak.
+  cpu_baseline  the oracle's CPU restatement (oracle/, "port") on a bounded
+                sample of the same problems, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "trajopt-1_amd"))
+
+import numpy as np  # noqa: E402
+
+from trajopt_amd import abi, problems  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def algorithmic_bytes(wl, results):
+    """B_iter = fixed + k * per_admm + s * 16 nnz(L) per problem
+    per SQP iteration; summed over the batch it needs only the per-problem
+    totals of SQP iterations, ADMM iterations and KKT solves."""
+    N, D = wl.n_steps, wl.n_dof
+    nx = N * D
+    R = 6 * wl.desc.n_cart
+    n = nx + 2 * R
+    m = R + D * wl.desc.n_fixed + n
+    nnz_a = R * (D + 2) + D * wl.desc.n_fixed + n
+    nnz_p = nx + (N - 1) * D
+    nnz_l = N * D * (D + 1) // 2 + (N - 1) * D * D  # block-tridiagonal Cholesky factor
+    fixed = 2 * 8 * nx + 8 * R * (1 + D) + 96 * wl.desc.n_cart + 2 * 8 * (n + 2 * m + R * (D + 2))
+    per_admm = 2 * 12 * nnz_a + 24 * nnz_p + 8 * (3 * n + 7 * m)
+    refine = wl.desc.osqp.polish_refine_iter
+    total = 0
+    for r in results:
+        kkt_solves = r.n_admm_iters + r.n_qp_solves * (1 + refine)
+        total += fixed * r.n_sqp_iters + per_admm * r.n_admm_iters + 16 * nnz_l * kkt_solves
+    return total, {"fixed": fixed, "per_admm": per_admm, "nnz_L": nnz_l}
+
+
+def cpu_baseline(config, n_problems, threads):
+    """Oracle (CPU restatement of the reference path) on a bounded sample."""
+    sys.path.insert(0, str(ROOT))
+    from oracle import oracle  # checker / baseline only
+
+    wl = problems.make_workload(config, n_problems)
+    t0 = time.perf_counter()
+    _, res = oracle.solve(wl, n_threads=threads)
+    dt = time.perf_counter() - t0
+    iters = sum(r.n_sqp_iters for r in res)
+    return {
+        "value": iters / dt,
+        "unit": "SQP iters/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"first {n_problems} problems of the same workload (seeds 20261015+b), "
+                  f"{iters} SQP iterations in {dt:.1f} s, one problem per thread",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=1024, help="problems per GPU")
+    ap.add_argument("--config", default="B")
+    ap.add_argument("--cpu-problems", type=int, default=256)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+
+    import torch
+    import torch.distributed as dist
+
+    abi.load_hip()  # after torch: one HIP runtime per process (see abi.load_hip)
+
+    if world > 1:
+        dist.init_process_group("gloo")  # barrier + max-time only; the data path has no collective
+
+    from trajopt_amd.runtime import BatchTrustRegionSQP
+
+    wl = problems.make_workload(args.config, args.batch, first_problem=rank * args.batch)
+    solver = BatchTrustRegionSQP(wl, device=local_rank)
+    solver.upload()
+    torch.cuda.set_device(local_rank)
+
+    for _ in range(args.warmup):
+        solver.run()
+    _, res = solver.download()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    kernel_ms = []
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        solver.run()
+        kernel_ms.append(solver.kernel_ms())  # HIP events on the solver's stream (waits for it)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    x_last, res_last = solver.download()
+
+    # every step solves the same problems: the counters must repeat exactly
+    same = all(a.n_sqp_iters == b.n_sqp_iters and a.n_admm_iters == b.n_admm_iters for a, b in zip(res, res_last))
+    if not same:
+        raise SystemExit("non-deterministic SQP counters between steps")
+    iters_local = sum(r.n_sqp_iters for r in res_last)
+    bytes_local, model = algorithmic_bytes(wl, res_last)
+    kms = float(np.mean(kernel_ms))
+
+    if world > 1:
+        t = torch.tensor([elapsed, float(iters_local)], dtype=torch.float64)
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0])
+        iters_total = float(tsum[1])
+    else:
+        iters_total = float(iters_local)
+
+    if rank == 0:
+        value = iters_total * args.steps / elapsed
+        achieved = bytes_local / (kms * 1e-3) / 1e9
+        out = {
+            "metric": "SQP iters/sec + achieved HBM GB/s, 7-DoF x 30-wpt x 1024-batch",
+            "value": value,
+            "unit": "SQP iters/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (splitmix64 seeds 20261015+b, PR2 right arm; SURVEY.md §8d)",
+            "config": {
+                "workload": f"config {args.config}: 7-DoF PR2 arm x {wl.n_steps} waypoints, JointVel + "
+                            f"{wl.desc.n_cart} CartPose ABS costs, batch {args.batch} per GPU "
+                            "(BasicTrustRegionSQP + OSQP-semantics ADMM/polish)",
+                "batch_per_gpu": args.batch,
+                "global_batch": args.batch * world,
+                "sqp_iters_per_step": iters_total,
+                "qp_solves_per_step_rank0": sum(r.n_qp_solves for r in res_last),
+                "admm_iters_per_step_rank0": sum(r.n_admm_iters for r in res_last),
+                "parallelism": f"shard{world} (independent problems, no collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "thip::sqp_kernel",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel_ms": kms,
+                "algorithmic_bytes_per_launch": bytes_local,
+                "model": model,
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_problems, args.cpu_threads)
+        print(json.dumps(out), flush=True)
+
+    solver.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,39 @@
+"""GPU vs oracle parity summary for a config/batch (diagnostic).
+
+    python tools/parity.py A 64 [B 64 ...]
+"""
+import sys
+import time
+
+sys.path.insert(0, "trajopt-1_amd")
+sys.path.insert(0, ".")
+import numpy as np
+
+from trajopt_amd import abi, problems
+from trajopt_amd.runtime import BatchTrustRegionSQP
+from oracle import oracle
+
+args = sys.argv[1:]
+for i in range(0, len(args), 2):
+    cfg, B = args[i], int(args[i + 1])
+    wl = problems.make_workload(cfg, B)
+    s = BatchTrustRegionSQP(wl)
+    t = time.time()
+    xg, rg = s.optimize()
+    tg = time.time() - t
+    s.close()
+    t = time.time()
+    xo, ro = oracle.solve(wl, n_threads=16)
+    to = time.time() - t
+    d = np.abs(xg - xo).reshape(B, -1).max(1)
+    st = np.array([a.status == b.status for a, b in zip(rg, ro)])
+    tol = wl.desc.sqp.cnt_tolerance
+    fl = np.array([(a.max_cnt_viol < tol) == (b.max_cnt_viol < tol) for a, b in zip(rg, ro)])
+    ok = (d <= 1e-5) & st & fl
+    cost_rel = np.array([abs(a.total_cost - b.total_cost) / max(1.0, abs(b.total_cost)) for a, b in zip(rg, ro)])
+    print(f"config {cfg} batch {B}: x within 1e-5 {np.sum(d <= 1e-5)}/{B}, status equal {st.sum()}/{B}, "
+          f"cnt-flag equal {fl.sum()}/{B}, all three {ok.sum()}/{B}; gpu {tg:.2f}s oracle {to:.2f}s (16 thr)")
+    print(f"   max|dx| quantiles 50/90/100%: {np.quantile(d, 0.5):.2e} {np.quantile(d, 0.9):.2e} {d.max():.2e}; "
+          f"cost rel diff of mismatches: {np.round(cost_rel[~ok], 6).tolist()[:12]}")
+    print(f"   mismatching problems: {np.nonzero(~ok)[0].tolist()[:20]}  statuses gpu/cpu: "
+          f"{[(rg[b].status, ro[b].status) for b in np.nonzero(~ok)[0][:8]]}")

@@ -1,0 +1,40 @@
+"""Per-phase cycle breakdown of sqp_kernel (thip_debug_profile), diagnostic.
+
+    python tools/phase_profile.py B 1024
+"""
+import sys
+import time
+
+sys.path.insert(0, "trajopt-1_amd")
+import numpy as np
+
+from trajopt_amd import problems
+from trajopt_amd.runtime import BatchTrustRegionSQP
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "B"
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+wl = problems.make_workload(cfg, B)
+s = BatchTrustRegionSQP(wl)
+s.upload()
+s.run()
+s.download()
+s.enable_profile(True)
+t = time.time()
+s.run()
+x, res = s.download()
+print(f"config {cfg} batch {B}: kernel {s.kernel_ms():.1f} ms (wall {time.time() - t:.2f}s)")
+pf = s.get_profile().astype(np.float64)
+admm = np.array([r.n_admm_iters for r in res], dtype=np.float64)
+qps = np.array([r.n_qp_solves for r in res], dtype=np.float64)
+sqp = np.array([r.n_sqp_iters for r in res], dtype=np.float64)
+mhz = pf[:, 13].sum() / pf[:, 14].sum() * 100.0
+print(f"shader clock ~{mhz:.0f} MHz; per problem: admm {admm.mean():.0f} (max {admm.max():.0f}), "
+      f"qp {qps.mean():.1f}, sqp {sqp.mean():.1f}")
+slowest = int(np.argmax(pf[:, 14]))
+print(f"slowest problem {slowest}: {pf[slowest, 14] / 100:.0f} us wall, admm {admm[slowest]:.0f}")
+tot = pf[:, 13].sum()
+for k, name in [kv for kv in enumerate(BatchTrustRegionSQP.PROFILE_SLOTS) if kv[0] != 14]:
+    v = pf[:, k].sum()
+    per_admm = v / admm.sum()
+    print(f"  {k:2d} {name:<16} {100 * v / tot:6.1f}%   {per_admm:10.0f} cyc/admm-iter   "
+          f"{v / qps.sum():12.0f} cyc/qp")

@@ -14,6 +14,11 @@ namespace thip
 {
 constexpr int kBlock = 256;  // threads per problem workgroup
 constexpr int kWaves = kBlock / 64;
+// dynamic LDS a problem may use (160 KB per CU on gfx950, one workgroup per
+// CU; the rest is the kernel's static LDS)
+constexpr long long kLdsBudgetBytes = 152 * 1024;
+// CartPose rows per waypoint the register-resident ADMM segment supports
+constexpr int kMaxStepRows = 12;
 
 // per-problem double workspace arrays
 enum DArr : int
@@ -100,6 +105,17 @@ struct Layout
   long long istride;  // ints per problem
   long long doff[A_COUNT];
   long long ioff[I_COUNT];
+  // LDS residency plan: offset (doubles) of array k inside the dynamic LDS
+  // block, or -1 if it stays in the per-problem HBM workspace.  The first
+  // lds_scratch doubles are the block-solve chain matrices / FK staging.
+  int loff[A_COUNT];
+  int lds_scratch;
+  int lds_doubles;
+  // register-resident ADMM segment (admm_segment): eligible when every
+  // waypoint has <= kMaxStepRows CartPose rows and the hot arrays are LDS
+  // resident; seg_slots = column/row slots per thread (1 or 2)
+  int seg_ok;
+  int seg_slots;
 };
 
 // shared (batch-wide) tables, device resident
@@ -130,6 +146,10 @@ struct KernelArgs
   double* trace;
   int* trace_n;
   int trace_cap;
+  // diagnostics: per-problem phase cycle counters [batch][kProfSlots] (null = off)
+  long long* prof;
 };
+
+constexpr int kProfSlots = 16;
 
 }  // namespace thip

@@ -66,6 +66,7 @@ struct Ctl
   double* trace;
   int trace_cap, trace_n;
   double rho0;
+  long long* prof;  // phase cycle counters of this problem (null = off)
 };
 
 struct Ctx
@@ -77,21 +78,44 @@ struct Ctx
   int* iw;
   double* big;
   Ctl* s;
+  double* const* ptab;  // LDS table of array base pointers (LDS-resident or HBM), or null
   int tid, lane, wave;
   __device__ Ctx(const Layout& l, const Tables& t, const thip_problem_desc* dd, double* ww, int* ii, double* bb,
-                 Ctl* ss)
-    : L(l), T(t), d(dd), w(ww), iw(ii), big(bb), s(ss)
+                 Ctl* ss, double* const* pt = nullptr)
+    : L(l), T(t), d(dd), w(ww), iw(ii), big(bb), s(ss), ptab(pt)
   {
     tid = threadIdx.x;
     lane = tid & 63;
     wave = tid >> 6;
   }
-  __device__ __forceinline__ double* a(int k) const { return w + L.doff[k]; }
+  __device__ __forceinline__ double* a(int k) const { return ptab ? ptab[k] : w + L.doff[k]; }
   __device__ __forceinline__ int* ia(int k) const { return iw + L.ioff[k]; }
 };
 
 #define FOR(i, n) for (int i = c.tid; i < (n); i += kBlock)
 #define BSYNC() __syncthreads()
+
+// Phase profiling (thip_debug_profile): shader-clock cycles accumulated per
+// slot by thread 0.  Slots: 0 admm_step, 1 residuals, 2 termination check,
+// 3 factor, 4 polish, 5 linearize, 6 evaluate, 7 build_and_scale,
+// 8 solve rhs + block diag (segment: phase A), 9 forward chain, 10 backward
+// chain, 11 aux back-substitution (segment: phase E), 12 qp_solve, 13 sqp
+// total, 14 sqp total (wall clock, 100 MHz ticks), 15 segment phases B + C2.
+struct ProfScope
+{
+  long long* p;
+  int slot;
+  long long t0;
+  __device__ ProfScope(const Ctx& c, int s) : p(c.tid == 0 ? c.s->prof : nullptr), slot(s), t0(p ? clock64() : 0) {}
+  __device__ ~ProfScope()
+  {
+    if (p)
+      p[slot] += clock64() - t0;
+  }
+};
+#define PROF_CAT2(a, b) a##b
+#define PROF_CAT(a, b) PROF_CAT2(a, b)
+#define PROF(slot) ProfScope PROF_CAT(prof_scope_, __LINE__)(c, slot)
 
 __device__ __forceinline__ double wave_max(double v)
 {
@@ -161,6 +185,7 @@ __device__ __forceinline__ double limit_scaling(double a)
 // ======================================================================
 __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
 {
+  PROF(5);
   const Layout& L = c.L;
   const int D = L.D;
   const thip_chain& ch = c.d->chain;
@@ -273,6 +298,7 @@ __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
 // ======================================================================
 __device__ void evaluate(Ctx& c, const double* x, double* costs, double* viols)
 {
+  PROF(6);
   const Layout& L = c.L;
   const int D = L.D;
   const thip_chain& ch = c.d->chain;
@@ -331,6 +357,7 @@ __device__ __forceinline__ int bound_row(const Layout& L, int col) { return L.n_
 
 __device__ void build_and_scale(Ctx& c)
 {
+  PROF(7);
   const Layout& L = c.L;
   const int D = L.D, nx = L.nx;
   const thip_osqp_settings& os = c.d->osqp;
@@ -538,6 +565,7 @@ __device__ __forceinline__ double rho_k(const Ctx& c, int r, bool polish, double
 // returns false if the reduced matrix is not positive definite
 __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delta)
 {
+  PROF(3);
   const Layout& L = c.L;
   const int D = L.D, nx = L.nx, N = L.N;
   const double *PD = c.a(A_PD), *PO = c.a(A_PO), *BS = c.a(A_BS), *GS = c.a(A_GS), *WS = c.a(A_WS),
@@ -695,6 +723,127 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
   return ok;
 }
 
+// Arrays the residency plan always places in LDS (chain matrices, LINV, CV,
+// YV: thip_create rejects problems where they would not fit) are accessed
+// through LDS-typed pointers so the compiler emits ds_read/ds_write instead of
+// flat accesses (flat ops count on vmcnt and lgkmcnt, so every wait would also
+// drain outstanding stores).
+typedef __attribute__((address_space(3))) double lds_f64;
+__device__ __forceinline__ lds_f64* lds(double* p) { return (lds_f64*)p; }
+__device__ __forceinline__ const lds_f64* lds(const double* p) { return (const lds_f64*)p; }
+
+// ---- wave-level chain of the block solve ---------------------------------
+// 64-bit DPP move (two 32-bit halves)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v)
+{
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+// sum over the 8 lanes of a lane octet (lane & 7): xor 1, xor 2 (quad_perm),
+// then the mirrored octet half (row_half_mirror)
+__device__ __forceinline__ double octet_sum(double v)
+{
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  return v;
+}
+// sum over the 8 octets (lane >> 3) at fixed lane & 7: xor 8 (row_ror:8),
+// xor 16 (v_permlane16_swap), xor 32 (v_permlane32_swap) -- gfx950
+__device__ __forceinline__ double cross_octet_sum(double v)
+{
+  v += dpp_f64<0x128>(v);  // row_ror:8 within each 16-lane row
+  {
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+    v = __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+  }
+  {
+    const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+    v = __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+  }
+  return v;
+}
+
+// Block-bidiagonal recurrence v_t = c_t - G_t v_{t-1} (FWD, t = 1..N-1) or
+// v_t = c_t - G_t v_{t+1} (backward, t = N-2..0), run by one wave.  Lane
+// (i, k) = (lane >> 3, lane & 7) multiplies one element of the D x D block.
+// The vector alternates between "column" layout (value indexed by k) and
+// "row" layout (indexed by i): odd steps reduce over k inside an octet, even
+// steps use the transposed block and reduce over i across octets, so no
+// lane permutation (ds_bpermute) sits on the serial path.  Blocks and c
+// values are loaded kChainChunk steps at a time into registers (one LDS wait
+// per chunk); inside a chunk the steps are unrolled with static parity.
+constexpr int kChainChunk = 8;
+
+template <bool FWD>
+__device__ __forceinline__ void block_chain(const double* Gp, const double* cvp, double* outp, int N, int D,
+                                            int lane)
+{
+  const lds_f64* G = lds(Gp);
+  const lds_f64* cv = lds(cvp);
+  lds_f64* out = lds(outp);
+  const int i = lane >> 3, k = lane & 7;
+  const bool act = (i < D) && (k < D);
+  const int DD = D * D;
+  const int t0 = FWD ? 0 : N - 1;
+  double v = (k < D) ? cv[t0 * D + k] : 0.0;  // column layout
+  if (i == 0 && k < D)
+    out[t0 * D + k] = v;
+  // offsets of this lane's element in the normal / transposed block
+  const int off_n = i * D + k, off_t = k * D + i;
+  for (int s0 = 1; s0 < N; s0 += kChainChunk)
+  {
+    double g[kChainChunk], cc[kChainChunk];
+#pragma unroll
+    for (int u = 0; u < kChainChunk; ++u)
+    {
+      const int s = s0 + u;
+      const int t = FWD ? s : N - 1 - s;
+      const bool ok = s < N;
+      // s0 is odd, so even u are odd steps (normal block, c by row i)
+      if ((u & 1) == 0)
+      {
+        g[u] = (ok && act) ? G[t * DD + off_n] : 0.0;
+        cc[u] = (ok && i < D) ? cv[t * D + i] : 0.0;
+      }
+      else
+      {
+        g[u] = (ok && act) ? G[t * DD + off_t] : 0.0;
+        cc[u] = (ok && k < D) ? cv[t * D + k] : 0.0;
+      }
+    }
+    // serial part: no loads, stores or branches (steps past N compute zeros)
+    double vs[kChainChunk];
+#pragma unroll
+    for (int u = 0; u < kChainChunk; ++u)
+    {
+      const double p = g[u] * v;
+      if ((u & 1) == 0)
+        v = cc[u] - octet_sum(p);  // row layout: v = v_t[i]
+      else
+        v = cc[u] - cross_octet_sum(p);  // column layout: v = v_t[k]
+      vs[u] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < kChainChunk; ++u)
+    {
+      const int s = s0 + u;
+      const int t = FWD ? s : N - 1 - s;
+      if ((u & 1) == 0)
+      {
+        if (s < N && k == 0 && i < D)
+          out[t * D + i] = vs[u];
+      }
+      else if (s < N && i == 0 && k < D)
+        out[t * D + k] = vs[u];
+    }
+  }
+}
+
 // Solve K [x; aux] = r + A' eta, with r (n_cols) in A_BXW (overwritten) and
 // eta over all m rows; K = P + diag(sigK) + A' diag(rho) A as in factor().
 // The 2x2 aux block of each CartPose row is eliminated with its explicit
@@ -703,6 +852,15 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
 // O(1/delta^2) quantities and loses ~12 digits.
 __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, const double* eta, double* out)
 {
+  long long* pf = (c.tid == 0) ? c.s->prof : nullptr;
+  long long tq = pf ? clock64() : 0;
+#define PROF_LAP(slot)          \
+  if (pf)                       \
+  {                             \
+    const long long tn = clock64(); \
+    pf[slot] += tn - tq;        \
+    tq = tn;                    \
+  }
   const Layout& L = c.L;
   const int D = L.D, nx = L.nx, N = L.N, DD = D * D, nfr = L.n_fixed_rows;
   const double *GS = c.a(A_GS), *WS = c.a(A_WS), *DG = c.a(A_DG), *LI = c.a(A_LINV), *BS = c.a(A_BS),
@@ -741,61 +899,32 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     const int t = col / D, i = col % D;
     double v = 0;
     for (int k = 0; k <= i; ++k)
-      v += LI[t * DD + i * D + k] * BX[t * D + k];
-    CV[col] = v;
+      v += lds(LI)[t * DD + i * D + k] * BX[t * D + k];
+    lds(CV)[col] = v;
   }
   BSYNC();
+  PROF_LAP(8);
   // forward chain y_t = c_t - M_t y_{t-1}
   if (c.wave == 0)
-  {
-    const int i = c.lane >> 3, k = c.lane & 7;
-    const bool act = (i < D) && (k < D);
-    double yk = (k < D) ? CV[k] : 0.0;
-    if (c.lane < D)
-      YV[c.lane] = CV[c.lane];
-    for (int t = 1; t < N; ++t)
-    {
-      double pr = act ? sv.M[t * DD + i * D + k] * yk : 0.0;
-      pr += __shfl_xor(pr, 1);
-      pr += __shfl_xor(pr, 2);
-      pr += __shfl_xor(pr, 4);
-      const double yi = (i < D) ? CV[t * D + i] - pr : 0.0;
-      yk = __shfl(yi, (k < D ? k : 0) * 8);
-      if (i == 0 && k < D)
-        YV[t * D + k] = yk;
-    }
-  }
+    block_chain<true>(sv.M, CV, YV, N, D, c.lane);
   BSYNC();
+  PROF_LAP(9);
   FOR(col, nx)
   {
     const int t = col / D, i = col % D;
     double v = 0;
     for (int k = i; k < D; ++k)
-      v += LI[t * DD + k * D + i] * YV[t * D + k];
-    CV[col] = v;
+      v += lds(LI)[t * DD + k * D + i] * lds(YV)[t * D + k];
+    lds(CV)[col] = v;
   }
   BSYNC();
+  PROF_LAP(8);
   // backward chain x_t = d_t - N_t x_{t+1}
   if (c.wave == 0)
-  {
-    const int i = c.lane >> 3, k = c.lane & 7;
-    const bool act = (i < D) && (k < D);
-    double xk = (k < D) ? CV[(N - 1) * D + k] : 0.0;
-    if (c.lane < D)
-      out[(N - 1) * D + c.lane] = CV[(N - 1) * D + c.lane];
-    for (int t = N - 2; t >= 0; --t)
-    {
-      double pr = act ? sv.Nb[t * DD + i * D + k] * xk : 0.0;
-      pr += __shfl_xor(pr, 1);
-      pr += __shfl_xor(pr, 2);
-      pr += __shfl_xor(pr, 4);
-      const double xi = (i < D) ? CV[t * D + i] - pr : 0.0;
-      xk = __shfl(xi, (k < D ? k : 0) * 8);
-      if (i == 0 && k < D)
-        out[t * D + k] = xk;
-    }
-  }
+    block_chain<false>(sv.Nb, CV, CV, N, D, c.lane);  // in place: x lands in CV
   BSYNC();
+  PROF_LAP(10);
+  FOR(col, nx) out[col] = CV[col];
   // aux back-substitution
   FOR(r, L.n_abs)
   {
@@ -803,7 +932,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     const int ca = nx + 2 * r;
     double g = 0;
     for (int j = 0; j < D; ++j)
-      g += GS[r * D + j] * out[t * D + j];
+      g += GS[r * D + j] * lds(CV)[t * D + j];
     const double rr = rho_k(c, nfr + r, polish, delta);
     const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
     const double rn = BA[ca], rp = BA[ca + 1];
@@ -814,6 +943,8 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     out[ca + 1] = (dn * rp - rr * wn * cross + wp * dn * h) / det;
   }
   BSYNC();
+  PROF_LAP(11);
+#undef PROF_LAP
 }
 
 // A x for one row (scaled); x over n_cols
@@ -929,6 +1060,7 @@ struct Norms
 
 __device__ void compute_residuals(Ctx& c, const double* x, const double* z, const double* y, Norms& nm)
 {
+  PROF(1);
   const Layout& L = c.L;
   double *AX = c.a(A_AX), *PX = c.a(A_PX), *ATY = c.a(A_ATY), *PRV = c.a(A_PRV), *DRV = c.a(A_DRV);
   const double *E = c.a(A_E), *DS = c.a(A_DS), *Q = c.a(A_Q);
@@ -1044,6 +1176,7 @@ __device__ bool is_dual_infeasible(Ctx& c, double eps)
 // check_termination; sets c.s->qp_status when it fires
 __device__ bool check_termination(Ctx& c, const Norms& nm, bool approx)
 {
+  PROF(2);
   const thip_osqp_settings& os = c.d->osqp;
   double ea = os.eps_abs, er = os.eps_rel, epi = os.eps_prim_inf, edi = os.eps_dual_inf;
   if (approx)
@@ -1084,6 +1217,7 @@ __device__ bool check_termination(Ctx& c, const Norms& nm, bool approx)
 
 __device__ void admm_step(Ctx& c, Solver& sv)
 {
+  PROF(0);
   const Layout& L = c.L;
   const thip_osqp_settings& os = c.d->osqp;
   const double sig = os.sigma, al = os.alpha;
@@ -1096,7 +1230,7 @@ __device__ void admm_step(Ctx& c, Solver& sv)
   const double* xp = c.a(cur ? A_XA0 : A_XA1);
   double* z = c.a(cur ? A_Z1 : A_Z0);
   const double* zp = c.a(cur ? A_Z0 : A_Z1);
-  double *Y = c.a(A_Y), *XT = c.a(A_XT), *ZT = c.a(A_ZT), *DX = c.a(A_DX), *DY = c.a(A_DY);
+  double *Y = c.a(A_Y), *XT = c.a(A_XT), *DX = c.a(A_DX), *DY = c.a(A_DY);
   double* BX = c.a(A_BXW);
   const double *Q = c.a(A_Q), *RH = c.a(A_RHO), *Lo = c.a(A_L), *Up = c.a(A_U);
   double* ETA = c.a(A_PZ);  // eta = rho zp - y over all rows (scratch)
@@ -1108,7 +1242,6 @@ __device__ void admm_step(Ctx& c, Solver& sv)
   FOR(r, L.m)
   {
     const double zt = row_ax(c, r, XT);
-    ZT[r] = zt;
     const double rho = RH[r];
     double zr = (1.0 / rho) * Y[r];
     zr = zr + al * zt;
@@ -1128,6 +1261,341 @@ __device__ void admm_step(Ctx& c, Solver& sv)
   BSYNC();
 }
 
+// ======================================================================
+// Register-resident ADMM segment (the hot loop)
+// ======================================================================
+// Runs n_iter ADMM iterations with the per-QP constants and the x/z/y state
+// of every owned row/column in registers; only the coupling values travel
+// through LDS.  Ownership (static for the whole segment):
+//   column slot q = tid + kBlock*u  -> waypoint t = q / 8, dof i = q % 8:
+//       x column (t, i), its bound row and its fixed-timestep row;
+//   abs slot    a = tid + kBlock*u  -> CartPose row a, its two aux columns
+//       and their bound rows.
+// Per iteration: A (abs rows: row multipliers MR), B (columns: waypoint rhs
+// and Linv_t b_t, gathered inside each lane octet), forward chain, Linv_t^T,
+// backward chain, E (aux back-substitution, z~ = A x~, relaxed z/y/x
+// updates).  The arithmetic (operation order and expression shapes) is that
+// of admm_step() + reduced_solve(), so both paths give identical iterates.
+// State is written back to A_XA0/A_Z0/A_Y/A_DX/A_DY at the end of the segment
+// for the residual / termination / rho-update / polish code.
+__device__ __forceinline__ void admm_row_update(double& z, double& y, double& dy, double zt, double rho, double lo,
+                                                double up, double al)
+{
+  double zr = (1.0 / rho) * y;
+  zr = zr + al * zt;
+  zr = zr + (1.0 - al) * z;
+  zr = fmin(fmax(zr, lo), up);
+  dy = rho * (al * zt + (1.0 - al) * z - zr);
+  y += dy;
+  z = zr;
+}
+
+template <int CS, int AS>
+__device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
+{
+  PROF(0);
+  const Layout& L = c.L;
+  const int D = L.D, N = L.N, nx = L.nx, DD = D * D, nfr = L.n_fixed_rows, nr = L.n_rows;
+  const thip_osqp_settings& os = c.d->osqp;
+  const double sig = os.sigma, al = os.alpha;
+  double *XA = c.a(A_XA0), *Z = c.a(A_Z0), *Y = c.a(A_Y), *DX = c.a(A_DX), *DY = c.a(A_DY);
+  const double *Q = c.a(A_Q), *BS = c.a(A_BS), *RH = c.a(A_RHO), *Lo = c.a(A_L), *Up = c.a(A_U);
+  const double *FS = c.a(A_FS), *GS = c.a(A_GS), *WS = c.a(A_WS), *DG = c.a(A_DG), *LI = c.a(A_LINV);
+  double *MR = c.a(A_MR), *BXW = c.a(A_BXW), *CV = c.a(A_CV), *YV = c.a(A_YV);
+  if (c.tid == 0)
+    c.s->cur = 0;
+
+  // ---- column owners: constants + state
+  bool cact[CS];
+  int ccol[CS], cfr[CS], cnrow[CS], crow[CS][kMaxStepRows];
+  double cq[CS], cbs[CS], clb[CS], cub[CS], crb[CS], cfs[CS], clf[CS], cuf[CS], crf[CS];
+  double cx[CS], czb[CS], cyb[CS], czf[CS], cyf[CS], cdx[CS], cdyb[CS], cdyf[CS];
+  double cli[CS][THIP_MAX_DOF], clc[CS][THIP_MAX_DOF], cgs[CS][kMaxStepRows];
+#pragma unroll
+  for (int u = 0; u < CS; ++u)
+  {
+    const int q = c.tid + kBlock * u;
+    const int t = q >> 3, i = q & 7;
+    cact[u] = (t < N) && (i < D);
+    cfr[u] = -1;
+    cnrow[u] = 0;
+    if (cact[u])
+    {
+      const int col = t * D + i, br = nr + col;
+      ccol[u] = col;
+      cq[u] = Q[col];
+      cbs[u] = BS[col];
+      clb[u] = Lo[br];
+      cub[u] = Up[br];
+      crb[u] = RH[br];
+      cx[u] = XA[col];
+      czb[u] = Z[br];
+      cyb[u] = Y[br];
+      const int f = c.T.fixed_of_step[t];
+      if (f >= 0)
+      {
+        const int fr = f * D + i;
+        cfr[u] = fr;
+        cfs[u] = FS[fr];
+        clf[u] = Lo[fr];
+        cuf[u] = Up[fr];
+        crf[u] = RH[fr];
+        czf[u] = Z[fr];
+        cyf[u] = Y[fr];
+      }
+      const int p0 = c.T.step_ptr[t], p1 = c.T.step_ptr[t + 1];
+      cnrow[u] = p1 - p0;
+#pragma unroll
+      for (int p = 0; p < kMaxStepRows; ++p)
+        if (p < p1 - p0)
+        {
+          const int r = c.T.step_rows[p0 + p];
+          crow[u][p] = r;
+          cgs[u][p] = GS[r * D + i];
+        }
+#pragma unroll
+      for (int k = 0; k < THIP_MAX_DOF; ++k)
+      {
+        cli[u][k] = (k <= i && k < D) ? LI[t * DD + i * D + k] : 0.0;
+        clc[u][k] = (k >= i && k < D) ? LI[t * DD + k * D + i] : 0.0;
+      }
+    }
+    cdx[u] = cdyb[u] = cdyf[u] = 0.0;
+  }
+  // ---- abs-row owners
+  bool aact[AS];
+  int at[AS];
+  double arr[AS], alr[AS], aur[AS], awn[AS], awp[AS], adn[AS], adp[AS], adet[AS], ags[AS][THIP_MAX_DOF];
+  double aqn[AS], aqp[AS], absn[AS], absp[AS], albn[AS], aubn[AS], arbn[AS], albp[AS], aubp[AS], arbp[AS];
+  double axn[AS], axp[AS], azr[AS], ayr[AS], azbn[AS], aybn[AS], azbp[AS], aybp[AS];
+  double adxn[AS], adxp[AS], adyr[AS], adybn[AS], adybp[AS];
+  double arn[AS], arp[AS], aeta[AS];
+#pragma unroll
+  for (int u = 0; u < AS; ++u)
+  {
+    const int a = c.tid + kBlock * u;
+    aact[u] = a < L.n_abs;
+    if (aact[u])
+    {
+      const int r = nfr + a, ca = nx + 2 * a, brn = nr + ca, brp = brn + 1;
+      at[u] = c.T.row_step[a];
+      arr[u] = RH[r];
+      alr[u] = Lo[r];
+      aur[u] = Up[r];
+      awn[u] = WS[2 * a];
+      awp[u] = WS[2 * a + 1];
+      adn[u] = DG[ca];
+      adp[u] = DG[ca + 1];
+      adet[u] = adn[u] * adp[u] + arr[u] * (adn[u] * awp[u] * awp[u] + adp[u] * awn[u] * awn[u]);
+#pragma unroll
+      for (int j = 0; j < THIP_MAX_DOF; ++j)
+        ags[u][j] = (j < D) ? GS[a * D + j] : 0.0;
+      aqn[u] = Q[ca];
+      aqp[u] = Q[ca + 1];
+      absn[u] = BS[ca];
+      absp[u] = BS[ca + 1];
+      albn[u] = Lo[brn];
+      aubn[u] = Up[brn];
+      arbn[u] = RH[brn];
+      albp[u] = Lo[brp];
+      aubp[u] = Up[brp];
+      arbp[u] = RH[brp];
+      axn[u] = XA[ca];
+      axp[u] = XA[ca + 1];
+      azr[u] = Z[r];
+      ayr[u] = Y[r];
+      azbn[u] = Z[brn];
+      aybn[u] = Y[brn];
+      azbp[u] = Z[brp];
+      aybp[u] = Y[brp];
+    }
+    adxn[u] = adxp[u] = adyr[u] = adybn[u] = adybp[u] = 0.0;
+  }
+  BSYNC();
+
+  long long* pf = (c.tid == 0) ? c.s->prof : nullptr;
+  long long tq = pf ? clock64() : 0;
+#define SEG_LAP(slot)                 \
+  if (pf)                             \
+  {                                   \
+    const long long tn = clock64();   \
+    pf[slot] += tn - tq;              \
+    tq = tn;                          \
+  }
+  for (int iter = 0; iter < n_iter; ++iter)
+  {
+    // A: CartPose rows -> MR (aux block eliminated, see reduced_solve)
+#pragma unroll
+    for (int u = 0; u < AS; ++u)
+      if (aact[u])
+      {
+        const double bxn = sig * axn[u] - aqn[u];
+        const double bxp = sig * axp[u] - aqp[u];
+        const double ebn = arbn[u] * azbn[u] - aybn[u];
+        const double ebp = arbp[u] * azbp[u] - aybp[u];
+        aeta[u] = arr[u] * azr[u] - ayr[u];
+        arn[u] = bxn + absn[u] * ebn;
+        arp[u] = bxp + absp[u] * ebp;
+        const double dn = adn[u], dp = adp[u], wn = awn[u], wp = awp[u], rr = arr[u];
+        MR[c.tid + kBlock * u] = (aeta[u] * dn * dp - rr * (wn * dp * arn[u] + wp * dn * arp[u])) / adet[u];
+      }
+    BSYNC();
+    SEG_LAP(8);
+    // B: waypoint right-hand sides, c_t = Linv_t b_t (octet gather in-wave)
+#pragma unroll
+    for (int u = 0; u < CS; ++u)
+    {
+      if (cact[u])
+      {
+        const double bx = sig * cx[u] - cq[u];
+        const double eb = crb[u] * czb[u] - cyb[u];
+        double b = bx + cbs[u] * eb;
+        if (cfr[u] >= 0)
+        {
+          const double ef = crf[u] * czf[u] - cyf[u];
+          b += cfs[u] * ef;
+        }
+#pragma unroll
+        for (int p = 0; p < kMaxStepRows; ++p)
+          if (p < cnrow[u])
+            b += cgs[u][p] * MR[crow[u][p]];
+        lds(BXW)[ccol[u]] = b;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (cact[u])
+      {
+        const int i = (c.tid + kBlock * u) & 7;
+        const int base = ccol[u] - i;
+        double v = 0;
+#pragma unroll
+        for (int k = 0; k < THIP_MAX_DOF; ++k)
+          if (k <= i)
+            v += cli[u][k] * lds(BXW)[base + k];
+        lds(CV)[ccol[u]] = v;
+      }
+    }
+    BSYNC();
+    SEG_LAP(15);
+    if (c.wave == 0)
+      block_chain<true>(sv.M, CV, YV, N, D, c.lane);
+    BSYNC();
+    SEG_LAP(9);
+#pragma unroll
+    for (int u = 0; u < CS; ++u)
+      if (cact[u])
+      {
+        const int i = (c.tid + kBlock * u) & 7;
+        const int base = ccol[u] - i;
+        double v = 0;
+#pragma unroll
+        for (int k = 0; k < THIP_MAX_DOF; ++k)
+          if (k >= i && k < D)
+            v += clc[u][k] * lds(YV)[base + k];
+        lds(CV)[ccol[u]] = v;
+      }
+    BSYNC();
+    SEG_LAP(15);
+    if (c.wave == 0)
+      block_chain<false>(sv.Nb, CV, CV, N, D, c.lane);
+    BSYNC();
+    SEG_LAP(10);
+    // E: back-substitution, z~ = A x~, relaxed updates
+    const bool last = (iter == n_iter - 1);
+#pragma unroll
+    for (int u = 0; u < CS; ++u)
+      if (cact[u])
+      {
+        const double xt = lds(CV)[ccol[u]];
+        admm_row_update(czb[u], cyb[u], cdyb[u], cbs[u] * xt, crb[u], clb[u], cub[u], al);
+        if (cfr[u] >= 0)
+          admm_row_update(czf[u], cyf[u], cdyf[u], cfs[u] * xt, crf[u], clf[u], cuf[u], al);
+        const double xv = al * xt + (1.0 - al) * cx[u];
+        cdx[u] = xv - cx[u];
+        cx[u] = xv;
+      }
+#pragma unroll
+    for (int u = 0; u < AS; ++u)
+      if (aact[u])
+      {
+        const int t = at[u];
+        double g = 0;
+#pragma unroll
+        for (int j = 0; j < THIP_MAX_DOF; ++j)
+          if (j < D)
+            g += ags[u][j] * lds(CV)[t * D + j];
+        const double dn = adn[u], dp = adp[u], wn = awn[u], wp = awp[u], rr = arr[u];
+        const double rn = arn[u], rp = arp[u];
+        const double det = adet[u];
+        const double cross = wp * rn - wn * rp;
+        const double h = aeta[u] - rr * g;
+        const double an = (dp * rn + rr * wp * cross + wn * dp * h) / det;
+        const double ap = (dn * rp - rr * wn * cross + wp * dn * h) / det;
+        double zt = g;
+        zt += wn * an + wp * ap;
+        admm_row_update(azr[u], ayr[u], adyr[u], zt, rr, alr[u], aur[u], al);
+        admm_row_update(azbn[u], aybn[u], adybn[u], absn[u] * an, arbn[u], albn[u], aubn[u], al);
+        admm_row_update(azbp[u], aybp[u], adybp[u], absp[u] * ap, arbp[u], albp[u], aubp[u], al);
+        const double xvn = al * an + (1.0 - al) * axn[u];
+        const double xvp = al * ap + (1.0 - al) * axp[u];
+        adxn[u] = xvn - axn[u];
+        adxp[u] = xvp - axp[u];
+        axn[u] = xvn;
+        axp[u] = xvp;
+      }
+    (void)last;
+    SEG_LAP(11);
+  }
+#undef SEG_LAP
+  // write back
+#pragma unroll
+  for (int u = 0; u < CS; ++u)
+    if (cact[u])
+    {
+      const int col = ccol[u], br = nr + col;
+      XA[col] = cx[u];
+      DX[col] = cdx[u];
+      Z[br] = czb[u];
+      Y[br] = cyb[u];
+      DY[br] = cdyb[u];
+      if (cfr[u] >= 0)
+      {
+        Z[cfr[u]] = czf[u];
+        Y[cfr[u]] = cyf[u];
+        DY[cfr[u]] = cdyf[u];
+      }
+    }
+#pragma unroll
+  for (int u = 0; u < AS; ++u)
+    if (aact[u])
+    {
+      const int a = c.tid + kBlock * u;
+      const int r = nfr + a, ca = nx + 2 * a, brn = nr + ca, brp = brn + 1;
+      XA[ca] = axn[u];
+      XA[ca + 1] = axp[u];
+      DX[ca] = adxn[u];
+      DX[ca + 1] = adxp[u];
+      Z[r] = azr[u];
+      Y[r] = ayr[u];
+      DY[r] = adyr[u];
+      Z[brn] = azbn[u];
+      Y[brn] = aybn[u];
+      DY[brn] = adybn[u];
+      Z[brp] = azbp[u];
+      Y[brp] = aybp[u];
+      DY[brp] = adybp[u];
+    }
+  BSYNC();
+}
+
+__device__ void admm_iterations(Ctx& c, Solver& sv, int n_iter)
+{
+  if (c.L.seg_slots == 1)
+    admm_segment<1, 1>(c, sv, n_iter);
+  else
+    admm_segment<2, 2>(c, sv, n_iter);
+}
+
 __device__ double rho_estimate(Ctx& c, const Norms& nm)
 {
   double pr = nm.pr, dr = nm.dr;
@@ -1142,6 +1610,7 @@ __device__ double rho_estimate(Ctx& c, const Norms& nm)
 // polish: returns nothing; updates x/z/y buffers on success
 __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
 {
+  PROF(4);
   const Layout& L = c.L;
   const thip_osqp_settings& os = c.d->osqp;
   const double delta = os.delta;
@@ -1271,6 +1740,7 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
 // Returns the CvxOptStatus.
 __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
 {
+  PROF(12);
   const Layout& L = c.L;
   const int nx = L.nx, D = L.D;
   const thip_osqp_settings& os = c.d->osqp;
@@ -1373,10 +1843,24 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   bool can_check = false;
   int it;
   bool fail = false;
+  const int ct = os.check_termination;
   for (it = 1; it <= os.max_iter; ++it)
   {
-    admm_step(c, sv);
-    can_check = os.check_termination && (it % os.check_termination == 0);
+    if (L.seg_ok)
+    {
+      // register-resident segment up to the next iteration that checks
+      // termination or adapts rho (same iterates as admm_step)
+      int stop = os.max_iter;
+      if (ct)
+        stop = min(stop, (it + ct - 1) / ct * ct);
+      if (os.adaptive_rho && interval)
+        stop = min(stop, (it + interval - 1) / interval * interval);
+      admm_iterations(c, sv, stop - it + 1);
+      it = stop;
+    }
+    else
+      admm_step(c, sv);
+    can_check = ct && (it % ct == 0);
     const int cur = c.s->cur;
     const double* xc = c.a(cur ? A_XA1 : A_XA0);
     const double* zc = c.a(cur ? A_Z1 : A_Z0);
@@ -1498,6 +1982,7 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
 // ======================================================================
 __device__ void sqp_optimize(Ctx& c, Solver& sv)
 {
+  PROF(13);
   const Layout& L = c.L;
   const int nx = L.nx, D = L.D;
   const thip_sqp_params& P = c.d->sqp;
@@ -1759,7 +2244,13 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
   if (b >= args.batch)
     return;
   const Layout& L = args.L;
-  Ctx c(L, args.T, args.desc, args.ws + (long long)b * L.dstride, args.iws + (long long)b * L.istride, dyn, &ctl);
+  // LDS residency plan (Layout::loff): hot QP arrays live in LDS for the
+  // whole launch, the rest in this problem's HBM workspace
+  __shared__ double* ptab[A_COUNT];
+  double* wsb = args.ws + (long long)b * L.dstride;
+  for (int k = threadIdx.x; k < A_COUNT; k += kBlock)
+    ptab[k] = L.loff[k] >= 0 ? dyn + L.loff[k] : wsb + L.doff[k];
+  Ctx c(L, args.T, args.desc, wsb, args.iws + (long long)b * L.istride, dyn, &ctl, ptab);
   Solver sv;
   sv.M = dyn;
   sv.Nb = dyn + L.N * L.D * L.D;
@@ -1768,9 +2259,13 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
     ctl.trace = args.trace ? args.trace + (long long)b * args.trace_cap * 10 : nullptr;
     ctl.trace_cap = args.trace_cap;
     ctl.trace_n = 0;
+    ctl.prof = args.prof ? args.prof + (long long)b * kProfSlots : nullptr;
   }
   __syncthreads();
+  const long long w0 = wall_clock64();
   sqp_optimize(c, sv);
+  if (threadIdx.x == 0 && ctl.prof)
+    ctl.prof[14] += wall_clock64() - w0;
   if (threadIdx.x == 0 && args.trace_n)
     args.trace_n[b] = ctl.trace_n;
   if (c.tid == 0)

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <cstdlib>
 
 #include "layout.hpp"
 
@@ -47,9 +48,11 @@ struct thip_ctx
   double* d_trace = nullptr;
   int* d_trace_n = nullptr;
   int trace_cap = 0;
+  long long* d_prof = nullptr;
   bool uploaded = false;
   bool ran = false;
-  size_t lds_bytes = 0;
+  size_t lds_bytes = 0;      // sqp_kernel: scratch + LDS-resident arrays
+  size_t lds_lin_bytes = 0;  // linearize_kernel: scratch only
   std::string err;
 };
 
@@ -273,7 +276,45 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   L.istride = ioff;
   const size_t lds_d = std::max<size_t>({ (size_t)(2 * NDD), (size_t)(30 * std::max(L.n_cart, 1)),
                                           (size_t)(L.n_costs + L.n_cnts + 2) });
-  ctx->lds_bytes = lds_d * sizeof(double);
+  ctx->lds_lin_bytes = lds_d * sizeof(double);
+  // LDS residency plan: the per-ADMM-iteration working set, hottest first,
+  // until the budget of one workgroup per CU is used; the rest stays in HBM.
+  {
+    const int order[] = { A_LINV, A_CV,  A_YV, A_BXW, A_BA, A_MR, A_DG, A_GS, A_WS, A_FS, A_BS, A_XA0, A_XA1,
+                          A_Z0,   A_Z1,  A_Y,  A_XT,  A_PZ, A_RHO, A_L, A_U,  A_Q,  A_DX, A_DY, A_PD,  A_PO,
+                          A_E,    A_DS,  A_RE, A_PB,  A_PS, A_PR };
+    long long used = static_cast<long long>(lds_d);
+    used = (used + 7) / 8 * 8;
+    L.lds_scratch = static_cast<int>(used);
+    for (int k = 0; k < A_COUNT; ++k)
+      L.loff[k] = -1;
+    const long long budget = kLdsBudgetBytes / static_cast<long long>(sizeof(double));
+    for (int k : order)
+    {
+      const long long n = (sizes[k] + 7) / 8 * 8;
+      if (used + n > budget)
+        continue;
+      L.loff[k] = static_cast<int>(used);
+      used += n;
+    }
+    L.lds_doubles = static_cast<int>(used);
+    int max_step_rows = 0;
+    for (int t = 0; t < L.N; ++t)
+      max_step_rows = std::max(max_step_rows, step_ptr[static_cast<size_t>(t) + 1] - step_ptr[static_cast<size_t>(t)]);
+    L.seg_ok = (max_step_rows <= kMaxStepRows && L.D <= 8 && L.loff[A_BXW] >= 0 && L.N * 8 <= 2 * kBlock &&
+                L.n_abs <= 2 * kBlock) ? 1 : 0;
+    if (const char* e = std::getenv("THIP_NO_SEGMENT"))
+      if (e[0] == '1')
+        L.seg_ok = 0;
+    L.seg_slots = (L.N * 8 <= kBlock && L.n_abs <= kBlock) ? 1 : 2;
+    if (L.loff[A_LINV] < 0 || L.loff[A_CV] < 0 || L.loff[A_YV] < 0)
+    {
+      g_create_err = "thip_create: problem too large, the block-solve factor does not fit in LDS";
+      delete ctx;
+      return THIP_E_INVALID;
+    }
+    ctx->lds_bytes = static_cast<size_t>(used) * sizeof(double);
+  }
 
   auto fail = [&](const std::string& msg) {
     g_create_err = msg;
@@ -283,7 +324,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess)
     return fail(std::string("hipSetDevice: ") + hipGetErrorString(e));
-  if (ctx->lds_bytes > 60 * 1024)
+  if (ctx->lds_lin_bytes > 60 * 1024)
     return fail("problem too large for the LDS-resident block solve");
   // tables
   std::vector<int> itab;
@@ -335,9 +376,10 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   ctx->own_stream = true;
   hipEventCreate(&ctx->ev0);
   hipEventCreate(&ctx->ev1);
-  if (ctx->lds_bytes > 48 * 1024)
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&sqp_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        static_cast<int>(ctx->lds_bytes));
+  hipFuncSetAttribute(reinterpret_cast<const void*>(&sqp_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                      static_cast<int>(ctx->lds_bytes));
+  hipFuncSetAttribute(reinterpret_cast<const void*>(&linearize_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                      static_cast<int>(ctx->lds_lin_bytes));
   *out = ctx;
   return THIP_OK;
 }
@@ -368,6 +410,7 @@ static KernelArgs make_args(thip_ctx* ctx)
   a.trace = ctx->d_trace;
   a.trace_n = ctx->d_trace_n;
   a.trace_cap = ctx->trace_cap;
+  a.prof = ctx->d_prof;
   return a;
 }
 
@@ -479,7 +522,7 @@ int thip_linearize(thip_ctx* ctx, const double* x, double* err, double* jac)
   HIPCHK(ctx, hipMalloc(&dj, std::max<size_t>(nj, 1) * sizeof(double)));
   hipMemcpyAsync(dx, x, B * static_cast<size_t>(L.nx) * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
   KernelArgs a = make_args(ctx);
-  hipLaunchKernelGGL(linearize_kernel, dim3(ctx->batch), dim3(kBlock), ctx->lds_bytes, ctx->stream, a, dx, de, dj);
+  hipLaunchKernelGGL(linearize_kernel, dim3(ctx->batch), dim3(kBlock), ctx->lds_lin_bytes, ctx->stream, a, dx, de, dj);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess)
   {
@@ -531,6 +574,7 @@ int thip_debug_trace(thip_ctx* ctx, int capacity)
     hipFree(ctx->d_trace);
   if (ctx->d_trace_n)
     hipFree(ctx->d_trace_n);
+  hipFree(ctx->d_prof);
   ctx->d_trace = nullptr;
   ctx->d_trace_n = nullptr;
   ctx->trace_cap = capacity;
@@ -568,6 +612,33 @@ int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws)
   HIPCHK(ctx, hipMemcpy(dws, ctx->d_ws, B * static_cast<size_t>(ctx->L.dstride) * sizeof(double),
                         hipMemcpyDeviceToHost));
   HIPCHK(ctx, hipMemcpy(iws, ctx->d_iws, B * static_cast<size_t>(ctx->L.istride) * sizeof(int),
+                        hipMemcpyDeviceToHost));
+  return THIP_OK;
+}
+
+int thip_debug_profile(thip_ctx* ctx, int enable)
+{
+  if (!ctx)
+    return THIP_E_INVALID;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  if (ctx->d_prof)
+    hipFree(ctx->d_prof);
+  ctx->d_prof = nullptr;
+  if (!enable)
+    return THIP_OK;
+  const size_t n = static_cast<size_t>(ctx->batch) * kProfSlots;
+  HIPCHK(ctx, hipMalloc(&ctx->d_prof, n * sizeof(long long)));
+  HIPCHK(ctx, hipMemset(ctx->d_prof, 0, n * sizeof(long long)));
+  return THIP_OK;
+}
+
+int thip_debug_get_profile(thip_ctx* ctx, long long* counters)
+{
+  if (!ctx || !ctx->d_prof || !counters)
+    return THIP_E_INVALID;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipMemcpy(counters, ctx->d_prof, static_cast<size_t>(ctx->batch) * kProfSlots * sizeof(long long),
                         hipMemcpyDeviceToHost));
   return THIP_OK;
 }

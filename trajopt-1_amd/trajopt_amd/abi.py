@@ -231,6 +231,10 @@ def _declare(lib):
     lib.thip_debug_trace.restype = C.c_int
     lib.thip_debug_get_trace.argtypes = [vp, dp, P(C.c_int)]
     lib.thip_debug_get_trace.restype = C.c_int
+    lib.thip_debug_profile.argtypes = [vp, C.c_int]
+    lib.thip_debug_profile.restype = C.c_int
+    lib.thip_debug_get_profile.argtypes = [vp, P(C.c_longlong)]
+    lib.thip_debug_get_profile.restype = C.c_int
     lib.thip_sizeof_desc.argtypes = []
     lib.thip_sizeof_desc.restype = C.c_int
     return lib
@@ -241,6 +245,14 @@ def load_hip():
     product has no fallback path."""
     global _hip
     if _hip is None:
+        # torch bundles its own libamdhip64.so.7 (same soname as /opt/rocm's):
+        # load it first so the process has one HIP runtime that torch (device
+        # memory, streams, torch.distributed) and this library share.  If ours
+        # loaded first, torch would see no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not HIP_LIB.exists():
             raise RuntimeError(
                 f"{HIP_LIB} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)"

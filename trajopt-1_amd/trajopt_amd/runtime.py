@@ -97,6 +97,19 @@ class BatchTrustRegionSQP:
         self._check(self.lib.thip_debug_get_trace(self.ctx, _dp(rec), cnt), "thip_debug_get_trace")
         return [rec[b, : cnt[b]] for b in range(self.batch)]
 
+    PROFILE_SLOTS = ["admm_step", "residuals", "termination", "factor", "polish", "linearize", "evaluate",
+                     "build_and_scale", "solve_rhs_diag", "fwd_chain", "bwd_chain", "aux_backsub", "qp_solve",
+                     "sqp_total", "sqp_wall_ticks", "seg_rhs_linv"]
+
+    def enable_profile(self, on=True):
+        self._check(self.lib.thip_debug_profile(self.ctx, 1 if on else 0), "thip_debug_profile")
+
+    def get_profile(self):
+        out = np.zeros((self.batch, 16), dtype=np.int64)
+        self._check(self.lib.thip_debug_get_profile(self.ctx, out.ctypes.data_as(C.POINTER(C.c_longlong))),
+                    "thip_debug_get_profile")
+        return out
+
     def close(self):
         if self.ctx:
             self.lib.thip_destroy(self.ctx)
