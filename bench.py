@@ -34,7 +34,7 @@ sys.path.insert(0, str(ROOT / "trajopt-1_amd"))
 
 import numpy as np  # noqa: E402
 
-from trajopt_amd import abi, problems  # noqa: E402
+from trajopt_amd import abi, problems, sharding  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 
@@ -110,14 +110,14 @@ def main():
 
     from trajopt_amd.runtime import BatchTrustRegionSQP
 
-    wl = problems.make_workload(args.config, args.batch, first_problem=rank * args.batch)
+    wl = sharding.rank_workload(args.config, args.batch, rank)
     solver = BatchTrustRegionSQP(wl, device=local_rank)
     solver.upload()
     torch.cuda.set_device(local_rank)
 
     for _ in range(args.warmup):
         solver.run()
-    _, res = solver.download()
+    res = solver.download()[1] if args.warmup > 0 else None
 
     def barrier():
         if world > 1:
@@ -136,23 +136,15 @@ def main():
     x_last, res_last = solver.download()
 
     # every step solves the same problems: the counters must repeat exactly
-    same = all(a.n_sqp_iters == b.n_sqp_iters and a.n_admm_iters == b.n_admm_iters for a, b in zip(res, res_last))
+    same = res is None or all(a.n_sqp_iters == b.n_sqp_iters and a.n_admm_iters == b.n_admm_iters
+                              for a, b in zip(res, res_last))
     if not same:
         raise SystemExit("non-deterministic SQP counters between steps")
     iters_local = sum(r.n_sqp_iters for r in res_last)
     bytes_local, model = algorithmic_bytes(wl, res_last)
     kms = float(np.mean(kernel_ms))
 
-    if world > 1:
-        t = torch.tensor([elapsed, float(iters_local)], dtype=torch.float64)
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed = float(tmax[0])
-        iters_total = float(tsum[1])
-    else:
-        iters_total = float(iters_local)
+    elapsed, iters_total = sharding.reduce_step_stats(elapsed, iters_local, world)
 
     if rank == 0:
         value = iters_total * args.steps / elapsed

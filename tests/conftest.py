@@ -1,0 +1,39 @@
+"""Test configuration.
+
+Markers: `gpu` tests need an MI355X (run on the GPU box with `-m gpu`); all
+other tests run on CPU.  The oracle (oracle/, CPU restatement of the
+reference path) is imported here only as the checker.
+"""
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+for p in (REPO, REPO / "trajopt-1_amd"):
+    if str(p) not in sys.path:
+        sys.path.insert(0, str(p))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD Instinct GPU (MI355X, gfx950)")
+
+
+@pytest.fixture(scope="session")
+def oracle_mod():
+    from oracle import oracle
+
+    oracle.build()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import numpy as np
+
+    d = REPO / "tests" / "golden"
+
+    def load(name):
+        return dict(np.load(d / f"{name}.npz"))
+
+    return load

@@ -1655,16 +1655,13 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
     PS[nc + r] = 0.0;
   }
   BSYNC();
-  // OSQP refines polish_refine_iter times with an LDL factor of the
-  // quasi-definite KKT.  The waypoint-block normal-equation solve used here is
-  // a weaker preconditioner for the same iteration (its dual part is formed as
-  // (A dx - r_y) / delta), so refinement continues until the unregularised KKT
-  // residual stops decreasing: both converge to the same polished KKT point.
-  double rnorm_prev = INFINITY;
-  double bscale[1] = { 0 };
-  FOR(k, nc + L.m) bscale[0] = fmax(bscale[0], fabs(PB[k]));
-  block_max<1>(c, bscale);
-  const int max_refine = os.polish_refine_iter + 24;
+  // OSQP 1.0 polish: one solve with the delta-regularised KKT, then exactly
+  // polish_refine_iter iterative-refinement steps on the unregularised KKT.
+  // In exact arithmetic the refinement iterates depend only on K_delta^-1,
+  // not on how it is applied (OSQP: LDL of the quasi-definite KKT; here the
+  // waypoint-block normal equations), so the same step count reproduces
+  // OSQP's polished point, including when 3 steps leave it inexact.
+  const int max_refine = os.polish_refine_iter;
   for (int it = 0; it <= max_refine; ++it)
   {
     // solve K_delta d = PR  (rhs_x + A_act' r_y / delta), d_y = (A_act d_x - r_y) / delta
@@ -1683,23 +1680,9 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
     if (it == max_refine)
       break;
     // residual of the unregularised KKT: PR = PB - K [x; y]
-    double rn[1] = { 0 };
-    FOR(col, nc)
-    {
-      const double v = PB[col] - col_px(c, col, PS) - col_aty(c, col, PS + nc);
-      PR[col] = v;
-      rn[0] = fmax(rn[0], fabs(v));
-    }
-    FOR(r, L.m)
-    {
-      const double v = (ACT[r] != 0) ? PB[nc + r] - row_ax(c, r, PS) : 0.0;
-      PR[nc + r] = v;
-      rn[0] = fmax(rn[0], fabs(v));
-    }
-    block_max<1>(c, rn);
-    if (it >= os.polish_refine_iter && (rn[0] <= 1e-15 * (1.0 + bscale[0]) || rn[0] >= 0.5 * rnorm_prev))
-      break;
-    rnorm_prev = rn[0];
+    FOR(col, nc) PR[col] = PB[col] - col_px(c, col, PS) - col_aty(c, col, PS + nc);
+    FOR(r, L.m) PR[nc + r] = (ACT[r] != 0) ? PB[nc + r] - row_ax(c, r, PS) : 0.0;
+    BSYNC();
   }
   // polished point: x, z = A x, y (active) -> normal cone projection
   double* pz = PZ;
