@@ -61,6 +61,22 @@ def algorithmic_bytes(wl, results):
     return total, {"fixed": fixed, "per_admm": per_admm, "nnz_L": nnz_l}
 
 
+def measured_traffic(workload_name, batch):
+    """HBM bytes per sqp_kernel launch from the newest committed PMC summary
+    (profiles/*_pmc_hbm.json, tools/collect_profiles.sh) for this workload."""
+    best = None
+    for p in sorted((ROOT / "profiles").glob("*_pmc_hbm.json")):
+        try:
+            d = json.loads(p.read_text())
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload_name and d.get("batch_per_gpu") == batch:
+            best = (p.name, d)
+    if best is None:
+        return None, None
+    return best[1]["hbm_bytes_per_launch"], best[0]
+
+
 def cpu_baseline(config, n_problems, threads):
     """Oracle (CPU restatement of the reference path) on a bounded sample."""
     sys.path.insert(0, str(ROOT))
@@ -149,6 +165,10 @@ def main():
     if rank == 0:
         value = iters_total * args.steps / elapsed
         achieved = bytes_local / (kms * 1e-3) / 1e9
+        workload_name = (f"config {args.config}: 7-DoF PR2 arm x {wl.n_steps} waypoints, JointVel + "
+                         f"{wl.desc.n_cart} CartPose ABS costs, batch {args.batch} per GPU "
+                         "(BasicTrustRegionSQP + OSQP-semantics ADMM/polish)")
+        traffic, traffic_src = measured_traffic(workload_name, args.batch)
         out = {
             "metric": "SQP iters/sec + achieved HBM GB/s, 7-DoF x 30-wpt x 1024-batch",
             "value": value,
@@ -163,9 +183,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (splitmix64 seeds 20261015+b, PR2 right arm; SURVEY.md §8d)",
             "config": {
-                "workload": f"config {args.config}: 7-DoF PR2 arm x {wl.n_steps} waypoints, JointVel + "
-                            f"{wl.desc.n_cart} CartPose ABS costs, batch {args.batch} per GPU "
-                            "(BasicTrustRegionSQP + OSQP-semantics ADMM/polish)",
+                "workload": workload_name,
                 "batch_per_gpu": args.batch,
                 "global_batch": args.batch * world,
                 "sqp_iters_per_step": iters_total,
@@ -180,7 +198,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel_ms": kms,
                 "algorithmic_bytes_per_launch": bytes_local,
                 "model": model,

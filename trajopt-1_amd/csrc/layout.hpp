@@ -18,7 +18,7 @@ constexpr int kWaves = kBlock / 64;
 // CU; the rest is the kernel's static LDS)
 constexpr long long kLdsBudgetBytes = 152 * 1024;
 // CartPose rows per waypoint the register-resident ADMM segment supports
-constexpr int kMaxStepRows = 12;
+constexpr int kMaxStepRows = 8;
 
 // per-problem double workspace arrays
 enum DArr : int

@@ -1310,7 +1310,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   int ccol[CS], cfr[CS], cnrow[CS], crow[CS][kMaxStepRows];
   double cq[CS], cbs[CS], clb[CS], cub[CS], crb[CS], cfs[CS], clf[CS], cuf[CS], crf[CS];
   double cx[CS], czb[CS], cyb[CS], czf[CS], cyf[CS], cdx[CS], cdyb[CS], cdyf[CS];
-  double cli[CS][THIP_MAX_DOF], clc[CS][THIP_MAX_DOF], cgs[CS][kMaxStepRows];
+  double cli[CS][THIP_MAX_DOF], cgs[CS][kMaxStepRows];
 #pragma unroll
   for (int u = 0; u < CS; ++u)
   {
@@ -1357,7 +1357,6 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       for (int k = 0; k < THIP_MAX_DOF; ++k)
       {
         cli[u][k] = (k <= i && k < D) ? LI[t * DD + i * D + k] : 0.0;
-        clc[u][k] = (k >= i && k < D) ? LI[t * DD + k * D + i] : 0.0;
       }
     }
     cdx[u] = cdyb[u] = cdyf[u] = 0.0;
@@ -1487,11 +1486,12 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       {
         const int i = (c.tid + kBlock * u) & 7;
         const int base = ccol[u] - i;
+        const int lbase = (base / D) * DD + i;  // Linv_t[k][i] = LI[t*DD + k*D + i]
         double v = 0;
 #pragma unroll
         for (int k = 0; k < THIP_MAX_DOF; ++k)
           if (k >= i && k < D)
-            v += clc[u][k] * lds(YV)[base + k];
+            v += lds(LI)[lbase + k * D] * lds(YV)[base + k];
         lds(CV)[ccol[u]] = v;
       }
     BSYNC();
@@ -1590,10 +1590,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
 
 __device__ void admm_iterations(Ctx& c, Solver& sv, int n_iter)
 {
-  if (c.L.seg_slots == 1)
-    admm_segment<1, 1>(c, sv, n_iter);
-  else
-    admm_segment<2, 2>(c, sv, n_iter);
+  admm_segment<1, 1>(c, sv, n_iter);
 }
 
 __device__ double rho_estimate(Ctx& c, const Norms& nm)

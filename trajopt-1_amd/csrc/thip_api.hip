@@ -301,12 +301,14 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     int max_step_rows = 0;
     for (int t = 0; t < L.N; ++t)
       max_step_rows = std::max(max_step_rows, step_ptr[static_cast<size_t>(t) + 1] - step_ptr[static_cast<size_t>(t)]);
-    L.seg_ok = (max_step_rows <= kMaxStepRows && L.D <= 8 && L.loff[A_BXW] >= 0 && L.N * 8 <= 2 * kBlock &&
-                L.n_abs <= 2 * kBlock) ? 1 : 0;
+    // one column slot (t, i) and one CartPose row per thread: N <= 32 and
+    // n_abs <= 256; larger problems run the generic admm_step()
+    L.seg_ok = (max_step_rows <= kMaxStepRows && L.D <= 8 && L.loff[A_BXW] >= 0 && L.N * 8 <= kBlock &&
+                L.n_abs <= kBlock) ? 1 : 0;
     if (const char* e = std::getenv("THIP_NO_SEGMENT"))
       if (e[0] == '1')
         L.seg_ok = 0;
-    L.seg_slots = (L.N * 8 <= kBlock && L.n_abs <= kBlock) ? 1 : 2;
+    L.seg_slots = 1;
     if (L.loff[A_LINV] < 0 || L.loff[A_CV] < 0 || L.loff[A_YV] < 0)
     {
       g_create_err = "thip_create: problem too large, the block-solve factor does not fit in LDS";
