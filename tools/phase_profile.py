@@ -33,7 +33,7 @@ print(f"shader clock ~{mhz:.0f} MHz; per problem: admm {admm.mean():.0f} (max {a
 slowest = int(np.argmax(pf[:, 14]))
 print(f"slowest problem {slowest}: {pf[slowest, 14] / 100:.0f} us wall, admm {admm[slowest]:.0f}")
 tot = pf[:, 13].sum()
-for k, name in [kv for kv in enumerate(BatchTrustRegionSQP.PROFILE_SLOTS) if kv[0] != 14]:
+for k, name in [kv for kv in enumerate(BatchTrustRegionSQP.PROFILE_SLOTS) if kv[0] != 14 and not kv[1].startswith('unused')]:
     v = pf[:, k].sum()
     per_admm = v / admm.sum()
     print(f"  {k:2d} {name:<16} {100 * v / tot:6.1f}%   {per_admm:10.0f} cyc/admm-iter   "

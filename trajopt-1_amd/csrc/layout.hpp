@@ -116,6 +116,8 @@ struct Layout
   // resident; seg_slots = column/row slots per thread (1 or 2)
   int seg_ok;
   int seg_slots;
+  // middle block of the twisted block factorisation (N / 2)
+  int tw_mid;
 };
 
 // shared (batch-wide) tables, device resident
@@ -150,6 +152,6 @@ struct KernelArgs
   long long* prof;
 };
 
-constexpr int kProfSlots = 16;
+constexpr int kProfSlots = 24;
 
 }  // namespace thip

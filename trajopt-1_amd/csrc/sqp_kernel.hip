@@ -100,7 +100,8 @@ struct Ctx
 // 3 factor, 4 polish, 5 linearize, 6 evaluate, 7 build_and_scale,
 // 8 solve rhs + block diag (segment: phase A), 9 forward chain, 10 backward
 // chain, 11 aux back-substitution (segment: phase E), 12 qp_solve, 13 sqp
-// total, 14 sqp total (wall clock, 100 MHz ticks), 15 segment phases B + C2.
+// total, 14 sqp total (wall clock, 100 MHz ticks), 15 segment phase B
+// (rhs + Linv b), 16 segment phase C2 (Linv^T y + middle block).
 struct ProfScope
 {
   long long* p;
@@ -562,6 +563,59 @@ __device__ __forceinline__ double rho_k(const Ctx& c, int r, bool polish, double
   return c.ia(I_ACT)[r] != 0 ? 1.0 / delta : 0.0;
 }
 
+__device__ __forceinline__ void wave_sync()
+{
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// In-place lower Cholesky of the D x D block S (one wave; lane i owns row i),
+// then Li = L^-1 (lane j solves column j).  Flags `bad` if S is not positive
+// definite.
+__device__ __forceinline__ void chol_inv_block(double* S, double* Li, int D, int lane, int& bad)
+{
+  for (int j = 0; j < D; ++j)
+  {
+    if (lane == j)
+    {
+      double v = S[j * D + j];
+      for (int k = 0; k < j; ++k)
+        v -= S[j * D + k] * S[j * D + k];
+      if (!(v > 0))
+      {
+        bad = 1;
+        v = 1.0;
+      }
+      S[j * D + j] = sqrt(v);
+    }
+    wave_sync();
+    if (lane > j && lane < D)
+    {
+      const int i = lane;
+      double v = S[i * D + j];
+      for (int k = 0; k < j; ++k)
+        v -= S[i * D + k] * S[j * D + k];
+      S[i * D + j] = v / S[j * D + j];
+    }
+    wave_sync();
+  }
+  if (lane < D)
+  {
+    const int j = lane;
+    double xcol[THIP_MAX_DOF];
+    for (int i = 0; i < D; ++i)
+    {
+      double v = (i == j) ? 1.0 : 0.0;
+      for (int k = 0; k < i; ++k)
+        v -= S[i * D + k] * xcol[k];
+      xcol[i] = (i < j) ? 0.0 : v / S[i * D + i];
+    }
+    for (int i = 0; i < D; ++i)
+      Li[i * D + j] = xcol[i];
+  }
+  wave_sync();
+}
+
 // returns false if the reduced matrix is not positive definite
 __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delta)
 {
@@ -611,110 +665,106 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
     KB[e] = v;
   }
   BSYNC();
-  // sequential block Cholesky by wave 0; lanes own rows of the 7x7 blocks
-  __shared__ double Sblk[THIP_MAX_DOF * THIP_MAX_DOF];
-  __shared__ double Lsub[THIP_MAX_DOF * THIP_MAX_DOF];
+  // Twisted ("burn at both ends") block Cholesky.  Wave 0 eliminates the
+  // waypoints 0..m-1 from the top, wave 1 eliminates N-1..m+1 from the bottom
+  // (the same recurrence on the reversed block order; the JointVel couplings
+  // K_{t+1,t} = diag(PO_t) are symmetric), concurrently; the middle block m
+  // takes both Schur complements.  Per eliminated block t:
+  //   S_t = KB_t - Lsub Lsub^T, L_t = chol(S_t), LI_t = L_t^-1,
+  //   M_t = LI_t Lsub (coupling from the previous block of its half),
+  //   Lsub <- O LI_t^T (coupling into the next block), N_t = LI_t^T Lsub^T.
+  // Bottom-half matrices are stored at their own waypoint index; the middle
+  // stores M_m (top coupling) in M[m] and M'_m (bottom coupling) in Nb[m].
+  __shared__ double Sblk[2][THIP_MAX_DOF * THIP_MAX_DOF];
+  __shared__ double Lsub[2][THIP_MAX_DOF * THIP_MAX_DOF];
   __shared__ int bad;
+  const int m = L.tw_mid;
+  const int DD = D * D;
   if (c.tid == 0)
     bad = 0;
   BSYNC();
-  if (c.wave == 0)
+  if (c.wave < 2)
   {
-    const int DD = D * D;
-    for (int t = 0; t < N; ++t)
+    const int w = c.wave;
+    const int len = (w == 0) ? m : (N - 1 - m);
+    double* S = Sblk[w];
+    double* Ls = Lsub[w];
+    for (int k = 0; k < len; ++k)
     {
-      // S = KB_t - Lsub Lsub^T   (Lsub = L_{t,t-1})
+      const int t = (w == 0) ? k : (N - 1 - k);
+      const int cpl = (w == 0) ? t : t - 1;  // PO index of the coupling to the next block
       for (int e = c.lane; e < DD; e += 64)
       {
         const int i = e / D, j = e % D;
         double v = KB[t * DD + e];
-        if (t > 0)
-          for (int k = 0; k < D; ++k)
-            v -= Lsub[i * D + k] * Lsub[j * D + k];
-        Sblk[e] = v;
+        if (k > 0)
+          for (int q = 0; q < D; ++q)
+            v -= Ls[i * D + q] * Ls[j * D + q];
+        S[e] = v;
       }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      // in-place Cholesky (lower) of Sblk: lane i owns row i
-      for (int j = 0; j < D; ++j)
-      {
-        if (c.lane == j)
-        {
-          double v = Sblk[j * D + j];
-          for (int k = 0; k < j; ++k)
-            v -= Sblk[j * D + k] * Sblk[j * D + k];
-          if (!(v > 0))
-          {
-            bad = 1;
-            v = 1.0;
-          }
-          Sblk[j * D + j] = sqrt(v);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (c.lane > j && c.lane < D)
-        {
-          const int i = c.lane;
-          double v = Sblk[i * D + j];
-          for (int k = 0; k < j; ++k)
-            v -= Sblk[i * D + k] * Sblk[j * D + k];
-          Sblk[i * D + j] = v / Sblk[j * D + j];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-      }
-      // Linv_t: lane j solves L x = e_j (column j of the inverse)
-      double* Li = LI + t * DD;
-      if (c.lane < D)
-      {
-        const int j = c.lane;
-        double xcol[THIP_MAX_DOF];
-        for (int i = 0; i < D; ++i)
-        {
-          double v = (i == j) ? 1.0 : 0.0;
-          for (int k = 0; k < i; ++k)
-            v -= Sblk[i * D + k] * xcol[k];
-          xcol[i] = (i < j) ? 0.0 : v / Sblk[i * D + i];
-        }
-        for (int i = 0; i < D; ++i)
-          Li[i * D + j] = xcol[i];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      // M_t = Linv_t * L_{t,t-1}
-      if (t > 0)
+      wave_sync();
+      chol_inv_block(S, LI + t * DD, D, c.lane, bad);
+      const double* Li = LI + t * DD;
+      if (k > 0)
         for (int e = c.lane; e < DD; e += 64)
         {
           const int i = e / D, j = e % D;
           double v = 0;
-          for (int k = 0; k <= i; ++k)
-            v += Li[i * D + k] * Lsub[k * D + j];
+          for (int q = 0; q <= i; ++q)
+            v += Li[i * D + q] * Ls[q * D + j];
           sv.M[t * DD + e] = v;
         }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      if (t < N - 1)
+      wave_sync();
+      for (int e = c.lane; e < DD; e += 64)
       {
-        // L_{t+1,t} = O_t Linv_t^T, O_t = diag(PO[t*D + i])
-        for (int e = c.lane; e < DD; e += 64)
-        {
-          const int i = e / D, k = e % D;
-          Lsub[e] = PO[t * D + i] * Li[k * D + i];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        // N_t = Linv_t^T L_{t+1,t}^T : N[i][j] = sum_k Linv[k][i] Lsub[j][k]
-        for (int e = c.lane; e < DD; e += 64)
-        {
-          const int i = e / D, j = e % D;
-          double v = 0;
-          for (int k = i; k < D; ++k)
-            v += Li[k * D + i] * Lsub[j * D + k];
-          sv.Nb[t * DD + e] = v;
-        }
+        const int i = e / D, q = e % D;
+        Ls[e] = PO[cpl * D + i] * Li[q * D + i];
       }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
+      for (int e = c.lane; e < DD; e += 64)
+      {
+        const int i = e / D, j = e % D;
+        double v = 0;
+        for (int q = i; q < D; ++q)
+          v += Li[q * D + i] * Ls[j * D + q];
+        sv.Nb[t * DD + e] = v;
+      }
+      wave_sync();
+    }
+  }
+  BSYNC();
+  if (c.wave == 0)
+  {
+    const bool top = m > 0, bot = (N - 1 - m) > 0;
+    double* S = Sblk[0];
+    for (int e = c.lane; e < DD; e += 64)
+    {
+      const int i = e / D, j = e % D;
+      double v = KB[m * DD + e];
+      if (top)
+        for (int q = 0; q < D; ++q)
+          v -= Lsub[0][i * D + q] * Lsub[0][j * D + q];
+      if (bot)
+        for (int q = 0; q < D; ++q)
+          v -= Lsub[1][i * D + q] * Lsub[1][j * D + q];
+      S[e] = v;
+    }
+    wave_sync();
+    chol_inv_block(S, LI + m * DD, D, c.lane, bad);
+    const double* Li = LI + m * DD;
+    for (int e = c.lane; e < DD; e += 64)
+    {
+      const int i = e / D, j = e % D;
+      double vt = 0, vb = 0;
+      for (int q = 0; q <= i; ++q)
+      {
+        vt += Li[i * D + q] * Lsub[0][q * D + j];
+        vb += Li[i * D + q] * Lsub[1][q * D + j];
+      }
+      if (top)
+        sv.M[m * DD + e] = vt;
+      if (bot)
+        sv.Nb[m * DD + e] = vb;
     }
   }
   BSYNC();
@@ -779,9 +829,10 @@ __device__ __forceinline__ double cross_octet_sum(double v)
 // per chunk); inside a chunk the steps are unrolled with static parity.
 constexpr int kChainChunk = 8;
 
-template <bool FWD>
-__device__ __forceinline__ void block_chain(const double* Gp, const double* cvp, double* outp, int N, int D,
-                                            int lane)
+// v_t = c_t - G_t v_{t-dir} for t = t0 + dir, ..., t0 + dir * nsteps, from
+// v_{t0} = c_{t0} (written to out[t0] if store_first).
+__device__ __forceinline__ void block_chain(const double* Gp, const double* cvp, double* outp, int t0, int nsteps,
+                                            int dir, bool store_first, int D, int lane)
 {
   const lds_f64* G = lds(Gp);
   const lds_f64* cv = lds(cvp);
@@ -789,34 +840,27 @@ __device__ __forceinline__ void block_chain(const double* Gp, const double* cvp,
   const int i = lane >> 3, k = lane & 7;
   const bool act = (i < D) && (k < D);
   const int DD = D * D;
-  const int t0 = FWD ? 0 : N - 1;
   double v = (k < D) ? cv[t0 * D + k] : 0.0;  // column layout
-  if (i == 0 && k < D)
+  if (store_first && i == 0 && k < D)
     out[t0 * D + k] = v;
   // offsets of this lane's element in the normal / transposed block
   const int off_n = i * D + k, off_t = k * D + i;
-  for (int s0 = 1; s0 < N; s0 += kChainChunk)
+  for (int s0 = 1; s0 <= nsteps; s0 += kChainChunk)
   {
     double g[kChainChunk], cc[kChainChunk];
 #pragma unroll
     for (int u = 0; u < kChainChunk; ++u)
     {
       const int s = s0 + u;
-      const int t = FWD ? s : N - 1 - s;
-      const bool ok = s < N;
+      const bool ok = s <= nsteps;
+      const int t = ok ? t0 + dir * s : t0;  // clamped: every lane loads a valid address
       // s0 is odd, so even u are odd steps (normal block, c by row i)
-      if ((u & 1) == 0)
-      {
-        g[u] = (ok && act) ? G[t * DD + off_n] : 0.0;
-        cc[u] = (ok && i < D) ? cv[t * D + i] : 0.0;
-      }
-      else
-      {
-        g[u] = (ok && act) ? G[t * DD + off_t] : 0.0;
-        cc[u] = (ok && k < D) ? cv[t * D + k] : 0.0;
-      }
+      const double gv = G[t * DD + (((u & 1) == 0) ? off_n : off_t)];
+      const double cvv = cv[t * D + (((u & 1) == 0) ? (i < D ? i : 0) : (k < D ? k : 0))];
+      g[u] = (ok && act) ? gv : 0.0;
+      cc[u] = (ok && (((u & 1) == 0) ? (i < D) : (k < D))) ? cvv : 0.0;
     }
-    // serial part: no loads, stores or branches (steps past N compute zeros)
+    // serial part: no loads, stores or branches (steps past nsteps compute zeros)
     double vs[kChainChunk];
 #pragma unroll
     for (int u = 0; u < kChainChunk; ++u)
@@ -832,16 +876,85 @@ __device__ __forceinline__ void block_chain(const double* Gp, const double* cvp,
     for (int u = 0; u < kChainChunk; ++u)
     {
       const int s = s0 + u;
-      const int t = FWD ? s : N - 1 - s;
+      const int t = t0 + dir * s;
       if ((u & 1) == 0)
       {
-        if (s < N && k == 0 && i < D)
+        if (s <= nsteps && k == 0 && i < D)
           out[t * D + i] = vs[u];
       }
-      else if (s < N && i == 0 && k < D)
+      else if (s <= nsteps && i == 0 && k < D)
         out[t * D + k] = vs[u];
     }
   }
+}
+
+// Forward solve of the twisted factor: y = L^-1 b given c_t = LI_t b_t in
+// CV.  Wave 0 runs the top chain (t = 1..m-1), wave 1 the bottom chain
+// (t = N-2..m+1); the middle block is finished by twisted_middle().
+__device__ __forceinline__ void twisted_forward(const Ctx& c, const Solver& sv, double* CV, double* YV)
+{
+  const int N = c.L.N, m = c.L.tw_mid;
+  if (c.wave == 0)
+    block_chain(sv.M, CV, YV, 0, m - 1, +1, true, c.L.D, c.lane);
+  else if (c.wave == 1 && N - 1 - m > 0)
+    block_chain(sv.M, CV, YV, N - 1, N - 2 - m, -1, true, c.L.D, c.lane);
+}
+
+// Backward solve of the twisted factor, in place in CV (holding d_t =
+// LI_t^T y_t and x_m at the middle): top chain x_t = d_t - N_t x_{t+1} on
+// wave 0, bottom chain x_t = d_t - N'_t x_{t-1} on wave 1.
+__device__ __forceinline__ void twisted_backward(const Ctx& c, const Solver& sv, double* CV)
+{
+  const int N = c.L.N, m = c.L.tw_mid;
+  if (c.wave == 0)
+    block_chain(sv.Nb, CV, CV, m, m, -1, false, c.L.D, c.lane);
+  else if (c.wave == 1)
+    block_chain(sv.Nb, CV, CV, m, N - 1 - m, +1, false, c.L.D, c.lane);
+}
+
+// d_t[i] = (LI_t^T y_t)[i] for column (t, i), t != middle.
+__device__ __forceinline__ double twisted_dvalue(const Ctx& c, const double* LIp, const double* YVp, int t, int i)
+{
+  const int D = c.L.D, DD = D * D;
+  const lds_f64* LI = lds(LIp);
+  const lds_f64* YV = lds(YVp);
+  double v = 0;
+#pragma unroll
+  for (int k = 0; k < THIP_MAX_DOF; ++k)
+    if (k >= i && k < D)
+      v += LI[t * DD + k * D + i] * YV[t * D + k];
+  return v;
+}
+
+// The middle block of the twisted solve, by one whole wave in the chain's
+// octet layout: y_m = c_m - M_m y_{m-1} - M'_m y_{m+1} (octet reduction),
+// x_m = LI_m^T y_m (cross-octet reduction), written over c_m in CV.
+__device__ __forceinline__ void twisted_middle(const Ctx& c, const Solver& sv, const double* LIp, double* CVp,
+                                               const double* YVp)
+{
+  const int D = c.L.D, DD = D * D, m = c.L.tw_mid, N = c.L.N;
+  const int i = c.lane >> 3, k = c.lane & 7;
+  const bool act = (i < D) && (k < D);
+  const lds_f64* LI = lds(LIp);
+  const lds_f64* YV = lds(YVp);
+  const lds_f64* M = lds(sv.M);
+  const lds_f64* Mb = lds(sv.Nb);
+  lds_f64* CV = lds(CVp);
+  double p = 0.0;
+  if (act)
+  {
+    if (m > 0)
+      p = M[m * DD + i * D + k] * YV[(m - 1) * D + k];
+    if (N - 1 - m > 0)
+      p += Mb[m * DD + i * D + k] * YV[(m + 1) * D + k];
+  }
+  const double s = octet_sum(p);
+  const double ym = (i < D) ? CV[m * D + i] - s : 0.0;  // row layout
+  const double q = act ? LI[m * DD + i * D + k] * ym : 0.0;
+  const double xm = cross_octet_sum(q);                  // column layout
+  wave_sync();
+  if (i == 0 && k < D)
+    CV[m * D + k] = xm;
 }
 
 // Solve K [x; aux] = r + A' eta, with r (n_cols) in A_BXW (overwritten) and
@@ -862,7 +975,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     tq = tn;                    \
   }
   const Layout& L = c.L;
-  const int D = L.D, nx = L.nx, N = L.N, DD = D * D, nfr = L.n_fixed_rows;
+  const int D = L.D, nx = L.nx, DD = D * D, nfr = L.n_fixed_rows;
   const double *GS = c.a(A_GS), *WS = c.a(A_WS), *DG = c.a(A_DG), *LI = c.a(A_LINV), *BS = c.a(A_BS),
                *FS = c.a(A_FS);
   double *BX = c.a(A_BXW), *BA = c.a(A_BA), *MR = c.a(A_MR), *CV = c.a(A_CV), *YV = c.a(A_YV);
@@ -904,24 +1017,31 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   }
   BSYNC();
   PROF_LAP(8);
-  // forward chain y_t = c_t - M_t y_{t-1}
-  if (c.wave == 0)
-    block_chain<true>(sv.M, CV, YV, N, D, c.lane);
+  // forward chains (twisted factor): y = L^-1 b
+  twisted_forward(c, sv, CV, YV);
   BSYNC();
   PROF_LAP(9);
-  FOR(col, nx)
   {
-    const int t = col / D, i = col % D;
-    double v = 0;
-    for (int k = i; k < D; ++k)
-      v += lds(LI)[t * DD + k * D + i] * lds(YV)[t * D + k];
-    lds(CV)[col] = v;
+    // d = LI^T y off the middle block (all columns read before any write),
+    // x_m at the middle block by the last wave
+    static_assert(THIP_MAX_STEPS * THIP_MAX_DOF <= 2 * kBlock, "two columns per thread");
+    const int m = L.tw_mid;
+    const int c0 = c.tid, c1 = c.tid + kBlock;
+    const bool w0 = c0 < nx && c0 / D != m, w1 = c1 < nx && c1 / D != m;
+    const double d0 = w0 ? twisted_dvalue(c, LI, YV, c0 / D, c0 % D) : 0.0;
+    const double d1 = w1 ? twisted_dvalue(c, LI, YV, c1 / D, c1 % D) : 0.0;
+    if (c.wave == kWaves - 1)
+      twisted_middle(c, sv, LI, CV, YV);
+    BSYNC();
+    if (w0)
+      lds(CV)[c0] = d0;
+    if (w1)
+      lds(CV)[c1] = d1;
   }
   BSYNC();
   PROF_LAP(8);
-  // backward chain x_t = d_t - N_t x_{t+1}
-  if (c.wave == 0)
-    block_chain<false>(sv.Nb, CV, CV, N, D, c.lane);  // in place: x lands in CV
+  // backward chains, in place: x lands in CV
+  twisted_backward(c, sv, CV);
   BSYNC();
   PROF_LAP(10);
   FOR(col, nx) out[col] = CV[col];
@@ -1278,10 +1398,11 @@ __device__ void admm_step(Ctx& c, Solver& sv)
 // of admm_step() + reduced_solve(), so both paths give identical iterates.
 // State is written back to A_XA0/A_Z0/A_Y/A_DX/A_DY at the end of the segment
 // for the residual / termination / rho-update / polish code.
-__device__ __forceinline__ void admm_row_update(double& z, double& y, double& dy, double zt, double rho, double lo,
-                                                double up, double al)
+// rinv = 1 / rho, precomputed per segment (OSQP keeps rho_inv_vec)
+__device__ __forceinline__ void admm_row_update(double& z, double& y, double& dy, double zt, double rho, double rinv,
+                                                double lo, double up, double al)
 {
-  double zr = (1.0 / rho) * y;
+  double zr = rinv * y;
   zr = zr + al * zt;
   zr = zr + (1.0 - al) * z;
   zr = fmin(fmax(zr, lo), up);
@@ -1309,7 +1430,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   bool cact[CS];
   int ccol[CS], cfr[CS], cnrow[CS], crow[CS][kMaxStepRows];
   double cq[CS], cbs[CS], clb[CS], cub[CS], crb[CS], cfs[CS], clf[CS], cuf[CS], crf[CS];
-  double cx[CS], czb[CS], cyb[CS], czf[CS], cyf[CS], cdx[CS], cdyb[CS], cdyf[CS];
+  double cx[CS], czb[CS], cyb[CS], czf[CS], cyf[CS], cdx[CS], cdyb[CS], cdyf[CS], crbi[CS], crfi[CS];
   double cli[CS][THIP_MAX_DOF], cgs[CS][kMaxStepRows];
 #pragma unroll
   for (int u = 0; u < CS; ++u)
@@ -1328,6 +1449,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       clb[u] = Lo[br];
       cub[u] = Up[br];
       crb[u] = RH[br];
+      crbi[u] = 1.0 / crb[u];
       cx[u] = XA[col];
       czb[u] = Z[br];
       cyb[u] = Y[br];
@@ -1340,6 +1462,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
         clf[u] = Lo[fr];
         cuf[u] = Up[fr];
         crf[u] = RH[fr];
+        crfi[u] = 1.0 / crf[u];
         czf[u] = Z[fr];
         cyf[u] = Y[fr];
       }
@@ -1368,7 +1491,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   double aqn[AS], aqp[AS], absn[AS], absp[AS], albn[AS], aubn[AS], arbn[AS], albp[AS], aubp[AS], arbp[AS];
   double axn[AS], axp[AS], azr[AS], ayr[AS], azbn[AS], aybn[AS], azbp[AS], aybp[AS];
   double adxn[AS], adxp[AS], adyr[AS], adybn[AS], adybp[AS];
-  double arn[AS], arp[AS], aeta[AS];
+  double arn[AS], arp[AS], aeta[AS], arri[AS], arbni[AS], arbpi[AS], adeti[AS];
 #pragma unroll
   for (int u = 0; u < AS; ++u)
   {
@@ -1386,6 +1509,8 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       adn[u] = DG[ca];
       adp[u] = DG[ca + 1];
       adet[u] = adn[u] * adp[u] + arr[u] * (adn[u] * awp[u] * awp[u] + adp[u] * awn[u] * awn[u]);
+      adeti[u] = 1.0 / adet[u];
+      arri[u] = 1.0 / arr[u];
 #pragma unroll
       for (int j = 0; j < THIP_MAX_DOF; ++j)
         ags[u][j] = (j < D) ? GS[a * D + j] : 0.0;
@@ -1399,6 +1524,8 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       albp[u] = Lo[brp];
       aubp[u] = Up[brp];
       arbp[u] = RH[brp];
+      arbni[u] = 1.0 / arbn[u];
+      arbpi[u] = 1.0 / arbp[u];
       axn[u] = XA[ca];
       axp[u] = XA[ca + 1];
       azr[u] = Z[r];
@@ -1412,13 +1539,16 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   }
   BSYNC();
 
+  // phase laps accumulate in registers and are flushed once per segment
+  // (a global read-modify-write per lap would stall wave 0 inside the loop)
   long long* pf = (c.tid == 0) ? c.s->prof : nullptr;
   long long tq = pf ? clock64() : 0;
-#define SEG_LAP(slot)                 \
+  long long lap8 = 0, lap9 = 0, lap10 = 0, lap11 = 0, lap15 = 0, lap16 = 0;
+#define SEG_LAP(acc)                  \
   if (pf)                             \
   {                                   \
     const long long tn = clock64();   \
-    pf[slot] += tn - tq;              \
+    acc += tn - tq;                   \
     tq = tn;                          \
   }
   for (int iter = 0; iter < n_iter; ++iter)
@@ -1436,10 +1566,10 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
         arn[u] = bxn + absn[u] * ebn;
         arp[u] = bxp + absp[u] * ebp;
         const double dn = adn[u], dp = adp[u], wn = awn[u], wp = awp[u], rr = arr[u];
-        MR[c.tid + kBlock * u] = (aeta[u] * dn * dp - rr * (wn * dp * arn[u] + wp * dn * arp[u])) / adet[u];
+        MR[c.tid + kBlock * u] = (aeta[u] * dn * dp - rr * (wn * dp * arn[u] + wp * dn * arp[u])) * adeti[u];
       }
     BSYNC();
-    SEG_LAP(8);
+    SEG_LAP(lap8);
     // B: waypoint right-hand sides, c_t = Linv_t b_t (octet gather in-wave)
 #pragma unroll
     for (int u = 0; u < CS; ++u)
@@ -1475,31 +1605,27 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       }
     }
     BSYNC();
-    SEG_LAP(15);
-    if (c.wave == 0)
-      block_chain<true>(sv.M, CV, YV, N, D, c.lane);
+    SEG_LAP(lap15);
+    twisted_forward(c, sv, CV, YV);
     BSYNC();
-    SEG_LAP(9);
+    SEG_LAP(lap9);
+    // d = LI^T y off the middle block; x_m by the last wave (no other thread
+    // touches CV[m])
 #pragma unroll
     for (int u = 0; u < CS; ++u)
       if (cact[u])
       {
-        const int i = (c.tid + kBlock * u) & 7;
-        const int base = ccol[u] - i;
-        const int lbase = (base / D) * DD + i;  // Linv_t[k][i] = LI[t*DD + k*D + i]
-        double v = 0;
-#pragma unroll
-        for (int k = 0; k < THIP_MAX_DOF; ++k)
-          if (k >= i && k < D)
-            v += lds(LI)[lbase + k * D] * lds(YV)[base + k];
-        lds(CV)[ccol[u]] = v;
+        const int q = c.tid + kBlock * u;
+        if ((q >> 3) != L.tw_mid)
+          lds(CV)[ccol[u]] = twisted_dvalue(c, LI, YV, q >> 3, q & 7);
       }
+    if (c.wave == kWaves - 1)
+      twisted_middle(c, sv, LI, CV, YV);
     BSYNC();
-    SEG_LAP(15);
-    if (c.wave == 0)
-      block_chain<false>(sv.Nb, CV, CV, N, D, c.lane);
+    SEG_LAP(lap16);
+    twisted_backward(c, sv, CV);
     BSYNC();
-    SEG_LAP(10);
+    SEG_LAP(lap10);
     // E: back-substitution, z~ = A x~, relaxed updates
     const bool last = (iter == n_iter - 1);
 #pragma unroll
@@ -1507,9 +1633,9 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       if (cact[u])
       {
         const double xt = lds(CV)[ccol[u]];
-        admm_row_update(czb[u], cyb[u], cdyb[u], cbs[u] * xt, crb[u], clb[u], cub[u], al);
+        admm_row_update(czb[u], cyb[u], cdyb[u], cbs[u] * xt, crb[u], crbi[u], clb[u], cub[u], al);
         if (cfr[u] >= 0)
-          admm_row_update(czf[u], cyf[u], cdyf[u], cfs[u] * xt, crf[u], clf[u], cuf[u], al);
+          admm_row_update(czf[u], cyf[u], cdyf[u], cfs[u] * xt, crf[u], crfi[u], clf[u], cuf[u], al);
         const double xv = al * xt + (1.0 - al) * cx[u];
         cdx[u] = xv - cx[u];
         cx[u] = xv;
@@ -1526,16 +1652,16 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
             g += ags[u][j] * lds(CV)[t * D + j];
         const double dn = adn[u], dp = adp[u], wn = awn[u], wp = awp[u], rr = arr[u];
         const double rn = arn[u], rp = arp[u];
-        const double det = adet[u];
+        const double deti = adeti[u];
         const double cross = wp * rn - wn * rp;
         const double h = aeta[u] - rr * g;
-        const double an = (dp * rn + rr * wp * cross + wn * dp * h) / det;
-        const double ap = (dn * rp - rr * wn * cross + wp * dn * h) / det;
+        const double an = (dp * rn + rr * wp * cross + wn * dp * h) * deti;
+        const double ap = (dn * rp - rr * wn * cross + wp * dn * h) * deti;
         double zt = g;
         zt += wn * an + wp * ap;
-        admm_row_update(azr[u], ayr[u], adyr[u], zt, rr, alr[u], aur[u], al);
-        admm_row_update(azbn[u], aybn[u], adybn[u], absn[u] * an, arbn[u], albn[u], aubn[u], al);
-        admm_row_update(azbp[u], aybp[u], adybp[u], absp[u] * ap, arbp[u], albp[u], aubp[u], al);
+        admm_row_update(azr[u], ayr[u], adyr[u], zt, rr, arri[u], alr[u], aur[u], al);
+        admm_row_update(azbn[u], aybn[u], adybn[u], absn[u] * an, arbn[u], arbni[u], albn[u], aubn[u], al);
+        admm_row_update(azbp[u], aybp[u], adybp[u], absp[u] * ap, arbp[u], arbpi[u], albp[u], aubp[u], al);
         const double xvn = al * an + (1.0 - al) * axn[u];
         const double xvp = al * ap + (1.0 - al) * axp[u];
         adxn[u] = xvn - axn[u];
@@ -1544,9 +1670,18 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
         axp[u] = xvp;
       }
     (void)last;
-    SEG_LAP(11);
+    SEG_LAP(lap11);
   }
 #undef SEG_LAP
+  if (pf)
+  {
+    pf[8] += lap8;
+    pf[9] += lap9;
+    pf[10] += lap10;
+    pf[11] += lap11;
+    pf[15] += lap15;
+    pf[16] += lap16;
+  }
   // write back
 #pragma unroll
   for (int u = 0; u < CS; ++u)

@@ -309,6 +309,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
       if (e[0] == '1')
         L.seg_ok = 0;
     L.seg_slots = 1;
+    L.tw_mid = L.N / 2;
     if (L.loff[A_LINV] < 0 || L.loff[A_CV] < 0 || L.loff[A_YV] < 0)
     {
       g_create_err = "thip_create: problem too large, the block-solve factor does not fit in LDS";

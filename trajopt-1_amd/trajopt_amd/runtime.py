@@ -99,13 +99,14 @@ class BatchTrustRegionSQP:
 
     PROFILE_SLOTS = ["admm_step", "residuals", "termination", "factor", "polish", "linearize", "evaluate",
                      "build_and_scale", "solve_rhs_diag", "fwd_chain", "bwd_chain", "aux_backsub", "qp_solve",
-                     "sqp_total", "sqp_wall_ticks", "seg_rhs_linv"]
+                     "sqp_total", "sqp_wall_ticks", "seg_B_rhs_linv", "seg_C2_linvT_middle",
+                     "unused17", "unused18", "unused19", "unused20", "unused21", "unused22", "unused23"]
 
     def enable_profile(self, on=True):
         self._check(self.lib.thip_debug_profile(self.ctx, 1 if on else 0), "thip_debug_profile")
 
     def get_profile(self):
-        out = np.zeros((self.batch, 16), dtype=np.int64)
+        out = np.zeros((self.batch, 24), dtype=np.int64)
         self._check(self.lib.thip_debug_get_profile(self.ctx, out.ctypes.data_as(C.POINTER(C.c_longlong))),
                     "thip_debug_get_profile")
         return out
