@@ -76,7 +76,14 @@ extern "C" {
 #define THIP_CVX_INFEASIBLE 1
 #define THIP_CVX_FAILED 2
 
-/* scene primitive types (collision, config C) */
+/* scene primitive types (collision, config C).  A primitive record is 16
+ * doubles: [0] type, then
+ *   SPHERE  [1..3] center, [4] radius
+ *   BOX     [1..3] center, [4..12] rotation (row-major, columns = box axes in
+ *           world), [13..15] half extents
+ *   CAPSULE [1..3] end a, [4..6] end b, [7] radius
+ * Distances are closed-form sphere-vs-primitive signed distances (robot
+ * links carry spheres), the same arithmetic in the oracle and on the GPU. */
 #define THIP_PRIM_SPHERE 0
 #define THIP_PRIM_BOX 1
 #define THIP_PRIM_CAPSULE 2

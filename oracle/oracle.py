@@ -119,6 +119,36 @@ def fwd_kin(chain, q):
     return out
 
 
+def collision_rows(wl, b, x=None, cap=8192):
+    """Linearised collision rows of problem b at trajectory x (default: the
+    initial trajectory); see oracle_collision_rows.  Returns an array
+    [n, 8 + 2 D + 1]."""
+    L = lib()
+    L.oracle_collision_rows.argtypes = [C.POINTER(abi.ProblemDesc), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                        C.POINTER(C.c_double), C.c_int]
+    L.oracle_collision_rows.restype = C.c_int
+    D = wl.n_dof
+    W = 8 + 2 * D + 1
+    xb = np.ascontiguousarray(wl.init[b] if x is None else x, dtype=np.float64)
+    sc = np.ascontiguousarray(wl.scene[b], dtype=np.float64)
+    out = np.zeros((cap, W))
+    n = L.oracle_collision_rows(C.byref(wl.desc), _dp(sc), _dp(xb), _dp(out), cap)
+    if n < 0:
+        raise RuntimeError(L.oracle_last_error().decode())
+    return out[:min(n, cap)]
+
+
+def sphere_prim(c, r, prim):
+    L = lib()
+    L.oracle_sphere_prim.argtypes = [C.POINTER(C.c_double), C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.oracle_sphere_prim.restype = None
+    c = np.ascontiguousarray(c, dtype=np.float64)
+    prim = np.ascontiguousarray(prim, dtype=np.float64)
+    out = np.zeros(8)
+    L.oracle_sphere_prim(_dp(c), float(r), _dp(prim), _dp(out))
+    return out[0], out[1:4], out[4:7]
+
+
 def run_kats():
     if not KAT.exists():
         build()

@@ -3,12 +3,14 @@
 // C entry points of the CPU oracle, loaded (ctypes) only by tests/,
 // __graft_entry__.smoke() and bench.py's cpu_baseline leg.
 #include <atomic>
+#include <cmath>
 #include <cstring>
 #include <exception>
 #include <string>
 #include <thread>
 #include <vector>
 
+#include "collision.hpp"
 #include "terms.hpp"
 
 using namespace orc;
@@ -193,6 +195,134 @@ void oracle_jacobian_transform_error_diff(const double* target, const double* so
                                           double* err6)
 {
   calcJacobianTransformErrorDiff(Iso3::from12(target), Iso3::from12(source), Iso3::from12(source_pert), err6);
+}
+
+// Collision rows of one problem at trajectory x (one record per contact, in
+// flattened ContactResultMap order per step pair): the linearised distance
+// expression CalcDistExpressions* (collision_terms.cpp:463-536) before the
+// hinge.  Record (8 + 2 D + 1 doubles): [t, link, prim, sphere, substate,
+// distance, cc_time, n_kept_coeffs, a_t[D], a_t+1[D], constant]; coefficients
+// dropped by cleanupAff are 0.  Returns the number of records (or -1; if the
+// count exceeds cap only cap records are written).
+int oracle_collision_rows(const thip_problem_desc* d, const double* scene, const double* x, double* out, int cap)
+{
+  try
+  {
+    const int N = d->n_steps, D = d->chain.n_dof;
+    CollisionModel cm;
+    cm.chain = &d->chain;
+    cm.n_spheres = d->n_spheres;
+    for (int s = 0; s < d->n_spheres; ++s)
+    {
+      cm.sphere_link[s] = d->sphere_link[s];
+      cm.sphere_radius[s] = d->sphere_radius[s];
+      for (int i = 0; i < 3; ++i)
+        cm.sphere_center[s][i] = d->sphere_center[s][i];
+    }
+    cm.n_prims = d->n_prims;
+    cm.scene = scene;
+    cm.margin = d->coll_margin;
+    cm.coeff = d->coll_coeff;
+    cm.buffer = d->coll_buffer;
+    cm.lvs = d->coll_lvs;
+    const int first = d->coll_first_step;
+    const int last = (d->coll_last_step < 0) ? N - 1 : d->coll_last_step;
+    auto fixed = [&](int t) {
+      for (int k = 0; k < d->coll_n_fixed; ++k)
+        if (d->coll_fixed_steps[k] == t)
+          return true;
+      return false;
+    };
+    const int W = 8 + 2 * D + 1;
+    int n = 0;
+    for (int t = first; t < last; ++t)
+    {
+      const bool f0 = fixed(t), f1 = fixed(t + 1);
+      const double* q0 = x + t * D;
+      const double* q1 = x + (t + 1) * D;
+      const auto contacts = calcCollisions(cm, q0, q1, f0, f1);
+      for (const auto& c : contacts)
+      {
+        double a0[THIP_MAX_DOF] = {}, a1[THIP_MAX_DOF] = {};
+        double cst = c.distance;
+        if (!f0)
+        {
+          double g[THIP_MAX_DOF], sc;
+          contactGradient(cm, q0, c, false, g, sc);
+          double gd = 0;
+          for (int j = 0; j < D; ++j)
+          {
+            a0[j] = sc * g[j];
+            gd += g[j] * q0[j];
+          }
+          cst += sc * -gd;
+        }
+        if (!f1)
+        {
+          double g[THIP_MAX_DOF], sc;
+          contactGradient(cm, q1, c, true, g, sc);
+          double gd = 0;
+          for (int j = 0; j < D; ++j)
+          {
+            a1[j] = sc * g[j];
+            gd += g[j] * q1[j];
+          }
+          cst += sc * -gd;
+        }
+        int kept = 0;
+        for (int j = 0; j < D; ++j)
+        {
+          if (std::fabs(a0[j]) > 1e-7)
+            ++kept;
+          else
+            a0[j] = 0;
+          if (std::fabs(a1[j]) > 1e-7)
+            ++kept;
+          else
+            a1[j] = 0;
+        }
+        if (n < cap)
+        {
+          double* r = out + static_cast<std::size_t>(n) * W;
+          r[0] = t;
+          r[1] = c.link;
+          r[2] = c.prim;
+          r[3] = c.sphere;
+          r[4] = c.substate;
+          r[5] = c.distance;
+          r[6] = c.cc_time;
+          r[7] = kept;
+          for (int j = 0; j < D; ++j)
+          {
+            r[8 + j] = a0[j];
+            r[8 + D + j] = a1[j];
+          }
+          r[8 + 2 * D] = cst;
+        }
+        ++n;
+      }
+    }
+    return n;
+  }
+  catch (const std::exception& e)
+  {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// Signed distance of one robot sphere against one primitive (test helper).
+void oracle_sphere_prim(const double* c, double r, const double* prim, double* out8)
+{
+  double n[3], pr[3], pp[3], d;
+  spherePrimDistance(c, r, prim, d, n, pr, pp);
+  out8[0] = d;
+  for (int i = 0; i < 3; ++i)
+  {
+    out8[1 + i] = n[i];
+    out8[4 + i] = pr[i];
+  }
+  out8[7] = 0;
 }
 
 int oracle_sizeof_desc() { return static_cast<int>(sizeof(thip_problem_desc)); }

@@ -1,12 +1,361 @@
 // ORACLE — test infrastructure only (see sco_expr.hpp header).
 #include "collision.hpp"
 
+#include <cmath>
+#include <map>
 #include <stdexcept>
+#include <utility>
 
 namespace orc
 {
-void addCollisionTerms(TrajProblem&, const std::vector<VarVector>&, const thip_problem_desc&, const double*)
+// ------------------------------------------------------------ signed distance
+// Closed-form distance between a robot sphere (center c, radius r) and a scene
+// primitive record (16 doubles, include/trajopt_hip.h).  normal points from
+// the robot sphere toward the primitive, so d(distance)/d(c) = -normal.
+void spherePrimDistance(const double c[3], double r, const double* prim, double& dist, double n[3],
+                        double p_robot[3], double p_prim[3])
 {
-  throw std::runtime_error("collision terms: not yet restated in the oracle");
+  const int type = static_cast<int>(prim[0]);
+  auto sphere_sphere = [&](const double s[3], double rs) {
+    double v[3] = { s[0] - c[0], s[1] - c[1], s[2] - c[2] };
+    const double L = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    if (L < 1e-12)
+    {
+      n[0] = 0;
+      n[1] = 0;
+      n[2] = 1;
+    }
+    else
+      for (int i = 0; i < 3; ++i)
+        n[i] = v[i] / L;
+    dist = L - r - rs;
+    for (int i = 0; i < 3; ++i)
+    {
+      p_robot[i] = c[i] + r * n[i];
+      p_prim[i] = s[i] - rs * n[i];
+    }
+  };
+  if (type == THIP_PRIM_SPHERE)
+  {
+    sphere_sphere(prim + 1, prim[4]);
+    return;
+  }
+  if (type == THIP_PRIM_CAPSULE)
+  {
+    const double* a = prim + 1;
+    const double* b = prim + 4;
+    const double ab[3] = { b[0] - a[0], b[1] - a[1], b[2] - a[2] };
+    const double den = ab[0] * ab[0] + ab[1] * ab[1] + ab[2] * ab[2];
+    double t = 0;
+    if (den > 1e-24)
+      t = ((c[0] - a[0]) * ab[0] + (c[1] - a[1]) * ab[1] + (c[2] - a[2]) * ab[2]) / den;
+    t = std::fmin(std::fmax(t, 0.0), 1.0);
+    const double s[3] = { a[0] + t * ab[0], a[1] + t * ab[1], a[2] + t * ab[2] };
+    sphere_sphere(s, prim[7]);
+    return;
+  }
+  if (type != THIP_PRIM_BOX)
+    throw std::runtime_error("unknown scene primitive type");
+  const double* ctr = prim + 1;
+  const double* R = prim + 4;  // row-major, columns = box axes
+  const double* h = prim + 13;
+  const double w[3] = { c[0] - ctr[0], c[1] - ctr[1], c[2] - ctr[2] };
+  double cl[3];
+  for (int i = 0; i < 3; ++i)
+    cl[i] = R[0 * 3 + i] * w[0] + R[1 * 3 + i] * w[1] + R[2 * 3 + i] * w[2];
+  const bool inside = std::fabs(cl[0]) <= h[0] && std::fabs(cl[1]) <= h[1] && std::fabs(cl[2]) <= h[2];
+  double ql[3];
+  if (!inside)
+  {
+    for (int i = 0; i < 3; ++i)
+      ql[i] = std::fmin(std::fmax(cl[i], -h[i]), h[i]);
+    const double vl[3] = { ql[0] - cl[0], ql[1] - cl[1], ql[2] - cl[2] };
+    const double L = std::sqrt(vl[0] * vl[0] + vl[1] * vl[1] + vl[2] * vl[2]);
+    for (int i = 0; i < 3; ++i)
+      n[i] = (R[i * 3 + 0] * vl[0] + R[i * 3 + 1] * vl[1] + R[i * 3 + 2] * vl[2]) / L;
+    dist = L - r;
+  }
+  else
+  {
+    int k = 0;
+    double depth = h[0] - std::fabs(cl[0]);
+    for (int i = 1; i < 3; ++i)
+    {
+      const double dd = h[i] - std::fabs(cl[i]);
+      if (dd < depth)
+      {
+        depth = dd;
+        k = i;
+      }
+    }
+    const double sgn = (cl[k] < 0) ? -1.0 : 1.0;
+    for (int i = 0; i < 3; ++i)
+      ql[i] = cl[i];
+    ql[k] = sgn * h[k];
+    // outward face normal o = sgn R e_k; the normal toward the obstacle is -o
+    for (int i = 0; i < 3; ++i)
+      n[i] = -sgn * R[i * 3 + k];
+    dist = -depth - r;
+  }
+  for (int i = 0; i < 3; ++i)
+  {
+    p_prim[i] = ctr[i] + R[i * 3 + 0] * ql[0] + R[i * 3 + 1] * ql[1] + R[i * 3 + 2] * ql[2];
+    p_robot[i] = c[i] + r * n[i];
+  }
 }
+
+namespace
+{
+// Eigen::VectorXd::LinSpaced(size, low, high)(i) for floating point
+// (Eigen 3.4 linspaced_op_impl<Scalar, false>)
+double linspaced(int size, double low, double high, int i)
+{
+  if (size == 1)
+    return high;
+  const int size1 = size - 1;
+  const double step = (high - low) / size1;
+  const bool flip = std::fabs(high) < std::fabs(low);
+  if (flip)
+    return (i == 0) ? low : high - double(size1 - i) * step;
+  return (i == size1) ? high : low + double(i) * step;
+}
+
+constexpr int kCCNone = 0, kCCTime0 = 1, kCCTime1 = 2, kCCBetween = 3;
+}  // namespace
+
+// DiscreteCollisionEvaluator::CalcCollisions (collision_terms.cpp:817-898) for
+// the step pair (q0, q1); results flattened in ContactResultMap order: link
+// pair key (robot link, primitive), then insertion (sub-state, sphere).
+std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, const double* q1, bool vars0_fixed,
+                                    bool vars1_fixed)
+{
+  const thip_chain& ch = *cm.chain;
+  const int D = ch.n_dof;
+  double dist = 0;
+  for (int j = 0; j < D; ++j)
+    dist += (q1[j] - q0[j]) * (q1[j] - q0[j]);
+  dist = std::sqrt(dist);
+  long cnt = 2;
+  if (dist > cm.lvs)
+    cnt = static_cast<long>(std::ceil(dist / cm.lvs)) + 1;
+  const long last = cnt - 1;
+  const double dt = 1.0 / double(last);
+  const double threshold = cm.margin + cm.buffer;  // incrementCollisionMargin(buffer)
+  std::map<std::pair<int, int>, std::vector<Contact>> results;
+  std::vector<double> q(static_cast<std::size_t>(D));
+  std::vector<Iso3> T;
+  for (long i = 0; i < cnt; ++i)
+  {
+    for (int j = 0; j < D; ++j)
+      q[static_cast<std::size_t>(j)] = linspaced(static_cast<int>(cnt), q0[j], q1[j], static_cast<int>(i));
+    chainFwdKin(ch, q.data(), T);
+    for (int s = 0; s < cm.n_spheres; ++s)
+    {
+      const int link = cm.sphere_link[s];
+      const Iso3& Tl = T[static_cast<std::size_t>(link)];
+      double c[3];
+      for (int r = 0; r < 3; ++r)
+        c[r] = Tl.R[r * 3 + 0] * cm.sphere_center[s][0] + Tl.R[r * 3 + 1] * cm.sphere_center[s][1] +
+               Tl.R[r * 3 + 2] * cm.sphere_center[s][2] + Tl.t[r];
+      for (int p = 0; p < cm.n_prims; ++p)
+      {
+        Contact ct;
+        spherePrimDistance(c, cm.sphere_radius[s], cm.scene + 16 * p, ct.distance, ct.normal, ct.p_robot,
+                           ct.p_prim);
+        if (!(ct.distance < threshold))  // contactTest: within the contact distance
+          continue;
+        ct.link = link;
+        ct.prim = p;
+        ct.sphere = s;
+        ct.substate = static_cast<int>(i);
+        ct.transform = Tl;
+        // nearest_points_local[0]: the robot point in the link frame
+        const double w[3] = { ct.p_robot[0] - Tl.t[0], ct.p_robot[1] - Tl.t[1], ct.p_robot[2] - Tl.t[2] };
+        for (int r = 0; r < 3; ++r)
+          ct.p_local[r] = Tl.R[0 * 3 + r] * w[0] + Tl.R[1 * 3 + r] * w[1] + Tl.R[2 * 3 + r] * w[2];
+        // addInterpolatedCollisionResults(.., discrete = true): active link only
+        ct.cc_time = double(i) * dt;
+        ct.cc_type = (i == 0) ? kCCTime0 : ((i == last) ? kCCTime1 : kCCBetween);
+        // filter: zero coeffs (none), removeInvalidContactResults
+        // (collision_utils.cpp:73-114); the static primitive has CCType_None
+        if (ct.distance > cm.margin + cm.buffer)
+          continue;
+        if (vars0_fixed || vars1_fixed)
+        {
+          const bool keep = (vars0_fixed && ct.cc_type != kCCNone && ct.cc_type != kCCTime0) ||
+                            (vars1_fixed && ct.cc_type != kCCNone && ct.cc_type != kCCTime1);
+          if (!keep)
+            continue;
+        }
+        results[{ link, p }].push_back(ct);
+      }
+    }
+  }
+  std::vector<Contact> flat;
+  for (auto& kv : results)
+    flat.insert(flat.end(), kv.second.begin(), kv.second.end());
+  return flat;
+}
+
+// CollisionEvaluator::GetGradient (collision_terms.cpp:195-242) for the robot
+// link (link_ids[0]): jacobian at the step's own joint values, reference point
+// moved to transform.linear() * nearest_points_local (the sub-state pose; for
+// discrete-continuous results cc_transform == transform), gradient
+// -normal^T J_lin, scale 1 - cc_time (timestep 0) or cc_time (timestep 1).
+void contactGradient(const CollisionModel& cm, const double* dofvals, const Contact& ct, bool timestep1,
+                     double* grad, double& scale)
+{
+  const thip_chain& ch = *cm.chain;
+  const int D = ch.n_dof;
+  double J[6 * THIP_MAX_DOF];
+  chainJacobian(ch, dofvals, ct.link, J);
+  double r[3];
+  for (int i = 0; i < 3; ++i)
+    r[i] = ct.transform.R[i * 3 + 0] * ct.p_local[0] + ct.transform.R[i * 3 + 1] * ct.p_local[1] +
+           ct.transform.R[i * 3 + 2] * ct.p_local[2];
+  scale = timestep1 ? ct.cc_time : (1 - ct.cc_time);
+  for (int j = 0; j < D; ++j)
+  {
+    // jacobianChangeRefPoint: J_lin += J_ang x r
+    const double wx = J[3 * D + j], wy = J[4 * D + j], wz = J[5 * D + j];
+    const double l0 = J[0 * D + j] + (wy * r[2] - wz * r[1]);
+    const double l1 = J[1 * D + j] + (wz * r[0] - wx * r[2]);
+    const double l2 = J[2 * D + j] + (wx * r[1] - wy * r[0]);
+    grad[j] = -1.0 * (ct.normal[0] * l0 + ct.normal[1] * l1 + ct.normal[2] * l2);
+  }
+}
+
+namespace
+{
+// One CollisionCost term per step pair (CollisionTermInfo::hatch,
+// problem_description.cpp:1735-1781), LVS_DISCRETE expression evaluator.
+class CollisionPairCost : public Cost
+{
+public:
+  CollisionPairCost(std::shared_ptr<const CollisionModel> cm, VarVector v0, VarVector v1, int type)
+    : cm_(std::move(cm)), vars0_(std::move(v0)), vars1_(std::move(v1)), type_(type)
+  {
+  }
+
+  VarVector getVars() override
+  {
+    VarVector v = vars0_;
+    v.insert(v.end(), vars1_.begin(), vars1_.end());
+    return v;
+  }
+
+  // CollisionCost::value (collision_terms.cpp:1287-1306): no buffer
+  double value(const DblVec& x) override
+  {
+    const auto contacts = collide(x);
+    double out = 0;
+    for (const auto& c : contacts)
+      out += std::fmax(cm_->margin - c.distance, 0.0) * cm_->coeff;
+    return out;
+  }
+
+  // CollisionCost::convex (collision_terms.cpp:1267-1284)
+  ConvexObjective::Ptr convex(const DblVec& x, Model* model) override
+  {
+    auto out = std::make_shared<ConvexObjective>(model);
+    const auto contacts = collide(x);
+    const DblVec q0 = getDblVec(x, vars0_), q1 = getDblVec(x, vars1_);
+    const int D = cm_->chain->n_dof;
+    for (const auto& c : contacts)
+    {
+      AffExpr e(c.distance);
+      auto add_part = [&](const VarVector& vars, const DblVec& dof, bool ts1) {
+        double g[THIP_MAX_DOF], scale;
+        contactGradient(*cm_, dof.data(), c, ts1, g, scale);
+        // CollisionsToDistanceExpressions: varDot(scale * g, vars) + scale * -g.dot(dofvals)
+        AffExpr part;
+        double gd = 0;
+        for (int j = 0; j < D; ++j)
+        {
+          part.coeffs.push_back(scale * g[j]);
+          part.vars.push_back(vars[static_cast<std::size_t>(j)]);
+          gd += g[j] * dof[static_cast<std::size_t>(j)];
+        }
+        part.constant = scale * -gd;
+        exprInc(e, part);
+      };
+      if (type_ == kBothFree)
+      {
+        add_part(vars0_, q0, false);
+        add_part(vars1_, q1, true);
+      }
+      else if (type_ == kStartFixedEndFree)
+        add_part(vars1_, q1, true);
+      else
+        add_part(vars0_, q0, false);
+      e = cleanupAff(e);
+      out->addHinge(exprSub(AffExpr(cm_->margin), e), cm_->coeff);
+    }
+    return out;
+  }
+
+  static constexpr int kBothFree = 0, kStartFixedEndFree = 1, kStartFreeEndFixed = 2;
+
+private:
+  std::vector<Contact> collide(const DblVec& x) const
+  {
+    const DblVec q0 = getDblVec(x, vars0_), q1 = getDblVec(x, vars1_);
+    return calcCollisions(*cm_, q0.data(), q1.data(), type_ == kStartFixedEndFree, type_ == kStartFreeEndFixed);
+  }
+
+  std::shared_ptr<const CollisionModel> cm_;
+  VarVector vars0_, vars1_;
+  int type_;
+};
+}  // namespace
+
+void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, const thip_problem_desc& d,
+                       const double* scene)
+{
+  if (d.coll_is_cnt)
+    throw std::runtime_error("collision constraints: not restated (config C uses the LVS-discrete cost)");
+  auto cm = std::make_shared<CollisionModel>();
+  cm->chain = &d.chain;
+  cm->n_spheres = d.n_spheres;
+  for (int s = 0; s < d.n_spheres; ++s)
+  {
+    cm->sphere_link[s] = d.sphere_link[s];
+    cm->sphere_radius[s] = d.sphere_radius[s];
+    for (int i = 0; i < 3; ++i)
+      cm->sphere_center[s][i] = d.sphere_center[s][i];
+  }
+  cm->n_prims = d.n_prims;
+  cm->scene_store.assign(scene, scene + 16 * d.n_prims);
+  cm->scene = cm->scene_store.data();
+  cm->margin = d.coll_margin;
+  cm->coeff = d.coll_coeff;
+  cm->buffer = d.coll_buffer;
+  cm->lvs = d.coll_lvs;
+  const int first = d.coll_first_step;
+  const int last = (d.coll_last_step < 0) ? d.n_steps - 1 : d.coll_last_step;
+  auto fixed = [&](int t) {
+    for (int k = 0; k < d.coll_n_fixed; ++k)
+      if (d.coll_fixed_steps[k] == t)
+        return true;
+    return false;
+  };
+  for (int i = first; i < last; ++i)
+  {
+    const bool cf = fixed(i), nf = fixed(i + 1);
+    int type;
+    if (!cf && !nf)
+      type = CollisionPairCost::kBothFree;
+    else if (cf && nf)
+      throw std::runtime_error("Currently two adjacent fixed steps are not supported in collision term.");
+    else if (cf)
+      type = CollisionPairCost::kStartFixedEndFree;
+    else
+      type = CollisionPairCost::kStartFreeEndFixed;
+    auto c = std::make_shared<CollisionPairCost>(cm, rows[static_cast<std::size_t>(i)],
+                                                 rows[static_cast<std::size_t>(i + 1)], type);
+    c->setName("collision_" + std::to_string(i));
+    tp.prob->addCost(c);
+  }
+}
+
 }  // namespace orc

@@ -6,9 +6,15 @@
 //   CollisionsToDistanceExpressions             trajopt/src/collision_terms.cpp:341-386
 //   CalcDistExpressions{BothFree,..}            trajopt/src/collision_terms.cpp:463-536
 //   CollisionCost::convex / value               trajopt/src/collision_terms.cpp:1267-1306
+//   CollisionTermInfo::hatch (cost branch)      trajopt/src/problem_description.cpp:1735-1781
 //   removeInvalidContactResults                 trajopt_common/src/collision_utils.cpp:73-114
-// Bullet's contactTest is replaced by closed-form sphere-vs-primitive signed
-// distance shared with the GPU path ("parity unpinned" against Bullet).
+// tesseract's ContactResultMap::addInterpolatedCollisionResults [ext] is
+// restated as SURVEY.md §8c.1 item 7 (cc_time = i dt, Time0 / Between /
+// Time1, cc_transform = transform for discrete results).  Bullet's
+// contactTest is replaced by closed-form sphere-vs-primitive signed distance
+// shared with the GPU path: contact values are "parity unpinned" against
+// Bullet; the map order is (robot link, primitive) rather than tesseract's
+// link-id hash order.
 #pragma once
 #include <vector>
 
@@ -16,6 +22,41 @@
 
 namespace orc
 {
+struct CollisionModel
+{
+  const thip_chain* chain = nullptr;
+  int n_spheres = 0;
+  int sphere_link[THIP_MAX_SPHERES];
+  double sphere_center[THIP_MAX_SPHERES][3];
+  double sphere_radius[THIP_MAX_SPHERES];
+  int n_prims = 0;
+  std::vector<double> scene_store;
+  const double* scene = nullptr;  // [n_prims][16]
+  double margin = 0, coeff = 0, buffer = 0, lvs = 0;
+};
+
+// A contact between a robot link sphere (link_ids[0], active) and a scene
+// primitive (link_ids[1], static).
+struct Contact
+{
+  int link = 0, prim = 0, sphere = 0, substate = 0;
+  double distance = 0;
+  double normal[3];    // from the robot sphere toward the primitive
+  double p_robot[3];   // nearest points, world
+  double p_prim[3];
+  double p_local[3];   // nearest_points_local[0] (robot link frame at the sub-state)
+  Iso3 transform;      // robot link pose at the sub-state (= cc_transform)
+  double cc_time = 0;  // interpolation time of the sub-state
+  int cc_type = 0;     // 1 Time0, 2 Time1, 3 Between
+};
+
+void spherePrimDistance(const double c[3], double r, const double* prim, double& dist, double n[3],
+                        double p_robot[3], double p_prim[3]);
+std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, const double* q1, bool vars0_fixed,
+                                    bool vars1_fixed);
+void contactGradient(const CollisionModel& cm, const double* dofvals, const Contact& ct, bool timestep1,
+                     double* grad, double& scale);
+
 void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, const thip_problem_desc& d,
                        const double* scene);
-}
+}  // namespace orc

@@ -197,4 +197,38 @@ void chainFwdKin(const thip_chain& chain, const double* q, std::vector<Iso3>& ou
   }
 }
 
+void chainJacobian(const thip_chain& chain, const double* q, int link, double* J)
+{
+  std::vector<Iso3> T;
+  chainFwdKin(chain, q, T);
+  const int D = chain.n_dof;
+  for (int e = 0; e < 6 * D; ++e)
+    J[e] = 0.0;
+  const double* p = T[static_cast<std::size_t>(link)].t;
+  for (int k = 1; k <= link; ++k)
+  {
+    const int type = chain.joint_type[k];
+    if (type == THIP_JOINT_FIXED)
+      continue;
+    const Iso3& Tk = T[static_cast<std::size_t>(k)];
+    const double* ax = chain.joint_axis[k];
+    double a[3];
+    for (int r = 0; r < 3; ++r)
+      a[r] = Tk.R[r * 3 + 0] * ax[0] + Tk.R[r * 3 + 1] * ax[1] + Tk.R[r * 3 + 2] * ax[2];
+    const int j = chain.joint_dof[k];
+    if (type == THIP_JOINT_PRISMATIC)
+    {
+      for (int r = 0; r < 3; ++r)
+        J[r * D + j] = a[r];
+      continue;
+    }
+    const double d[3] = { p[0] - Tk.t[0], p[1] - Tk.t[1], p[2] - Tk.t[2] };
+    J[0 * D + j] = a[1] * d[2] - a[2] * d[1];
+    J[1 * D + j] = a[2] * d[0] - a[0] * d[2];
+    J[2 * D + j] = a[0] * d[1] - a[1] * d[0];
+    for (int r = 0; r < 3; ++r)
+      J[(3 + r) * D + j] = a[r];
+  }
+}
+
 }  // namespace orc

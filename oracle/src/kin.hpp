@@ -67,4 +67,9 @@ void applyTolerances(double err[6], const double* lower, const double* upper, in
 // link poses of the chain at q: out[n_links]
 void chainFwdKin(const thip_chain& chain, const double* q, std::vector<Iso3>& out);
 
+// Geometric jacobian (world frame, reference point = origin of `link`) at q:
+// J[6][n_dof] row-major, rows 0-2 linear, 3-5 angular; revolute column
+// [a x (p - o); a], prismatic [a; 0] (tesseract JointGroup::calcJacobian [ext])
+void chainJacobian(const thip_chain& chain, const double* q, int link, double* J);
+
 }  // namespace orc

@@ -19,6 +19,10 @@ Contents (all fp64):
                     config A problems 0..7
   sqp_B.npz         the same for config B problems 0..1
   sqp_jv.npz        JointVel-only (no CartPose) variant, 12 steps, 4 problems
+  sqp_C.npz         config C (B + LVS-discrete collision cost, 10-primitive
+                    scene) problems 0..2
+  collision_rows_C.npz  linearised collision rows of those problems at their
+                    converged trajectories (oracle_collision_rows)
 """
 from __future__ import annotations
 
@@ -69,9 +73,13 @@ def main():
         np.savez(HERE / f"cartpose_{cfg}.npz", x=wl.init, targets=wl.targets, err=err, jac=jac)
 
     for name, wl in (("sqp_A", problems.make_workload("A", 8)), ("sqp_B", problems.make_workload("B", 2)),
-                     ("sqp_jv", jointvel_only(4))):
+                     ("sqp_jv", jointvel_only(4)), ("sqp_C", problems.make_workload("C", 3))):
         x, res = oracle.solve(wl, n_threads=8)
-        np.savez(HERE / f"{name}.npz", init=wl.init, targets=wl.targets, x=x, **result_arrays(res))
+        np.savez(HERE / f"{name}.npz", init=wl.init, targets=wl.targets, scene=wl.scene, x=x, **result_arrays(res))
+    wl = problems.make_workload("C", 3)
+    x, _ = oracle.solve(wl, n_threads=3)
+    np.savez(HERE / "collision_rows_C.npz", x=x,
+             **{f"rows{b}": oracle.collision_rows(wl, b, x[b]) for b in range(3)})
     print("golden fixtures written to", HERE)
 
 

@@ -1,0 +1,180 @@
+"""Config C collision model and synthetic scenes.
+
+Robot collision model: 2 spheres on each of the 7 moving links of the PR2
+right arm (radii 0.06-0.09 m), a committed fixture (PR2_ARM_SPHERES).  Scene:
+10 primitives per problem, 4 spheres (r ~ U(0.05, 0.12)), 3 boxes (half
+extents ~ U(0.04, 0.1), random orientation) and 3 capsules (r ~ U(0.03,
+0.06), half length ~ U(0.05, 0.15)), each placed next to a robot sphere of
+q_ref(t) for a random waypoint t, in a random direction, with a clearance of
+U(0.08, 0.2) m between the robot sphere and the primitive's bounding sphere
+(SURVEY.md's "offset by U(0.08, 0.2) m" read as surface clearance).  A
+placement is redrawn (at most 64 times, same splitmix64 stream) until every
+robot sphere at every waypoint of q_ref is farther than the contact distance
+(dist_pen + buffer = 0.075 m) from it: the reference path is collision free,
+contacts come from the interpolated initial trajectory deviating toward the
+obstacles, and only part of the problems start in collision.  The collision term is the reference's LVS_DISCRETE cost with
+dist_pen 0.025, coeffs 20, safety_margin_buffer 0.05, lvs 0.05 and
+fixed_steps [0] (CollisionTermInfo, problem_description.cpp:1636-1733).
+Primitive record layout: include/trajopt_hip.h (THIP_PRIM_*).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import abi
+from .robots import fwd_kin
+
+# (link index, center in the link frame, radius); link indices of
+# robots.pr2_right_arm(): 1 shoulder_pan, 2 shoulder_lift, 3 upper_arm_roll,
+# 5 elbow_flex, 6 forearm_roll, 8 wrist_flex, 9 wrist_roll
+PR2_ARM_SPHERES = [
+    (1, (0.0, 0.0, 0.0), 0.09),
+    (1, (0.1, 0.0, 0.0), 0.08),
+    (2, (0.0, 0.0, 0.0), 0.08),
+    (2, (0.1, 0.0, 0.0), 0.07),
+    (3, (0.15, 0.0, 0.0), 0.07),
+    (3, (0.3, 0.0, 0.0), 0.07),
+    (5, (0.0, 0.0, 0.0), 0.07),
+    (5, (0.08, 0.0, 0.0), 0.06),
+    (6, (0.12, 0.0, 0.0), 0.06),
+    (6, (0.24, 0.0, 0.0), 0.06),
+    (8, (0.0, 0.0, 0.0), 0.06),
+    (8, (0.08, 0.0, 0.0), 0.06),
+    (9, (0.12, 0.0, 0.0), 0.06),
+    (9, (0.18, 0.0, 0.0), 0.06),
+]
+
+N_PRIMS = 10
+MARGIN, COEFF, BUFFER, LVS = 0.025, 20.0, 0.05, 0.05
+
+
+def add_collision_model(d: abi.ProblemDesc):
+    """LVS_DISCRETE collision cost over all step pairs, step 0 fixed."""
+    d.coll_enabled = 1
+    d.coll_is_cnt = 0
+    d.coll_first_step = 0
+    d.coll_last_step = d.n_steps - 1
+    d.coll_n_fixed = 1
+    d.coll_fixed_steps[0] = 0
+    d.coll_margin = MARGIN
+    d.coll_coeff = COEFF
+    d.coll_buffer = BUFFER
+    d.coll_lvs = LVS
+    d.n_spheres = len(PR2_ARM_SPHERES)
+    for s, (link, c, r) in enumerate(PR2_ARM_SPHERES):
+        d.sphere_link[s] = link
+        for i in range(3):
+            d.sphere_center[s][i] = c[i]
+        d.sphere_radius[s] = r
+    d.n_prims = N_PRIMS
+
+
+def _unit(rng):
+    v = np.array([rng.normal(), rng.normal(), rng.normal()])
+    n = np.linalg.norm(v)
+    return v / n if n > 1e-12 else np.array([0.0, 0.0, 1.0])
+
+
+def _rotation(rng):
+    q = np.array([rng.normal(), rng.normal(), rng.normal(), rng.normal()])
+    q = q / max(np.linalg.norm(q), 1e-12)
+    w, x, y, z = q
+    return np.array([
+        [1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+        [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+        [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)],
+    ])
+
+
+def sphere_centers(chain, q):
+    """World centers of the robot spheres at joint values q."""
+    T = fwd_kin(chain, q)
+    return np.array([T[link][:3, :3] @ np.array(c) + T[link][:3, 3] for link, c, _ in PR2_ARM_SPHERES])
+
+
+def make_scene(rng, chain, q_ref, d) -> np.ndarray:
+    """10 primitive records near the reference path of one problem."""
+    N = q_ref.shape[0]
+    prims = np.zeros((N_PRIMS, 16))
+    path = [sphere_centers(chain, q_ref[t]) for t in range(N)]
+    radii = [r for _, _, r in PR2_ARM_SPHERES]
+    for k in range(N_PRIMS):
+        for _attempt in range(64):
+            rec = _draw_prim(rng, k, N, path)
+            if all(sphere_prim_distance(c[s], radii[s], rec)[0] > MARGIN + BUFFER
+                   for c in path for s in range(len(radii))):
+                break
+        prims[k] = rec
+    return prims
+
+
+def _draw_prim(rng, k, N, path):
+    rec = np.zeros(16)
+    if True:  # one placement draw
+        t = min(int(rng.uniform() * N), N - 1)
+        s = min(int(rng.uniform() * len(PR2_ARM_SPHERES)), len(PR2_ARM_SPHERES) - 1)
+        anchor = path[t][s]
+        direction = _unit(rng)
+        if k < 4:
+            radius = rng.uniform(0.05, 0.12)
+            bound = radius
+        elif k < 7:
+            R = _rotation(rng)
+            h = np.array([rng.uniform(0.04, 0.1) for _ in range(3)])
+            bound = float(np.linalg.norm(h))
+        else:
+            axis = _unit(rng)
+            half = rng.uniform(0.05, 0.15)
+            cap_r = rng.uniform(0.03, 0.06)
+            bound = half + cap_r
+        center = anchor + direction * (PR2_ARM_SPHERES[s][2] + bound + rng.uniform(0.08, 0.2))
+        if k < 4:
+            rec[0] = abi.PRIM_SPHERE
+            rec[1:4] = center
+            rec[4] = radius
+        elif k < 7:
+            rec[0] = abi.PRIM_BOX
+            rec[1:4] = center
+            rec[4:13] = R.reshape(9)
+            rec[13:16] = h
+        else:
+            rec[0] = abi.PRIM_CAPSULE
+            rec[1:4] = center - half * axis
+            rec[4:7] = center + half * axis
+            rec[7] = cap_r
+    return rec
+
+
+def sphere_prim_distance(c, r, prim):
+    """numpy restatement of the closed-form signed distance (test helper)."""
+    c = np.asarray(c, dtype=float)
+    typ = int(prim[0])
+
+    def sph(s, rs):
+        v = s - c
+        L = math.sqrt(float(v @ v))
+        n = v / L if L >= 1e-12 else np.array([0.0, 0.0, 1.0])
+        return L - r - rs, n
+
+    if typ == abi.PRIM_SPHERE:
+        return sph(prim[1:4], prim[4])
+    if typ == abi.PRIM_CAPSULE:
+        a, b = prim[1:4], prim[4:7]
+        ab = b - a
+        den = float(ab @ ab)
+        t = float((c - a) @ ab) / den if den > 1e-24 else 0.0
+        t = min(max(t, 0.0), 1.0)
+        return sph(a + t * ab, prim[7])
+    ctr, R, h = prim[1:4], prim[4:13].reshape(3, 3), prim[13:16]
+    cl = R.T @ (c - ctr)
+    if np.any(np.abs(cl) > h):
+        ql = np.clip(cl, -h, h)
+        vl = ql - cl
+        L = float(np.linalg.norm(vl))
+        return L - r, R @ vl / L
+    depth = h - np.abs(cl)
+    k = int(np.argmin(depth))
+    sgn = -1.0 if cl[k] < 0 else 1.0
+    return -depth[k] - r, -sgn * R[:, k]
