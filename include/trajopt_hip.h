@@ -212,7 +212,12 @@ typedef struct thip_result {
   double final_trust_box;
   int n_costs;
   int n_cnts;
+  int flags;          /* THIP_FLAG_* */
 } thip_result;
+
+/* thip_result.flags */
+#define THIP_FLAG_CONTACT_OVERFLOW 1 /* contacts exceeded the hinge-row capacity (or > 64 LVS
+                                        sub-states in a step pair): the run is OPT_FAILED */
 
 typedef struct thip_ctx thip_ctx;
 
@@ -271,6 +276,7 @@ const char* thip_build_info(void);
 
 /* sizeof(thip_problem_desc) as compiled into the library (ABI check). */
 int thip_sizeof_desc(void);
+int thip_sizeof_result(void);
 
 /* Diagnostics: record one 10-double entry per QP solve of every problem
  * (warm_started, rho_initial, admm_iters, osqp_status, polish_status,
@@ -279,6 +285,14 @@ int thip_sizeof_desc(void);
 int thip_debug_trace(thip_ctx* ctx, int capacity);
 /* records [batch][capacity][10], counts [batch] */
 int thip_debug_get_trace(thip_ctx* ctx, double* records, int* counts);
+
+/* Linearised collision rows (config C) of every problem at trajectories x
+ * [batch][N][D]: the distance expressions of CollisionCost::convex
+ * (trajopt/src/collision_terms.cpp:463-536, 1267-1284), one record per
+ * contact in hinge-row order, [t, link, prim, sphere, substate, distance,
+ * cc_time, n_kept, a_t[D], a_t+1[D], constant] (8 + 2 D + 1 doubles);
+ * records [batch][cap][...], counts[batch] (-1 on contact overflow). */
+int thip_collision_rows(thip_ctx* ctx, const double* x, double* records, int cap, int* counts);
 
 /* Diagnostics: per-problem phase cycle counters (24 slots per problem; see
  * the slot list in sqp_kernel.hip).  enable = 0 frees them.  Counters

@@ -54,6 +54,8 @@ def lib():
         L.oracle_last_error.restype = C.c_char_p
         L.oracle_sizeof_desc.restype = C.c_int
         assert L.oracle_sizeof_desc() == C.sizeof(abi.ProblemDesc), "descriptor layout mismatch"
+        L.oracle_sizeof_result.restype = C.c_int
+        assert L.oracle_sizeof_result() == C.sizeof(abi.Result), "result layout mismatch (rebuild the oracle)"
         _lib = L
     return _lib
 

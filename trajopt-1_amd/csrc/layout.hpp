@@ -19,6 +19,10 @@ constexpr int kWaves = kBlock / 64;
 constexpr long long kLdsBudgetBytes = 152 * 1024;
 // CartPose rows per waypoint the register-resident ADMM segment supports
 constexpr int kMaxStepRows = 8;
+// LVS sub-states per step pair the contact scan supports (one per lane)
+constexpr int kSubCap = 64;
+// hinge rows (contacts) per problem and SQP iteration
+constexpr int kHingeCap = 2048;
 
 // per-problem double workspace arrays
 enum DArr : int
@@ -75,6 +79,16 @@ enum DArr : int
   A_PR,      // polish residual (n_cols + m)
   A_PZ,      // polish z (m)
   A_BXW,     // column rhs work (n_cols)
+  // collision (LVS-discrete cost, config C); sized 1 when disabled
+  A_HC0,     // hinge rows: distance-expression coefficients [h_cap][2D] (x_t, x_t+1), unscaled
+  A_HK,      // distance-expression constant (h_cap)
+  A_HC,      // scaled row coefficients [h_cap][2D]
+  A_HW,      // scaled hinge-variable coefficient (h_cap)
+  A_HRE,     // effective rho of hinge rows after eliminating the hinge variable (h_cap)
+  A_CPL,     // coupling blocks K_{t+1,t} (N*D*D)
+  A_CSCR,    // contact-scan scratch: sphere centers [kWaves][kSubCap][n_spheres][3]
+  A_HCOST,   // per step-pair collision cost scratch (N)
+  A_HDIST,   // contact distance of each hinge row (h_cap)
   A_COUNT
 };
 
@@ -84,6 +98,13 @@ enum IArr : int
   I_PMASK,     // mask of the previous QP setup (n_abs)
   I_TYPE,      // constraint type per row: -1 loose, 0 ineq, 1 eq (m)
   I_ACT,       // polish active flags (m)
+  I_HT,        // hinge row start waypoint (h_cap)
+  I_HMASK,     // kept-coefficient mask of hinge rows (h_cap), current QP
+  I_PHMASK,    // ... of the previous QP setup (h_cap)
+  I_PHT,       // start waypoints of the previous QP setup (h_cap)
+  I_HPTR,      // CSR: hinge rows starting at waypoint t (N+1)
+  I_CONT,      // contact list [h_cap][3]: sub-state, sphere, primitive
+  I_PCNT,      // contacts per step pair (N)
   I_COUNT
 };
 
@@ -95,9 +116,17 @@ struct Layout
   int n_cart;
   int n_abs;      // CartPose rows (cost rows first, then constraint rows)
   int n_abs_cost; // rows belonging to cost terms
-  int n_cols;     // nx + 2*n_abs
+  int n_cols;     // column capacity: nc_base + h_cap
   int n_rows;     // n_fixed_rows + n_abs
-  int m;          // n_rows + n_cols
+  int m;          // row capacity: m_base + 2*h_cap
+  // base sizes without collision rows; hinge row h is row m_base + 2h, the
+  // bound row of its hinge variable (column nc_base + h) is m_base + 2h + 1
+  int nc_base;    // nx + 2*n_abs
+  int m_base;     // n_rows + nc_base
+  int h_cap;      // hinge-row capacity (0 without collision)
+  int coll;       // collision cost enabled
+  int coll_first, coll_last;  // step pairs [coll_first, coll_last)
+  int coll_cost0; // cost slot of the first step pair
   int n_costs;    // JointVel (0/1) + CartPose cost terms
   int n_cnts;     // CartPose constraint terms
   int jv_first, jv_last;
@@ -133,6 +162,14 @@ struct Tables
   int* term_nrow;  // rows of each term (n_cart)
   int* term_slot;  // cost index or constraint index of each term (n_cart)
   int* fixed_of_step;  // fixed-step slot of each waypoint or -1 (N)
+  // collision model: robot spheres grouped by link in ascending link order
+  // (the ContactResultMap key order of the contact scan)
+  int n_groups;
+  int* grp_link;   // link of group g
+  int* grp_s0;     // first entry of the group in sph_order
+  int* grp_ns;     // spheres in the group
+  int* sph_order;  // sphere indices sorted by (link, index)
+  int* coll_fixed; // per waypoint: 1 if a collision fixed step (N)
 };
 
 struct KernelArgs
@@ -140,6 +177,7 @@ struct KernelArgs
   Layout L;
   Tables T;
   const thip_problem_desc* desc;  // device copy
+  const double* scene;  // [batch][n_prims][16] (null without collision)
   double* ws;
   int* iws;
   thip_result* res;

@@ -17,6 +17,7 @@
 
 #include <cfloat>
 
+#include "collision_device.hpp"
 #include "kin_device.hpp"
 #include "layout.hpp"
 
@@ -67,6 +68,11 @@ struct Ctl
   int trace_cap, trace_n;
   double rho0;
   long long* prof;  // phase cycle counters of this problem (null = off)
+  // collision rows of the current QP
+  int n_h;
+  int n_h_prev;
+  int coll_overflow;  // set by the last contact scan
+  int flags;          // sticky THIP_FLAG_* of the run
 };
 
 struct Ctx
@@ -79,6 +85,7 @@ struct Ctx
   double* big;
   Ctl* s;
   double* const* ptab;  // LDS table of array base pointers (LDS-resident or HBM), or null
+  const double* scene = nullptr;  // this problem's primitives [n_prims][16]
   int tid, lane, wave;
   __device__ Ctx(const Layout& l, const Tables& t, const thip_problem_desc* dd, double* ww, int* ii, double* bb,
                  Ctl* ss, double* const* pt = nullptr)
@@ -89,6 +96,9 @@ struct Ctx
     wave = tid >> 6;
   }
   __device__ __forceinline__ double* a(int k) const { return ptab ? ptab[k] : w + L.doff[k]; }
+  // dynamic QP sizes (base sizes plus the current hinge rows)
+  __device__ __forceinline__ int m() const { return L.m_base + 2 * s->n_h; }
+  __device__ __forceinline__ int nc() const { return L.nc_base + s->n_h; }
   __device__ __forceinline__ int* ia(int k) const { return iw + L.ioff[k]; }
 };
 
@@ -184,6 +194,8 @@ __device__ __forceinline__ double limit_scaling(double a)
 //   A_G [n_abs][D]: weight * cleanupAff(J row), A_GC: weight * (y - J.x),
 //   I_MASK: kept-entry bit mask (|J| > 1e-7)
 // ======================================================================
+__device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows);
+
 __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
 {
   PROF(5);
@@ -291,6 +303,270 @@ __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
     GC[row] = (y - dot) * wgt;
   }
   BSYNC();
+  if (L.coll && !raw_jac)
+    coll_scan(c, x, nullptr, true);
+}
+
+// ======================================================================
+// LVS-discrete collision term (config C): contact scan, pair costs, hinge
+// rows.  DiscreteCollisionEvaluator::CalcCollisions
+// (trajopt/src/collision_terms.cpp:817-898), GetGradient (:195-242),
+// CalcDistExpressions* (:463-536), CollisionCost::value (:1287-1306);
+// the same arithmetic as oracle/src/collision.cpp.
+//
+// Each wave takes step pairs t = first + wave, + kWaves, ...; per pair the
+// lanes compute the sphere centers of the LVS sub-states (one sub-state per
+// lane, scratch in A_CSCR), then scan the candidates (robot sphere s of link
+// group g, primitive p, sub-state i) in the flattened ContactResultMap order
+// (link, primitive, then insertion order sub-state, sphere) 64 at a time; a
+// ballot gives each contact its rank.  Pass 0 counts contacts and sums the
+// pair's cost; pass 1 (rows only) writes the ordered contact list.
+// ======================================================================
+__device__ __forceinline__ bool coll_fixed_step(const Ctx& c, int t) { return c.T.coll_fixed[t] != 0; }
+
+template <int PASS>
+__device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
+{
+  const Layout& L = c.L;
+  const int D = L.D, ns = c.d->n_spheres, P = c.d->n_prims;
+  const thip_chain& ch = c.d->chain;
+  const double margin = c.d->coll_margin, buffer = c.d->coll_buffer, coeff = c.d->coll_coeff;
+  const double threshold = margin + buffer;  // contact distance after incrementCollisionMargin(buffer)
+  double* SCR = c.a(A_CSCR) + (long long)c.wave * kSubCap * ns * 3;
+  int* PCNT = c.ia(I_PCNT);
+  double* HCOST = c.a(A_HCOST);
+  int* CONT = c.ia(I_CONT);
+  int* HT = c.ia(I_HT);
+  for (int t = L.coll_first + c.wave; t < L.coll_last; t += kWaves)
+  {
+    const double* q0 = x + t * D;
+    const double* q1 = x + (t + 1) * D;
+    const int cnt = lvs_count(q0, q1, D, c.d->coll_lvs);
+    if (cnt > kSubCap)
+    {
+      if (c.lane == 0)
+      {
+        c.s->coll_overflow = 1;
+        if (PASS == 0)
+        {
+          PCNT[t] = 0;
+          HCOST[t] = 0.0;
+        }
+      }
+      continue;
+    }
+    const bool f0 = coll_fixed_step(c, t), f1 = coll_fixed_step(c, t + 1);
+    if (c.lane < cnt)
+    {
+      double q[THIP_MAX_DOF];
+      for (int j = 0; j < D; ++j)
+        q[j] = linspaced(cnt, q0[j], q1[j], c.lane);
+      for (int g = 0; g < c.T.n_groups; ++g)
+      {
+        Pose T;
+        chain_fk(ch, q, c.T.grp_link[g], T);
+        for (int e = 0; e < c.T.grp_ns[g]; ++e)
+        {
+          const int s = c.T.sph_order[c.T.grp_s0[g] + e];
+          const double* cs = c.d->sphere_center[s];
+          double* dst = SCR + (c.lane * ns + s) * 3;
+          for (int r = 0; r < 3; ++r)
+            dst[r] = T.r[r * 3 + 0] * cs[0] + T.r[r * 3 + 1] * cs[1] + T.r[r * 3 + 2] * cs[2] + T.t[r];
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    int total = 0;
+    for (int g = 0; g < c.T.n_groups; ++g)
+      total += P * cnt * c.T.grp_ns[g];
+    int running = 0;
+    double cost = 0.0;
+    const int base = (PASS == 1) ? out_base[t] : 0;
+    for (int c0 = 0; c0 < total; c0 += 64)
+    {
+      const int cand = c0 + c.lane;
+      bool hit = false;
+      double dist = 0.0;
+      int i = 0, s = 0, p = 0;
+      if (cand < total)
+      {
+        int rem = cand, g = 0;
+        while (rem >= P * cnt * c.T.grp_ns[g])
+        {
+          rem -= P * cnt * c.T.grp_ns[g];
+          ++g;
+        }
+        const int gn = c.T.grp_ns[g];
+        p = rem / (cnt * gn);
+        const int r2 = rem % (cnt * gn);
+        i = r2 / gn;
+        s = c.T.sph_order[c.T.grp_s0[g] + r2 % gn];
+        double n[3], pr[3];
+        sphere_prim_distance(SCR + (i * ns + s) * 3, c.d->sphere_radius[s], c.scene + 16 * p, dist, n, pr);
+        hit = dist < threshold && !(dist > margin + buffer);
+        // removeInvalidContactResults (collision_utils.cpp:73-114): at a
+        // fixed end keep only contacts not at that end (cc_type of the
+        // robot link: Time0 at i = 0, Time1 at i = cnt - 1, else Between)
+        if (hit && (f0 || f1))
+          hit = (f0 && i != 0) || (f1 && i != cnt - 1);
+      }
+      const unsigned long long mask = __ballot(hit);
+      if (PASS == 0)
+      {
+        double term = hit ? fmax(margin - dist, 0.0) * coeff : 0.0;
+        cost += wave_sum(term);
+      }
+      else if (hit)
+      {
+        const int rank = __popcll(mask & ((1ull << c.lane) - 1ull));
+        const int k = base + running + rank;
+        if (k < L.h_cap)
+        {
+          CONT[3 * k + 0] = i;
+          CONT[3 * k + 1] = s;
+          CONT[3 * k + 2] = p;
+          HT[k] = t;
+        }
+      }
+      running += __popcll(mask);
+    }
+    if (PASS == 0 && c.lane == 0)
+    {
+      PCNT[t] = running;
+      HCOST[t] = cost;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Collision costs at x (Cost::value of each step-pair term); with rows, also
+// the linearised hinge rows of the QP (CollisionCost::convex) at x.
+__device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
+{
+  const Layout& L = c.L;
+  const int D = L.D;
+  int* PCNT = c.ia(I_PCNT);
+  if (c.tid == 0)
+    c.s->coll_overflow = 0;
+  BSYNC();
+  coll_scan_pairs<0>(c, x, nullptr);
+  BSYNC();
+  if (costs)
+    FOR(k, L.coll_last - L.coll_first) costs[L.coll_cost0 + k] = c.a(A_HCOST)[L.coll_first + k];
+  if (c.tid == 0 && c.s->coll_overflow)
+    c.s->flags |= THIP_FLAG_CONTACT_OVERFLOW;
+  if (!rows)
+  {
+    BSYNC();
+    return;
+  }
+  int* HP = c.ia(I_HPTR);
+  if (c.tid == 0)
+  {
+    int acc = 0;
+    for (int t = 0; t <= L.N; ++t)
+    {
+      HP[t] = acc;
+      if (t >= L.coll_first && t < L.coll_last)
+        acc += PCNT[t];
+    }
+    if (acc > L.h_cap)
+    {
+      c.s->coll_overflow = 1;
+      acc = 0;
+      for (int t = 0; t <= L.N; ++t)
+        HP[t] = 0;
+    }
+    c.s->n_h = acc;
+  }
+  BSYNC();
+  if (c.s->coll_overflow)
+  {
+    if (c.tid == 0)
+    {
+      c.s->n_h = 0;
+      c.s->flags |= THIP_FLAG_CONTACT_OVERFLOW;
+    }
+    BSYNC();
+    return;
+  }
+  coll_scan_pairs<1>(c, x, HP);
+  BSYNC();
+  // rows: distance expression k + a_t.x_t + a_t+1.x_t+1 per contact
+  const thip_chain& ch = c.d->chain;
+  const int* CONT = c.ia(I_CONT);
+  const int* HT = c.ia(I_HT);
+  double *HC0 = c.a(A_HC0), *HK = c.a(A_HK);
+  int* HM = c.ia(I_HMASK);
+  FOR(k, c.s->n_h)
+  {
+    const int t = HT[k], i = CONT[3 * k + 0], s = CONT[3 * k + 1], p = CONT[3 * k + 2];
+    const double* q0 = x + t * D;
+    const double* q1 = x + (t + 1) * D;
+    const int cnt = lvs_count(q0, q1, D, c.d->coll_lvs);
+    const int link = c.d->sphere_link[s];
+    double q[THIP_MAX_DOF];
+    for (int j = 0; j < D; ++j)
+      q[j] = linspaced(cnt, q0[j], q1[j], i);
+    Pose T;
+    chain_fk(ch, q, link, T);
+    const double* cs = c.d->sphere_center[s];
+    double ctr[3];
+    for (int r = 0; r < 3; ++r)
+      ctr[r] = T.r[r * 3 + 0] * cs[0] + T.r[r * 3 + 1] * cs[1] + T.r[r * 3 + 2] * cs[2] + T.t[r];
+    double dist, n[3], pr[3];
+    sphere_prim_distance(ctr, c.d->sphere_radius[s], c.scene + 16 * p, dist, n, pr);
+    // nearest_points_local[0] and the reference-point offset
+    // link_transform.linear() * nearest_points_local (sub-state pose)
+    const double w[3] = { pr[0] - T.t[0], pr[1] - T.t[1], pr[2] - T.t[2] };
+    double pl[3], rv[3];
+    for (int r = 0; r < 3; ++r)
+      pl[r] = T.r[0 * 3 + r] * w[0] + T.r[1 * 3 + r] * w[1] + T.r[2 * 3 + r] * w[2];
+    for (int r = 0; r < 3; ++r)
+      rv[r] = T.r[r * 3 + 0] * pl[0] + T.r[r * 3 + 1] * pl[1] + T.r[r * 3 + 2] * pl[2];
+    const double cc_time = double(i) * (1.0 / double(cnt - 1));
+    const bool f0 = coll_fixed_step(c, t), f1 = coll_fixed_step(c, t + 1);
+    double cst = dist;
+    int mask = 0;
+    double* a = HC0 + k * 2 * D;
+    for (int e = 0; e < 2; ++e)
+    {
+      const bool skip = (e == 0) ? f0 : f1;
+      const double* qe = (e == 0) ? q0 : q1;
+      if (skip)
+      {
+        for (int j = 0; j < D; ++j)
+          a[e * D + j] = 0.0;
+        continue;
+      }
+      const double scale = (e == 1) ? cc_time : (1 - cc_time);
+      double J[6 * THIP_MAX_DOF];
+      chain_jacobian(ch, qe, link, J);
+      double gd = 0;
+      for (int j = 0; j < D; ++j)
+      {
+        const double wx = J[3 * D + j], wy = J[4 * D + j], wz = J[5 * D + j];
+        const double l0 = J[0 * D + j] + (wy * rv[2] - wz * rv[1]);
+        const double l1 = J[1 * D + j] + (wz * rv[0] - wx * rv[2]);
+        const double l2 = J[2 * D + j] + (wx * rv[1] - wy * rv[0]);
+        const double g = -1.0 * (n[0] * l0 + n[1] * l1 + n[2] * l2);
+        const double av = scale * g;
+        gd += g * qe[j];
+        // cleanupAff (expr_ops.cpp:88-99)
+        const bool keep = fabs(av) > 1e-7;
+        a[e * D + j] = keep ? av : 0.0;
+        mask |= keep ? (1 << (e * D + j)) : 0;
+      }
+      cst += scale * -gd;
+    }
+    HK[k] = cst;
+    HM[k] = mask;
+    c.a(A_HDIST)[k] = dist;
+  }
+  BSYNC();
 }
 
 // ======================================================================
@@ -348,13 +624,52 @@ __device__ void evaluate(Ctx& c, const double* x, double* costs, double* viols)
     }
   }
   BSYNC();
+  if (L.coll)
+    coll_scan(c, x, costs, false);
 }
 
 // ======================================================================
 // QP assembly + Ruiz scaling (osqp scale_data) on the structured QP.
 // Rows: [fixed rows | abs rows | bound rows(n_cols)].
 // ======================================================================
-__device__ __forceinline__ int bound_row(const Layout& L, int col) { return L.n_rows + col; }
+__device__ __forceinline__ int bound_row(const Layout& L, int col)
+{
+  return col < L.nc_base ? L.n_rows + col : L.m_base + 2 * (col - L.nc_base) + 1;
+}
+// row kinds: fixed-timestep, CartPose (abs), bound of a column, hinge
+enum RowKind : int
+{
+  RK_FIXED = 0,
+  RK_ABS,
+  RK_BOUND,
+  RK_HINGE
+};
+__device__ __forceinline__ int row_kind(const Layout& L, int r, int& idx)
+{
+  if (r < L.n_fixed_rows)
+  {
+    idx = r;
+    return RK_FIXED;
+  }
+  if (r < L.n_rows)
+  {
+    idx = r - L.n_fixed_rows;
+    return RK_ABS;
+  }
+  if (r < L.m_base)
+  {
+    idx = r - L.n_rows;
+    return RK_BOUND;
+  }
+  const int h2 = r - L.m_base;
+  if (h2 & 1)
+  {
+    idx = L.nc_base + (h2 >> 1);
+    return RK_BOUND;
+  }
+  idx = h2 >> 1;
+  return RK_HINGE;
+}
 
 __device__ void build_and_scale(Ctx& c)
 {
@@ -419,7 +734,24 @@ __device__ void build_and_scale(Ctx& c)
       GS[r * D + j] = G[r * D + j];
   }
   FOR(f, L.n_fixed_rows) FS[f] = 1.0;
-  FOR(r, L.m) E[r] = 1.0;
+  // hinge rows (CollisionCost::convex -> addHinge): viol - h <= 0 with
+  // viol = margin - (k + a.x): row coefficients -a (x_t, x_t+1) and -1 (h),
+  // objective coeff * h (modeling.cpp:19-27)
+  const int nh = c.s->n_h;
+  {
+    const double* HC0 = c.a(A_HC0);
+    double *HC = c.a(A_HC), *HW = c.a(A_HW);
+    FOR(e, nh * 2 * D) HC[e] = -HC0[e];
+    FOR(h, nh)
+    {
+      HW[h] = -1.0;
+      const int col = L.nc_base + h;
+      Q[col] = c.d->coll_coeff;
+      DS[col] = 1.0;
+      BS[col] = 1.0;
+    }
+  }
+  FOR(r, c.m()) E[r] = 1.0;
   if (c.tid == 0)
     c.s->c = 1.0;
   BSYNC();
@@ -428,7 +760,7 @@ __device__ void build_and_scale(Ctx& c)
   for (int it = 0; it < os.scaling; ++it)
   {
     // column norms of [P; A]
-    FOR(col, L.n_cols)
+    FOR(col, c.nc())
     {
       double v;
       if (col < nx)
@@ -444,35 +776,57 @@ __device__ void build_and_scale(Ctx& c)
           v = fmax(v, fabs(FS[f * D + j]));
         for (int p = c.T.step_ptr[t]; p < c.T.step_ptr[t + 1]; ++p)
           v = fmax(v, fabs(GS[c.T.step_rows[p] * D + j]));
+        if (nh > 0)
+        {
+          const double* HC = c.a(A_HC);
+          const int* HP = c.ia(I_HPTR);
+          for (int h = HP[t]; h < HP[t + 1]; ++h)
+            v = fmax(v, fabs(HC[h * 2 * D + j]));
+          if (t > 0)
+            for (int h = HP[t - 1]; h < HP[t]; ++h)
+              v = fmax(v, fabs(HC[h * 2 * D + D + j]));
+        }
         v = fmax(v, fabs(BS[col]));
       }
-      else
+      else if (col < L.nc_base)
       {
         const int r = (col - nx) >> 1, sd = (col - nx) & 1;
         v = fmax(fabs(WS[2 * r + sd]), fabs(BS[col]));
       }
+      else
+        v = fmax(fabs(c.a(A_HW)[col - L.nc_base]), fabs(BS[col]));
       Dt[col] = 1.0 / sqrt(limit_scaling(v));
     }
-    FOR(r, L.m)
+    FOR(r, c.m())
     {
       double v;
-      if (r < L.n_fixed_rows)
+      int idx;
+      const int kind = row_kind(L, r, idx);
+      if (kind == RK_FIXED)
         v = fabs(FS[r]);
-      else if (r < L.n_rows)
+      else if (kind == RK_ABS)
       {
-        const int a = r - L.n_fixed_rows;
+        const int a = idx;
         v = 0;
         for (int j = 0; j < D; ++j)
           v = fmax(v, fabs(GS[a * D + j]));
         v = fmax(v, fabs(WS[2 * a]));
         v = fmax(v, fabs(WS[2 * a + 1]));
       }
+      else if (kind == RK_BOUND)
+        v = fabs(BS[idx]);
       else
-        v = fabs(BS[r - L.n_rows]);
+      {
+        const double* HC = c.a(A_HC);
+        v = 0;
+        for (int k = 0; k < 2 * D; ++k)
+          v = fmax(v, fabs(HC[idx * 2 * D + k]));
+        v = fmax(v, fabs(c.a(A_HW)[idx]));
+      }
       Et[r] = 1.0 / sqrt(limit_scaling(v));
     }
     BSYNC();
-    FOR(col, L.n_cols)
+    FOR(col, c.nc())
     {
       if (col < nx)
       {
@@ -500,11 +854,23 @@ __device__ void build_and_scale(Ctx& c)
       const int col = c.d->fixed_steps[slot] * D + j;
       FS[f] = (FS[f] * Et[f]) * Dt[col];
     }
-    FOR(r, L.m) E[r] *= Et[r];
+    if (nh > 0)
+    {
+      double *HC = c.a(A_HC), *HW = c.a(A_HW);
+      const int* HT = c.ia(I_HT);
+      FOR(e, nh * 2 * D)
+      {
+        const int h = e / (2 * D), k = e % (2 * D);
+        const int col = (HT[h] + (k >= D ? 1 : 0)) * D + (k % D);
+        HC[e] = (HC[e] * Et[L.m_base + 2 * h]) * Dt[col];
+      }
+      FOR(h, nh) HW[h] = (HW[h] * Et[L.m_base + 2 * h]) * Dt[L.nc_base + h];
+    }
+    FOR(r, c.m()) E[r] *= Et[r];
     BSYNC();
     // cost normalisation
     double colsum = 0, qn = 0;
-    FOR(col, L.n_cols)
+    FOR(col, c.nc())
     {
       if (col < nx)
       {
@@ -521,12 +887,12 @@ __device__ void build_and_scale(Ctx& c)
     colsum = block_sum(c, colsum);
     double qq[1] = { qn };
     block_max<1>(c, qq);
-    double ct = colsum / (double)L.n_cols;
+    double ct = colsum / (double)c.nc();
     const double iq = limit_scaling(qq[0]);
     ct = fmax(ct, iq);
     ct = limit_scaling(ct);
     ct = 1.0 / ct;
-    FOR(col, L.n_cols)
+    FOR(col, c.nc())
     {
       if (col < nx)
       {
@@ -625,7 +991,7 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
   const double *PD = c.a(A_PD), *PO = c.a(A_PO), *BS = c.a(A_BS), *GS = c.a(A_GS), *WS = c.a(A_WS),
                *FS = c.a(A_FS);
   double *DG = c.a(A_DG), *RE = c.a(A_RE), *KB = c.a(A_KB), *LI = c.a(A_LINV);
-  FOR(col, L.n_cols)
+  FOR(col, c.nc())
   {
     const double rb = rho_k(c, bound_row(L, col), polish, delta);
     DG[col] = sigK + rb * (BS[col] * BS[col]);
@@ -640,6 +1006,15 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
     const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
     const double det = dn * dp + rr * (dn * wp * wp + dp * wn * wn);
     RE[r] = rr * dn * dp / det;
+  }
+  // hinge rows: one hinge variable, rho_eff = rho d / (d + rho w^2)
+  const int nh = c.s->n_h;
+  FOR(h, nh)
+  {
+    const int col = L.nc_base + h;
+    const double rr = rho_k(c, L.m_base + 2 * h, polish, delta);
+    const double dn = DG[col], w = c.a(A_HW)[h];
+    c.a(A_HRE)[h] = rr * dn / (dn + rr * w * w);
   }
   BSYNC();
   // diagonal blocks
@@ -662,7 +1037,32 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
       const int r = c.T.step_rows[p];
       v += RE[r] * (GS[r * D + i] * GS[r * D + j]);
     }
+    if (nh > 0)
+    {
+      const double *HC = c.a(A_HC), *HRE = c.a(A_HRE);
+      const int* HP = c.ia(I_HPTR);
+      for (int h = HP[t]; h < HP[t + 1]; ++h)
+        v += HRE[h] * (HC[h * 2 * D + i] * HC[h * 2 * D + j]);
+      if (t > 0)
+        for (int h = HP[t - 1]; h < HP[t]; ++h)
+          v += HRE[h] * (HC[h * 2 * D + D + i] * HC[h * 2 * D + D + j]);
+    }
     KB[e] = v;
+  }
+  if (L.coll)
+  {
+    // dense couplings K_{t+1,t} = diag(PO_t) + sum_h rho_eff a_t+1 a_t^T
+    double* CPL = c.a(A_CPL);
+    const double *HC = c.a(A_HC), *HRE = c.a(A_HRE);
+    const int* HP = c.ia(I_HPTR);
+    FOR(e, (N - 1) * D * D)
+    {
+      const int t = e / (D * D), i = (e / D) % D, j = e % D;
+      double v = (i == j) ? PO[t * D + i] : 0.0;
+      for (int h = HP[t]; h < HP[t + 1]; ++h)
+        v += HRE[h] * (HC[h * 2 * D + D + i] * HC[h * 2 * D + j]);
+      CPL[e] = v;
+    }
   }
   BSYNC();
   // Twisted ("burn at both ends") block Cholesky.  Wave 0 eliminates the
@@ -715,10 +1115,25 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
           sv.M[t * DD + e] = v;
         }
       wave_sync();
-      for (int e = c.lane; e < DD; e += 64)
+      if (!L.coll)
+        for (int e = c.lane; e < DD; e += 64)
+        {
+          const int i = e / D, q = e % D;
+          Ls[e] = PO[cpl * D + i] * Li[q * D + i];
+        }
+      else
       {
-        const int i = e / D, q = e % D;
-        Ls[e] = PO[cpl * D + i] * Li[q * D + i];
+        // Lsub[i][q] = sum_j K[i][j] LI_t[q][j] with K = K_{t+1,t} (top)
+        // or K_{t-1,t} = K_{t,t-1}^T (bottom)
+        const double* Kc = c.a(A_CPL) + cpl * DD;
+        for (int e = c.lane; e < DD; e += 64)
+        {
+          const int i = e / D, q = e % D;
+          double v = 0;
+          for (int j = 0; j <= q; ++j)
+            v += ((w == 0) ? Kc[i * D + j] : Kc[j * D + i]) * Li[q * D + j];
+          Ls[e] = v;
+        }
       }
       wave_sync();
       for (int e = c.lane; e < DD; e += 64)
@@ -991,6 +1406,16 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     BA[ca] = rn;
     BA[ca + 1] = rp;
   }
+  const int nh = c.s->n_h;
+  FOR(h, nh)
+  {
+    const int col = L.nc_base + h;
+    const double rr = rho_k(c, L.m_base + 2 * h, polish, delta);
+    const double dn = DG[col], w = c.a(A_HW)[h];
+    const double rn = BX[col] + BS[col] * eta[bound_row(L, col)];
+    MR[L.n_rows + h] = (eta[L.m_base + 2 * h] * dn - rr * w * rn) / (dn + rr * w * w);
+    BA[col] = rn;
+  }
   BSYNC();
   FOR(col, nx)
   {
@@ -1003,6 +1428,16 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     {
       const int r = c.T.step_rows[p];
       b += GS[r * D + j] * MR[r];
+    }
+    if (nh > 0)
+    {
+      const double* HC = c.a(A_HC);
+      const int* HP = c.ia(I_HPTR);
+      for (int h = HP[t]; h < HP[t + 1]; ++h)
+        b += HC[h * 2 * D + j] * MR[L.n_rows + h];
+      if (t > 0)
+        for (int h = HP[t - 1]; h < HP[t]; ++h)
+          b += HC[h * 2 * D + D + j] * MR[L.n_rows + h];
     }
     BX[col] = b;
   }
@@ -1062,6 +1497,18 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     out[ca] = (dp * rn + rr * wp * cross + wn * dp * h) / det;
     out[ca + 1] = (dn * rp - rr * wn * cross + wp * dn * h) / det;
   }
+  FOR(h, nh)
+  {
+    const int t = c.ia(I_HT)[h];
+    const double* HC = c.a(A_HC) + h * 2 * D;
+    double g = 0;
+    for (int k = 0; k < 2 * D; ++k)
+      g += HC[k] * lds(CV)[t * D + k];
+    const int col = L.nc_base + h;
+    const double rr = rho_k(c, L.m_base + 2 * h, polish, delta);
+    const double dn = DG[col], w = c.a(A_HW)[h];
+    out[col] = (BA[col] + w * (eta[L.m_base + 2 * h] - rr * g)) / (dn + rr * w * w);
+  }
   BSYNC();
   PROF_LAP(11);
 #undef PROF_LAP
@@ -1089,8 +1536,25 @@ __device__ __forceinline__ double row_ax(const Ctx& c, int r, const double* x)
     v += c.a(A_WS)[2 * a] * x[ca] + c.a(A_WS)[2 * a + 1] * x[ca + 1];
     return v;
   }
-  const int col = r - L.n_rows;
-  return c.a(A_BS)[col] * x[col];
+  if (r < L.m_base)
+  {
+    const int col = r - L.n_rows;
+    return c.a(A_BS)[col] * x[col];
+  }
+  const int h2 = r - L.m_base, h = h2 >> 1;
+  if (h2 & 1)
+  {
+    const int col = L.nc_base + h;
+    return c.a(A_BS)[col] * x[col];
+  }
+  // hinge row: a_t.x_t + a_t+1.x_t+1 + w h
+  const int t = c.ia(I_HT)[h];
+  const double* HC = c.a(A_HC) + h * 2 * D;
+  double v = 0;
+  for (int k = 0; k < 2 * D; ++k)
+    v += HC[k] * x[t * D + k];
+  v += c.a(A_HW)[h] * x[L.nc_base + h];
+  return v;
 }
 
 // (P x)_col and (A' y)_col (scaled)
@@ -1125,11 +1589,26 @@ __device__ __forceinline__ double col_aty(const Ctx& c, int col, const double* y
       const int a = c.T.step_rows[p];
       v += GS[a * D + j] * y[L.n_fixed_rows + a];
     }
+    if (c.s->n_h > 0)
+    {
+      const double* HC = c.a(A_HC);
+      const int* HP = c.ia(I_HPTR);
+      for (int h = HP[t]; h < HP[t + 1]; ++h)
+        v += HC[h * 2 * D + j] * y[L.m_base + 2 * h];
+      if (t > 0)
+        for (int h = HP[t - 1]; h < HP[t]; ++h)
+          v += HC[h * 2 * D + D + j] * y[L.m_base + 2 * h];
+    }
   }
-  else
+  else if (col < L.nc_base)
   {
     const int a = (col - L.nx) >> 1, sd = (col - L.nx) & 1;
     v += c.a(A_WS)[2 * a + sd] * y[L.n_fixed_rows + a];
+  }
+  else
+  {
+    const int h = col - L.nc_base;
+    v += c.a(A_HW)[h] * y[L.m_base + 2 * h];
   }
   return v;
 }
@@ -1139,12 +1618,11 @@ __device__ __forceinline__ double col_aty(const Ctx& c, int col, const double* y
 // ======================================================================
 __device__ void set_rho_vec(Ctx& c)
 {
-  const Layout& L = c.L;
   const double *Lo = c.a(A_L), *Up = c.a(A_U);
   double* RH = c.a(A_RHO);
   int* TY = c.ia(I_TYPE);
   const double rho = c.s->rho;
-  FOR(r, L.m)
+  FOR(r, c.m())
   {
     int ty;
     double rv;
@@ -1181,11 +1659,10 @@ struct Norms
 __device__ void compute_residuals(Ctx& c, const double* x, const double* z, const double* y, Norms& nm)
 {
   PROF(1);
-  const Layout& L = c.L;
   double *AX = c.a(A_AX), *PX = c.a(A_PX), *ATY = c.a(A_ATY), *PRV = c.a(A_PRV), *DRV = c.a(A_DRV);
   const double *E = c.a(A_E), *DS = c.a(A_DS), *Q = c.a(A_Q);
   double v[12] = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
-  FOR(r, L.m)
+  FOR(r, c.m())
   {
     const double ax = row_ax(c, r, x);
     const double pr = ax - z[r];
@@ -1199,7 +1676,7 @@ __device__ void compute_residuals(Ctx& c, const double* x, const double* z, cons
     v[4] = fmax(v[4], fabs(z[r]));
     v[5] = fmax(v[5], fabs(ax));
   }
-  FOR(col, L.n_cols)
+  FOR(col, c.nc())
   {
     const double px = col_px(c, col, x);
     const double aty = col_aty(c, col, y);
@@ -1216,7 +1693,7 @@ __device__ void compute_residuals(Ctx& c, const double* x, const double* z, cons
     v[11] = fmax(v[11], fmax(fabs(Q[col]), fmax(fabs(aty), fabs(px))));
   }
   block_max<12>(c, v);
-  nm.prim_res = (L.m > 0) ? v[0] : 0.0;
+  nm.prim_res = (c.m() > 0) ? v[0] : 0.0;
   nm.zE = v[1];
   nm.axE = v[2];
   nm.pr = v[3];
@@ -1232,11 +1709,10 @@ __device__ void compute_residuals(Ctx& c, const double* x, const double* z, cons
 
 __device__ bool is_primal_infeasible(Ctx& c, double eps)
 {
-  const Layout& L = c.L;
   double* DY = c.a(A_DY);
   const double *Lo = c.a(A_L), *Up = c.a(A_U), *E = c.a(A_E), *DS = c.a(A_DS);
   double nv[1] = { 0 };
-  FOR(r, L.m)
+  FOR(r, c.m())
   {
     double dy = DY[r];
     if (Up[r] > kInf * kMinScal)
@@ -1251,39 +1727,38 @@ __device__ bool is_primal_infeasible(Ctx& c, double eps)
   if (!(ndy > kDivTol))
     return false;
   double lhs = 0;
-  FOR(r, L.m) lhs += Up[r] * fmax(DY[r], 0.0) + Lo[r] * fmin(DY[r], 0.0);
+  FOR(r, c.m()) lhs += Up[r] * fmax(DY[r], 0.0) + Lo[r] * fmin(DY[r], 0.0);
   lhs = block_sum(c, lhs);
   if (!(lhs < eps * ndy))
     return false;
   double av[1] = { 0 };
-  FOR(col, L.n_cols) av[0] = fmax(av[0], fabs((1.0 / DS[col]) * col_aty(c, col, DY)));
+  FOR(col, c.nc()) av[0] = fmax(av[0], fabs((1.0 / DS[col]) * col_aty(c, col, DY)));
   block_max<1>(c, av);
   return av[0] < eps * ndy;
 }
 
 __device__ bool is_dual_infeasible(Ctx& c, double eps)
 {
-  const Layout& L = c.L;
   const double *DX = c.a(A_DX), *DS = c.a(A_DS), *Q = c.a(A_Q), *E = c.a(A_E), *Lo = c.a(A_L), *Up = c.a(A_U);
   double nv[1] = { 0 };
-  FOR(col, L.n_cols) nv[0] = fmax(nv[0], fabs(DS[col] * DX[col]));
+  FOR(col, c.nc()) nv[0] = fmax(nv[0], fabs(DS[col] * DX[col]));
   block_max<1>(c, nv);
   const double ndx = nv[0];
   const double cs = c.s->c;
   if (!(ndx > kDivTol))
     return false;
   double qdx = 0;
-  FOR(col, L.n_cols) qdx += Q[col] * DX[col];
+  FOR(col, c.nc()) qdx += Q[col] * DX[col];
   qdx = block_sum(c, qdx);
   if (!(qdx < cs * eps * ndx))
     return false;
   double pv[1] = { 0 };
-  FOR(col, L.n_cols) pv[0] = fmax(pv[0], fabs((1.0 / DS[col]) * col_px(c, col, DX)));
+  FOR(col, c.nc()) pv[0] = fmax(pv[0], fabs((1.0 / DS[col]) * col_px(c, col, DX)));
   block_max<1>(c, pv);
   if (!(pv[0] < cs * eps * ndx))
     return false;
   double bad[1] = { 0 };
-  FOR(r, L.m)
+  FOR(r, c.m())
   {
     const double adx = (1.0 / E[r]) * row_ax(c, r, DX);
     if (((Up[r] < kInf * kMinScal) && (adx > eps * ndx)) || ((Lo[r] > -kInf * kMinScal) && (adx < -eps * ndx)))
@@ -1307,7 +1782,7 @@ __device__ bool check_termination(Ctx& c, const Norms& nm, bool approx)
     edi *= 10;
   }
   bool prim_ok = false, dual_ok = false, pinf = false, dinf = false;
-  if (c.L.m == 0)
+  if (c.m() == 0)
     prim_ok = true;
   else
   {
@@ -1338,7 +1813,6 @@ __device__ bool check_termination(Ctx& c, const Norms& nm, bool approx)
 __device__ void admm_step(Ctx& c, Solver& sv)
 {
   PROF(0);
-  const Layout& L = c.L;
   const thip_osqp_settings& os = c.d->osqp;
   const double sig = os.sigma, al = os.alpha;
   // swap buffers
@@ -1354,12 +1828,12 @@ __device__ void admm_step(Ctx& c, Solver& sv)
   double* BX = c.a(A_BXW);
   const double *Q = c.a(A_Q), *RH = c.a(A_RHO), *Lo = c.a(A_L), *Up = c.a(A_U);
   double* ETA = c.a(A_PZ);  // eta = rho zp - y over all rows (scratch)
-  FOR(r, L.m) ETA[r] = RH[r] * zp[r] - Y[r];
-  FOR(col, L.n_cols) BX[col] = sig * xp[col] - Q[col];
+  FOR(r, c.m()) ETA[r] = RH[r] * zp[r] - Y[r];
+  FOR(col, c.nc()) BX[col] = sig * xp[col] - Q[col];
   BSYNC();
   reduced_solve(c, sv, false, 0.0, ETA, XT);
   // z tilde = A x tilde; updates
-  FOR(r, L.m)
+  FOR(r, c.m())
   {
     const double zt = row_ax(c, r, XT);
     const double rho = RH[r];
@@ -1372,7 +1846,7 @@ __device__ void admm_step(Ctx& c, Solver& sv)
     DY[r] = dy;
     Y[r] += dy;
   }
-  FOR(col, L.n_cols)
+  FOR(col, c.nc())
   {
     const double xv = al * XT[col] + (1.0 - al) * xp[col];
     x[col] = xv;
@@ -1743,7 +2217,6 @@ __device__ double rho_estimate(Ctx& c, const Norms& nm)
 __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
 {
   PROF(4);
-  const Layout& L = c.L;
   const thip_osqp_settings& os = c.d->osqp;
   const double delta = os.delta;
   const int cur = c.s->cur;
@@ -1752,7 +2225,7 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
   double* Y = c.a(A_Y);
   const double *Lo = c.a(A_L), *Up = c.a(A_U), *Q = c.a(A_Q);
   int* ACT = c.ia(I_ACT);
-  FOR(r, L.m)
+  FOR(r, c.m())
   {
     int f = 0;
     if (z[r] - Lo[r] < -Y[r])
@@ -1772,14 +2245,14 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
   // PB = [b_x (n_cols); b_y (m)], PS = solution [x; y], PR = residual
   double *PB = c.a(A_PB), *PS = c.a(A_PS), *PR = c.a(A_PR), *PZ = c.a(A_PZ);
   double *BX = c.a(A_BXW), *XT = c.a(A_XT);
-  const int nc = L.n_cols;
+  const int nc = c.nc();
   FOR(col, nc)
   {
     PB[col] = -Q[col];
     PR[col] = -Q[col];
     PS[col] = 0.0;
   }
-  FOR(r, L.m)
+  FOR(r, c.m())
   {
     const double b = (ACT[r] < 0) ? Lo[r] : ((ACT[r] > 0) ? Up[r] : 0.0);
     PB[nc + r] = b;
@@ -1798,12 +2271,12 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
   {
     // solve K_delta d = PR  (rhs_x + A_act' r_y / delta), d_y = (A_act d_x - r_y) / delta
     double* eta = PZ;  // r_y / delta on active rows
-    FOR(r, L.m) eta[r] = (ACT[r] != 0) ? PR[nc + r] / delta : 0.0;
+    FOR(r, c.m()) eta[r] = (ACT[r] != 0) ? PR[nc + r] / delta : 0.0;
     FOR(col, nc) BX[col] = PR[col];
     BSYNC();
     reduced_solve(c, sv, true, delta, eta, XT);
     FOR(col, nc) PS[col] += XT[col];
-    FOR(r, L.m)
+    FOR(r, c.m())
     {
       if (ACT[r] != 0)
         PS[nc + r] += (row_ax(c, r, XT) - PR[nc + r]) / delta;
@@ -1813,13 +2286,13 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
       break;
     // residual of the unregularised KKT: PR = PB - K [x; y]
     FOR(col, nc) PR[col] = PB[col] - col_px(c, col, PS) - col_aty(c, col, PS + nc);
-    FOR(r, L.m) PR[nc + r] = (ACT[r] != 0) ? PB[nc + r] - row_ax(c, r, PS) : 0.0;
+    FOR(r, c.m()) PR[nc + r] = (ACT[r] != 0) ? PB[nc + r] - row_ax(c, r, PS) : 0.0;
     BSYNC();
   }
   // polished point: x, z = A x, y (active) -> normal cone projection
   double* pz = PZ;
   double* py = PR + nc;  // reuse
-  FOR(r, L.m)
+  FOR(r, c.m())
   {
     const double zr = row_ax(c, r, PS);
     const double yr = (ACT[r] != 0) ? PS[nc + r] : 0.0;
@@ -1837,7 +2310,7 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
   if (ok)
   {
     FOR(col, nc) x[col] = PS[col];
-    FOR(r, L.m)
+    FOR(r, c.m())
     {
       z[r] = pz[r];
       Y[r] = py[r];
@@ -1865,21 +2338,29 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   const double *E = c.a(A_E), *GC = c.a(A_GC), *INIT = c.a(A_INIT), *DS = c.a(A_DS);
   // bounds (unscaled -> scaled by E)
   const double tb = c.s->trust;
-  FOR(r, L.m)
+  FOR(r, c.m())
   {
     double lo, up;
-    if (r < L.n_fixed_rows)
+    int idx;
+    const int kind = row_kind(L, r, idx);
+    if (kind == RK_FIXED)
     {
       const int slot = r / D, j = r % D;
       lo = up = INIT[c.d->fixed_steps[slot] * D + j];
     }
-    else if (r < L.n_rows)
+    else if (kind == RK_ABS)
     {
-      lo = up = -GC[r - L.n_fixed_rows];
+      lo = up = -GC[idx];
+    }
+    else if (kind == RK_HINGE)
+    {
+      // ineq row viol - h <= 0: l = -inf, u = -(margin - k) (osqp_interface.cpp:213-281)
+      lo = -kInf;
+      up = -(c.d->coll_margin - c.a(A_HK)[idx]);
     }
     else
     {
-      const int col = r - L.n_rows;
+      const int col = idx;
       if (col < nx)
       {
         const int j = col % D;
@@ -1918,15 +2399,15 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   const double *SX = c.a(A_SOLX), *SY = c.a(A_SOLY);
   if (warm)
   {
-    FOR(col, L.n_cols) x[col] = SX[col] * (1.0 / DS[col]);
-    FOR(r, L.m) Y[r] = (SY[r] * (1.0 / E[r])) * c.s->c;
+    FOR(col, c.nc()) x[col] = SX[col] * (1.0 / DS[col]);
+    FOR(r, c.m()) Y[r] = (SY[r] * (1.0 / E[r])) * c.s->c;
     BSYNC();
-    FOR(r, L.m) z[r] = row_ax(c, r, x);
+    FOR(r, c.m()) z[r] = row_ax(c, r, x);
   }
   else
   {
-    FOR(col, L.n_cols) x[col] = 0.0;
-    FOR(r, L.m)
+    FOR(col, c.nc()) x[col] = 0.0;
+    FOR(r, c.m())
     {
       z[r] = 0.0;
       Y[r] = 0.0;
@@ -2000,7 +2481,7 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
         const double nr = c.s->rho;
         double* RH = c.a(A_RHO);
         const int* TY = c.ia(I_TYPE);
-        FOR(r, L.m)
+        FOR(r, c.m())
         {
           if (TY[r] == 0)
             RH[r] = nr;
@@ -2052,8 +2533,8 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   const int st = c.s->qp_status;
   const bool inf = (st == ST_PINF || st == ST_PINF_INACC || st == ST_DINF || st == ST_DINF_INACC);
   double *SXw = c.a(A_SOLX), *SYw = c.a(A_SOLY);
-  FOR(col, L.n_cols) SXw[col] = inf ? NAN : DS[col] * xc[col];
-  FOR(r, L.m) SYw[r] = inf ? NAN : c.s->cinv * (E[r] * Y[r]);
+  FOR(col, c.nc()) SXw[col] = inf ? NAN : DS[col] * xc[col];
+  FOR(r, c.m()) SYw[r] = inf ? NAN : c.s->cinv * (E[r] * Y[r]);
   BSYNC();
   if (c.tid == 0)
   {
@@ -2066,7 +2547,7 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   if (c.s->trace)
   {
     double xs = 0;
-    FOR(col, L.n_cols) xs += fabs(SXw[col]);
+    FOR(col, c.nc()) xs += fabs(SXw[col]);
     xs = block_sum(c, xs);
     if (c.tid == 0 && c.s->trace_n < c.s->trace_cap)
     {
@@ -2121,6 +2602,10 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
     c.s->n_admm = 0;
     c.s->prev_status = 0;
     c.s->prev_rho = c.d->osqp.rho;
+    c.s->n_h = 0;
+    c.s->n_h_prev = -1;
+    c.s->flags = 0;
+    c.s->coll_overflow = 0;
   }
   BSYNC();
   int* mask = c.ia(I_MASK);
@@ -2148,9 +2633,35 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
       // pattern of A (jacobian drops) vs previous QP setup
       double diff[1] = { 0 };
       FOR(r, L.n_abs) if (mask[r] != pmask[r]) diff[0] = 1.0;
+      if (L.coll)
+      {
+        // hinge rows: same count, start steps and kept coefficients
+        // (OSQPModel compares the CSC pattern of A bytewise)
+        const int nh = c.s->n_h;
+        if (nh != c.s->n_h_prev)
+          diff[0] = 1.0;
+        else
+        {
+          const int *HT = c.ia(I_HT), *HM = c.ia(I_HMASK), *PHT = c.ia(I_PHT), *PHM = c.ia(I_PHMASK);
+          FOR(h, nh) if (HT[h] != PHT[h] || HM[h] != PHM[h]) diff[0] = 1.0;
+        }
+      }
       block_max<1>(c, diff);
       bool pattern_equal = have_prev_setup && diff[0] == 0.0;
       FOR(r, L.n_abs) pmask[r] = mask[r];
+      if (L.coll)
+      {
+        const int *HT = c.ia(I_HT), *HM = c.ia(I_HMASK);
+        int *PHT = c.ia(I_PHT), *PHM = c.ia(I_PHMASK);
+        FOR(h, c.s->n_h)
+        {
+          PHT[h] = HT[h];
+          PHM[h] = HM[h];
+        }
+        BSYNC();
+        if (c.tid == 0)
+          c.s->n_h_prev = c.s->n_h;
+      }
       have_prev_setup = true;
       BSYNC();
       int qp_failures = 0;
@@ -2232,6 +2743,19 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
               v += SX[ca + 1];
             }
             mcost[c.T.term_slot[k]] = v;
+          }
+        }
+        if (L.coll)
+        {
+          // ConvexObjective::value of each step-pair term: sum coeff * h
+          const int* HP = c.ia(I_HPTR);
+          FOR(k, L.coll_last - L.coll_first)
+          {
+            const int t = L.coll_first + k;
+            double v = 0;
+            for (int h = HP[t]; h < HP[t + 1]; ++h)
+              v += c.d->coll_coeff * SX[L.nc_base + h];
+            mcost[L.coll_cost0 + k] = v;
           }
         }
         BSYNC();
@@ -2366,6 +2890,7 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
   for (int k = threadIdx.x; k < A_COUNT; k += kBlock)
     ptab[k] = L.loff[k] >= 0 ? dyn + L.loff[k] : wsb + L.doff[k];
   Ctx c(L, args.T, args.desc, wsb, args.iws + (long long)b * L.istride, dyn, &ctl, ptab);
+  c.scene = args.scene ? args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16 : nullptr;
   Solver sv;
   sv.M = dyn;
   sv.Nb = dyn + L.N * L.D * L.D;
@@ -2405,6 +2930,9 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
     r.final_trust_box = ctl.trust;
     r.n_costs = L.n_costs;
     r.n_cnts = L.n_cnts;
+    r.flags = ctl.flags;
+    if (ctl.flags & THIP_FLAG_CONTACT_OVERFLOW)
+      r.status = THIP_OPT_FAILED;
     args.res[b] = r;
   }
 }
@@ -2469,4 +2997,57 @@ __global__ __launch_bounds__(kBlock) void fwd_kin_kernel(KernelArgs args, const 
   }
 }
 
+// Linearised collision rows at a given trajectory (parity/debug entry
+// thip_collision_rows): records [t, link, prim, sphere, substate, distance,
+// cc_time, n_kept, a_t[D], a_t+1[D], constant] in the hinge-row order.
+__global__ __launch_bounds__(kBlock) void coll_rows_kernel(KernelArgs args, const double* xin, double* out, int cap,
+                                                          int* counts)
+{
+  __shared__ Ctl ctl;
+  const int b = blockIdx.x;
+  if (b >= args.batch)
+    return;
+  const Layout& L = args.L;
+  Ctx c(L, args.T, args.desc, args.ws + (long long)b * L.dstride, args.iws + (long long)b * L.istride, nullptr,
+        &ctl);
+  c.scene = args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16;
+  if (threadIdx.x == 0)
+  {
+    ctl.n_h = 0;
+    ctl.flags = 0;
+    ctl.coll_overflow = 0;
+    ctl.prof = nullptr;
+  }
+  double* XN = c.a(A_XN);
+  FOR(i, L.nx) XN[i] = xin[(long long)b * L.nx + i];
+  BSYNC();
+  coll_scan(c, XN, nullptr, true);
+  const int D = L.D, W = 8 + 2 * D + 1;
+  const int* CONT = c.ia(I_CONT);
+  const int* HT = c.ia(I_HT);
+  const int* HM = c.ia(I_HMASK);
+  const double *HC0 = c.a(A_HC0), *HK = c.a(A_HK), *HD = c.a(A_HDIST);
+  double* ob = out + (long long)b * cap * W;
+  FOR(k, ctl.n_h < cap ? ctl.n_h : cap)
+  {
+    const int t = HT[k], i = CONT[3 * k];
+    const int cnt = lvs_count(XN + t * D, XN + (t + 1) * D, D, args.desc->coll_lvs);
+    double* r = ob + (long long)k * W;
+    r[0] = t;
+    r[1] = args.desc->sphere_link[CONT[3 * k + 1]];
+    r[2] = CONT[3 * k + 2];
+    r[3] = CONT[3 * k + 1];
+    r[4] = i;
+    r[5] = HD[k];
+    r[6] = double(i) * (1.0 / double(cnt - 1));
+    r[7] = __popc(HM[k]);
+    for (int j = 0; j < 2 * D; ++j)
+      r[8 + j] = HC0[k * 2 * D + j];
+    r[8 + 2 * D] = HK[k];
+  }
+  if (threadIdx.x == 0)
+    counts[b] = (ctl.flags & THIP_FLAG_CONTACT_OVERFLOW) ? -1 : ctl.n_h;
+}
+
 }  // namespace thip
+

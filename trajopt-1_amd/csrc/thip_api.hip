@@ -4,6 +4,7 @@
 // across the boundary.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -20,6 +21,7 @@ __global__ void linearize_kernel(KernelArgs args, const double* xin, double* err
 __global__ void fwd_kin_kernel(KernelArgs args, const double* xin, double* poses);
 __global__ void stage_inputs_kernel(KernelArgs args, const double* init, const double* tgt);
 __global__ void gather_x_kernel(KernelArgs args, double* xout);
+__global__ void coll_rows_kernel(KernelArgs args, const double* xin, double* out, int cap, int* counts);
 }  // namespace thip
 
 using namespace thip;
@@ -74,6 +76,7 @@ extern "C" {
 const char* thip_build_info(void) { return "trajopt-1_amd thip 0.1 gfx950 fp64 (one workgroup per problem)"; }
 
 int thip_sizeof_desc(void) { return static_cast<int>(sizeof(thip_problem_desc)); }
+int thip_sizeof_result(void) { return static_cast<int>(sizeof(thip_result)); }
 
 void thip_default_sqp_params(thip_sqp_params* p)
 {
@@ -152,7 +155,34 @@ static int validate(const thip_problem_desc* d, std::string& why)
       return why = "CartPose source frame must be an active chain link", THIP_E_INVALID;
   }
   if (d->coll_enabled)
-    return why = "collision terms are not supported by this build yet", THIP_E_INVALID;
+  {
+    if (d->coll_is_cnt)
+      return why = "collision constraints are not supported (LVS-discrete collision cost only)", THIP_E_INVALID;
+    if (d->n_spheres < 1 || d->n_spheres > THIP_MAX_SPHERES)
+      return why = "collision: n_spheres out of range", THIP_E_INVALID;
+    for (int s = 0; s < d->n_spheres; ++s)
+      if (d->sphere_link[s] < 1 || d->sphere_link[s] >= ch.n_links || !(d->sphere_radius[s] >= 0))
+        return why = "collision: bad robot sphere", THIP_E_INVALID;
+    if (d->n_prims < 0 || d->n_prims > THIP_MAX_PRIMS)
+      return why = "collision: n_prims out of range", THIP_E_INVALID;
+    const int last = d->coll_last_step < 0 ? d->n_steps - 1 : d->coll_last_step;
+    if (d->coll_first_step < 0 || d->coll_first_step >= d->n_steps || last < d->coll_first_step ||
+        last >= d->n_steps)
+      return why = "collision: bad first/last step", THIP_E_INVALID;
+    if (!(d->coll_lvs > 0) || !(d->coll_buffer >= 0))
+      return why = "collision: bad longest_valid_segment_length / buffer", THIP_E_INVALID;
+    for (int t = d->coll_first_step; t < last; ++t)
+    {
+      bool a = false, b = false;
+      for (int k = 0; k < d->coll_n_fixed; ++k)
+      {
+        a |= d->coll_fixed_steps[k] == t;
+        b |= d->coll_fixed_steps[k] == t + 1;
+      }
+      if (a && b)
+        return why = "Currently two adjacent fixed steps are not supported in collision term.", THIP_E_INVALID;
+    }
+  }
   if (d->osqp.check_termination < 0 || d->osqp.max_iter < 1 || d->osqp.scaling < 0)
     return why = "bad OSQP settings", THIP_E_INVALID;
   return THIP_OK;
@@ -228,11 +258,22 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   for (int r = 0; r < L.n_abs; ++r)
     if (!d.cart_is_cnt[row_term[static_cast<size_t>(r)]])
       L.n_abs_cost++;
+  // collision: one cost term per step pair after the CartPose costs
+  // (cost_infos order; CollisionTermInfo::hatch, problem_description.cpp:1747)
+  L.coll = d.coll_enabled ? 1 : 0;
+  L.coll_first = d.coll_first_step;
+  L.coll_last = (d.coll_last_step < 0) ? L.N - 1 : d.coll_last_step;
+  L.coll_cost0 = n_costs;
+  if (L.coll)
+    n_costs += L.coll_last - L.coll_first;
+  L.h_cap = L.coll ? kHingeCap : 0;
   L.n_costs = n_costs;
   L.n_cnts = n_cnts;
-  L.n_cols = L.nx + 2 * L.n_abs;
+  L.nc_base = L.nx + 2 * L.n_abs;
   L.n_rows = L.n_fixed_rows + L.n_abs;
-  L.m = L.n_rows + L.n_cols;
+  L.m_base = L.n_rows + L.nc_base;
+  L.n_cols = L.nc_base + L.h_cap;
+  L.m = L.m_base + 2 * L.h_cap;
   // step -> rows CSR
   std::vector<int> step_ptr(static_cast<size_t>(L.N + 1), 0), step_rows(static_cast<size_t>(std::max(L.n_abs, 1)));
   for (int r = 0; r < L.n_abs; ++r)
@@ -250,15 +291,40 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
 
   // workspace layout (doubles)
   const long long nx = L.nx, nc = L.n_cols, m = L.m, NDD = (long long)L.N * L.D * L.D;
-  const long long sizes[A_COUNT] = {
-    nx, nx, nx, (long long)std::max(L.n_cart, 1) * 12, (long long)std::max(L.n_abs, 1) * L.D, std::max(L.n_abs, 1),
-    std::max(L.n_costs, 1), std::max(L.n_cnts, 1), std::max(L.n_costs, 1), std::max(L.n_cnts, 1),
-    std::max(L.n_cnts, 1), nx, nx, nc, nc, nc, (long long)std::max(L.n_abs, 1) * L.D,
-    (long long)std::max(L.n_abs, 1) * 2, std::max(L.n_fixed_rows, 1), m, m, m, m, nc, nc, m, m, m, nc, m, nc, m, nc,
-    std::max(L.n_rows, 1), m, nc, nc, m, nc, nc, std::max(L.n_rows, 1), NDD, NDD, nx, nx, nc, m, std::max(nc + m, (long long)std::max(L.n_abs, 1) * L.D), nc + m,
-    nc + m, m, nc
-  };
-  static_assert(sizeof(sizes) / sizeof(sizes[0]) == A_COUNT, "workspace size table");
+  const long long nab = std::max(L.n_abs, 1), D = L.D, hc = std::max(L.h_cap, 1);
+  long long sizes[A_COUNT];
+  for (int k = 0; k < A_COUNT; ++k)
+    sizes[k] = -1;
+  sizes[A_X] = sizes[A_XN] = sizes[A_INIT] = nx;
+  sizes[A_TGT] = (long long)std::max(L.n_cart, 1) * 12;
+  sizes[A_G] = sizes[A_GS] = nab * D;
+  sizes[A_GC] = nab;
+  sizes[A_COST] = sizes[A_NCOST] = std::max(L.n_costs, 1);
+  sizes[A_VIOL] = sizes[A_NVIOL] = sizes[A_MU] = std::max(L.n_cnts, 1);
+  sizes[A_PD] = sizes[A_PO] = sizes[A_CV] = sizes[A_YV] = nx;
+  sizes[A_Q] = sizes[A_DS] = sizes[A_BS] = sizes[A_XA0] = sizes[A_XA1] = sizes[A_XT] = sizes[A_DX] = nc;
+  sizes[A_BA] = sizes[A_PX] = sizes[A_ATY] = sizes[A_DRV] = sizes[A_DG] = sizes[A_SOLX] = sizes[A_BXW] = nc;
+  sizes[A_WS] = nab * 2;
+  sizes[A_FS] = std::max(L.n_fixed_rows, 1);
+  sizes[A_E] = sizes[A_L] = sizes[A_U] = sizes[A_RHO] = sizes[A_Z0] = sizes[A_Z1] = sizes[A_Y] = m;
+  sizes[A_ZT] = sizes[A_DY] = sizes[A_AX] = sizes[A_PRV] = sizes[A_SOLY] = sizes[A_PZ] = m;
+  sizes[A_MR] = std::max(L.n_rows, 1) + L.h_cap;
+  sizes[A_RE] = std::max(L.n_rows, 1);
+  sizes[A_LINV] = sizes[A_KB] = NDD;
+  sizes[A_PB] = std::max(nc + m, nab * D);
+  sizes[A_PS] = sizes[A_PR] = nc + m;
+  sizes[A_HC0] = sizes[A_HC] = hc * 2 * D;
+  sizes[A_HK] = sizes[A_HW] = sizes[A_HRE] = sizes[A_HDIST] = hc;
+  sizes[A_CPL] = L.coll ? NDD : 1;
+  sizes[A_CSCR] = L.coll ? (long long)kWaves * kSubCap * d.n_spheres * 3 : 1;
+  sizes[A_HCOST] = L.N;
+  for (int k = 0; k < A_COUNT; ++k)
+    if (sizes[k] < 0)
+    {
+      g_create_err = "internal: workspace size table incomplete";
+      delete ctx;
+      return THIP_E_INVALID;
+    }
   long long off = 0;
   for (int k = 0; k < A_COUNT; ++k)
   {
@@ -266,7 +332,13 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     off += (sizes[k] + 7) / 8 * 8;
   }
   L.dstride = off;
-  const long long isizes[I_COUNT] = { std::max(L.n_abs, 1), std::max(L.n_abs, 1), m, m };
+  long long isizes[I_COUNT];
+  isizes[I_MASK] = isizes[I_PMASK] = nab;
+  isizes[I_TYPE] = isizes[I_ACT] = m;
+  isizes[I_HT] = isizes[I_HMASK] = isizes[I_PHMASK] = isizes[I_PHT] = hc;
+  isizes[I_HPTR] = L.N + 1;
+  isizes[I_CONT] = 3 * hc;
+  isizes[I_PCNT] = L.N;
   long long ioff = 0;
   for (int k = 0; k < I_COUNT; ++k)
   {
@@ -304,7 +376,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     // one column slot (t, i) and one CartPose row per thread: N <= 32 and
     // n_abs <= 256; larger problems run the generic admm_step()
     L.seg_ok = (max_step_rows <= kMaxStepRows && L.D <= 8 && L.loff[A_BXW] >= 0 && L.N * 8 <= kBlock &&
-                L.n_abs <= kBlock) ? 1 : 0;
+                L.n_abs <= kBlock && !L.coll) ? 1 : 0;
     if (const char* e = std::getenv("THIP_NO_SEGMENT"))
       if (e[0] == '1')
         L.seg_ok = 0;
@@ -344,6 +416,32 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   const size_t o_t0 = push(term_row0, THIP_MAX_CART), o_tn = push(term_nrow, THIP_MAX_CART),
                o_ts = push(term_slot, THIP_MAX_CART);
   const size_t o_fs = push(fixed_of_step, static_cast<size_t>(L.N));
+  // collision model tables: spheres grouped by link, ascending (scan order)
+  std::vector<int> grp_link, grp_s0, grp_ns, sph_order, coll_fixed(static_cast<size_t>(L.N), 0);
+  if (L.coll)
+  {
+    for (int s2 = 0; s2 < d.n_spheres; ++s2)
+      sph_order.push_back(s2);
+    std::stable_sort(sph_order.begin(), sph_order.end(),
+                     [&](int a, int b) { return d.sphere_link[a] < d.sphere_link[b]; });
+    for (size_t k = 0; k < sph_order.size(); ++k)
+    {
+      const int link = d.sphere_link[sph_order[k]];
+      if (grp_link.empty() || grp_link.back() != link)
+      {
+        grp_link.push_back(link);
+        grp_s0.push_back(static_cast<int>(k));
+        grp_ns.push_back(0);
+      }
+      grp_ns.back()++;
+    }
+    for (int k = 0; k < d.coll_n_fixed; ++k)
+      if (d.coll_fixed_steps[k] >= 0 && d.coll_fixed_steps[k] < L.N)
+        coll_fixed[static_cast<size_t>(d.coll_fixed_steps[k])] = 1;
+  }
+  const size_t o_gl = push(grp_link, grp_link.size()), o_g0 = push(grp_s0, grp_s0.size()),
+               o_gn = push(grp_ns, grp_ns.size()), o_so = push(sph_order, sph_order.size()),
+               o_cf = push(coll_fixed, coll_fixed.size());
   row_w.resize(std::max<size_t>(na, 1));
   if ((e = hipMalloc(&ctx->d_tables, itab.size() * sizeof(int))) != hipSuccess ||
       (e = hipMalloc(&ctx->d_tables_f, row_w.size() * sizeof(double))) != hipSuccess ||
@@ -362,6 +460,12 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   T.term_nrow = ctx->d_tables + o_tn;
   T.term_slot = ctx->d_tables + o_ts;
   T.fixed_of_step = ctx->d_tables + o_fs;
+  T.n_groups = static_cast<int>(grp_link.size());
+  T.grp_link = ctx->d_tables + o_gl;
+  T.grp_s0 = ctx->d_tables + o_g0;
+  T.grp_ns = ctx->d_tables + o_gn;
+  T.sph_order = ctx->d_tables + o_so;
+  T.coll_fixed = ctx->d_tables + o_cf;
   T.row_w = ctx->d_tables_f;
   const size_t B = static_cast<size_t>(batch);
   if ((e = hipMalloc(&ctx->d_ws, B * static_cast<size_t>(L.dstride) * sizeof(double))) != hipSuccess ||
@@ -410,6 +514,7 @@ static KernelArgs make_args(thip_ctx* ctx)
   a.iws = ctx->d_iws;
   a.res = ctx->d_res;
   a.batch = ctx->batch;
+  a.scene = ctx->d_scene;
   a.trace = ctx->d_trace;
   a.trace_n = ctx->d_trace_n;
   a.trace_cap = ctx->trace_cap;
@@ -439,11 +544,27 @@ static int upload_common(thip_ctx* ctx, const double* init, const double* tgt, h
   return THIP_OK;
 }
 
+static int upload_scene(thip_ctx* ctx, const double* scene, hipMemcpyKind kind)
+{
+  if (!ctx->L.coll)
+    return THIP_OK;
+  if (!scene && ctx->desc.n_prims > 0)
+    return ctx->err = "thip_upload: scene required when collision is enabled", THIP_E_INVALID;
+  const size_t bytes = static_cast<size_t>(ctx->batch) * std::max(ctx->desc.n_prims, 1) * 16 * sizeof(double);
+  if (!ctx->d_scene)
+    HIPCHK(ctx, hipMalloc(&ctx->d_scene, bytes));
+  if (ctx->desc.n_prims > 0)
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_scene, scene, bytes, kind, ctx->stream));
+  return THIP_OK;
+}
+
 int thip_upload(thip_ctx* ctx, const double* init_traj, const double* cart_targets, const double* scene)
 {
   if (!ctx)
     return THIP_E_INVALID;
-  (void)scene;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  if (const int rs = upload_scene(ctx, scene, hipMemcpyHostToDevice); rs != THIP_OK)
+    return rs;
   const int rc = upload_common(ctx, init_traj, cart_targets, hipMemcpyHostToDevice);
   if (rc == THIP_OK)
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -454,7 +575,9 @@ int thip_upload_device(thip_ctx* ctx, const double* d_init_traj, const double* d
 {
   if (!ctx)
     return THIP_E_INVALID;
-  (void)d_scene;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  if (const int rs = upload_scene(ctx, d_scene, hipMemcpyDeviceToDevice); rs != THIP_OK)
+    return rs;
   return upload_common(ctx, d_init_traj, d_cart_targets, hipMemcpyDeviceToDevice);
 }
 
@@ -616,6 +739,50 @@ int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws)
                         hipMemcpyDeviceToHost));
   HIPCHK(ctx, hipMemcpy(iws, ctx->d_iws, B * static_cast<size_t>(ctx->L.istride) * sizeof(int),
                         hipMemcpyDeviceToHost));
+  return THIP_OK;
+}
+
+int thip_collision_rows(thip_ctx* ctx, const double* x, double* records, int cap, int* counts)
+{
+  if (!ctx || !x || !records || !counts || cap <= 0)
+    return THIP_E_INVALID;
+  if (!ctx->L.coll)
+    return ctx->err = "thip_collision_rows: collision is not enabled", THIP_E_STATE;
+  if (!ctx->uploaded || !ctx->d_scene)
+    return ctx->err = "thip_collision_rows: call thip_upload first (scene)", THIP_E_STATE;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const size_t B = static_cast<size_t>(ctx->batch);
+  const Layout& L = ctx->L;
+  const size_t W = 8 + 2 * static_cast<size_t>(L.D) + 1;
+  double *dx = nullptr, *dout = nullptr;
+  int* dcnt = nullptr;
+  hipError_t e;
+  if ((e = hipMalloc(&dx, B * L.nx * sizeof(double))) != hipSuccess ||
+      (e = hipMalloc(&dout, B * static_cast<size_t>(cap) * W * sizeof(double))) != hipSuccess ||
+      (e = hipMalloc(&dcnt, B * sizeof(int))) != hipSuccess)
+  {
+    hipFree(dx);
+    hipFree(dout);
+    hipFree(dcnt);
+    return ctx->err = std::string("thip_collision_rows: hipMalloc: ") + hipGetErrorString(e), THIP_E_NOMEM;
+  }
+  hipMemcpyAsync(dx, x, B * L.nx * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
+  hipMemsetAsync(dout, 0, B * static_cast<size_t>(cap) * W * sizeof(double), ctx->stream);
+  KernelArgs a = make_args(ctx);
+  hipLaunchKernelGGL(coll_rows_kernel, dim3(ctx->batch), dim3(kBlock), 0, ctx->stream, a, dx, dout, cap, dcnt);
+  e = hipGetLastError();
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(records, dout, B * static_cast<size_t>(cap) * W * sizeof(double), hipMemcpyDeviceToHost,
+                       ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(counts, dcnt, B * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess)
+    e = hipStreamSynchronize(ctx->stream);
+  hipFree(dx);
+  hipFree(dout);
+  hipFree(dcnt);
+  if (e != hipSuccess)
+    return ctx->err = std::string("thip_collision_rows: ") + hipGetErrorString(e), THIP_E_HIP;
   return THIP_OK;
 }
 

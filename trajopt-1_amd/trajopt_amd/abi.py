@@ -139,6 +139,7 @@ class Result(C.Structure):
         ("final_trust_box", C.c_double),
         ("n_costs", C.c_int),
         ("n_cnts", C.c_int),
+        ("flags", C.c_int),
     ]
 
 
@@ -231,12 +232,16 @@ def _declare(lib):
     lib.thip_debug_trace.restype = C.c_int
     lib.thip_debug_get_trace.argtypes = [vp, dp, P(C.c_int)]
     lib.thip_debug_get_trace.restype = C.c_int
+    lib.thip_collision_rows.argtypes = [vp, dp, dp, C.c_int, P(C.c_int)]
+    lib.thip_collision_rows.restype = C.c_int
     lib.thip_debug_profile.argtypes = [vp, C.c_int]
     lib.thip_debug_profile.restype = C.c_int
     lib.thip_debug_get_profile.argtypes = [vp, P(C.c_longlong)]
     lib.thip_debug_get_profile.restype = C.c_int
     lib.thip_sizeof_desc.argtypes = []
     lib.thip_sizeof_desc.restype = C.c_int
+    lib.thip_sizeof_result.argtypes = []
+    lib.thip_sizeof_result.restype = C.c_int
     return lib
 
 
@@ -258,8 +263,8 @@ def load_hip():
                 f"{HIP_LIB} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)"
             )
         _hip = _declare(C.CDLL(str(HIP_LIB)))
-        if _hip.thip_sizeof_desc() != C.sizeof(ProblemDesc):
-            raise RuntimeError("thip_problem_desc layout mismatch between Python and the HIP library")
+        if _hip.thip_sizeof_desc() != C.sizeof(ProblemDesc) or _hip.thip_sizeof_result() != C.sizeof(Result):
+            raise RuntimeError("thip_problem_desc / thip_result layout mismatch between Python and the HIP library")
     return _hip
 
 

@@ -87,6 +87,23 @@ class BatchTrustRegionSQP:
         self._check(self.lib.thip_fwd_kin(self.ctx, _dp(x), _dp(poses)), "thip_fwd_kin")
         return poses
 
+    def collision_rows(self, x, cap=4096):
+        """Linearised collision rows at trajectories x [B, N, D] (list of
+        [n, 8 + 2 D + 1] arrays, one per problem; see thip_collision_rows)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        if not self.uploaded:
+            self.upload()
+        W = 8 + 2 * self.wl.n_dof + 1
+        rec = np.zeros((self.batch, cap, W))
+        cnt = (C.c_int * self.batch)()
+        self._check(self.lib.thip_collision_rows(self.ctx, _dp(x), _dp(rec), cap, cnt), "thip_collision_rows")
+        out = []
+        for b in range(self.batch):
+            if cnt[b] < 0:
+                raise HipError(f"problem {b}: contact overflow")
+            out.append(rec[b, : min(cnt[b], cap)])
+        return out
+
     def enable_trace(self, capacity=512):
         self._trace_cap = capacity
         self._check(self.lib.thip_debug_trace(self.ctx, capacity), "thip_debug_trace")
