@@ -2,9 +2,12 @@
 """Batched trust-region SQP benchmark (BASELINE.json metric).
 
 A "step" is one sco::BasicTrustRegionSQP::optimize of every problem in the
-per-GPU batch (1024 problems of 7-DoF x 30 waypoints), run by one fused HIP
-launch from inputs already resident in HBM.  `value` is SQP (outer) iterations
-per second summed over all problems of all ranks.
+per-GPU batch, run by one fused HIP launch from inputs already resident in
+HBM.  The default workload is BASELINE.json configs[2] (config C): 7-DoF PR2
+arm, 30 waypoints, JointVel + 29 CartPose costs + the LVS-discrete collision
+cost against a 10-primitive scene, 1024 problems per GPU.  `value` is SQP
+(outer) iterations per second summed over all problems of all ranks
+(SURVEY.md §8d).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 1024]
 
@@ -39,6 +42,14 @@ from trajopt_amd import abi, problems, sharding  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 
 
+def workload_name(wl, config, batch):
+    terms = f"JointVel + {wl.desc.n_cart} CartPose ABS costs"
+    if wl.desc.coll_enabled:
+        terms += f" + LVS-discrete collision cost ({wl.desc.n_prims}-primitive scene)"
+    return (f"config {config}: 7-DoF PR2 arm x {wl.n_steps} waypoints, {terms}, batch {batch} per GPU "
+            "(BasicTrustRegionSQP + OSQP-semantics ADMM/polish)")
+
+
 def algorithmic_bytes(wl, results):
     """B_iter = fixed + k * per_admm + s * 16 nnz(L) per problem
     per SQP iteration; summed over the batch it needs only the per-problem
@@ -54,11 +65,16 @@ def algorithmic_bytes(wl, results):
     fixed = 2 * 8 * nx + 8 * R * (1 + D) + 96 * wl.desc.n_cart + 2 * 8 * (n + 2 * m + R * (D + 2))
     per_admm = 2 * 12 * nnz_a + 24 * nnz_p + 8 * (3 * n + 7 * m)
     refine = wl.desc.osqp.polish_refine_iter
+    # config C (§8d): per contact row 8*(1 + 14) when built and 2*12*16 per
+    # ADMM iteration; 10 primitives x 16 doubles read per sub-state pass
+    row_b, admm_b, sub_b = 8 * (1 + 2 * D), 2 * 12 * (2 * D + 2), 8 * 16 * wl.desc.n_prims
     total = 0
     for r in results:
         kkt_solves = r.n_admm_iters + r.n_qp_solves * (1 + refine)
         total += fixed * r.n_sqp_iters + per_admm * r.n_admm_iters + 16 * nnz_l * kkt_solves
-    return total, {"fixed": fixed, "per_admm": per_admm, "nnz_L": nnz_l}
+        total += row_b * r.n_contact_rows + admm_b * r.n_hinge_admm + sub_b * r.n_substates
+    return total, {"fixed": fixed, "per_admm": per_admm, "nnz_L": nnz_l, "per_contact_row": row_b,
+                   "per_contact_admm": admm_b, "per_substate": sub_b}
 
 
 def measured_traffic(workload_name, batch):
@@ -103,7 +119,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1024, help="problems per GPU")
-    ap.add_argument("--config", default="B")
+    ap.add_argument("--config", default="C")
     ap.add_argument("--cpu-problems", type=int, default=256)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -165,10 +181,8 @@ def main():
     if rank == 0:
         value = iters_total * args.steps / elapsed
         achieved = bytes_local / (kms * 1e-3) / 1e9
-        workload_name = (f"config {args.config}: 7-DoF PR2 arm x {wl.n_steps} waypoints, JointVel + "
-                         f"{wl.desc.n_cart} CartPose ABS costs, batch {args.batch} per GPU "
-                         "(BasicTrustRegionSQP + OSQP-semantics ADMM/polish)")
-        traffic, traffic_src = measured_traffic(workload_name, args.batch)
+        wname = workload_name(wl, args.config, args.batch)
+        traffic, traffic_src = measured_traffic(wname, args.batch)
         out = {
             "metric": "SQP iters/sec + achieved HBM GB/s, 7-DoF x 30-wpt x 1024-batch",
             "value": value,
@@ -183,7 +197,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (splitmix64 seeds 20261015+b, PR2 right arm; SURVEY.md §8d)",
             "config": {
-                "workload": workload_name,
+                "workload": wname,
                 "batch_per_gpu": args.batch,
                 "global_batch": args.batch * world,
                 "sqp_iters_per_step": iters_total,

@@ -213,6 +213,10 @@ typedef struct thip_result {
   int n_costs;
   int n_cnts;
   int flags;          /* THIP_FLAG_* */
+  /* collision work counters (bench roofline model) */
+  long long n_contact_rows;  /* sum over linearisations of the hinge rows built */
+  long long n_hinge_admm;    /* sum over QP solves of hinge rows x ADMM iterations */
+  long long n_substates;     /* LVS sub-state passes over the scene (all contact scans) */
 } thip_result;
 
 /* thip_result.flags */

@@ -160,6 +160,53 @@ def test_sqp_parity(oracle_mod, cfg, B):
     check_parity(wl, oracle_mod, x, res, tr, label=cfg)
 
 
+# ------------------------------------------------------------------ collision (config C)
+def _check_rows(rg, rc, label):
+    assert rg.shape == rc.shape, f"{label}: {len(rg)} contact rows vs {len(rc)}"
+    if len(rc) == 0:
+        return
+    # identity and order: step pair, link, primitive, sphere, sub-state, kept coefficients
+    np.testing.assert_array_equal(rg[:, [0, 1, 2, 3, 4, 7]], rc[:, [0, 1, 2, 3, 4, 7]], err_msg=label)
+    np.testing.assert_allclose(rg[:, 5], rc[:, 5], rtol=0, atol=1e-12, err_msg=label)   # distance
+    np.testing.assert_allclose(rg[:, 6], rc[:, 6], rtol=0, atol=0, err_msg=label)       # cc_time
+    np.testing.assert_allclose(rg[:, 8:], rc[:, 8:], rtol=0, atol=1e-11, err_msg=label)  # gradient row, constant
+
+
+def test_collision_rows_parity(oracle_mod):
+    wl = problems.make_workload("C", 16)
+    xo, _ = oracle_mod.solve(wl, n_threads=16)
+    s = BatchTrustRegionSQP(wl)
+    rows = s.collision_rows(xo)
+    rows_init = s.collision_rows(wl.init)
+    s.close()
+    assert sum(len(r) for r in rows) > 100
+    for b in range(wl.batch):
+        _check_rows(rows[b], oracle_mod.collision_rows(wl, b, xo[b]), f"problem {b} (solution)")
+        _check_rows(rows_init[b], oracle_mod.collision_rows(wl, b, wl.init[b]), f"problem {b} (init)")
+
+
+def test_collision_rows_golden(golden):
+    g = golden("collision_rows_C")
+    wl = problems.make_workload("C", 3)
+    s = BatchTrustRegionSQP(wl)
+    rows = s.collision_rows(g["x"])
+    s.close()
+    for b in range(3):
+        _check_rows(rows[b], g[f"rows{b}"], f"golden problem {b}")
+
+
+def test_sqp_parity_collision(oracle_mod, golden):
+    g = golden("sqp_C")
+    wl = problems.make_workload("C", 3)
+    x, res, _ = solve_gpu(wl)
+    np.testing.assert_array_equal([r.status for r in res], g["status"])
+    assert np.abs(x - g["x"]).max() <= TOL_X
+    wl = problems.make_workload("C", 32)
+    x, res, tr = solve_gpu(wl, trace=2048)
+    assert all(r.flags == 0 for r in res)
+    check_parity(wl, oracle_mod, x, res, tr, label="C")
+
+
 def _variant(name):
     if name == "jointvel_only":
         return _jv(6)

@@ -73,6 +73,7 @@ struct Ctl
   int n_h_prev;
   int coll_overflow;  // set by the last contact scan
   int flags;          // sticky THIP_FLAG_* of the run
+  long long n_contact_rows, n_hinge_admm, n_substates;
 };
 
 struct Ctx
@@ -436,6 +437,7 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
     {
       PCNT[t] = running;
       HCOST[t] = cost;
+      atomicAdd(reinterpret_cast<unsigned long long*>(&c.s->n_substates), static_cast<unsigned long long>(cnt));
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -481,6 +483,7 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
         HP[t] = 0;
     }
     c.s->n_h = acc;
+    c.s->n_contact_rows += acc;
   }
   BSYNC();
   if (c.s->coll_overflow)
@@ -2542,6 +2545,7 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
     c.s->prev_rho = c.s->rho;
     c.s->iter = iters;
     c.s->n_admm += iters;
+    c.s->n_hinge_admm += static_cast<long long>(c.s->n_h) * iters;
   }
   BSYNC();
   if (c.s->trace)
@@ -2606,6 +2610,7 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
     c.s->n_h_prev = -1;
     c.s->flags = 0;
     c.s->coll_overflow = 0;
+    c.s->n_contact_rows = c.s->n_hinge_admm = c.s->n_substates = 0;
   }
   BSYNC();
   int* mask = c.ia(I_MASK);
@@ -2931,6 +2936,9 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
     r.n_costs = L.n_costs;
     r.n_cnts = L.n_cnts;
     r.flags = ctl.flags;
+    r.n_contact_rows = ctl.n_contact_rows;
+    r.n_hinge_admm = ctl.n_hinge_admm;
+    r.n_substates = ctl.n_substates;
     if (ctl.flags & THIP_FLAG_CONTACT_OVERFLOW)
       r.status = THIP_OPT_FAILED;
     args.res[b] = r;
@@ -3017,6 +3025,7 @@ __global__ __launch_bounds__(kBlock) void coll_rows_kernel(KernelArgs args, cons
     ctl.flags = 0;
     ctl.coll_overflow = 0;
     ctl.prof = nullptr;
+    ctl.n_contact_rows = ctl.n_hinge_admm = ctl.n_substates = 0;
   }
   double* XN = c.a(A_XN);
   FOR(i, L.nx) XN[i] = xin[(long long)b * L.nx + i];

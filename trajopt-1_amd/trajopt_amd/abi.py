@@ -140,6 +140,9 @@ class Result(C.Structure):
         ("n_costs", C.c_int),
         ("n_cnts", C.c_int),
         ("flags", C.c_int),
+        ("n_contact_rows", C.c_longlong),
+        ("n_hinge_admm", C.c_longlong),
+        ("n_substates", C.c_longlong),
     ]
 
 
