@@ -140,6 +140,7 @@ struct Layout
   int loff[A_COUNT];
   int lds_scratch;
   int lds_doubles;
+  int lds_budget;  // doubles of dynamic LDS the launch provides (dynamic plan)
   // register-resident ADMM segment (admm_segment): eligible when every
   // waypoint has <= kMaxStepRows CartPose rows and the hot arrays are LDS
   // resident; seg_slots = column/row slots per thread (1 or 2)

@@ -86,6 +86,7 @@ struct Ctx
   double* big;
   Ctl* s;
   double* const* ptab;  // LDS table of array base pointers (LDS-resident or HBM), or null
+  double** ptab_w = nullptr;  // the same table, writable (dynamic residency plan)
   const double* scene = nullptr;  // this problem's primitives [n_prims][16]
   int tid, lane, wave;
   __device__ Ctx(const Layout& l, const Tables& t, const thip_problem_desc* dd, double* ww, int* ii, double* bb,
@@ -2578,6 +2579,57 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
 }
 
 // ======================================================================
+// Dynamic LDS residency plan (collision problems): the QP size changes with
+// the contact count, so after every linearisation the QP-internal arrays are
+// re-placed greedily (same priority order as the host plan, plus the hinge
+// arrays) for the actual sizes.  Only arrays recomputed within the SQP
+// iteration after this point are planned.
+// ======================================================================
+__device__ void plan_lds_dynamic(Ctx& c)
+{
+  if (!c.ptab_w)
+    return;
+  if (c.tid == 0)
+  {
+    const Layout& L = c.L;
+    const long long nx = L.nx, nc = c.nc(), m = c.m(), nh = c.s->n_h, D = L.D;
+    const long long NDD = (long long)L.N * D * D, nab = L.n_abs > 0 ? L.n_abs : 1;
+    const int order[] = { A_LINV, A_CV, A_YV, A_BXW, A_BA, A_MR, A_HC, A_HW, A_HRE, A_DG, A_GS, A_WS, A_FS,
+                          A_BS,   A_XA0, A_XA1, A_Z0, A_Z1, A_Y, A_XT, A_PZ, A_RHO, A_L,  A_U,   A_Q,  A_DX,
+                          A_DY,   A_PD,  A_PO,  A_E,  A_DS, A_RE, A_CPL, A_PB, A_PS, A_PR };
+    long long used = L.lds_scratch;
+    for (int k : order)
+    {
+      long long n;
+      switch (k)
+      {
+        case A_LINV: case A_CPL: n = NDD; break;
+        case A_CV: case A_YV: case A_PD: case A_PO: n = nx; break;
+        case A_MR: n = L.n_rows + nh; break;
+        case A_RE: n = L.n_rows; break;
+        case A_HC: n = nh * 2 * D; break;
+        case A_HW: case A_HRE: n = nh; break;
+        case A_GS: n = nab * D; break;
+        case A_WS: n = nab * 2; break;
+        case A_FS: n = L.n_fixed_rows; break;
+        case A_Z0: case A_Z1: case A_Y: case A_PZ: case A_RHO: case A_L: case A_U: case A_DY: case A_E: n = m; break;
+        case A_PB: case A_PS: case A_PR: n = nc + m; break;
+        default: n = nc; break;
+      }
+      n = (n + 7) / 8 * 8;
+      if (n > 0 && used + n <= L.lds_budget)
+      {
+        c.ptab_w[k] = c.big + used;
+        used += n;
+      }
+      else
+        c.ptab_w[k] = c.w + L.doff[k];
+    }
+  }
+  BSYNC();
+}
+
+// ======================================================================
 // The SQP driver kernel: BasicTrustRegionSQP::optimize per workgroup
 // ======================================================================
 __device__ void sqp_optimize(Ctx& c, Solver& sv)
@@ -2634,6 +2686,8 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
       }
       // convexify
       linearize(c, X);
+      if (L.coll)
+        plan_lds_dynamic(c);
       build_and_scale(c);
       // pattern of A (jacobian drops) vs previous QP setup
       double diff[1] = { 0 };
@@ -2895,6 +2949,7 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
   for (int k = threadIdx.x; k < A_COUNT; k += kBlock)
     ptab[k] = L.loff[k] >= 0 ? dyn + L.loff[k] : wsb + L.doff[k];
   Ctx c(L, args.T, args.desc, wsb, args.iws + (long long)b * L.istride, dyn, &ctl, ptab);
+  c.ptab_w = L.coll ? ptab : nullptr;
   c.scene = args.scene ? args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16 : nullptr;
   Solver sv;
   sv.M = dyn;

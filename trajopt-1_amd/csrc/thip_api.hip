@@ -389,6 +389,18 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
       return THIP_E_INVALID;
     }
     ctx->lds_bytes = static_cast<size_t>(used) * sizeof(double);
+    if (L.coll)
+    {
+      // collision: the kernel re-plans residency for every QP with the
+      // actual contact count (plan_lds_dynamic, same priority order, so
+      // LINV/CV/YV keep their offsets); the launch provides the whole budget
+      for (int k = 0; k < A_COUNT; ++k)
+        if (k != A_LINV && k != A_CV && k != A_YV)
+          L.loff[k] = -1;
+      ctx->lds_bytes = static_cast<size_t>(budget) * sizeof(double);
+      L.lds_doubles = static_cast<int>(budget);
+    }
+    L.lds_budget = static_cast<int>(ctx->lds_bytes / sizeof(double));
   }
 
   auto fail = [&](const std::string& msg) {
