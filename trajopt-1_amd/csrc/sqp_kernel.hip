@@ -3011,6 +3011,15 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(KernelArgs args, cons
     return;
   const Layout& L = args.L;
   Ctx c(L, args.T, args.desc, args.ws + (long long)b * L.dstride, args.iws + (long long)b * L.istride, dyn, &ctl);
+  c.scene = args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16;
+  if (threadIdx.x == 0)
+  {
+    ctl.n_h = 0;
+    ctl.flags = 0;
+    ctl.coll_overflow = 0;
+    ctl.prof = nullptr;
+    ctl.n_contact_rows = ctl.n_hinge_admm = ctl.n_substates = 0;
+  }
   const int D = L.D;
   double* X = c.a(A_XN);
   FOR(i, L.nx) X[i] = xin[(long long)b * L.nx + i];
