@@ -38,3 +38,13 @@ for k, name in [kv for kv in enumerate(BatchTrustRegionSQP.PROFILE_SLOTS) if kv[
     per_admm = v / admm.sum()
     print(f"  {k:2d} {name:<16} {100 * v / tot:6.1f}%   {per_admm:10.0f} cyc/admm-iter   "
           f"{v / qps.sum():12.0f} cyc/qp")
+
+# the slowest problems: per-ADMM breakdown and contact-row load
+print("slowest problems (per-ADMM cycles by phase):")
+nh_avg = np.array([r.n_hinge_admm for r in res], dtype=np.float64) / np.maximum(admm, 1)
+for b in np.argsort(-pf[:, 14])[:4]:
+    parts = "  ".join(f"{BatchTrustRegionSQP.PROFILE_SLOTS[k]}={pf[b, k] / max(admm[b], 1):.0f}"
+                      for k in (0, 1, 3, 5, 6, 8, 9, 10, 11, 15, 16, 17, 18, 19, 20, 21, 22))
+    print(f"  problem {b}: {pf[b, 14] / 100:.0f} us, admm {admm[b]:.0f}, qp {qps[b]:.0f}, sqp {sqp[b]:.0f}, "
+          f"mean hinge rows {nh_avg[b]:.0f}, contact rows {res[b].n_contact_rows}\n    {parts}")
+print(f"mean hinge rows per ADMM iteration (all): {nh_avg.mean():.1f}, max {nh_avg.max():.0f}")

@@ -89,6 +89,10 @@ enum DArr : int
   A_CSCR,    // contact-scan scratch: sphere centers [kWaves][kSubCap][n_spheres][3]
   A_HCOST,   // per step-pair collision cost scratch (N)
   A_HDIST,   // contact distance of each hinge row (h_cap)
+  A_HPK,     // ADMM-segment pack of the hinge rows, field-major [kHPack][n_h] (see admm_segment)
+  A_HCHK,    // hinge chunk table: (first row, end row) int pairs, one double per chunk
+  A_HPART,   // hinge chunk partial sums [n_chunks][16]
+  A_HCT,     // ADMM-segment copy of A_HC, field-major [2D][n_h | 1] (odd stride: no LDS bank conflicts)
   A_COUNT
 };
 
@@ -191,6 +195,8 @@ struct KernelArgs
   long long* prof;
 };
 
+constexpr int kHPack = 14;  // doubles per hinge row in A_HPK
+constexpr int kHChunk = 8;  // hinge rows per gather chunk (rows of one step pair)
 constexpr int kProfSlots = 24;
 
 }  // namespace thip

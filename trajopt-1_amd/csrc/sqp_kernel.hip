@@ -74,6 +74,7 @@ struct Ctl
   int coll_overflow;  // set by the last contact scan
   int flags;          // sticky THIP_FLAG_* of the run
   long long n_contact_rows, n_hinge_admm, n_substates;
+  int hcp[THIP_MAX_STEPS + 1];  // first hinge chunk of each step pair (admm_segment)
 };
 
 struct Ctx
@@ -1200,6 +1201,19 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
 typedef __attribute__((address_space(3))) double lds_f64;
 __device__ __forceinline__ lds_f64* lds(double* p) { return (lds_f64*)p; }
 __device__ __forceinline__ const lds_f64* lds(const double* p) { return (const lds_f64*)p; }
+// HBM-resident arrays as global-address-space pointers: global_* instead of
+// FLAT instructions (a FLAT access also counts against lgkmcnt, so every LDS
+// wait would drain it too)
+typedef __attribute__((address_space(1))) double gbl_f64;
+__device__ __forceinline__ gbl_f64* gbl(double* p) { return (gbl_f64*)p; }
+__device__ __forceinline__ const gbl_f64* gbl(const double* p) { return (const gbl_f64*)p; }
+
+// is p (a generic pointer from the residency plan) inside this workgroup's
+// dynamic LDS?
+__device__ __forceinline__ bool lds_resident(const Ctx& c, const double* p)
+{
+  return p >= c.big && p < c.big + c.L.lds_budget;
+}
 
 // ---- wave-level chain of the block solve ---------------------------------
 // 64-bit DPP move (two 32-bit halves)
@@ -1382,6 +1396,42 @@ __device__ __forceinline__ void twisted_middle(const Ctx& c, const Solver& sv, c
 // inverse, expanded so that the rho^2 and eta_r terms cancel analytically:
 // with polish rho = 1/delta the textbook Sherman-Morrison form subtracts
 // O(1/delta^2) quantities and loses ~12 digits.
+// b + sum over hinge rows h in [h0, h1) of HC[h][k] * mr[h] (a column's
+// share of the hinge rows of one step pair), summed per chunk of kHChunk rows
+// (even and odd rows apart) and the chunk sums added in order: the association of admm_segment's
+// row-parallel gather, so that both paths give identical iterates
+__device__ __forceinline__ double hinge_gather(const double* HC, const double* mr, int stride, int k, int h0, int h1,
+                                               double b)
+{
+  for (int q = h0; q < h1; q += kHChunk)
+  {
+    const int qe = min(q + kHChunk, h1);
+    double s0 = 0, s1 = 0;
+    for (int h = q; h < qe; h += 2)
+    {
+      s0 += HC[h * stride + k] * mr[h];
+      if (h + 1 < qe)
+        s1 += HC[(h + 1) * stride + k] * mr[h + 1];
+    }
+    b += s0 + s1;
+  }
+  return b;
+}
+
+// a hinge row's distance-expression value a_t.x_t + a_t+1.x_t+1 (two
+// independent partial sums, one per waypoint); x points at x_t
+template <typename XP>
+__device__ __forceinline__ double hinge_dot(const double* hc, XP x, int D)
+{
+  double s0 = 0, s1 = 0;
+  for (int k = 0; k < D; ++k)
+  {
+    s0 += hc[k] * x[k];
+    s1 += hc[D + k] * x[D + k];
+  }
+  return s0 + s1;
+}
+
 __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, const double* eta, double* out)
 {
   long long* pf = (c.tid == 0) ? c.s->prof : nullptr;
@@ -1437,11 +1487,8 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     {
       const double* HC = c.a(A_HC);
       const int* HP = c.ia(I_HPTR);
-      for (int h = HP[t]; h < HP[t + 1]; ++h)
-        b += HC[h * 2 * D + j] * MR[L.n_rows + h];
-      if (t > 0)
-        for (int h = HP[t - 1]; h < HP[t]; ++h)
-          b += HC[h * 2 * D + D + j] * MR[L.n_rows + h];
+      b = hinge_gather(HC, MR + L.n_rows, 2 * D, j, HP[t], HP[t + 1], b);
+      b = hinge_gather(HC, MR + L.n_rows, 2 * D, D + j, t > 0 ? HP[t - 1] : HP[t], HP[t], b);
     }
     BX[col] = b;
   }
@@ -1504,10 +1551,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   FOR(h, nh)
   {
     const int t = c.ia(I_HT)[h];
-    const double* HC = c.a(A_HC) + h * 2 * D;
-    double g = 0;
-    for (int k = 0; k < 2 * D; ++k)
-      g += HC[k] * lds(CV)[t * D + k];
+    const double g = hinge_dot(c.a(A_HC) + h * 2 * D, lds(CV) + t * D, D);
     const int col = L.nc_base + h;
     const double rr = rho_k(c, L.m_base + 2 * h, polish, delta);
     const double dn = DG[col], w = c.a(A_HW)[h];
@@ -1553,10 +1597,7 @@ __device__ __forceinline__ double row_ax(const Ctx& c, int r, const double* x)
   }
   // hinge row: a_t.x_t + a_t+1.x_t+1 + w h
   const int t = c.ia(I_HT)[h];
-  const double* HC = c.a(A_HC) + h * 2 * D;
-  double v = 0;
-  for (int k = 0; k < 2 * D; ++k)
-    v += HC[k] * x[t * D + k];
+  double v = hinge_dot(c.a(A_HC) + h * 2 * D, x + t * D, D);
   v += c.a(A_HW)[h] * x[L.nc_base + h];
   return v;
 }
@@ -1900,13 +1941,189 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   double *XA = c.a(A_XA0), *Z = c.a(A_Z0), *Y = c.a(A_Y), *DX = c.a(A_DX), *DY = c.a(A_DY);
   const double *Q = c.a(A_Q), *BS = c.a(A_BS), *RH = c.a(A_RHO), *Lo = c.a(A_L), *Up = c.a(A_U);
   const double *FS = c.a(A_FS), *GS = c.a(A_GS), *WS = c.a(A_WS), *DG = c.a(A_DG), *LI = c.a(A_LINV);
-  double *MR = c.a(A_MR), *BXW = c.a(A_BXW), *CV = c.a(A_CV), *YV = c.a(A_YV);
+  double *MR = c.a(A_MR), *CV = c.a(A_CV), *YV = c.a(A_YV);
+  // hinge rows (collision, config C): owned by h = tid + kBlock*j, state kept
+  // in the planned arrays (LDS-resident under plan_lds_dynamic)
+  const int nh = c.s->n_h;
+  const int mb = L.m_base, ncb = L.nc_base;
+  const double *HC = c.a(A_HC), *HW = c.a(A_HW);
+  const int *HT = c.ia(I_HT), *HP = c.ia(I_HPTR);
+  double* HPK = c.a(A_HPK);
+#define HP_(f) HPK[(f) * nh + h]
+  // pack fields: 0 z, 1 z_bound, 2 y, 3 y_bound, 4 x (hinge variable), 5 u,
+  // 6 DG, 7 w, 8 bound-row coefficient, 9 q, 10 rn, 11 eta (A -> E scratch),
+  // 12 first x column, 13 1 / (DG + rho w^2).  Both rows of a hinge are
+  // inequalities (u finite, l = -inf; bound row l = 0, u = +inf), so their
+  // rho is the scalar rho (set_rho_vec) and only the finite bounds are kept.
+  const double rho_s = c.s->rho, rho_si = 1.0 / rho_s;
+  for (int h = c.tid; h < nh; h += kBlock)
+  {
+    const int rh = mb + 2 * h, rb = rh + 1, col = ncb + h;
+    HP_(0) = Z[rh];
+    HP_(1) = Z[rb];
+    HP_(2) = Y[rh];
+    HP_(3) = Y[rb];
+    HP_(4) = XA[col];
+    HP_(5) = Up[rh];
+    HP_(6) = DG[col];
+    HP_(7) = HW[h];
+    HP_(8) = BS[col];
+    HP_(9) = Q[col];
+    HP_(12) = static_cast<double>(HT[h] * D);
+    HP_(13) = 1.0 / (DG[col] + rho_s * HW[h] * HW[h]);
+  }
+  // field-major copy of the hinge coefficients (odd stride)
+  const int nhs = nh | 1;
+  double* HCT = c.a(A_HCT);
+  FOR(e, nh * 2 * D)
+  {
+    const int h = e / (2 * D), k = e - h * 2 * D;
+    HCT[k * nhs + h] = HC[e];
+  }
+  // hinge chunk table: chunks of kHChunk rows inside each step pair
+  int* CHK = reinterpret_cast<int*>(c.a(A_HCHK));
+  double* PART = c.a(A_HPART);
+  if (nh > 0)
+  {
+    if (c.tid == 0)
+    {
+      int acc = 0;
+      for (int t = 0; t < N; ++t)
+      {
+        c.s->hcp[t] = acc;
+        acc += (HP[t + 1] - HP[t] + kHChunk - 1) / kHChunk;
+      }
+      c.s->hcp[N] = acc;
+    }
+    BSYNC();
+    for (int t = c.tid; t < N; t += kBlock)
+    {
+      const int h1 = HP[t + 1];
+      int q = c.s->hcp[t];
+      for (int h = HP[t]; h < h1; h += kHChunk, ++q)
+      {
+        CHK[2 * q] = h;
+        CHK[2 * q + 1] = min(h + kHChunk, h1);
+      }
+    }
+  }
+  const int nchk = (nh > 0) ? c.s->hcp[N] : 0;
   if (c.tid == 0)
     c.s->cur = 0;
+  // MR, the chunk table and the chunk sums are LDS-resident (qp_solve checks
+  // it): ds_* instructions.  The pack and HCT are LDS-resident when the QP's
+  // plan has room for them, else in HBM: each hinge phase is instantiated
+  // for both pointer kinds (a generic pointer would make every access a FLAT
+  // instruction, which pays the vector-memory latency even on LDS).
+  lds_f64* const MRl = lds(MR);
+  const lds_f64* const PARTl = lds(static_cast<const double*>(PART));
+  lds_f64* const PARTlw = lds(PART);
+  const int* const CHKc = CHK;
+  const __attribute__((address_space(3))) int* const CHKl = (const __attribute__((address_space(3))) int*)CHKc;
+  const bool pk_l = lds_resident(c, HPK), hct_l = lds_resident(c, HCT);
+  // phase A, hinge rows: multipliers MR_h; rn, eta kept in the pack
+  auto hinge_a = [&](auto PKP) {
+    for (int h = c.tid; h < nh; h += kBlock)
+    {
+      const double dn = PKP[6 * nh + h], w = PKP[7 * nh + h];
+      const double eta = rho_s * PKP[h] - PKP[2 * nh + h];
+      const double rn = (sig * PKP[4 * nh + h] - PKP[9 * nh + h]) +
+                        PKP[8 * nh + h] * (rho_s * PKP[nh + h] - PKP[3 * nh + h]);
+      MRl[nr + h] = (eta * dn - rho_s * w * rn) * PKP[13 * nh + h];
+      PKP[10 * nh + h] = rn;
+      PKP[11 * nh + h] = eta;
+    }
+  };
+  // phase B': hinge-row share of the waypoint rhs, row-parallel: 16 lanes
+  // per chunk, lane k sums HC[h][k] * MR_h over the chunk's rows
+  auto hinge_gather_seg = [&](auto HTP) {
+    const int k = c.tid & 15;
+    if (k < 2 * D)
+#pragma unroll 2
+      for (int q = c.tid >> 4; q < nchk; q += kBlock / 16)
+      {
+        const int h0 = CHKl[2 * q], h1 = CHKl[2 * q + 1];
+        double s0 = 0, s1 = 0;
+#pragma unroll
+        for (int i = 0; i < kHChunk; i += 2)
+        {
+          const int ha = min(h0 + i, h1 - 1), hb = min(h0 + i + 1, h1 - 1);  // in bounds
+          const double aa = HTP[k * nhs + ha], ma = MRl[nr + ha];
+          const double ab = HTP[k * nhs + hb], mb2 = MRl[nr + hb];
+          s0 = (h0 + i < h1) ? s0 + aa * ma : s0;
+          s1 = (h0 + i + 1 < h1) ? s1 + ab * mb2 : s1;
+        }
+        PARTlw[q * 16 + k] = s0 + s1;
+      }
+  };
+  // phase E, hinge rows: hinge variable, z~ = A x~, relaxed z/y/x updates
+  // (admm_row_update with the infinite bound dropped)
+  long long hq = 0, hl[5] = { 0, 0, 0, 0, 0 };
+#define HLAP(k)                               \
+  if (c.tid == 0 && c.s->prof)                \
+  {                                           \
+    const long long tn = clock64();           \
+    if (k > 0)                                \
+      hl[k] += tn - hq;                       \
+    hq = tn;                                  \
+  }
+  auto hinge_e = [&](auto PKP, auto HTP, bool last) {
+    for (int h = c.tid; h < nh; h += kBlock)
+    {
+      HLAP(0);
+      const int t0 = static_cast<int>(PKP[12 * nh + h]);
+      HLAP(1);
+      double g0 = 0, g1 = 0;
+      // clamped indices (always in bounds), masked accumulation: the loads
+      // of all terms are in flight together
+#pragma unroll
+      for (int k = 0; k < THIP_MAX_DOF; ++k)
+      {
+        const int kk = (k < D) ? k : D - 1;
+        const double a0 = HTP[kk * nhs + h], a1 = HTP[(D + kk) * nhs + h];
+        const double x0 = lds(CV)[t0 + kk], x1 = lds(CV)[t0 + D + kk];
+        g0 = (k < D) ? g0 + a0 * x0 : g0;
+        g1 = (k < D) ? g1 + a1 * x1 : g1;
+      }
+      const double g = g0 + g1;
+      HLAP(2);
+      const double w = PKP[7 * nh + h];
+      const double av = (PKP[10 * nh + h] + w * (PKP[11 * nh + h] - rho_s * g)) * PKP[13 * nh + h];
+      const double zh = PKP[h], zth = g + w * av;
+      double zr = rho_si * PKP[2 * nh + h];
+      zr = zr + al * zth;
+      zr = zr + (1.0 - al) * zh;
+      zr = fmin(zr, PKP[5 * nh + h]);
+      const double dyh = rho_s * (al * zth + (1.0 - al) * zh - zr);
+      const double zb = PKP[nh + h], ztb = PKP[8 * nh + h] * av;
+      double zs = rho_si * PKP[3 * nh + h];
+      zs = zs + al * ztb;
+      zs = zs + (1.0 - al) * zb;
+      zs = fmax(zs, 0.0);
+      const double dyb = rho_s * (al * ztb + (1.0 - al) * zb - zs);
+      const double xo = PKP[4 * nh + h];
+      const double xv = al * av + (1.0 - al) * xo;
+      HLAP(3);
+      PKP[h] = zr;
+      PKP[nh + h] = zs;
+      PKP[2 * nh + h] += dyh;
+      PKP[3 * nh + h] += dyb;
+      PKP[4 * nh + h] = xv;
+      if (last)
+      {
+        const int rh = mb + 2 * h;
+        DY[rh] = dyh;
+        DY[rh + 1] = dyb;
+        DX[ncb + h] = xv - xo;
+      }
+      HLAP(4);
+    }
+  };
 
   // ---- column owners: constants + state
   bool cact[CS];
   int ccol[CS], cfr[CS], cnrow[CS], crow[CS][kMaxStepRows];
+  int chp0[CS], chp1[CS], chp2[CS];  // hinge chunks of pair t-1: [chp0, chp1), of pair t: [chp1, chp2)
   double cq[CS], cbs[CS], clb[CS], cub[CS], crb[CS], cfs[CS], clf[CS], cuf[CS], crf[CS];
   double cx[CS], czb[CS], cyb[CS], czf[CS], cyf[CS], cdx[CS], cdyb[CS], cdyf[CS], crbi[CS], crfi[CS];
   double cli[CS][THIP_MAX_DOF], cgs[CS][kMaxStepRows];
@@ -1918,6 +2135,13 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
     cact[u] = (t < N) && (i < D);
     cfr[u] = -1;
     cnrow[u] = 0;
+    chp0[u] = chp1[u] = chp2[u] = 0;
+    if (cact[u] && nh > 0)
+    {
+      chp1[u] = c.s->hcp[t];
+      chp2[u] = c.s->hcp[t + 1];
+      chp0[u] = (t > 0) ? c.s->hcp[t - 1] : chp1[u];
+    }
     if (cact[u])
     {
       const int col = t * D + i, br = nr + col;
@@ -2021,7 +2245,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   // (a global read-modify-write per lap would stall wave 0 inside the loop)
   long long* pf = (c.tid == 0) ? c.s->prof : nullptr;
   long long tq = pf ? clock64() : 0;
-  long long lap8 = 0, lap9 = 0, lap10 = 0, lap11 = 0, lap15 = 0, lap16 = 0;
+  long long lap8 = 0, lap9 = 0, lap10 = 0, lap11 = 0, lap15 = 0, lap16 = 0, lap17 = 0, lap18 = 0;
 #define SEG_LAP(acc)                  \
   if (pf)                             \
   {                                   \
@@ -2044,10 +2268,26 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
         arn[u] = bxn + absn[u] * ebn;
         arp[u] = bxp + absp[u] * ebp;
         const double dn = adn[u], dp = adp[u], wn = awn[u], wp = awp[u], rr = arr[u];
-        MR[c.tid + kBlock * u] = (aeta[u] * dn * dp - rr * (wn * dp * arn[u] + wp * dn * arp[u])) * adeti[u];
+        MRl[c.tid + kBlock * u] = (aeta[u] * dn * dp - rr * (wn * dp * arn[u] + wp * dn * arp[u])) * adeti[u];
       }
+    if (nh > 0)
+    {
+      if (pk_l)
+        hinge_a(lds(HPK));
+      else
+        hinge_a(gbl(HPK));
+    }
     BSYNC();
     SEG_LAP(lap8);
+    if (nh > 0)
+    {
+      if (hct_l)
+        hinge_gather_seg(lds(static_cast<const double*>(HCT)));
+      else
+        hinge_gather_seg(gbl(static_cast<const double*>(HCT)));
+      BSYNC();
+    }
+    SEG_LAP(lap17);
     // B: waypoint right-hand sides, c_t = Linv_t b_t (octet gather in-wave)
 #pragma unroll
     for (int u = 0; u < CS; ++u)
@@ -2065,8 +2305,16 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
 #pragma unroll
         for (int p = 0; p < kMaxStepRows; ++p)
           if (p < cnrow[u])
-            b += cgs[u][p] * MR[crow[u][p]];
-        lds(BXW)[ccol[u]] = b;
+            b += cgs[u][p] * MRl[crow[u][p]];
+        if (nh > 0)
+        {
+          const int j = (c.tid + kBlock * u) & 7;
+          for (int q = chp1[u]; q < chp2[u]; ++q)
+            b += PARTl[q * 16 + j];
+          for (int q = chp0[u]; q < chp1[u]; ++q)
+            b += PARTl[q * 16 + D + j];
+        }
+        lds(YV)[ccol[u]] = b;  // YV is free until the forward chain
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -2075,10 +2323,14 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
         const int i = (c.tid + kBlock * u) & 7;
         const int base = ccol[u] - i;
         double v = 0;
+        // unconditional loads (in the LDS window), masked accumulation: no
+        // per-term branch, so the loads issue together
 #pragma unroll
         for (int k = 0; k < THIP_MAX_DOF; ++k)
-          if (k <= i)
-            v += cli[u][k] * lds(BXW)[base + k];
+        {
+          const double y = lds(YV)[base + k];
+          v = (k <= i) ? v + cli[u][k] * y : v;
+        }
         lds(CV)[ccol[u]] = v;
       }
     }
@@ -2126,8 +2378,10 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
         double g = 0;
 #pragma unroll
         for (int j = 0; j < THIP_MAX_DOF; ++j)
-          if (j < D)
-            g += ags[u][j] * lds(CV)[t * D + j];
+        {
+          const double xv = lds(CV)[t * D + j];
+          g = (j < D) ? g + ags[u][j] * xv : g;
+        }
         const double dn = adn[u], dp = adp[u], wn = awn[u], wp = awp[u], rr = arr[u];
         const double rn = arn[u], rp = arp[u];
         const double deti = adeti[u];
@@ -2147,8 +2401,17 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
         axn[u] = xvn;
         axp[u] = xvp;
       }
-    (void)last;
     SEG_LAP(lap11);
+    if (nh > 0)
+    {
+      if (pk_l && hct_l)
+        hinge_e(lds(HPK), lds(static_cast<const double*>(HCT)), last);
+      else if (pk_l)
+        hinge_e(lds(HPK), gbl(static_cast<const double*>(HCT)), last);
+      else
+        hinge_e(gbl(HPK), gbl(static_cast<const double*>(HCT)), last);
+    }
+    SEG_LAP(lap18);
   }
 #undef SEG_LAP
   if (pf)
@@ -2159,6 +2422,12 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
     pf[11] += lap11;
     pf[15] += lap15;
     pf[16] += lap16;
+    pf[17] += lap17;
+    pf[18] += lap18;
+    pf[19] += hl[1];
+    pf[20] += hl[2];
+    pf[21] += hl[3];
+    pf[22] += hl[4];
   }
   // write back
 #pragma unroll
@@ -2198,6 +2467,16 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       Y[brp] = aybp[u];
       DY[brp] = adybp[u];
     }
+  for (int h = c.tid; h < nh; h += kBlock)
+  {
+    const int rh = mb + 2 * h;
+    Z[rh] = HP_(0);
+    Z[rh + 1] = HP_(1);
+    Y[rh] = HP_(2);
+    Y[rh + 1] = HP_(3);
+    XA[ncb + h] = HP_(4);
+  }
+#undef HP_
   BSYNC();
 }
 
@@ -2444,9 +2723,12 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   int it;
   bool fail = false;
   const int ct = os.check_termination;
+  // the segment addresses MR, the hinge chunk table and chunk sums as LDS
+  const bool seg = L.seg_ok && lds_resident(c, c.a(A_MR)) &&
+                   (c.s->n_h == 0 || (lds_resident(c, c.a(A_HCHK)) && lds_resident(c, c.a(A_HPART))));
   for (it = 1; it <= os.max_iter; ++it)
   {
-    if (L.seg_ok)
+    if (seg)
     {
       // register-resident segment up to the next iteration that checks
       // termination or adapts rho (same iterates as admm_step)
@@ -2594,9 +2876,11 @@ __device__ void plan_lds_dynamic(Ctx& c)
     const Layout& L = c.L;
     const long long nx = L.nx, nc = c.nc(), m = c.m(), nh = c.s->n_h, D = L.D;
     const long long NDD = (long long)L.N * D * D, nab = L.n_abs > 0 ? L.n_abs : 1;
-    const int order[] = { A_LINV, A_CV, A_YV, A_BXW, A_BA, A_MR, A_HC, A_HW, A_HRE, A_DG, A_GS, A_WS, A_FS,
-                          A_BS,   A_XA0, A_XA1, A_Z0, A_Z1, A_Y, A_XT, A_PZ, A_RHO, A_L,  A_U,   A_Q,  A_DX,
-                          A_DY,   A_PD,  A_PO,  A_E,  A_DS, A_RE, A_CPL, A_PB, A_PS, A_PR };
+    // the ADMM segment's working set first (chains, rhs, multipliers, the
+    // hinge-row pack and coefficients), then the rest as in the host plan
+    const int order[] = { A_LINV, A_CV, A_YV, A_MR, A_HPART, A_HCHK, A_HPK, A_HCT, A_HC, A_BXW, A_BA, A_HW, A_HRE, A_DG, A_GS, A_WS,
+                          A_FS,   A_BS, A_XA0, A_XA1, A_Z0, A_Z1, A_Y, A_XT, A_PZ, A_RHO, A_L,  A_U,  A_Q,
+                          A_DX,   A_DY, A_PD,  A_PO,  A_E,  A_DS, A_RE, A_CPL, A_PB, A_PS, A_PR };
     long long used = L.lds_scratch;
     for (int k : order)
     {
@@ -2609,6 +2893,10 @@ __device__ void plan_lds_dynamic(Ctx& c)
         case A_RE: n = L.n_rows; break;
         case A_HC: n = nh * 2 * D; break;
         case A_HW: case A_HRE: n = nh; break;
+        case A_HPK: n = nh * kHPack; break;
+        case A_HCT: n = (nh | 1) * 2 * D; break;
+        case A_HCHK: n = nh / kHChunk + L.N + 1; break;
+        case A_HPART: n = (nh / kHChunk + L.N + 1) * 16; break;
         case A_GS: n = nab * D; break;
         case A_WS: n = nab * 2; break;
         case A_FS: n = L.n_fixed_rows; break;

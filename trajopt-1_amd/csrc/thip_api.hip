@@ -318,6 +318,11 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   sizes[A_CPL] = L.coll ? NDD : 1;
   sizes[A_CSCR] = L.coll ? (long long)kWaves * kSubCap * d.n_spheres * 3 : 1;
   sizes[A_HCOST] = L.N;
+  sizes[A_HPK] = L.coll ? hc * kHPack : 1;
+  const long long nchk_cap = hc / kHChunk + L.N + 1;
+  sizes[A_HCHK] = L.coll ? nchk_cap : 1;
+  sizes[A_HPART] = L.coll ? nchk_cap * 16 : 1;
+  sizes[A_HCT] = L.coll ? 2 * D * (hc + 1) : 1;
   for (int k = 0; k < A_COUNT; ++k)
     if (sizes[k] < 0)
     {
@@ -375,8 +380,8 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
       max_step_rows = std::max(max_step_rows, step_ptr[static_cast<size_t>(t) + 1] - step_ptr[static_cast<size_t>(t)]);
     // one column slot (t, i) and one CartPose row per thread: N <= 32 and
     // n_abs <= 256; larger problems run the generic admm_step()
-    L.seg_ok = (max_step_rows <= kMaxStepRows && L.D <= 8 && L.loff[A_BXW] >= 0 && L.N * 8 <= kBlock &&
-                L.n_abs <= kBlock && !L.coll) ? 1 : 0;
+    // (collision problems: hinge rows are loop-owned inside the segment)
+    L.seg_ok = (max_step_rows <= kMaxStepRows && L.D <= 8 && L.N * 8 <= kBlock && L.n_abs <= kBlock) ? 1 : 0;
     if (const char* e = std::getenv("THIP_NO_SEGMENT"))
       if (e[0] == '1')
         L.seg_ok = 0;
