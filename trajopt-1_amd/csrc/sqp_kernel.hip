@@ -2025,11 +2025,12 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   auto hinge_a = [&](auto PKP) {
     for (int h = c.tid; h < nh; h += kBlock)
     {
-      const double dn = PKP[6 * nh + h], w = PKP[7 * nh + h];
-      const double eta = rho_s * PKP[h] - PKP[2 * nh + h];
-      const double rn = (sig * PKP[4 * nh + h] - PKP[9 * nh + h]) +
-                        PKP[8 * nh + h] * (rho_s * PKP[nh + h] - PKP[3 * nh + h]);
-      MRl[nr + h] = (eta * dn - rho_s * w * rn) * PKP[13 * nh + h];
+      const double zh = PKP[h], zb = PKP[nh + h], yh = PKP[2 * nh + h], yb = PKP[3 * nh + h];
+      const double xa = PKP[4 * nh + h], dn = PKP[6 * nh + h], w = PKP[7 * nh + h], bs = PKP[8 * nh + h];
+      const double q = PKP[9 * nh + h], deni = PKP[13 * nh + h];
+      const double eta = rho_s * zh - yh;
+      const double rn = (sig * xa - q) + bs * (rho_s * zb - yb);
+      MRl[nr + h] = (eta * dn - rho_s * w * rn) * deni;
       PKP[10 * nh + h] = rn;
       PKP[11 * nh + h] = eta;
     }
@@ -2058,21 +2059,15 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   };
   // phase E, hinge rows: hinge variable, z~ = A x~, relaxed z/y/x updates
   // (admm_row_update with the infinite bound dropped)
-  long long hq = 0, hl[5] = { 0, 0, 0, 0, 0 };
-#define HLAP(k)                               \
-  if (c.tid == 0 && c.s->prof)                \
-  {                                           \
-    const long long tn = clock64();           \
-    if (k > 0)                                \
-      hl[k] += tn - hq;                       \
-    hq = tn;                                  \
-  }
   auto hinge_e = [&](auto PKP, auto HTP, bool last) {
     for (int h = c.tid; h < nh; h += kBlock)
     {
-      HLAP(0);
+      // every pack field is read before any store (the stores could alias
+      // them as far as the compiler knows)
       const int t0 = static_cast<int>(PKP[12 * nh + h]);
-      HLAP(1);
+      const double zh = PKP[h], zb = PKP[nh + h], yh = PKP[2 * nh + h], yb = PKP[3 * nh + h];
+      const double xo = PKP[4 * nh + h], uh = PKP[5 * nh + h], w = PKP[7 * nh + h], bs = PKP[8 * nh + h];
+      const double rn = PKP[10 * nh + h], eta = PKP[11 * nh + h], deni = PKP[13 * nh + h];
       double g0 = 0, g1 = 0;
       // clamped indices (always in bounds), masked accumulation: the loads
       // of all terms are in flight together
@@ -2086,28 +2081,24 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
         g1 = (k < D) ? g1 + a1 * x1 : g1;
       }
       const double g = g0 + g1;
-      HLAP(2);
-      const double w = PKP[7 * nh + h];
-      const double av = (PKP[10 * nh + h] + w * (PKP[11 * nh + h] - rho_s * g)) * PKP[13 * nh + h];
-      const double zh = PKP[h], zth = g + w * av;
-      double zr = rho_si * PKP[2 * nh + h];
+      const double av = (rn + w * (eta - rho_s * g)) * deni;
+      const double zth = g + w * av;
+      double zr = rho_si * yh;
       zr = zr + al * zth;
       zr = zr + (1.0 - al) * zh;
-      zr = fmin(zr, PKP[5 * nh + h]);
+      zr = fmin(zr, uh);
       const double dyh = rho_s * (al * zth + (1.0 - al) * zh - zr);
-      const double zb = PKP[nh + h], ztb = PKP[8 * nh + h] * av;
-      double zs = rho_si * PKP[3 * nh + h];
+      const double ztb = bs * av;
+      double zs = rho_si * yb;
       zs = zs + al * ztb;
       zs = zs + (1.0 - al) * zb;
       zs = fmax(zs, 0.0);
       const double dyb = rho_s * (al * ztb + (1.0 - al) * zb - zs);
-      const double xo = PKP[4 * nh + h];
       const double xv = al * av + (1.0 - al) * xo;
-      HLAP(3);
       PKP[h] = zr;
       PKP[nh + h] = zs;
-      PKP[2 * nh + h] += dyh;
-      PKP[3 * nh + h] += dyb;
+      PKP[2 * nh + h] = yh + dyh;
+      PKP[3 * nh + h] = yb + dyb;
       PKP[4 * nh + h] = xv;
       if (last)
       {
@@ -2116,7 +2107,6 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
         DY[rh + 1] = dyb;
         DX[ncb + h] = xv - xo;
       }
-      HLAP(4);
     }
   };
 
@@ -2424,10 +2414,6 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
     pf[16] += lap16;
     pf[17] += lap17;
     pf[18] += lap18;
-    pf[19] += hl[1];
-    pf[20] += hl[2];
-    pf[21] += hl[3];
-    pf[22] += hl[4];
   }
   // write back
 #pragma unroll

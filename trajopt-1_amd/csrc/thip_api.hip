@@ -717,7 +717,6 @@ int thip_debug_trace(thip_ctx* ctx, int capacity)
     hipFree(ctx->d_trace);
   if (ctx->d_trace_n)
     hipFree(ctx->d_trace_n);
-  hipFree(ctx->d_prof);
   ctx->d_trace = nullptr;
   ctx->d_trace_n = nullptr;
   ctx->trace_cap = capacity;
