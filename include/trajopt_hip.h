@@ -49,6 +49,7 @@ extern "C" {
 #define THIP_MAX_CART 64
 #define THIP_MAX_SPHERES 32
 #define THIP_MAX_PRIMS 16
+#define THIP_MAX_JPOS 8
 
 /* error codes */
 #define THIP_OK 0
@@ -176,6 +177,23 @@ typedef struct thip_problem_desc {
   double cart_pos_coeffs[THIP_MAX_CART][3];
   double cart_rot_coeffs[THIP_MAX_CART][3];
 
+  /* JointPosTermInfo (problem_description.cpp:1097-1196), zero tolerances:
+   * is_cnt 0 -> JointPosEqCost (quadratic, trajectory_costs.cpp:28-65),
+   * is_cnt 1 -> JointPosEqConstraint (one EQ row coeff*(x - target) per
+   * (step, joint), trajectory_costs.cpp:137-181).  first/last_step follow the
+   * hatch clamping rules (-1 = last step).  jpos_targets is the default for
+   * every problem; thip_upload_joint_targets sets them per problem.  Nonzero
+   * upper/lower tolerances (the hinge forms JointPosIneqCost/Constraint) are
+   * rejected by thip_create. */
+  int n_jpos;
+  int jpos_is_cnt[THIP_MAX_JPOS];
+  int jpos_first_step[THIP_MAX_JPOS];
+  int jpos_last_step[THIP_MAX_JPOS];
+  double jpos_coeffs[THIP_MAX_JPOS][THIP_MAX_DOF];
+  double jpos_targets[THIP_MAX_JPOS][THIP_MAX_DOF];
+  double jpos_upper_tols[THIP_MAX_JPOS][THIP_MAX_DOF];
+  double jpos_lower_tols[THIP_MAX_JPOS][THIP_MAX_DOF];
+
   /* CollisionTermInfo, LVS_DISCRETE cost (collision_terms.cpp:737-906,1267-1306):
    * robot collision model = spheres rigidly attached to chain links; the scene
    * is per problem (n_prims primitives of 16 doubles each, see THIP_PRIM_*). */
@@ -241,6 +259,11 @@ int thip_set_stream(thip_ctx* ctx, void* stream);
  *   cart_targets [batch][n_cart][12]     target-frame offset poses (may be NULL if n_cart == 0)
  *   scene        [batch][n_prims][16]    primitive records (may be NULL if n_prims == 0)  */
 int thip_upload(thip_ctx* ctx, const double* init_traj, const double* cart_targets, const double* scene);
+
+/* Per-problem JointPos targets [batch][n_jpos][n_dof] (host pointer); without
+ * this call every problem uses desc->jpos_targets.  Replaces the per-problem
+ * JointPosTermInfo::targets of the reference (problem_description.cpp:1061-1095). */
+int thip_upload_joint_targets(thip_ctx* ctx, const double* jpos_targets);
 
 /* Device-to-device variant: pointers are device pointers (e.g. torch tensors). */
 int thip_upload_device(thip_ctx* ctx, const double* d_init_traj, const double* d_cart_targets,

@@ -43,7 +43,7 @@ def lib():
         L = C.CDLL(str(LIB))
         P = C.POINTER
         dp = P(C.c_double)
-        L.oracle_solve_batch.argtypes = [P(abi.ProblemDesc), C.c_int, dp, dp, dp, dp, P(abi.Result), C.c_int]
+        L.oracle_solve_batch.argtypes = [P(abi.ProblemDesc), C.c_int, dp, dp, dp, dp, dp, P(abi.Result), C.c_int]
         L.oracle_solve_batch.restype = C.c_int
         L.oracle_linearize.argtypes = [P(abi.ProblemDesc), C.c_int, dp, dp, dp, dp]
         L.oracle_linearize.restype = C.c_int
@@ -66,6 +66,13 @@ def _dp(a):
     return a.ctypes.data_as(C.POINTER(C.c_double))
 
 
+def _jpos(wl, b=None):
+    jt = getattr(wl, "jpos_targets", None)
+    if jt is None:
+        return None
+    return np.ascontiguousarray(jt if b is None else jt[b], dtype=np.float64)
+
+
 def solve(wl, n_threads=1):
     """BasicTrustRegionSQP::optimize for every problem of the workload.
     Returns (x [B,N,D], list of abi.Result)."""
@@ -74,9 +81,10 @@ def solve(wl, n_threads=1):
     init = np.ascontiguousarray(wl.init, dtype=np.float64)
     tg = np.ascontiguousarray(wl.targets, dtype=np.float64) if wl.targets.size else None
     sc = np.ascontiguousarray(wl.scene, dtype=np.float64) if wl.scene.size else None
+    jt = _jpos(wl)
     x = np.zeros_like(init)
     res = (abi.Result * B)()
-    rc = L.oracle_solve_batch(C.byref(wl.desc), B, _dp(init), _dp(tg), _dp(sc), _dp(x), res, n_threads)
+    rc = L.oracle_solve_batch(C.byref(wl.desc), B, _dp(init), _dp(tg), _dp(sc), _dp(jt), _dp(x), res, n_threads)
     if rc != 0:
         raise RuntimeError("oracle_solve_batch: " + L.oracle_last_error().decode())
     return x, list(res)
@@ -86,8 +94,8 @@ def solve_trace(wl, b, cap=2048):
     """Problem b with its per-QP trace records (see oracle_solve_trace)."""
     L = lib()
     L.oracle_solve_trace.argtypes = [C.POINTER(abi.ProblemDesc), C.POINTER(C.c_double), C.POINTER(C.c_double),
-                                     C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(abi.Result),
-                                     C.POINTER(C.c_double), C.c_int]
+                                     C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                     C.POINTER(abi.Result), C.POINTER(C.c_double), C.c_int]
     L.oracle_solve_trace.restype = C.c_int
     init = np.ascontiguousarray(wl.init[b], dtype=np.float64)
     tg = np.ascontiguousarray(wl.targets[b], dtype=np.float64) if wl.targets.size else None
@@ -95,7 +103,8 @@ def solve_trace(wl, b, cap=2048):
     x = np.zeros_like(init)
     res = abi.Result()
     rec = np.zeros((cap, 10))
-    n = L.oracle_solve_trace(C.byref(wl.desc), _dp(init), _dp(tg), _dp(sc), _dp(x), C.byref(res), _dp(rec), cap)
+    n = L.oracle_solve_trace(C.byref(wl.desc), _dp(init), _dp(tg), _dp(sc), _dp(_jpos(wl, b)), _dp(x), C.byref(res),
+                             _dp(rec), cap)
     if n < 0:
         raise RuntimeError(L.oracle_last_error().decode())
     return x, res, rec[:n]

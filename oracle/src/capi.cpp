@@ -20,10 +20,10 @@ namespace
 thread_local std::string g_err;
 
 void solveOne(const thip_problem_desc* d, const double* init, const double* targets, const double* scene,
-              double* out_x, thip_result* res)
+              const double* jpos_targets, double* out_x, thip_result* res)
 {
   const int N = d->n_steps, D = d->chain.n_dof;
-  TrajProblem tp = constructProblem(*d, init, targets, scene);
+  TrajProblem tp = constructProblem(*d, init, targets, scene, jpos_targets);
   BasicTrustRegionSQP opt(tp.prob);
   opt.getParameters() = toSqpParams(d->sqp);
   opt.initialize(tp.init);
@@ -54,7 +54,8 @@ const char* oracle_last_error() { return g_err.c_str(); }
 
 // BasicTrustRegionSQP::optimize over a batch, problems spread over n_threads.
 int oracle_solve_batch(const thip_problem_desc* d, int batch, const double* init, const double* targets,
-                       const double* scene, double* out_x, thip_result* res, int n_threads)
+                       const double* scene, const double* jpos_targets, double* out_x, thip_result* res,
+                       int n_threads)
 {
   const int N = d->n_steps, D = d->chain.n_dof;
   std::atomic<int> next{ 0 };
@@ -72,7 +73,7 @@ int oracle_solve_batch(const thip_problem_desc* d, int batch, const double* init
         solveOne(d, init + static_cast<std::size_t>(b) * N * D,
                  targets ? targets + static_cast<std::size_t>(b) * d->n_cart * 12 : nullptr,
                  scene ? scene + static_cast<std::size_t>(b) * d->n_prims * 16 : nullptr,
-                 out_x + static_cast<std::size_t>(b) * N * D, res ? res + b : nullptr);
+                 jpos_targets ? jpos_targets + static_cast<std::size_t>(b) * d->n_jpos * D : nullptr, out_x + static_cast<std::size_t>(b) * N * D, res ? res + b : nullptr);
       }
       catch (const std::exception& e)
       {
@@ -139,12 +140,12 @@ int oracle_linearize(const thip_problem_desc* d, int batch, const double* x, con
 // one problem with a per-QP trace: rec[cap][10] =
 // (warm, rho0, iters, status, polish, rho1, prim_res, dual_res, sum|x|, trust_box); returns #records
 int oracle_solve_trace(const thip_problem_desc* d, const double* init, const double* targets, const double* scene,
-                       double* out_x, thip_result* res, double* rec, int cap)
+                       const double* jpos_targets, double* out_x, thip_result* res, double* rec, int cap)
 {
   try
   {
     const int N = d->n_steps, D = d->chain.n_dof;
-    TrajProblem tp = constructProblem(*d, init, targets, scene);
+    TrajProblem tp = constructProblem(*d, init, targets, scene, jpos_targets);
     auto* om = dynamic_cast<OSQPModel*>(tp.prob->getModel().get());
     std::vector<OSQPModel::Trace> tr;
     om->trace = &tr;

@@ -1,6 +1,7 @@
 // ORACLE — test infrastructure only (see sco_expr.hpp header).
 #include "terms.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 #include <string>
@@ -111,7 +112,236 @@ private:
   int first_, last_;
   QuadExpr expr_;
 };
+// ------------------------------------------------------------ JointPos
+// JointPosEqCost / JointPosIneqCost / JointPosEqConstraint / JointPosIneqConstraint
+// (trajopt/src/trajectory_costs.cpp:28-254).  value() sums follow the Eigen
+// expressions' element order only up to rounding (column-major over the
+// [step x joint] block).
+struct JointPosData
+{
+  std::vector<VarVector> rows;
+  DblVec coeffs, targets, upper, lower;
+  int first = 0, last = 0;
+  double diff(const DblVec& x, int i, std::size_t j) const
+  {
+    return rows[static_cast<std::size_t>(i)][j].value(x) - targets[j];
+  }
+  VarVector vars() const
+  {
+    VarVector v;
+    for (auto& r : rows)
+      v.insert(v.end(), r.begin(), r.end());
+    return v;
+  }
+  // expr_ / expr_vec_ of the ctors
+  AffExpr pos(int i, std::size_t j) const
+  {
+    AffExpr p;
+    exprInc(p, exprMult(rows[static_cast<std::size_t>(i)][j], 1));
+    exprDec(p, targets[j]);
+    return p;
+  }
+  AffExprVector ineqExprs() const
+  {
+    AffExprVector out;
+    for (int i = first; i <= last; ++i)
+      for (std::size_t j = 0; j < coeffs.size(); ++j)
+      {
+        const AffExpr p = pos(i, j);
+        AffExpr e;  // (pos - upper_tol) * coeff
+        exprInc(e, p);
+        exprDec(e, upper[j]);
+        exprScale(e, coeffs[j]);
+        out.push_back(e);
+        AffExpr en;  // (lower_tol - pos) * coeff
+        exprInc(en, lower[j]);
+        exprDec(en, p);
+        exprScale(en, coeffs[j]);
+        out.push_back(en);
+      }
+    return out;
+  }
+  // [diff1 | diff2] of the Ineq value(): (d - upper) c and (lower - d) c
+  void ineqValues(const DblVec& x, DblVec& up, DblVec& lo) const
+  {
+    for (std::size_t j = 0; j < coeffs.size(); ++j)
+      for (int i = first; i <= last; ++i)
+      {
+        const double d = diff(x, i, j);
+        up.push_back((d - upper[j]) * coeffs[j]);
+        lo.push_back(((d * -1) + lower[j]) * coeffs[j]);
+      }
+  }
+};
+
+class JointPosEqCost : public Cost
+{
+public:
+  explicit JointPosEqCost(JointPosData d) : Cost("JointPosEq"), d_(std::move(d))
+  {
+    for (int i = d_.first; i <= d_.last; ++i)
+      for (std::size_t j = 0; j < d_.coeffs.size(); ++j)
+        exprInc(expr_, exprMult(exprSquare(d_.pos(i, j)), d_.coeffs[j]));
+  }
+  double value(const DblVec& x) override
+  {
+    double s = 0;
+    for (std::size_t j = 0; j < d_.coeffs.size(); ++j)
+      for (int i = d_.first; i <= d_.last; ++i)
+      {
+        const double dd = d_.diff(x, i, j);
+        s += (dd * dd) * d_.coeffs[j];
+      }
+    return s;
+  }
+  ConvexObjective::Ptr convex(const DblVec&, Model* model) override
+  {
+    auto out = std::make_shared<ConvexObjective>(model);
+    out->addQuadExpr(expr_);
+    return out;
+  }
+  VarVector getVars() override { return d_.vars(); }
+
+private:
+  JointPosData d_;
+  QuadExpr expr_;
+};
+
+class JointPosIneqCost : public Cost
+{
+public:
+  explicit JointPosIneqCost(JointPosData d) : Cost("JointPosIneq"), d_(std::move(d)), exprs_(d_.ineqExprs()) {}
+  double value(const DblVec& x) override
+  {
+    DblVec up, lo;
+    d_.ineqValues(x, up, lo);
+    double s1 = 0, s2 = 0;
+    for (double v : up)
+      s1 += std::max(v, 0.0);
+    for (double v : lo)
+      s2 += std::max(v, 0.0);
+    return s1 + s2;
+  }
+  ConvexObjective::Ptr convex(const DblVec&, Model* model) override
+  {
+    auto out = std::make_shared<ConvexObjective>(model);
+    for (const AffExpr& e : exprs_)
+      out->addHinge(e, 1);
+    return out;
+  }
+  VarVector getVars() override { return d_.vars(); }
+
+private:
+  JointPosData d_;
+  AffExprVector exprs_;
+};
+
+class JointPosEqConstraint : public Constraint
+{
+public:
+  explicit JointPosEqConstraint(JointPosData d) : Constraint("JointPosEq"), d_(std::move(d))
+  {
+    for (int i = d_.first; i <= d_.last; ++i)
+      for (std::size_t j = 0; j < d_.coeffs.size(); ++j)
+        exprs_.push_back(exprMult(d_.pos(i, j), d_.coeffs[j]));
+  }
+  ConstraintType type() override { return EQ; }
+  // quirk (trajectory_costs.cpp:162-171): the value is the *squared* error times coeff
+  DblVec value(const DblVec& x) override
+  {
+    DblVec out;
+    for (std::size_t j = 0; j < d_.coeffs.size(); ++j)
+      for (int i = d_.first; i <= d_.last; ++i)
+      {
+        const double dd = d_.diff(x, i, j);
+        out.push_back((dd * dd) * d_.coeffs[j]);
+      }
+    return out;
+  }
+  ConvexConstraints::Ptr convex(const DblVec&, Model* model) override
+  {
+    auto out = std::make_shared<ConvexConstraints>(model);
+    for (const AffExpr& e : exprs_)
+      out->addEqCnt(e);
+    return out;
+  }
+  VarVector getVars() override { return d_.vars(); }
+
+private:
+  JointPosData d_;
+  AffExprVector exprs_;
+};
+
+class JointPosIneqConstraint : public Constraint
+{
+public:
+  explicit JointPosIneqConstraint(JointPosData d)
+    : Constraint("JointPosIneq"), d_(std::move(d)), exprs_(d_.ineqExprs())
+  {
+  }
+  ConstraintType type() override { return INEQ; }
+  DblVec value(const DblVec& x) override
+  {
+    DblVec up, lo;
+    d_.ineqValues(x, up, lo);
+    up.insert(up.end(), lo.begin(), lo.end());
+    return up;
+  }
+  ConvexConstraints::Ptr convex(const DblVec&, Model* model) override
+  {
+    auto out = std::make_shared<ConvexConstraints>(model);
+    for (const AffExpr& e : exprs_)
+      out->addIneqCnt(e);
+    return out;
+  }
+  VarVector getVars() override { return d_.vars(); }
+
+private:
+  JointPosData d_;
+  AffExprVector exprs_;
+};
 }  // namespace
+
+// JointPosTermInfo::hatch (problem_description.cpp:1097-1196) for term k of the descriptor.
+static void addJointPosTerm(TrajProblem& tp, const std::vector<VarVector>& rows, const thip_problem_desc& d, int k,
+                            const double* targets)
+{
+  const int N = d.n_steps, D = d.chain.n_dof;
+  JointPosData jd;
+  jd.rows = rows;
+  jd.coeffs.assign(d.jpos_coeffs[k], d.jpos_coeffs[k] + D);
+  jd.targets.assign(targets, targets + D);
+  jd.upper.assign(d.jpos_upper_tols[k], d.jpos_upper_tols[k] + D);
+  jd.lower.assign(d.jpos_lower_tols[k], d.jpos_lower_tols[k] + D);
+  int first = d.jpos_first_step[k], last = d.jpos_last_step[k];
+  if (last <= -1)
+    last = N - 1;
+  if ((N - 1) <= first)
+    first = N - 1;
+  if ((N - 1) <= last)
+    last = N - 1;
+  if (last < first)
+    std::swap(first, last);
+  jd.first = first;
+  jd.last = last;
+  bool zero_tols = true;
+  for (int j = 0; j < D; ++j)
+    zero_tols = zero_tols && jd.upper[static_cast<std::size_t>(j)] == 0.0 && jd.lower[static_cast<std::size_t>(j)] == 0.0;
+  if (!d.jpos_is_cnt[k])
+  {
+    if (zero_tols)
+      tp.prob->addCost(std::make_shared<JointPosEqCost>(jd));
+    else
+      tp.prob->addCost(std::make_shared<JointPosIneqCost>(jd));
+  }
+  else
+  {
+    if (zero_tols)
+      tp.prob->addConstraint(std::make_shared<JointPosEqConstraint>(jd));
+    else
+      tp.prob->addConstraint(std::make_shared<JointPosIneqConstraint>(jd));
+  }
+}
 
 // ------------------------------------------------------------ CartPose
 void cartPoseIndices(const thip_problem_desc& d, int term, std::vector<int>& indices, DblVec& coeffs)
@@ -171,8 +401,11 @@ Mat CartPoseCalc::jac(const DblVec& q) const
 
 // ------------------------------------------------------------ construction
 TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj, const double* cart_targets,
-                             const double* scene)
+                             const double* scene, const double* jpos_targets)
 {
+  auto jposTargets = [&](int k) {
+    return jpos_targets ? jpos_targets + static_cast<std::size_t>(k) * d.chain.n_dof : d.jpos_targets[k];
+  };
   TrajProblem tp;
   const int N = d.n_steps, D = d.chain.n_dof;
   tp.n_steps = N;
@@ -242,6 +475,9 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
                                                        rows[static_cast<std::size_t>(d.cart_step[k])], coeffs, ABS,
                                                        "cart_pose_" + std::to_string(k)));
   }
+  for (int k = 0; k < d.n_jpos; ++k)
+    if (!d.jpos_is_cnt[k])
+      addJointPosTerm(tp, rows, d, k, jposTargets(k));
   if (d.coll_enabled && !d.coll_is_cnt)
     addCollisionTerms(tp, rows, d, scene);
   // cnt_infos: CartPose constraints, collision constraint
@@ -254,6 +490,9 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
         [calc](const DblVec& q) { return (*calc)(q); }, [calc](const DblVec& q) { return calc->jac(q); },
         rows[static_cast<std::size_t>(d.cart_step[k])], coeffs, EQ, "cart_pose_cnt_" + std::to_string(k)));
   }
+  for (int k = 0; k < d.n_jpos; ++k)
+    if (d.jpos_is_cnt[k])
+      addJointPosTerm(tp, rows, d, k, jposTargets(k));
   if (d.coll_enabled && d.coll_is_cnt)
     addCollisionTerms(tp, rows, d, scene);
   return tp;

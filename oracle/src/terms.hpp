@@ -4,6 +4,8 @@
 // construction from the lowered descriptor:
 //   JointVelEqCost                  trajopt/src/trajectory_costs.cpp:257-301
 //   JointVelTermInfo::hatch         trajopt/src/problem_description.cpp:1216-1391 (step clamping)
+//   JointPos{Eq,Ineq}{Cost,Constraint} trajopt/src/trajectory_costs.cpp:28-254
+//   JointPosTermInfo::hatch         trajopt/src/problem_description.cpp:1097-1196
 //   CartPoseErrCalculator           trajopt/src/kinematic_terms.cpp:189-266
 //   CartPoseJacCalculator           trajopt/src/kinematic_terms.cpp:289-370
 //   CartPoseTermInfo::hatch         trajopt/src/problem_description.cpp:919-1005
@@ -43,7 +45,8 @@ struct CartPoseCalc
 void cartPoseIndices(const thip_problem_desc& d, int term, std::vector<int>& indices, DblVec& coeffs);
 
 // Build the TrajOptProb of problem b of a batch (ConstructProblem restated).
+// jpos_targets [n_jpos][D] (null: the descriptor's targets)
 TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj, const double* cart_targets,
-                             const double* scene);
+                             const double* scene, const double* jpos_targets = nullptr);
 
 }  // namespace orc

@@ -65,6 +65,9 @@ def _create(lib, desc, batch=4):
         (lambda d: setattr(d.osqp, "max_iter", 0), "OSQP"),
         (lambda d: setattr(d, "coll_enabled", 1), "collision"),
         (lambda d: setattr(d, "n_cart", 65), "cart"),
+        (lambda d: setattr(d, "n_jpos", 9), "n_jpos"),
+        (lambda d: (setattr(d, "n_jpos", 1), d.jpos_upper_tols[0].__setitem__(2, 0.1)), "tolerances"),
+        (lambda d: (setattr(d, "n_jpos", 1), d.jpos_coeffs[0].__setitem__(0, float("nan"))), "finite"),
     ],
 )
 def test_create_rejects_invalid_descriptors(lib, mutate, needle):
@@ -87,6 +90,7 @@ def test_create_rejects_bad_batch(lib):
 def test_calls_on_null_context_fail_cleanly(lib):
     assert lib.thip_sqp_run(None) == -1
     assert lib.thip_upload(None, None, None, None) == -1
+    assert lib.thip_upload_joint_targets(None, None) == -1
     assert lib.thip_download(None, None, None) == -1
     assert lib.thip_last_kernel_ms(None) < 0
     lib.thip_destroy(None)

@@ -247,13 +247,31 @@ def _variant(name):
         wl.desc.osqp.adaptive_rho = 0
         wl.desc.osqp.warm_starting = 0
         return wl
+    if name == "jointpos_goal":
+        return problems.make_workload("J", 32)
+    if name == "jointpos_goal_offset":
+        return problems.make_workload("J", 16, goal_offset=0.05, first_problem=100)
+    if name == "jointpos_far_goal_penalty_limit":
+        return problems.make_workload("J", 8, goal_offset=0.3)
+    if name == "jointpos_with_cartpose":
+        wl = problems.make_workload("A", 8)
+        d = wl.desc
+        d.n_jpos = 1
+        d.jpos_is_cnt[0] = 0
+        d.jpos_first_step[0] = 2
+        d.jpos_last_step[0] = -1
+        for j in range(wl.n_dof):
+            d.jpos_coeffs[0][j] = 0.5
+            d.jpos_targets[0][j] = float(wl.q_ref[0, 4, j])
+        return wl
     if name == "single_problem":
         return problems.make_workload("B", 1, first_problem=5)
     raise KeyError(name)
 
 
 VARIANTS = ["jointvel_only", "short_horizon", "two_fixed_steps", "position_only_cartpose", "admm_iteration_cap",
-            "sqp_iteration_cap", "sqp_iteration_cap_costs_only", "no_scaling", "no_polish", "no_adaptive_rho_no_warm_start", "single_problem"]
+            "sqp_iteration_cap", "sqp_iteration_cap_costs_only", "no_scaling", "no_polish", "no_adaptive_rho_no_warm_start", "single_problem",
+            "jointpos_goal", "jointpos_goal_offset", "jointpos_far_goal_penalty_limit", "jointpos_with_cartpose"]
 
 
 @pytest.mark.parametrize("name", VARIANTS)
@@ -344,3 +362,26 @@ def test_bench_json_line():
     assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and 0 < rf["frac"] == pytest.approx(rf["achieved"] / 8000.0)
     cb = line["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
+
+
+def test_joint_pos_reference_unit(oracle_mod):
+    """joint_costs_unit.cpp:63-150 (equality_jointPos) on the HIP path: the
+    reference's EXPECTs plus parity with the oracle."""
+    wl = problems.make_reference_unit("joint_pos_eq", 4)
+    x, res, tr = solve_gpu(wl, trace=512)
+    for b in range(wl.batch):
+        assert res[b].status == 0
+        assert np.abs(x[b, 0]).max() < 1e-4
+        assert np.abs(x[b, 1:] + 0.1).max() < 0.01
+    check_parity(wl, oracle_mod, x, res, tr, label="joint_pos_eq")
+
+
+def test_joint_pos_per_problem_targets():
+    """thip_upload_joint_targets: problems with different goals in one batch
+    reach their own goals (and the shared-target default is overridden)."""
+    wl = problems.make_workload("J", 8)
+    assert not np.allclose(wl.jpos_targets[0, 0], wl.jpos_targets[1, 0])
+    x, res, _ = solve_gpu(wl)
+    for b in range(wl.batch):
+        assert res[b].status == 0
+        assert np.abs(x[b, -1] - wl.jpos_targets[b, 0]).max() < 1e-4

@@ -84,3 +84,38 @@ def test_sqp_jointvel_only_converges_to_constant(oracle_mod):
         assert res[b].status == 0
         np.testing.assert_allclose(x[b], np.broadcast_to(x[b, 0], x[b].shape), atol=1e-6)
         assert res[b].total_cost < 1e-10
+
+
+def test_joint_pos_reference_units(oracle_mod):
+    """joint_costs_unit.cpp:63-150 (equality_jointPos) and :152-262
+    (inequality_jointPos): the reference's own EXPECTs on the oracle."""
+    from trajopt_amd import problems
+
+    wl = problems.make_reference_unit("joint_pos_eq", 1)
+    x, res = oracle_mod.solve(wl)
+    assert res[0].status == 0
+    assert np.abs(x[0, 0] - 0.0).max() < 1e-4          # cnt_tol
+    assert np.abs(x[0, 1:] - (-0.1)).max() < 0.01      # cost_tol
+    wl = problems.make_reference_unit("joint_pos_ineq", 1)
+    x, res = oracle_mod.solve(wl)
+    assert res[0].status == 0
+    for i in list(range(0, 5)) + list(range(6, 10)):   # the test's two loops skip row 5
+        assert (x[0, i] < 0.2 + 1e-4).all() and (x[0, i] > -0.1 - 1e-4).all()
+
+
+def test_joint_pos_goal_workload(oracle_mod):
+    """Config J (arm_around_table.json's term set without collision): the goal
+    constraint holds at convergence; a goal offset of 0.3 rad hits the
+    squared-violation quirk (trajectory_costs.cpp:162-171) and ends in the
+    penalty limit, as the reference does."""
+    from trajopt_amd import problems
+
+    wl = problems.make_workload("J", 8)
+    x, res = oracle_mod.solve(wl, n_threads=4)
+    for b in range(wl.batch):
+        assert res[b].status == 0
+        assert res[b].max_cnt_viol < wl.desc.sqp.cnt_tolerance
+        assert np.abs(x[b, -1] - wl.jpos_targets[b, 0]).max() < 1e-4
+    wl = problems.make_workload("J", 4, goal_offset=0.3)
+    _, res = oracle_mod.solve(wl, n_threads=4)
+    assert all(r.status == 2 for r in res)

@@ -131,8 +131,9 @@ struct Layout
   int coll;       // collision cost enabled
   int coll_first, coll_last;  // step pairs [coll_first, coll_last)
   int coll_cost0; // cost slot of the first step pair
-  int n_costs;    // JointVel (0/1) + CartPose cost terms
-  int n_cnts;     // CartPose constraint terms
+  int n_costs;    // JointVel (0/1) + CartPose cost terms + JointPos cost terms + collision step pairs
+  int n_cnts;     // CartPose constraint terms + JointPos constraint terms
+  int n_jpos;     // JointPos terms
   int jv_first, jv_last;
   long long dstride;  // doubles per problem
   long long istride;  // ints per problem
@@ -167,6 +168,15 @@ struct Tables
   int* term_nrow;  // rows of each term (n_cart)
   int* term_slot;  // cost index or constraint index of each term (n_cart)
   int* fixed_of_step;  // fixed-step slot of each waypoint or -1 (N)
+  // abs rows of every source (CartPose rows, JointPos constraint rows)
+  int* row_slot;   // merit slot of the row's constraint term, -1 for cost rows (n_abs)
+  int* row_jpos;   // 1: JointPos EQ constraint row (row_term = JointPos term, row_comp = joint) (n_abs)
+  // JointPos terms (hatch-clamped steps, cost or constraint slot)
+  int* jpos_first; // (THIP_MAX_JPOS)
+  int* jpos_last;
+  int* jpos_slot;
+  int* jpos_row0;  // first abs row of a JointPos constraint term
+  int* jpos_nrow;
   // collision model: robot spheres grouped by link in ascending link order
   // (the ContactResultMap key order of the contact scan)
   int n_groups;
@@ -183,6 +193,7 @@ struct KernelArgs
   Tables T;
   const thip_problem_desc* desc;  // device copy
   const double* scene;  // [batch][n_prims][16] (null without collision)
+  const double* jpt;    // JointPos targets [batch][max(n_jpos,1)][D]
   double* ws;
   int* iws;
   thip_result* res;

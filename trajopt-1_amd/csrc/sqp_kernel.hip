@@ -89,6 +89,7 @@ struct Ctx
   double* const* ptab;  // LDS table of array base pointers (LDS-resident or HBM), or null
   double** ptab_w = nullptr;  // the same table, writable (dynamic residency plan)
   const double* scene = nullptr;  // this problem's primitives [n_prims][16]
+  const double* jpt = nullptr;    // this problem's JointPos targets [n_jpos][D]
   int tid, lane, wave;
   __device__ Ctx(const Layout& l, const Tables& t, const thip_problem_desc* dd, double* ww, int* ii, double* bb,
                  Ctl* ss, double* const* pt = nullptr)
@@ -285,6 +286,21 @@ __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
   FOR(row, L.n_abs)
   {
     const int k = c.T.row_term[row];
+    if (c.T.row_jpos[row])
+    {
+      // JointPosEqConstraint row (trajectory_costs.cpp:151-160): exprMult(x_tj - target_j, coeff_j);
+      // constant, so identical at every linearisation; the coefficient is kept even when 0 (no cleanupAff)
+      const int j = c.T.row_comp[row];
+      const double wgt = c.T.row_w[row];
+      for (int p = 0; p < D; ++p)
+        G[row * D + p] = p == j ? 1.0 * wgt : 0.0;
+      if (raw_jac)
+        for (int p = 0; p < D; ++p)
+          raw_jac[row * D + p] = p == j ? 1.0 : 0.0;
+      mask[row] = 1 << j;
+      GC[row] = (-c.jpt[k * D + j]) * wgt;
+      continue;
+    }
     const int t = c.d->cart_step[k];
     const double y = stage[30 * k + 24 + c.T.row_comp[row]];
     double dot = 0;
@@ -575,6 +591,34 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
 }
 
 // ======================================================================
+// JointPos terms at x: JointPosEqCost::value = sum c_j (x_tj - targ_j)^2
+// (trajectory_costs.cpp:54-63); JointPosEqConstraint::value returns
+// c_j (x_tj - targ_j)^2 per (t, j) (squared, :162-171) and the violation is
+// sum |value| (modeling.cpp:151-170).  Costs and violations by slot.
+// ======================================================================
+__device__ void jpos_values(Ctx& c, const double* x, double* costs, double* viols)
+{
+  const Layout& L = c.L;
+  const int D = L.D;
+  for (int k = 0; k < L.n_jpos; ++k)
+  {
+    const int f = c.T.jpos_first[k], n = (c.T.jpos_last[k] - f + 1) * D;
+    const bool cnt = c.d->jpos_is_cnt[k] != 0;
+    double v = 0;
+    FOR(i, n)
+    {
+      const int t = f + i / D, j = i % D;
+      const double dd = x[t * D + j] - c.jpt[k * D + j];
+      const double e = (dd * dd) * c.d->jpos_coeffs[k][j];
+      v += cnt ? fabs(e) : e;
+    }
+    v = block_sum(c, v);
+    if (c.tid == 0)
+      (cnt ? viols : costs)[c.T.jpos_slot[k]] = v;
+  }
+}
+
+// ======================================================================
 // Exact cost values / constraint violations at x (Cost::value,
 // Constraint::violation).  costs[n_costs], viols[n_cnts]
 // ======================================================================
@@ -629,6 +673,7 @@ __device__ void evaluate(Ctx& c, const double* x, double* costs, double* viols)
     }
   }
   BSYNC();
+  jpos_values(c, x, costs, viols);
   if (L.coll)
     coll_scan(c, x, costs, false);
 }
@@ -718,6 +763,16 @@ __device__ void build_and_scale(Ctx& c)
       }
       q = qa;
     }
+    // JointPosEqCost: exprSquare(x - targ) * c -> P diagonal 2c, q -2 targ c (trajectory_costs.cpp:40-51)
+    for (int k = 0; k < L.n_jpos; ++k)
+      if (!c.d->jpos_is_cnt[k] && t >= c.T.jpos_first[k] && t <= c.T.jpos_last[k])
+      {
+        const double cj = c.d->jpos_coeffs[k][j];
+        pd += cj + cj;
+        const double v = (2 * (-c.jpt[k * D + j]) * 1.0) * cj;
+        if (v != 0.)
+          q += v;
+      }
     PD[col] = pd;
     PO[col] = po;
     Q[col] = q;
@@ -727,8 +782,8 @@ __device__ void build_and_scale(Ctx& c)
   FOR(r, L.n_abs)
   {
     const int ca = nx + 2 * r;
-    const int k = c.T.row_term[r];
-    const double qv = c.d->cart_is_cnt[k] ? MU[c.T.term_slot[k]] : 1.0;
+    const int sl = c.T.row_slot[r];
+    const double qv = sl >= 0 ? MU[sl] : 1.0;
     Q[ca] = qv;
     Q[ca + 1] = qv;
     DS[ca] = DS[ca + 1] = 1.0;
@@ -3049,23 +3104,45 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
         if (c.tid == 0 && c.d->jv_enabled)
           mcost[0] = jvm;
         const double *G = c.a(A_G), *GC = c.a(A_GC);
-        FOR(k, L.n_cart)
+        // JointPos: costs are quadratic (model = exact value), constraint
+        // rows are abs rows like CartPose constraint rows (below)
+        for (int k = 0; k < L.n_jpos; ++k)
         {
-          const int r0 = c.T.term_row0[k], nr = c.T.term_nrow[k];
+          if (c.d->jpos_is_cnt[k])
+            continue;
+          const int f = c.T.jpos_first[k], n = (c.T.jpos_last[k] - f + 1) * D;
           double v = 0;
-          if (c.d->cart_is_cnt[k])
+          FOR(i, n)
           {
-            const int t = c.d->cart_step[k];
+            const int t = f + i / D, j = i % D;
+            const double dd = XN[t * D + j] - c.jpt[k * D + j];
+            v += (dd * dd) * c.d->jpos_coeffs[k][j];
+          }
+          v = block_sum(c, v);
+          if (c.tid == 0)
+            mcost[c.T.jpos_slot[k]] = v;
+        }
+        FOR(k, L.n_cart + L.n_jpos)
+        {
+          const bool jp = k >= L.n_cart;
+          const int kk = jp ? k - L.n_cart : k;
+          if (jp && !c.d->jpos_is_cnt[kk])
+            continue;
+          const int r0 = jp ? c.T.jpos_row0[kk] : c.T.term_row0[k], nr = jp ? c.T.jpos_nrow[kk] : c.T.term_nrow[k];
+          double v = 0;
+          if (jp || c.d->cart_is_cnt[k])
+          {
             for (int rr = 0; rr < nr; ++rr)
             {
               const int row = r0 + rr;
+              const int t = c.T.row_step[row];
               double a = GC[row];
               for (int j = 0; j < D; ++j)
                 if (mask[row] & (1 << j))
                   a += G[row * D + j] * XN[t * D + j];
               v += fabs(a);
             }
-            mviol[c.T.term_slot[k]] = v;
+            mviol[jp ? c.T.jpos_slot[kk] : c.T.term_slot[k]] = v;
           }
           else
           {
@@ -3225,6 +3302,7 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
   Ctx c(L, args.T, args.desc, wsb, args.iws + (long long)b * L.istride, dyn, &ctl, ptab);
   c.ptab_w = L.coll ? ptab : nullptr;
   c.scene = args.scene ? args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16 : nullptr;
+  c.jpt = args.jpt + (long long)b * (L.n_jpos > 0 ? L.n_jpos : 1) * L.D;
   Solver sv;
   sv.M = dyn;
   sv.Nb = dyn + L.N * L.D * L.D;
@@ -3286,6 +3364,7 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(KernelArgs args, cons
   const Layout& L = args.L;
   Ctx c(L, args.T, args.desc, args.ws + (long long)b * L.dstride, args.iws + (long long)b * L.istride, dyn, &ctl);
   c.scene = args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16;
+  c.jpt = args.jpt + (long long)b * (L.n_jpos > 0 ? L.n_jpos : 1) * L.D;
   if (threadIdx.x == 0)
   {
     ctl.n_h = 0;
@@ -3357,6 +3436,7 @@ __global__ __launch_bounds__(kBlock) void coll_rows_kernel(KernelArgs args, cons
   Ctx c(L, args.T, args.desc, args.ws + (long long)b * L.dstride, args.iws + (long long)b * L.istride, nullptr,
         &ctl);
   c.scene = args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16;
+  c.jpt = args.jpt + (long long)b * (L.n_jpos > 0 ? L.n_jpos : 1) * L.D;
   if (threadIdx.x == 0)
   {
     ctl.n_h = 0;

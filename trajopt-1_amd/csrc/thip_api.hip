@@ -43,6 +43,7 @@ struct thip_ctx
   double* d_init = nullptr;
   double* d_tgt = nullptr;
   double* d_scene = nullptr;
+  double* d_jpt = nullptr;   // JointPos targets [batch][max(n_jpos,1)][D]
   double* d_x = nullptr;
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -154,6 +155,18 @@ static int validate(const thip_problem_desc* d, std::string& why)
     if (d->cart_source_link[k] <= 0 || d->cart_source_link[k] >= ch.n_links)
       return why = "CartPose source frame must be an active chain link", THIP_E_INVALID;
   }
+  if (d->n_jpos < 0 || d->n_jpos > THIP_MAX_JPOS)
+    return why = "n_jpos out of range", THIP_E_INVALID;
+  for (int k = 0; k < d->n_jpos; ++k)
+    for (int j = 0; j < ch.n_dof; ++j)
+    {
+      if (d->jpos_upper_tols[k][j] != 0.0 || d->jpos_lower_tols[k][j] != 0.0)
+        return why = "JointPos terms with nonzero tolerances (JointPosIneqCost / JointPosIneqConstraint) are not "
+                     "supported yet",
+               THIP_E_INVALID;
+      if (!std::isfinite(d->jpos_coeffs[k][j]) || !std::isfinite(d->jpos_targets[k][j]))
+        return why = "JointPos coeffs / targets must be finite", THIP_E_INVALID;
+    }
   if (d->coll_enabled)
   {
     if (d->coll_is_cnt)
@@ -253,10 +266,54 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
       term_nrow[k] = static_cast<int>(row_term.size()) - term_row0[k];
       term_slot[k] = (pass == 0) ? n_costs++ : n_cnts++;
     }
+  std::vector<int> row_slot, row_jpos(row_term.size(), 0);
+  for (size_t r = 0; r < row_term.size(); ++r)
+    row_slot.push_back(d.cart_is_cnt[row_term[r]] ? term_slot[static_cast<size_t>(row_term[r])] : -1);
+  // JointPosTermInfo::hatch (problem_description.cpp:1097-1196): step clamping; costs are
+  // quadratic (no rows), constraints add one EQ row per (step, joint) after the CartPose
+  // constraint rows (cnt_infos order, JointPosEqConstraint ctor order: step-major)
+  std::vector<int> jpos_first(THIP_MAX_JPOS, 0), jpos_last(THIP_MAX_JPOS, 0), jpos_slot(THIP_MAX_JPOS, 0),
+      jpos_row0(THIP_MAX_JPOS, 0), jpos_nrow(THIP_MAX_JPOS, 0);
+  L.n_jpos = d.n_jpos;
+  for (int k = 0; k < d.n_jpos; ++k)
+  {
+    int f = d.jpos_first_step[k], l = d.jpos_last_step[k];
+    if (l <= -1)
+      l = L.N - 1;
+    if ((L.N - 1) <= f)
+      f = L.N - 1;
+    if ((L.N - 1) <= l)
+      l = L.N - 1;
+    if (l < f)
+      std::swap(f, l);
+    f = std::max(f, 0);
+    jpos_first[static_cast<size_t>(k)] = f;
+    jpos_last[static_cast<size_t>(k)] = l;
+    if (!d.jpos_is_cnt[k])
+      jpos_slot[static_cast<size_t>(k)] = n_costs++;
+  }
+  for (int k = 0; k < d.n_jpos; ++k)
+  {
+    if (!d.jpos_is_cnt[k])
+      continue;
+    jpos_slot[static_cast<size_t>(k)] = n_cnts++;
+    jpos_row0[static_cast<size_t>(k)] = static_cast<int>(row_term.size());
+    for (int t = jpos_first[static_cast<size_t>(k)]; t <= jpos_last[static_cast<size_t>(k)]; ++t)
+      for (int j = 0; j < L.D; ++j)
+      {
+        row_term.push_back(k);
+        row_comp.push_back(j);
+        row_step.push_back(t);
+        row_w.push_back(d.jpos_coeffs[k][j]);
+        row_slot.push_back(jpos_slot[static_cast<size_t>(k)]);
+        row_jpos.push_back(1);
+      }
+    jpos_nrow[static_cast<size_t>(k)] = static_cast<int>(row_term.size()) - jpos_row0[static_cast<size_t>(k)];
+  }
   L.n_abs = static_cast<int>(row_term.size());
   L.n_abs_cost = 0;
   for (int r = 0; r < L.n_abs; ++r)
-    if (!d.cart_is_cnt[row_term[static_cast<size_t>(r)]])
+    if (row_slot[static_cast<size_t>(r)] < 0)
       L.n_abs_cost++;
   // collision: one cost term per step pair after the CartPose costs
   // (cost_infos order; CollisionTermInfo::hatch, problem_description.cpp:1747)
@@ -433,6 +490,10 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   const size_t o_t0 = push(term_row0, THIP_MAX_CART), o_tn = push(term_nrow, THIP_MAX_CART),
                o_ts = push(term_slot, THIP_MAX_CART);
   const size_t o_fs = push(fixed_of_step, static_cast<size_t>(L.N));
+  const size_t o_rsl = push(row_slot, na), o_rjp = push(row_jpos, na);
+  const size_t o_jf = push(jpos_first, THIP_MAX_JPOS), o_jl = push(jpos_last, THIP_MAX_JPOS),
+               o_js = push(jpos_slot, THIP_MAX_JPOS), o_j0 = push(jpos_row0, THIP_MAX_JPOS),
+               o_jn = push(jpos_nrow, THIP_MAX_JPOS);
   // collision model tables: spheres grouped by link, ascending (scan order)
   std::vector<int> grp_link, grp_s0, grp_ns, sph_order, coll_fixed(static_cast<size_t>(L.N), 0);
   if (L.coll)
@@ -477,6 +538,13 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   T.term_nrow = ctx->d_tables + o_tn;
   T.term_slot = ctx->d_tables + o_ts;
   T.fixed_of_step = ctx->d_tables + o_fs;
+  T.row_slot = ctx->d_tables + o_rsl;
+  T.row_jpos = ctx->d_tables + o_rjp;
+  T.jpos_first = ctx->d_tables + o_jf;
+  T.jpos_last = ctx->d_tables + o_jl;
+  T.jpos_slot = ctx->d_tables + o_js;
+  T.jpos_row0 = ctx->d_tables + o_j0;
+  T.jpos_nrow = ctx->d_tables + o_jn;
   T.n_groups = static_cast<int>(grp_link.size());
   T.grp_link = ctx->d_tables + o_gl;
   T.grp_s0 = ctx->d_tables + o_g0;
@@ -491,8 +559,21 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
       (e = hipMalloc(&ctx->d_init, B * static_cast<size_t>(nx) * sizeof(double))) != hipSuccess ||
       (e = hipMalloc(&ctx->d_tgt, B * static_cast<size_t>(std::max(L.n_cart, 1)) * 12 * sizeof(double))) !=
           hipSuccess ||
-      (e = hipMalloc(&ctx->d_x, B * static_cast<size_t>(nx) * sizeof(double))) != hipSuccess)
+      (e = hipMalloc(&ctx->d_x, B * static_cast<size_t>(nx) * sizeof(double))) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_jpt, B * static_cast<size_t>(std::max(L.n_jpos, 1) * L.D) * sizeof(double))) !=
+          hipSuccess)
     return fail(std::string("hipMalloc(workspace): ") + hipGetErrorString(e));
+  {
+    // every problem starts with the descriptor's JointPos targets
+    const size_t per = static_cast<size_t>(std::max(L.n_jpos, 1) * L.D);
+    std::vector<double> jpt(B * per, 0.0);
+    for (size_t b = 0; b < B; ++b)
+      for (int k = 0; k < L.n_jpos; ++k)
+        for (int j = 0; j < L.D; ++j)
+          jpt[b * per + static_cast<size_t>(k * L.D + j)] = d.jpos_targets[k][j];
+    if ((e = hipMemcpy(ctx->d_jpt, jpt.data(), jpt.size() * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+      return fail(std::string("hipMemcpy(jpos targets): ") + hipGetErrorString(e));
+  }
   hipMemset(ctx->d_iws, 0, B * static_cast<size_t>(L.istride) * sizeof(int));
   hipMemset(ctx->d_res, 0, B * sizeof(thip_result));
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
@@ -532,6 +613,7 @@ static KernelArgs make_args(thip_ctx* ctx)
   a.res = ctx->d_res;
   a.batch = ctx->batch;
   a.scene = ctx->d_scene;
+  a.jpt = ctx->d_jpt;
   a.trace = ctx->d_trace;
   a.trace_n = ctx->d_trace_n;
   a.trace_cap = ctx->trace_cap;
@@ -586,6 +668,24 @@ int thip_upload(thip_ctx* ctx, const double* init_traj, const double* cart_targe
   if (rc == THIP_OK)
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return rc;
+}
+
+int thip_upload_joint_targets(thip_ctx* ctx, const double* jpos_targets)
+{
+  if (!ctx)
+    return THIP_E_INVALID;
+  if (ctx->L.n_jpos == 0)
+    return THIP_OK;
+  if (!jpos_targets)
+    return ctx->err = "thip_upload_joint_targets: null targets", THIP_E_INVALID;
+  const size_t n = static_cast<size_t>(ctx->batch) * ctx->L.n_jpos * ctx->L.D;
+  for (size_t i = 0; i < n; ++i)
+    if (!std::isfinite(jpos_targets[i]))
+      return ctx->err = "thip_upload_joint_targets: non-finite target", THIP_E_INVALID;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->d_jpt, jpos_targets, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return THIP_OK;
 }
 
 int thip_upload_device(thip_ctx* ctx, const double* d_init_traj, const double* d_cart_targets, const double* d_scene)
@@ -857,6 +957,7 @@ void thip_destroy(thip_ctx* ctx)
   hipFree(ctx->d_init);
   hipFree(ctx->d_tgt);
   hipFree(ctx->d_scene);
+  hipFree(ctx->d_jpt);
   hipFree(ctx->d_x);
   hipFree(ctx->d_trace);
   hipFree(ctx->d_trace_n);

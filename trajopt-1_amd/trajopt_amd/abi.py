@@ -16,6 +16,7 @@ MAX_STEPS = 64
 MAX_CART = 64
 MAX_SPHERES = 32
 MAX_PRIMS = 16
+MAX_JPOS = 8
 
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_CONTINUOUS, JOINT_PRISMATIC = 0, 1, 2, 3
 PRIM_SPHERE, PRIM_BOX, PRIM_CAPSULE = 0, 1, 2
@@ -106,6 +107,14 @@ class ProblemDesc(C.Structure):
         ("cart_source_offset", _D12 * MAX_CART),
         ("cart_pos_coeffs", _D3 * MAX_CART),
         ("cart_rot_coeffs", _D3 * MAX_CART),
+        ("n_jpos", C.c_int),
+        ("jpos_is_cnt", C.c_int * MAX_JPOS),
+        ("jpos_first_step", C.c_int * MAX_JPOS),
+        ("jpos_last_step", C.c_int * MAX_JPOS),
+        ("jpos_coeffs", (C.c_double * MAX_DOF) * MAX_JPOS),
+        ("jpos_targets", (C.c_double * MAX_DOF) * MAX_JPOS),
+        ("jpos_upper_tols", (C.c_double * MAX_DOF) * MAX_JPOS),
+        ("jpos_lower_tols", (C.c_double * MAX_DOF) * MAX_JPOS),
         ("coll_enabled", C.c_int),
         ("coll_is_cnt", C.c_int),
         ("coll_first_step", C.c_int),
@@ -207,6 +216,8 @@ def _declare(lib):
     lib.thip_set_stream.restype = C.c_int
     lib.thip_upload.argtypes = [vp, dp, dp, dp]
     lib.thip_upload.restype = C.c_int
+    lib.thip_upload_joint_targets.argtypes = [vp, dp]
+    lib.thip_upload_joint_targets.restype = C.c_int
     lib.thip_upload_device.argtypes = [vp, vp, vp, vp]
     lib.thip_upload_device.restype = C.c_int
     lib.thip_sqp_run.argtypes = [vp]

@@ -14,6 +14,17 @@ Configs (BASELINE.json):
      at the last step (target = FK(q_ref(mid-horizon)), a reaching problem).
   B  30 steps, JointVel cost + CartPose ABS costs at t = 1..29 (tracking).
   C  B + 10-primitive scene + LVS-discrete collision cost.
+  J  joint-space planning (arm_around_table.json's term set without the
+     collision cost, trajopt_common/data/config/arm_around_table.json:2-36):
+     10 steps, JointVel cost, a JointPos EQ constraint at the last step with a
+     per-problem goal q_ref(N-1), a JointPos EQ cost (coeff 0.1) on the
+     interior steps toward the joint-range midpoint; the initial trajectory
+     interpolates q_ref(0) -> goal + U(-goal_offset, goal_offset) like
+     planning_unit.cpp's given_traj (which ends at the goal).  With an offset
+     the goal starts violated; the constraint's exact violation is the
+     *squared* error (trajectory_costs.cpp:162-171) while the model's is
+     linear, so the trust region shrinks and the penalty loop runs out in the
+     reference too (OPT_PENALTY_ITERATION_LIMIT).
 """
 from __future__ import annotations
 
@@ -58,6 +69,7 @@ class Workload:
     targets: np.ndarray   # [B, n_cart, 12]
     scene: np.ndarray     # [B, n_prims, 16]
     q_ref: np.ndarray     # [B, N, D]
+    jpos_targets: np.ndarray | None = None  # [B, n_jpos, D]; None: desc.jpos_targets for every problem
 
     @property
     def batch(self):
@@ -73,7 +85,8 @@ class Workload:
 
     def slice(self, lo, hi):
         return Workload(self.name, self.desc, self.init[lo:hi].copy(), self.targets[lo:hi].copy(),
-                        self.scene[lo:hi].copy(), self.q_ref[lo:hi].copy())
+                        self.scene[lo:hi].copy(), self.q_ref[lo:hi].copy(),
+                        None if self.jpos_targets is None else self.jpos_targets[lo:hi].copy())
 
 
 def _ref_path(rng: SplitMix64, lo, hi, types, n_steps):
@@ -124,12 +137,15 @@ def _add_cart(d, k, step, is_cnt):
         d.cart_rot_coeffs[k][i] = 1.0
 
 
-def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int | None = None) -> Workload:
+def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int | None = None,
+                  goal_offset: float = 0.0) -> Workload:
     config = config.upper()
     if config == "A":
         N = n_steps or 10
     elif config in ("B", "C"):
         N = n_steps or 30
+    elif config == "J":
+        N = n_steps or 10
     else:
         raise ValueError(f"unknown config {config}")
     d = base_desc(N)
@@ -139,6 +155,8 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
     if config == "A":
         d.n_cart = 1
         _add_cart(d, 0, N - 1, True)
+    elif config == "J":
+        d.n_cart = 0
     else:
         d.n_cart = N - 1
         for k, t in enumerate(range(1, N)):
@@ -146,6 +164,24 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
     if config == "C":
         from .scene import add_collision_model
         add_collision_model(d)
+    jpos_targets = None
+    if config == "J":
+        q_lo = np.where(types == abi.JOINT_CONTINUOUS, -math.pi, lo)
+        q_hi = np.where(types == abi.JOINT_CONTINUOUS, math.pi, hi)
+        d.n_jpos = 2
+        # term 0: JointPosEqConstraint at the last step (goal, per problem)
+        d.jpos_is_cnt[0] = 1
+        d.jpos_first_step[0] = N - 1
+        d.jpos_last_step[0] = N - 1
+        # term 1: JointPosEqCost on the interior steps toward the range midpoint
+        d.jpos_is_cnt[1] = 0
+        d.jpos_first_step[1] = 1
+        d.jpos_last_step[1] = N - 2
+        for j in range(D):
+            d.jpos_coeffs[0][j] = 1.0
+            d.jpos_coeffs[1][j] = 0.1
+            d.jpos_targets[1][j] = 0.5 * (q_lo[j] + q_hi[j])
+        jpos_targets = np.zeros((batch, 2, D))
 
     init = np.zeros((batch, N, D))
     targets = np.zeros((batch, d.n_cart, 12))
@@ -156,6 +192,10 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
         q_ref = _ref_path(rng, lo, hi, types, N)
         q_refs[b] = q_ref
         start, end = q_ref[0], q_ref[N - 1]
+        if config == "J":
+            end = q_ref[N - 1] + np.array([rng.uniform(-goal_offset, goal_offset) for _ in range(D)])
+            jpos_targets[b, 0] = q_ref[N - 1]
+            jpos_targets[b, 1] = [d.jpos_targets[1][j] for j in range(D)]
         for t in range(N):
             init[b, t] = start + (end - start) * (t / (N - 1))
         for t in range(1, N - 1):
@@ -169,4 +209,47 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
         if config == "C":
             from .scene import make_scene
             scene[b] = make_scene(rng, chain, q_ref, d)
-    return Workload(config, d, init, targets, scene, q_refs)
+    return Workload(config, d, init, targets, scene, q_refs, jpos_targets)
+
+
+def make_reference_unit(name: str, batch: int = 1) -> Workload:
+    """Problems of the reference's own unit tests, replicated `batch` times.
+
+    joint_pos_eq    trajopt/test/joint_costs_unit.cpp:63-150 (equality_jointPos):
+                    10 steps, STATIONARY init at the zero state, JointPos EQ
+                    constraint x_0 = 0 (coeff 10), JointPos EQ cost x_t = -0.1
+                    on every step (coeff 10); no JointVel, no fixed steps.
+    joint_pos_ineq  joint_costs_unit.cpp:152-262 (inequality_jointPos): JointPos
+                    constraint 0 with tolerances [-0.1, 0.2] on all steps, hinge
+                    costs toward +0.5 / -0.5 (tolerance 0.01) on each half.
+    """
+    N = 10
+    d = base_desc(N)
+    D = d.chain.n_dof
+    d.n_fixed = 0
+    d.jv_enabled = 0
+    d.n_cart = 0
+    if name == "joint_pos_eq":
+        d.n_jpos = 2
+        d.jpos_is_cnt[0], d.jpos_first_step[0], d.jpos_last_step[0] = 1, 0, 0
+        d.jpos_is_cnt[1], d.jpos_first_step[1], d.jpos_last_step[1] = 0, 0, N - 1
+        for j in range(D):
+            d.jpos_coeffs[0][j] = 10.0
+            d.jpos_targets[0][j] = 0.0
+            d.jpos_coeffs[1][j] = 10.0
+            d.jpos_targets[1][j] = -0.1
+    elif name == "joint_pos_ineq":
+        d.n_jpos = 3
+        d.jpos_is_cnt[0], d.jpos_first_step[0], d.jpos_last_step[0] = 1, 0, N - 1
+        d.jpos_is_cnt[1], d.jpos_first_step[1], d.jpos_last_step[1] = 0, 0, (N - 1) // 2
+        d.jpos_is_cnt[2], d.jpos_first_step[2], d.jpos_last_step[2] = 0, (N - 1) // 2 + 1, N - 1
+        for j in range(D):
+            for k in range(3):
+                d.jpos_coeffs[k][j] = 1.0
+            d.jpos_lower_tols[0][j], d.jpos_upper_tols[0][j] = -0.1, 0.2
+            d.jpos_targets[1][j], d.jpos_lower_tols[1][j], d.jpos_upper_tols[1][j] = 0.5, -0.01, 0.01
+            d.jpos_targets[2][j], d.jpos_lower_tols[2][j], d.jpos_upper_tols[2][j] = -0.5, -0.01, 0.01
+    else:
+        raise ValueError(f"unknown reference unit {name}")
+    init = np.zeros((batch, N, D))
+    return Workload(name, d, init, np.zeros((batch, 0, 12)), np.zeros((batch, 0, 16)), init.copy())

@@ -49,6 +49,10 @@ class BatchTrustRegionSQP:
                                  _dp(self._scene) if self._scene is not None else None),
             "thip_upload",
         )
+        jt = getattr(wl, "jpos_targets", None)
+        if jt is not None:
+            self._jpt = np.ascontiguousarray(jt, dtype=np.float64)
+            self._check(self.lib.thip_upload_joint_targets(self.ctx, _dp(self._jpt)), "thip_upload_joint_targets")
         self.uploaded = True
 
     def run(self):
