@@ -227,37 +227,34 @@ void contactGradient(const CollisionModel& cm, const double* dofvals, const Cont
 
 namespace
 {
-// One CollisionCost term per step pair (CollisionTermInfo::hatch,
-// problem_description.cpp:1735-1781), LVS_DISCRETE expression evaluator.
-class CollisionPairCost : public Cost
+// The distance expressions of one step pair (CollisionEvaluator::CalcDistExpressions,
+// LVS_DISCRETE evaluator, collision_terms.cpp:463-536) shared by the cost and
+// constraint forms below.
+class CollisionPairCalc
 {
 public:
-  CollisionPairCost(std::shared_ptr<const CollisionModel> cm, VarVector v0, VarVector v1, int type)
+  CollisionPairCalc(std::shared_ptr<const CollisionModel> cm, VarVector v0, VarVector v1, int type)
     : cm_(std::move(cm)), vars0_(std::move(v0)), vars1_(std::move(v1)), type_(type)
   {
   }
 
-  VarVector getVars() override
+  VarVector vars() const
   {
     VarVector v = vars0_;
     v.insert(v.end(), vars1_.begin(), vars1_.end());
     return v;
   }
 
-  // CollisionCost::value (collision_terms.cpp:1287-1306): no buffer
-  double value(const DblVec& x) override
+  std::vector<Contact> collide(const DblVec& x) const
   {
-    const auto contacts = collide(x);
-    double out = 0;
-    for (const auto& c : contacts)
-      out += std::fmax(cm_->margin - c.distance, 0.0) * cm_->coeff;
-    return out;
+    const DblVec q0 = getDblVec(x, vars0_), q1 = getDblVec(x, vars1_);
+    return calcCollisions(*cm_, q0.data(), q1.data(), type_ == kStartFixedEndFree, type_ == kStartFreeEndFixed);
   }
 
-  // CollisionCost::convex (collision_terms.cpp:1267-1284)
-  ConvexObjective::Ptr convex(const DblVec& x, Model* model) override
+  // dist = d + sum scale * g (q - q0) over the free ends, cleanupAff'd
+  AffExprVector exprs(const DblVec& x) const
   {
-    auto out = std::make_shared<ConvexObjective>(model);
+    AffExprVector out;
     const auto contacts = collide(x);
     const DblVec q0 = getDblVec(x, vars0_), q1 = getDblVec(x, vars1_);
     const int D = cm_->chain->n_dof;
@@ -288,32 +285,90 @@ public:
         add_part(vars1_, q1, true);
       else
         add_part(vars0_, q0, false);
-      e = cleanupAff(e);
-      out->addHinge(exprSub(AffExpr(cm_->margin), e), cm_->coeff);
+      out.push_back(cleanupAff(e));
     }
     return out;
   }
 
+  const CollisionModel& model() const { return *cm_; }
+
   static constexpr int kBothFree = 0, kStartFixedEndFree = 1, kStartFreeEndFixed = 2;
 
 private:
-  std::vector<Contact> collide(const DblVec& x) const
-  {
-    const DblVec q0 = getDblVec(x, vars0_), q1 = getDblVec(x, vars1_);
-    return calcCollisions(*cm_, q0.data(), q1.data(), type_ == kStartFixedEndFree, type_ == kStartFreeEndFixed);
-  }
-
   std::shared_ptr<const CollisionModel> cm_;
   VarVector vars0_, vars1_;
   int type_;
+};
+
+// One CollisionCost term per step pair (CollisionTermInfo::hatch,
+// problem_description.cpp:1735-1781).
+class CollisionPairCost : public Cost
+{
+public:
+  explicit CollisionPairCost(CollisionPairCalc calc) : calc_(std::move(calc)) {}
+  VarVector getVars() override { return calc_.vars(); }
+
+  // CollisionCost::value (collision_terms.cpp:1287-1306): no buffer
+  double value(const DblVec& x) override
+  {
+    const auto contacts = calc_.collide(x);
+    const CollisionModel& cm = calc_.model();
+    double out = 0;
+    for (const auto& c : contacts)
+      out += std::fmax(cm.margin - c.distance, 0.0) * cm.coeff;
+    return out;
+  }
+
+  // CollisionCost::convex (collision_terms.cpp:1267-1284): hinge(margin - dist) * coeff
+  ConvexObjective::Ptr convex(const DblVec& x, Model* model) override
+  {
+    auto out = std::make_shared<ConvexObjective>(model);
+    for (const AffExpr& e : calc_.exprs(x))
+      out->addHinge(exprSub(AffExpr(calc_.model().margin), e), calc_.model().coeff);
+    return out;
+  }
+
+private:
+  CollisionPairCalc calc_;
+};
+
+// One CollisionConstraint per step pair (problem_description.cpp:1797-1840,
+// prob.addIneqConstraint).
+class CollisionPairConstraint : public Constraint
+{
+public:
+  explicit CollisionPairConstraint(CollisionPairCalc calc) : calc_(std::move(calc)) {}
+  VarVector getVars() override { return calc_.vars(); }
+  ConstraintType type() override { return INEQ; }
+
+  // CollisionConstraint::value (collision_terms.cpp:1366-1386)
+  DblVec value(const DblVec& x) override
+  {
+    const auto contacts = calc_.collide(x);
+    const CollisionModel& cm = calc_.model();
+    DblVec out;
+    for (const auto& c : contacts)
+      out.push_back(std::fmax(cm.margin - c.distance, 0.0) * cm.coeff);
+    return out;
+  }
+
+  // CollisionConstraint::convex (collision_terms.cpp:1347-1364): ineq exprMult(margin - dist, coeff)
+  ConvexConstraints::Ptr convex(const DblVec& x, Model* model) override
+  {
+    auto out = std::make_shared<ConvexConstraints>(model);
+    for (const AffExpr& e : calc_.exprs(x))
+      out->addIneqCnt(exprMult(exprSub(AffExpr(calc_.model().margin), e), calc_.model().coeff));
+    return out;
+  }
+
+private:
+  CollisionPairCalc calc_;
 };
 }  // namespace
 
 void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, const thip_problem_desc& d,
                        const double* scene)
 {
-  if (d.coll_is_cnt)
-    throw std::runtime_error("collision constraints: not restated (config C uses the LVS-discrete cost)");
   auto cm = std::make_shared<CollisionModel>();
   cm->chain = &d.chain;
   cm->n_spheres = d.n_spheres;
@@ -344,17 +399,26 @@ void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, cons
     const bool cf = fixed(i), nf = fixed(i + 1);
     int type;
     if (!cf && !nf)
-      type = CollisionPairCost::kBothFree;
+      type = CollisionPairCalc::kBothFree;
     else if (cf && nf)
       throw std::runtime_error("Currently two adjacent fixed steps are not supported in collision term.");
     else if (cf)
-      type = CollisionPairCost::kStartFixedEndFree;
+      type = CollisionPairCalc::kStartFixedEndFree;
     else
-      type = CollisionPairCost::kStartFreeEndFixed;
-    auto c = std::make_shared<CollisionPairCost>(cm, rows[static_cast<std::size_t>(i)],
-                                                 rows[static_cast<std::size_t>(i + 1)], type);
-    c->setName("collision_" + std::to_string(i));
-    tp.prob->addCost(c);
+      type = CollisionPairCalc::kStartFreeEndFixed;
+    CollisionPairCalc calc(cm, rows[static_cast<std::size_t>(i)], rows[static_cast<std::size_t>(i + 1)], type);
+    if (d.coll_is_cnt)
+    {
+      auto c = std::make_shared<CollisionPairConstraint>(std::move(calc));
+      c->setName("collision_" + std::to_string(i));
+      tp.prob->addConstraint(c);
+    }
+    else
+    {
+      auto c = std::make_shared<CollisionPairCost>(std::move(calc));
+      c->setName("collision_" + std::to_string(i));
+      tp.prob->addCost(c);
+    }
   }
 }
 

@@ -63,7 +63,7 @@ def _create(lib, desc, batch=4):
         (lambda d: setattr(d, "n_steps", 1), "n_steps"),
         (lambda d: setattr(d, "n_steps", 65), "n_steps"),
         (lambda d: setattr(d.osqp, "max_iter", 0), "OSQP"),
-        (lambda d: setattr(d, "coll_enabled", 1), "collision"),
+        (lambda d: setattr(d, "coll_enabled", 1), "n_spheres"),
         (lambda d: setattr(d, "n_cart", 65), "cart"),
         (lambda d: setattr(d, "n_jpos", 9), "n_jpos"),
         (lambda d: (setattr(d, "n_jpos", 1), d.jpos_upper_tols[0].__setitem__(2, 0.1)), "tolerances"),

@@ -207,6 +207,18 @@ def test_sqp_parity_collision(oracle_mod, golden):
     check_parity(wl, oracle_mod, x, res, tr, label="C")
 
 
+def test_sqp_parity_collision_constraint(oracle_mod):
+    """CollisionConstraint (LVS-discrete, collision_terms.cpp:1308-1386) as a
+    constraint: ineq rows coeff*(margin - dist) inflated by the per-step-pair
+    merit coefficients, violations counted in the penalty loop."""
+    wl = problems.make_workload("C", 32, first_problem=64)
+    wl.desc.coll_is_cnt = 1
+    x, res, tr = solve_gpu(wl, trace=2048)
+    assert all(r.flags == 0 for r in res)
+    assert all(r.n_cnts == wl.n_steps - 1 for r in res)
+    check_parity(wl, oracle_mod, x, res, tr, label="C-cnt")
+
+
 def _variant(name):
     if name == "jointvel_only":
         return _jv(6)

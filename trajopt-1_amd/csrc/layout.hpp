@@ -130,7 +130,8 @@ struct Layout
   int h_cap;      // hinge-row capacity (0 without collision)
   int coll;       // collision cost enabled
   int coll_first, coll_last;  // step pairs [coll_first, coll_last)
-  int coll_cost0; // cost slot of the first step pair
+  int coll_cost0; // cost slot (or, with coll_cnt, constraint slot) of the first step pair
+  int coll_cnt;   // collision term is a constraint (CollisionConstraint, ineq rows inflated by mu)
   int n_costs;    // JointVel (0/1) + CartPose cost terms + JointPos cost terms + collision step pairs
   int n_cnts;     // CartPose constraint terms + JointPos constraint terms
   int n_jpos;     // JointPos terms

@@ -675,7 +675,7 @@ __device__ void evaluate(Ctx& c, const double* x, double* costs, double* viols)
   BSYNC();
   jpos_values(c, x, costs, viols);
   if (L.coll)
-    coll_scan(c, x, costs, false);
+    coll_scan(c, x, L.coll_cnt ? viols : costs, false);
 }
 
 // ======================================================================
@@ -801,12 +801,21 @@ __device__ void build_and_scale(Ctx& c)
   {
     const double* HC0 = c.a(A_HC0);
     double *HC = c.a(A_HC), *HW = c.a(A_HW);
-    FOR(e, nh * 2 * D) HC[e] = -HC0[e];
+    // constraint form (CollisionConstraint::convex + cntsToCosts): row exprMult(margin - dist, coeff) - h <= 0,
+    // objective mu_pair * h (collision_terms.cpp:1347-1364, optimizers.cpp:59-81)
+    if (L.coll_cnt)
+    {
+      const double cf = c.d->coll_coeff;
+      FOR(e, nh * 2 * D) HC[e] = (-HC0[e]) * cf;
+    }
+    else
+      FOR(e, nh * 2 * D) HC[e] = -HC0[e];
+    const int* HTq = c.ia(I_HT);
     FOR(h, nh)
     {
       HW[h] = -1.0;
       const int col = L.nc_base + h;
-      Q[col] = c.d->coll_coeff;
+      Q[col] = L.coll_cnt ? MU[L.coll_cost0 + HTq[h] - L.coll_first] : c.d->coll_coeff;
       DS[col] = 1.0;
       BS[col] = 1.0;
     }
@@ -2680,7 +2689,8 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
     {
       // ineq row viol - h <= 0: l = -inf, u = -(margin - k) (osqp_interface.cpp:213-281)
       lo = -kInf;
-      up = -(c.d->coll_margin - c.a(A_HK)[idx]);
+      up = L.coll_cnt ? -((c.d->coll_margin - c.a(A_HK)[idx]) * c.d->coll_coeff)
+                      : -(c.d->coll_margin - c.a(A_HK)[idx]);
     }
     else
     {
@@ -3163,9 +3173,28 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
           {
             const int t = L.coll_first + k;
             double v = 0;
-            for (int h = HP[t]; h < HP[t + 1]; ++h)
-              v += c.d->coll_coeff * SX[L.nc_base + h];
-            mcost[L.coll_cost0 + k] = v;
+            if (L.coll_cnt)
+            {
+              // ConvexConstraints::violation: sum pospart(aff(x)), aff = exprMult(margin - dist, coeff)
+              const double *HC0 = c.a(A_HC0), *HKv = c.a(A_HK);
+              const int* HMv = c.ia(I_HMASK);
+              const double cf = c.d->coll_coeff;
+              for (int h = HP[t]; h < HP[t + 1]; ++h)
+              {
+                double a = (c.d->coll_margin - HKv[h]) * cf;
+                for (int e = 0; e < 2 * D; ++e)
+                  if (HMv[h] & (1 << e))
+                    a += ((-HC0[h * 2 * D + e]) * cf) * SX[(t + e / D) * D + e % D];
+                v += fmax(a, 0.0);
+              }
+              mviol[L.coll_cost0 + k] = v;
+            }
+            else
+            {
+              for (int h = HP[t]; h < HP[t + 1]; ++h)
+                v += c.d->coll_coeff * SX[L.nc_base + h];
+              mcost[L.coll_cost0 + k] = v;
+            }
           }
         }
         BSYNC();

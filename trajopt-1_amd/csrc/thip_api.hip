@@ -169,8 +169,6 @@ static int validate(const thip_problem_desc* d, std::string& why)
     }
   if (d->coll_enabled)
   {
-    if (d->coll_is_cnt)
-      return why = "collision constraints are not supported (LVS-discrete collision cost only)", THIP_E_INVALID;
     if (d->n_spheres < 1 || d->n_spheres > THIP_MAX_SPHERES)
       return why = "collision: n_spheres out of range", THIP_E_INVALID;
     for (int s = 0; s < d->n_spheres; ++s)
@@ -320,9 +318,12 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   L.coll = d.coll_enabled ? 1 : 0;
   L.coll_first = d.coll_first_step;
   L.coll_last = (d.coll_last_step < 0) ? L.N - 1 : d.coll_last_step;
-  L.coll_cost0 = n_costs;
+  // (constraint form: one ineq constraint term per step pair after the other
+  // constraints, problem_description.cpp:1797-1840 / OptProb eq-then-ineq order)
+  L.coll_cnt = (L.coll && d.coll_is_cnt) ? 1 : 0;
+  L.coll_cost0 = L.coll_cnt ? n_cnts : n_costs;
   if (L.coll)
-    n_costs += L.coll_last - L.coll_first;
+    (L.coll_cnt ? n_cnts : n_costs) += L.coll_last - L.coll_first;
   L.h_cap = L.coll ? kHingeCap : 0;
   L.n_costs = n_costs;
   L.n_cnts = n_cnts;
