@@ -50,6 +50,7 @@ extern "C" {
 #define THIP_MAX_SPHERES 32
 #define THIP_MAX_PRIMS 16
 #define THIP_MAX_JPOS 8
+#define THIP_MAX_CONTACTS 131072
 
 /* error codes */
 #define THIP_OK 0
@@ -212,6 +213,12 @@ typedef struct thip_problem_desc {
   double sphere_center[THIP_MAX_SPHERES][3];  /* in link frame */
   double sphere_radius[THIP_MAX_SPHERES];
   int n_prims;
+  /* hinge-row (contact) capacity per QP; 0 = automatic: the largest possible
+   * contact count (step pairs x 64 LVS sub-states x spheres x primitives),
+   * capped at THIP_MAX_CONTACTS and at what fits a 16 GB share of HBM for the
+   * batch (~800 B per row and problem), at least 2048.  A QP with more
+   * contacts ends the run with OPT_FAILED and THIP_FLAG_CONTACT_OVERFLOW. */
+  int coll_max_contacts;
 
   thip_sqp_params sqp;
   thip_osqp_settings osqp;
@@ -238,7 +245,7 @@ typedef struct thip_result {
 } thip_result;
 
 /* thip_result.flags */
-#define THIP_FLAG_CONTACT_OVERFLOW 1 /* contacts exceeded the hinge-row capacity (or > 64 LVS
+#define THIP_FLAG_CONTACT_OVERFLOW 1 /* contacts exceeded the hinge-row capacity (or > 1024 LVS
                                         sub-states in a step pair): the run is OPT_FAILED */
 
 typedef struct thip_ctx thip_ctx;

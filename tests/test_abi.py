@@ -30,6 +30,19 @@ def test_exports_every_declared_symbol(lib):
         assert hasattr(lib, s)
 
 
+def test_host_library_exports_every_declared_symbol(lib):
+    import re
+
+    from trajopt_amd import host
+
+    hdr = (abi.PKG_DIR.parent / "include" / "trajopt_host.h").read_text()
+    declared = sorted(set(re.findall(r"\b(thost_[a-z_]+)\s*\(", hdr)))
+    assert len(declared) >= 2
+    out = subprocess.run(["nm", "-D", "--defined-only", str(host.HOST_LIB)], capture_output=True, text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    assert not [s for s in declared if s not in exported]
+
+
 def test_struct_layout_and_build_info(lib):
     assert lib.thip_sizeof_desc() == C.sizeof(abi.ProblemDesc)
     info = lib.thip_build_info().decode()

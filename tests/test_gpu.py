@@ -392,8 +392,89 @@ def test_joint_pos_per_problem_targets():
     """thip_upload_joint_targets: problems with different goals in one batch
     reach their own goals (and the shared-target default is overridden)."""
     wl = problems.make_workload("J", 8)
-    assert not np.allclose(wl.jpos_targets[0, 0], wl.jpos_targets[1, 0])
+    assert not np.allclose(wl.jpos_targets[0, 1], wl.jpos_targets[1, 1])
     x, res, _ = solve_gpu(wl)
     for b in range(wl.batch):
         assert res[b].status == 0
-        assert np.abs(x[b, -1] - wl.jpos_targets[b, 0]).max() < 1e-4
+        assert np.abs(x[b, -1] - wl.jpos_targets[b, 1]).max() < 1e-4
+
+
+# ------------------------------------------------------------------ C++ front door
+def _lowered_workload(texts, scenes=None):
+    """Workload built from the C++ front door's lowering of JSON problems (the
+    oracle then solves exactly what the HIP path was given)."""
+    from trajopt_amd import host
+
+    parts = [host.lower_json(t, None if scenes is None else scenes[b]) for b, t in enumerate(texts)]
+    desc = parts[0][0]
+    init = np.stack([p[1] for p in parts])
+    tgt = np.stack([p[2] for p in parts])
+    jpt = np.stack([p[3] for p in parts]) if desc.n_jpos else None
+    sc = np.zeros((len(texts), 0, 16)) if scenes is None else np.asarray(scenes)
+    return problems.Workload("json", desc, init, tgt, sc, init.copy(), jpt)
+
+
+@pytest.mark.parametrize("cfg,B", [("J", 16), ("A", 8), ("C", 4)])
+def test_frontdoor_json_batch_parity(oracle_mod, cfg, B):
+    """JSON problems -> C++ ProblemConstructionInfo/ConstructProblem ->
+    BatchTrustRegionSQP (C++) -> HIP kernel, against the oracle on the same
+    lowered problems."""
+    from trajopt_amd import host
+
+    wl0 = problems.make_workload(cfg, B)
+    texts = [host.workload_to_json(wl0, b) for b in range(B)]
+    scenes = wl0.scene if wl0.scene.size else None
+    x, res = host.solve_json_batch(texts, scenes)
+    wl = _lowered_workload(texts, scenes)
+    check_parity(wl, oracle_mod, x, res, label=f"json-{cfg}")
+
+
+def test_frontdoor_reference_planning_config(oracle_mod):
+    """The reference's arm_around_table.json (tests/golden/json) with the
+    LVS_DISCRETE evaluator and a box standing in for the table mesh (parity
+    with the oracle; contact values are not pinned against Bullet)."""
+    import json
+    from pathlib import Path
+
+    from trajopt_amd import host
+
+    doc = json.loads((Path(__file__).resolve().parent / "golden" / "json" / "arm_around_table.json").read_text())
+    doc["costs"][1]["params"]["evaluator_type"] = 2
+    text = json.dumps(doc)
+    table = np.zeros(16)
+    table[0] = abi.PRIM_BOX
+    table[1:4] = [1.11, 0.0, 0.635]  # table_joint origin (world = base_footprint, like the FK poses)
+    table[4:13] = np.eye(3).reshape(9)
+    table[13:16] = [0.35, 0.6, 0.03]
+    scenes = np.stack([table[None, :]] * 4)
+    x, res = host.solve_json_batch([text] * 4, scenes)
+    assert len({r.status for r in res}) == 1
+    np.testing.assert_array_equal(x[0], x[3])  # identical problems, identical answers
+    wl = _lowered_workload([text] * 4, scenes)
+    check_parity(wl, oracle_mod, x, res, label="arm_around_table")
+
+
+def test_frontdoor_cli(tmp_path):
+    from trajopt_amd import host
+
+    wl = problems.make_workload("J", 2)
+    files = []
+    for b in range(2):
+        f = tmp_path / f"p{b}.json"
+        f.write_text(host.workload_to_json(wl, b))
+        files.append(str(f))
+    exe = abi.LIB_DIR / "trajopt_batch"
+    p = subprocess.run([str(exe), "--repeat", "3", *files], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.count("OPT_CONVERGED") == 6
+
+
+def test_contact_capacity_overflow_fails_loudly():
+    """A QP with more contacts than coll_max_contacts ends the run with
+    OPT_FAILED and THIP_FLAG_CONTACT_OVERFLOW; contacts are never dropped."""
+    wl = problems.make_workload("C", 8)
+    wl.desc.coll_max_contacts = 4
+    _, res, _ = solve_gpu(wl)
+    over = [r for r in res if r.flags & 1]
+    assert over, "expected at least one problem over 4 contacts"
+    assert all(r.status == 4 for r in over)

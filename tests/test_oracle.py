@@ -115,7 +115,7 @@ def test_joint_pos_goal_workload(oracle_mod):
     for b in range(wl.batch):
         assert res[b].status == 0
         assert res[b].max_cnt_viol < wl.desc.sqp.cnt_tolerance
-        assert np.abs(x[b, -1] - wl.jpos_targets[b, 0]).max() < 1e-4
+        assert np.abs(x[b, -1] - wl.jpos_targets[b, 1]).max() < 1e-4
     wl = problems.make_workload("J", 4, goal_offset=0.3)
     _, res = oracle_mod.solve(wl, n_threads=4)
     assert all(r.status == 2 for r in res)

@@ -19,10 +19,9 @@ constexpr int kWaves = kBlock / 64;
 constexpr long long kLdsBudgetBytes = 152 * 1024;
 // CartPose rows per waypoint the register-resident ADMM segment supports
 constexpr int kMaxStepRows = 8;
-// LVS sub-states per step pair the contact scan supports (one per lane)
-constexpr int kSubCap = 64;
-// hinge rows (contacts) per problem and SQP iteration
-constexpr int kHingeCap = 2048;
+// LVS sub-states per step pair the contact scan supports (sphere-center
+// scratch in HBM; lanes loop over the sub-states)
+constexpr int kSubCap = 1024;
 
 // per-problem double workspace arrays
 enum DArr : int

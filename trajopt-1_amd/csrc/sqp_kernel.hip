@@ -375,11 +375,11 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       continue;
     }
     const bool f0 = coll_fixed_step(c, t), f1 = coll_fixed_step(c, t + 1);
-    if (c.lane < cnt)
+    for (int isub = c.lane; isub < cnt; isub += 64)
     {
       double q[THIP_MAX_DOF];
       for (int j = 0; j < D; ++j)
-        q[j] = linspaced(cnt, q0[j], q1[j], c.lane);
+        q[j] = linspaced(cnt, q0[j], q1[j], isub);
       for (int g = 0; g < c.T.n_groups; ++g)
       {
         Pose T;
@@ -388,7 +388,7 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
         {
           const int s = c.T.sph_order[c.T.grp_s0[g] + e];
           const double* cs = c.d->sphere_center[s];
-          double* dst = SCR + (c.lane * ns + s) * 3;
+          double* dst = SCR + (isub * ns + s) * 3;
           for (int r = 0; r < 3; ++r)
             dst[r] = T.r[r * 3 + 0] * cs[0] + T.r[r * 3 + 1] * cs[1] + T.r[r * 3 + 2] * cs[2] + T.t[r];
         }

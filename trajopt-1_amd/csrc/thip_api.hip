@@ -194,6 +194,8 @@ static int validate(const thip_problem_desc* d, std::string& why)
         return why = "Currently two adjacent fixed steps are not supported in collision term.", THIP_E_INVALID;
     }
   }
+  if (d->coll_enabled && (d->coll_max_contacts < 0 || d->coll_max_contacts > THIP_MAX_CONTACTS))
+    return why = "collision: coll_max_contacts out of range", THIP_E_INVALID;
   if (d->osqp.check_termination < 0 || d->osqp.max_iter < 1 || d->osqp.scaling < 0)
     return why = "bad OSQP settings", THIP_E_INVALID;
   return THIP_OK;
@@ -324,7 +326,20 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   L.coll_cost0 = L.coll_cnt ? n_cnts : n_costs;
   if (L.coll)
     (L.coll_cnt ? n_cnts : n_costs) += L.coll_last - L.coll_first;
-  L.h_cap = L.coll ? kHingeCap : 0;
+  if (L.coll)
+  {
+    // every (sphere, primitive, sub-state) candidate of every step pair is at most one contact
+    const long long bound = static_cast<long long>(L.coll_last - L.coll_first) * 64 * d.n_spheres *
+                            std::max(d.n_prims, 1);
+    // automatic: the bound, within THIP_MAX_CONTACTS and a 16 GB share of HBM for the
+    // hinge-row arrays of the whole batch (~800 B per row and problem), at least 2048
+    const long long by_mem = std::max<long long>(2048, (16LL << 30) / (800LL * batch));
+    L.h_cap = d.coll_max_contacts > 0
+                  ? d.coll_max_contacts
+                  : static_cast<int>(std::min<long long>({ bound, (long long)THIP_MAX_CONTACTS, by_mem }));
+  }
+  else
+    L.h_cap = 0;
   L.n_costs = n_costs;
   L.n_cnts = n_cnts;
   L.nc_base = L.nx + 2 * L.n_abs;

@@ -1,0 +1,109 @@
+// C entry points of the host front door (include/trajopt_host.h).
+#include "trajopt_host.h"
+
+#include <algorithm>
+#include <cstring>
+#include <exception>
+#include <string>
+
+#include "trajopt_amd/batch_sqp.hpp"
+
+namespace
+{
+void setErr(char* err, int err_len, const std::string& msg)
+{
+  if (!err || err_len <= 0)
+    return;
+  const std::size_t n = std::min<std::size_t>(msg.size(), static_cast<std::size_t>(err_len - 1));
+  std::memcpy(err, msg.data(), n);
+  err[n] = '\0';
+}
+
+trajopt::TrajOptProb::Ptr construct(const char* json_text, const double* scene, int n_prims)
+{
+  if (!json_text)
+    throw std::runtime_error("null json text");
+  if (n_prims < 0 || (n_prims > 0 && !scene))
+    throw std::runtime_error("bad scene");
+  auto env = trajopt::Environment::makePR2();
+  for (int p = 0; p < n_prims; ++p)
+  {
+    std::array<double, 16> rec{};
+    std::copy(scene + 16 * p, scene + 16 * (p + 1), rec.begin());
+    env->scene.push_back(rec);
+  }
+  return trajopt::ConstructProblem(Json::parse(json_text), env);
+}
+}  // namespace
+
+extern "C" {
+
+int thost_lower_json(const char* json_text, const double* scene, int n_prims, thip_problem_desc* desc, double* init,
+                     double* cart_targets, double* jpos_targets, char* err, int err_len)
+{
+  try
+  {
+    auto prob = construct(json_text, scene, n_prims);
+    if (desc)
+      *desc = prob->desc();
+    if (init)
+    {
+      double* o = init;
+      for (const auto& row : prob->GetInitTraj())
+        o = std::copy(row.begin(), row.end(), o);
+    }
+    if (cart_targets)
+      std::copy(prob->cart_targets.begin(), prob->cart_targets.end(), cart_targets);
+    if (jpos_targets)
+      std::copy(prob->jpos_targets.begin(), prob->jpos_targets.end(), jpos_targets);
+    setErr(err, err_len, "");
+    return 0;
+  }
+  catch (const std::exception& e)
+  {
+    setErr(err, err_len, e.what());
+    return -1;
+  }
+}
+
+int thost_solve_json_batch(const char* const* json_texts, int batch, const double* scenes, int n_prims, int device,
+                           double* x, thip_result* results, char* err, int err_len)
+{
+  try
+  {
+    if (!json_texts || batch <= 0 || !x)
+      throw std::runtime_error("thost_solve_json_batch: bad arguments");
+    std::vector<trajopt::TrajOptProb::Ptr> probs;
+    for (int b = 0; b < batch; ++b)
+      probs.push_back(construct(json_texts[b], scenes ? scenes + static_cast<std::size_t>(b) * n_prims * 16 : nullptr,
+                                n_prims));
+    trajopt::BatchTrustRegionSQP opt(probs, device);
+    const auto res = opt.optimize();
+    for (int b = 0; b < batch; ++b)
+    {
+      const auto& r = res[static_cast<std::size_t>(b)];
+      std::copy(r.x.begin(), r.x.end(), x + static_cast<std::size_t>(b) * r.x.size());
+      if (results)
+      {
+        thip_result& o = results[b];
+        std::memset(&o, 0, sizeof(o));
+        o.status = static_cast<int>(r.status);
+        o.n_sqp_iters = r.n_sqp_iters;
+        o.n_qp_solves = r.n_qp_solves;
+        o.n_func_evals = r.n_func_evals;
+        o.n_admm_iters = r.n_admm_iters;
+        o.total_cost = r.total_cost;
+        o.max_cnt_viol = r.max_cnt_viol;
+        o.flags = r.flags;
+      }
+    }
+    setErr(err, err_len, "");
+    return 0;
+  }
+  catch (const std::exception& e)
+  {
+    setErr(err, err_len, e.what());
+    return -1;
+  }
+}
+}

@@ -1,0 +1,822 @@
+// Host front door: ProblemConstructionInfo::fromJson, the TermInfo registry,
+// hatch() lowering and ConstructProblem, restating
+// trajopt/src/problem_description.cpp:36-598 (+ the term infos at
+// :843-1005, :1078-1391, :1636-1858) over the C-ABI descriptor.
+#include "trajopt_amd/problem_description.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <iostream>
+#include <stdexcept>
+
+namespace
+{
+bool gRegisteredMakers = false;
+std::map<std::string, trajopt::TermInfo::MakerFunc>& name2maker()
+{
+  static std::map<std::string, trajopt::TermInfo::MakerFunc> m;
+  return m;
+}
+
+// problem_description.cpp:36-54
+void ensure_only_members(const Json::Value& v, const char** fields, int nvalid)
+{
+  for (const auto& name : v.getMemberNames())
+  {
+    bool valid = false;
+    for (int j = 0; j < nvalid; ++j)
+      if (name == fields[j])
+      {
+        valid = true;
+        break;
+      }
+    if (!valid)
+      throw std::runtime_error("invalid field found: " + name);
+  }
+}
+
+// problem_description.cpp:80-95
+void checkParameterSize(trajopt::DblVec& parameter, unsigned expected_size, const std::string& name,
+                        bool apply_first = true)
+{
+  if (apply_first && parameter.size() == 1)
+    parameter = trajopt::DblVec(expected_size, parameter[0]);
+  else if (parameter.size() != expected_size)
+    throw std::runtime_error("wrong number of " + name + ". expected " + std::to_string(expected_size) + " got " +
+                             std::to_string(parameter.size()));
+}
+
+bool doubleEquals(double a, double b) { return std::fabs(a - b) < 1e-5; }  // trajopt_common::doubleEquals
+
+[[noreturn]] void unsupported(const std::string& what)
+{
+  throw std::runtime_error(what + " is not supported on the HIP path");
+}
+
+// A registered maker whose lowering does not exist on the HIP path.
+struct UnsupportedTermInfo : public trajopt::TermInfo
+{
+  std::string type;
+  explicit UnsupportedTermInfo(std::string t)
+    : TermInfo(trajopt::TermType::TT_COST | trajopt::TermType::TT_CNT | trajopt::TermType::TT_USE_TIME)
+    , type(std::move(t))
+  {
+  }
+  void fromJson(trajopt::ProblemConstructionInfo&, const Json::Value&) override {}
+  void hatch(trajopt::TrajOptProb&) override { unsupported("term type '" + type + "'"); }
+};
+template <const char* kName>
+trajopt::TermInfo::Ptr makeUnsupported()
+{
+  return std::make_shared<UnsupportedTermInfo>(kName);
+}
+constexpr char kDynCart[] = "dynamic_cart_pose";
+constexpr char kCartVel[] = "cart_vel";
+constexpr char kJointAcc[] = "joint_acc";
+constexpr char kJointJerk[] = "joint_jerk";
+constexpr char kTotalTime[] = "total_time";
+
+// problem_description.cpp:57-70
+void RegisterMakers()
+{
+  gRegisteredMakers = true;  // first: RegisterMaker() below checks it
+  trajopt::TermInfo::RegisterMaker("dynamic_cart_pose", &makeUnsupported<kDynCart>);
+  trajopt::TermInfo::RegisterMaker("cart_pose", &trajopt::CartPoseTermInfo::create);
+  trajopt::TermInfo::RegisterMaker("cart_vel", &makeUnsupported<kCartVel>);
+  trajopt::TermInfo::RegisterMaker("joint_pos", &trajopt::JointPosTermInfo::create);
+  trajopt::TermInfo::RegisterMaker("joint_vel", &trajopt::JointVelTermInfo::create);
+  trajopt::TermInfo::RegisterMaker("joint_acc", &makeUnsupported<kJointAcc>);
+  trajopt::TermInfo::RegisterMaker("joint_jerk", &makeUnsupported<kJointJerk>);
+  trajopt::TermInfo::RegisterMaker("collision", &trajopt::CollisionTermInfo::create);
+  trajopt::TermInfo::RegisterMaker("total_time", &makeUnsupported<kTotalTime>);
+}
+
+bool iequals(const std::string& a, const std::string& b)
+{
+  if (a.size() != b.size())
+    return false;
+  for (std::size_t i = 0; i < a.size(); ++i)
+    if (std::tolower(static_cast<unsigned char>(a[i])) != std::tolower(static_cast<unsigned char>(b[i])))
+      return false;
+  return true;
+}
+
+using Pose12 = std::array<double, 12>;
+Pose12 poseMul(const Pose12& a, const Pose12& b)
+{
+  Pose12 o{};
+  for (int r = 0; r < 3; ++r)
+  {
+    for (int c = 0; c < 3; ++c)
+      o[r * 4 + c] = a[r * 4 + 0] * b[0 * 4 + c] + a[r * 4 + 1] * b[1 * 4 + c] + a[r * 4 + 2] * b[2 * 4 + c];
+    o[r * 4 + 3] = a[r * 4 + 0] * b[3] + a[r * 4 + 1] * b[7] + a[r * 4 + 2] * b[11] + a[r * 4 + 3];
+  }
+  return o;
+}
+Pose12 poseInv(const Pose12& a)
+{
+  Pose12 o{};
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      o[r * 4 + c] = a[c * 4 + r];
+  for (int r = 0; r < 3; ++r)
+    o[r * 4 + 3] = -(o[r * 4 + 0] * a[3] + o[r * 4 + 1] * a[7] + o[r * 4 + 2] * a[11]);
+  return o;
+}
+
+// Eigen::Quaterniond(w, x, y, z).matrix() (Eigen/src/Geometry/Quaternion.h toRotationMatrix)
+Pose12 poseFromXyzWxyz(const std::array<double, 3>& p, const std::array<double, 4>& q)
+{
+  const double w = q[0], x = q[1], y = q[2], z = q[3];
+  const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+  const double twx = tx * w, twy = ty * w, twz = tz * w;
+  const double txx = tx * x, txy = ty * x, txz = tz * x;
+  const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+  return Pose12{ { 1.0 - (tyy + tzz), txy - twz, txz + twy, p[0],  //
+                   txy + twz, 1.0 - (txx + tzz), tyz - twx, p[1],  //
+                   txz - twy, tyz + twx, 1.0 - (txx + tyy), p[2] } };
+}
+
+void readVec3(const Json::Value& params, const char* name, std::array<double, 3>& out, std::array<double, 3> df)
+{
+  if (!params.isMember(name))
+  {
+    out = df;
+    return;
+  }
+  std::vector<double> v;
+  json_marshal::fromJsonArray(params[name], v, 3);
+  std::copy(v.begin(), v.end(), out.begin());
+}
+void readVec4(const Json::Value& params, const char* name, std::array<double, 4>& out, std::array<double, 4> df)
+{
+  if (!params.isMember(name))
+  {
+    out = df;
+    return;
+  }
+  std::vector<double> v;
+  json_marshal::fromJsonArray(params[name], v, 4);
+  std::copy(v.begin(), v.end(), out.begin());
+}
+
+// Eigen 3.4 LinSpaced(size, low, high)(i), as in collision_device.hpp
+double linspaced(int size, double low, double high, int i)
+{
+  if (size == 1)
+    return high;
+  const int size1 = size - 1;
+  const double step = (high - low) / size1;
+  if (std::fabs(high) < std::fabs(low))
+    return (i == 0) ? low : high - double(size1 - i) * step;
+  return (i == size1) ? high : low + double(i) * step;
+}
+}  // namespace
+
+namespace sco
+{
+std::string toString(OptStatus status)
+{
+  static const char* names[] = { "OPT_CONVERGED",   "OPT_SCO_ITERATION_LIMIT", "OPT_PENALTY_ITERATION_LIMIT",
+                                 "OPT_TIME_LIMIT", "OPT_FAILED",              "INVALID" };
+  const int i = static_cast<int>(status);
+  return (i >= 0 && i <= 5) ? names[i] : "INVALID";
+}
+}  // namespace sco
+
+namespace trajopt
+{
+// ------------------------------------------------------------ kinematics / environment
+int KinematicGroup::linkIndex(const std::string& link) const
+{
+  for (std::size_t k = 0; k < link_names.size(); ++k)
+    if (link_names[k] == link)
+      return static_cast<int>(k);
+  return -1;
+}
+
+bool KinematicGroup::isActiveLinkId(const std::string& link) const
+{
+  const int k = linkIndex(link);
+  if (k < 0)
+    return false;
+  for (int i = 1; i <= k; ++i)
+    if (chain.joint_type[i] != THIP_JOINT_FIXED)
+      return true;
+  return false;
+}
+
+std::array<double, 12> KinematicGroup::staticWorldPose(const std::string& link) const
+{
+  const int k = linkIndex(link);
+  if (k >= 0)
+  {
+    for (int i = 1; i <= k; ++i)
+      if (chain.joint_type[i] != THIP_JOINT_FIXED)
+        throw std::runtime_error("staticWorldPose: link " + link + " is active");
+    Pose12 T;
+    std::copy(chain.base_pose, chain.base_pose + 12, T.begin());
+    for (int i = 1; i <= k; ++i)
+    {
+      Pose12 O;
+      std::copy(chain.joint_origin[i], chain.joint_origin[i] + 12, O.begin());
+      T = poseMul(T, O);
+    }
+    return T;
+  }
+  auto it = static_frames.find(link);
+  if (it == static_frames.end())
+    throw std::runtime_error("unknown link " + link);
+  return it->second;
+}
+
+void Environment::addJointGroup(KinematicGroup g)
+{
+  const std::string name = g.name;
+  state_[name] = DblVec(static_cast<std::size_t>(g.chain.n_dof), 0.0);
+  groups_[name] = std::make_shared<const KinematicGroup>(std::move(g));
+}
+
+KinematicGroup::ConstPtr Environment::getJointGroup(const std::string& name) const
+{
+  auto it = groups_.find(name);
+  return it == groups_.end() ? nullptr : it->second;
+}
+
+DblVec Environment::getCurrentJointValues(const std::string& group) const
+{
+  auto it = state_.find(group);
+  if (it == state_.end())
+    throw std::runtime_error("unknown joint group " + group);
+  return it->second;
+}
+
+void Environment::setState(const std::string& group, const DblVec& q)
+{
+  auto g = getJointGroup(group);
+  if (!g || static_cast<int>(q.size()) != g->numJoints())
+    throw std::runtime_error("setState: bad group or joint count");
+  state_[group] = q;
+}
+
+// ------------------------------------------------------------ registry
+void TermInfo::RegisterMaker(const std::string& type, MakerFunc f)
+{
+  if (!gRegisteredMakers)
+    RegisterMakers();
+  name2maker()[type] = f;
+}
+
+TermInfo::Ptr TermInfo::fromName(const std::string& type)
+{
+  if (!gRegisteredMakers)
+    RegisterMakers();
+  auto it = name2maker().find(type);
+  if (it != name2maker().end())
+    return (*it->second)();
+  return {};
+}
+
+// ------------------------------------------------------------ ProblemConstructionInfo
+ProblemConstructionInfo::ProblemConstructionInfo(Environment::ConstPtr e) : env(std::move(e))
+{
+  thip_default_osqp_settings(&osqp);
+}
+
+void ProblemConstructionInfo::readBasicInfo(const Json::Value& v)
+{
+  json_marshal::childFromJson(v, basic_info.n_steps, "n_steps");
+  json_marshal::childFromJson(v, basic_info.manip, "manip");
+  json_marshal::childFromJson(v, basic_info.fixed_timesteps, "fixed_timesteps", IntVec());
+  json_marshal::childFromJson(v, basic_info.fixed_dofs, "fixed_dofs", IntVec());
+  json_marshal::childFromJson(v, basic_info.convex_solver, "convex_solver", std::string("OSQP"));
+  json_marshal::childFromJson(v, basic_info.dt_lower_lim, "dt_lower_lim", 1.0);
+  json_marshal::childFromJson(v, basic_info.dt_upper_lim, "dt_upper_lim", 1.0);
+  json_marshal::childFromJson(v, basic_info.use_time, "use_time", false);
+  if (basic_info.dt_lower_lim <= 0 || basic_info.dt_upper_lim < basic_info.dt_lower_lim)
+    throw std::runtime_error("dt limits (Basic Info) invalid. The lower limit must be positive, "
+                             "and the minimum upper limit is equal to the lower limit.");
+}
+
+void ProblemConstructionInfo::readOptInfo(const Json::Value& v)
+{
+  auto& o = opt_info;
+  json_marshal::childFromJson(v, o.improve_ratio_threshold, "improve_ratio_threshold", o.improve_ratio_threshold);
+  json_marshal::childFromJson(v, o.min_trust_box_size, "min_trust_box_size", o.min_trust_box_size);
+  json_marshal::childFromJson(v, o.min_approx_improve, "min_approx_improve", o.min_approx_improve);
+  json_marshal::childFromJson(v, o.min_approx_improve_frac, "min_approx_improve_frac", o.min_approx_improve_frac);
+  json_marshal::childFromJson(v, o.max_iter, "max_iter", o.max_iter);
+  json_marshal::childFromJson(v, o.trust_shrink_ratio, "trust_shrink_ratio", o.trust_shrink_ratio);
+  json_marshal::childFromJson(v, o.trust_expand_ratio, "trust_expand_ratio", o.trust_expand_ratio);
+  json_marshal::childFromJson(v, o.cnt_tolerance, "cnt_tolerance", o.cnt_tolerance);
+  json_marshal::childFromJson(v, o.max_merit_coeff_increases, "max_merit_coeff_increases",
+                              o.max_merit_coeff_increases);
+  json_marshal::childFromJson(v, o.merit_coeff_increase_ratio, "merit_coeff_increase_ratio",
+                              o.merit_coeff_increase_ratio);
+  json_marshal::childFromJson(v, o.max_time, "max_time", o.max_time);
+  json_marshal::childFromJson(v, o.initial_merit_error_coeff, "initial_merit_error_coeff",
+                              o.initial_merit_error_coeff);
+  json_marshal::childFromJson(v, o.inflate_constraints_individually, "inflate_constraints_individually",
+                              o.inflate_constraints_individually);
+  json_marshal::childFromJson(v, o.trust_box_size, "trust_box_size", o.trust_box_size);
+}
+
+void ProblemConstructionInfo::readCosts(const Json::Value& v)
+{
+  cost_infos.clear();
+  for (const auto& it : v)
+  {
+    std::string type;
+    bool use_time = false;
+    json_marshal::childFromJson(it, type, "type");
+    json_marshal::childFromJson(it, use_time, "use_time", false);
+    const TermInfo::Ptr term = TermInfo::fromName(type);
+    if (!term)
+      throw std::runtime_error("failed to construct cost named " + type);
+    if (use_time)
+    {
+      term->term_type = TermType::TT_COST | TermType::TT_USE_TIME;
+      basic_info.use_time = true;
+    }
+    else
+      term->term_type = TermType::TT_COST;
+    term->fromJson(*this, it);
+    json_marshal::childFromJson(it, term->name, "name", type);
+    cost_infos.push_back(term);
+  }
+}
+
+void ProblemConstructionInfo::readConstraints(const Json::Value& v)
+{
+  cnt_infos.clear();
+  for (const auto& it : v)
+  {
+    std::string type;
+    bool use_time = false;
+    json_marshal::childFromJson(it, type, "type");
+    json_marshal::childFromJson(it, use_time, "use_time", false);
+    const TermInfo::Ptr term = TermInfo::fromName(type);
+    if (!term)
+      throw std::runtime_error("failed to construct constraint named " + type);
+    if (use_time)
+    {
+      term->term_type = TermType::TT_CNT | TermType::TT_USE_TIME;
+      basic_info.use_time = true;
+    }
+    else
+      term->term_type = TermType::TT_CNT;
+    term->fromJson(*this, it);
+    json_marshal::childFromJson(it, term->name, "name", type);
+    cnt_infos.push_back(term);
+  }
+}
+
+void ProblemConstructionInfo::readInitInfo(const Json::Value& v)
+{
+  std::string type_str;
+  json_marshal::childFromJson(v, type_str, "type");
+  json_marshal::childFromJson(v, init_info.dt, "dt", 1.0);
+  const int n_steps = basic_info.n_steps;
+  const int n_dof = kin->numJoints();
+  if (iequals(type_str, "stationary"))
+    init_info.type = InitInfo::STATIONARY;
+  else if (iequals(type_str, "given_traj"))
+  {
+    init_info.type = InitInfo::GIVEN_TRAJ;
+    if (!v.isMember("data"))
+      throw std::runtime_error("init_info given_traj: missing data");
+    const Json::Value& vdata = v["data"];
+    if (static_cast<int>(vdata.size()) != n_steps)
+      throw std::runtime_error("given initialization traj has wrong length");
+    init_info.data.assign(static_cast<std::size_t>(n_steps), DblVec());
+    for (int i = 0; i < n_steps; ++i)
+      json_marshal::fromJsonArray(vdata[i], init_info.data[static_cast<std::size_t>(i)], n_dof);
+  }
+  else if (iequals(type_str, "joint_interpolated"))
+  {
+    init_info.type = InitInfo::JOINT_INTERPOLATED;
+    if (!v.isMember("endpoint"))
+      throw std::runtime_error("init_info joint_interpolated: missing endpoint");
+    DblVec endpoint;
+    json_marshal::childFromJson(v, endpoint, "endpoint");
+    if (static_cast<int>(endpoint.size()) != n_dof)
+      throw std::runtime_error("wrong number of dof values in initialization. expected " + std::to_string(n_dof) +
+                               " got " + std::to_string(endpoint.size()));
+    init_info.data = { endpoint };
+  }
+  else
+    throw std::runtime_error("init_info did not have a valid type from Json. Valid types are "
+                             "stationary, joint_interpolated, or given_traj");
+}
+
+void ProblemConstructionInfo::fromJson(const Json::Value& v)
+{
+  if (v.isMember("basic_info"))
+    readBasicInfo(v["basic_info"]);
+  else
+    throw std::runtime_error("Json missing required section basic_info!");
+  if (v.isMember("opt_info"))
+    readOptInfo(v["opt_info"]);
+  kin = env ? env->getJointGroup(basic_info.manip) : nullptr;
+  if (!kin)
+    throw std::runtime_error("Manipulator does not exist: " + basic_info.manip);
+  if (v.isMember("costs"))
+    readCosts(v["costs"]);
+  if (v.isMember("constraints"))
+    readConstraints(v["constraints"]);
+  if (v.isMember("init_info"))
+    readInitInfo(v["init_info"]);
+  else
+    throw std::runtime_error("Json missing required section init_info!");
+}
+
+// ------------------------------------------------------------ JointPos
+void JointPosTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value& v)
+{
+  if (!v.isMember("params"))
+    throw std::runtime_error("JointPosTermInfo: missing params");
+  const Json::Value& params = v["params"];
+  const auto n_dof = static_cast<std::size_t>(pci.kin->numJoints());
+  json_marshal::childFromJson(params, targets, "targets");
+  json_marshal::childFromJson(params, coeffs, "coeffs", DblVec(n_dof, 1));
+  json_marshal::childFromJson(params, upper_tols, "upper_tols", DblVec(n_dof, 0));
+  json_marshal::childFromJson(params, lower_tols, "lower_tols", DblVec(n_dof, 0));
+  json_marshal::childFromJson(params, first_step, "first_step", 0);
+  json_marshal::childFromJson(params, last_step, "last_step", pci.basic_info.n_steps - 1);
+  const char* all_fields[] = { "coeffs", "first_step", "last_step", "targets", "lower_tols", "upper_tols" };
+  ensure_only_members(params, all_fields, sizeof(all_fields) / sizeof(char*));
+}
+
+// problem_description.cpp:1097-1196
+void JointPosTermInfo::hatch(TrajOptProb& prob)
+{
+  const auto n_dof = static_cast<unsigned>(prob.GetNumDOF());
+  if (coeffs.empty())
+    coeffs = DblVec(n_dof, 1);
+  if (upper_tols.empty())
+    upper_tols = DblVec(n_dof, 0);
+  if (lower_tols.empty())
+    lower_tols = DblVec(n_dof, 0);
+  if (last_step <= -1)
+    last_step = prob.GetNumSteps() - 1;
+  if ((prob.GetNumSteps() - 1) <= first_step)
+    first_step = prob.GetNumSteps() - 1;
+  if ((prob.GetNumSteps() - 1) <= last_step)
+    last_step = prob.GetNumSteps() - 1;
+  if (last_step < first_step)
+    std::swap(first_step, last_step);
+  checkParameterSize(coeffs, n_dof, "JointPosTermInfo coeffs", true);
+  checkParameterSize(targets, n_dof, "JointPosTermInfo targets", true);
+  checkParameterSize(upper_tols, n_dof, "JointPosTermInfo upper_tols", true);
+  checkParameterSize(lower_tols, n_dof, "JointPosTermInfo lower_tols", true);
+  const bool zero_tols = std::all_of(upper_tols.begin(), upper_tols.end(), [](double i) { return doubleEquals(i, 0.); }) &&
+                         std::all_of(lower_tols.begin(), lower_tols.end(), [](double i) { return doubleEquals(i, 0.); });
+  if (!zero_tols)
+    unsupported("JointPosTermInfo with tolerances (JointPosIneqCost / JointPosIneqConstraint)");
+  thip_problem_desc& d = prob.desc();
+  if (d.n_jpos >= THIP_MAX_JPOS)
+    unsupported("more than " + std::to_string(THIP_MAX_JPOS) + " JointPos terms");
+  const int k = d.n_jpos++;
+  d.jpos_is_cnt[k] = any(term_type & TermType::TT_COST) ? 0 : 1;
+  d.jpos_first_step[k] = first_step;
+  d.jpos_last_step[k] = last_step;
+  for (unsigned j = 0; j < n_dof; ++j)
+  {
+    d.jpos_coeffs[k][j] = coeffs[j];
+    d.jpos_targets[k][j] = 0.0;  // per problem: TrajOptProb::jpos_targets
+    prob.jpos_targets.push_back(targets[j]);
+  }
+}
+
+// ------------------------------------------------------------ JointVel
+void JointVelTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value& v)
+{
+  if (!v.isMember("params"))
+    throw std::runtime_error("JointVelTermInfo: missing params");
+  const Json::Value& params = v["params"];
+  const auto n_dof = static_cast<std::size_t>(pci.kin->numJoints());
+  json_marshal::childFromJson(params, targets, "targets");
+  json_marshal::childFromJson(params, coeffs, "coeffs", DblVec(n_dof, 1));
+  json_marshal::childFromJson(params, upper_tols, "upper_tols", DblVec(n_dof, 0));
+  json_marshal::childFromJson(params, lower_tols, "lower_tols", DblVec(n_dof, 0));
+  json_marshal::childFromJson(params, first_step, "first_step", 0);
+  json_marshal::childFromJson(params, last_step, "last_step", pci.basic_info.n_steps - 1);
+  const char* all_fields[] = { "coeffs", "first_step", "last_step", "targets", "lower_tols", "upper_tols", "use_time" };
+  ensure_only_members(params, all_fields, sizeof(all_fields) / sizeof(char*));
+}
+
+// problem_description.cpp:1216-1391 (the step clamping itself is applied by
+// thip_create on the raw first/last steps, identically)
+void JointVelTermInfo::hatch(TrajOptProb& prob)
+{
+  const auto n_dof = static_cast<unsigned>(prob.GetNumDOF());
+  if (coeffs.empty())
+    coeffs = DblVec(n_dof, 1);
+  if (upper_tols.empty())
+    upper_tols = DblVec(n_dof, 0);
+  if (lower_tols.empty())
+    lower_tols = DblVec(n_dof, 0);
+  checkParameterSize(coeffs, n_dof, "JointVelTermInfo coeffs", true);
+  checkParameterSize(targets, n_dof, "JointVelTermInfo targets", true);
+  checkParameterSize(upper_tols, n_dof, "JointVelTermInfo upper_tols", true);
+  checkParameterSize(lower_tols, n_dof, "JointVelTermInfo lower_tols", true);
+  const bool zero_tols = std::all_of(upper_tols.begin(), upper_tols.end(), [](double i) { return doubleEquals(i, 0.); }) &&
+                         std::all_of(lower_tols.begin(), lower_tols.end(), [](double i) { return doubleEquals(i, 0.); });
+  if (any(term_type & TermType::TT_USE_TIME))
+    unsupported("JointVelTermInfo with use_time");
+  if (!any(term_type & TermType::TT_COST))
+    unsupported("JointVelTermInfo as a constraint (JointVelEqConstraint / JointVelIneqConstraint)");
+  if (!zero_tols)
+    unsupported("JointVelTermInfo with tolerances (JointVelIneqCost)");
+  thip_problem_desc& d = prob.desc();
+  if (d.jv_enabled)
+    unsupported("more than one joint_vel cost");
+  d.jv_enabled = 1;
+  d.jv_first_step = first_step;
+  d.jv_last_step = last_step;
+  for (unsigned j = 0; j < n_dof; ++j)
+  {
+    d.jv_coeffs[j] = coeffs[j];
+    d.jv_targets[j] = targets[j];
+  }
+}
+
+// ------------------------------------------------------------ CartPose
+void CartPoseTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value& v)
+{
+  if (!v.isMember("params"))
+    throw std::runtime_error("CartPoseTermInfo: missing params");
+  const Json::Value& params = v["params"];
+  json_marshal::childFromJson(params, timestep, "timestep", pci.basic_info.n_steps - 1);
+  readVec3(params, "pos_coeffs", pos_coeffs, { 1, 1, 1 });
+  readVec3(params, "rot_coeffs", rot_coeffs, { 1, 1, 1 });
+  json_marshal::childFromJson(params, source_frame, "source_frame");
+  json_marshal::childFromJson(params, target_frame, "target_frame");
+  std::array<double, 3> sxyz, txyz;
+  std::array<double, 4> swxyz, twxyz;
+  readVec3(params, "source_frame_offset_xyz", sxyz, { 0, 0, 0 });
+  readVec4(params, "source_frame_offset_wxyz", swxyz, { 1, 0, 0, 0 });
+  readVec3(params, "target_frame_offset_xyz", txyz, { 0, 0, 0 });
+  readVec4(params, "target_frame_offset_wxyz", twxyz, { 1, 0, 0, 0 });
+  source_frame_offset = poseFromXyzWxyz(sxyz, swxyz);
+  target_frame_offset = poseFromXyzWxyz(txyz, twxyz);
+  if (!pci.kin->hasLinkId(source_frame))
+    throw std::runtime_error("invalid source frame: " + source_frame);
+  if (!pci.kin->hasLinkId(target_frame))
+    throw std::runtime_error("invalid target frame: " + target_frame);
+  const bool source_active = pci.kin->isActiveLinkId(source_frame);
+  const bool target_active = pci.kin->isActiveLinkId(target_frame);
+  if (source_active && target_active)
+    throw std::runtime_error("source '" + source_frame + "' and target '" + target_frame + "' are both active");
+  if (!source_active && !target_active)
+    throw std::runtime_error("source '" + source_frame + "' and target '" + target_frame + "' are both static");
+  const char* all_fields[] = { "timestep",
+                               "pos_coeffs",
+                               "rot_coeffs",
+                               "source_frame",
+                               "target_frame",
+                               "source_frame_offset_xyz",
+                               "source_frame_offset_wxyz",
+                               "target_frame_offset_xyz",
+                               "target_frame_offset_wxyz" };
+  ensure_only_members(params, all_fields, sizeof(all_fields) / sizeof(char*));
+}
+
+// problem_description.cpp:919-1005
+void CartPoseTermInfo::hatch(TrajOptProb& prob)
+{
+  if (any(term_type & TermType::TT_USE_TIME))
+  {
+    // the reference logs and adds nothing (problem_description.cpp:948-955)
+    std::cerr << "CartPoseTermInfo: Use time version of this term has not been defined.\n";
+    return;
+  }
+  const auto kin = prob.GetKin();
+  if (kin->isActiveLinkId(target_frame) || !kin->isActiveLinkId(source_frame))
+    unsupported("CartPoseTermInfo with an active target frame (source static)");
+  if (!lower_tolerance.empty() || !upper_tolerance.empty())
+  {
+    bool equal = lower_tolerance.size() == upper_tolerance.size();
+    for (std::size_t i = 0; equal && i < lower_tolerance.size(); ++i)
+      equal = doubleEquals(lower_tolerance[i], upper_tolerance[i]);
+    if (!equal)
+      unsupported("CartPoseTermInfo with tolerances");
+  }
+  if (timestep < 0 || timestep >= prob.GetNumSteps())
+    throw std::runtime_error("CartPoseTermInfo: timestep " + std::to_string(timestep) + " out of range");
+  thip_problem_desc& d = prob.desc();
+  if (d.n_cart >= THIP_MAX_CART)
+    unsupported("more than " + std::to_string(THIP_MAX_CART) + " CartPose terms");
+  const int k = d.n_cart++;
+  d.cart_step[k] = timestep;
+  d.cart_is_cnt[k] = any(term_type & TermType::TT_COST) ? 0 : 1;
+  d.cart_source_link[k] = kin->linkIndex(source_frame);
+  for (int i = 0; i < 12; ++i)
+    d.cart_source_offset[k][i] = source_frame_offset[static_cast<std::size_t>(i)];
+  for (int i = 0; i < 3; ++i)
+  {
+    d.cart_pos_coeffs[k][i] = pos_coeffs[static_cast<std::size_t>(i)];
+    d.cart_rot_coeffs[k][i] = rot_coeffs[static_cast<std::size_t>(i)];
+  }
+  // per-problem target: the offset in the chain root frame (the kernel forms base_pose * offset)
+  Pose12 off = target_frame_offset;
+  if (kin->linkIndex(target_frame) != 0)
+  {
+    Pose12 base;
+    std::copy(kin->chain.base_pose, kin->chain.base_pose + 12, base.begin());
+    off = poseMul(poseInv(base), poseMul(kin->staticWorldPose(target_frame), target_frame_offset));
+  }
+  prob.cart_targets.insert(prob.cart_targets.end(), off.begin(), off.end());
+}
+
+// ------------------------------------------------------------ Collision
+void CollisionTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value& v)
+{
+  if (!v.isMember("params"))
+    throw std::runtime_error("CollisionTermInfo: missing params");
+  const Json::Value& params = v["params"];
+  const int n_steps = pci.basic_info.n_steps;
+  json_marshal::childFromJson(params, evaluator_type, "evaluator_type", 1);
+  json_marshal::childFromJson(params, first_step, "first_step", 0);
+  json_marshal::childFromJson(params, last_step, "last_step", n_steps - 1);
+  json_marshal::childFromJson(params, longest_valid_segment_length, "longest_valid_segment_length", 0.5);
+  // read, but not in all_fields below: a JSON that sets it is rejected (reference quirk,
+  // problem_description.cpp:1649,1722-1732), so JSON problems always get 0.5
+  json_marshal::childFromJson(params, collision_margin_buffer, "safety_margin_buffer", 0.5);
+  if (!(longest_valid_segment_length >= 0) || !(first_step >= 0 && first_step < n_steps) ||
+      !(last_step >= first_step && last_step < n_steps) || !(evaluator_type <= 4) || !(collision_margin_buffer >= 0))
+    throw std::runtime_error("CollisionTermInfo: invalid params");
+  json_marshal::childFromJson(params, fixed_steps, "fixed_steps", IntVec());
+  for (int fs : fixed_steps)
+    if (fs < first_step || fs > last_step)
+      throw std::runtime_error("Fixed step " + std::to_string(fs) + " is not between first step " +
+                               std::to_string(first_step) + " and last step " + std::to_string(last_step));
+  json_marshal::childFromJson(params, contact_test_type, "contact_test_type", 2);
+  if (contact_test_type < 0 || contact_test_type >= 3)
+    throw std::runtime_error("CollisionTermInfo: invalid contact_test_type");
+  json_marshal::childFromJson(params, coeff, "coeffs");
+  json_marshal::childFromJson(params, dist_pen, "dist_pen");
+  has_pairs = params.isMember("pairs");
+  const char* all_fields[] = { "type",           "first_step",        "last_step",
+                               "evaluator_type", "fixed_steps",       "contact_test_type",
+                               "longest_valid_segment_length", "coeffs", "dist_pen", "pairs" };
+  ensure_only_members(params, all_fields, sizeof(all_fields) / sizeof(char*));
+}
+
+// problem_description.cpp:1735-1858, LVS_DISCRETE branch
+void CollisionTermInfo::hatch(TrajOptProb& prob)
+{
+  if (evaluator_type != 2)
+    unsupported("collision evaluator_type " + std::to_string(evaluator_type) + " (only LVS_DISCRETE = 2)");
+  if (contact_test_type != 2)
+    unsupported("collision contact_test_type " + std::to_string(contact_test_type) + " (only ALL = 2)");
+  if (has_pairs)
+    unsupported("per link-pair collision margins / coeffs (\"pairs\")");
+  const auto env = prob.GetEnv();
+  thip_problem_desc& d = prob.desc();
+  if (d.coll_enabled)
+    unsupported("more than one collision term");
+  const int n_steps = prob.GetNumSteps();
+  for (int i = first_step; i < last_step; ++i)
+  {
+    const bool a = std::find(fixed_steps.begin(), fixed_steps.end(), i) != fixed_steps.end();
+    const bool b = std::find(fixed_steps.begin(), fixed_steps.end(), i + 1) != fixed_steps.end();
+    if (a && b)
+      throw std::runtime_error("Currently two adjacent fixed steps are not supported in collision term.");
+  }
+  if (env->collision_spheres.empty() || static_cast<int>(env->collision_spheres.size()) > THIP_MAX_SPHERES)
+    unsupported("a collision model with " + std::to_string(env->collision_spheres.size()) + " spheres");
+  if (static_cast<int>(env->scene.size()) > THIP_MAX_PRIMS)
+    unsupported("a scene of more than " + std::to_string(THIP_MAX_PRIMS) + " primitives");
+  if (static_cast<int>(fixed_steps.size()) > THIP_MAX_STEPS)
+    throw std::runtime_error("CollisionTermInfo: too many fixed steps");
+  d.coll_enabled = 1;
+  d.coll_is_cnt = any(term_type & TermType::TT_COST) ? 0 : 1;
+  d.coll_first_step = first_step;
+  d.coll_last_step = std::min(last_step, n_steps - 1);
+  d.coll_n_fixed = static_cast<int>(fixed_steps.size());
+  for (std::size_t k = 0; k < fixed_steps.size(); ++k)
+    d.coll_fixed_steps[k] = fixed_steps[k];
+  d.coll_margin = dist_pen;
+  d.coll_coeff = coeff;
+  d.coll_buffer = collision_margin_buffer;
+  d.coll_lvs = longest_valid_segment_length;
+  d.n_spheres = static_cast<int>(env->collision_spheres.size());
+  for (int s = 0; s < d.n_spheres; ++s)
+  {
+    const CollisionSphere& cs = env->collision_spheres[static_cast<std::size_t>(s)];
+    d.sphere_link[s] = cs.link;
+    for (int i = 0; i < 3; ++i)
+      d.sphere_center[s][i] = cs.center[i];
+    d.sphere_radius[s] = cs.radius;
+  }
+  d.n_prims = static_cast<int>(env->scene.size());
+  for (const auto& p : env->scene)
+    prob.scene.insert(prob.scene.end(), p.begin(), p.end());
+}
+
+// ------------------------------------------------------------ ConstructProblem
+// problem_description.cpp:414-546 + generateInitTraj (:314-360)
+TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci)
+{
+  const BasicInfo& bi = pci.basic_info;
+  const int n_steps = bi.n_steps;
+  if (!pci.kin)
+    throw std::runtime_error("ConstructProblem: pci.kin is null");
+  for (const auto& ci : pci.cost_infos)
+    if (!any(ci->getSupportedTypes() & TermType::TT_COST) ||
+        (any(ci->term_type & TermType::TT_USE_TIME) && !any(ci->getSupportedTypes() & TermType::TT_USE_TIME)))
+      throw std::runtime_error(ci->name + " is not a supported cost type");
+  for (const auto& ci : pci.cnt_infos)
+    if (!any(ci->getSupportedTypes() & TermType::TT_CNT) ||
+        (any(ci->term_type & TermType::TT_USE_TIME) && !any(ci->getSupportedTypes() & TermType::TT_USE_TIME)))
+      throw std::runtime_error(ci->name + " is not a supported constraint type");
+  if (bi.use_time)
+    unsupported("use_time (the 1/dt column)");
+  if (!bi.fixed_dofs.empty())
+    unsupported("basic_info.fixed_dofs");
+  if (!iequals(bi.convex_solver, "OSQP") && !iequals(bi.convex_solver, "AUTO_SOLVER"))
+    unsupported("convex_solver " + bi.convex_solver);
+  if (n_steps < 2 || n_steps > THIP_MAX_STEPS)
+    throw std::runtime_error("n_steps must be in [2, " + std::to_string(THIP_MAX_STEPS) + "]");
+
+  auto prob = std::make_shared<TrajOptProb>();
+  prob->kin_ = pci.kin;
+  prob->env_ = pci.env;
+  thip_problem_desc& d = prob->desc_;
+  std::memset(&d, 0, sizeof(d));
+  d.n_steps = n_steps;
+  d.chain = pci.kin->chain;
+  const int n_dof = pci.kin->numJoints();
+
+  // initial trajectory
+  const DblVec start = pci.env->getCurrentJointValues(pci.kin->name);
+  std::vector<DblVec> init;
+  if (pci.init_info.type == InitInfo::STATIONARY)
+    init.assign(static_cast<std::size_t>(n_steps), start);
+  else if (pci.init_info.type == InitInfo::JOINT_INTERPOLATED)
+  {
+    if (pci.init_info.data.size() != 1 || static_cast<int>(pci.init_info.data[0].size()) != n_dof)
+      throw std::runtime_error("JOINT_INTERPOLATED selected, but init_info.data is the wrong size. It should be 1 x "
+                               "pci.kin->numJoints()");
+    const DblVec& end = pci.init_info.data[0];
+    init.assign(static_cast<std::size_t>(n_steps), DblVec(static_cast<std::size_t>(n_dof)));
+    for (int j = 0; j < n_dof; ++j)
+      for (int i = 0; i < n_steps; ++i)
+        init[static_cast<std::size_t>(i)][static_cast<std::size_t>(j)] =
+            linspaced(n_steps, start[static_cast<std::size_t>(j)], end[static_cast<std::size_t>(j)], i);
+  }
+  else
+    init = pci.init_info.data;
+  if (static_cast<int>(init.size()) != n_steps)
+    throw std::runtime_error("initial trajectory has " + std::to_string(init.size()) + " rows, expected " +
+                             std::to_string(n_steps));
+  for (const auto& row : init)
+    if (static_cast<int>(row.size()) != n_dof)
+      throw std::runtime_error("initial trajectory row has the wrong number of dofs");
+  prob->init_ = init;
+
+  // fixed timesteps (problem_description.cpp:489-510)
+  if (bi.fixed_timesteps.size() > THIP_MAX_STEPS)
+    throw std::runtime_error("too many fixed timesteps");
+  for (int t : bi.fixed_timesteps)
+  {
+    if (t < 0 || t >= n_steps)
+      throw std::runtime_error("Fixed timestep index is outside the bounds of the initial trajectory.");
+    d.fixed_steps[d.n_fixed++] = t;
+  }
+
+  // optimizer parameters: BasicTrustRegionSQP(prob) takes them from the caller
+  // in the reference; here they travel with the problem (opt_info)
+  const auto& o = pci.opt_info;
+  d.sqp.improve_ratio_threshold = o.improve_ratio_threshold;
+  d.sqp.min_trust_box_size = o.min_trust_box_size;
+  d.sqp.min_approx_improve = o.min_approx_improve;
+  d.sqp.min_approx_improve_frac = o.min_approx_improve_frac;
+  d.sqp.max_iter = o.max_iter;
+  d.sqp.trust_shrink_ratio = o.trust_shrink_ratio;
+  d.sqp.trust_expand_ratio = o.trust_expand_ratio;
+  d.sqp.cnt_tolerance = o.cnt_tolerance;
+  d.sqp.max_merit_coeff_increases = o.max_merit_coeff_increases;
+  d.sqp.max_qp_solver_failures = o.max_qp_solver_failures;
+  d.sqp.merit_coeff_increase_ratio = o.merit_coeff_increase_ratio;
+  d.sqp.initial_merit_error_coeff = o.initial_merit_error_coeff;
+  d.sqp.inflate_constraints_individually = o.inflate_constraints_individually ? 1 : 0;
+  d.sqp.trust_box_size = o.trust_box_size;
+  d.osqp = pci.osqp;
+
+  for (const auto& ci : pci.cost_infos)
+    ci->hatch(*prob);
+  for (const auto& ci : pci.cnt_infos)
+    ci->hatch(*prob);
+  return prob;
+}
+
+TrajOptProb::Ptr ConstructProblem(const Json::Value& root, const Environment::ConstPtr& env)
+{
+  ProblemConstructionInfo pci(env);
+  pci.fromJson(root);
+  return ConstructProblem(pci);
+}
+}  // namespace trajopt

@@ -130,6 +130,7 @@ class ProblemDesc(C.Structure):
         ("sphere_center", _D3 * MAX_SPHERES),
         ("sphere_radius", C.c_double * MAX_SPHERES),
         ("n_prims", C.c_int),
+        ("coll_max_contacts", C.c_int),
         ("sqp", SqpParams),
         ("osqp", OsqpSettings),
     ]

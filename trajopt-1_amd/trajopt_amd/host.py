@@ -1,0 +1,149 @@
+"""ctypes binding of the C++ host front door (include/trajopt_host.h).
+
+The front door parses problems in the reference's JSON format
+(ProblemConstructionInfo::fromJson, trajopt/src/problem_description.cpp:276-312)
+on the built-in PR2 "right_arm" environment and lowers them with the
+TermInfo::hatch restatements; `solve_json_batch` runs them through the C++
+BatchTrustRegionSQP on the HIP path.  `workload_to_json` writes a synthetic
+workload problem in that format (used by the tests to drive the front door).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import math
+
+import numpy as np
+
+from . import abi
+
+HOST_LIB = abi.LIB_DIR / "libtrajopt_host.so"
+_host = None
+
+
+class HostError(RuntimeError):
+    pass
+
+
+def load_host():
+    global _host
+    if _host is None:
+        abi.load_hip()  # one HIP runtime: torch first, then libtrajopt_hip.so
+        if not HOST_LIB.exists():
+            raise RuntimeError(f"{HOST_LIB} is missing: run __graft_entry__.build()")
+        L = C.CDLL(str(HOST_LIB))
+        dp = C.POINTER(C.c_double)
+        L.thost_lower_json.argtypes = [C.c_char_p, dp, C.c_int, C.POINTER(abi.ProblemDesc), dp, dp, dp, C.c_char_p,
+                                       C.c_int]
+        L.thost_lower_json.restype = C.c_int
+        L.thost_solve_json_batch.argtypes = [C.POINTER(C.c_char_p), C.c_int, dp, C.c_int, C.c_int, dp,
+                                             C.POINTER(abi.Result), C.c_char_p, C.c_int]
+        L.thost_solve_json_batch.restype = C.c_int
+        _host = L
+    return _host
+
+
+def _dp(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def lower_json(text: str, scene=None):
+    """-> (desc, init [N, D], cart_targets [n_cart, 12], jpos_targets [n_jpos, D])."""
+    L = load_host()
+    sc = None if scene is None or len(scene) == 0 else np.ascontiguousarray(scene, dtype=np.float64)
+    n_prims = 0 if sc is None else sc.shape[0]
+    desc = abi.ProblemDesc()
+    init = np.zeros((abi.MAX_STEPS, abi.MAX_DOF))
+    tgt = np.zeros((abi.MAX_CART, 12))
+    jpt = np.zeros((abi.MAX_JPOS, abi.MAX_DOF))
+    err = C.create_string_buffer(4096)
+    rc = L.thost_lower_json(text.encode(), _dp(sc), n_prims, C.byref(desc), _dp(init), _dp(tgt), _dp(jpt), err, 4096)
+    if rc != 0:
+        raise HostError(err.value.decode())
+    N, D = desc.n_steps, desc.chain.n_dof
+    init = init.reshape(-1)[: N * D].reshape(N, D)
+    tgt = tgt.reshape(-1)[: desc.n_cart * 12].reshape(desc.n_cart, 12)
+    jpt = jpt.reshape(-1)[: desc.n_jpos * D].reshape(desc.n_jpos, D)
+    return desc, init, tgt, jpt
+
+
+def solve_json_batch(texts, scenes=None, device=0):
+    """-> (x [B, N, D], list of abi.Result) through trajopt::BatchTrustRegionSQP."""
+    L = load_host()
+    B = len(texts)
+    desc, _, _, _ = lower_json(texts[0], None if scenes is None else scenes[0])
+    N, D = desc.n_steps, desc.chain.n_dof
+    sc = None if scenes is None else np.ascontiguousarray(scenes, dtype=np.float64)
+    n_prims = 0 if sc is None else sc.shape[1]
+    arr = (C.c_char_p * B)(*[t.encode() for t in texts])
+    x = np.zeros((B, N, D))
+    res = (abi.Result * B)()
+    err = C.create_string_buffer(4096)
+    rc = L.thost_solve_json_batch(arr, B, _dp(sc), n_prims, device, _dp(x), res, err, 4096)
+    if rc != 0:
+        raise HostError(err.value.decode())
+    return x, list(res)
+
+
+def _quat_wxyz(R):
+    """Unit quaternion (w, x, y, z) of a rotation matrix (Shepperd)."""
+    R = np.asarray(R, dtype=float)
+    tr = R[0, 0] + R[1, 1] + R[2, 2]
+    if tr > 0:
+        s = math.sqrt(tr + 1.0) * 2
+        q = [0.25 * s, (R[2, 1] - R[1, 2]) / s, (R[0, 2] - R[2, 0]) / s, (R[1, 0] - R[0, 1]) / s]
+    elif R[0, 0] > R[1, 1] and R[0, 0] > R[2, 2]:
+        s = math.sqrt(1.0 + R[0, 0] - R[1, 1] - R[2, 2]) * 2
+        q = [(R[2, 1] - R[1, 2]) / s, 0.25 * s, (R[0, 1] + R[1, 0]) / s, (R[0, 2] + R[2, 0]) / s]
+    elif R[1, 1] > R[2, 2]:
+        s = math.sqrt(1.0 + R[1, 1] - R[0, 0] - R[2, 2]) * 2
+        q = [(R[0, 2] - R[2, 0]) / s, (R[0, 1] + R[1, 0]) / s, 0.25 * s, (R[1, 2] + R[2, 1]) / s]
+    else:
+        s = math.sqrt(1.0 + R[2, 2] - R[0, 0] - R[1, 1]) * 2
+        q = [(R[1, 0] - R[0, 1]) / s, (R[0, 2] + R[2, 0]) / s, (R[1, 2] + R[2, 1]) / s, 0.25 * s]
+    q = np.array(q)
+    return (q / np.linalg.norm(q)).tolist()
+
+
+def workload_to_json(wl, b: int) -> str:
+    """Problem b of a synthetic workload (configs A, B, C, J) in the
+    reference's TrajOptRequest JSON format: given_traj init, joint_vel cost,
+    cart_pose terms with target_frame torso_lift_link and the target as
+    target_frame_offset, joint_pos terms, and the LVS_DISCRETE collision term."""
+    d = wl.desc
+    N, D = wl.n_steps, wl.n_dof
+    costs, cnts = [], []
+    if d.jv_enabled:
+        costs.append({"type": "joint_vel", "params": {
+            "coeffs": [d.jv_coeffs[j] for j in range(D)], "targets": [d.jv_targets[j] for j in range(D)],
+            "first_step": d.jv_first_step, "last_step": d.jv_last_step}})
+    for k in range(d.n_cart):
+        T = np.asarray(wl.targets[b, k]).reshape(3, 4)
+        term = {"type": "cart_pose", "params": {
+            "timestep": d.cart_step[k], "source_frame": "r_gripper_tool_frame", "target_frame": "torso_lift_link",
+            "pos_coeffs": [d.cart_pos_coeffs[k][i] for i in range(3)],
+            "rot_coeffs": [d.cart_rot_coeffs[k][i] for i in range(3)],
+            "target_frame_offset_xyz": T[:, 3].tolist(), "target_frame_offset_wxyz": _quat_wxyz(T[:, :3])}}
+        (cnts if d.cart_is_cnt[k] else costs).append(term)
+    jt = wl.jpos_targets
+    for k in range(d.n_jpos):
+        tg = jt[b, k] if jt is not None else [d.jpos_targets[k][j] for j in range(D)]
+        term = {"type": "joint_pos", "params": {
+            "coeffs": [d.jpos_coeffs[k][j] for j in range(D)], "targets": [float(v) for v in tg],
+            "first_step": d.jpos_first_step[k], "last_step": d.jpos_last_step[k]}}
+        (cnts if d.jpos_is_cnt[k] else costs).append(term)
+    if d.coll_enabled:
+        term = {"type": "collision", "params": {
+            "coeffs": d.coll_coeff, "dist_pen": d.coll_margin, "evaluator_type": 2,
+            "first_step": d.coll_first_step, "last_step": d.coll_last_step if d.coll_last_step >= 0 else N - 1,
+            "fixed_steps": [d.coll_fixed_steps[i] for i in range(d.coll_n_fixed)],
+            "longest_valid_segment_length": d.coll_lvs}}
+        (cnts if d.coll_is_cnt else costs).append(term)
+    doc = {
+        "basic_info": {"n_steps": N, "manip": "right_arm",
+                       "fixed_timesteps": [d.fixed_steps[i] for i in range(d.n_fixed)]},
+        "costs": costs,
+        "constraints": cnts,
+        "init_info": {"type": "given_traj", "data": np.asarray(wl.init[b]).tolist()},
+    }
+    return json.dumps(doc)

@@ -169,18 +169,19 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
         q_lo = np.where(types == abi.JOINT_CONTINUOUS, -math.pi, lo)
         q_hi = np.where(types == abi.JOINT_CONTINUOUS, math.pi, hi)
         d.n_jpos = 2
-        # term 0: JointPosEqConstraint at the last step (goal, per problem)
-        d.jpos_is_cnt[0] = 1
-        d.jpos_first_step[0] = N - 1
-        d.jpos_last_step[0] = N - 1
-        # term 1: JointPosEqCost on the interior steps toward the range midpoint
-        d.jpos_is_cnt[1] = 0
-        d.jpos_first_step[1] = 1
-        d.jpos_last_step[1] = N - 2
+        # term 0: JointPosEqCost on the interior steps toward the range midpoint
+        # (costs are hatched before constraints, so a JSON problem lowers in this order)
+        d.jpos_is_cnt[0] = 0
+        d.jpos_first_step[0] = 1
+        d.jpos_last_step[0] = N - 2
+        # term 1: JointPosEqConstraint at the last step (goal, per problem)
+        d.jpos_is_cnt[1] = 1
+        d.jpos_first_step[1] = N - 1
+        d.jpos_last_step[1] = N - 1
         for j in range(D):
-            d.jpos_coeffs[0][j] = 1.0
-            d.jpos_coeffs[1][j] = 0.1
-            d.jpos_targets[1][j] = 0.5 * (q_lo[j] + q_hi[j])
+            d.jpos_coeffs[0][j] = 0.1
+            d.jpos_targets[0][j] = 0.5 * (q_lo[j] + q_hi[j])
+            d.jpos_coeffs[1][j] = 1.0
         jpos_targets = np.zeros((batch, 2, D))
 
     init = np.zeros((batch, N, D))
@@ -194,8 +195,8 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
         start, end = q_ref[0], q_ref[N - 1]
         if config == "J":
             end = q_ref[N - 1] + np.array([rng.uniform(-goal_offset, goal_offset) for _ in range(D)])
-            jpos_targets[b, 0] = q_ref[N - 1]
-            jpos_targets[b, 1] = [d.jpos_targets[1][j] for j in range(D)]
+            jpos_targets[b, 0] = [d.jpos_targets[0][j] for j in range(D)]
+            jpos_targets[b, 1] = q_ref[N - 1]
         for t in range(N):
             init[b, t] = start + (end - start) * (t / (N - 1))
         for t in range(1, N - 1):
