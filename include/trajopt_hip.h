@@ -159,13 +159,18 @@ typedef struct thip_problem_desc {
   int n_fixed;
   int fixed_steps[THIP_MAX_STEPS];
 
-  /* JointVelTermInfo as a cost, zero tolerances -> JointVelEqCost
-   * (problem_description.cpp:1216-1391, trajectory_costs.cpp:257-301) */
+  /* JointVelTermInfo as a cost (problem_description.cpp:1216-1391): zero
+   * tolerances -> JointVelEqCost (quadratic, trajectory_costs.cpp:257-301),
+   * otherwise JointVelIneqCost (two hinge rows per (step, joint),
+   * trajectory_costs.cpp:303-374).  A tolerance counts as zero when
+   * |tol| < 1e-5 (trajopt_common::doubleEquals). */
   int jv_enabled;
   int jv_first_step;
   int jv_last_step;
   double jv_coeffs[THIP_MAX_DOF];
   double jv_targets[THIP_MAX_DOF];
+  double jv_upper_tols[THIP_MAX_DOF];
+  double jv_lower_tols[THIP_MAX_DOF];
 
   /* CartPoseTermInfo (problem_description.cpp:919-1005): source = chain link
    * (active) with source offset, target = static chain root frame with a
@@ -178,14 +183,15 @@ typedef struct thip_problem_desc {
   double cart_pos_coeffs[THIP_MAX_CART][3];
   double cart_rot_coeffs[THIP_MAX_CART][3];
 
-  /* JointPosTermInfo (problem_description.cpp:1097-1196), zero tolerances:
+  /* JointPosTermInfo (problem_description.cpp:1097-1196).  Zero tolerances:
    * is_cnt 0 -> JointPosEqCost (quadratic, trajectory_costs.cpp:28-65),
    * is_cnt 1 -> JointPosEqConstraint (one EQ row coeff*(x - target) per
-   * (step, joint), trajectory_costs.cpp:137-181).  first/last_step follow the
-   * hatch clamping rules (-1 = last step).  jpos_targets is the default for
-   * every problem; thip_upload_joint_targets sets them per problem.  Nonzero
-   * upper/lower tolerances (the hinge forms JointPosIneqCost/Constraint) are
-   * rejected by thip_create. */
+   * (step, joint), trajectory_costs.cpp:137-181).  Nonzero tolerances (|tol| >=
+   * 1e-5 for some joint): JointPosIneqCost / JointPosIneqConstraint, two hinge
+   * rows per (step, joint) (trajectory_costs.cpp:66-135, 183-254).
+   * first/last_step follow the hatch clamping rules (-1 = last step).
+   * jpos_targets is the default for every problem; thip_upload_joint_targets
+   * sets them per problem. */
   int n_jpos;
   int jpos_is_cnt[THIP_MAX_JPOS];
   int jpos_first_step[THIP_MAX_JPOS];

@@ -112,6 +112,76 @@ private:
   int first_, last_;
   QuadExpr expr_;
 };
+// JointVelIneqCost (trajectory_costs.cpp:303-374): hinge rows
+// -(upper - (vel - targ)) * c and (lower - (vel - targ)) * c per (step, joint)
+class JointVelIneqCost : public Cost
+{
+public:
+  JointVelIneqCost(std::vector<VarVector> rows, DblVec coeffs, DblVec targets, DblVec upper, DblVec lower,
+                   int first_step, int last_step)
+    : Cost("JointVelIneq")
+    , rows_(std::move(rows))
+    , coeffs_(std::move(coeffs))
+    , targets_(std::move(targets))
+    , upper_(std::move(upper))
+    , lower_(std::move(lower))
+    , first_(first_step)
+    , last_(last_step)
+  {
+    if (((last_ - 1) - first_) < 0)
+      throw std::runtime_error("JointVelIneqCost, trajectory is too short!");
+    for (int i = first_; i <= last_ - 1; ++i)
+      for (std::size_t j = 0; j < coeffs_.size(); ++j)
+      {
+        AffExpr vel, expr, expr_neg;
+        exprInc(vel, exprMult(rows_[static_cast<std::size_t>(i)][j], -1));
+        exprInc(vel, exprMult(rows_[static_cast<std::size_t>(i + 1)][j], 1));
+        exprDec(vel, targets_[j]);
+        exprInc(expr, upper_[j]);
+        exprDec(expr, vel);
+        exprScale(expr, -coeffs_[j]);
+        exprs_.push_back(expr);
+        exprInc(expr_neg, lower_[j]);
+        exprDec(expr_neg, vel);
+        exprScale(expr_neg, coeffs_[j]);
+        exprs_.push_back(expr_neg);
+      }
+  }
+  double value(const DblVec& x) override
+  {
+    double s1 = 0, s2 = 0;
+    for (std::size_t j = 0; j < coeffs_.size(); ++j)
+      for (int i = first_; i <= last_ - 1; ++i)
+      {
+        const double vel = rows_[static_cast<std::size_t>(i + 1)][j].value(x) - rows_[static_cast<std::size_t>(i)][j].value(x);
+        const double d0 = vel - targets_[j];
+        s1 += std::max((d0 - upper_[j]) * coeffs_[j], 0.0);
+        s2 += std::max(((d0 * -1) + lower_[j]) * coeffs_[j], 0.0);
+      }
+    return s1 + s2;
+  }
+  ConvexObjective::Ptr convex(const DblVec&, Model* model) override
+  {
+    auto out = std::make_shared<ConvexObjective>(model);
+    for (const AffExpr& e : exprs_)
+      out->addHinge(e, 1);
+    return out;
+  }
+  VarVector getVars() override
+  {
+    VarVector v;
+    for (auto& r : rows_)
+      v.insert(v.end(), r.begin(), r.end());
+    return v;
+  }
+
+private:
+  std::vector<VarVector> rows_;
+  DblVec coeffs_, targets_, upper_, lower_;
+  int first_, last_;
+  AffExprVector exprs_;
+};
+
 // ------------------------------------------------------------ JointPos
 // JointPosEqCost / JointPosIneqCost / JointPosEqConstraint / JointPosIneqConstraint
 // (trajopt/src/trajectory_costs.cpp:28-254).  value() sums follow the Eigen
@@ -324,9 +394,10 @@ static void addJointPosTerm(TrajProblem& tp, const std::vector<VarVector>& rows,
     std::swap(first, last);
   jd.first = first;
   jd.last = last;
-  bool zero_tols = true;
+  bool zero_tols = true;  // trajopt_common::doubleEquals(tol, 0.)
   for (int j = 0; j < D; ++j)
-    zero_tols = zero_tols && jd.upper[static_cast<std::size_t>(j)] == 0.0 && jd.lower[static_cast<std::size_t>(j)] == 0.0;
+    zero_tols = zero_tols && std::fabs(jd.upper[static_cast<std::size_t>(j)]) < 1e-5 &&
+                std::fabs(jd.lower[static_cast<std::size_t>(j)]) < 1e-5;
   if (!d.jpos_is_cnt[k])
   {
     if (zero_tols)
@@ -452,8 +523,16 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
       last += 1;
     if (last < first)
       std::swap(first, last);
-    tp.prob->addCost(std::make_shared<JointVelEqCost>(rows, DblVec(d.jv_coeffs, d.jv_coeffs + D),
-                                                      DblVec(d.jv_targets, d.jv_targets + D), first, last));
+    bool zero_tols = true;
+    for (int j = 0; j < D; ++j)
+      zero_tols = zero_tols && std::fabs(d.jv_upper_tols[j]) < 1e-5 && std::fabs(d.jv_lower_tols[j]) < 1e-5;
+    if (zero_tols)
+      tp.prob->addCost(std::make_shared<JointVelEqCost>(rows, DblVec(d.jv_coeffs, d.jv_coeffs + D),
+                                                        DblVec(d.jv_targets, d.jv_targets + D), first, last));
+    else
+      tp.prob->addCost(std::make_shared<JointVelIneqCost>(
+          rows, DblVec(d.jv_coeffs, d.jv_coeffs + D), DblVec(d.jv_targets, d.jv_targets + D),
+          DblVec(d.jv_upper_tols, d.jv_upper_tols + D), DblVec(d.jv_lower_tols, d.jv_lower_tols + D), first, last));
   }
   auto makeCalc = [&](int k) {
     auto calc = std::make_shared<CartPoseCalc>();

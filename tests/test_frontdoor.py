@@ -76,8 +76,8 @@ def _doc(**over):
         (_doc(costs=[{"type": "joint_vel", "params": {"targets": [0, 0]}}]),
          "wrong number of JointVelTermInfo targets. expected 7 got 2"),
         (_doc(costs=[{"type": "joint_acc", "params": {}}]), "term type 'joint_acc' is not supported on the HIP path"),
-        (_doc(costs=[{"type": "joint_pos", "params": {"targets": [0], "upper_tols": [0.1]}}]),
-         "not supported on the HIP path"),
+        (_doc(constraints=[{"type": "joint_vel", "params": {"targets": [0]}}]),
+         "JointVelTermInfo as a constraint (JointVelEqConstraint / JointVelIneqConstraint) is not supported"),
         (_doc(costs=[{"type": "collision", "params": {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 4}}]),
          "collision evaluator_type 4 (only LVS_DISCRETE = 2) is not supported on the HIP path"),
         (_doc(costs=[{"type": "collision", "params": {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 2,

@@ -108,7 +108,17 @@ enum IArr : int
   I_HPTR,      // CSR: hinge rows starting at waypoint t (N+1)
   I_CONT,      // contact list [h_cap][3]: sub-state, sphere, primitive
   I_PCNT,      // contacts per step pair (N)
+  I_HKIND,     // hinge row kind: 0 collision (margin - dist), 1 affine (static rows) (h_cap)
+  I_HSLOT,     // affine hinge rows: merit slot (constraint) or -1 (cost, objective 1) (h_cap)
   I_COUNT
+};
+
+enum ShKind : int
+{
+  SH_JP_UP = 0,  // (x - targ - upper) * c
+  SH_JP_LO,      // (lower - (x - targ)) * c
+  SH_JV_UP,      // -(upper - (vel - targ)) * c
+  SH_JV_LO,      // (lower - (vel - targ)) * c
 };
 
 struct Layout
@@ -135,6 +145,8 @@ struct Layout
   int n_cnts;     // CartPose constraint terms + JointPos constraint terms
   int n_jpos;     // JointPos terms
   int jv_first, jv_last;
+  int jv_ineq;    // JointVelIneqCost (tolerances) instead of the quadratic JointVelEqCost
+  int hinge;      // the QP has hinge rows (collision contacts and/or static hinge rows)
   long long dstride;  // doubles per problem
   long long istride;  // ints per problem
   long long doff[A_COUNT];
@@ -177,6 +189,17 @@ struct Tables
   int* jpos_slot;
   int* jpos_row0;  // first abs row of a JointPos constraint term
   int* jpos_nrow;
+  int* jpos_ineq;  // 1: tolerance (hinge) form (JointPosIneqCost / JointPosIneqConstraint)
+  // static hinge rows (JointPos / JointVel tolerance forms, trajectory_costs.cpp:66-135,183-254,303-374),
+  // filed under step pairs after the pair's contacts; sorted by pair (CSR sh_ptr)
+  int n_sh;
+  int* sh_kind;    // ShKind
+  int* sh_owner;   // JointPos term k, or n_jpos for the JointVel term
+  int* sh_joint;
+  int* sh_step;    // waypoint of the row's first variable
+  int* sh_pair;    // step pair the row is filed under
+  int* sh_slot;    // merit slot of a constraint term (objective mu), -1 for costs (objective 1)
+  int* sh_ptr;     // CSR pair -> static rows (N+1)
   // collision model: robot spheres grouped by link in ascending link order
   // (the ContactResultMap key order of the contact scan)
   int n_groups;

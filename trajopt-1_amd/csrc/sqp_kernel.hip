@@ -322,7 +322,7 @@ __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
     GC[row] = (y - dot) * wgt;
   }
   BSYNC();
-  if (L.coll && !raw_jac)
+  if (L.hinge && !raw_jac)
     coll_scan(c, x, nullptr, true);
 }
 
@@ -447,6 +447,7 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
           CONT[3 * k + 1] = s;
           CONT[3 * k + 2] = p;
           HT[k] = t;
+          c.ia(I_HKIND)[k] = 0;
         }
       }
       running += __popcll(mask);
@@ -462,6 +463,164 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
   }
 }
 
+// Static hinge rows (JointPos / JointVel tolerance forms) into the hinge list:
+// row s of the (pair-sorted) static table goes after its pair's contacts.
+// The affine expressions are built as the reference's ctors build them
+// (trajectory_costs.cpp:66-135, 183-254, 303-374) and stored as is (kind 1):
+// row aff(x) - h <= 0.  Constant across SQP iterations.
+__device__ void static_hinge_rows(Ctx& c, const int* HP)
+{
+  const Layout& L = c.L;
+  const int D = L.D;
+  const int* PCNT = c.ia(I_PCNT);
+  int *HT = c.ia(I_HT), *HM = c.ia(I_HMASK), *HKD = c.ia(I_HKIND), *HSL = c.ia(I_HSLOT);
+  double *HC0 = c.a(A_HC0), *HK = c.a(A_HK);
+  FOR(sr, c.T.n_sh)
+  {
+    const int p = c.T.sh_pair[sr];
+    const int ncoll = (L.coll && p >= L.coll_first && p < L.coll_last) ? PCNT[p] : 0;
+    const int h = HP[p] + ncoll + (sr - c.T.sh_ptr[p]);
+    const int kind = c.T.sh_kind[sr], k = c.T.sh_owner[sr], j = c.T.sh_joint[sr], t = c.T.sh_step[sr];
+    double* a = HC0 + h * 2 * D;
+    for (int e = 0; e < 2 * D; ++e)
+      a[e] = 0.0;
+    double cst;
+    int mask;
+    if (kind == SH_JP_UP || kind == SH_JP_LO)
+    {
+      const double cf = c.d->jpos_coeffs[k][j], tg = c.jpt[k * D + j];
+      const int e = (t - p) * D + j;
+      mask = 1 << e;
+      if (kind == SH_JP_UP)
+      {
+        // expr = pos - upper_tol, scaled: pos = x - targ
+        a[e] = 1.0 * cf;
+        cst = ((0.0 - tg) - c.d->jpos_upper_tols[k][j]) * cf;
+      }
+      else
+      {
+        // expr = lower_tol - pos, scaled
+        a[e] = -1.0 * cf;
+        cst = (c.d->jpos_lower_tols[k][j] - (0.0 - tg)) * cf;
+      }
+    }
+    else
+    {
+      // vel = -x_t + x_t+1 - targ
+      const double cf = c.d->jv_coeffs[j], tg = c.d->jv_targets[j];
+      mask = (1 << j) | (1 << (D + j));
+      if (kind == SH_JV_UP)
+      {
+        // expr = (upper_tol - vel) * -coeff
+        a[j] = 1.0 * -cf;
+        a[D + j] = -1.0 * -cf;
+        cst = (c.d->jv_upper_tols[j] - (0.0 - tg)) * -cf;
+      }
+      else
+      {
+        // expr = (lower_tol - vel) * coeff
+        a[j] = 1.0 * cf;
+        a[D + j] = -1.0 * cf;
+        cst = (c.d->jv_lower_tols[j] - (0.0 - tg)) * cf;
+      }
+    }
+    HK[h] = cst;
+    HM[h] = mask;
+    HT[h] = p;
+    HKD[h] = 1;
+    HSL[h] = c.T.sh_slot[sr];
+  }
+}
+
+// Exact values of the static hinge terms at x: JointVelIneqCost::value
+// (trajectory_costs.cpp:348-361), JointPosIneqCost::value (:97-110) and
+// JointPosIneqConstraint::value + INEQ violation (:216-233, modeling.cpp:151-170).
+__device__ void sh_values(Ctx& c, const double* x, double* costs, double* viols)
+{
+  const Layout& L = c.L;
+  const int D = L.D;
+  if (L.jv_ineq)
+  {
+    const int nv = (L.jv_last - L.jv_first) * D;
+    double s1 = 0, s2 = 0;
+    FOR(i, nv)
+    {
+      const int t = L.jv_first + i / D, j = i % D;
+      const double cf = c.d->jv_coeffs[j];
+      const double d0 = (x[(t + 1) * D + j] - x[t * D + j]) - c.d->jv_targets[j];
+      s1 += fmax((d0 - c.d->jv_upper_tols[j]) * cf, 0.0);
+      s2 += fmax(((d0 * -1) + c.d->jv_lower_tols[j]) * cf, 0.0);
+    }
+    s1 = block_sum(c, s1);
+    s2 = block_sum(c, s2);
+    if (c.tid == 0)
+      costs[0] = s1 + s2;
+  }
+  for (int k = 0; k < L.n_jpos; ++k)
+  {
+    if (!c.T.jpos_ineq[k])
+      continue;
+    const int f = c.T.jpos_first[k], n = (c.T.jpos_last[k] - f + 1) * D;
+    double s1 = 0, s2 = 0;
+    FOR(i, n)
+    {
+      const int t = f + i / D, j = i % D;
+      const double cf = c.d->jpos_coeffs[k][j];
+      const double d0 = x[t * D + j] - c.jpt[k * D + j];
+      s1 += fmax((d0 - c.d->jpos_upper_tols[k][j]) * cf, 0.0);
+      s2 += fmax(((d0 * -1) + c.d->jpos_lower_tols[k][j]) * cf, 0.0);
+    }
+    s1 = block_sum(c, s1);
+    s2 = block_sum(c, s2);
+    if (c.tid == 0)
+      (c.d->jpos_is_cnt[k] ? viols : costs)[c.T.jpos_slot[k]] = s1 + s2;
+  }
+}
+
+// Model values of the static hinge terms at the QP solution SX: costs are
+// sum 1 * h (ConvexObjective::value of addHinge(expr, 1)), constraints sum
+// pospart(aff(x)) (ConvexConstraints::violation).
+__device__ void sh_model_values(Ctx& c, const double* SX, double* mcost, double* mviol)
+{
+  const Layout& L = c.L;
+  const int D = L.D;
+  if (c.T.n_sh == 0)
+    return;
+  const int* HP = c.ia(I_HPTR);
+  const int* PCNT = c.ia(I_PCNT);
+  const int* HMv = c.ia(I_HMASK);
+  const double *HC0 = c.a(A_HC0), *HKv = c.a(A_HK);
+  for (int o = 0; o <= L.n_jpos; ++o)
+  {
+    const bool jv = (o == L.n_jpos);
+    if (jv ? !L.jv_ineq : !c.T.jpos_ineq[o])
+      continue;
+    const bool cnt = !jv && c.d->jpos_is_cnt[o];
+    double v = 0;
+    FOR(sr, c.T.n_sh)
+    {
+      if (c.T.sh_owner[sr] != o)
+        continue;
+      const int p = c.T.sh_pair[sr];
+      const int ncoll = (L.coll && p >= L.coll_first && p < L.coll_last) ? PCNT[p] : 0;
+      const int h = HP[p] + ncoll + (sr - c.T.sh_ptr[p]);
+      if (!cnt)
+        v += SX[L.nc_base + h];
+      else
+      {
+        double a = HKv[h];
+        for (int e = 0; e < 2 * D; ++e)
+          if (HMv[h] & (1 << e))
+            a += HC0[h * 2 * D + e] * SX[(p + e / D) * D + e % D];
+        v += fmax(a, 0.0);
+      }
+    }
+    v = block_sum(c, v);
+    if (c.tid == 0)
+      (cnt ? mviol : mcost)[jv ? 0 : c.T.jpos_slot[o]] = v;
+  }
+}
+
 // Collision costs at x (Cost::value of each step-pair term); with rows, also
 // the linearised hinge rows of the QP (CollisionCost::convex) at x.
 __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
@@ -472,12 +631,15 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
   if (c.tid == 0)
     c.s->coll_overflow = 0;
   BSYNC();
-  coll_scan_pairs<0>(c, x, nullptr);
-  BSYNC();
-  if (costs)
-    FOR(k, L.coll_last - L.coll_first) costs[L.coll_cost0 + k] = c.a(A_HCOST)[L.coll_first + k];
-  if (c.tid == 0 && c.s->coll_overflow)
-    c.s->flags |= THIP_FLAG_CONTACT_OVERFLOW;
+  if (L.coll)
+  {
+    coll_scan_pairs<0>(c, x, nullptr);
+    BSYNC();
+    if (costs)
+      FOR(k, L.coll_last - L.coll_first) costs[L.coll_cost0 + k] = c.a(A_HCOST)[L.coll_first + k];
+    if (c.tid == 0 && c.s->coll_overflow)
+      c.s->flags |= THIP_FLAG_CONTACT_OVERFLOW;
+  }
   if (!rows)
   {
     BSYNC();
@@ -486,12 +648,15 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
   int* HP = c.ia(I_HPTR);
   if (c.tid == 0)
   {
+    // per pair: its contacts, then its static hinge rows
     int acc = 0;
     for (int t = 0; t <= L.N; ++t)
     {
       HP[t] = acc;
-      if (t >= L.coll_first && t < L.coll_last)
+      if (L.coll && t >= L.coll_first && t < L.coll_last)
         acc += PCNT[t];
+      if (t < L.N)
+        acc += c.T.sh_ptr[t + 1] - c.T.sh_ptr[t];
     }
     if (acc > L.h_cap)
     {
@@ -514,16 +679,23 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
     BSYNC();
     return;
   }
-  coll_scan_pairs<1>(c, x, HP);
+  static_hinge_rows(c, HP);
+  if (L.coll)
+    coll_scan_pairs<1>(c, x, HP);
   BSYNC();
+  if (!L.coll)
+    return;
   // rows: distance expression k + a_t.x_t + a_t+1.x_t+1 per contact
   const thip_chain& ch = c.d->chain;
   const int* CONT = c.ia(I_CONT);
   const int* HT = c.ia(I_HT);
+  const int* HKD = c.ia(I_HKIND);
   double *HC0 = c.a(A_HC0), *HK = c.a(A_HK);
   int* HM = c.ia(I_HMASK);
   FOR(k, c.s->n_h)
   {
+    if (HKD[k] != 0)
+      continue;
     const int t = HT[k], i = CONT[3 * k + 0], s = CONT[3 * k + 1], p = CONT[3 * k + 2];
     const double* q0 = x + t * D;
     const double* q1 = x + (t + 1) * D;
@@ -602,6 +774,8 @@ __device__ void jpos_values(Ctx& c, const double* x, double* costs, double* viol
   const int D = L.D;
   for (int k = 0; k < L.n_jpos; ++k)
   {
+    if (c.T.jpos_ineq[k])
+      continue;  // sh_values
     const int f = c.T.jpos_first[k], n = (c.T.jpos_last[k] - f + 1) * D;
     const bool cnt = c.d->jpos_is_cnt[k] != 0;
     double v = 0;
@@ -630,7 +804,7 @@ __device__ void evaluate(Ctx& c, const double* x, double* costs, double* viols)
   const thip_chain& ch = c.d->chain;
   // JointVel: sum_{t,j} c_j (x_{t+1,j} - x_{t,j} - targ_j)^2
   double jv = 0;
-  if (c.d->jv_enabled)
+  if (c.d->jv_enabled && !L.jv_ineq)
   {
     const int nv = (L.jv_last - L.jv_first) * D;
     FOR(i, nv)
@@ -641,7 +815,7 @@ __device__ void evaluate(Ctx& c, const double* x, double* costs, double* viols)
     }
   }
   jv = block_sum(c, jv);
-  if (c.tid == 0 && c.d->jv_enabled)
+  if (c.tid == 0 && c.d->jv_enabled && !L.jv_ineq)
     costs[0] = jv;
   const double* tgt = c.a(A_TGT);
   FOR(k, L.n_cart)
@@ -674,6 +848,7 @@ __device__ void evaluate(Ctx& c, const double* x, double* costs, double* viols)
   }
   BSYNC();
   jpos_values(c, x, costs, viols);
+  sh_values(c, x, costs, viols);
   if (L.coll)
     coll_scan(c, x, L.coll_cnt ? viols : costs, false);
 }
@@ -735,7 +910,7 @@ __device__ void build_and_scale(Ctx& c)
   {
     const int t = col / D, j = col % D;
     double pd = 0, po = 0, q = 0;
-    if (c.d->jv_enabled)
+    if (c.d->jv_enabled && !L.jv_ineq)
     {
       const double cj = c.d->jv_coeffs[j], tg = c.d->jv_targets[j];
       const bool prev = (t - 1 >= L.jv_first) && (t - 1 <= L.jv_last - 1);
@@ -765,7 +940,7 @@ __device__ void build_and_scale(Ctx& c)
     }
     // JointPosEqCost: exprSquare(x - targ) * c -> P diagonal 2c, q -2 targ c (trajectory_costs.cpp:40-51)
     for (int k = 0; k < L.n_jpos; ++k)
-      if (!c.d->jpos_is_cnt[k] && t >= c.T.jpos_first[k] && t <= c.T.jpos_last[k])
+      if (!c.d->jpos_is_cnt[k] && !c.T.jpos_ineq[k] && t >= c.T.jpos_first[k] && t <= c.T.jpos_last[k])
       {
         const double cj = c.d->jpos_coeffs[k][j];
         pd += cj + cj;
@@ -803,19 +978,25 @@ __device__ void build_and_scale(Ctx& c)
     double *HC = c.a(A_HC), *HW = c.a(A_HW);
     // constraint form (CollisionConstraint::convex + cntsToCosts): row exprMult(margin - dist, coeff) - h <= 0,
     // objective mu_pair * h (collision_terms.cpp:1347-1364, optimizers.cpp:59-81)
-    if (L.coll_cnt)
+    // static rows (kind 1) are stored as the affine expression itself: addHinge(aff, 1) for
+    // costs, cntsToCosts' addHinge(aff, mu) for constraints
+    const int *HTq = c.ia(I_HT), *HKDq = c.ia(I_HKIND), *HSLq = c.ia(I_HSLOT);
     {
       const double cf = c.d->coll_coeff;
-      FOR(e, nh * 2 * D) HC[e] = (-HC0[e]) * cf;
+      FOR(e, nh * 2 * D)
+      {
+        const int h = e / (2 * D);
+        HC[e] = HKDq[h] ? HC0[e] : (L.coll_cnt ? (-HC0[e]) * cf : -HC0[e]);
+      }
     }
-    else
-      FOR(e, nh * 2 * D) HC[e] = -HC0[e];
-    const int* HTq = c.ia(I_HT);
     FOR(h, nh)
     {
       HW[h] = -1.0;
       const int col = L.nc_base + h;
-      Q[col] = L.coll_cnt ? MU[L.coll_cost0 + HTq[h] - L.coll_first] : c.d->coll_coeff;
+      if (HKDq[h])
+        Q[col] = HSLq[h] >= 0 ? MU[HSLq[h]] : 1.0;
+      else
+        Q[col] = L.coll_cnt ? MU[L.coll_cost0 + HTq[h] - L.coll_first] : c.d->coll_coeff;
       DS[col] = 1.0;
       BS[col] = 1.0;
     }
@@ -1118,7 +1299,7 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
     }
     KB[e] = v;
   }
-  if (L.coll)
+  if (L.hinge)
   {
     // dense couplings K_{t+1,t} = diag(PO_t) + sum_h rho_eff a_t+1 a_t^T
     double* CPL = c.a(A_CPL);
@@ -1184,7 +1365,7 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
           sv.M[t * DD + e] = v;
         }
       wave_sync();
-      if (!L.coll)
+      if (!L.hinge)
         for (int e = c.lane; e < DD; e += 64)
         {
           const int i = e / D, q = e % D;
@@ -2689,8 +2870,11 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
     {
       // ineq row viol - h <= 0: l = -inf, u = -(margin - k) (osqp_interface.cpp:213-281)
       lo = -kInf;
-      up = L.coll_cnt ? -((c.d->coll_margin - c.a(A_HK)[idx]) * c.d->coll_coeff)
-                      : -(c.d->coll_margin - c.a(A_HK)[idx]);
+      if (c.ia(I_HKIND)[idx])
+        up = -c.a(A_HK)[idx];  // affine row aff - h <= 0
+      else
+        up = L.coll_cnt ? -((c.d->coll_margin - c.a(A_HK)[idx]) * c.d->coll_coeff)
+                        : -(c.d->coll_margin - c.a(A_HK)[idx]);
     }
     else
     {
@@ -3025,13 +3209,13 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
       }
       // convexify
       linearize(c, X);
-      if (L.coll)
+      if (L.hinge)
         plan_lds_dynamic(c);
       build_and_scale(c);
       // pattern of A (jacobian drops) vs previous QP setup
       double diff[1] = { 0 };
       FOR(r, L.n_abs) if (mask[r] != pmask[r]) diff[0] = 1.0;
-      if (L.coll)
+      if (L.hinge)
       {
         // hinge rows: same count, start steps and kept coefficients
         // (OSQPModel compares the CSC pattern of A bytewise)
@@ -3047,7 +3231,7 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
       block_max<1>(c, diff);
       bool pattern_equal = have_prev_setup && diff[0] == 0.0;
       FOR(r, L.n_abs) pmask[r] = mask[r];
-      if (L.coll)
+      if (L.hinge)
       {
         const int *HT = c.ia(I_HT), *HM = c.ia(I_HMASK);
         int *PHT = c.ia(I_PHT), *PHM = c.ia(I_PHMASK);
@@ -3098,7 +3282,7 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
         BSYNC();
         // JointVel model value (quadratic, exact), CartPose model values
         double jvm = 0;
-        if (c.d->jv_enabled)
+        if (c.d->jv_enabled && !L.jv_ineq)
         {
           const int nv = (L.jv_last - L.jv_first) * D;
           FOR(i, nv)
@@ -3111,14 +3295,15 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
         jvm = block_sum(c, jvm);
         double* mcost = c.big;                 // [n_costs]
         double* mviol = c.big + L.n_costs;     // [n_cnts]
-        if (c.tid == 0 && c.d->jv_enabled)
+        if (c.tid == 0 && c.d->jv_enabled && !L.jv_ineq)
           mcost[0] = jvm;
         const double *G = c.a(A_G), *GC = c.a(A_GC);
         // JointPos: costs are quadratic (model = exact value), constraint
         // rows are abs rows like CartPose constraint rows (below)
+        sh_model_values(c, SX, mcost, mviol);
         for (int k = 0; k < L.n_jpos; ++k)
         {
-          if (c.d->jpos_is_cnt[k])
+          if (c.d->jpos_is_cnt[k] || c.T.jpos_ineq[k])
             continue;
           const int f = c.T.jpos_first[k], n = (c.T.jpos_last[k] - f + 1) * D;
           double v = 0;
@@ -3136,7 +3321,7 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
         {
           const bool jp = k >= L.n_cart;
           const int kk = jp ? k - L.n_cart : k;
-          if (jp && !c.d->jpos_is_cnt[kk])
+          if (jp && (!c.d->jpos_is_cnt[kk] || c.T.jpos_ineq[kk]))
             continue;
           const int r0 = jp ? c.T.jpos_row0[kk] : c.T.term_row0[k], nr = jp ? c.T.jpos_nrow[kk] : c.T.term_nrow[k];
           double v = 0;
@@ -3178,9 +3363,12 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
               // ConvexConstraints::violation: sum pospart(aff(x)), aff = exprMult(margin - dist, coeff)
               const double *HC0 = c.a(A_HC0), *HKv = c.a(A_HK);
               const int* HMv = c.ia(I_HMASK);
+              const int* HKD = c.ia(I_HKIND);
               const double cf = c.d->coll_coeff;
               for (int h = HP[t]; h < HP[t + 1]; ++h)
               {
+                if (HKD[h])
+                  continue;
                 double a = (c.d->coll_margin - HKv[h]) * cf;
                 for (int e = 0; e < 2 * D; ++e)
                   if (HMv[h] & (1 << e))
@@ -3191,8 +3379,10 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
             }
             else
             {
+              const int* HKD = c.ia(I_HKIND);
               for (int h = HP[t]; h < HP[t + 1]; ++h)
-                v += c.d->coll_coeff * SX[L.nc_base + h];
+                if (!HKD[h])
+                  v += c.d->coll_coeff * SX[L.nc_base + h];
               mcost[L.coll_cost0 + k] = v;
             }
           }
@@ -3329,7 +3519,7 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
   for (int k = threadIdx.x; k < A_COUNT; k += kBlock)
     ptab[k] = L.loff[k] >= 0 ? dyn + L.loff[k] : wsb + L.doff[k];
   Ctx c(L, args.T, args.desc, wsb, args.iws + (long long)b * L.istride, dyn, &ctl, ptab);
-  c.ptab_w = L.coll ? ptab : nullptr;
+  c.ptab_w = L.hinge ? ptab : nullptr;
   c.scene = args.scene ? args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16 : nullptr;
   c.jpt = args.jpt + (long long)b * (L.n_jpos > 0 ? L.n_jpos : 1) * L.D;
   Solver sv;
@@ -3484,11 +3674,17 @@ __global__ __launch_bounds__(kBlock) void coll_rows_kernel(KernelArgs args, cons
   const int* HM = c.ia(I_HMASK);
   const double *HC0 = c.a(A_HC0), *HK = c.a(A_HK), *HD = c.a(A_HDIST);
   double* ob = out + (long long)b * cap * W;
-  FOR(k, ctl.n_h < cap ? ctl.n_h : cap)
+  const int* HKD = c.ia(I_HKIND);
+  FOR(k, ctl.n_h)
   {
+    if (HKD[k] != 0)
+      continue;  // static hinge rows follow each pair's contacts
     const int t = HT[k], i = CONT[3 * k];
+    const int o = k - c.T.sh_ptr[t];
+    if (o >= cap)
+      continue;
     const int cnt = lvs_count(XN + t * D, XN + (t + 1) * D, D, args.desc->coll_lvs);
-    double* r = ob + (long long)k * W;
+    double* r = ob + (long long)o * W;
     r[0] = t;
     r[1] = args.desc->sphere_link[CONT[3 * k + 1]];
     r[2] = CONT[3 * k + 2];
@@ -3502,7 +3698,7 @@ __global__ __launch_bounds__(kBlock) void coll_rows_kernel(KernelArgs args, cons
     r[8 + 2 * D] = HK[k];
   }
   if (threadIdx.x == 0)
-    counts[b] = (ctl.flags & THIP_FLAG_CONTACT_OVERFLOW) ? -1 : ctl.n_h;
+    counts[b] = (ctl.flags & THIP_FLAG_CONTACT_OVERFLOW) ? -1 : ctl.n_h - c.T.n_sh;
 }
 
 }  // namespace thip

@@ -160,12 +160,9 @@ static int validate(const thip_problem_desc* d, std::string& why)
   for (int k = 0; k < d->n_jpos; ++k)
     for (int j = 0; j < ch.n_dof; ++j)
     {
-      if (d->jpos_upper_tols[k][j] != 0.0 || d->jpos_lower_tols[k][j] != 0.0)
-        return why = "JointPos terms with nonzero tolerances (JointPosIneqCost / JointPosIneqConstraint) are not "
-                     "supported yet",
-               THIP_E_INVALID;
-      if (!std::isfinite(d->jpos_coeffs[k][j]) || !std::isfinite(d->jpos_targets[k][j]))
-        return why = "JointPos coeffs / targets must be finite", THIP_E_INVALID;
+      if (!std::isfinite(d->jpos_coeffs[k][j]) || !std::isfinite(d->jpos_targets[k][j]) ||
+          !std::isfinite(d->jpos_upper_tols[k][j]) || !std::isfinite(d->jpos_lower_tols[k][j]))
+        return why = "JointPos coeffs / targets / tolerances must be finite", THIP_E_INVALID;
     }
   if (d->coll_enabled)
   {
@@ -241,6 +238,18 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     std::swap(first, last);
   L.jv_first = first;
   L.jv_last = last;
+  // zero tolerances: trajopt_common::doubleEquals(tol, 0.) (problem_description.cpp:1135-1138,1249-1252)
+  auto zero_tol = [](double v) { return std::fabs(v) < 1e-5; };
+  L.jv_ineq = 0;
+  if (d.jv_enabled)
+    for (int j = 0; j < L.D; ++j)
+      if (!zero_tol(d.jv_upper_tols[j]) || !zero_tol(d.jv_lower_tols[j]))
+        L.jv_ineq = 1;
+  std::vector<int> jpos_ineq(THIP_MAX_JPOS, 0);
+  for (int k = 0; k < d.n_jpos; ++k)
+    for (int j = 0; j < L.D; ++j)
+      if (!zero_tol(d.jpos_upper_tols[k][j]) || !zero_tol(d.jpos_lower_tols[k][j]))
+        jpos_ineq[static_cast<size_t>(k)] = 1;
   // CartPose rows: cost terms first (convexifyCosts order), then constraint terms (cntsToCosts)
   std::vector<int> row_term, row_comp, row_step, term_row0(THIP_MAX_CART, 0), term_nrow(THIP_MAX_CART, 0),
       term_slot(THIP_MAX_CART, 0);
@@ -297,6 +306,8 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     if (!d.jpos_is_cnt[k])
       continue;
     jpos_slot[static_cast<size_t>(k)] = n_cnts++;
+    if (jpos_ineq[static_cast<size_t>(k)])
+      continue;  // hinge rows (static hinge table below), no abs rows
     jpos_row0[static_cast<size_t>(k)] = static_cast<int>(row_term.size());
     for (int t = jpos_first[static_cast<size_t>(k)]; t <= jpos_last[static_cast<size_t>(k)]; ++t)
       for (int j = 0; j < L.D; ++j)
@@ -315,6 +326,60 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   for (int r = 0; r < L.n_abs; ++r)
     if (row_slot[static_cast<size_t>(r)] < 0)
       L.n_abs_cost++;
+  // static hinge rows: JointVelIneqCost (owner n_jpos, cost slot 0) and the
+  // JointPos tolerance terms; a row on waypoint t alone is filed under pair
+  // min(t, N-2) (second half when t = N-1), a velocity row under pair t
+  std::vector<int> sh_kind, sh_owner, sh_joint, sh_step, sh_pair, sh_slot;
+  auto add_sh = [&](int kind, int owner, int j, int t, int pair, int slot) {
+    sh_kind.push_back(kind);
+    sh_owner.push_back(owner);
+    sh_joint.push_back(j);
+    sh_step.push_back(t);
+    sh_pair.push_back(pair);
+    sh_slot.push_back(slot);
+  };
+  if (L.jv_ineq)
+    for (int t = L.jv_first; t <= L.jv_last - 1; ++t)
+      for (int j = 0; j < L.D; ++j)
+      {
+        add_sh(SH_JV_UP, d.n_jpos, j, t, t, -1);
+        add_sh(SH_JV_LO, d.n_jpos, j, t, t, -1);
+      }
+  for (int k = 0; k < d.n_jpos; ++k)
+  {
+    if (!jpos_ineq[static_cast<size_t>(k)])
+      continue;
+    const int slot = d.jpos_is_cnt[k] ? jpos_slot[static_cast<size_t>(k)] : -1;
+    for (int t = jpos_first[static_cast<size_t>(k)]; t <= jpos_last[static_cast<size_t>(k)]; ++t)
+      for (int j = 0; j < L.D; ++j)
+      {
+        add_sh(SH_JP_UP, k, j, t, std::min(t, L.N - 2), slot);
+        add_sh(SH_JP_LO, k, j, t, std::min(t, L.N - 2), slot);
+      }
+  }
+  const int n_sh = static_cast<int>(sh_kind.size());
+  std::vector<int> sh_ptr(static_cast<size_t>(L.N + 1), 0), sh_order(static_cast<size_t>(n_sh));
+  for (int s2 = 0; s2 < n_sh; ++s2)
+    sh_ptr[static_cast<size_t>(sh_pair[static_cast<size_t>(s2)] + 1)]++;
+  for (int t = 0; t < L.N; ++t)
+    sh_ptr[static_cast<size_t>(t + 1)] += sh_ptr[static_cast<size_t>(t)];
+  {
+    std::vector<int> nxt(sh_ptr.begin(), sh_ptr.end() - 1);
+    for (int s2 = 0; s2 < n_sh; ++s2)
+      sh_order[static_cast<size_t>(nxt[static_cast<size_t>(sh_pair[static_cast<size_t>(s2)])]++)] = s2;
+  }
+  auto permute = [&](std::vector<int>& v) {
+    std::vector<int> o(v.size());
+    for (size_t i = 0; i < v.size(); ++i)
+      o[i] = v[static_cast<size_t>(sh_order[i])];
+    v.swap(o);
+  };
+  permute(sh_kind);
+  permute(sh_owner);
+  permute(sh_joint);
+  permute(sh_step);
+  permute(sh_pair);
+  permute(sh_slot);
   // collision: one cost term per step pair after the CartPose costs
   // (cost_infos order; CollisionTermInfo::hatch, problem_description.cpp:1747)
   L.coll = d.coll_enabled ? 1 : 0;
@@ -340,6 +405,8 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   }
   else
     L.h_cap = 0;
+  L.h_cap += n_sh;
+  L.hinge = (L.h_cap > 0) ? 1 : 0;
   L.n_costs = n_costs;
   L.n_cnts = n_cnts;
   L.nc_base = L.nx + 2 * L.n_abs;
@@ -388,14 +455,14 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   sizes[A_PS] = sizes[A_PR] = nc + m;
   sizes[A_HC0] = sizes[A_HC] = hc * 2 * D;
   sizes[A_HK] = sizes[A_HW] = sizes[A_HRE] = sizes[A_HDIST] = hc;
-  sizes[A_CPL] = L.coll ? NDD : 1;
+  sizes[A_CPL] = L.hinge ? NDD : 1;
   sizes[A_CSCR] = L.coll ? (long long)kWaves * kSubCap * d.n_spheres * 3 : 1;
   sizes[A_HCOST] = L.N;
-  sizes[A_HPK] = L.coll ? hc * kHPack : 1;
+  sizes[A_HPK] = L.hinge ? hc * kHPack : 1;
   const long long nchk_cap = hc / kHChunk + L.N + 1;
-  sizes[A_HCHK] = L.coll ? nchk_cap : 1;
-  sizes[A_HPART] = L.coll ? nchk_cap * 16 : 1;
-  sizes[A_HCT] = L.coll ? 2 * D * (hc + 1) : 1;
+  sizes[A_HCHK] = L.hinge ? nchk_cap : 1;
+  sizes[A_HPART] = L.hinge ? nchk_cap * 16 : 1;
+  sizes[A_HCT] = L.hinge ? 2 * D * (hc + 1) : 1;
   for (int k = 0; k < A_COUNT; ++k)
     if (sizes[k] < 0)
     {
@@ -417,6 +484,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   isizes[I_HPTR] = L.N + 1;
   isizes[I_CONT] = 3 * hc;
   isizes[I_PCNT] = L.N;
+  isizes[I_HKIND] = isizes[I_HSLOT] = hc;
   long long ioff = 0;
   for (int k = 0; k < I_COUNT; ++k)
   {
@@ -467,7 +535,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
       return THIP_E_INVALID;
     }
     ctx->lds_bytes = static_cast<size_t>(used) * sizeof(double);
-    if (L.coll)
+    if (L.hinge)
     {
       // collision: the kernel re-plans residency for every QP with the
       // actual contact count (plan_lds_dynamic, same priority order, so
@@ -507,6 +575,11 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
                o_ts = push(term_slot, THIP_MAX_CART);
   const size_t o_fs = push(fixed_of_step, static_cast<size_t>(L.N));
   const size_t o_rsl = push(row_slot, na), o_rjp = push(row_jpos, na);
+  const size_t o_jq = push(jpos_ineq, THIP_MAX_JPOS);
+  const size_t nsh = static_cast<size_t>(n_sh);
+  const size_t o_shk = push(sh_kind, nsh), o_sho = push(sh_owner, nsh), o_shj = push(sh_joint, nsh),
+               o_shs = push(sh_step, nsh), o_shp = push(sh_pair, nsh), o_shl = push(sh_slot, nsh),
+               o_shq = push(sh_ptr, static_cast<size_t>(L.N + 1));
   const size_t o_jf = push(jpos_first, THIP_MAX_JPOS), o_jl = push(jpos_last, THIP_MAX_JPOS),
                o_js = push(jpos_slot, THIP_MAX_JPOS), o_j0 = push(jpos_row0, THIP_MAX_JPOS),
                o_jn = push(jpos_nrow, THIP_MAX_JPOS);
@@ -561,6 +634,15 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   T.jpos_slot = ctx->d_tables + o_js;
   T.jpos_row0 = ctx->d_tables + o_j0;
   T.jpos_nrow = ctx->d_tables + o_jn;
+  T.jpos_ineq = ctx->d_tables + o_jq;
+  T.n_sh = n_sh;
+  T.sh_kind = ctx->d_tables + o_shk;
+  T.sh_owner = ctx->d_tables + o_sho;
+  T.sh_joint = ctx->d_tables + o_shj;
+  T.sh_step = ctx->d_tables + o_shs;
+  T.sh_pair = ctx->d_tables + o_shp;
+  T.sh_slot = ctx->d_tables + o_shl;
+  T.sh_ptr = ctx->d_tables + o_shq;
   T.n_groups = static_cast<int>(grp_link.size());
   T.grp_link = ctx->d_tables + o_gl;
   T.grp_s0 = ctx->d_tables + o_g0;

@@ -470,10 +470,8 @@ void JointPosTermInfo::hatch(TrajOptProb& prob)
   checkParameterSize(targets, n_dof, "JointPosTermInfo targets", true);
   checkParameterSize(upper_tols, n_dof, "JointPosTermInfo upper_tols", true);
   checkParameterSize(lower_tols, n_dof, "JointPosTermInfo lower_tols", true);
-  const bool zero_tols = std::all_of(upper_tols.begin(), upper_tols.end(), [](double i) { return doubleEquals(i, 0.); }) &&
-                         std::all_of(lower_tols.begin(), lower_tols.end(), [](double i) { return doubleEquals(i, 0.); });
-  if (!zero_tols)
-    unsupported("JointPosTermInfo with tolerances (JointPosIneqCost / JointPosIneqConstraint)");
+  // zero tolerances -> JointPosEq*, otherwise JointPosIneq* (thip_create applies the same
+  // doubleEquals(tol, 0.) rule to the lowered tolerances)
   thip_problem_desc& d = prob.desc();
   if (d.n_jpos >= THIP_MAX_JPOS)
     unsupported("more than " + std::to_string(THIP_MAX_JPOS) + " JointPos terms");
@@ -484,6 +482,8 @@ void JointPosTermInfo::hatch(TrajOptProb& prob)
   for (unsigned j = 0; j < n_dof; ++j)
   {
     d.jpos_coeffs[k][j] = coeffs[j];
+    d.jpos_upper_tols[k][j] = upper_tols[j];
+    d.jpos_lower_tols[k][j] = lower_tols[j];
     d.jpos_targets[k][j] = 0.0;  // per problem: TrajOptProb::jpos_targets
     prob.jpos_targets.push_back(targets[j]);
   }
@@ -521,14 +521,10 @@ void JointVelTermInfo::hatch(TrajOptProb& prob)
   checkParameterSize(targets, n_dof, "JointVelTermInfo targets", true);
   checkParameterSize(upper_tols, n_dof, "JointVelTermInfo upper_tols", true);
   checkParameterSize(lower_tols, n_dof, "JointVelTermInfo lower_tols", true);
-  const bool zero_tols = std::all_of(upper_tols.begin(), upper_tols.end(), [](double i) { return doubleEquals(i, 0.); }) &&
-                         std::all_of(lower_tols.begin(), lower_tols.end(), [](double i) { return doubleEquals(i, 0.); });
   if (any(term_type & TermType::TT_USE_TIME))
     unsupported("JointVelTermInfo with use_time");
   if (!any(term_type & TermType::TT_COST))
     unsupported("JointVelTermInfo as a constraint (JointVelEqConstraint / JointVelIneqConstraint)");
-  if (!zero_tols)
-    unsupported("JointVelTermInfo with tolerances (JointVelIneqCost)");
   thip_problem_desc& d = prob.desc();
   if (d.jv_enabled)
     unsupported("more than one joint_vel cost");
@@ -539,6 +535,8 @@ void JointVelTermInfo::hatch(TrajOptProb& prob)
   {
     d.jv_coeffs[j] = coeffs[j];
     d.jv_targets[j] = targets[j];
+    d.jv_upper_tols[j] = upper_tols[j];  // nonzero: JointVelIneqCost
+    d.jv_lower_tols[j] = lower_tols[j];
   }
 }
 

@@ -100,6 +100,8 @@ class ProblemDesc(C.Structure):
         ("jv_last_step", C.c_int),
         ("jv_coeffs", C.c_double * MAX_DOF),
         ("jv_targets", C.c_double * MAX_DOF),
+        ("jv_upper_tols", C.c_double * MAX_DOF),
+        ("jv_lower_tols", C.c_double * MAX_DOF),
         ("n_cart", C.c_int),
         ("cart_step", C.c_int * MAX_CART),
         ("cart_is_cnt", C.c_int * MAX_CART),
