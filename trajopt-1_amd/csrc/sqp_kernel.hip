@@ -1847,6 +1847,71 @@ __device__ __forceinline__ double row_ax(const Ctx& c, int r, const double* x)
   return v;
 }
 
+// Hinge chunk table: chunks of kHChunk rows inside each step pair
+// (c.s->hcp: first chunk of each pair; A_HCHK: (first row, end row)).
+// Returns the chunk count.  Also used by the ADMM segment.
+__device__ int build_hinge_chunks(Ctx& c)
+{
+  const int N = c.L.N, nh = c.s->n_h;
+  const int* HP = c.ia(I_HPTR);
+  int* CHK = reinterpret_cast<int*>(c.a(A_HCHK));
+  if (nh == 0)
+    return 0;
+  if (c.tid == 0)
+  {
+    int acc = 0;
+    for (int t = 0; t < N; ++t)
+    {
+      c.s->hcp[t] = acc;
+      acc += (HP[t + 1] - HP[t] + kHChunk - 1) / kHChunk;
+    }
+    c.s->hcp[N] = acc;
+  }
+  BSYNC();
+  for (int t = c.tid; t < N; t += kBlock)
+  {
+    const int h1 = HP[t + 1];
+    int q = c.s->hcp[t];
+    for (int h = HP[t]; h < h1; h += kHChunk, ++q)
+    {
+      CHK[2 * q] = h;
+      CHK[2 * q + 1] = min(h + kHChunk, h1);
+    }
+  }
+  BSYNC();
+  return c.s->hcp[N];
+}
+
+// Row-parallel hinge share of A'v: A_HPART[q][k] = sum over chunk q of
+// HC[h][k] * v[hinge row h] (16 lanes per chunk, lane k = coefficient k).
+// col_aty then adds the chunk sums of its two step pairs instead of looping
+// over every hinge row of them (a serial chain of loads per column).
+__device__ void hinge_chunk_sums(Ctx& c, const double* v, int nchk)
+{
+  const int D = c.L.D, mb = c.L.m_base;
+  const double* HC = c.a(A_HC);
+  const int* CHK = reinterpret_cast<const int*>(c.a(A_HCHK));
+  double* PART = c.a(A_HPART);
+  const int k = c.tid & 15;
+  if (k < 2 * D)
+    for (int q = c.tid >> 4; q < nchk; q += kBlock / 16)
+    {
+      const int h0 = CHK[2 * q], h1 = CHK[2 * q + 1];
+      double s0 = 0, s1 = 0;
+#pragma unroll
+      for (int i = 0; i < kHChunk; i += 2)
+      {
+        const int ha = min(h0 + i, h1 - 1), hb = min(h0 + i + 1, h1 - 1);
+        const double aa = HC[ha * 2 * D + k] * v[mb + 2 * ha];
+        const double ab = HC[hb * 2 * D + k] * v[mb + 2 * hb];
+        s0 = (h0 + i < h1) ? s0 + aa : s0;
+        s1 = (h0 + i + 1 < h1) ? s1 + ab : s1;
+      }
+      PART[q * 16 + k] = s0 + s1;
+    }
+  BSYNC();
+}
+
 // (P x)_col and (A' y)_col (scaled)
 __device__ __forceinline__ double col_px(const Ctx& c, int col, const double* x)
 {
@@ -1862,7 +1927,7 @@ __device__ __forceinline__ double col_px(const Ctx& c, int col, const double* x)
     v += PO[col - D] * x[col - D];
   return v;
 }
-__device__ __forceinline__ double col_aty(const Ctx& c, int col, const double* y)
+__device__ __forceinline__ double col_aty(const Ctx& c, int col, const double* y, bool chunked = false)
 {
   const Layout& L = c.L;
   const int D = L.D;
@@ -1879,7 +1944,16 @@ __device__ __forceinline__ double col_aty(const Ctx& c, int col, const double* y
       const int a = c.T.step_rows[p];
       v += GS[a * D + j] * y[L.n_fixed_rows + a];
     }
-    if (c.s->n_h > 0)
+    if (c.s->n_h > 0 && chunked)
+    {
+      const double* PART = c.a(A_HPART);
+      for (int q = c.s->hcp[t]; q < c.s->hcp[t + 1]; ++q)
+        v += PART[q * 16 + j];
+      if (t > 0)
+        for (int q = c.s->hcp[t - 1]; q < c.s->hcp[t]; ++q)
+          v += PART[q * 16 + D + j];
+    }
+    else if (c.s->n_h > 0)
     {
       const double* HC = c.a(A_HC);
       const int* HP = c.ia(I_HPTR);
@@ -1966,10 +2040,15 @@ __device__ void compute_residuals(Ctx& c, const double* x, const double* z, cons
     v[4] = fmax(v[4], fabs(z[r]));
     v[5] = fmax(v[5], fabs(ax));
   }
+  // hinge share of A'y from row-parallel chunk sums (many contacts: the
+  // per-column loop over a step pair's hinge rows was a serial load chain)
+  const bool chunked = c.s->n_h > 0;
+  if (chunked)
+    hinge_chunk_sums(c, y, build_hinge_chunks(c));
   FOR(col, c.nc())
   {
     const double px = col_px(c, col, x);
-    const double aty = col_aty(c, col, y);
+    const double aty = col_aty(c, col, y, chunked);
     PX[col] = px;
     ATY[col] = aty;
     const double dr = Q[col] + px + aty;
@@ -2022,7 +2101,13 @@ __device__ bool is_primal_infeasible(Ctx& c, double eps)
   if (!(lhs < eps * ndy))
     return false;
   double av[1] = { 0 };
-  FOR(col, c.nc()) av[0] = fmax(av[0], fabs((1.0 / DS[col]) * col_aty(c, col, DY)));
+  const bool chunked = c.s->n_h > 0;
+  if (chunked)
+  {
+    BSYNC();  // DY rewritten above
+    hinge_chunk_sums(c, DY, build_hinge_chunks(c));
+  }
+  FOR(col, c.nc()) av[0] = fmax(av[0], fabs((1.0 / DS[col]) * col_aty(c, col, DY, chunked)));
   block_max<1>(c, av);
   return av[0] < eps * ndy;
 }
@@ -2192,7 +2277,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   const int nh = c.s->n_h;
   const int mb = L.m_base, ncb = L.nc_base;
   const double *HC = c.a(A_HC), *HW = c.a(A_HW);
-  const int *HT = c.ia(I_HT), *HP = c.ia(I_HPTR);
+  const int* HT = c.ia(I_HT);
   double* HPK = c.a(A_HPK);
 #define HP_(f) HPK[(f) * nh + h]
   // pack fields: 0 z, 1 z_bound, 2 y, 3 y_bound, 4 x (hinge variable), 5 u,
@@ -2228,31 +2313,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   // hinge chunk table: chunks of kHChunk rows inside each step pair
   int* CHK = reinterpret_cast<int*>(c.a(A_HCHK));
   double* PART = c.a(A_HPART);
-  if (nh > 0)
-  {
-    if (c.tid == 0)
-    {
-      int acc = 0;
-      for (int t = 0; t < N; ++t)
-      {
-        c.s->hcp[t] = acc;
-        acc += (HP[t + 1] - HP[t] + kHChunk - 1) / kHChunk;
-      }
-      c.s->hcp[N] = acc;
-    }
-    BSYNC();
-    for (int t = c.tid; t < N; t += kBlock)
-    {
-      const int h1 = HP[t + 1];
-      int q = c.s->hcp[t];
-      for (int h = HP[t]; h < h1; h += kHChunk, ++q)
-      {
-        CHK[2 * q] = h;
-        CHK[2 * q + 1] = min(h + kHChunk, h1);
-      }
-    }
-  }
-  const int nchk = (nh > 0) ? c.s->hcp[N] : 0;
+  const int nchk = build_hinge_chunks(c);
   if (c.tid == 0)
     c.s->cur = 0;
   // MR, the chunk table and the chunk sums are LDS-resident (qp_solve checks
@@ -2643,6 +2704,8 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
         hinge_e(lds(HPK), lds(static_cast<const double*>(HCT)), last);
       else if (pk_l)
         hinge_e(lds(HPK), gbl(static_cast<const double*>(HCT)), last);
+      else if (hct_l)
+        hinge_e(gbl(HPK), lds(static_cast<const double*>(HCT)), last);
       else
         hinge_e(gbl(HPK), gbl(static_cast<const double*>(HCT)), last);
     }
@@ -3113,7 +3176,7 @@ __device__ void plan_lds_dynamic(Ctx& c)
     const long long NDD = (long long)L.N * D * D, nab = L.n_abs > 0 ? L.n_abs : 1;
     // the ADMM segment's working set first (chains, rhs, multipliers, the
     // hinge-row pack and coefficients), then the rest as in the host plan
-    const int order[] = { A_LINV, A_CV, A_YV, A_MR, A_HPART, A_HCHK, A_HPK, A_HCT, A_HC, A_BXW, A_BA, A_HW, A_HRE, A_DG, A_GS, A_WS,
+    const int order[] = { A_LINV, A_CV, A_YV, A_MR, A_HPART, A_HCHK, A_HCT, A_HPK, A_HC, A_BXW, A_BA, A_HW, A_HRE, A_DG, A_GS, A_WS,
                           A_FS,   A_BS, A_XA0, A_XA1, A_Z0, A_Z1, A_Y, A_XT, A_PZ, A_RHO, A_L,  A_U,  A_Q,
                           A_DX,   A_DY, A_PD,  A_PO,  A_E,  A_DS, A_RE, A_CPL, A_PB, A_PS, A_PR };
     long long used = L.lds_scratch;
