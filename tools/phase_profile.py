@@ -27,6 +27,10 @@ pf = s.get_profile().astype(np.float64)
 admm = np.array([r.n_admm_iters for r in res], dtype=np.float64)
 qps = np.array([r.n_qp_solves for r in res], dtype=np.float64)
 sqp = np.array([r.n_sqp_iters for r in res], dtype=np.float64)
+subs = np.array([r.n_substates for r in res], dtype=np.float64)
+fev = np.array([r.n_func_evals for r in res], dtype=np.float64)
+print(f"LVS sub-state passes per problem {subs.mean():.0f}; per scan call and step pair "
+      f"{subs.sum() / max(1.0, (fev + sqp).sum() * (wl.n_steps - 1)):.2f}")
 mhz = pf[:, 13].sum() / pf[:, 14].sum() * 100.0
 print(f"shader clock ~{mhz:.0f} MHz; per problem: admm {admm.mean():.0f} (max {admm.max():.0f}), "
       f"qp {qps.mean():.1f}, sqp {sqp.mean():.1f}")

@@ -52,6 +52,7 @@ struct Ctl
   double trust;
   int status;
   int n_sqp, n_qp, n_fev, n_merit;
+  int scan_at_x;  // the contact counts / costs of the last scan are those of X (GetContactResultCached)
   long long n_admm;
   // OSQP state
   double c, cinv;
@@ -90,6 +91,7 @@ struct Ctx
   double** ptab_w = nullptr;  // the same table, writable (dynamic residency plan)
   const double* scene = nullptr;  // this problem's primitives [n_prims][16]
   const double* jpt = nullptr;    // this problem's JointPos targets [n_jpos][D]
+  struct CollStage* cs = nullptr; // contact-scan tables staged in static LDS
   int tid, lane, wave;
   __device__ Ctx(const Layout& l, const Tables& t, const thip_problem_desc* dd, double* ww, int* ii, double* bb,
                  Ctl* ss, double* const* pt = nullptr)
@@ -343,9 +345,45 @@ __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
 // ======================================================================
 __device__ __forceinline__ bool coll_fixed_step(const Ctx& c, int t) { return c.T.coll_fixed[t] != 0; }
 
+// Contact-scan tables and this problem's scene, staged in static LDS once per
+// scan (the candidate decode read them from global memory, a chain of
+// dependent loads per ballot round).
+struct CollStage
+{
+  double scene[THIP_MAX_PRIMS * 16];
+  double rad[THIP_MAX_SPHERES];
+  double ctr[THIP_MAX_SPHERES * 3];
+  int grp_ns[THIP_MAX_LINKS];
+  int grp_s0[THIP_MAX_LINKS];
+  int grp_link[THIP_MAX_LINKS];
+  int sph_order[THIP_MAX_SPHERES];
+};
+
+__device__ void coll_stage(Ctx& c)
+{
+  CollStage& S = *c.cs;
+  const int P = c.d->n_prims, ns = c.d->n_spheres, ng = c.T.n_groups;
+  FOR(e, P * 16) S.scene[e] = c.scene[e];
+  FOR(e, ns)
+  {
+    S.rad[e] = c.d->sphere_radius[e];
+    S.sph_order[e] = c.T.sph_order[e];
+    for (int r = 0; r < 3; ++r)
+      S.ctr[e * 3 + r] = c.d->sphere_center[e][r];
+  }
+  FOR(e, ng)
+  {
+    S.grp_ns[e] = c.T.grp_ns[e];
+    S.grp_s0[e] = c.T.grp_s0[e];
+    S.grp_link[e] = c.T.grp_link[e];
+  }
+  BSYNC();
+}
+
 template <int PASS>
 __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
 {
+  const CollStage& S = *c.cs;
   const Layout& L = c.L;
   const int D = L.D, ns = c.d->n_spheres, P = c.d->n_prims;
   const thip_chain& ch = c.d->chain;
@@ -375,33 +413,119 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       continue;
     }
     const bool f0 = coll_fixed_step(c, t), f1 = coll_fixed_step(c, t + 1);
+    const int ngr = c.T.n_groups;
+    long long* pf22 = (c.tid == 0) ? c.s->prof : nullptr;
+    const long long tfk0 = pf22 ? clock64() : 0;
     for (int isub = c.lane; isub < cnt; isub += 64)
     {
       double q[THIP_MAX_DOF];
       for (int j = 0; j < D; ++j)
         q[j] = linspaced(cnt, q0[j], q1[j], isub);
-      for (int g = 0; g < c.T.n_groups; ++g)
+      // one FK walk up the chain; each group's link pose is the walk's prefix
+      // (the same operations as chain_fk(.., link, ..))
+      Pose T;
+      pose_load(T, ch.base_pose);
+      const int last_link = S.grp_link[ngr - 1];
+      int g = 0;
+      for (int k = 1; k <= last_link; ++k)
       {
-        Pose T;
-        chain_fk(ch, q, c.T.grp_link[g], T);
-        for (int e = 0; e < c.T.grp_ns[g]; ++e)
+        Pose O, Tn;
+        pose_load(O, ch.joint_origin[k]);
+        pose_mul(T, O, Tn);
+        const int type = ch.joint_type[k];
+        if (type == THIP_JOINT_REVOLUTE || type == THIP_JOINT_CONTINUOUS)
         {
-          const int s = c.T.sph_order[c.T.grp_s0[g] + e];
-          const double* cs = c.d->sphere_center[s];
-          double* dst = SCR + (isub * ns + s) * 3;
-          for (int r = 0; r < 3; ++r)
-            dst[r] = T.r[r * 3 + 0] * cs[0] + T.r[r * 3 + 1] * cs[1] + T.r[r * 3 + 2] * cs[2] + T.t[r];
+          Pose M;
+          rot_axis_angle(ch.joint_axis[k], q[ch.joint_dof[k]], M.r);
+          M.t[0] = M.t[1] = M.t[2] = 0;
+          pose_mul(Tn, M, T);
         }
+        else if (type == THIP_JOINT_PRISMATIC)
+        {
+          Pose M;
+          const double v = q[ch.joint_dof[k]];
+          M.r[0] = M.r[4] = M.r[8] = 1;
+          M.r[1] = M.r[2] = M.r[3] = M.r[5] = M.r[6] = M.r[7] = 0;
+          M.t[0] = ch.joint_axis[k][0] * v;
+          M.t[1] = ch.joint_axis[k][1] * v;
+          M.t[2] = ch.joint_axis[k][2] * v;
+          pose_mul(Tn, M, T);
+        }
+        else
+          T = Tn;
+        for (; g < ngr && S.grp_link[g] == k; ++g)
+          for (int e = 0; e < S.grp_ns[g]; ++e)
+          {
+            const int s = S.sph_order[S.grp_s0[g] + e];
+            const double* cs = S.ctr + s * 3;
+            double* dst = SCR + (isub * ns + s) * 3;
+            for (int r = 0; r < 3; ++r)
+              dst[r] = T.r[r * 3 + 0] * cs[0] + T.r[r * 3 + 1] * cs[1] + T.r[r * 3 + 2] * cs[2] + T.t[r];
+          }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (pf22)
+      pf22[22] += clock64() - tfk0;
+    if (PASS == 0)
+    {
+      // counts and cost only: lane = (primitive, sphere), looping over the
+      // sub-states (the primitive and radius are loaded once per lane; the
+      // order of the candidates does not matter for a count and a sum)
+      double lcost = 0.0, lcount = 0.0;
+      for (int ps = c.lane; ps < P * ns; ps += 64)
+      {
+        const int p = ps / ns, s = ps - p * ns;
+        double prim[16];
+        for (int e = 0; e < 16; ++e)
+          prim[e] = S.scene[16 * p + e];
+        const double rad = S.rad[s];
+        constexpr int kU = 8;  // sub-states per batch: their center loads are in flight together
+        for (int i0 = 0; i0 < cnt; i0 += kU)
+        {
+          double cx[kU][3];
+#pragma unroll
+          for (int u = 0; u < kU; ++u)
+          {
+            const int i = min(i0 + u, cnt - 1);  // clamped: always a valid address
+            const double* cp = SCR + (i * ns + s) * 3;
+            cx[u][0] = cp[0];
+            cx[u][1] = cp[1];
+            cx[u][2] = cp[2];
+          }
+#pragma unroll
+          for (int u = 0; u < kU; ++u)
+          {
+            const int i = i0 + u;
+            double dist, n[3], pr[3];
+            sphere_prim_distance(cx[u], rad, prim, dist, n, pr);
+            bool hit = (i < cnt) && dist < threshold && !(dist > margin + buffer);
+            if (hit && (f0 || f1))
+              hit = (f0 && i != 0) || (f1 && i != cnt - 1);
+            lcount += hit ? 1.0 : 0.0;
+            lcost += hit ? fmax(margin - dist, 0.0) * coeff : 0.0;
+          }
+        }
+      }
+      const double cost = wave_sum(lcost);
+      const int found = static_cast<int>(wave_sum(lcount));
+      if (c.lane == 0)
+      {
+        PCNT[t] = found;
+        HCOST[t] = cost;
+        atomicAdd(reinterpret_cast<unsigned long long*>(&c.s->n_substates), static_cast<unsigned long long>(cnt));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
     int total = 0;
-    for (int g = 0; g < c.T.n_groups; ++g)
-      total += P * cnt * c.T.grp_ns[g];
+    for (int g = 0; g < ngr; ++g)
+      total += P * cnt * S.grp_ns[g];
     int running = 0;
-    double cost = 0.0;
+    double lcost = 0.0;  // per-lane partial cost, reduced once per pair
     const int base = (PASS == 1) ? out_base[t] : 0;
     for (int c0 = 0; c0 < total; c0 += 64)
     {
@@ -411,19 +535,28 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       int i = 0, s = 0, p = 0;
       if (cand < total)
       {
+        // flattened (group, primitive, sub-state, sphere) index; the group
+        // walk is uniform, the selects per lane
         int rem = cand, g = 0;
-        while (rem >= P * cnt * c.T.grp_ns[g])
+        for (int gg = 0; gg + 1 < ngr; ++gg)
         {
-          rem -= P * cnt * c.T.grp_ns[g];
-          ++g;
+          const int sz = P * cnt * S.grp_ns[gg];
+          const bool adv = (g == gg) && (rem >= sz);
+          rem = adv ? rem - sz : rem;
+          g = adv ? g + 1 : g;
         }
-        const int gn = c.T.grp_ns[g];
+        const int gn = S.grp_ns[g];
         p = rem / (cnt * gn);
         const int r2 = rem % (cnt * gn);
         i = r2 / gn;
-        s = c.T.sph_order[c.T.grp_s0[g] + r2 % gn];
+        s = S.sph_order[S.grp_s0[g] + r2 % gn];
+        double prim[16];
+        for (int e = 0; e < 16; ++e)
+          prim[e] = S.scene[16 * p + e];
+        const double* cp = SCR + (i * ns + s) * 3;
+        const double ctr[3] = { cp[0], cp[1], cp[2] };
         double n[3], pr[3];
-        sphere_prim_distance(SCR + (i * ns + s) * 3, c.d->sphere_radius[s], c.scene + 16 * p, dist, n, pr);
+        sphere_prim_distance(ctr, S.rad[s], prim, dist, n, pr);
         hit = dist < threshold && !(dist > margin + buffer);
         // removeInvalidContactResults (collision_utils.cpp:73-114): at a
         // fixed end keep only contacts not at that end (cc_type of the
@@ -433,10 +566,7 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       }
       const unsigned long long mask = __ballot(hit);
       if (PASS == 0)
-      {
-        double term = hit ? fmax(margin - dist, 0.0) * coeff : 0.0;
-        cost += wave_sum(term);
-      }
+        lcost += hit ? fmax(margin - dist, 0.0) * coeff : 0.0;
       else if (hit)
       {
         const int rank = __popcll(mask & ((1ull << c.lane) - 1ull));
@@ -452,6 +582,7 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       }
       running += __popcll(mask);
     }
+    const double cost = (PASS == 0) ? wave_sum(lcost) : 0.0;
     if (PASS == 0 && c.lane == 0)
     {
       PCNT[t] = running;
@@ -632,9 +763,17 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
     c.s->coll_overflow = 0;
   BSYNC();
   if (L.coll)
+    coll_stage(c);
+  // linearize at an accepted point reuses the counts of evaluate() at that
+  // same point (the reference's x-keyed contact cache, collision_terms.cpp:435-461)
+  const bool counts_current = rows && c.s->scan_at_x;
+  if (L.coll && !counts_current)
   {
-    coll_scan_pairs<0>(c, x, nullptr);
-    BSYNC();
+    {
+      PROF(19);
+      coll_scan_pairs<0>(c, x, nullptr);
+      BSYNC();
+    }
     if (costs)
       FOR(k, L.coll_last - L.coll_first) costs[L.coll_cost0 + k] = c.a(A_HCOST)[L.coll_first + k];
     if (c.tid == 0 && c.s->coll_overflow)
@@ -680,11 +819,15 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
     return;
   }
   static_hinge_rows(c, HP);
-  if (L.coll)
-    coll_scan_pairs<1>(c, x, HP);
-  BSYNC();
+  {
+    PROF(20);
+    if (L.coll)
+      coll_scan_pairs<1>(c, x, HP);
+    BSYNC();
+  }
   if (!L.coll)
     return;
+  PROF(21);
   // rows: distance expression k + a_t.x_t + a_t+1.x_t+1 per contact
   const thip_chain& ch = c.d->chain;
   const int* CONT = c.ia(I_CONT);
@@ -1535,19 +1678,23 @@ __device__ __forceinline__ void block_chain(const double* Gp, const double* cvp,
       // s0 is odd, so even u are odd steps (normal block, c by row i)
       const double gv = G[t * DD + (((u & 1) == 0) ? off_n : off_t)];
       const double cvv = cv[t * D + (((u & 1) == 0) ? (i < D ? i : 0) : (k < D ? k : 0))];
-      g[u] = (ok && act) ? gv : 0.0;
-      cc[u] = (ok && (((u & 1) == 0) ? (i < D) : (k < D))) ? cvv : 0.0;
+      g[u] = (ok && act) ? -gv : 0.0;
+      // c_t enters the reduction on one lane of each output (k == 0 for the
+      // octet sum, i == 0 for the cross-octet sum): v_t = sum(c_t - G v),
+      // one fma per lane and no subtraction after the reduction
+      const bool lead = ((u & 1) == 0) ? (k == 0) : (i == 0);
+      cc[u] = (ok && lead && (((u & 1) == 0) ? (i < D) : (k < D))) ? cvv : 0.0;
     }
     // serial part: no loads, stores or branches (steps past nsteps compute zeros)
     double vs[kChainChunk];
 #pragma unroll
     for (int u = 0; u < kChainChunk; ++u)
     {
-      const double p = g[u] * v;
+      const double p = fma(g[u], v, cc[u]);
       if ((u & 1) == 0)
-        v = cc[u] - octet_sum(p);  // row layout: v = v_t[i]
+        v = octet_sum(p);  // row layout: v = v_t[i]
       else
-        v = cc[u] - cross_octet_sum(p);  // column layout: v = v_t[k]
+        v = cross_octet_sum(p);  // column layout: v = v_t[k]
       vs[u] = v;
     }
 #pragma unroll
@@ -3246,6 +3393,7 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
     c.s->prev_rho = c.d->osqp.rho;
     c.s->n_h = 0;
     c.s->n_h_prev = -1;
+    c.s->scan_at_x = 0;
     c.s->flags = 0;
     c.s->coll_overflow = 0;
     c.s->n_contact_rows = c.s->n_hinge_admm = c.s->n_substates = 0;
@@ -3266,6 +3414,8 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
       if (first_eval)
       {
         evaluate(c, X, COST, VIOL);
+        if (c.tid == 0)
+          c.s->scan_at_x = 1;
         if (c.tid == 0)
           c.s->n_fev++;
         first_eval = false;
@@ -3452,6 +3602,8 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
         }
         BSYNC();
         evaluate(c, XN, NCOST, NVIOL);
+        if (c.tid == 0)
+          c.s->scan_at_x = 0;
         int decision = 0;  // 1 converged, 2 shrink, 3 accept
         if (c.tid == 0)
         {
@@ -3499,6 +3651,8 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
         }
         if (decision == 3)
         {
+          if (c.tid == 0)
+            c.s->scan_at_x = 1;  // X := XN, the point just scanned
           FOR(col, nx) X[col] = XN[col];
           FOR(i, L.n_costs) COST[i] = NCOST[i];
           FOR(i, L.n_cnts) VIOL[i] = NVIOL[i];
@@ -3583,6 +3737,8 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
     ptab[k] = L.loff[k] >= 0 ? dyn + L.loff[k] : wsb + L.doff[k];
   Ctx c(L, args.T, args.desc, wsb, args.iws + (long long)b * L.istride, dyn, &ctl, ptab);
   c.ptab_w = L.hinge ? ptab : nullptr;
+  __shared__ CollStage cstage;
+  c.cs = &cstage;
   c.scene = args.scene ? args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16 : nullptr;
   c.jpt = args.jpt + (long long)b * (L.n_jpos > 0 ? L.n_jpos : 1) * L.D;
   Solver sv;
@@ -3652,6 +3808,7 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(KernelArgs args, cons
     ctl.n_h = 0;
     ctl.flags = 0;
     ctl.coll_overflow = 0;
+    ctl.scan_at_x = 0;
     ctl.prof = nullptr;
     ctl.n_contact_rows = ctl.n_hinge_admm = ctl.n_substates = 0;
   }
@@ -3719,11 +3876,14 @@ __global__ __launch_bounds__(kBlock) void coll_rows_kernel(KernelArgs args, cons
         &ctl);
   c.scene = args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16;
   c.jpt = args.jpt + (long long)b * (L.n_jpos > 0 ? L.n_jpos : 1) * L.D;
+  __shared__ CollStage cstage;
+  c.cs = &cstage;
   if (threadIdx.x == 0)
   {
     ctl.n_h = 0;
     ctl.flags = 0;
     ctl.coll_overflow = 0;
+    ctl.scan_at_x = 0;
     ctl.prof = nullptr;
     ctl.n_contact_rows = ctl.n_hinge_admm = ctl.n_substates = 0;
   }

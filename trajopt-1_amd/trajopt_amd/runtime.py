@@ -121,7 +121,8 @@ class BatchTrustRegionSQP:
     PROFILE_SLOTS = ["admm_step", "residuals", "termination", "factor", "polish", "linearize", "evaluate",
                      "build_and_scale", "solve_rhs_diag", "fwd_chain", "bwd_chain", "aux_backsub", "qp_solve",
                      "sqp_total", "sqp_wall_ticks", "seg_B_rhs_linv", "seg_C2_linvT_middle",
-                     "seg_hinge_gather", "seg_hinge_E", "unused19", "unused20", "unused21", "unused22", "unused23"]
+                     "seg_hinge_gather", "seg_hinge_E", "coll_count_pass", "coll_rank_pass", "coll_rows", "coll_fk_substates",
+                     "unused23"]
 
     def enable_profile(self, on=True):
         self._check(self.lib.thip_debug_profile(self.ctx, 1 if on else 0), "thip_debug_profile")
