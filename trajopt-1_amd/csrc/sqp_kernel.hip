@@ -1743,12 +1743,21 @@ __device__ __forceinline__ double twisted_dvalue(const Ctx& c, const double* LIp
   const int D = c.L.D, DD = D * D;
   const lds_f64* LI = lds(LIp);
   const lds_f64* YV = lds(YVp);
-  double v = 0;
+  // unconditional loads from clamped indices, two accumulators (even / odd k):
+  // no branch per term and half the dependent adds
+  double v0 = 0, v1 = 0;
 #pragma unroll
   for (int k = 0; k < THIP_MAX_DOF; ++k)
-    if (k >= i && k < D)
-      v += LI[t * DD + k * D + i] * YV[t * D + k];
-  return v;
+  {
+    const int kk = (k < D) ? k : D - 1;
+    const double a = LI[t * DD + kk * D + i] * YV[t * D + kk];
+    const bool use = (k >= i) && (k < D);
+    if (k & 1)
+      v1 = use ? v1 + a : v1;
+    else
+      v0 = use ? v0 + a : v0;
+  }
+  return v0 + v1;
 }
 
 // The middle block of the twisted solve, by one whole wave in the chain's
@@ -2765,16 +2774,19 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       {
         const int i = (c.tid + kBlock * u) & 7;
         const int base = ccol[u] - i;
-        double v = 0;
-        // unconditional loads (in the LDS window), masked accumulation: no
-        // per-term branch, so the loads issue together
+        double v0 = 0, v1 = 0;
+        // unconditional loads (in the LDS window), masked accumulation in two
+        // partial sums: no per-term branch, half the dependent adds
 #pragma unroll
         for (int k = 0; k < THIP_MAX_DOF; ++k)
         {
           const double y = lds(YV)[base + k];
-          v = (k <= i) ? v + cli[u][k] * y : v;
+          if (k & 1)
+            v1 = (k <= i) ? fma(cli[u][k], y, v1) : v1;
+          else
+            v0 = (k <= i) ? fma(cli[u][k], y, v0) : v0;
         }
-        lds(CV)[ccol[u]] = v;
+        lds(CV)[ccol[u]] = v0 + v1;
       }
     }
     BSYNC();
@@ -2818,13 +2830,17 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       if (aact[u])
       {
         const int t = at[u];
-        double g = 0;
+        double g0 = 0, g1 = 0;
 #pragma unroll
         for (int j = 0; j < THIP_MAX_DOF; ++j)
         {
-          const double xv = lds(CV)[t * D + j];
-          g = (j < D) ? g + ags[u][j] * xv : g;
+          const double xv = lds(CV)[t * D + ((j < D) ? j : D - 1)];
+          if (j & 1)
+            g1 = (j < D) ? g1 + ags[u][j] * xv : g1;
+          else
+            g0 = (j < D) ? g0 + ags[u][j] * xv : g0;
         }
+        const double g = g0 + g1;
         const double dn = adn[u], dp = adp[u], wn = awn[u], wp = awp[u], rr = arr[u];
         const double rn = arn[u], rp = arp[u];
         const double deti = adeti[u];
