@@ -319,6 +319,30 @@ def _variant(name):
             d.jpos_upper_tols[0][j] = 0.8
             d.jpos_lower_tols[0][j] = -0.8
         return wl
+    if name == "max_horizon_64":
+        # THIP_MAX_STEPS waypoints, 63 CartPose costs: past the register segment's N <= 32
+        # (the generic ADMM step runs)
+        return problems.make_workload("B", 4, n_steps=64)
+    if name == "min_horizon_2":
+        return problems.make_workload("A", 8, n_steps=2)
+    if name == "collision_empty_scene":
+        wl = problems.make_workload("C", 4)
+        wl.desc.n_prims = 0
+        wl.scene = np.zeros((wl.batch, 0, 16))
+        return wl
+    if name == "collision_fixed_both_ends":
+        # fixed collision steps at both ends: removeInvalidContactResults drops
+        # the contacts at a fixed end (collision_utils.cpp:73-114)
+        wl = problems.make_workload("C", 8)
+        wl.desc.coll_n_fixed = 2
+        wl.desc.coll_fixed_steps[1] = wl.n_steps - 1
+        return wl
+    if name == "collision_step_subrange":
+        wl = problems.make_workload("C", 8)
+        wl.desc.coll_first_step = 5
+        wl.desc.coll_last_step = 20
+        wl.desc.coll_n_fixed = 0
+        return wl
     if name == "single_problem":
         return problems.make_workload("B", 1, first_problem=5)
     raise KeyError(name)
@@ -327,7 +351,8 @@ def _variant(name):
 VARIANTS = ["jointvel_only", "short_horizon", "two_fixed_steps", "position_only_cartpose", "admm_iteration_cap",
             "sqp_iteration_cap", "sqp_iteration_cap_costs_only", "no_scaling", "no_polish", "no_adaptive_rho_no_warm_start", "single_problem",
             "jointpos_goal", "jointpos_goal_offset", "jointpos_far_goal_penalty_limit", "jointpos_with_cartpose",
-            "jointvel_ineq_cost", "jointpos_ineq_cost_and_cnt", "collision_with_static_hinges"]
+            "jointvel_ineq_cost", "jointpos_ineq_cost_and_cnt", "collision_with_static_hinges", "max_horizon_64",
+            "min_horizon_2", "collision_empty_scene", "collision_fixed_both_ends", "collision_step_subrange"]
 
 
 @pytest.mark.parametrize("name", VARIANTS)
