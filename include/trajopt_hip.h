@@ -201,7 +201,8 @@ typedef struct thip_problem_desc {
   double jpos_upper_tols[THIP_MAX_JPOS][THIP_MAX_DOF];
   double jpos_lower_tols[THIP_MAX_JPOS][THIP_MAX_DOF];
 
-  /* CollisionTermInfo, LVS_DISCRETE cost (collision_terms.cpp:737-906,1267-1306):
+  /* CollisionTermInfo, LVS_DISCRETE or LVS_CONTINUOUS, cost or constraint
+   * (collision_terms.cpp:737-1161,1267-1386):
    * robot collision model = spheres rigidly attached to chain links; the scene
    * is per problem (n_prims primitives of 16 doubles each, see THIP_PRIM_*). */
   int coll_enabled;
@@ -214,6 +215,11 @@ typedef struct thip_problem_desc {
   double coll_coeff;       /* coeffs */
   double coll_buffer;      /* collision_margin_buffer */
   double coll_lvs;         /* longest_valid_segment_length */
+  int coll_continuous;     /* 0: LVS_DISCRETE (DiscreteCollisionEvaluator, sub-state contacts);
+                              1: LVS_CONTINUOUS / CONTINUOUS (CastCollisionEvaluator,
+                              collision_terms.cpp:978-1161): each robot sphere is swept between
+                              consecutive sub-states (a capsule) and tested against the scene;
+                              CONTINUOUS is LVS_CONTINUOUS with coll_lvs = +inf (one cast per pair) */
   int n_spheres;
   int sphere_link[THIP_MAX_SPHERES];
   double sphere_center[THIP_MAX_SPHERES][3];  /* in link frame */

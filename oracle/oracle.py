@@ -149,6 +149,20 @@ def collision_rows(wl, b, x=None, cap=8192):
     return out[:min(n, cap)]
 
 
+def swept_sphere_prim(a, b, r, prim):
+    """(dist, normal, p_robot, t_star) of the sphere swept a -> b vs a primitive."""
+    L = lib()
+    dp = C.POINTER(C.c_double)
+    L.oracle_swept_sphere_prim.argtypes = [dp, dp, C.c_double, dp, dp]
+    L.oracle_swept_sphere_prim.restype = None
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    prim = np.ascontiguousarray(prim, dtype=np.float64)
+    out = np.zeros(9)
+    L.oracle_swept_sphere_prim(_dp(a), _dp(b), r, _dp(prim), _dp(out))
+    return out[0], out[1:4], out[4:7], out[7]
+
+
 def sphere_prim(c, r, prim):
     L = lib()
     L.oracle_sphere_prim.argtypes = [C.POINTER(C.c_double), C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double)]

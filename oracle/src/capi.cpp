@@ -226,6 +226,7 @@ int oracle_collision_rows(const thip_problem_desc* d, const double* scene, const
     cm.coeff = d->coll_coeff;
     cm.buffer = d->coll_buffer;
     cm.lvs = d->coll_lvs;
+    cm.continuous = d->coll_continuous != 0;
     const int first = d->coll_first_step;
     const int last = (d->coll_last_step < 0) ? N - 1 : d->coll_last_step;
     auto fixed = [&](int t) {
@@ -313,6 +314,21 @@ int oracle_collision_rows(const thip_problem_desc* d, const double* scene, const
 }
 
 // Signed distance of one robot sphere against one primitive (test helper).
+// swept sphere a -> b vs primitive: out9 = [dist, n(3), p_robot(3), t_star, 0]
+void oracle_swept_sphere_prim(const double* a, const double* b, double r, const double* prim, double* out9)
+{
+  double n[3], pr[3], pp[3], dist, t;
+  sweptSpherePrimDistance(a, b, r, prim, dist, n, pr, pp, t);
+  out9[0] = dist;
+  for (int i = 0; i < 3; ++i)
+  {
+    out9[1 + i] = n[i];
+    out9[4 + i] = pr[i];
+  }
+  out9[7] = t;
+  out9[8] = 0;
+}
+
 void oracle_sphere_prim(const double* c, double r, const double* prim, double* out8)
 {
   double n[3], pr[3], pp[3], d;

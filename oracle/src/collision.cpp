@@ -104,6 +104,171 @@ void spherePrimDistance(const double c[3], double r, const double* prim, double&
   }
 }
 
+// ------------------------------------------------------------ swept sphere
+// Bullet's cast (castVsCast on the convex hull of the link shape at the two
+// poses) replaced for a sphere: its center moves on the segment a -> b, so
+// the swept shape is a capsule.  dist = min over t in [0, 1] of the sphere's
+// signed distance at a + t (b - a); t_star is the minimiser chosen by a fixed
+// rule (closed form for spheres and capsules; for boxes the smallest value
+// among the breakpoints and piecewise stationary points of the box SDF along
+// the segment, ties within 1e-14 to the smaller t).  The same rule runs on
+// the GPU (collision_device.hpp).
+namespace
+{
+inline double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+// Closest points of segments p1 + s d1 and p2 + t d2 (s, t in [0, 1]);
+// returns s (Ericson, Real-Time Collision Detection 5.1.9).
+double segSegParam(const double p1[3], const double d1[3], const double p2[3], const double d2[3])
+{
+  const double r[3] = { p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2] };
+  const double a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+  const double eps = 1e-24;
+  double s, t;
+  if (a <= eps && e <= eps)
+    return 0.0;
+  if (a <= eps)
+    return 0.0;
+  const double cc = dot3(d1, r);
+  if (e <= eps)
+    return std::fmin(std::fmax(-cc / a, 0.0), 1.0);
+  const double b = dot3(d1, d2);
+  const double denom = a * e - b * b;
+  s = (denom > eps) ? std::fmin(std::fmax((b * f - cc * e) / denom, 0.0), 1.0) : 0.0;
+  t = (b * s + f) / e;
+  if (t < 0.0)
+    s = std::fmin(std::fmax(-cc / a, 0.0), 1.0);
+  else if (t > 1.0)
+    s = std::fmin(std::fmax((b - cc) / a, 0.0), 1.0);
+  return s;
+}
+}  // namespace
+
+void sweptSpherePrimDistance(const double a[3], const double b[3], double r, const double* prim, double& dist,
+                             double n[3], double p_robot[3], double p_prim[3], double& t_star)
+{
+  const int type = static_cast<int>(prim[0]);
+  const double u[3] = { b[0] - a[0], b[1] - a[1], b[2] - a[2] };
+  const double uu = dot3(u, u);
+  auto at = [&](double t, double c[3]) {
+    for (int i = 0; i < 3; ++i)
+      c[i] = a[i] + t * u[i];
+  };
+  double t = 0.0;
+  if (type == THIP_PRIM_SPHERE)
+  {
+    const double w[3] = { prim[1] - a[0], prim[2] - a[1], prim[3] - a[2] };
+    t = (uu > 1e-24) ? std::fmin(std::fmax(dot3(w, u) / uu, 0.0), 1.0) : 0.0;
+  }
+  else if (type == THIP_PRIM_CAPSULE)
+  {
+    const double d2[3] = { prim[4] - prim[1], prim[5] - prim[2], prim[6] - prim[3] };
+    t = segSegParam(a, u, prim + 1, d2);
+  }
+  else
+  {
+    // box: a and u in box coordinates
+    const double* ctr = prim + 1;
+    const double* R = prim + 4;
+    const double* h = prim + 13;
+    const double w[3] = { a[0] - ctr[0], a[1] - ctr[1], a[2] - ctr[2] };
+    double al[3], ul[3];
+    for (int i = 0; i < 3; ++i)
+    {
+      al[i] = R[0 * 3 + i] * w[0] + R[1 * 3 + i] * w[1] + R[2 * 3 + i] * w[2];
+      ul[i] = R[0 * 3 + i] * u[0] + R[1 * 3 + i] * u[1] + R[2 * 3 + i] * u[2];
+    }
+    // breakpoints where a coordinate crosses a face plane or zero (the kink
+    // of |p_i|), sorted
+    double bp[11];
+    int nb = 0;
+    bp[nb++] = 0.0;
+    for (int i = 0; i < 3; ++i)
+      if (std::fabs(ul[i]) > 1e-300)
+        for (int sg = -1; sg <= 1; ++sg)
+        {
+          const double tb = (sg * h[i] - al[i]) / ul[i];
+          if (tb > 0.0 && tb < 1.0)
+            bp[nb++] = tb;
+        }
+    bp[nb++] = 1.0;
+    for (int i = 1; i < nb; ++i)  // insertion sort
+      for (int j = i; j > 0 && bp[j - 1] > bp[j]; --j)
+      {
+        const double tmp = bp[j];
+        bp[j] = bp[j - 1];
+        bp[j - 1] = tmp;
+      }
+    double cand[48];
+    int nc = 0;
+    for (int k = 0; k < nb; ++k)
+      cand[nc++] = bp[k];
+    for (int k = 0; k + 1 < nb; ++k)
+    {
+      const double t0 = bp[k], t1 = bp[k + 1];
+      if (!(t1 > t0))
+        continue;
+      const double tm = 0.5 * (t0 + t1);
+      double sg[3];
+      bool out = false;
+      for (int i = 0; i < 3; ++i)
+      {
+        const double pm = al[i] + tm * ul[i];
+        sg[i] = (pm < 0) ? -1.0 : 1.0;
+        out = out || (std::fabs(pm) > h[i]);
+      }
+      if (out)
+      {
+        // outside: minimise sum over the outside axes of (p_i - sg_i h_i)^2
+        double num = 0, den = 0;
+        for (int i = 0; i < 3; ++i)
+        {
+          const double pm = al[i] + tm * ul[i];
+          if (std::fabs(pm) > h[i])
+          {
+            num += (al[i] - sg[i] * h[i]) * ul[i];
+            den += ul[i] * ul[i];
+          }
+        }
+        if (den > 0)
+          cand[nc++] = std::fmin(std::fmax(-num / den, t0), t1);
+      }
+      else
+        // inside: max_i (sg_i p_i - h_i); stationary points where two terms are equal
+        for (int i = 0; i < 3; ++i)
+          for (int j = i + 1; j < 3; ++j)
+          {
+            const double den = sg[i] * ul[i] - sg[j] * ul[j];
+            if (std::fabs(den) > 1e-300)
+            {
+              const double tc = (h[i] - h[j] - sg[i] * al[i] + sg[j] * al[j]) / den;
+              if (tc > t0 && tc < t1)
+                cand[nc++] = tc;
+            }
+          }
+    }
+    // the smallest value; among values within 1e-14 of it, the smallest t
+    double val[48];
+    double best = 0;
+    for (int k = 0; k < nc; ++k)
+    {
+      double c[3], nn[3], pr[3], pp[3];
+      at(cand[k], c);
+      spherePrimDistance(c, r, prim, val[k], nn, pr, pp);
+      best = (k == 0) ? val[k] : std::fmin(best, val[k]);
+    }
+    double bt = 2.0;
+    for (int k = 0; k < nc; ++k)
+      if (val[k] <= best + 1e-14 && cand[k] < bt)
+        bt = cand[k];
+    t = bt;
+  }
+  double c[3];
+  at(t, c);
+  spherePrimDistance(c, r, prim, dist, n, p_robot, p_prim);
+  t_star = t;
+}
+
 namespace
 {
 // Eigen::VectorXd::LinSpaced(size, low, high)(i) for floating point
@@ -144,6 +309,74 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
   std::map<std::pair<int, int>, std::vector<Contact>> results;
   std::vector<double> q(static_cast<std::size_t>(D));
   std::vector<Iso3> T;
+  if (cm.continuous)
+  {
+    // CastCollisionEvaluator::CalcCollisions (collision_terms.cpp:1106-1161): one cast per
+    // consecutive sub-state pair (a single cast q0 -> q1 when dist <= lvs); the contact's
+    // cc_time is the closest point's time along the whole step pair,
+    // (i + t) / (cnt - 1) (addInterpolatedCollisionResults, discrete = false)
+    std::vector<Iso3> T1;
+    std::vector<double> qn(static_cast<std::size_t>(D));
+    for (long i = 0; i + 1 < cnt; ++i)
+    {
+      for (int j = 0; j < D; ++j)
+      {
+        q[static_cast<std::size_t>(j)] = linspaced(static_cast<int>(cnt), q0[j], q1[j], static_cast<int>(i));
+        qn[static_cast<std::size_t>(j)] = linspaced(static_cast<int>(cnt), q0[j], q1[j], static_cast<int>(i + 1));
+      }
+      chainFwdKin(ch, q.data(), T);
+      chainFwdKin(ch, qn.data(), T1);
+      for (int s = 0; s < cm.n_spheres; ++s)
+      {
+        const int link = cm.sphere_link[s];
+        const Iso3& Ta = T[static_cast<std::size_t>(link)];
+        const Iso3& Tb = T1[static_cast<std::size_t>(link)];
+        double ca[3], cb[3];
+        for (int r = 0; r < 3; ++r)
+        {
+          ca[r] = Ta.R[r * 3 + 0] * cm.sphere_center[s][0] + Ta.R[r * 3 + 1] * cm.sphere_center[s][1] +
+                  Ta.R[r * 3 + 2] * cm.sphere_center[s][2] + Ta.t[r];
+          cb[r] = Tb.R[r * 3 + 0] * cm.sphere_center[s][0] + Tb.R[r * 3 + 1] * cm.sphere_center[s][1] +
+                  Tb.R[r * 3 + 2] * cm.sphere_center[s][2] + Tb.t[r];
+        }
+        for (int p = 0; p < cm.n_prims; ++p)
+        {
+          Contact ct;
+          double ts = 0;
+          sweptSpherePrimDistance(ca, cb, cm.sphere_radius[s], cm.scene + 16 * p, ct.distance, ct.normal, ct.p_robot,
+                                  ct.p_prim, ts);
+          if (!(ct.distance < threshold))
+            continue;
+          ct.link = link;
+          ct.prim = p;
+          ct.sphere = s;
+          ct.substate = static_cast<int>(i);
+          ct.transform = Ta;
+          ct.cc_transform = Tb;
+          // nearest_points_local[0] in the link frame at the cast's start state
+          const double w[3] = { ct.p_robot[0] - Ta.t[0], ct.p_robot[1] - Ta.t[1], ct.p_robot[2] - Ta.t[2] };
+          for (int r = 0; r < 3; ++r)
+            ct.p_local[r] = Ta.R[0 * 3 + r] * w[0] + Ta.R[1 * 3 + r] * w[1] + Ta.R[2 * 3 + r] * w[2];
+          ct.cc_time = (double(i) + ts) * dt;
+          ct.cc_type = (i == 0 && ts == 0.0) ? kCCTime0 : ((i + 1 == last && ts == 1.0) ? kCCTime1 : kCCBetween);
+          if (ct.distance > cm.margin + cm.buffer)
+            continue;
+          if (vars0_fixed || vars1_fixed)
+          {
+            const bool keep = (vars0_fixed && ct.cc_type != kCCNone && ct.cc_type != kCCTime0) ||
+                              (vars1_fixed && ct.cc_type != kCCNone && ct.cc_type != kCCTime1);
+            if (!keep)
+              continue;
+          }
+          results[{ link, p }].push_back(ct);
+        }
+      }
+    }
+    std::vector<Contact> flat;
+    for (auto& kv : results)
+      flat.insert(flat.end(), kv.second.begin(), kv.second.end());
+    return flat;
+  }
   for (long i = 0; i < cnt; ++i)
   {
     for (int j = 0; j < D; ++j)
@@ -169,6 +402,7 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
         ct.sphere = s;
         ct.substate = static_cast<int>(i);
         ct.transform = Tl;
+        ct.cc_transform = Tl;
         // nearest_points_local[0]: the robot point in the link frame
         const double w[3] = { ct.p_robot[0] - Tl.t[0], ct.p_robot[1] - Tl.t[1], ct.p_robot[2] - Tl.t[2] };
         for (int r = 0; r < 3; ++r)
@@ -209,10 +443,11 @@ void contactGradient(const CollisionModel& cm, const double* dofvals, const Cont
   const int D = ch.n_dof;
   double J[6 * THIP_MAX_DOF];
   chainJacobian(ch, dofvals, ct.link, J);
+  // link_transform = isTimestep1 ? cc_transform : transform (collision_terms.cpp:278-279)
+  const Iso3& lt = timestep1 ? ct.cc_transform : ct.transform;
   double r[3];
   for (int i = 0; i < 3; ++i)
-    r[i] = ct.transform.R[i * 3 + 0] * ct.p_local[0] + ct.transform.R[i * 3 + 1] * ct.p_local[1] +
-           ct.transform.R[i * 3 + 2] * ct.p_local[2];
+    r[i] = lt.R[i * 3 + 0] * ct.p_local[0] + lt.R[i * 3 + 1] * ct.p_local[1] + lt.R[i * 3 + 2] * ct.p_local[2];
   scale = timestep1 ? ct.cc_time : (1 - ct.cc_time);
   for (int j = 0; j < D; ++j)
   {
@@ -386,6 +621,7 @@ void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, cons
   cm->coeff = d.coll_coeff;
   cm->buffer = d.coll_buffer;
   cm->lvs = d.coll_lvs;
+  cm->continuous = d.coll_continuous != 0;
   const int first = d.coll_first_step;
   const int last = (d.coll_last_step < 0) ? d.n_steps - 1 : d.coll_last_step;
   auto fixed = [&](int t) {

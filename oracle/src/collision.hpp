@@ -2,6 +2,7 @@
 //
 // CPU restatement of the LVS-discrete collision term on a primitive scene:
 //   DiscreteCollisionEvaluator::CalcCollisions  trajopt/src/collision_terms.cpp:817-898
+//   CastCollisionEvaluator::CalcCollisions      trajopt/src/collision_terms.cpp:1065-1161 (LVS_CONTINUOUS)
 //   CollisionEvaluator::GetGradient             trajopt/src/collision_terms.cpp:195-242
 //   CollisionsToDistanceExpressions             trajopt/src/collision_terms.cpp:341-386
 //   CalcDistExpressions{BothFree,..}            trajopt/src/collision_terms.cpp:463-536
@@ -33,6 +34,7 @@ struct CollisionModel
   std::vector<double> scene_store;
   const double* scene = nullptr;  // [n_prims][16]
   double margin = 0, coeff = 0, buffer = 0, lvs = 0;
+  bool continuous = false;  // LVS_CONTINUOUS (CastCollisionEvaluator) instead of LVS_DISCRETE
 };
 
 // A contact between a robot link sphere (link_ids[0], active) and a scene
@@ -45,13 +47,18 @@ struct Contact
   double p_robot[3];   // nearest points, world
   double p_prim[3];
   double p_local[3];   // nearest_points_local[0] (robot link frame at the sub-state)
-  Iso3 transform;      // robot link pose at the sub-state (= cc_transform)
-  double cc_time = 0;  // interpolation time of the sub-state
+  Iso3 transform;      // robot link pose at the sub-state (discrete) / at the cast's start state (continuous)
+  Iso3 cc_transform;   // = transform (discrete) / link pose at the cast's end state (continuous)
+  double cc_time = 0;  // interpolation time of the sub-state / of the closest point along the cast
   int cc_type = 0;     // 1 Time0, 2 Time1, 3 Between
 };
 
 void spherePrimDistance(const double c[3], double r, const double* prim, double& dist, double n[3],
                         double p_robot[3], double p_prim[3]);
+// Swept sphere (center a -> b, radius r: a capsule) vs primitive: the signed
+// distance min_t d(a + t (b - a)) and its first minimiser t (see collision.cpp).
+void sweptSpherePrimDistance(const double a[3], const double b[3], double r, const double* prim, double& dist,
+                             double n[3], double p_robot[3], double p_prim[3], double& t_star);
 std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, const double* q1, bool vars0_fixed,
                                     bool vars1_fixed);
 void contactGradient(const CollisionModel& cm, const double* dofvals, const Contact& ct, bool timestep1,

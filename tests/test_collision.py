@@ -116,3 +116,43 @@ def test_sqp_collision_golden(oracle_mod, golden):
     np.testing.assert_array_equal([r.status for r in res], g["status"])
     np.testing.assert_allclose(x, g["x"], rtol=0, atol=1e-9)
     assert all(r.n_costs == 1 + 29 + 29 for r in res)
+
+
+def test_swept_sphere_distance_is_the_minimum_along_the_cast(oracle_mod):
+    """LVS_CONTINUOUS contact geometry (oracle/src/collision.cpp,
+    sweptSpherePrimDistance): the cast distance of a sphere swept a -> b equals
+    the minimum of the sphere's signed distance over the segment (checked
+    against 2001 samples), and the returned time attains it."""
+    rng = np.random.default_rng(7)
+
+    def rot():
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        w, x, y, z = q
+        return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                         [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                         [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+    for trial in range(600):
+        typ = trial % 3
+        prim = np.zeros(16)
+        prim[0] = typ
+        prim[1:4] = rng.normal(size=3) * 0.3
+        if typ == 0:
+            prim[4] = rng.uniform(0.05, 0.2)
+        elif typ == 1:
+            prim[4:13] = rot().reshape(9)
+            prim[13:16] = rng.uniform(0.05, 0.3, 3)
+        else:
+            prim[4:7] = prim[1:4] + rng.normal(size=3) * 0.3
+            prim[7] = rng.uniform(0.03, 0.1)
+        a = rng.normal(size=3) * 0.4
+        b = a if trial % 7 == 0 else a + rng.normal(size=3) * 0.3
+        r = rng.uniform(0.05, 0.1)
+        d, n, pr, t = oracle_mod.swept_sphere_prim(a, b, r, prim)
+        ts = np.linspace(0, 1, 2001)
+        sampled = min(oracle_mod.sphere_prim(a + tt * (b - a), r, prim)[0] for tt in ts)
+        assert d <= sampled + 1e-12
+        assert sampled - d < 1e-3
+        assert 0.0 <= t <= 1.0
+        assert abs(oracle_mod.sphere_prim(a + t * (b - a), r, prim)[0] - d) < 1e-14

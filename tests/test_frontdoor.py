@@ -78,8 +78,8 @@ def _doc(**over):
         (_doc(costs=[{"type": "joint_acc", "params": {}}]), "term type 'joint_acc' is not supported on the HIP path"),
         (_doc(constraints=[{"type": "joint_vel", "params": {"targets": [0]}}]),
          "JointVelTermInfo as a constraint (JointVelEqConstraint / JointVelIneqConstraint) is not supported"),
-        (_doc(costs=[{"type": "collision", "params": {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 4}}]),
-         "collision evaluator_type 4 (only LVS_DISCRETE = 2) is not supported on the HIP path"),
+        (_doc(costs=[{"type": "collision", "params": {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 1}}]),
+         "collision evaluator_type 1 (LVS_DISCRETE = 2, CONTINUOUS = 3, LVS_CONTINUOUS = 4 are) is not supported"),
         (_doc(costs=[{"type": "collision", "params": {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 2,
                                                       "safety_margin_buffer": 0.05}}]),
          "invalid field found: safety_margin_buffer"),
@@ -114,15 +114,18 @@ def test_init_info_types():
 
 
 def test_reference_arm_around_table_config():
-    """The reference's planning config: evaluator_type 4 (LVS_CONTINUOUS) is
-    config E's continuous collision, not on the HIP path yet; with
-    LVS_DISCRETE the rest lowers as the reference reads it."""
+    """The reference's planning config (evaluator_type 4, LVS_CONTINUOUS)
+    lowers as the reference reads it; evaluator 2 / 3 select LVS_DISCRETE /
+    CONTINUOUS (one cast per step pair)."""
     text = (GOLDEN / "arm_around_table.json").read_text()
-    with pytest.raises(host.HostError, match="evaluator_type 4"):
-        host.lower_json(text)
     doc = json.loads(text)
-    doc["costs"][1]["params"]["evaluator_type"] = 2
-    desc, init, tgt, jpt = host.lower_json(json.dumps(doc))
+    desc, init, tgt, jpt = host.lower_json(text)
+    assert desc.coll_continuous == 1 and desc.coll_lvs == 0.02
+    for ev, cont in ((2, 0), (3, 1)):
+        doc["costs"][1]["params"]["evaluator_type"] = ev
+        d2, _, _, _ = host.lower_json(json.dumps(doc))
+        assert d2.coll_continuous == cont
+    assert d2.coll_lvs > 1e300
     assert desc.n_steps == 6 and desc.n_fixed == 1 and desc.fixed_steps[0] == 0
     assert desc.jv_enabled == 1 and desc.n_jpos == 1 and desc.jpos_is_cnt[0] == 1
     assert desc.jpos_first_step[0] == 5 and desc.jpos_last_step[0] == 5

@@ -97,6 +97,187 @@ __device__ inline void sphere_prim_distance(const double c[3], double r, const d
     p_robot[i] = c[i] + r * n[i];
 }
 
+// Swept sphere (center a -> b, radius r: a capsule) vs primitive, the
+// restatement of Bullet's cast for a sphere (oracle/src/collision.cpp,
+// sweptSpherePrimDistance, the same rule): dist = min over t in [0, 1] of the
+// signed distance at a + t (b - a), t_star its minimiser (closed form for
+// spheres and capsules; for boxes the smallest value among the breakpoints
+// and piecewise stationary points of the box SDF on the segment, ties within
+// 1e-14 to the smaller t).
+__device__ inline double sseg_param(const double p1[3], const double d1[3], const double p2[3], const double d2[3])
+{
+  const double r[3] = { p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2] };
+  const double a = d1[0] * d1[0] + d1[1] * d1[1] + d1[2] * d1[2];
+  const double e = d2[0] * d2[0] + d2[1] * d2[1] + d2[2] * d2[2];
+  const double f = d2[0] * r[0] + d2[1] * r[1] + d2[2] * r[2];
+  const double eps = 1e-24;
+  if (a <= eps)
+    return 0.0;
+  const double cc = d1[0] * r[0] + d1[1] * r[1] + d1[2] * r[2];
+  if (e <= eps)
+    return fmin(fmax(-cc / a, 0.0), 1.0);
+  const double b = d1[0] * d2[0] + d1[1] * d2[1] + d1[2] * d2[2];
+  const double denom = a * e - b * b;
+  double s = (denom > eps) ? fmin(fmax((b * f - cc * e) / denom, 0.0), 1.0) : 0.0;
+  const double t = (b * s + f) / e;
+  if (t < 0.0)
+    s = fmin(fmax(-cc / a, 0.0), 1.0);
+  else if (t > 1.0)
+    s = fmin(fmax((b - cc) / a, 0.0), 1.0);
+  return s;
+}
+
+__device__ inline void swept_sphere_prim_distance(const double a[3], const double b[3], double r, const double* prim,
+                                                  double& dist, double n[3], double p_robot[3], double& t_star)
+{
+  const int type = static_cast<int>(prim[0]);
+  const double u[3] = { b[0] - a[0], b[1] - a[1], b[2] - a[2] };
+  const double uu = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
+  double t = 0.0;
+  if (type == THIP_PRIM_SPHERE)
+  {
+    const double w[3] = { prim[1] - a[0], prim[2] - a[1], prim[3] - a[2] };
+    t = (uu > 1e-24) ? fmin(fmax((w[0] * u[0] + w[1] * u[1] + w[2] * u[2]) / uu, 0.0), 1.0) : 0.0;
+  }
+  else if (type == THIP_PRIM_CAPSULE)
+  {
+    const double d2[3] = { prim[4] - prim[1], prim[5] - prim[2], prim[6] - prim[3] };
+    t = sseg_param(a, u, prim + 1, d2);
+  }
+  else
+  {
+    const double* ctr = prim + 1;
+    const double* R = prim + 4;
+    const double* h = prim + 13;
+    const double w[3] = { a[0] - ctr[0], a[1] - ctr[1], a[2] - ctr[2] };
+    double al[3], ul[3];
+    for (int i = 0; i < 3; ++i)
+    {
+      al[i] = R[0 * 3 + i] * w[0] + R[1 * 3 + i] * w[1] + R[2 * 3 + i] * w[2];
+      ul[i] = R[0 * 3 + i] * u[0] + R[1 * 3 + i] * u[1] + R[2 * 3 + i] * u[2];
+    }
+    double bp[11];
+    int nb = 0;
+    bp[nb++] = 0.0;
+    for (int i = 0; i < 3; ++i)
+      if (fabs(ul[i]) > 1e-300)
+        for (int sg = -1; sg <= 1; ++sg)
+        {
+          const double tb = (sg * h[i] - al[i]) / ul[i];
+          if (tb > 0.0 && tb < 1.0)
+            bp[nb++] = tb;
+        }
+    bp[nb++] = 1.0;
+    for (int i = 1; i < nb; ++i)
+      for (int j = i; j > 0 && bp[j - 1] > bp[j]; --j)
+      {
+        const double tmp = bp[j];
+        bp[j] = bp[j - 1];
+        bp[j - 1] = tmp;
+      }
+    double cand[48];
+    int nc = 0;
+    for (int k = 0; k < nb; ++k)
+      cand[nc++] = bp[k];
+    for (int k = 0; k + 1 < nb; ++k)
+    {
+      const double t0 = bp[k], t1 = bp[k + 1];
+      if (!(t1 > t0))
+        continue;
+      const double tm = 0.5 * (t0 + t1);
+      double sg[3];
+      bool out = false;
+      for (int i = 0; i < 3; ++i)
+      {
+        const double pm = al[i] + tm * ul[i];
+        sg[i] = (pm < 0) ? -1.0 : 1.0;
+        out = out || (fabs(pm) > h[i]);
+      }
+      if (out)
+      {
+        double num = 0, den = 0;
+        for (int i = 0; i < 3; ++i)
+        {
+          const double pm = al[i] + tm * ul[i];
+          if (fabs(pm) > h[i])
+          {
+            num += (al[i] - sg[i] * h[i]) * ul[i];
+            den += ul[i] * ul[i];
+          }
+        }
+        if (den > 0)
+          cand[nc++] = fmin(fmax(-num / den, t0), t1);
+      }
+      else
+        for (int i = 0; i < 3; ++i)
+          for (int j = i + 1; j < 3; ++j)
+          {
+            const double den = sg[i] * ul[i] - sg[j] * ul[j];
+            if (fabs(den) > 1e-300)
+            {
+              const double tc = (h[i] - h[j] - sg[i] * al[i] + sg[j] * al[j]) / den;
+              if (tc > t0 && tc < t1)
+                cand[nc++] = tc;
+            }
+          }
+    }
+    double val[48];
+    double best = 0;
+    for (int k = 0; k < nc; ++k)
+    {
+      const double c[3] = { a[0] + cand[k] * u[0], a[1] + cand[k] * u[1], a[2] + cand[k] * u[2] };
+      double nn[3], pr[3];
+      sphere_prim_distance(c, r, prim, val[k], nn, pr);
+      best = (k == 0) ? val[k] : fmin(best, val[k]);
+    }
+    double bt = 2.0;
+    for (int k = 0; k < nc; ++k)
+      if (val[k] <= best + 1e-14 && cand[k] < bt)
+        bt = cand[k];
+    t = bt;
+  }
+  const double c[3] = { a[0] + t * u[0], a[1] + t * u[1], a[2] + t * u[2] };
+  sphere_prim_distance(c, r, prim, dist, n, p_robot);
+  t_star = t;
+}
+
+// A lower bound of the swept distance (segment to the primitive's bounding
+// sphere): a candidate whose bound exceeds the contact distance cannot be a
+// contact, so the exact cast is skipped.
+__device__ inline double swept_lower_bound(const double a[3], const double b[3], double r, const double* prim)
+{
+  const int type = static_cast<int>(prim[0]);
+  double c[3], rad;
+  if (type == THIP_PRIM_SPHERE)
+  {
+    c[0] = prim[1];
+    c[1] = prim[2];
+    c[2] = prim[3];
+    rad = prim[4];
+  }
+  else if (type == THIP_PRIM_CAPSULE)
+  {
+    for (int i = 0; i < 3; ++i)
+      c[i] = 0.5 * (prim[1 + i] + prim[4 + i]);
+    const double hl[3] = { 0.5 * (prim[4] - prim[1]), 0.5 * (prim[5] - prim[2]), 0.5 * (prim[6] - prim[3]) };
+    rad = sqrt(hl[0] * hl[0] + hl[1] * hl[1] + hl[2] * hl[2]) + prim[7];
+  }
+  else
+  {
+    c[0] = prim[1];
+    c[1] = prim[2];
+    c[2] = prim[3];
+    rad = sqrt(prim[13] * prim[13] + prim[14] * prim[14] + prim[15] * prim[15]);
+  }
+  const double u[3] = { b[0] - a[0], b[1] - a[1], b[2] - a[2] };
+  const double uu = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
+  const double w[3] = { c[0] - a[0], c[1] - a[1], c[2] - a[2] };
+  const double t = (uu > 1e-24) ? fmin(fmax((w[0] * u[0] + w[1] * u[1] + w[2] * u[2]) / uu, 0.0), 1.0) : 0.0;
+  const double v[3] = { w[0] - t * u[0], w[1] - t * u[1], w[2] - t * u[2] };
+  // slack for rounding: the bound only filters candidates far from contact
+  return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]) - rad - r - 1e-9;
+}
+
 // Eigen::VectorXd::LinSpaced(size, low, high)(i) (Eigen 3.4 linspaced_op_impl)
 __device__ __forceinline__ double linspaced(int size, double low, double high, int i)
 {

@@ -88,6 +88,7 @@ enum DArr : int
   A_CSCR,    // contact-scan scratch: sphere centers [kWaves][kSubCap][n_spheres][3]
   A_HCOST,   // per step-pair collision cost scratch (N)
   A_HDIST,   // contact distance of each hinge row (h_cap)
+  A_HCCT,    // contact cc_time of each hinge row (h_cap; diagnostics, thip_collision_rows)
   A_HPK,     // ADMM-segment pack of the hinge rows, field-major [kHPack][n_h] (see admm_segment)
   A_HCHK,    // hinge chunk table: (first row, end row) int pairs, one double per chunk
   A_HPART,   // hinge chunk partial sums [n_chunks][16]

@@ -414,6 +414,10 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
     }
     const bool f0 = coll_fixed_step(c, t), f1 = coll_fixed_step(c, t + 1);
     const int ngr = c.T.n_groups;
+    // LVS_CONTINUOUS: candidates are the casts between consecutive sub-states
+    const bool cont = c.d->coll_continuous != 0;
+    const int nseg = cont ? cnt - 1 : cnt;
+    const int last = cnt - 1;
     long long* pf22 = (c.tid == 0) ? c.s->prof : nullptr;
     const long long tfk0 = pf22 ? clock64() : 0;
     for (int isub = c.lane; isub < cnt; isub += 64)
@@ -482,28 +486,52 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
         for (int e = 0; e < 16; ++e)
           prim[e] = S.scene[16 * p + e];
         const double rad = S.rad[s];
-        constexpr int kU = 8;  // sub-states per batch: their center loads are in flight together
-        for (int i0 = 0; i0 < cnt; i0 += kU)
+        constexpr int kU = 8;  // time indices per batch: their center loads are in flight together
+        for (int i0 = 0; i0 < nseg; i0 += kU)
         {
-          double cx[kU][3];
+          double cx[kU][3], cy[kU][3];
 #pragma unroll
           for (int u = 0; u < kU; ++u)
           {
-            const int i = min(i0 + u, cnt - 1);  // clamped: always a valid address
+            const int i = min(i0 + u, nseg - 1);  // clamped: always a valid address
             const double* cp = SCR + (i * ns + s) * 3;
-            cx[u][0] = cp[0];
-            cx[u][1] = cp[1];
-            cx[u][2] = cp[2];
+            const double* cq = SCR + ((cont ? i + 1 : i) * ns + s) * 3;
+            for (int r = 0; r < 3; ++r)
+            {
+              cx[u][r] = cp[r];
+              cy[u][r] = cq[r];
+            }
           }
 #pragma unroll
           for (int u = 0; u < kU; ++u)
           {
             const int i = i0 + u;
-            double dist, n[3], pr[3];
-            sphere_prim_distance(cx[u], rad, prim, dist, n, pr);
-            bool hit = (i < cnt) && dist < threshold && !(dist > margin + buffer);
+            double dist = 0.0;
+            bool hit = false;
+            int cct = 3;  // CCType of the robot link: 1 Time0, 2 Time1, 3 Between
+            if (i < nseg)
+            {
+              double n[3], pr[3];
+              if (cont)
+              {
+                if (swept_lower_bound(cx[u], cy[u], rad, prim) < threshold)
+                {
+                  double ts;
+                  swept_sphere_prim_distance(cx[u], cy[u], rad, prim, dist, n, pr, ts);
+                  hit = dist < threshold;
+                  cct = (i == 0 && ts == 0.0) ? 1 : ((i + 1 == last && ts == 1.0) ? 2 : 3);
+                }
+              }
+              else
+              {
+                sphere_prim_distance(cx[u], rad, prim, dist, n, pr);
+                hit = dist < threshold;
+                cct = (i == 0) ? 1 : ((i == last) ? 2 : 3);
+              }
+            }
+            hit = hit && !(dist > margin + buffer);
             if (hit && (f0 || f1))
-              hit = (f0 && i != 0) || (f1 && i != cnt - 1);
+              hit = (f0 && cct != 1) || (f1 && cct != 2);
             lcount += hit ? 1.0 : 0.0;
             lcost += hit ? fmax(margin - dist, 0.0) * coeff : 0.0;
           }
@@ -523,7 +551,7 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
     }
     int total = 0;
     for (int g = 0; g < ngr; ++g)
-      total += P * cnt * S.grp_ns[g];
+      total += P * nseg * S.grp_ns[g];
     int running = 0;
     double lcost = 0.0;  // per-lane partial cost, reduced once per pair
     const int base = (PASS == 1) ? out_base[t] : 0;
@@ -540,14 +568,14 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
         int rem = cand, g = 0;
         for (int gg = 0; gg + 1 < ngr; ++gg)
         {
-          const int sz = P * cnt * S.grp_ns[gg];
+          const int sz = P * nseg * S.grp_ns[gg];
           const bool adv = (g == gg) && (rem >= sz);
           rem = adv ? rem - sz : rem;
           g = adv ? g + 1 : g;
         }
         const int gn = S.grp_ns[g];
-        p = rem / (cnt * gn);
-        const int r2 = rem % (cnt * gn);
+        p = rem / (nseg * gn);
+        const int r2 = rem % (nseg * gn);
         i = r2 / gn;
         s = S.sph_order[S.grp_s0[g] + r2 % gn];
         double prim[16];
@@ -556,13 +584,31 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
         const double* cp = SCR + (i * ns + s) * 3;
         const double ctr[3] = { cp[0], cp[1], cp[2] };
         double n[3], pr[3];
-        sphere_prim_distance(ctr, S.rad[s], prim, dist, n, pr);
+        int cct;
+        if (cont)
+        {
+          const double* cq = SCR + ((i + 1) * ns + s) * 3;
+          const double ctr1[3] = { cq[0], cq[1], cq[2] };
+          dist = threshold;  // not a contact unless the cast says so
+          cct = 3;
+          if (swept_lower_bound(ctr, ctr1, S.rad[s], prim) < threshold)
+          {
+            double ts;
+            swept_sphere_prim_distance(ctr, ctr1, S.rad[s], prim, dist, n, pr, ts);
+            cct = (i == 0 && ts == 0.0) ? 1 : ((i + 1 == last && ts == 1.0) ? 2 : 3);
+          }
+        }
+        else
+        {
+          sphere_prim_distance(ctr, S.rad[s], prim, dist, n, pr);
+          cct = (i == 0) ? 1 : ((i == last) ? 2 : 3);
+        }
         hit = dist < threshold && !(dist > margin + buffer);
         // removeInvalidContactResults (collision_utils.cpp:73-114): at a
         // fixed end keep only contacts not at that end (cc_type of the
-        // robot link: Time0 at i = 0, Time1 at i = cnt - 1, else Between)
+        // robot link: Time0 / Time1 / Between)
         if (hit && (f0 || f1))
-          hit = (f0 && i != 0) || (f1 && i != cnt - 1);
+          hit = (f0 && cct != 1) || (f1 && cct != 2);
       }
       const unsigned long long mask = __ballot(hit);
       if (PASS == 0)
@@ -844,26 +890,46 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
     const double* q1 = x + (t + 1) * D;
     const int cnt = lvs_count(q0, q1, D, c.d->coll_lvs);
     const int link = c.d->sphere_link[s];
+    const bool cont = c.d->coll_continuous != 0;
     double q[THIP_MAX_DOF];
     for (int j = 0; j < D; ++j)
       q[j] = linspaced(cnt, q0[j], q1[j], i);
-    Pose T;
+    Pose T, T1;  // link pose at sub-state i (transform) and, for a cast, at i + 1 (cc_transform)
     chain_fk(ch, q, link, T);
     const double* cs = c.d->sphere_center[s];
     double ctr[3];
     for (int r = 0; r < 3; ++r)
       ctr[r] = T.r[r * 3 + 0] * cs[0] + T.r[r * 3 + 1] * cs[1] + T.r[r * 3 + 2] * cs[2] + T.t[r];
-    double dist, n[3], pr[3];
-    sphere_prim_distance(ctr, c.d->sphere_radius[s], c.scene + 16 * p, dist, n, pr);
-    // nearest_points_local[0] and the reference-point offset
-    // link_transform.linear() * nearest_points_local (sub-state pose)
+    double dist, n[3], pr[3], ts = 0.0;
+    if (cont)
+    {
+      double qn[THIP_MAX_DOF];
+      for (int j = 0; j < D; ++j)
+        qn[j] = linspaced(cnt, q0[j], q1[j], i + 1);
+      chain_fk(ch, qn, link, T1);
+      double ctr1[3];
+      for (int r = 0; r < 3; ++r)
+        ctr1[r] = T1.r[r * 3 + 0] * cs[0] + T1.r[r * 3 + 1] * cs[1] + T1.r[r * 3 + 2] * cs[2] + T1.t[r];
+      swept_sphere_prim_distance(ctr, ctr1, c.d->sphere_radius[s], c.scene + 16 * p, dist, n, pr, ts);
+    }
+    else
+    {
+      sphere_prim_distance(ctr, c.d->sphere_radius[s], c.scene + 16 * p, dist, n, pr);
+      T1 = T;
+    }
+    // nearest_points_local[0] in the frame of the sub-state (cast start) pose and the
+    // reference-point offsets link_transform.linear() * nearest_points_local with
+    // link_transform = transform (x_t part) / cc_transform (x_t+1 part), collision_terms.cpp:217-223
     const double w[3] = { pr[0] - T.t[0], pr[1] - T.t[1], pr[2] - T.t[2] };
-    double pl[3], rv[3];
+    double pl[3], rv0[3], rv1[3];
     for (int r = 0; r < 3; ++r)
       pl[r] = T.r[0 * 3 + r] * w[0] + T.r[1 * 3 + r] * w[1] + T.r[2 * 3 + r] * w[2];
     for (int r = 0; r < 3; ++r)
-      rv[r] = T.r[r * 3 + 0] * pl[0] + T.r[r * 3 + 1] * pl[1] + T.r[r * 3 + 2] * pl[2];
-    const double cc_time = double(i) * (1.0 / double(cnt - 1));
+    {
+      rv0[r] = T.r[r * 3 + 0] * pl[0] + T.r[r * 3 + 1] * pl[1] + T.r[r * 3 + 2] * pl[2];
+      rv1[r] = T1.r[r * 3 + 0] * pl[0] + T1.r[r * 3 + 1] * pl[1] + T1.r[r * 3 + 2] * pl[2];
+    }
+    const double cc_time = (cont ? (double(i) + ts) : double(i)) * (1.0 / double(cnt - 1));
     const bool f0 = coll_fixed_step(c, t), f1 = coll_fixed_step(c, t + 1);
     double cst = dist;
     int mask = 0;
@@ -879,6 +945,7 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
         continue;
       }
       const double scale = (e == 1) ? cc_time : (1 - cc_time);
+      const double* rv = (e == 1) ? rv1 : rv0;
       double J[6 * THIP_MAX_DOF];
       chain_jacobian(ch, qe, link, J);
       double gd = 0;
@@ -901,6 +968,7 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
     HK[k] = cst;
     HM[k] = mask;
     c.a(A_HDIST)[k] = dist;
+    c.a(A_HCCT)[k] = cc_time;
   }
   BSYNC();
 }
@@ -3930,7 +3998,8 @@ __global__ __launch_bounds__(kBlock) void coll_rows_kernel(KernelArgs args, cons
     r[3] = CONT[3 * k + 1];
     r[4] = i;
     r[5] = HD[k];
-    r[6] = double(i) * (1.0 / double(cnt - 1));
+    r[6] = c.a(A_HCCT)[k];
+    (void)cnt;
     r[7] = __popc(HM[k]);
     for (int j = 0; j < 2 * D; ++j)
       r[8 + j] = HC0[k * 2 * D + j];

@@ -177,6 +177,8 @@ static int validate(const thip_problem_desc* d, std::string& why)
     if (d->coll_first_step < 0 || d->coll_first_step >= d->n_steps || last < d->coll_first_step ||
         last >= d->n_steps)
       return why = "collision: bad first/last step", THIP_E_INVALID;
+    if (d->coll_continuous != 0 && d->coll_continuous != 1)
+      return why = "collision: coll_continuous must be 0 (LVS_DISCRETE) or 1 (LVS_CONTINUOUS)", THIP_E_INVALID;
     if (!(d->coll_lvs > 0) || !(d->coll_buffer >= 0))
       return why = "collision: bad longest_valid_segment_length / buffer", THIP_E_INVALID;
     for (int t = d->coll_first_step; t < last; ++t)
@@ -454,7 +456,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   sizes[A_PB] = std::max(nc + m, nab * D);
   sizes[A_PS] = sizes[A_PR] = nc + m;
   sizes[A_HC0] = sizes[A_HC] = hc * 2 * D;
-  sizes[A_HK] = sizes[A_HW] = sizes[A_HRE] = sizes[A_HDIST] = hc;
+  sizes[A_HK] = sizes[A_HW] = sizes[A_HRE] = sizes[A_HDIST] = sizes[A_HCCT] = hc;
   sizes[A_CPL] = L.hinge ? NDD : 1;
   sizes[A_CSCR] = L.coll ? (long long)kWaves * kSubCap * d.n_spheres * 3 : 1;
   sizes[A_HCOST] = L.N;

@@ -665,8 +665,10 @@ void CollisionTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value
 // problem_description.cpp:1735-1858, LVS_DISCRETE branch
 void CollisionTermInfo::hatch(TrajOptProb& prob)
 {
-  if (evaluator_type != 2)
-    unsupported("collision evaluator_type " + std::to_string(evaluator_type) + " (only LVS_DISCRETE = 2)");
+  // tesseract CollisionEvaluatorType {NONE, DISCRETE, LVS_DISCRETE, CONTINUOUS, LVS_CONTINUOUS}
+  if (evaluator_type < 2 || evaluator_type > 4)
+    unsupported("collision evaluator_type " + std::to_string(evaluator_type) +
+                " (LVS_DISCRETE = 2, CONTINUOUS = 3, LVS_CONTINUOUS = 4 are)");
   if (contact_test_type != 2)
     unsupported("collision contact_test_type " + std::to_string(contact_test_type) + " (only ALL = 2)");
   if (has_pairs)
@@ -699,7 +701,9 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
   d.coll_margin = dist_pen;
   d.coll_coeff = coeff;
   d.coll_buffer = collision_margin_buffer;
-  d.coll_lvs = longest_valid_segment_length;
+  // CONTINUOUS casts each step pair once (lvs = max(), problem_description.cpp:1742-1744)
+  d.coll_continuous = (evaluator_type >= 3) ? 1 : 0;
+  d.coll_lvs = (evaluator_type == 3) ? 1.7976931348623157e308 : longest_valid_segment_length;
   d.n_spheres = static_cast<int>(env->collision_spheres.size());
   for (int s = 0; s < d.n_spheres; ++s)
   {

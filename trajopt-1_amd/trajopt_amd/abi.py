@@ -127,6 +127,7 @@ class ProblemDesc(C.Structure):
         ("coll_coeff", C.c_double),
         ("coll_buffer", C.c_double),
         ("coll_lvs", C.c_double),
+        ("coll_continuous", C.c_int),
         ("n_spheres", C.c_int),
         ("sphere_link", C.c_int * MAX_SPHERES),
         ("sphere_center", _D3 * MAX_SPHERES),
