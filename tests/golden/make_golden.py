@@ -21,6 +21,7 @@ Contents (all fp64):
   sqp_jv.npz        JointVel-only (no CartPose) variant, 12 steps, 4 problems
   sqp_C.npz         config C (B + LVS-discrete collision cost, 10-primitive
                     scene) problems 0..2
+  collision_rows_C_cont.npz  LVS_CONTINUOUS rows of 3 config C problems at init
   collision_rows_C.npz  linearised collision rows of those problems at their
                     converged trajectories (oracle_collision_rows)
 """
@@ -80,7 +81,17 @@ def main():
     x, _ = oracle.solve(wl, n_threads=3)
     np.savez(HERE / "collision_rows_C.npz", x=x,
              **{f"rows{b}": oracle.collision_rows(wl, b, x[b]) for b in range(3)})
+    continuous_fixture()
     print("golden fixtures written to", HERE)
+
+
+def continuous_fixture():
+    """collision_rows_C_cont.npz: LVS_CONTINUOUS rows (swept-sphere casts) of
+    3 config C problems at their initial trajectories."""
+    wl = problems.make_workload("C", 3)
+    wl.desc.coll_continuous = 1
+    np.savez(HERE / "collision_rows_C_cont.npz", x=wl.init,
+             **{f"rows{b}": oracle.collision_rows(wl, b, wl.init[b]) for b in range(3)})
 
 
 if __name__ == "__main__":

@@ -156,3 +156,14 @@ def test_swept_sphere_distance_is_the_minimum_along_the_cast(oracle_mod):
         assert sampled - d < 1e-3
         assert 0.0 <= t <= 1.0
         assert abs(oracle_mod.sphere_prim(a + t * (b - a), r, prim)[0] - d) < 1e-14
+
+
+def test_continuous_collision_rows_golden(oracle_mod, golden):
+    """The oracle's LVS_CONTINUOUS rows against the committed fixture
+    (tests/golden/make_golden.py: continuous_fixture)."""
+    g = golden("collision_rows_C_cont")
+    wl = problems.make_workload("C", 3)
+    wl.desc.coll_continuous = 1
+    for b in range(3):
+        r = oracle_mod.collision_rows(wl, b, g["x"][b])
+        np.testing.assert_array_equal(r, g[f"rows{b}"])

@@ -239,6 +239,16 @@ def test_collision_rows_golden(golden):
         _check_rows(rows[b], g[f"rows{b}"], f"golden problem {b}")
 
 
+def test_collision_rows_golden_continuous(golden):
+    g = golden("collision_rows_C_cont")
+    wl = _continuous(problems.make_workload("C", 3))
+    s = BatchTrustRegionSQP(wl)
+    rows = s.collision_rows(g["x"])
+    s.close()
+    for b in range(3):
+        _check_rows(rows[b], g[f"rows{b}"], f"golden continuous problem {b}", cc_atol=1e-12)
+
+
 def test_sqp_parity_collision(oracle_mod, golden):
     g = golden("sqp_C")
     wl = problems.make_workload("C", 3)
