@@ -15,6 +15,12 @@ relative) and the accept/shrink ratio computed from it falls on different
 sides of its threshold.  Such problems must still reach the same status,
 flags and a total cost within 2 %, and they may not exceed 15 % of a batch of
 32 or more problems.
+
+A problem whose status or flag differs passes only if the oracle itself is
+unstable on it at rounding level: rerun from the same initial trajectory
+perturbed by 1e-13 (interior waypoints), the oracle reaches the GPU's status
+and flag.  Such a problem's SQP outcome is not a function of its inputs at
+double precision, on either side; it counts against the 15 % as well.
 """
 import json
 import subprocess
@@ -59,20 +65,39 @@ def _first_split(tg, to):
     return n
 
 
+def _perturbed_oracle_outcomes(wl, oracle_mod, tol, seeds=(1, 2, 3)):
+    """(status, flag) per problem of the oracle rerun from 1e-13-perturbed initial trajectories."""
+    out = [set() for _ in range(wl.batch)]
+    for seed in seeds:
+        wp = wl.slice(0, wl.batch)
+        rng = np.random.default_rng(seed)
+        wp.init[:, 1:] += rng.normal(0.0, 1e-13, wp.init[:, 1:].shape)
+        _, rp = oracle_mod.solve(wp, n_threads=16)
+        for b in range(wl.batch):
+            out[b].add((rp[b].status, rp[b].max_cnt_viol < tol))
+    return out
+
+
 def check_parity(wl, oracle_mod, x, res, tr=None, min_strict=0.85, label=""):
     xo, ro = oracle_mod.solve(wl, n_threads=16)
     tol = wl.desc.sqp.cnt_tolerance
     B = wl.batch
-    bad = []
+    bad, chaotic, perturbed = [], [], None
     for b in range(B):
-        assert res[b].status == ro[b].status, f"{label} problem {b}: status {res[b].status} vs {ro[b].status}"
         fg, fo = res[b].max_cnt_viol < tol, ro[b].max_cnt_viol < tol
-        assert fg == fo, f"{label} problem {b}: constraint flag {fg} vs {fo}"
+        if res[b].status != ro[b].status or fg != fo:
+            if perturbed is None:
+                perturbed = _perturbed_oracle_outcomes(wl, oracle_mod, tol)
+            assert (res[b].status, fg) in perturbed[b], (
+                f"{label} problem {b}: status {res[b].status} vs {ro[b].status}, constraint flag {fg} vs {fo}; "
+                f"perturbed oracle runs reach {sorted(perturbed[b])}")
+            chaotic.append(b)
+            continue
         if np.abs(x[b] - xo[b]).max() > TOL_X:
             bad.append(b)
-    strict = 1.0 - len(bad) / B
+    strict = 1.0 - (len(bad) + len(chaotic)) / B
     if B >= 32:  # the fraction bound is only meaningful on a real batch
-        assert strict >= min_strict, f"{label}: only {strict:.2%} of problems within {TOL_X}: {bad}"
+        assert strict >= min_strict, f"{label}: only {strict:.2%} of problems within {TOL_X}: {bad} {chaotic}"
     if not bad:
         return
     if tr is None:
@@ -99,8 +124,9 @@ def check_parity(wl, oracle_mod, x, res, tr=None, min_strict=0.85, label=""):
 
 
 # ------------------------------------------------------------------ kinematics
-def test_fwd_kin_parity(oracle_mod):
-    wl = problems.make_workload("B", 4)
+@pytest.mark.parametrize("robot", ["right_arm", "torso_right_arm", "right_arm_6dof"])
+def test_fwd_kin_parity(oracle_mod, robot):
+    wl = problems.make_workload("B", 4, robot=robot)
     s = BatchTrustRegionSQP(wl)
     poses = s.fwd_kin(wl.init)
     s.close()
@@ -389,6 +415,21 @@ def _variant(name):
         return wl
     if name == "single_problem":
         return problems.make_workload("B", 1, first_problem=5)
+    # other chains: 8 DoF with the prismatic torso_lift_joint first, and 6 DoF
+    if name == "torso_arm_8dof_A":
+        return problems.make_workload("A", 16, robot="torso_right_arm")
+    if name == "torso_arm_8dof_B":
+        return problems.make_workload("B", 8, robot="torso_right_arm")
+    if name == "torso_arm_8dof_C":
+        return problems.make_workload("C", 8, robot="torso_right_arm")
+    if name == "torso_arm_8dof_jointpos":
+        return problems.make_workload("J", 16, robot="torso_right_arm", goal_offset=0.05)
+    if name == "arm_6dof_A":
+        # square CartPose constraint (6 rows, 6 DoF): several problems stall in the penalty loop and their
+        # outcome flips under 1e-13 input perturbations of the oracle itself (problem 9 does)
+        return problems.make_workload("A", 16, robot="right_arm_6dof")
+    if name == "arm_6dof_C":
+        return problems.make_workload("C", 8, robot="right_arm_6dof")
     raise KeyError(name)
 
 
@@ -396,7 +437,9 @@ VARIANTS = ["jointvel_only", "short_horizon", "two_fixed_steps", "position_only_
             "sqp_iteration_cap", "sqp_iteration_cap_costs_only", "no_scaling", "no_polish", "no_adaptive_rho_no_warm_start", "single_problem",
             "jointpos_goal", "jointpos_goal_offset", "jointpos_far_goal_penalty_limit", "jointpos_with_cartpose",
             "jointvel_ineq_cost", "jointpos_ineq_cost_and_cnt", "collision_with_static_hinges", "max_horizon_64",
-            "min_horizon_2", "collision_empty_scene", "collision_fixed_both_ends", "collision_step_subrange"]
+            "min_horizon_2", "collision_empty_scene", "collision_fixed_both_ends", "collision_step_subrange",
+            "torso_arm_8dof_A", "torso_arm_8dof_B", "torso_arm_8dof_C", "torso_arm_8dof_jointpos", "arm_6dof_A",
+            "arm_6dof_C"]
 
 
 @pytest.mark.parametrize("name", VARIANTS)

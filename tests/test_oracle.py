@@ -27,6 +27,25 @@ def test_fk_oracle_vs_numpy(oracle_mod, golden):
     np.testing.assert_allclose(poses, g["poses_numpy"], rtol=0, atol=1e-12)
 
 
+@pytest.mark.parametrize("robot", ["torso_right_arm", "right_arm_6dof"])
+def test_fk_oracle_vs_numpy_other_chains(oracle_mod, robot):
+    """The prismatic torso_lift_joint (8 DoF) and a 6-DoF chain: oracle FK
+    against the numpy FK, and the torso joint moves the arm along +z."""
+    wl = problems.make_workload("A", 4, robot=robot)
+    chain = wl.desc.chain
+    q = wl.init.reshape(-1, wl.n_dof)
+    poses = oracle_mod.fwd_kin(chain, q)
+    for i in range(q.shape[0]):
+        ref = robots.fwd_kin(chain, q[i])
+        for k in range(chain.n_links):
+            np.testing.assert_allclose(poses[i, k], ref[k][:3, :].reshape(12), rtol=0, atol=1e-12)
+    if robot == "torso_right_arm":
+        q2 = q.copy()
+        q2[:, 0] += 0.1
+        d = oracle_mod.fwd_kin(chain, q2)[:, -1, [3, 7, 11]] - poses[:, -1, [3, 7, 11]]
+        np.testing.assert_allclose(d, np.tile([0.0, 0.0, 0.1], (q.shape[0], 1)), atol=1e-12)
+
+
 @pytest.mark.parametrize("cfg", ["A", "B"])
 def test_cartpose_linearization_golden(oracle_mod, golden, cfg):
     g = golden(f"cartpose_{cfg}")

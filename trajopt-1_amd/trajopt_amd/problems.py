@@ -34,7 +34,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import abi
-from .robots import PR2_TOOL_LINK, chain_limits, fwd_kin, pr2_right_arm
+from .robots import PR2_TOOL_LINK, ROBOTS, chain_limits, fwd_kin
 
 SEED_BASE = 20261015
 _MASK = (1 << 64) - 1
@@ -108,10 +108,10 @@ def _pose12_in_root(chain, q, link):
     return rel[:3, :].reshape(12)
 
 
-def base_desc(n_steps: int) -> abi.ProblemDesc:
+def base_desc(n_steps: int, robot: str = "right_arm") -> abi.ProblemDesc:
     d = abi.ProblemDesc()
     d.n_steps = n_steps
-    d.chain = pr2_right_arm()
+    d.chain = ROBOTS[robot][0]()
     d.n_fixed = 1
     d.fixed_steps[0] = 0
     d.jv_enabled = 1
@@ -125,10 +125,10 @@ def base_desc(n_steps: int) -> abi.ProblemDesc:
     return d
 
 
-def _add_cart(d, k, step, is_cnt):
+def _add_cart(d, k, step, is_cnt, tool=PR2_TOOL_LINK):
     d.cart_step[k] = step
     d.cart_is_cnt[k] = 1 if is_cnt else 0
-    d.cart_source_link[k] = PR2_TOOL_LINK
+    d.cart_source_link[k] = tool
     eye = [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0]
     for i in range(12):
         d.cart_source_offset[k][i] = eye[i]
@@ -138,7 +138,9 @@ def _add_cart(d, k, step, is_cnt):
 
 
 def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int | None = None,
-                  goal_offset: float = 0.0) -> Workload:
+                  goal_offset: float = 0.0, robot: str = "right_arm") -> Workload:
+    """Synthetic workload of SURVEY.md §8d config A/B/C (or J: JointPos terms).  robot picks the chain
+    (robots.ROBOTS); the default is the reference's PR2 right_arm group."""
     config = config.upper()
     if config == "A":
         N = n_steps or 10
@@ -148,22 +150,23 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
         N = n_steps or 10
     else:
         raise ValueError(f"unknown config {config}")
-    d = base_desc(N)
+    d = base_desc(N, robot)
     chain = d.chain
+    _, tool, link_offset = ROBOTS[robot]
     lo, hi, types = chain_limits(chain)
     D = chain.n_dof
     if config == "A":
         d.n_cart = 1
-        _add_cart(d, 0, N - 1, True)
+        _add_cart(d, 0, N - 1, True, tool)
     elif config == "J":
         d.n_cart = 0
     else:
         d.n_cart = N - 1
         for k, t in enumerate(range(1, N)):
-            _add_cart(d, k, t, False)
+            _add_cart(d, k, t, False, tool)
     if config == "C":
         from .scene import add_collision_model
-        add_collision_model(d)
+        add_collision_model(d, link_offset)
     jpos_targets = None
     if config == "J":
         q_lo = np.where(types == abi.JOINT_CONTINUOUS, -math.pi, lo)
@@ -203,13 +206,13 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
             for j in range(D):
                 init[b, t, j] += rng.normal(0.02)
         if config == "A":
-            targets[b, 0] = _pose12_in_root(chain, q_ref[(N - 1) // 2], PR2_TOOL_LINK)
+            targets[b, 0] = _pose12_in_root(chain, q_ref[(N - 1) // 2], tool)
         else:
             for k in range(d.n_cart):
-                targets[b, k] = _pose12_in_root(chain, q_ref[d.cart_step[k]], PR2_TOOL_LINK)
+                targets[b, k] = _pose12_in_root(chain, q_ref[d.cart_step[k]], tool)
         if config == "C":
             from .scene import make_scene
-            scene[b] = make_scene(rng, chain, q_ref, d)
+            scene[b] = make_scene(rng, chain, q_ref, d, link_offset)
     return Workload(config, d, init, targets, scene, q_refs, jpos_targets)
 
 

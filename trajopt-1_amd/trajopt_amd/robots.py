@@ -14,7 +14,7 @@ import math
 
 import numpy as np
 
-from .abi import JOINT_CONTINUOUS, JOINT_FIXED, JOINT_REVOLUTE, Chain
+from .abi import JOINT_CONTINUOUS, JOINT_FIXED, JOINT_PRISMATIC, JOINT_REVOLUTE, Chain
 
 
 def _pose(xyz=(0.0, 0.0, 0.0)):
@@ -41,16 +41,45 @@ PR2_RIGHT_ARM = [
 # world pose of torso_lift_link: base_footprint -> base_link (0,0,0.051) -> torso (-0.05,0,0.739675), q_torso = 0
 PR2_TORSO_WORLD = (-0.05, 0.0, 0.051 + 0.739675)
 PR2_TOOL_LINK = 11  # r_gripper_tool_frame
+# torso_lift_joint (arm_around_table.urdf:735-745): prismatic along z, base_link -> torso_lift_link
+PR2_TORSO_JOINT = ("torso_lift_joint", JOINT_PRISMATIC, (-0.05, 0.0, 0.739675), (0, 0, 1), (0.0, 0.33))
+PR2_BASE_LINK_WORLD = (0.0, 0.0, 0.051)
+
+# Robots the synthetic workloads can use: name -> (chain builder, tool link, link offset of the arm links).
+# "right_arm" is the reference's right_arm group (7 DoF); "torso_right_arm" prepends the prismatic torso
+# joint (8 DoF, the full_body group's torso + right arm joints, pr2.srdf:51-70); "right_arm_6dof" is a
+# synthetic 6-DoF variant with r_wrist_roll_joint held fixed at 0.
 
 
 def pr2_right_arm() -> Chain:
+    return _chain(PR2_TORSO_WORLD, PR2_RIGHT_ARM)
+
+
+def pr2_torso_right_arm() -> Chain:
+    return _chain(PR2_BASE_LINK_WORLD, [PR2_TORSO_JOINT] + PR2_RIGHT_ARM)
+
+
+def pr2_right_arm_6dof() -> Chain:
+    joints = [(n, JOINT_FIXED, xyz, None, None) if n == "r_wrist_roll_joint" else (n, t, xyz, ax, lim)
+              for n, t, xyz, ax, lim in PR2_RIGHT_ARM]
+    return _chain(PR2_TORSO_WORLD, joints)
+
+
+ROBOTS = {
+    "right_arm": (pr2_right_arm, PR2_TOOL_LINK, 0),
+    "torso_right_arm": (pr2_torso_right_arm, PR2_TOOL_LINK + 1, 1),
+    "right_arm_6dof": (pr2_right_arm_6dof, PR2_TOOL_LINK, 0),
+}
+
+
+def _chain(base_xyz, joints) -> Chain:
     c = Chain()
-    c.n_links = len(PR2_RIGHT_ARM) + 1
-    base = _pose(PR2_TORSO_WORLD)
+    c.n_links = len(joints) + 1
+    base = _pose(base_xyz)
     for i in range(12):
         c.base_pose[i] = base[i]
     dof = 0
-    for k, (_, jtype, xyz, axis, lim) in enumerate(PR2_RIGHT_ARM, start=1):
+    for k, (_, jtype, xyz, axis, lim) in enumerate(joints, start=1):
         c.joint_type[k] = jtype
         o = _pose(xyz)
         for i in range(12):

@@ -50,8 +50,9 @@ N_PRIMS = 10
 MARGIN, COEFF, BUFFER, LVS = 0.025, 20.0, 0.05, 0.05
 
 
-def add_collision_model(d: abi.ProblemDesc):
-    """LVS_DISCRETE collision cost over all step pairs, step 0 fixed."""
+def add_collision_model(d: abi.ProblemDesc, link_offset: int = 0):
+    """LVS_DISCRETE collision cost over all step pairs, step 0 fixed.  link_offset shifts the sphere links
+    for chains with extra links before the arm (robots.ROBOTS)."""
     d.coll_enabled = 1
     d.coll_is_cnt = 0
     d.coll_first_step = 0
@@ -64,7 +65,7 @@ def add_collision_model(d: abi.ProblemDesc):
     d.coll_lvs = LVS
     d.n_spheres = len(PR2_ARM_SPHERES)
     for s, (link, c, r) in enumerate(PR2_ARM_SPHERES):
-        d.sphere_link[s] = link
+        d.sphere_link[s] = link + link_offset
         for i in range(3):
             d.sphere_center[s][i] = c[i]
         d.sphere_radius[s] = r
@@ -88,17 +89,18 @@ def _rotation(rng):
     ])
 
 
-def sphere_centers(chain, q):
+def sphere_centers(chain, q, link_offset: int = 0):
     """World centers of the robot spheres at joint values q."""
     T = fwd_kin(chain, q)
-    return np.array([T[link][:3, :3] @ np.array(c) + T[link][:3, 3] for link, c, _ in PR2_ARM_SPHERES])
+    return np.array([T[link + link_offset][:3, :3] @ np.array(c) + T[link + link_offset][:3, 3]
+                     for link, c, _ in PR2_ARM_SPHERES])
 
 
-def make_scene(rng, chain, q_ref, d) -> np.ndarray:
+def make_scene(rng, chain, q_ref, d, link_offset: int = 0) -> np.ndarray:
     """10 primitive records near the reference path of one problem."""
     N = q_ref.shape[0]
     prims = np.zeros((N_PRIMS, 16))
-    path = [sphere_centers(chain, q_ref[t]) for t in range(N)]
+    path = [sphere_centers(chain, q_ref[t], link_offset) for t in range(N)]
     radii = [r for _, _, r in PR2_ARM_SPHERES]
     for k in range(N_PRIMS):
         for _attempt in range(64):
