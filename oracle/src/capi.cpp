@@ -226,7 +226,7 @@ int oracle_collision_rows(const thip_problem_desc* d, const double* scene, const
     cm.coeff = d->coll_coeff;
     cm.buffer = d->coll_buffer;
     cm.lvs = d->coll_lvs;
-    cm.continuous = d->coll_continuous != 0;
+    cm.continuous = d->coll_continuous == 1;
     const int first = d->coll_first_step;
     const int last = (d->coll_last_step < 0) ? N - 1 : d->coll_last_step;
     auto fixed = [&](int t) {
@@ -237,6 +237,56 @@ int oracle_collision_rows(const thip_problem_desc* d, const double* scene, const
     };
     const int W = 8 + 2 * D + 1;
     int n = 0;
+    if (d->coll_continuous == 2)
+    {
+      // DISCRETE: one record per contact of each free waypoint t, a_t = the
+      // single-timestep expression's coefficients, a_t+1 = 0, cc_time 0
+      for (int t = first; t <= last; ++t)
+      {
+        if (fixed(t))
+          continue;
+        const double* q = x + t * D;
+        for (const auto& c : calcCollisionsSingle(cm, q))
+        {
+          double g[THIP_MAX_DOF], sc, gd = 0;
+          contactGradient(cm, q, c, false, g, sc);
+          double cst = 0;
+          int kept = 0;
+          double a0[THIP_MAX_DOF] = {};
+          for (int j = 0; j < D; ++j)
+          {
+            a0[j] = sc * g[j];
+            gd += g[j] * q[j];
+            if (std::fabs(a0[j]) > 1e-7)
+              ++kept;
+            else
+              a0[j] = 0;
+          }
+          cst += sc * -gd;
+          cst += c.distance;
+          if (n < cap)
+          {
+            double* r = out + static_cast<std::size_t>(n) * W;
+            r[0] = t;
+            r[1] = c.link;
+            r[2] = c.prim;
+            r[3] = c.sphere;
+            r[4] = 0;
+            r[5] = c.distance;
+            r[6] = 0;
+            r[7] = kept;
+            for (int j = 0; j < D; ++j)
+            {
+              r[8 + j] = a0[j];
+              r[8 + D + j] = 0;
+            }
+            r[8 + 2 * D] = cst;
+          }
+          ++n;
+        }
+      }
+      return n;
+    }
     for (int t = first; t < last; ++t)
     {
       const bool f0 = fixed(t), f1 = fixed(t + 1);

@@ -288,6 +288,50 @@ double linspaced(int size, double low, double high, int i)
 constexpr int kCCNone = 0, kCCTime0 = 1, kCCTime1 = 2, kCCBetween = 3;
 }  // namespace
 
+// SingleTimestepCollisionEvaluator::CalcCollisions (collision_terms.cpp:653-688):
+// FK at one state, contactTest, then the filter drops contacts beyond
+// margin + buffer (no cc_type filtering; the results keep CCType_None).
+std::vector<Contact> calcCollisionsSingle(const CollisionModel& cm, const double* q)
+{
+  const thip_chain& ch = *cm.chain;
+  const double threshold = cm.margin + cm.buffer;
+  std::map<std::pair<int, int>, std::vector<Contact>> results;
+  std::vector<Iso3> T;
+  chainFwdKin(ch, q, T);
+  for (int s = 0; s < cm.n_spheres; ++s)
+  {
+    const int link = cm.sphere_link[s];
+    const Iso3& Tl = T[static_cast<std::size_t>(link)];
+    double c[3];
+    for (int r = 0; r < 3; ++r)
+      c[r] = Tl.R[r * 3 + 0] * cm.sphere_center[s][0] + Tl.R[r * 3 + 1] * cm.sphere_center[s][1] +
+             Tl.R[r * 3 + 2] * cm.sphere_center[s][2] + Tl.t[r];
+    for (int p = 0; p < cm.n_prims; ++p)
+    {
+      Contact ct;
+      spherePrimDistance(c, cm.sphere_radius[s], cm.scene + 16 * p, ct.distance, ct.normal, ct.p_robot, ct.p_prim);
+      if (!(ct.distance < threshold) || ct.distance > cm.margin + cm.buffer)
+        continue;
+      ct.link = link;
+      ct.prim = p;
+      ct.sphere = s;
+      ct.substate = 0;
+      ct.transform = Tl;
+      ct.cc_transform = Tl;
+      const double w[3] = { ct.p_robot[0] - Tl.t[0], ct.p_robot[1] - Tl.t[1], ct.p_robot[2] - Tl.t[2] };
+      for (int r = 0; r < 3; ++r)
+        ct.p_local[r] = Tl.R[0 * 3 + r] * w[0] + Tl.R[1 * 3 + r] * w[1] + Tl.R[2 * 3 + r] * w[2];
+      ct.cc_time = 0;
+      ct.cc_type = 0;  // CCType_None
+      results[{ link, p }].push_back(ct);
+    }
+  }
+  std::vector<Contact> flat;
+  for (auto& kv : results)
+    flat.insert(flat.end(), kv.second.begin(), kv.second.end());
+  return flat;
+}
+
 // DiscreteCollisionEvaluator::CalcCollisions (collision_terms.cpp:817-898) for
 // the step pair (q0, q1); results flattened in ContactResultMap order: link
 // pair key (robot link, primitive), then insertion (sub-state, sphere).
@@ -443,12 +487,15 @@ void contactGradient(const CollisionModel& cm, const double* dofvals, const Cont
   const int D = ch.n_dof;
   double J[6 * THIP_MAX_DOF];
   chainJacobian(ch, dofvals, ct.link, J);
-  // link_transform = isTimestep1 ? cc_transform : transform (collision_terms.cpp:278-279)
-  const Iso3& lt = timestep1 ? ct.cc_transform : ct.transform;
+  // scale 1 and link_transform = transform for CCType_None; otherwise scale
+  // (1 - cc_time) / cc_time and link_transform = transform / cc_transform
+  // (collision_terms.cpp:214-221)
+  const bool none = ct.cc_type == kCCNone;
+  const Iso3& lt = (timestep1 && !none) ? ct.cc_transform : ct.transform;
   double r[3];
   for (int i = 0; i < 3; ++i)
     r[i] = lt.R[i * 3 + 0] * ct.p_local[0] + lt.R[i * 3 + 1] * ct.p_local[1] + lt.R[i * 3 + 2] * ct.p_local[2];
-  scale = timestep1 ? ct.cc_time : (1 - ct.cc_time);
+  scale = none ? 1.0 : (timestep1 ? ct.cc_time : (1 - ct.cc_time));
   for (int j = 0; j < D; ++j)
   {
     // jacobianChangeRefPoint: J_lin += J_ang x r
@@ -535,12 +582,66 @@ private:
   int type_;
 };
 
+// The distance expressions of one waypoint (DISCRETE evaluator,
+// CalcDistExpressionsSingleTimeStep, collision_terms.cpp:538-554):
+// dist = 0 + g.x - g.q (CollisionsToDistanceExpressions with vars0, scale 1),
+// then + d, cleanupAff'd.
+class CollisionSingleCalc
+{
+public:
+  CollisionSingleCalc(std::shared_ptr<const CollisionModel> cm, VarVector v0) : cm_(std::move(cm)), vars0_(std::move(v0))
+  {
+  }
+
+  VarVector vars() const { return vars0_; }
+
+  std::vector<Contact> collide(const DblVec& x) const
+  {
+    const DblVec q = getDblVec(x, vars0_);
+    return calcCollisionsSingle(*cm_, q.data());
+  }
+
+  AffExprVector exprs(const DblVec& x) const
+  {
+    AffExprVector out;
+    const auto contacts = collide(x);
+    const DblVec q = getDblVec(x, vars0_);
+    const int D = cm_->chain->n_dof;
+    for (const auto& c : contacts)
+    {
+      AffExpr e(0.0);
+      double g[THIP_MAX_DOF], scale;
+      contactGradient(*cm_, q.data(), c, false, g, scale);
+      AffExpr part;
+      double gd = 0;
+      for (int j = 0; j < D; ++j)
+      {
+        part.coeffs.push_back(scale * g[j]);
+        part.vars.push_back(vars0_[static_cast<std::size_t>(j)]);
+        gd += g[j] * q[static_cast<std::size_t>(j)];
+      }
+      exprInc(e, part);
+      exprInc(e, scale * -gd);
+      exprInc(e, c.distance);
+      out.push_back(cleanupAff(e));
+    }
+    return out;
+  }
+
+  const CollisionModel& model() const { return *cm_; }
+
+private:
+  std::shared_ptr<const CollisionModel> cm_;
+  VarVector vars0_;
+};
+
 // One CollisionCost term per step pair (CollisionTermInfo::hatch,
-// problem_description.cpp:1735-1781).
+// problem_description.cpp:1735-1781) or per free waypoint (DISCRETE, :1782-1796).
+template <class Calc>
 class CollisionPairCost : public Cost
 {
 public:
-  explicit CollisionPairCost(CollisionPairCalc calc) : calc_(std::move(calc)) {}
+  explicit CollisionPairCost(Calc calc) : calc_(std::move(calc)) {}
   VarVector getVars() override { return calc_.vars(); }
 
   // CollisionCost::value (collision_terms.cpp:1287-1306): no buffer
@@ -564,15 +665,16 @@ public:
   }
 
 private:
-  CollisionPairCalc calc_;
+  Calc calc_;
 };
 
 // One CollisionConstraint per step pair (problem_description.cpp:1797-1840,
-// prob.addIneqConstraint).
+// prob.addIneqConstraint) or per free waypoint (DISCRETE, :1842-1856).
+template <class Calc>
 class CollisionPairConstraint : public Constraint
 {
 public:
-  explicit CollisionPairConstraint(CollisionPairCalc calc) : calc_(std::move(calc)) {}
+  explicit CollisionPairConstraint(Calc calc) : calc_(std::move(calc)) {}
   VarVector getVars() override { return calc_.vars(); }
   ConstraintType type() override { return INEQ; }
 
@@ -597,7 +699,7 @@ public:
   }
 
 private:
-  CollisionPairCalc calc_;
+  Calc calc_;
 };
 }  // namespace
 
@@ -621,7 +723,7 @@ void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, cons
   cm->coeff = d.coll_coeff;
   cm->buffer = d.coll_buffer;
   cm->lvs = d.coll_lvs;
-  cm->continuous = d.coll_continuous != 0;
+  cm->continuous = d.coll_continuous == 1;
   const int first = d.coll_first_step;
   const int last = (d.coll_last_step < 0) ? d.n_steps - 1 : d.coll_last_step;
   auto fixed = [&](int t) {
@@ -630,6 +732,29 @@ void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, cons
         return true;
     return false;
   };
+  if (d.coll_continuous == 2)
+  {
+    // DISCRETE: SINGLE_TIME_STEP terms on the free waypoints of [first, last]
+    for (int i = first; i <= last; ++i)
+    {
+      if (fixed(i))
+        continue;
+      CollisionSingleCalc calc(cm, rows[static_cast<std::size_t>(i)]);
+      if (d.coll_is_cnt)
+      {
+        auto c = std::make_shared<CollisionPairConstraint<CollisionSingleCalc>>(std::move(calc));
+        c->setName("collision_" + std::to_string(i));
+        tp.prob->addConstraint(c);
+      }
+      else
+      {
+        auto c = std::make_shared<CollisionPairCost<CollisionSingleCalc>>(std::move(calc));
+        c->setName("collision_" + std::to_string(i));
+        tp.prob->addCost(c);
+      }
+    }
+    return;
+  }
   for (int i = first; i < last; ++i)
   {
     const bool cf = fixed(i), nf = fixed(i + 1);
@@ -645,13 +770,13 @@ void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, cons
     CollisionPairCalc calc(cm, rows[static_cast<std::size_t>(i)], rows[static_cast<std::size_t>(i + 1)], type);
     if (d.coll_is_cnt)
     {
-      auto c = std::make_shared<CollisionPairConstraint>(std::move(calc));
+      auto c = std::make_shared<CollisionPairConstraint<CollisionPairCalc>>(std::move(calc));
       c->setName("collision_" + std::to_string(i));
       tp.prob->addConstraint(c);
     }
     else
     {
-      auto c = std::make_shared<CollisionPairCost>(std::move(calc));
+      auto c = std::make_shared<CollisionPairCost<CollisionPairCalc>>(std::move(calc));
       c->setName("collision_" + std::to_string(i));
       tp.prob->addCost(c);
     }

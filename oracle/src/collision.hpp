@@ -2,6 +2,7 @@
 //
 // CPU restatement of the LVS-discrete collision term on a primitive scene:
 //   DiscreteCollisionEvaluator::CalcCollisions  trajopt/src/collision_terms.cpp:817-898
+//   SingleTimestepCollisionEvaluator            trajopt/src/collision_terms.cpp:538-554,600-688 (DISCRETE)
 //   CastCollisionEvaluator::CalcCollisions      trajopt/src/collision_terms.cpp:1065-1161 (LVS_CONTINUOUS)
 //   CollisionEvaluator::GetGradient             trajopt/src/collision_terms.cpp:195-242
 //   CollisionsToDistanceExpressions             trajopt/src/collision_terms.cpp:341-386
@@ -50,7 +51,7 @@ struct Contact
   Iso3 transform;      // robot link pose at the sub-state (discrete) / at the cast's start state (continuous)
   Iso3 cc_transform;   // = transform (discrete) / link pose at the cast's end state (continuous)
   double cc_time = 0;  // interpolation time of the sub-state / of the closest point along the cast
-  int cc_type = 0;     // 1 Time0, 2 Time1, 3 Between
+  int cc_type = 0;     // 0 None (single-timestep contactTest), 1 Time0, 2 Time1, 3 Between
 };
 
 void spherePrimDistance(const double c[3], double r, const double* prim, double& dist, double n[3],
@@ -59,6 +60,7 @@ void spherePrimDistance(const double c[3], double r, const double* prim, double&
 // distance min_t d(a + t (b - a)) and its first minimiser t (see collision.cpp).
 void sweptSpherePrimDistance(const double a[3], const double b[3], double r, const double* prim, double& dist,
                              double n[3], double p_robot[3], double p_prim[3], double& t_star);
+std::vector<Contact> calcCollisionsSingle(const CollisionModel& cm, const double* q);
 std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, const double* q1, bool vars0_fixed,
                                     bool vars1_fixed);
 void contactGradient(const CollisionModel& cm, const double* dofvals, const Contact& ct, bool timestep1,

@@ -82,6 +82,7 @@ def main():
     np.savez(HERE / "collision_rows_C.npz", x=x,
              **{f"rows{b}": oracle.collision_rows(wl, b, x[b]) for b in range(3)})
     continuous_fixture()
+    discrete_fixture()
     print("golden fixtures written to", HERE)
 
 
@@ -91,6 +92,16 @@ def continuous_fixture():
     wl = problems.make_workload("C", 3)
     wl.desc.coll_continuous = 1
     np.savez(HERE / "collision_rows_C_cont.npz", x=wl.init,
+             **{f"rows{b}": oracle.collision_rows(wl, b, wl.init[b]) for b in range(3)})
+
+
+def discrete_fixture():
+    """collision_rows_C_single.npz: DISCRETE (single-timestep) rows of 3
+    config C problems at their initial trajectories."""
+    wl = problems.make_workload("C", 3)
+    wl.desc.coll_continuous = 2
+    wl.desc.coll_buffer = 0.1
+    np.savez(HERE / "collision_rows_C_single.npz", x=wl.init,
              **{f"rows{b}": oracle.collision_rows(wl, b, wl.init[b]) for b in range(3)})
 
 

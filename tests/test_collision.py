@@ -167,3 +167,42 @@ def test_continuous_collision_rows_golden(oracle_mod, golden):
     for b in range(3):
         r = oracle_mod.collision_rows(wl, b, g["x"][b])
         np.testing.assert_array_equal(r, g[f"rows{b}"])
+
+
+def test_discrete_collision_rows_golden(oracle_mod, golden):
+    """The oracle's DISCRETE (single-timestep) rows against the committed
+    fixture (tests/golden/make_golden.py: discrete_fixture): one record per
+    contact of each free waypoint, second half zero."""
+    g = golden("collision_rows_C_single")
+    wl = problems.make_workload("C", 3)
+    wl.desc.coll_continuous = 2
+    wl.desc.coll_buffer = 0.1
+    for b in range(3):
+        r = oracle_mod.collision_rows(wl, b, g["x"][b])
+        np.testing.assert_array_equal(r, g[f"rows{b}"])
+        assert not r[:, 8 + wl.n_dof:8 + 2 * wl.n_dof].any()
+        assert 0 not in r[:, 0]  # waypoint 0 is a fixed collision step
+        assert b == 0 or len(r) > 50
+
+
+def test_discrete_rows_match_lvs_substate_zero(oracle_mod):
+    """A DISCRETE contact at waypoint t is the LVS_DISCRETE pair (t, t+1)'s
+    sub-state 0 contact with the (t+1) half absent: same distance, same
+    gradient at q_t (scale 1 - 0)."""
+    wl = problems.make_workload("C", 2)
+    x = wl.init.copy()
+    x[:, 1:] = x[:, :1]  # a stationary trajectory: every pair has cnt = 2
+    wl.desc.coll_buffer = 0.1
+    ws = problems.make_workload("C", 2)
+    ws.desc.coll_continuous = 2
+    ws.desc.coll_buffer = 0.1
+    for b in range(2):
+        rs = oracle_mod.collision_rows(ws, b, x[b])
+        rl = oracle_mod.collision_rows(wl, b, x[b])
+        D = wl.n_dof
+        for t in range(1, wl.n_steps - 1):
+            a = rs[rs[:, 0] == t]
+            l = rl[(rl[:, 0] == t) & (rl[:, 4] == 0)]
+            assert len(a) == len(l)
+            np.testing.assert_array_equal(a[:, [1, 2, 3, 5, 7]], l[:, [1, 2, 3, 5, 7]])
+            np.testing.assert_array_equal(a[:, 8:], l[:, 8:])

@@ -78,8 +78,9 @@ def _doc(**over):
         (_doc(costs=[{"type": "joint_acc", "params": {}}]), "term type 'joint_acc' is not supported on the HIP path"),
         (_doc(constraints=[{"type": "joint_vel", "params": {"targets": [0]}}]),
          "JointVelTermInfo as a constraint (JointVelEqConstraint / JointVelIneqConstraint) is not supported"),
-        (_doc(costs=[{"type": "collision", "params": {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 1}}]),
-         "collision evaluator_type 1 (LVS_DISCRETE = 2, CONTINUOUS = 3, LVS_CONTINUOUS = 4 are) is not supported"),
+        (_doc(costs=[{"type": "collision", "params": {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 0}}]),
+         "collision evaluator_type 0 (DISCRETE = 1, LVS_DISCRETE = 2, CONTINUOUS = 3, LVS_CONTINUOUS = 4 are) "
+         "is not supported"),
         (_doc(costs=[{"type": "collision", "params": {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 2,
                                                       "safety_margin_buffer": 0.05}}]),
          "invalid field found: safety_margin_buffer"),
@@ -115,13 +116,13 @@ def test_init_info_types():
 
 def test_reference_arm_around_table_config():
     """The reference's planning config (evaluator_type 4, LVS_CONTINUOUS)
-    lowers as the reference reads it; evaluator 2 / 3 select LVS_DISCRETE /
-    CONTINUOUS (one cast per step pair)."""
+    lowers as the reference reads it; evaluator 1 / 2 / 3 select DISCRETE
+    (single-timestep terms) / LVS_DISCRETE / CONTINUOUS (one cast per step pair)."""
     text = (GOLDEN / "arm_around_table.json").read_text()
     doc = json.loads(text)
     desc, init, tgt, jpt = host.lower_json(text)
     assert desc.coll_continuous == 1 and desc.coll_lvs == 0.02
-    for ev, cont in ((2, 0), (3, 1)):
+    for ev, cont in ((1, 2), (2, 0), (3, 1)):
         doc["costs"][1]["params"]["evaluator_type"] = ev
         d2, _, _, _ = host.lower_json(json.dumps(doc))
         assert d2.coll_continuous == cont

@@ -255,6 +255,54 @@ def test_sqp_parity_collision_continuous(oracle_mod):
     check_parity(wl, oracle_mod, x, res, tr, label="C-continuous-cnt")
 
 
+def _single(wl):
+    wl.desc.coll_continuous = 2  # DISCRETE: SingleTimestepCollisionEvaluator per free waypoint
+    wl.desc.coll_buffer = 0.1  # (at the waypoints alone the 0.05 buffer finds few contacts)
+    return wl
+
+
+def test_collision_rows_parity_discrete(oracle_mod):
+    """DISCRETE (SingleTimestepCollisionEvaluator, collision_terms.cpp:538-554,
+    600-688): one term per free waypoint, contacts at q_t, gradient scale 1."""
+    wl = _single(problems.make_workload("C", 16))
+    wl.desc.coll_n_fixed = 2
+    wl.desc.coll_fixed_steps[1] = 7  # a fixed interior waypoint has no term
+    xo, _ = oracle_mod.solve(wl, n_threads=16)
+    s = BatchTrustRegionSQP(wl)
+    rows = s.collision_rows(xo)
+    rows_init = s.collision_rows(wl.init)
+    s.close()
+    assert sum(len(r) for r in rows_init) > 40
+    for b in range(wl.batch):
+        for r in (rows[b], rows_init[b]):
+            assert not np.isin(r[:, 0], [0, 7]).any()
+        _check_rows(rows[b], oracle_mod.collision_rows(wl, b, xo[b]), f"problem {b} (solution)")
+        _check_rows(rows_init[b], oracle_mod.collision_rows(wl, b, wl.init[b]), f"problem {b} (init)")
+
+
+def test_sqp_parity_collision_discrete(oracle_mod):
+    wl = _single(problems.make_workload("C", 32, first_problem=400))
+    x, res, tr = solve_gpu(wl, trace=2048)
+    assert all(r.flags == 0 for r in res)
+    assert all(r.n_costs == 1 + 29 + (wl.n_steps - 1) for r in res)
+    check_parity(wl, oracle_mod, x, res, tr, label="C-discrete")
+    wl = _single(problems.make_workload("C", 8, first_problem=500))
+    wl.desc.coll_is_cnt = 1
+    x, res, tr = solve_gpu(wl, trace=2048)
+    assert all(r.n_cnts == wl.n_steps - 1 for r in res)
+    check_parity(wl, oracle_mod, x, res, tr, label="C-discrete-cnt")
+
+
+def test_collision_rows_golden_discrete(golden):
+    g = golden("collision_rows_C_single")
+    wl = _single(problems.make_workload("C", 3))
+    s = BatchTrustRegionSQP(wl)
+    rows = s.collision_rows(g["x"])
+    s.close()
+    for b in range(3):
+        _check_rows(rows[b], g[f"rows{b}"], f"golden discrete problem {b}")
+
+
 def test_collision_rows_golden(golden):
     g = golden("collision_rows_C")
     wl = problems.make_workload("C", 3)
@@ -413,6 +461,23 @@ def _variant(name):
         wl.desc.coll_last_step = 20
         wl.desc.coll_n_fixed = 0
         return wl
+    if name == "discrete_fixed_both_ends_subrange":
+        # DISCRETE with the last waypoint free (its rows share step pair N - 2) and
+        # fixed waypoints inside a sub-range
+        wl = _single(problems.make_workload("C", 8, first_problem=40))
+        wl.desc.coll_first_step = 3
+        wl.desc.coll_last_step = -1
+        wl.desc.coll_n_fixed = 2
+        wl.desc.coll_fixed_steps[0] = 3
+        wl.desc.coll_fixed_steps[1] = 4
+        return wl
+    if name == "discrete_two_waypoints":
+        wl = _single(problems.make_workload("C", 8, n_steps=2, first_problem=60))
+        wl.desc.coll_n_fixed = 0
+        return wl
+    if name == "discrete_with_static_hinges_8dof":
+        wl = _single(_variant("collision_with_static_hinges"))
+        return wl
     if name == "single_problem":
         return problems.make_workload("B", 1, first_problem=5)
     # other chains: 8 DoF with the prismatic torso_lift_joint first, and 6 DoF
@@ -439,7 +504,8 @@ VARIANTS = ["jointvel_only", "short_horizon", "two_fixed_steps", "position_only_
             "jointvel_ineq_cost", "jointpos_ineq_cost_and_cnt", "collision_with_static_hinges", "max_horizon_64",
             "min_horizon_2", "collision_empty_scene", "collision_fixed_both_ends", "collision_step_subrange",
             "torso_arm_8dof_A", "torso_arm_8dof_B", "torso_arm_8dof_C", "torso_arm_8dof_jointpos", "arm_6dof_A",
-            "arm_6dof_C"]
+            "arm_6dof_C", "discrete_fixed_both_ends_subrange", "discrete_two_waypoints",
+            "discrete_with_static_hinges_8dof"]
 
 
 @pytest.mark.parametrize("name", VARIANTS)

@@ -139,7 +139,10 @@ struct Layout
   int m_base;     // n_rows + nc_base
   int h_cap;      // hinge-row capacity (0 without collision)
   int coll;       // collision cost enabled
-  int coll_first, coll_last;  // step pairs [coll_first, coll_last)
+  int coll_first, coll_last;  // collision units [coll_first, coll_last): step pairs, or
+                              // waypoints with coll_single
+  int coll_single; // DISCRETE (SingleTimestepCollisionEvaluator): one unit per waypoint, its
+                   // rows filed in step pair min(t, N - 2) on half t - pair
   int coll_cost0; // cost slot (or, with coll_cnt, constraint slot) of the first step pair
   int coll_cnt;   // collision term is a constraint (CollisionConstraint, ineq rows inflated by mu)
   int n_costs;    // JointVel (0/1) + CartPose cost terms + JointPos cost terms + collision step pairs
@@ -209,6 +212,8 @@ struct Tables
   int* grp_ns;     // spheres in the group
   int* sph_order;  // sphere indices sorted by (link, index)
   int* coll_fixed; // per waypoint: 1 if a collision fixed step (N)
+  int* coll_slot;  // per collision unit (step pair, or waypoint for DISCRETE): term slot
+                   // relative to coll_cost0, -1 for a fixed waypoint without a term (N)
 };
 
 struct KernelArgs

@@ -345,6 +345,36 @@ __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
 // ======================================================================
 __device__ __forceinline__ bool coll_fixed_step(const Ctx& c, int t) { return c.T.coll_fixed[t] != 0; }
 
+// Collision units: step pairs (LVS_DISCRETE / LVS_CONTINUOUS), or waypoints
+// (DISCRETE, SingleTimestepCollisionEvaluator).  A waypoint unit t files its
+// rows in step pair min(t, N - 2), on that pair's half t - pair; the last
+// waypoint's rows follow waypoint N - 2's in pair N - 2.
+__device__ __forceinline__ int coll_pair_of(const Layout& L, int t) { return L.coll_single ? min(t, L.N - 2) : t; }
+
+// contact rows filed in step pair p
+__device__ __forceinline__ int coll_pair_count(const Layout& L, const int* PCNT, int p)
+{
+  if (!L.coll)
+    return 0;
+  const bool in = p >= L.coll_first && p < L.coll_last;
+  if (!L.coll_single)
+    return in ? PCNT[p] : 0;
+  int n = (in && p <= L.N - 2) ? PCNT[p] : 0;
+  if (p == L.N - 2 && L.N - 1 >= L.coll_first && L.N - 1 < L.coll_last)
+    n += PCNT[L.N - 1];
+  return n;
+}
+
+// first hinge row of unit t (HP: per step pair)
+__device__ __forceinline__ int coll_unit_row0(const Layout& L, const int* PCNT, const int* HP, int t)
+{
+  const int p = coll_pair_of(L, t);
+  int r = HP[p];
+  if (L.coll_single && t > p && p >= L.coll_first)
+    r += PCNT[p];
+  return r;
+}
+
 // Contact-scan tables and this problem's scene, staged in static LDS once per
 // scan (the candidate decode read them from global memory, a chain of
 // dependent loads per ballot round).
@@ -396,9 +426,21 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
   int* HT = c.ia(I_HT);
   for (int t = L.coll_first + c.wave; t < L.coll_last; t += kWaves)
   {
+    const bool single = L.coll_single != 0;
+    if (single && coll_fixed_step(c, t))
+    {
+      // no term at a fixed waypoint
+      if (PASS == 0 && c.lane == 0)
+      {
+        PCNT[t] = 0;
+        HCOST[t] = 0.0;
+      }
+      continue;
+    }
     const double* q0 = x + t * D;
-    const double* q1 = x + (t + 1) * D;
-    const int cnt = lvs_count(q0, q1, D, c.d->coll_lvs);
+    // DISCRETE: one state, q_t (linspaced(1, .., high) = high)
+    const double* q1 = single ? q0 : x + (t + 1) * D;
+    const int cnt = single ? 1 : lvs_count(q0, q1, D, c.d->coll_lvs);
     if (cnt > kSubCap)
     {
       if (c.lane == 0)
@@ -412,10 +454,10 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       }
       continue;
     }
-    const bool f0 = coll_fixed_step(c, t), f1 = coll_fixed_step(c, t + 1);
+    const bool f0 = !single && coll_fixed_step(c, t), f1 = !single && coll_fixed_step(c, t + 1);
     const int ngr = c.T.n_groups;
     // LVS_CONTINUOUS: candidates are the casts between consecutive sub-states
-    const bool cont = c.d->coll_continuous != 0;
+    const bool cont = c.d->coll_continuous == 1;
     const int nseg = cont ? cnt - 1 : cnt;
     const int last = cnt - 1;
     long long* pf22 = (c.tid == 0) ? c.s->prof : nullptr;
@@ -554,7 +596,8 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       total += P * nseg * S.grp_ns[g];
     int running = 0;
     double lcost = 0.0;  // per-lane partial cost, reduced once per pair
-    const int base = (PASS == 1) ? out_base[t] : 0;
+    const int base = (PASS == 1) ? coll_unit_row0(L, PCNT, out_base, t) : 0;
+    const int pair = coll_pair_of(L, t);
     for (int c0 = 0; c0 < total; c0 += 64)
     {
       const int cand = c0 + c.lane;
@@ -619,10 +662,10 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
         const int k = base + running + rank;
         if (k < L.h_cap)
         {
-          CONT[3 * k + 0] = i;
+          CONT[3 * k + 0] = single ? t - pair : i;  // DISCRETE: the half of the pair
           CONT[3 * k + 1] = s;
           CONT[3 * k + 2] = p;
-          HT[k] = t;
+          HT[k] = pair;
           c.ia(I_HKIND)[k] = 0;
         }
       }
@@ -649,14 +692,13 @@ __device__ void static_hinge_rows(Ctx& c, const int* HP)
 {
   const Layout& L = c.L;
   const int D = L.D;
-  const int* PCNT = c.ia(I_PCNT);
   int *HT = c.ia(I_HT), *HM = c.ia(I_HMASK), *HKD = c.ia(I_HKIND), *HSL = c.ia(I_HSLOT);
   double *HC0 = c.a(A_HC0), *HK = c.a(A_HK);
   FOR(sr, c.T.n_sh)
   {
     const int p = c.T.sh_pair[sr];
-    const int ncoll = (L.coll && p >= L.coll_first && p < L.coll_last) ? PCNT[p] : 0;
-    const int h = HP[p] + ncoll + (sr - c.T.sh_ptr[p]);
+    // the pair's static rows close its range [HP[p], HP[p + 1])
+    const int h = HP[p + 1] - c.T.sh_ptr[p + 1] + sr;
     const int kind = c.T.sh_kind[sr], k = c.T.sh_owner[sr], j = c.T.sh_joint[sr], t = c.T.sh_step[sr];
     double* a = HC0 + h * 2 * D;
     for (int e = 0; e < 2 * D; ++e)
@@ -764,7 +806,6 @@ __device__ void sh_model_values(Ctx& c, const double* SX, double* mcost, double*
   if (c.T.n_sh == 0)
     return;
   const int* HP = c.ia(I_HPTR);
-  const int* PCNT = c.ia(I_PCNT);
   const int* HMv = c.ia(I_HMASK);
   const double *HC0 = c.a(A_HC0), *HKv = c.a(A_HK);
   for (int o = 0; o <= L.n_jpos; ++o)
@@ -779,8 +820,9 @@ __device__ void sh_model_values(Ctx& c, const double* SX, double* mcost, double*
       if (c.T.sh_owner[sr] != o)
         continue;
       const int p = c.T.sh_pair[sr];
-      const int ncoll = (L.coll && p >= L.coll_first && p < L.coll_last) ? PCNT[p] : 0;
-      const int h = HP[p] + ncoll + (sr - c.T.sh_ptr[p]);
+      // (from HP alone: after a rejected step PCNT holds the counts at the
+      // candidate point, not at the point these rows were built from)
+      const int h = HP[p + 1] - c.T.sh_ptr[p + 1] + sr;
       if (!cnt)
         v += SX[L.nc_base + h];
       else
@@ -821,7 +863,12 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
       BSYNC();
     }
     if (costs)
-      FOR(k, L.coll_last - L.coll_first) costs[L.coll_cost0 + k] = c.a(A_HCOST)[L.coll_first + k];
+      FOR(k, L.coll_last - L.coll_first)
+      {
+        const int slot = c.T.coll_slot[L.coll_first + k];
+        if (slot >= 0)
+          costs[L.coll_cost0 + slot] = c.a(A_HCOST)[L.coll_first + k];
+      }
     if (c.tid == 0 && c.s->coll_overflow)
       c.s->flags |= THIP_FLAG_CONTACT_OVERFLOW;
   }
@@ -838,8 +885,8 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
     for (int t = 0; t <= L.N; ++t)
     {
       HP[t] = acc;
-      if (L.coll && t >= L.coll_first && t < L.coll_last)
-        acc += PCNT[t];
+      if (t < L.N)
+        acc += coll_pair_count(L, PCNT, t);
       if (t < L.N)
         acc += c.T.sh_ptr[t + 1] - c.T.sh_ptr[t];
     }
@@ -888,12 +935,13 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
     const int t = HT[k], i = CONT[3 * k + 0], s = CONT[3 * k + 1], p = CONT[3 * k + 2];
     const double* q0 = x + t * D;
     const double* q1 = x + (t + 1) * D;
-    const int cnt = lvs_count(q0, q1, D, c.d->coll_lvs);
+    const bool single = L.coll_single != 0;  // i = the half (waypoint t + i)
+    const int cnt = single ? 1 : lvs_count(q0, q1, D, c.d->coll_lvs);
     const int link = c.d->sphere_link[s];
-    const bool cont = c.d->coll_continuous != 0;
+    const bool cont = c.d->coll_continuous == 1;
     double q[THIP_MAX_DOF];
     for (int j = 0; j < D; ++j)
-      q[j] = linspaced(cnt, q0[j], q1[j], i);
+      q[j] = single ? (i ? q1[j] : q0[j]) : linspaced(cnt, q0[j], q1[j], i);
     Pose T, T1;  // link pose at sub-state i (transform) and, for a cast, at i + 1 (cc_transform)
     chain_fk(ch, q, link, T);
     const double* cs = c.d->sphere_center[s];
@@ -929,8 +977,11 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
       rv0[r] = T.r[r * 3 + 0] * pl[0] + T.r[r * 3 + 1] * pl[1] + T.r[r * 3 + 2] * pl[2];
       rv1[r] = T1.r[r * 3 + 0] * pl[0] + T1.r[r * 3 + 1] * pl[1] + T1.r[r * 3 + 2] * pl[2];
     }
-    const double cc_time = (cont ? (double(i) + ts) : double(i)) * (1.0 / double(cnt - 1));
-    const bool f0 = coll_fixed_step(c, t), f1 = coll_fixed_step(c, t + 1);
+    // DISCRETE: CCType_None, GetGradient's scale 1 (collision_terms.cpp:214-221): the
+    // waypoint's half with scale 1 - 0 (half 0) or 1 (half 1), the other half absent
+    const double cc_time =
+        single ? double(i) : (cont ? (double(i) + ts) : double(i)) * (1.0 / double(cnt - 1));
+    const bool f0 = single ? (i == 1) : coll_fixed_step(c, t), f1 = single ? (i == 0) : coll_fixed_step(c, t + 1);
     double cst = dist;
     int mask = 0;
     double* a = HC0 + k * 2 * D;
@@ -968,7 +1019,7 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
     HK[k] = cst;
     HM[k] = mask;
     c.a(A_HDIST)[k] = dist;
-    c.a(A_HCCT)[k] = cc_time;
+    c.a(A_HCCT)[k] = single ? 0.0 : cc_time;
   }
   BSYNC();
 }
@@ -1207,7 +1258,8 @@ __device__ void build_and_scale(Ctx& c)
       if (HKDq[h])
         Q[col] = HSLq[h] >= 0 ? MU[HSLq[h]] : 1.0;
       else
-        Q[col] = L.coll_cnt ? MU[L.coll_cost0 + HTq[h] - L.coll_first] : c.d->coll_coeff;
+        Q[col] = L.coll_cnt ? MU[L.coll_cost0 + c.T.coll_slot[HTq[h] + (L.coll_single ? c.ia(I_CONT)[3 * h] : 0)]]
+                            : c.d->coll_coeff;
       DS[col] = 1.0;
       BS[col] = 1.0;
     }
@@ -3651,9 +3703,19 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
         {
           // ConvexObjective::value of each step-pair term: sum coeff * h
           const int* HP = c.ia(I_HPTR);
+          const int* HTv = c.ia(I_HT);
+          const int* CONTv = c.ia(I_CONT);
           FOR(k, L.coll_last - L.coll_first)
           {
-            const int t = L.coll_first + k;
+            const int u = L.coll_first + k, slot = c.T.coll_slot[u];
+            if (slot < 0)
+              continue;
+            // rows of unit u: the contact rows of step pair t (DISCRETE: those on u's half).
+            // From HP and the rows alone: after a rejected step PCNT holds the counts at
+            // the candidate point, not at the point these rows were built from.
+            const int t = coll_pair_of(L, u);
+            const int h0 = HP[t], h1 = HP[t + 1];
+            auto other = [&](int h) { return L.coll_single && HTv[h] + CONTv[3 * h] != u; };
             double v = 0;
             if (L.coll_cnt)
             {
@@ -3662,9 +3724,9 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
               const int* HMv = c.ia(I_HMASK);
               const int* HKD = c.ia(I_HKIND);
               const double cf = c.d->coll_coeff;
-              for (int h = HP[t]; h < HP[t + 1]; ++h)
+              for (int h = h0; h < h1; ++h)
               {
-                if (HKD[h])
+                if (HKD[h] || other(h))
                   continue;
                 double a = (c.d->coll_margin - HKv[h]) * cf;
                 for (int e = 0; e < 2 * D; ++e)
@@ -3672,15 +3734,15 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
                     a += ((-HC0[h * 2 * D + e]) * cf) * SX[(t + e / D) * D + e % D];
                 v += fmax(a, 0.0);
               }
-              mviol[L.coll_cost0 + k] = v;
+              mviol[L.coll_cost0 + slot] = v;
             }
             else
             {
               const int* HKD = c.ia(I_HKIND);
-              for (int h = HP[t]; h < HP[t + 1]; ++h)
-                if (!HKD[h])
+              for (int h = h0; h < h1; ++h)
+                if (!HKD[h] && !other(h))
                   v += c.d->coll_coeff * SX[L.nc_base + h];
-              mcost[L.coll_cost0 + k] = v;
+              mcost[L.coll_cost0 + slot] = v;
             }
           }
         }
@@ -3992,17 +4054,18 @@ __global__ __launch_bounds__(kBlock) void coll_rows_kernel(KernelArgs args, cons
       continue;
     const int cnt = lvs_count(XN + t * D, XN + (t + 1) * D, D, args.desc->coll_lvs);
     double* r = ob + (long long)o * W;
-    r[0] = t;
+    const bool single = L.coll_single != 0;  // DISCRETE: i is the half; record = waypoint t + i
+    r[0] = single ? t + i : t;
     r[1] = args.desc->sphere_link[CONT[3 * k + 1]];
     r[2] = CONT[3 * k + 2];
     r[3] = CONT[3 * k + 1];
-    r[4] = i;
+    r[4] = single ? 0 : i;
     r[5] = HD[k];
     r[6] = c.a(A_HCCT)[k];
     (void)cnt;
     r[7] = __popc(HM[k]);
     for (int j = 0; j < 2 * D; ++j)
-      r[8 + j] = HC0[k * 2 * D + j];
+      r[8 + j] = single ? (j < D ? HC0[k * 2 * D + i * D + j] : 0.0) : HC0[k * 2 * D + j];
     r[8 + 2 * D] = HK[k];
   }
   if (threadIdx.x == 0)

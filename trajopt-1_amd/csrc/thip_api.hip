@@ -177,11 +177,17 @@ static int validate(const thip_problem_desc* d, std::string& why)
     if (d->coll_first_step < 0 || d->coll_first_step >= d->n_steps || last < d->coll_first_step ||
         last >= d->n_steps)
       return why = "collision: bad first/last step", THIP_E_INVALID;
-    if (d->coll_continuous != 0 && d->coll_continuous != 1)
-      return why = "collision: coll_continuous must be 0 (LVS_DISCRETE) or 1 (LVS_CONTINUOUS)", THIP_E_INVALID;
-    if (!(d->coll_lvs > 0) || !(d->coll_buffer >= 0))
+    if (d->coll_continuous < 0 || d->coll_continuous > 2)
+      return why = "collision: coll_continuous must be 0 (LVS_DISCRETE), 1 (LVS_CONTINUOUS) or 2 (DISCRETE)",
+             THIP_E_INVALID;
+    const bool single = d->coll_continuous == 2;
+    if (single && d->n_steps < 2)
+      return why = "collision: DISCRETE needs at least 2 waypoints", THIP_E_INVALID;
+    if ((!single && !(d->coll_lvs > 0)) || !(d->coll_buffer >= 0))
       return why = "collision: bad longest_valid_segment_length / buffer", THIP_E_INVALID;
-    for (int t = d->coll_first_step; t < last; ++t)
+    // (single-timestep terms skip fixed waypoints; only the step-pair evaluators reject
+    // adjacent fixed steps, problem_description.cpp:1765-1767 vs :1785-1795)
+    for (int t = d->coll_first_step; !single && t < last; ++t)
     {
       bool a = false, b = false;
       for (int k = 0; k < d->coll_n_fixed; ++k)
@@ -387,16 +393,31 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   L.coll = d.coll_enabled ? 1 : 0;
   L.coll_first = d.coll_first_step;
   L.coll_last = (d.coll_last_step < 0) ? L.N - 1 : d.coll_last_step;
+  // DISCRETE: one SingleTimestepCollisionEvaluator term per waypoint of [first, last] that is
+  // not a fixed step (problem_description.cpp:1782-1796)
+  L.coll_single = (L.coll && d.coll_continuous == 2) ? 1 : 0;
+  if (L.coll_single)
+    L.coll_last += 1;
+  std::vector<int> coll_slot(static_cast<size_t>(L.N), -1);
+  int n_units = 0;
+  for (int t = L.coll_first; L.coll && t < L.coll_last; ++t)
+  {
+    bool fx = false;
+    for (int k = 0; k < d.coll_n_fixed; ++k)
+      fx |= d.coll_fixed_steps[k] == t;
+    if (!(L.coll_single && fx))
+      coll_slot[static_cast<size_t>(t)] = n_units++;
+  }
   // (constraint form: one ineq constraint term per step pair after the other
   // constraints, problem_description.cpp:1797-1840 / OptProb eq-then-ineq order)
   L.coll_cnt = (L.coll && d.coll_is_cnt) ? 1 : 0;
   L.coll_cost0 = L.coll_cnt ? n_cnts : n_costs;
   if (L.coll)
-    (L.coll_cnt ? n_cnts : n_costs) += L.coll_last - L.coll_first;
+    (L.coll_cnt ? n_cnts : n_costs) += n_units;
   if (L.coll)
   {
-    // every (sphere, primitive, sub-state) candidate of every step pair is at most one contact
-    const long long bound = static_cast<long long>(L.coll_last - L.coll_first) * 64 * d.n_spheres *
+    // every (sphere, primitive, sub-state) candidate of every unit is at most one contact
+    const long long bound = static_cast<long long>(n_units) * (L.coll_single ? 1 : 64) * d.n_spheres *
                             std::max(d.n_prims, 1);
     // automatic: the bound, within THIP_MAX_CONTACTS and a 16 GB share of HBM for the
     // hinge-row arrays of the whole batch (~800 B per row and problem), at least 2048
@@ -610,7 +631,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   }
   const size_t o_gl = push(grp_link, grp_link.size()), o_g0 = push(grp_s0, grp_s0.size()),
                o_gn = push(grp_ns, grp_ns.size()), o_so = push(sph_order, sph_order.size()),
-               o_cf = push(coll_fixed, coll_fixed.size());
+               o_cf = push(coll_fixed, coll_fixed.size()), o_cs = push(coll_slot, coll_slot.size());
   row_w.resize(std::max<size_t>(na, 1));
   if ((e = hipMalloc(&ctx->d_tables, itab.size() * sizeof(int))) != hipSuccess ||
       (e = hipMalloc(&ctx->d_tables_f, row_w.size() * sizeof(double))) != hipSuccess ||
@@ -651,6 +672,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   T.grp_ns = ctx->d_tables + o_gn;
   T.sph_order = ctx->d_tables + o_so;
   T.coll_fixed = ctx->d_tables + o_cf;
+  T.coll_slot = ctx->d_tables + o_cs;
   T.row_w = ctx->d_tables_f;
   const size_t B = static_cast<size_t>(batch);
   if ((e = hipMalloc(&ctx->d_ws, B * static_cast<size_t>(L.dstride) * sizeof(double))) != hipSuccess ||

@@ -662,13 +662,14 @@ void CollisionTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value
   ensure_only_members(params, all_fields, sizeof(all_fields) / sizeof(char*));
 }
 
-// problem_description.cpp:1735-1858, LVS_DISCRETE branch
+// problem_description.cpp:1735-1858: DISCRETE (single-timestep terms on the free waypoints),
+// LVS_DISCRETE, CONTINUOUS and LVS_CONTINUOUS (step-pair terms)
 void CollisionTermInfo::hatch(TrajOptProb& prob)
 {
   // tesseract CollisionEvaluatorType {NONE, DISCRETE, LVS_DISCRETE, CONTINUOUS, LVS_CONTINUOUS}
-  if (evaluator_type < 2 || evaluator_type > 4)
+  if (evaluator_type < 1 || evaluator_type > 4)
     unsupported("collision evaluator_type " + std::to_string(evaluator_type) +
-                " (LVS_DISCRETE = 2, CONTINUOUS = 3, LVS_CONTINUOUS = 4 are)");
+                " (DISCRETE = 1, LVS_DISCRETE = 2, CONTINUOUS = 3, LVS_CONTINUOUS = 4 are)");
   if (contact_test_type != 2)
     unsupported("collision contact_test_type " + std::to_string(contact_test_type) + " (only ALL = 2)");
   if (has_pairs)
@@ -678,7 +679,7 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
   if (d.coll_enabled)
     unsupported("more than one collision term");
   const int n_steps = prob.GetNumSteps();
-  for (int i = first_step; i < last_step; ++i)
+  for (int i = first_step; evaluator_type != 1 && i < last_step; ++i)
   {
     const bool a = std::find(fixed_steps.begin(), fixed_steps.end(), i) != fixed_steps.end();
     const bool b = std::find(fixed_steps.begin(), fixed_steps.end(), i + 1) != fixed_steps.end();
@@ -702,7 +703,8 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
   d.coll_coeff = coeff;
   d.coll_buffer = collision_margin_buffer;
   // CONTINUOUS casts each step pair once (lvs = max(), problem_description.cpp:1742-1744)
-  d.coll_continuous = (evaluator_type >= 3) ? 1 : 0;
+  // DISCRETE: SingleTimestepCollisionEvaluator per free waypoint (:1782-1796, :1842-1856)
+  d.coll_continuous = (evaluator_type == 1) ? 2 : (evaluator_type >= 3) ? 1 : 0;
   d.coll_lvs = (evaluator_type == 3) ? 1.7976931348623157e308 : longest_valid_segment_length;
   d.n_spheres = static_cast<int>(env->collision_spheres.size());
   for (int s = 0; s < d.n_spheres; ++s)
