@@ -289,8 +289,13 @@ int thip_upload_device(thip_ctx* ctx, const double* d_init_traj, const double* d
                        const double* d_scene);
 
 /* Run BasicTrustRegionSQP::optimize for every problem (asynchronous on the
- * ctx stream). */
+ * ctx stream).  Several contexts on their own streams keep several batches in
+ * flight: the next batch fills the CUs the current batch's longest problems
+ * leave idle. */
 int thip_sqp_run(thip_ctx* ctx);
+
+/* Wait for the ctx stream (every run queued on it has finished). */
+int thip_synchronize(thip_ctx* ctx);
 
 /* Convexify at trajectory x [batch][n_steps][n_dof] (host pointer): CartPose
  * error rows and forward-difference Jacobians, exactly as the SQP loop does.

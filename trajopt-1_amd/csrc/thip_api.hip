@@ -840,6 +840,15 @@ int thip_sqp_run(thip_ctx* ctx)
   return THIP_OK;
 }
 
+int thip_synchronize(thip_ctx* ctx)
+{
+  if (!ctx)
+    return THIP_E_INVALID;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
 double thip_last_kernel_ms(thip_ctx* ctx)
 {
   if (!ctx || !ctx->ran)

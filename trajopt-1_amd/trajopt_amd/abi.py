@@ -226,6 +226,8 @@ def _declare(lib):
     lib.thip_upload_device.restype = C.c_int
     lib.thip_sqp_run.argtypes = [vp]
     lib.thip_sqp_run.restype = C.c_int
+    lib.thip_synchronize.argtypes = [vp]
+    lib.thip_synchronize.restype = C.c_int
     lib.thip_linearize.argtypes = [vp, dp, dp, dp]
     lib.thip_linearize.restype = C.c_int
     lib.thip_fwd_kin.argtypes = [vp, dp, dp]

@@ -60,6 +60,9 @@ class BatchTrustRegionSQP:
             self.upload()
         self._check(self.lib.thip_sqp_run(self.ctx), "thip_sqp_run")
 
+    def sync(self):
+        self._check(self.lib.thip_synchronize(self.ctx), "thip_synchronize")
+
     def kernel_ms(self) -> float:
         return float(self.lib.thip_last_kernel_ms(self.ctx))
 
