@@ -182,6 +182,14 @@ typedef struct thip_problem_desc {
   double cart_source_offset[THIP_MAX_CART][12];
   double cart_pos_coeffs[THIP_MAX_CART][3];
   double cart_rot_coeffs[THIP_MAX_CART][3];
+  /* CartPose tolerance band (CartPoseErrCalculator / CartPoseJacCalculator,
+   * kinematic_terms.cpp:189-370): with cart_has_tol the error is
+   * applyTolerances(calcTransformError, lower, upper) over the 6 components
+   * (x, y, z, rx, ry, rz) and the finite-difference Jacobian uses the
+   * tolerance-aware error difference.  0 = no band (empty or equal bounds). */
+  int cart_has_tol[THIP_MAX_CART];
+  double cart_lower_tol[THIP_MAX_CART][6];
+  double cart_upper_tol[THIP_MAX_CART][6];
 
   /* JointPosTermInfo (problem_description.cpp:1097-1196).  Zero tolerances:
    * is_cnt 0 -> JointPosEqCost (quadratic, trajectory_costs.cpp:28-65),

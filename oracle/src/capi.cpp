@@ -119,6 +119,7 @@ int oracle_linearize(const thip_problem_desc* d, int batch, const double* x, con
       c.target_offset = Iso3::from12(targets + (static_cast<std::size_t>(b) * d->n_cart + k) * 12);
       DblVec coeffs;
       cartPoseIndices(*d, k, c.indices, coeffs);
+      setCartPoseTolerances(*d, k, c);
       const int t = d->cart_step[k];
       DblVec q(x + (static_cast<std::size_t>(b) * N + t) * D, x + (static_cast<std::size_t>(b) * N + t + 1) * D);
       const DblVec e = c(q);

@@ -163,6 +163,41 @@ void calcJacobianTransformErrorDiff(const Iso3& target, const Iso3& source, cons
     err[3 + i] = r1[i] - r0[i];
 }
 
+// The tolerance-aware error difference of tesseract's 5-argument
+// calcJacobianTransformErrorDiff [ext, unpinned; called at kinematic_terms.cpp:319-339]:
+// both errors [t; rotvec] with the rotation vector in [-pi, pi] (calcTransformError),
+// switched to the continuous [0, 2 pi) form (calcRotationalError2) for both when the
+// perturbation crosses the wrap (a component jumps by more than pi), then
+// applyTolerances on both; returns perturbed - unperturbed.  Pinned by
+// kinematic_costs_unit.cpp:79-254 (zero rows inside the band, FD consistency).
+void calcJacobianTransformErrorDiffTol(const Iso3& target, const Iso3& source, const Iso3& source_pert,
+                                       const double* lower, const double* upper, double err[6])
+{
+  const Iso3 ti = inverse(target);
+  const Iso3 pe = mul(ti, source);
+  const Iso3 ppe = mul(ti, source_pert);
+  double e0[6], e1[6];
+  for (int i = 0; i < 3; ++i)
+  {
+    e0[i] = pe.t[i];
+    e1[i] = ppe.t[i];
+  }
+  calcRotationalError(pe.R, e0 + 3);
+  calcRotationalError(ppe.R, e1 + 3);
+  bool wrap = false;
+  for (int i = 3; i < 6; ++i)
+    wrap = wrap || std::fabs(e1[i] - e0[i]) > M_PI;
+  if (wrap)
+  {
+    calcRotationalError2(pe.R, e0 + 3);
+    calcRotationalError2(ppe.R, e1 + 3);
+  }
+  applyTolerances(e0, lower, upper, 6);
+  applyTolerances(e1, lower, upper, 6);
+  for (int i = 0; i < 6; ++i)
+    err[i] = e1[i] - e0[i];
+}
+
 void applyTolerances(double err[6], const double* lower, const double* upper, int n)
 {
   for (int i = 0; i < n; ++i)

@@ -63,6 +63,8 @@ void calcRotationalError2(const double R[9], double out[3]);  // angle in [0, 2p
 void calcTransformError(const Iso3& t1, const Iso3& t2, double err[6]);
 void calcJacobianTransformErrorDiff(const Iso3& target, const Iso3& source, const Iso3& source_pert, double err[6]);
 void applyTolerances(double err[6], const double* lower, const double* upper, int n);
+void calcJacobianTransformErrorDiffTol(const Iso3& target, const Iso3& source, const Iso3& source_pert,
+                                       const double* lower, const double* upper, double err[6]);
 
 // link poses of the chain at q: out[n_links]
 void chainFwdKin(const thip_chain& chain, const double* q, std::vector<Iso3>& out);

@@ -433,6 +433,18 @@ void cartPoseIndices(const thip_problem_desc& d, int term, std::vector<int>& ind
     }
 }
 
+void setCartPoseTolerances(const thip_problem_desc& d, int term, CartPoseCalc& c)
+{
+  c.has_tol = d.cart_has_tol[term] != 0;
+  for (int i = 0; i < 6; ++i)
+  {
+    c.lower_tol[i] = d.cart_lower_tol[term][i];
+    c.upper_tol[i] = d.cart_upper_tol[term][i];
+    if (c.has_tol && c.lower_tol[i] > c.upper_tol[i])
+      throw std::runtime_error("CartPoseErrCalculator: Inverted tolerance band");
+  }
+}
+
 DblVec CartPoseCalc::operator()(const DblVec& q) const
 {
   std::vector<Iso3> fk;
@@ -441,6 +453,8 @@ DblVec CartPoseCalc::operator()(const DblVec& q) const
   const Iso3 target_tf = mul(fk[0], target_offset);
   double err[6];
   calcTransformError(target_tf, source_tf, err);
+  if (has_tol)
+    applyTolerances(err, lower_tol, upper_tol, 6);
   DblVec out(indices.size());
   for (std::size_t i = 0; i < indices.size(); ++i)
     out[i] = err[indices[i]];
@@ -462,7 +476,10 @@ Mat CartPoseCalc::jac(const DblVec& q) const
     chainFwdKin(*chain, qp.data(), fk);
     const Iso3 sp = mul(fk[static_cast<std::size_t>(source_link)], source_offset);
     double diff[6];
-    calcJacobianTransformErrorDiff(target_tf, source_tf, sp, diff);
+    if (has_tol)
+      calcJacobianTransformErrorDiffTol(target_tf, source_tf, sp, lower_tol, upper_tol, diff);
+    else
+      calcJacobianTransformErrorDiff(target_tf, source_tf, sp, diff);
     for (std::size_t r = 0; r < indices.size(); ++r)
       J(static_cast<int>(r), static_cast<int>(i)) = diff[indices[r]] / eps;
     qp[i] = q[i];
@@ -542,6 +559,7 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
     calc->target_offset = Iso3::from12(cart_targets + 12 * k);
     DblVec coeffs;
     cartPoseIndices(d, k, calc->indices, coeffs);
+    setCartPoseTolerances(d, k, *calc);
     return std::make_pair(calc, coeffs);
   };
   for (int k = 0; k < d.n_cart; ++k)

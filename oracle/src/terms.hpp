@@ -39,10 +39,13 @@ struct CartPoseCalc
   Iso3 source_offset;
   Iso3 target_offset;  // target frame = chain root (static)
   std::vector<int> indices;
+  bool has_tol = false;  // tolerance band (kinematic_terms.cpp:209-247, 319-339)
+  double lower_tol[6] = {}, upper_tol[6] = {};
   DblVec operator()(const DblVec& q) const;  // error
   Mat jac(const DblVec& q) const;            // forward-difference jacobian, eps = 1e-5
 };
 void cartPoseIndices(const thip_problem_desc& d, int term, std::vector<int>& indices, DblVec& coeffs);
+void setCartPoseTolerances(const thip_problem_desc& d, int term, CartPoseCalc& c);
 
 // Build the TrajOptProb of problem b of a batch (ConstructProblem restated).
 // jpos_targets [n_jpos][D] (null: the descriptor's targets)

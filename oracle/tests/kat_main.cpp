@@ -387,6 +387,61 @@ static void kat_kinematics()
     den += sqr(Jn.a[i]);
   }
   CHECK(std::sqrt(num) <= 1e-5 * std::sqrt(den), "CartPose jacobian isApprox(numerical, 1e-5)");
+
+  // Toleranced CartPose (kinematic_costs_unit.cpp:79-254): the pose error at the seed is a
+  // rotation of rx0 about x, band [-0.52, 0.52] on rx and [0, 0] elsewhere.  The reference
+  // tests put the active link in the target frame; here it is the source frame, which gives
+  // the same error (err = static^-1 * active).
+  const double axx[3] = { 1, 0, 0 };
+  auto tol_calc = [&](double rx0) {
+    CartPoseCalc t;
+    t.chain = &chain;
+    t.source_link = 7;
+    t.source_offset = axisAngle(axx, rx0);
+    t.target_offset = fk[7];
+    t.indices = { 0, 1, 2, 3, 4, 5 };
+    t.has_tol = true;
+    for (int i = 0; i < 6; ++i)
+      t.lower_tol[i] = t.upper_tol[i] = 0.0;
+    t.lower_tol[3] = -0.52;
+    t.upper_tol[3] = 0.52;
+    return t;
+  };
+  auto fd_consistent = [&](const CartPoseCalc& t) {
+    const Mat A = t.jac(q);
+    const Mat Nm = calcForwardNumJac([&](const DblVec& qq) { return t(qq); }, q, 1e-5);
+    double nu = 0, de = 0;
+    for (std::size_t i = 0; i < A.a.size(); ++i)
+    {
+      nu += sqr(A.a[i] - Nm.a[i]);
+      de += sqr(Nm.a[i]);
+    }
+    return std::sqrt(nu) <= 1e-5 * std::sqrt(de) || (de == 0 && nu == 0);
+  };
+  {
+    // inside the band (0.1 rad): f = 0 at the seed, the rx row of J is zero, FD-consistent
+    const CartPoseCalc t = tol_calc(0.1);
+    const DblVec e = t(q);
+    double emax = 0;
+    for (double v : e)
+      emax = std::fmax(emax, std::fabs(v));
+    CHECK(emax <= 1e-9, "toleranced error inside the band is zero at the seed");
+    const Mat A = t.jac(q);
+    double rmax = 0;
+    for (int j = 0; j < 7; ++j)
+      rmax = std::fmax(rmax, std::fabs(A(3, j)));
+    CHECK(rmax <= 1e-6, "rx row of the toleranced jacobian is zero inside the band");
+    CHECK(fd_consistent(t), "toleranced jacobian isApprox(numerical, 1e-5) inside the band");
+  }
+  {
+    // outside the band (0.8 rad): f = (true_err - upper) on rx, FD-consistent
+    const CartPoseCalc t = tol_calc(0.8);
+    const DblVec e = t(q);
+    NEAR(e[3], 0.8 - 0.52, 1e-9, "toleranced error outside the band = true_err - upper");
+    CHECK(fd_consistent(t), "toleranced jacobian isApprox(numerical, 1e-5) outside the band");
+    const CartPoseCalc tn = tol_calc(-0.8);
+    NEAR(tn(q)[3], -0.8 + 0.52, 1e-9, "below the band: true_err - lower");
+  }
 }
 
 int main()

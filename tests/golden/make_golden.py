@@ -83,6 +83,7 @@ def main():
              **{f"rows{b}": oracle.collision_rows(wl, b, x[b]) for b in range(3)})
     continuous_fixture()
     discrete_fixture()
+    tolerance_fixture()
     print("golden fixtures written to", HERE)
 
 
@@ -93,6 +94,14 @@ def continuous_fixture():
     wl.desc.coll_continuous = 1
     np.savez(HERE / "collision_rows_C_cont.npz", x=wl.init,
              **{f"rows{b}": oracle.collision_rows(wl, b, wl.init[b]) for b in range(3)})
+
+
+def tolerance_fixture():
+    """cartpose_B_tol.npz: toleranced CartPose rows (+-0.02 m, +-0.1 rad bands) of 2
+    config B problems at their initial trajectories."""
+    wl = problems.with_cart_tolerances(problems.make_workload("B", 2))
+    err, jac = oracle.linearize(wl, wl.init)
+    np.savez(HERE / "cartpose_B_tol.npz", x=wl.init, targets=wl.targets, err=err, jac=jac)
 
 
 def discrete_fixture():

@@ -30,7 +30,7 @@ import numpy as np
 import pytest
 
 from trajopt_amd import abi, problems, robots
-from trajopt_amd.runtime import BatchTrustRegionSQP
+from trajopt_amd.runtime import BatchTrustRegionSQP, HipError
 
 pytestmark = pytest.mark.gpu
 
@@ -65,14 +65,21 @@ def _first_split(tg, to):
     return n
 
 
-def _perturbed_oracle_outcomes(wl, oracle_mod, tol, seeds=(1, 2, 3)):
-    """(status, flag) per problem of the oracle rerun from 1e-13-perturbed initial trajectories."""
-    out = [set() for _ in range(wl.batch)]
+def _perturbed_oracle_runs(wl, oracle_mod, seeds=(1, 2, 3, 4, 5)):
+    """The oracle rerun from 1e-13-perturbed initial trajectories: [(x, results)] per seed."""
+    runs = []
     for seed in seeds:
         wp = wl.slice(0, wl.batch)
         rng = np.random.default_rng(seed)
         wp.init[:, 1:] += rng.normal(0.0, 1e-13, wp.init[:, 1:].shape)
-        _, rp = oracle_mod.solve(wp, n_threads=16)
+        runs.append(oracle_mod.solve(wp, n_threads=16))
+    return runs
+
+
+def _perturbed_oracle_outcomes(wl, oracle_mod, tol, seeds=(1, 2, 3)):
+    """(status, flag) per problem of the oracle rerun from 1e-13-perturbed initial trajectories."""
+    out = [set() for _ in range(wl.batch)]
+    for _, rp in _perturbed_oracle_runs(wl, oracle_mod, seeds):
         for b in range(wl.batch):
             out[b].add((rp[b].status, rp[b].max_cnt_viol < tol))
     return out
@@ -102,6 +109,7 @@ def check_parity(wl, oracle_mod, x, res, tr=None, min_strict=0.85, label=""):
         return
     if tr is None:
         _, _, tr = solve_gpu(wl, trace=2048)
+    runs = None
     for b in bad:
         _, _, to = oracle_mod.solve_trace(wl, b, cap=2048)
         tg = tr[b]
@@ -120,7 +128,19 @@ def check_parity(wl, oracle_mod, x, res, tr=None, min_strict=0.85, label=""):
                                     f"{np.abs(x[b] - xo[b]).max():.2e} but every QP up to the split ({k}) was "
                                     f"polished on both sides and no trust-region decision flipped")
         cg, co = res[b].total_cost, ro[b].total_cost
-        assert abs(cg - co) <= 0.02 * max(1.0, abs(co)), f"{label} problem {b}: cost {cg} vs {co}"
+        if abs(cg - co) <= 0.02 * max(1.0, abs(co)):
+            continue
+        # the oracle itself is not reproducible on this problem: its own reruns from
+        # 1e-13-perturbed inputs disagree beyond the 1e-5 bar, and the GPU's cost lies
+        # within the range those reruns reach (+-2 %)
+        if runs is None:
+            runs = _perturbed_oracle_runs(wl, oracle_mod)
+        spread = max(np.abs(xr[b] - xo[b]).max() for xr, _ in runs)
+        costs = [co] + [rr[b].total_cost for _, rr in runs]
+        lo, hi = min(costs), max(costs)
+        assert spread > TOL_X and lo - 0.02 * max(1.0, abs(lo)) <= cg <= hi + 0.02 * max(1.0, abs(hi)), (
+            f"{label} problem {b}: cost {cg} vs {co}; perturbed oracle reruns spread {spread:.1e}, "
+            f"costs [{lo}, {hi}]")
 
 
 # ------------------------------------------------------------------ kinematics
@@ -157,6 +177,40 @@ def test_cartpose_linearization_parity(oracle_mod, cfg, B):
     # forward differences with eps = 1e-5 (kinematic_terms.hpp:15) amplify
     # last-bit FK differences by 1e5
     np.testing.assert_allclose(jac, jo, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("cfg", ["A", "B"])
+def test_cartpose_linearization_parity_tolerance(oracle_mod, cfg):
+    """Toleranced CartPose rows (applyTolerances on the error, the tolerance-aware
+    error difference in the FD jacobian): some components inside their band (zero
+    rows), some outside."""
+    wl = problems.with_cart_tolerances(problems.make_workload(cfg, 16), pos=0.02, rot=0.1)
+    rng = np.random.default_rng(11)
+    x = wl.init + rng.normal(0, 0.05, wl.init.shape)
+    s = BatchTrustRegionSQP(wl)
+    err, jac = s.linearize(x)
+    s.close()
+    eo, jo = oracle_mod.linearize(wl, x)
+    assert (eo == 0).any() and (eo != 0).any()
+    np.testing.assert_allclose(err, eo, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(jac, jo, rtol=0, atol=1e-9)
+
+
+def test_cartpose_linearization_golden_tolerance(golden):
+    g = golden("cartpose_B_tol")
+    wl = problems.with_cart_tolerances(problems.make_workload("B", g["x"].shape[0]))
+    s = BatchTrustRegionSQP(wl)
+    err, jac = s.linearize(g["x"])
+    s.close()
+    np.testing.assert_allclose(err, g["err"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(jac, g["jac"], rtol=0, atol=1e-9)
+
+
+def test_cartpose_inverted_tolerance_band_rejected():
+    wl = problems.with_cart_tolerances(problems.make_workload("A", 2))
+    wl.desc.cart_lower_tol[0][3] = 0.3
+    with pytest.raises(HipError, match="Inverted tolerance band"):
+        BatchTrustRegionSQP(wl)
 
 
 @pytest.mark.parametrize("cfg", ["A", "B"])
@@ -478,6 +532,17 @@ def _variant(name):
     if name == "discrete_with_static_hinges_8dof":
         wl = _single(_variant("collision_with_static_hinges"))
         return wl
+    # SQP parity with tolerance bands: free rotation about the tool axis (rx, +-0.2 rad).
+    # With bands on all six components the reference algorithm itself is not
+    # reproducible (flat cost regions: 1e-13 input perturbations move the oracle's
+    # solutions by up to 5e-2 and its costs by 9 %); those bands are covered by the
+    # linearisation tests above.
+    if name == "cartpose_tolerance_cost":
+        return problems.with_cart_tolerances(problems.make_workload("B", 16, first_problem=20), rot=0.2, axes=(3,))
+    if name == "cartpose_tolerance_cnt":
+        return problems.with_cart_tolerances(problems.make_workload("A", 16, first_problem=20), rot=0.2, axes=(3,))
+    if name == "cartpose_tolerance_collision":
+        return problems.with_cart_tolerances(problems.make_workload("C", 8, first_problem=20), rot=0.2, axes=(3,))
     if name == "single_problem":
         return problems.make_workload("B", 1, first_problem=5)
     # other chains: 8 DoF with the prismatic torso_lift_joint first, and 6 DoF
@@ -505,7 +570,8 @@ VARIANTS = ["jointvel_only", "short_horizon", "two_fixed_steps", "position_only_
             "min_horizon_2", "collision_empty_scene", "collision_fixed_both_ends", "collision_step_subrange",
             "torso_arm_8dof_A", "torso_arm_8dof_B", "torso_arm_8dof_C", "torso_arm_8dof_jointpos", "arm_6dof_A",
             "arm_6dof_C", "discrete_fixed_both_ends_subrange", "discrete_two_waypoints",
-            "discrete_with_static_hinges_8dof"]
+            "discrete_with_static_hinges_8dof", "cartpose_tolerance_cost", "cartpose_tolerance_cnt",
+            "cartpose_tolerance_collision"]
 
 
 @pytest.mark.parametrize("name", VARIANTS)
@@ -584,7 +650,7 @@ def test_smoke_entry():
 
 def test_bench_json_line():
     repo = abi.PKG_DIR.parent
-    p = subprocess.run([sys.executable, str(repo / "bench.py"), "--batch", "64", "--steps", "1", "--warmup", "0",
+    p = subprocess.run([sys.executable, str(repo / "bench.py"), "--batch", "64", "--steps", "3", "--warmup", "0",
                         "--cpu-problems", "8"], capture_output=True, text=True, timeout=600, cwd=repo)
     assert p.returncode == 0, p.stderr
     line = json.loads(p.stdout.strip().splitlines()[-1])
@@ -592,6 +658,7 @@ def test_bench_json_line():
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in line, k
     assert line["value"] > 0 and line["n_gpus"] == 1 and line["dtype"] == "f64"
+    assert line["config"]["batches_in_flight"] == 2 and line["config"]["batch_latency_ms"] > 0
     rf = line["roofline"]
     assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and 0 < rf["frac"] == pytest.approx(rf["achieved"] / 8000.0)
     cb = line["cpu_baseline"]

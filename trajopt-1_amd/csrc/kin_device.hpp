@@ -207,4 +207,41 @@ __device__ inline void transform_error(const Pose& T1inv, const Pose& T2, double
   rot_error(E.r, err + 3, false);
 }
 
+// tesseract applyTolerances: 0 inside [lower, upper], else the excess past the band
+__device__ inline void apply_tolerances(double* err, const double* lower, const double* upper)
+{
+  for (int i = 0; i < 6; ++i)
+    err[i] = (err[i] < lower[i]) ? err[i] - lower[i] : ((err[i] > upper[i]) ? err[i] - upper[i] : 0.0);
+}
+
+// Tolerance-aware calcJacobianTransformErrorDiff(target, source, source_perturbed,
+// lower, upper) given pe = target^-1 source, ppe = target^-1 source_perturbed: both
+// errors with the [-pi, pi] rotation vector, or the continuous [0, 2 pi) one for
+// both when a component jumps by more than pi, banded, then differenced (the same
+// restatement as oracle/src/kin.cpp calcJacobianTransformErrorDiffTol).
+__device__ inline void transform_error_diff_tol(const Pose& pe, const Pose& ppe, const double* lower,
+                                                const double* upper, double* diff)
+{
+  double e0[6], e1[6];
+  for (int i = 0; i < 3; ++i)
+  {
+    e0[i] = pe.t[i];
+    e1[i] = ppe.t[i];
+  }
+  rot_error(pe.r, e0 + 3, false);
+  rot_error(ppe.r, e1 + 3, false);
+  bool wrap = false;
+  for (int i = 3; i < 6; ++i)
+    wrap = wrap || fabs(e1[i] - e0[i]) > M_PI;
+  if (wrap)
+  {
+    rot_error(pe.r, e0 + 3, true);
+    rot_error(ppe.r, e1 + 3, true);
+  }
+  apply_tolerances(e0, lower, upper);
+  apply_tolerances(e1, lower, upper);
+  for (int i = 0; i < 6; ++i)
+    diff[i] = e1[i] - e0[i];
+}
+
 }  // namespace thip

@@ -234,6 +234,8 @@ __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
       st[21 + i] = Ti.t[i];
     }
     transform_error(Ti, Ss, st + 24);
+    if (c.d->cart_has_tol[k])
+      apply_tolerances(st + 24, c.d->cart_lower_tol[k], c.d->cart_upper_tol[k]);
   }
   BSYNC();
   // perturbed FKs: item (k, p)
@@ -267,13 +269,19 @@ __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
     Pose pe, ppe;
     pose_mul(Ti, Ss, pe);
     pose_mul(Ti, Sp, ppe);
-    double diff[6], r0[3], r1[3];
-    for (int i = 0; i < 3; ++i)
-      diff[i] = ppe.t[i] - pe.t[i];
-    rot_error(pe.r, r0, true);
-    rot_error(ppe.r, r1, true);
-    for (int i = 0; i < 3; ++i)
-      diff[3 + i] = r1[i] - r0[i];
+    double diff[6];
+    if (c.d->cart_has_tol[k])
+      transform_error_diff_tol(pe, ppe, c.d->cart_lower_tol[k], c.d->cart_upper_tol[k], diff);
+    else
+    {
+      double r0[3], r1[3];
+      for (int i = 0; i < 3; ++i)
+        diff[i] = ppe.t[i] - pe.t[i];
+      rot_error(pe.r, r0, true);
+      rot_error(ppe.r, r1, true);
+      for (int i = 0; i < 3; ++i)
+        diff[3 + i] = r1[i] - r0[i];
+    }
     const int r0w = c.T.term_row0[k], nr = c.T.term_nrow[k];
     for (int rr = 0; rr < nr; ++rr)
     {
@@ -1093,6 +1101,8 @@ __device__ void evaluate(Ctx& c, const double* x, double* costs, double* viols)
     pose_inv(Tt, Ti);
     double err[6];
     transform_error(Ti, Ss, err);
+    if (c.d->cart_has_tol[k])
+      apply_tolerances(err, c.d->cart_lower_tol[k], c.d->cart_upper_tol[k]);
     const int r0 = c.T.term_row0[k], nr = c.T.term_nrow[k];
     double v = 0;
     if (c.d->cart_is_cnt[k])

@@ -199,6 +199,12 @@ static int validate(const thip_problem_desc* d, std::string& why)
         return why = "Currently two adjacent fixed steps are not supported in collision term.", THIP_E_INVALID;
     }
   }
+  for (int k = 0; k < d->n_cart; ++k)
+    if (d->cart_has_tol[k])
+      for (int i = 0; i < 6; ++i)
+        if (!(d->cart_lower_tol[k][i] <= d->cart_upper_tol[k][i]))
+          return why = "CartPoseErrCalculator: Inverted tolerance band - lower > upper at one or more indices",
+                 THIP_E_INVALID;
   if (d->coll_enabled && (d->coll_max_contacts < 0 || d->coll_max_contacts > THIP_MAX_CONTACTS))
     return why = "collision: coll_max_contacts out of range", THIP_E_INVALID;
   if (d->osqp.check_termination < 0 || d->osqp.max_iter < 1 || d->osqp.scaling < 0)

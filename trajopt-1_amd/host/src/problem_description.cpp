@@ -593,13 +593,26 @@ void CartPoseTermInfo::hatch(TrajOptProb& prob)
   const auto kin = prob.GetKin();
   if (kin->isActiveLinkId(target_frame) || !kin->isActiveLinkId(source_frame))
     unsupported("CartPoseTermInfo with an active target frame (source static)");
+  // validateTolerances (kinematic_terms.cpp:41-56), then the band is used unless both
+  // bounds are empty or almost equal (:209-212)
+  bool has_tol = false;
   if (!lower_tolerance.empty() || !upper_tolerance.empty())
   {
-    bool equal = lower_tolerance.size() == upper_tolerance.size();
-    for (std::size_t i = 0; equal && i < lower_tolerance.size(); ++i)
-      equal = doubleEquals(lower_tolerance[i], upper_tolerance[i]);
-    if (!equal)
-      unsupported("CartPoseTermInfo with tolerances");
+    if (lower_tolerance.size() != upper_tolerance.size())
+      throw std::runtime_error("CartPoseErrCalculator: Mismatched tolerance sizes. lower: " +
+                               std::to_string(lower_tolerance.size()) +
+                               ", upper: " + std::to_string(upper_tolerance.size()));
+    bool equal = true;
+    for (std::size_t i = 0; i < lower_tolerance.size(); ++i)
+    {
+      if (lower_tolerance[i] > upper_tolerance[i])
+        throw std::runtime_error("CartPoseErrCalculator: Inverted tolerance band - lower > upper at one or more "
+                                 "indices");
+      equal = equal && doubleEquals(lower_tolerance[i], upper_tolerance[i]);
+    }
+    if (!equal && lower_tolerance.size() != 6)
+      throw std::runtime_error("CartPoseTermInfo: tolerances must have 6 entries (x, y, z, rx, ry, rz)");
+    has_tol = !equal;
   }
   if (timestep < 0 || timestep >= prob.GetNumSteps())
     throw std::runtime_error("CartPoseTermInfo: timestep " + std::to_string(timestep) + " out of range");
@@ -608,6 +621,12 @@ void CartPoseTermInfo::hatch(TrajOptProb& prob)
     unsupported("more than " + std::to_string(THIP_MAX_CART) + " CartPose terms");
   const int k = d.n_cart++;
   d.cart_step[k] = timestep;
+  d.cart_has_tol[k] = has_tol ? 1 : 0;
+  for (int i = 0; has_tol && i < 6; ++i)
+  {
+    d.cart_lower_tol[k][i] = lower_tolerance[static_cast<std::size_t>(i)];
+    d.cart_upper_tol[k][i] = upper_tolerance[static_cast<std::size_t>(i)];
+  }
   d.cart_is_cnt[k] = any(term_type & TermType::TT_COST) ? 0 : 1;
   d.cart_source_link[k] = kin->linkIndex(source_frame);
   for (int i = 0; i < 12; ++i)

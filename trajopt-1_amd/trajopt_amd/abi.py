@@ -109,6 +109,9 @@ class ProblemDesc(C.Structure):
         ("cart_source_offset", _D12 * MAX_CART),
         ("cart_pos_coeffs", _D3 * MAX_CART),
         ("cart_rot_coeffs", _D3 * MAX_CART),
+        ("cart_has_tol", C.c_int * MAX_CART),
+        ("cart_lower_tol", (C.c_double * 6) * MAX_CART),
+        ("cart_upper_tol", (C.c_double * 6) * MAX_CART),
         ("n_jpos", C.c_int),
         ("jpos_is_cnt", C.c_int * MAX_JPOS),
         ("jpos_first_step", C.c_int * MAX_JPOS),

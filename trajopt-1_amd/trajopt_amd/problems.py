@@ -257,3 +257,17 @@ def make_reference_unit(name: str, batch: int = 1) -> Workload:
         raise ValueError(f"unknown reference unit {name}")
     init = np.zeros((batch, N, D))
     return Workload(name, d, init, np.zeros((batch, 0, 12)), np.zeros((batch, 0, 16)), init.copy())
+
+
+def with_cart_tolerances(wl, pos=0.02, rot=0.1, axes=range(6)):
+    """Give every CartPose term of wl a symmetric tolerance band (CartPoseErrCalculator
+    with lower/upper tolerances, kinematic_terms.cpp:209-247): +-pos on x, y, z and
+    +-rot on rx, ry, rz, for the components in axes (the others get a [0, 0] band)."""
+    d = wl.desc
+    for k in range(d.n_cart):
+        d.cart_has_tol[k] = 1
+        for i in range(6):
+            b = (pos if i < 3 else rot) if i in axes else 0.0
+            d.cart_lower_tol[k][i] = -b
+            d.cart_upper_tol[k][i] = b
+    return wl
