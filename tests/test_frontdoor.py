@@ -142,3 +142,25 @@ def test_cli_usage():
     assert exe.exists()
     p = subprocess.run([str(exe)], capture_output=True, text=True)
     assert p.returncode == 2 and "usage" in p.stderr
+
+
+def test_cartpose_active_target_frame():
+    """is_target_active (kinematic_terms.cpp:206-247, 313-339): a static source frame and an
+    active target frame lower with the roles swapped -- the error calcTransformError(source,
+    target) is static^-1 * active, the jacobian perturbs the active frame -- so the kernel's
+    active frame is the target with its offset and the static pose is the source's."""
+    src_off = [0.1, -0.2, 0.3]
+    tgt_off = [0.05, 0.0, 0.02]
+    fwd = {"type": "cart_pose", "params": {"timestep": 4, "source_frame": "r_gripper_tool_frame",
+                                           "target_frame": "torso_lift_link", "source_frame_offset_xyz": tgt_off,
+                                           "target_frame_offset_xyz": src_off}}
+    rev = {"type": "cart_pose", "params": {"timestep": 4, "source_frame": "torso_lift_link",
+                                           "target_frame": "r_gripper_tool_frame", "source_frame_offset_xyz": src_off,
+                                           "target_frame_offset_xyz": tgt_off}}
+    d1, _, t1, _ = host.lower_json(_doc(costs=[fwd]))
+    d2, _, t2, _ = host.lower_json(_doc(costs=[rev]))
+    assert d1.n_cart == d2.n_cart == 1
+    assert d1.cart_source_link[0] == d2.cart_source_link[0] > 0
+    np.testing.assert_array_equal(list(d1.cart_source_offset[0]), list(d2.cart_source_offset[0]))
+    np.testing.assert_array_equal(t1, t2)
+    np.testing.assert_allclose(np.asarray(t2).reshape(-1)[[3, 7, 11]], src_off, atol=1e-15)

@@ -591,8 +591,17 @@ void CartPoseTermInfo::hatch(TrajOptProb& prob)
     return;
   }
   const auto kin = prob.GetKin();
-  if (kin->isActiveLinkId(target_frame) || !kin->isActiveLinkId(source_frame))
-    unsupported("CartPoseTermInfo with an active target frame (source static)");
+  // is_target_active_ (kinematic_terms.cpp:206, 213-247, 313-339): the error is
+  // calcTransformError(static, active) and the jacobian perturbs the active frame either way,
+  // so an active target lowers as the kernel's active frame with the source as the static one
+  const bool target_active = kin->isActiveLinkId(target_frame);
+  if (target_active == kin->isActiveLinkId(source_frame))
+    throw std::runtime_error("CartPoseTermInfo: source and target frames are both " +
+                             std::string(target_active ? "active" : "static"));
+  const std::string& active_frame = target_active ? target_frame : source_frame;
+  const std::string& static_frame = target_active ? source_frame : target_frame;
+  const Pose12& active_offset = target_active ? target_frame_offset : source_frame_offset;
+  const Pose12& static_offset = target_active ? source_frame_offset : target_frame_offset;
   // validateTolerances (kinematic_terms.cpp:41-56), then the band is used unless both
   // bounds are empty or almost equal (:209-212)
   bool has_tol = false;
@@ -628,21 +637,22 @@ void CartPoseTermInfo::hatch(TrajOptProb& prob)
     d.cart_upper_tol[k][i] = upper_tolerance[static_cast<std::size_t>(i)];
   }
   d.cart_is_cnt[k] = any(term_type & TermType::TT_COST) ? 0 : 1;
-  d.cart_source_link[k] = kin->linkIndex(source_frame);
+  d.cart_source_link[k] = kin->linkIndex(active_frame);
   for (int i = 0; i < 12; ++i)
-    d.cart_source_offset[k][i] = source_frame_offset[static_cast<std::size_t>(i)];
+    d.cart_source_offset[k][i] = active_offset[static_cast<std::size_t>(i)];
   for (int i = 0; i < 3; ++i)
   {
     d.cart_pos_coeffs[k][i] = pos_coeffs[static_cast<std::size_t>(i)];
     d.cart_rot_coeffs[k][i] = rot_coeffs[static_cast<std::size_t>(i)];
   }
-  // per-problem target: the offset in the chain root frame (the kernel forms base_pose * offset)
-  Pose12 off = target_frame_offset;
-  if (kin->linkIndex(target_frame) != 0)
+  // per-problem static frame pose: the offset in the chain root frame (the kernel forms
+  // base_pose * offset)
+  Pose12 off = static_offset;
+  if (kin->linkIndex(static_frame) != 0)
   {
     Pose12 base;
     std::copy(kin->chain.base_pose, kin->chain.base_pose + 12, base.begin());
-    off = poseMul(poseInv(base), poseMul(kin->staticWorldPose(target_frame), target_frame_offset));
+    off = poseMul(poseInv(base), poseMul(kin->staticWorldPose(static_frame), static_offset));
   }
   prob.cart_targets.insert(prob.cart_targets.end(), off.begin(), off.end());
 }
