@@ -543,6 +543,12 @@ def _variant(name):
         return problems.with_cart_tolerances(problems.make_workload("A", 16, first_problem=20), rot=0.2, axes=(3,))
     if name == "cartpose_tolerance_collision":
         return problems.with_cart_tolerances(problems.make_workload("C", 8, first_problem=20), rot=0.2, axes=(3,))
+    if name == "continuous_50_waypoints":
+        # config E's horizon and evaluator (50 waypoints, LVS_CONTINUOUS) on the 7-DoF arm: past the
+        # register segment's N <= 32, the generic ADMM step with hinge rows
+        wl = problems.make_workload("C", 8, n_steps=50, first_problem=30)
+        wl.desc.coll_continuous = 1
+        return wl
     if name == "single_problem":
         return problems.make_workload("B", 1, first_problem=5)
     # other chains: 8 DoF with the prismatic torso_lift_joint first, and 6 DoF
@@ -571,7 +577,7 @@ VARIANTS = ["jointvel_only", "short_horizon", "two_fixed_steps", "position_only_
             "torso_arm_8dof_A", "torso_arm_8dof_B", "torso_arm_8dof_C", "torso_arm_8dof_jointpos", "arm_6dof_A",
             "arm_6dof_C", "discrete_fixed_both_ends_subrange", "discrete_two_waypoints",
             "discrete_with_static_hinges_8dof", "cartpose_tolerance_cost", "cartpose_tolerance_cnt",
-            "cartpose_tolerance_collision"]
+            "cartpose_tolerance_collision", "continuous_50_waypoints"]
 
 
 @pytest.mark.parametrize("name", VARIANTS)
