@@ -1,6 +1,11 @@
 """GPU vs oracle parity summary for a config/batch (diagnostic).
 
     python tools/parity.py A 64 [B 64 ...]
+
+Workload names: the configs of trajopt_amd.problems.make_workload (A, B, C, J) and
+the variants C-disc (DISCRETE evaluator, buffer 0.1), C-cont (LVS_CONTINUOUS),
+C-cnt (collision constraint), B-tol / A-tol (CartPose tool-axis tolerance band),
+C50-cont (50 waypoints, LVS_CONTINUOUS).
 """
 import sys
 import time
@@ -13,10 +18,28 @@ from trajopt_amd import abi, problems
 from trajopt_amd.runtime import BatchTrustRegionSQP
 from oracle import oracle
 
+
+
+def make(name, B):
+    base, _, var = name.partition("-")
+    n_steps = 50 if base == "C50" else None
+    wl = problems.make_workload("C" if base == "C50" else base, B, **({"n_steps": n_steps} if n_steps else {}))
+    if var == "disc":
+        wl.desc.coll_continuous = 2
+        wl.desc.coll_buffer = 0.1
+    elif var == "cont":
+        wl.desc.coll_continuous = 1
+    elif var == "cnt":
+        wl.desc.coll_is_cnt = 1
+    elif var == "tol":
+        problems.with_cart_tolerances(wl, rot=0.2, axes=(3,))
+    return wl
+
+
 args = sys.argv[1:]
 for i in range(0, len(args), 2):
     cfg, B = args[i], int(args[i + 1])
-    wl = problems.make_workload(cfg, B)
+    wl = make(cfg, B)
     s = BatchTrustRegionSQP(wl)
     t = time.time()
     xg, rg = s.optimize()
