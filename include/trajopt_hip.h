@@ -50,6 +50,7 @@ extern "C" {
 #define THIP_MAX_SPHERES 32
 #define THIP_MAX_PRIMS 16
 #define THIP_MAX_JPOS 8
+#define THIP_MAX_JVX 4
 #define THIP_MAX_CONTACTS 131072
 
 /* error codes */
@@ -208,6 +209,21 @@ typedef struct thip_problem_desc {
   double jpos_targets[THIP_MAX_JPOS][THIP_MAX_DOF];
   double jpos_upper_tols[THIP_MAX_JPOS][THIP_MAX_DOF];
   double jpos_lower_tols[THIP_MAX_JPOS][THIP_MAX_DOF];
+
+  /* Further JointVelTermInfo terms in the tolerance form, besides the jv_*
+   * term above: is_cnt 0 -> JointVelIneqCost (trajectory_costs.cpp:303-374),
+   * is_cnt 1 -> JointVelIneqConstraint (:426-500); two hinge rows per (step,
+   * joint).  Steps clamped as the jv_* term's (problem_description.cpp:1228-1245).
+   * Cost terms follow the JointPos cost terms, constraint terms the JointPos
+   * constraint terms. */
+  int n_jvx;
+  int jvx_is_cnt[THIP_MAX_JVX];
+  int jvx_first_step[THIP_MAX_JVX];
+  int jvx_last_step[THIP_MAX_JVX];
+  double jvx_coeffs[THIP_MAX_JVX][THIP_MAX_DOF];
+  double jvx_targets[THIP_MAX_JVX][THIP_MAX_DOF];
+  double jvx_upper_tols[THIP_MAX_JVX][THIP_MAX_DOF];
+  double jvx_lower_tols[THIP_MAX_JVX][THIP_MAX_DOF];
 
   /* CollisionTermInfo, LVS_DISCRETE or LVS_CONTINUOUS, cost or constraint
    * (collision_terms.cpp:737-1161,1267-1386):

@@ -174,12 +174,54 @@ public:
       v.insert(v.end(), r.begin(), r.end());
     return v;
   }
+  // JointVelIneqConstraint::value (trajectory_costs.cpp:472-487): [diff1, diff2] hinged,
+  // column-major over the [step x joint] blocks
+  DblVec values(const DblVec& x) const
+  {
+    DblVec up, lo;
+    for (std::size_t j = 0; j < coeffs_.size(); ++j)
+      for (int i = first_; i <= last_ - 1; ++i)
+      {
+        const double vel = rows_[static_cast<std::size_t>(i + 1)][j].value(x) - rows_[static_cast<std::size_t>(i)][j].value(x);
+        const double d0 = vel - targets_[j];
+        up.push_back(std::max((d0 - upper_[j]) * coeffs_[j], 0.0));
+        lo.push_back(std::max(((d0 * -1) + lower_[j]) * coeffs_[j], 0.0));
+      }
+    up.insert(up.end(), lo.begin(), lo.end());
+    return up;
+  }
+  const AffExprVector& exprs() const { return exprs_; }
 
 private:
   std::vector<VarVector> rows_;
   DblVec coeffs_, targets_, upper_, lower_;
   int first_, last_;
   AffExprVector exprs_;
+};
+
+// JointVelIneqConstraint (trajectory_costs.cpp:426-500): the same rows as
+// JointVelIneqCost, as inequality constraints
+class JointVelIneqConstraint : public Constraint
+{
+public:
+  JointVelIneqConstraint(std::vector<VarVector> rows, DblVec coeffs, DblVec targets, DblVec upper, DblVec lower,
+                         int first_step, int last_step)
+    : Constraint("JointVelIneq"), rows_(rows, coeffs, targets, upper, lower, first_step, last_step)
+  {
+  }
+  ConstraintType type() override { return INEQ; }
+  DblVec value(const DblVec& x) override { return rows_.values(x); }
+  ConvexConstraints::Ptr convex(const DblVec&, Model* model) override
+  {
+    auto out = std::make_shared<ConvexConstraints>(model);
+    for (const AffExpr& e : rows_.exprs())
+      out->addIneqCnt(e);
+    return out;
+  }
+  VarVector getVars() override { return rows_.getVars(); }
+
+private:
+  JointVelIneqCost rows_;
 };
 
 // ------------------------------------------------------------ JointPos
@@ -575,6 +617,31 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
   for (int k = 0; k < d.n_jpos; ++k)
     if (!d.jpos_is_cnt[k])
       addJointPosTerm(tp, rows, d, k, jposTargets(k));
+  // further JointVel tolerance terms (JointVelTermInfo::hatch with tolerances,
+  // problem_description.cpp:1346-1391), steps clamped as the first term's
+  auto jvxArgs = [&](int x, int& first, int& last) {
+    first = d.jvx_first_step[x];
+    last = d.jvx_last_step[x];
+    if (last <= -1)
+      last = N - 1;
+    if ((N - 2) <= first)
+      first = N - 2;
+    if ((N - 1) <= last)
+      last = N - 1;
+    if (last == first)
+      last += 1;
+    if (last < first)
+      std::swap(first, last);
+  };
+  auto dv = [&](const double* p) { return DblVec(p, p + D); };
+  for (int x = 0; x < d.n_jvx; ++x)
+    if (!d.jvx_is_cnt[x])
+    {
+      int f, l;
+      jvxArgs(x, f, l);
+      tp.prob->addCost(std::make_shared<JointVelIneqCost>(rows, dv(d.jvx_coeffs[x]), dv(d.jvx_targets[x]),
+                                                          dv(d.jvx_upper_tols[x]), dv(d.jvx_lower_tols[x]), f, l));
+    }
   if (d.coll_enabled && !d.coll_is_cnt)
     addCollisionTerms(tp, rows, d, scene);
   // cnt_infos: CartPose constraints, collision constraint
@@ -590,6 +657,14 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
   for (int k = 0; k < d.n_jpos; ++k)
     if (d.jpos_is_cnt[k])
       addJointPosTerm(tp, rows, d, k, jposTargets(k));
+  for (int x = 0; x < d.n_jvx; ++x)
+    if (d.jvx_is_cnt[x])
+    {
+      int f, l;
+      jvxArgs(x, f, l);
+      tp.prob->addConstraint(std::make_shared<JointVelIneqConstraint>(
+          rows, dv(d.jvx_coeffs[x]), dv(d.jvx_targets[x]), dv(d.jvx_upper_tols[x]), dv(d.jvx_lower_tols[x]), f, l));
+    }
   if (d.coll_enabled && d.coll_is_cnt)
     addCollisionTerms(tp, rows, d, scene);
   return tp;

@@ -77,7 +77,7 @@ def _doc(**over):
          "wrong number of JointVelTermInfo targets. expected 7 got 2"),
         (_doc(costs=[{"type": "joint_acc", "params": {}}]), "term type 'joint_acc' is not supported on the HIP path"),
         (_doc(constraints=[{"type": "joint_vel", "params": {"targets": [0]}}]),
-         "JointVelTermInfo as a constraint (JointVelEqConstraint / JointVelIneqConstraint) is not supported"),
+         "JointVelTermInfo as an equality constraint (JointVelEqConstraint) is not supported"),
         (_doc(costs=[{"type": "collision", "params": {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 0}}]),
          "collision evaluator_type 0 (DISCRETE = 1, LVS_DISCRETE = 2, CONTINUOUS = 3, LVS_CONTINUOUS = 4 are) "
          "is not supported"),
@@ -164,3 +164,19 @@ def test_cartpose_active_target_frame():
     np.testing.assert_array_equal(list(d1.cart_source_offset[0]), list(d2.cart_source_offset[0]))
     np.testing.assert_array_equal(t1, t2)
     np.testing.assert_allclose(np.asarray(t2).reshape(-1)[[3, 7, 11]], src_off, atol=1e-15)
+
+
+def test_joint_vel_tolerance_terms_lower_to_hinge_terms():
+    """JointVelTermInfo with tolerances as a constraint (JointVelIneqConstraint) and a
+    second tolerance-form cost lower to jvx terms; the first cost stays the jv_* term."""
+    band = {"targets": [0], "lower_tols": [-0.1], "upper_tols": [0.2], "first_step": 0, "last_step": 4}
+    doc = _doc(costs=[{"type": "joint_vel", "params": {"targets": [0.5], "lower_tols": [-0.01], "upper_tols": [0.0],
+                                                       "first_step": 0, "last_step": 2}},
+                      {"type": "joint_vel", "params": {"targets": [-0.5], "lower_tols": [-0.01],
+                                                       "upper_tols": [0.01], "first_step": 3, "last_step": 4}}],
+               constraints=[{"type": "joint_vel", "params": band}])
+    d, _, _, _ = host.lower_json(doc)
+    assert d.jv_enabled == 1 and d.jv_targets[0] == 0.5 and d.jv_lower_tols[0] == -0.01
+    assert d.n_jvx == 2
+    assert (d.jvx_is_cnt[0], d.jvx_first_step[0], d.jvx_last_step[0]) == (0, 3, 4)
+    assert (d.jvx_is_cnt[1], d.jvx_lower_tols[1][3], d.jvx_upper_tols[1][6]) == (1, -0.1, 0.2)

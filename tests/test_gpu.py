@@ -549,6 +549,18 @@ def _variant(name):
         wl = problems.make_workload("C", 8, n_steps=50, first_problem=30)
         wl.desc.coll_continuous = 1
         return wl
+    if name == "jointvel_cnt_band_with_cartpose":
+        # config A plus a JointVelIneqConstraint band and a second JointVelIneqCost
+        wl = problems.make_workload("A", 16, first_problem=50)
+        d = wl.desc
+        d.n_jvx = 2
+        d.jvx_is_cnt[0], d.jvx_first_step[0], d.jvx_last_step[0] = 1, 0, -1
+        d.jvx_is_cnt[1], d.jvx_first_step[1], d.jvx_last_step[1] = 0, 2, 6
+        for j in range(wl.n_dof):
+            d.jvx_coeffs[0][j], d.jvx_lower_tols[0][j], d.jvx_upper_tols[0][j] = 2.0, -0.15, 0.15
+            d.jvx_coeffs[1][j], d.jvx_targets[1][j] = 0.5, 0.02
+            d.jvx_lower_tols[1][j], d.jvx_upper_tols[1][j] = -0.01, 0.01
+        return wl
     if name == "single_problem":
         return problems.make_workload("B", 1, first_problem=5)
     # other chains: 8 DoF with the prismatic torso_lift_joint first, and 6 DoF
@@ -577,7 +589,7 @@ VARIANTS = ["jointvel_only", "short_horizon", "two_fixed_steps", "position_only_
             "torso_arm_8dof_A", "torso_arm_8dof_B", "torso_arm_8dof_C", "torso_arm_8dof_jointpos", "arm_6dof_A",
             "arm_6dof_C", "discrete_fixed_both_ends_subrange", "discrete_two_waypoints",
             "discrete_with_static_hinges_8dof", "cartpose_tolerance_cost", "cartpose_tolerance_cnt",
-            "cartpose_tolerance_collision", "continuous_50_waypoints"]
+            "cartpose_tolerance_collision", "continuous_50_waypoints", "jointvel_cnt_band_with_cartpose"]
 
 
 @pytest.mark.parametrize("name", VARIANTS)
@@ -693,6 +705,20 @@ def test_joint_pos_ineq_reference_unit(oracle_mod):
         for i in list(range(0, 5)) + list(range(6, 10)):
             assert (x[b, i] < 0.2 + 1e-4).all() and (x[b, i] > -0.1 - 1e-4).all()
     check_parity(wl, oracle_mod, x, res, tr, label="joint_pos_ineq")
+
+
+def test_joint_vel_ineq_reference_unit(oracle_mod):
+    """joint_costs_unit.cpp:354-463 (inequality_jointVel): a JointVelIneqConstraint
+    and two JointVelIneqCost terms (three JointVel terms, static hinge rows)."""
+    wl = problems.make_reference_unit("joint_vel_ineq", 4)
+    x, res, tr = solve_gpu(wl, trace=512)
+    N = wl.n_steps
+    for b in range(wl.batch):
+        assert res[b].n_cnts == 1 and res[b].n_costs == 2
+        v = np.diff(x[b], axis=0)
+        for i in list(range(0, N // 2)) + list(range(N // 2 + 1, N - 1)):
+            assert (v[i] < 0.2 + 1e-4).all() and (v[i] > -0.1 - 1e-4).all()
+    check_parity(wl, oracle_mod, x, res, tr, label="joint_vel_ineq")
 
 
 def test_joint_pos_per_problem_targets():

@@ -122,6 +122,21 @@ def test_joint_pos_reference_units(oracle_mod):
         assert (x[0, i] < 0.2 + 1e-4).all() and (x[0, i] > -0.1 - 1e-4).all()
 
 
+def test_joint_vel_ineq_reference_unit(oracle_mod):
+    """joint_costs_unit.cpp:354-463 (inequality_jointVel) on the oracle: the
+    velocities stay inside the constraint band [-0.1, 0.2] (cnt_tol 1e-4) on both
+    halves while the costs pull toward +0.5 / -0.5."""
+    wl = problems.make_reference_unit("joint_vel_ineq", 1)
+    x, res = oracle_mod.solve(wl, n_threads=1)
+    assert res[0].status == 0 and res[0].n_cnts == 1 and res[0].n_costs == 2
+    v = np.diff(x[0], axis=0)
+    N = wl.n_steps
+    for i in list(range(0, N // 2)) + list(range(N // 2 + 1, N - 1)):
+        assert (v[i] < 0.2 + 1e-4).all() and (v[i] > -0.1 - 1e-4).all()
+    np.testing.assert_allclose(v[:4], 0.2, atol=1e-4)
+    np.testing.assert_allclose(v[5:], -0.1, atol=1e-4)
+
+
 def test_joint_pos_goal_workload(oracle_mod):
     """Config J (arm_around_table.json's term set without collision): the goal
     constraint holds at convergence; a goal offset of 0.3 rad hits the

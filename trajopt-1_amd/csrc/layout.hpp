@@ -148,6 +148,7 @@ struct Layout
   int n_costs;    // JointVel (0/1) + CartPose cost terms + JointPos cost terms + collision step pairs
   int n_cnts;     // CartPose constraint terms + JointPos constraint terms
   int n_jpos;     // JointPos terms
+  int n_jvx;      // further JointVel tolerance terms (static hinge owners n_jpos + 1 + x)
   int jv_first, jv_last;
   int jv_ineq;    // JointVelIneqCost (tolerances) instead of the quadratic JointVelEqCost
   int hinge;      // the QP has hinge rows (collision contacts and/or static hinge rows)
@@ -212,6 +213,9 @@ struct Tables
   int* grp_ns;     // spheres in the group
   int* sph_order;  // sphere indices sorted by (link, index)
   int* coll_fixed; // per waypoint: 1 if a collision fixed step (N)
+  int* jvx_first;  // further JointVel terms: clamped steps and cost / constraint slot (THIP_MAX_JVX)
+  int* jvx_last;
+  int* jvx_slot;
   int* coll_slot;  // per collision unit (step pair, or waypoint for DISCRETE): term slot
                    // relative to coll_cost0, -1 for a fixed waypoint without a term (N)
 };

@@ -733,22 +733,26 @@ __device__ void static_hinge_rows(Ctx& c, const int* HP)
     }
     else
     {
-      // vel = -x_t + x_t+1 - targ
-      const double cf = c.d->jv_coeffs[j], tg = c.d->jv_targets[j];
+      // vel = -x_t + x_t+1 - targ; owner n_jpos: the jv_* term, n_jpos + 1 + x: jvx term x
+      const int xo = k - L.n_jpos - 1;
+      const double cf = (xo >= 0) ? c.d->jvx_coeffs[xo][j] : c.d->jv_coeffs[j];
+      const double tg = (xo >= 0) ? c.d->jvx_targets[xo][j] : c.d->jv_targets[j];
+      const double up = (xo >= 0) ? c.d->jvx_upper_tols[xo][j] : c.d->jv_upper_tols[j];
+      const double lo = (xo >= 0) ? c.d->jvx_lower_tols[xo][j] : c.d->jv_lower_tols[j];
       mask = (1 << j) | (1 << (D + j));
       if (kind == SH_JV_UP)
       {
         // expr = (upper_tol - vel) * -coeff
         a[j] = 1.0 * -cf;
         a[D + j] = -1.0 * -cf;
-        cst = (c.d->jv_upper_tols[j] - (0.0 - tg)) * -cf;
+        cst = (up - (0.0 - tg)) * -cf;
       }
       else
       {
         // expr = (lower_tol - vel) * coeff
         a[j] = 1.0 * cf;
         a[D + j] = -1.0 * cf;
-        cst = (c.d->jv_lower_tols[j] - (0.0 - tg)) * cf;
+        cst = (lo - (0.0 - tg)) * cf;
       }
     }
     HK[h] = cst;
@@ -783,6 +787,25 @@ __device__ void sh_values(Ctx& c, const double* x, double* costs, double* viols)
     if (c.tid == 0)
       costs[0] = s1 + s2;
   }
+  // further JointVel tolerance terms: JointVelIneqCost::value / JointVelIneqConstraint::value
+  // (trajectory_costs.cpp:348-361, 472-487; violation = sum of the nonnegative values)
+  for (int xo = 0; xo < L.n_jvx; ++xo)
+  {
+    const int f = c.T.jvx_first[xo], nv = (c.T.jvx_last[xo] - f) * D;
+    double s1 = 0, s2 = 0;
+    FOR(i, nv)
+    {
+      const int t = f + i / D, j = i % D;
+      const double cf = c.d->jvx_coeffs[xo][j];
+      const double d0 = (x[(t + 1) * D + j] - x[t * D + j]) - c.d->jvx_targets[xo][j];
+      s1 += fmax((d0 - c.d->jvx_upper_tols[xo][j]) * cf, 0.0);
+      s2 += fmax(((d0 * -1) + c.d->jvx_lower_tols[xo][j]) * cf, 0.0);
+    }
+    s1 = block_sum(c, s1);
+    s2 = block_sum(c, s2);
+    if (c.tid == 0)
+      (c.d->jvx_is_cnt[xo] ? viols : costs)[c.T.jvx_slot[xo]] = s1 + s2;
+  }
   for (int k = 0; k < L.n_jpos; ++k)
   {
     if (!c.T.jpos_ineq[k])
@@ -816,12 +839,14 @@ __device__ void sh_model_values(Ctx& c, const double* SX, double* mcost, double*
   const int* HP = c.ia(I_HPTR);
   const int* HMv = c.ia(I_HMASK);
   const double *HC0 = c.a(A_HC0), *HKv = c.a(A_HK);
-  for (int o = 0; o <= L.n_jpos; ++o)
+  for (int o = 0; o <= L.n_jpos + L.n_jvx; ++o)
   {
-    const bool jv = (o == L.n_jpos);
-    if (jv ? !L.jv_ineq : !c.T.jpos_ineq[o])
+    // owners: JointPos terms, the jv_* term (n_jpos), the jvx terms (n_jpos + 1 + x)
+    const bool jv = (o == L.n_jpos), jx = (o > L.n_jpos);
+    const int xo = o - L.n_jpos - 1;
+    if (jx ? false : (jv ? !L.jv_ineq : !c.T.jpos_ineq[o]))
       continue;
-    const bool cnt = !jv && c.d->jpos_is_cnt[o];
+    const bool cnt = jx ? (c.d->jvx_is_cnt[xo] != 0) : (!jv && c.d->jpos_is_cnt[o]);
     double v = 0;
     FOR(sr, c.T.n_sh)
     {
@@ -844,7 +869,7 @@ __device__ void sh_model_values(Ctx& c, const double* SX, double* mcost, double*
     }
     v = block_sum(c, v);
     if (c.tid == 0)
-      (cnt ? mviol : mcost)[jv ? 0 : c.T.jpos_slot[o]] = v;
+      (cnt ? mviol : mcost)[jx ? c.T.jvx_slot[xo] : (jv ? 0 : c.T.jpos_slot[o])] = v;
   }
 }
 

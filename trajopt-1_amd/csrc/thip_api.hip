@@ -155,6 +155,18 @@ static int validate(const thip_problem_desc* d, std::string& why)
     if (d->cart_source_link[k] <= 0 || d->cart_source_link[k] >= ch.n_links)
       return why = "CartPose source frame must be an active chain link", THIP_E_INVALID;
   }
+  if (d->n_jvx < 0 || d->n_jvx > THIP_MAX_JVX)
+    return why = "n_jvx out of range", THIP_E_INVALID;
+  for (int x = 0; x < d->n_jvx; ++x)
+  {
+    bool tol = false;
+    for (int j = 0; j < d->chain.n_dof; ++j)
+      tol = tol || std::fabs(d->jvx_upper_tols[x][j]) >= 1e-5 || std::fabs(d->jvx_lower_tols[x][j]) >= 1e-5;
+    if (!tol)
+      return why = "jvx terms are the tolerance forms (JointVelIneqCost / JointVelIneqConstraint): "
+                   "a term with zero tolerances goes in jv_*",
+             THIP_E_INVALID;
+  }
   if (d->n_jpos < 0 || d->n_jpos > THIP_MAX_JPOS)
     return why = "n_jpos out of range", THIP_E_INVALID;
   for (int k = 0; k < d->n_jpos; ++k)
@@ -239,19 +251,26 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   L.n_fixed_rows = d.n_fixed * L.D;
   L.n_cart = d.n_cart;
   // JointVelTermInfo::hatch step clamping (problem_description.cpp:1228-1245)
-  int first = d.jv_first_step, last = d.jv_last_step;
-  if (last <= -1)
-    last = L.N - 1;
-  if ((L.N - 2) <= first)
-    first = L.N - 2;
-  if ((L.N - 1) <= last)
-    last = L.N - 1;
-  if (last == first)
-    last += 1;
-  if (last < first)
-    std::swap(first, last);
-  L.jv_first = first;
-  L.jv_last = last;
+  auto jv_clamp = [&](int first, int last, int& f_out, int& l_out) {
+    if (last <= -1)
+      last = L.N - 1;
+    if ((L.N - 2) <= first)
+      first = L.N - 2;
+    if ((L.N - 1) <= last)
+      last = L.N - 1;
+    if (last == first)
+      last += 1;
+    if (last < first)
+      std::swap(first, last);
+    f_out = first;
+    l_out = last;
+  };
+  jv_clamp(d.jv_first_step, d.jv_last_step, L.jv_first, L.jv_last);
+  std::vector<int> jvx_first(THIP_MAX_JVX, 0), jvx_last(THIP_MAX_JVX, 0), jvx_slot(THIP_MAX_JVX, 0);
+  for (int x = 0; x < d.n_jvx; ++x)
+    jv_clamp(d.jvx_first_step[x], d.jvx_last_step[x], jvx_first[static_cast<size_t>(x)],
+             jvx_last[static_cast<size_t>(x)]);
+  L.n_jvx = d.n_jvx;
   // zero tolerances: trajopt_common::doubleEquals(tol, 0.) (problem_description.cpp:1135-1138,1249-1252)
   auto zero_tol = [](double v) { return std::fabs(v) < 1e-5; };
   L.jv_ineq = 0;
@@ -315,6 +334,9 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     if (!d.jpos_is_cnt[k])
       jpos_slot[static_cast<size_t>(k)] = n_costs++;
   }
+  for (int x = 0; x < d.n_jvx; ++x)
+    if (!d.jvx_is_cnt[x])
+      jvx_slot[static_cast<size_t>(x)] = n_costs++;
   for (int k = 0; k < d.n_jpos; ++k)
   {
     if (!d.jpos_is_cnt[k])
@@ -335,6 +357,9 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
       }
     jpos_nrow[static_cast<size_t>(k)] = static_cast<int>(row_term.size()) - jpos_row0[static_cast<size_t>(k)];
   }
+  for (int x = 0; x < d.n_jvx; ++x)
+    if (d.jvx_is_cnt[x])
+      jvx_slot[static_cast<size_t>(x)] = n_cnts++;
   L.n_abs = static_cast<int>(row_term.size());
   L.n_abs_cost = 0;
   for (int r = 0; r < L.n_abs; ++r)
@@ -359,6 +384,17 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
         add_sh(SH_JV_UP, d.n_jpos, j, t, t, -1);
         add_sh(SH_JV_LO, d.n_jpos, j, t, t, -1);
       }
+  // further JointVel tolerance terms: owner n_jpos + 1 + x
+  for (int x = 0; x < d.n_jvx; ++x)
+  {
+    const int slot = d.jvx_is_cnt[x] ? jvx_slot[static_cast<size_t>(x)] : -1;
+    for (int t = jvx_first[static_cast<size_t>(x)]; t <= jvx_last[static_cast<size_t>(x)] - 1; ++t)
+      for (int j = 0; j < L.D; ++j)
+      {
+        add_sh(SH_JV_UP, d.n_jpos + 1 + x, j, t, t, slot);
+        add_sh(SH_JV_LO, d.n_jpos + 1 + x, j, t, t, slot);
+      }
+  }
   for (int k = 0; k < d.n_jpos; ++k)
   {
     if (!jpos_ineq[static_cast<size_t>(k)])
@@ -612,6 +648,8 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   const size_t o_jf = push(jpos_first, THIP_MAX_JPOS), o_jl = push(jpos_last, THIP_MAX_JPOS),
                o_js = push(jpos_slot, THIP_MAX_JPOS), o_j0 = push(jpos_row0, THIP_MAX_JPOS),
                o_jn = push(jpos_nrow, THIP_MAX_JPOS);
+  const size_t o_xf = push(jvx_first, THIP_MAX_JVX), o_xl = push(jvx_last, THIP_MAX_JVX),
+               o_xs = push(jvx_slot, THIP_MAX_JVX);
   // collision model tables: spheres grouped by link, ascending (scan order)
   std::vector<int> grp_link, grp_s0, grp_ns, sph_order, coll_fixed(static_cast<size_t>(L.N), 0);
   if (L.coll)
@@ -664,6 +702,9 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   T.jpos_row0 = ctx->d_tables + o_j0;
   T.jpos_nrow = ctx->d_tables + o_jn;
   T.jpos_ineq = ctx->d_tables + o_jq;
+  T.jvx_first = ctx->d_tables + o_xf;
+  T.jvx_last = ctx->d_tables + o_xl;
+  T.jvx_slot = ctx->d_tables + o_xs;
   T.n_sh = n_sh;
   T.sh_kind = ctx->d_tables + o_shk;
   T.sh_owner = ctx->d_tables + o_sho;

@@ -523,11 +523,34 @@ void JointVelTermInfo::hatch(TrajOptProb& prob)
   checkParameterSize(lower_tols, n_dof, "JointVelTermInfo lower_tols", true);
   if (any(term_type & TermType::TT_USE_TIME))
     unsupported("JointVelTermInfo with use_time");
-  if (!any(term_type & TermType::TT_COST))
-    unsupported("JointVelTermInfo as a constraint (JointVelEqConstraint / JointVelIneqConstraint)");
+  // doubleEquals(tol, 0) (problem_description.cpp:1249-1252): zero tolerances -> the Eq forms
+  bool zero_tols = true;
+  for (unsigned j = 0; j < n_dof; ++j)
+    zero_tols = zero_tols && doubleEquals(upper_tols[j], 0.) && doubleEquals(lower_tols[j], 0.);
+  const bool is_cost = any(term_type & TermType::TT_COST);
   thip_problem_desc& d = prob.desc();
+  if (!zero_tols && (!is_cost || d.jv_enabled))
+  {
+    // JointVelIneqConstraint, or a further JointVelIneqCost: two hinge rows per (step, joint)
+    if (d.n_jvx >= THIP_MAX_JVX)
+      unsupported("more than " + std::to_string(THIP_MAX_JVX + 1) + " JointVel tolerance terms");
+    const int x = d.n_jvx++;
+    d.jvx_is_cnt[x] = is_cost ? 0 : 1;
+    d.jvx_first_step[x] = first_step;
+    d.jvx_last_step[x] = last_step;
+    for (unsigned j = 0; j < n_dof; ++j)
+    {
+      d.jvx_coeffs[x][j] = coeffs[j];
+      d.jvx_targets[x][j] = targets[j];
+      d.jvx_upper_tols[x][j] = upper_tols[j];
+      d.jvx_lower_tols[x][j] = lower_tols[j];
+    }
+    return;
+  }
+  if (!is_cost)
+    unsupported("JointVelTermInfo as an equality constraint (JointVelEqConstraint)");
   if (d.jv_enabled)
-    unsupported("more than one joint_vel cost");
+    unsupported("more than one JointVel cost without tolerances");
   d.jv_enabled = 1;
   d.jv_first_step = first_step;
   d.jv_last_step = last_step;

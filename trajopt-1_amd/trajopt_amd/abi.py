@@ -17,6 +17,7 @@ MAX_CART = 64
 MAX_SPHERES = 32
 MAX_PRIMS = 16
 MAX_JPOS = 8
+MAX_JVX = 4
 
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_CONTINUOUS, JOINT_PRISMATIC = 0, 1, 2, 3
 PRIM_SPHERE, PRIM_BOX, PRIM_CAPSULE = 0, 1, 2
@@ -120,6 +121,14 @@ class ProblemDesc(C.Structure):
         ("jpos_targets", (C.c_double * MAX_DOF) * MAX_JPOS),
         ("jpos_upper_tols", (C.c_double * MAX_DOF) * MAX_JPOS),
         ("jpos_lower_tols", (C.c_double * MAX_DOF) * MAX_JPOS),
+        ("n_jvx", C.c_int),
+        ("jvx_is_cnt", C.c_int * MAX_JVX),
+        ("jvx_first_step", C.c_int * MAX_JVX),
+        ("jvx_last_step", C.c_int * MAX_JVX),
+        ("jvx_coeffs", (C.c_double * MAX_DOF) * MAX_JVX),
+        ("jvx_targets", (C.c_double * MAX_DOF) * MAX_JVX),
+        ("jvx_upper_tols", (C.c_double * MAX_DOF) * MAX_JVX),
+        ("jvx_lower_tols", (C.c_double * MAX_DOF) * MAX_JVX),
         ("coll_enabled", C.c_int),
         ("coll_is_cnt", C.c_int),
         ("coll_first_step", C.c_int),

@@ -226,6 +226,11 @@ def make_reference_unit(name: str, batch: int = 1) -> Workload:
     joint_pos_ineq  joint_costs_unit.cpp:152-262 (inequality_jointPos): JointPos
                     constraint 0 with tolerances [-0.1, 0.2] on all steps, hinge
                     costs toward +0.5 / -0.5 (tolerance 0.01) on each half.
+    joint_vel_ineq  joint_costs_unit.cpp:354-463 (inequality_jointVel): JointVel
+                    constraint 0 with tolerances [-0.1, 0.2] on all steps
+                    (JointVelIneqConstraint, a jvx term), hinge costs toward
+                    +0.5 (tolerances [-0.01, 0]) on steps 0..4 (the jv_* term) and
+                    -0.5 (+-0.01) on steps 5..9 (a jvx term).
     """
     N = 10
     d = base_desc(N)
@@ -253,6 +258,18 @@ def make_reference_unit(name: str, batch: int = 1) -> Workload:
             d.jpos_lower_tols[0][j], d.jpos_upper_tols[0][j] = -0.1, 0.2
             d.jpos_targets[1][j], d.jpos_lower_tols[1][j], d.jpos_upper_tols[1][j] = 0.5, -0.01, 0.01
             d.jpos_targets[2][j], d.jpos_lower_tols[2][j], d.jpos_upper_tols[2][j] = -0.5, -0.01, 0.01
+    elif name == "joint_vel_ineq":
+        d.jv_enabled = 1
+        d.jv_first_step, d.jv_last_step = 0, (N - 1) // 2
+        d.n_jvx = 2
+        d.jvx_is_cnt[0], d.jvx_first_step[0], d.jvx_last_step[0] = 0, (N - 1) // 2 + 1, N - 1
+        d.jvx_is_cnt[1], d.jvx_first_step[1], d.jvx_last_step[1] = 1, 0, N - 1
+        for j in range(D):
+            d.jv_coeffs[j], d.jv_targets[j], d.jv_lower_tols[j], d.jv_upper_tols[j] = 1.0, 0.5, -0.01, 0.0
+            d.jvx_coeffs[0][j], d.jvx_targets[0][j] = 1.0, -0.5
+            d.jvx_lower_tols[0][j], d.jvx_upper_tols[0][j] = -0.01, 0.01
+            d.jvx_coeffs[1][j], d.jvx_targets[1][j] = 1.0, 0.0
+            d.jvx_lower_tols[1][j], d.jvx_upper_tols[1][j] = -0.1, 0.2
     else:
         raise ValueError(f"unknown reference unit {name}")
     init = np.zeros((batch, N, D))
