@@ -2334,15 +2334,14 @@ struct Norms
 __device__ void compute_residuals(Ctx& c, const double* x, const double* z, const double* y, Norms& nm)
 {
   PROF(1);
-  double *AX = c.a(A_AX), *PX = c.a(A_PX), *ATY = c.a(A_ATY), *PRV = c.a(A_PRV), *DRV = c.a(A_DRV);
   const double *E = c.a(A_E), *DS = c.a(A_DS), *Q = c.a(A_Q);
   double v[12] = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
+  // (no stores in these loops: the next rows' loads are not ordered behind them)
+#pragma unroll 2
   FOR(r, c.m())
   {
     const double ax = row_ax(c, r, x);
     const double pr = ax - z[r];
-    AX[r] = ax;
-    PRV[r] = pr;
     const double einv = 1.0 / E[r];
     v[0] = fmax(v[0], fabs(einv * pr));
     v[1] = fmax(v[1], fabs(einv * z[r]));
@@ -2356,14 +2355,12 @@ __device__ void compute_residuals(Ctx& c, const double* x, const double* z, cons
   const bool chunked = c.s->n_h > 0;
   if (chunked)
     hinge_chunk_sums(c, y, build_hinge_chunks(c));
+#pragma unroll 2
   FOR(col, c.nc())
   {
     const double px = col_px(c, col, x);
     const double aty = col_aty(c, col, y, chunked);
-    PX[col] = px;
-    ATY[col] = aty;
     const double dr = Q[col] + px + aty;
-    DRV[col] = dr;
     const double dinv = 1.0 / DS[col];
     v[6] = fmax(v[6], fabs(dinv * dr));
     v[7] = fmax(v[7], fabs(dinv * Q[col]));
