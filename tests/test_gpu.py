@@ -646,6 +646,38 @@ def test_full_batch_properties_and_sampled_parity(oracle_mod):
     assert within >= 0.85 * len(sample)
 
 
+def test_full_batch_collision_properties_and_sampled_parity(oracle_mod):
+    """The bench workload (config C, 1024 problems, LVS-discrete collision):
+    bitwise reruns, joint limits, the fixed timestep, no contact-capacity overflow,
+    consistent collision counters on every problem; oracle parity on a sample of 32."""
+    wl = problems.make_workload("C", 1024)
+    s = BatchTrustRegionSQP(wl)
+    x1, r1 = s.optimize()
+    x2, r2 = s.optimize()
+    s.close()
+    np.testing.assert_array_equal(x1, x2)
+    assert [r.n_admm_iters for r in r1] == [r.n_admm_iters for r in r2]
+    assert [r.n_contact_rows for r in r1] == [r.n_contact_rows for r in r2]
+    lo, hi, _ = robots.chain_limits(wl.desc.chain)
+    viol = max(float(np.max(lo - x1)), float(np.max(x1 - hi)), 0.0)
+    assert viol <= 1e-4, viol
+    np.testing.assert_allclose(x1[:, 0], wl.init[:, 0], rtol=0, atol=1e-6)
+    assert all(r.flags == 0 for r in r1)
+    assert all(r.status in (0, 1, 2) for r in r1)
+    assert all(r.n_substates >= 2 * (wl.n_steps - 1) * r.n_sqp_iters for r in r1)
+    assert sum(r.n_contact_rows for r in r1) > 0
+    sample = list(range(16)) + list(range(1008, 1024))
+    xo1, ro1 = oracle_mod.solve(problems.make_workload("C", 16), n_threads=16)
+    xo2, ro2 = oracle_mod.solve(problems.make_workload("C", 16, first_problem=1008), n_threads=16)
+    xo = np.concatenate([xo1, xo2])
+    ro = ro1 + ro2
+    within = 0
+    for k, b in enumerate(sample):
+        assert r1[b].status == ro[k].status
+        within += np.abs(x1[b] - xo[k]).max() <= TOL_X
+    assert within >= 0.85 * len(sample)
+
+
 def test_devices_stream_interop():
     """The solver runs on a caller-provided torch stream (plumbing for
     overlapping copies with the solve)."""
