@@ -64,6 +64,15 @@ def test_defaults_match_reference_values(lib):
     assert s.eps_abs == 1e-4 and s.eps_rel == 1e-6 and s.max_iter == 8192 and s.polish_refine_iter == 3
 
 
+def _with_collision(d, evaluator):
+    c = problems.make_workload("C", 1).desc
+    for name, _ in abi.ProblemDesc._fields_:
+        if name.startswith("coll_") or name in ("n_spheres", "sphere_link", "sphere_center", "sphere_radius", "n_prims"):
+            setattr(d, name, getattr(c, name))
+    d.coll_first_step, d.coll_last_step = 0, -1
+    d.coll_continuous = evaluator
+
+
 def _create(lib, desc, batch=4):
     ctx = C.c_void_p()
     rc = lib.thip_create(0, C.byref(desc), batch, C.byref(ctx))
@@ -81,6 +90,11 @@ def _create(lib, desc, batch=4):
         (lambda d: setattr(d, "n_jpos", 9), "n_jpos"),
         (lambda d: (setattr(d, "n_jpos", 1), d.jpos_upper_tols[0].__setitem__(2, float("inf"))), "finite"),
         (lambda d: (setattr(d, "n_jpos", 1), d.jpos_coeffs[0].__setitem__(0, float("nan"))), "finite"),
+        (lambda d: (d.cart_has_tol.__setitem__(0, 1), d.cart_lower_tol[0].__setitem__(3, 0.3)),
+         "Inverted tolerance band"),
+        (lambda d: setattr(d, "n_jvx", 5), "n_jvx"),
+        (lambda d: setattr(d, "n_jvx", 1), "tolerance forms"),
+        (lambda d: _with_collision(d, 3), "coll_continuous"),
     ],
 )
 def test_create_rejects_invalid_descriptors(lib, mutate, needle):
