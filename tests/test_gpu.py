@@ -836,6 +836,28 @@ def test_frontdoor_cli(tmp_path):
     assert p.stdout.count("OPT_CONVERGED") == 6
 
 
+def test_frontdoor_single_problem_dropin(tmp_path, oracle_mod):
+    """trajopt::BasicTrustRegionSQP (the reference's per-problem optimizer usage,
+    planning_unit.cpp:83-124: ConstructProblem, initialize, optimize, x()) as a batch of
+    one: same trajectory as the oracle on the lowered problem."""
+    from trajopt_amd import host
+
+    wl = problems.make_workload("A", 2)
+    exe = abi.LIB_DIR / "sqp_single"
+    for b in range(2):
+        f = tmp_path / f"p{b}.json"
+        f.write_text(host.workload_to_json(wl, b))
+        p = subprocess.run([str(exe), str(f)], capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0, p.stderr
+        lines = p.stdout.strip().splitlines()
+        status = lines[0].split()[1]
+        x = np.array([[float(v) for v in ln.split()] for ln in lines[1:]])
+        lw = _lowered_workload([f.read_text()])
+        xo, ro = oracle_mod.solve(lw, n_threads=1)
+        assert status == ["OPT_CONVERGED", "OPT_SCO_ITERATION_LIMIT", "OPT_PENALTY_ITERATION_LIMIT"][ro[0].status]
+        assert np.abs(x - xo[0]).max() <= TOL_X
+
+
 def test_contact_capacity_overflow_fails_loudly():
     """A QP with more contacts than coll_max_contacts ends the run with
     OPT_FAILED and THIP_FLAG_CONTACT_OVERFLOW; contacts are never dropped."""

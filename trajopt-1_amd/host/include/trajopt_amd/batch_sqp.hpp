@@ -34,4 +34,36 @@ private:
   std::vector<TrajOptProb::Ptr> probs_;
   struct thip_ctx* ctx_ = nullptr;
 };
+
+// Per-problem drop-in for the reference's optimizer usage (SURVEY.md §8b tier i):
+//   sco::BasicTrustRegionSQP opt(prob);            optimizers.hpp:142-194
+//   opt.initialize(trajToDblVec(prob->GetInitTraj()));
+//   opt.optimize();                                optimizers.cpp:699-991
+//   getTraj(opt.x(), ...), opt.results()           (planning_unit.cpp:83-124)
+// The problem runs as a batch of one on the device; parameters set here
+// replace the problem's opt_info for this run.
+class BasicTrustRegionSQP
+{
+public:
+  explicit BasicTrustRegionSQP(TrajOptProb::Ptr prob, int device = 0);
+  void setProblem(TrajOptProb::Ptr prob);
+  void setParameters(const sco::BasicTrustRegionSQPParameters& param) { param_ = param; }
+  const sco::BasicTrustRegionSQPParameters& getParameters() const { return param_; }
+  sco::BasicTrustRegionSQPParameters& getParameters() { return param_; }
+  // x: the trajectory row-major [step][dof] (trajToDblVec); size n_steps * n_dof
+  void initialize(const DblVec& x);
+  sco::OptStatus optimize();
+  const DblVec& x() const { return results_.x; }
+  const sco::OptResults& results() const { return results_; }
+
+private:
+  TrajOptProb::Ptr prob_;
+  int device_;
+  sco::BasicTrustRegionSQPParameters param_;
+  DblVec x0_;
+  sco::OptResults results_;
+};
+
+// trajopt/src/utils.cpp:13-24: the trajectory as one row-major vector
+DblVec trajToDblVec(const std::vector<DblVec>& traj);
 }  // namespace trajopt

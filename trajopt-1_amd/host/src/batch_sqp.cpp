@@ -97,4 +97,95 @@ std::vector<sco::OptResults> BatchTrustRegionSQP::optimize()
 }
 
 double BatchTrustRegionSQP::lastKernelMs() const { return thip_last_kernel_ms(ctx_); }
+
+DblVec trajToDblVec(const std::vector<DblVec>& traj)
+{
+  DblVec out;
+  for (const auto& row : traj)
+    out.insert(out.end(), row.begin(), row.end());
+  return out;
+}
+
+BasicTrustRegionSQP::BasicTrustRegionSQP(TrajOptProb::Ptr prob, int device) : device_(device)
+{
+  setProblem(std::move(prob));
+}
+
+void BasicTrustRegionSQP::setProblem(TrajOptProb::Ptr prob)
+{
+  if (!prob)
+    throw std::runtime_error("BasicTrustRegionSQP: null problem");
+  prob_ = std::move(prob);
+  // the problem's own parameters (ProblemConstructionInfo::opt_info) are the defaults
+  const thip_sqp_params& q = prob_->desc().sqp;
+  param_.improve_ratio_threshold = q.improve_ratio_threshold;
+  param_.min_trust_box_size = q.min_trust_box_size;
+  param_.min_approx_improve = q.min_approx_improve;
+  param_.min_approx_improve_frac = q.min_approx_improve_frac;
+  param_.max_iter = q.max_iter;
+  param_.trust_shrink_ratio = q.trust_shrink_ratio;
+  param_.trust_expand_ratio = q.trust_expand_ratio;
+  param_.cnt_tolerance = q.cnt_tolerance;
+  param_.max_merit_coeff_increases = q.max_merit_coeff_increases;
+  param_.max_qp_solver_failures = q.max_qp_solver_failures;
+  param_.merit_coeff_increase_ratio = q.merit_coeff_increase_ratio;
+  param_.initial_merit_error_coeff = q.initial_merit_error_coeff;
+  param_.inflate_constraints_individually = q.inflate_constraints_individually != 0;
+  param_.trust_box_size = q.trust_box_size;
+  x0_.clear();
+  results_ = sco::OptResults{};
+}
+
+void BasicTrustRegionSQP::initialize(const DblVec& x)
+{
+  const std::size_t n = static_cast<std::size_t>(prob_->GetNumSteps()) * static_cast<std::size_t>(prob_->GetNumDOF());
+  if (x.size() != n)
+    throw std::runtime_error("BasicTrustRegionSQP::initialize: expected " + std::to_string(n) + " values, got " +
+                             std::to_string(x.size()));
+  // fixed timesteps are linear equalities to ConstructProblem's initial trajectory
+  // (problem_description.cpp:489-510); the device path pins them to the uploaded start,
+  // so a start that moves a fixed step would change the problem: refuse it
+  const thip_problem_desc& d = prob_->desc();
+  const int D = prob_->GetNumDOF();
+  for (int f = 0; f < d.n_fixed; ++f)
+  {
+    const int t = d.fixed_steps[f];
+    for (int j = 0; j < D; ++j)
+      if (x[static_cast<std::size_t>(t * D + j)] != prob_->GetInitTraj()[static_cast<std::size_t>(t)][static_cast<std::size_t>(j)])
+        throw std::runtime_error("BasicTrustRegionSQP::initialize: fixed timestep " + std::to_string(t) +
+                                 " differs from the problem's initial trajectory");
+  }
+  x0_ = x;
+}
+
+sco::OptStatus BasicTrustRegionSQP::optimize()
+{
+  auto p = std::make_shared<TrajOptProb>(*prob_);
+  thip_sqp_params& q = p->desc().sqp;
+  q.improve_ratio_threshold = param_.improve_ratio_threshold;
+  q.min_trust_box_size = param_.min_trust_box_size;
+  q.min_approx_improve = param_.min_approx_improve;
+  q.min_approx_improve_frac = param_.min_approx_improve_frac;
+  q.max_iter = param_.max_iter;
+  q.trust_shrink_ratio = param_.trust_shrink_ratio;
+  q.trust_expand_ratio = param_.trust_expand_ratio;
+  q.cnt_tolerance = param_.cnt_tolerance;
+  q.max_merit_coeff_increases = param_.max_merit_coeff_increases;
+  q.max_qp_solver_failures = param_.max_qp_solver_failures;
+  q.merit_coeff_increase_ratio = param_.merit_coeff_increase_ratio;
+  q.initial_merit_error_coeff = param_.initial_merit_error_coeff;
+  q.inflate_constraints_individually = param_.inflate_constraints_individually ? 1 : 0;
+  q.trust_box_size = param_.trust_box_size;
+  if (!x0_.empty())
+  {
+    const int N = p->GetNumSteps(), D = p->GetNumDOF();
+    std::vector<DblVec> traj(static_cast<std::size_t>(N));
+    for (int t = 0; t < N; ++t)
+      traj[static_cast<std::size_t>(t)].assign(x0_.begin() + t * D, x0_.begin() + (t + 1) * D);
+    p->SetInitTraj(traj);
+  }
+  BatchTrustRegionSQP batch({ p }, device_);
+  results_ = batch.optimize()[0];
+  return results_.status;
+}
 }  // namespace trajopt

@@ -1,0 +1,34 @@
+// The reference's per-problem optimizer usage on the HIP path (planning_unit.cpp:83-124):
+//   ConstructProblem(pci) -> BasicTrustRegionSQP opt(prob); opt.initialize(...); opt.optimize()
+// usage: sqp_single problem.json   -> prints "status <s> iters <n> cost <c>" and the trajectory
+#include <cstdio>
+
+#include "trajopt_amd/batch_sqp.hpp"
+
+int main(int argc, char** argv)
+{
+  if (argc != 2)
+  {
+    std::fprintf(stderr, "usage: sqp_single problem.json\n");
+    return 2;
+  }
+  try
+  {
+    const auto env = trajopt::Environment::makePR2();
+    trajopt::TrajOptProb::Ptr prob = trajopt::ConstructProblem(Json::parseFile(argv[1]), env);
+    trajopt::BasicTrustRegionSQP opt(prob);
+    opt.initialize(trajopt::trajToDblVec(prob->GetInitTraj()));
+    const sco::OptStatus st = opt.optimize();
+    std::printf("status %s iters %d cost %.17g\n", sco::toString(st).c_str(), opt.results().n_sqp_iters,
+                opt.results().total_cost);
+    const int D = prob->GetNumDOF();
+    for (std::size_t i = 0; i < opt.x().size(); ++i)
+      std::printf("%.17g%c", opt.x()[i], (static_cast<int>(i) % D == D - 1) ? '\n' : ' ');
+    return 0;
+  }
+  catch (const std::exception& e)
+  {
+    std::fprintf(stderr, "error: %s\n", e.what());
+    return 1;
+  }
+}
