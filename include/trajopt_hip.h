@@ -358,7 +358,14 @@ int thip_sizeof_result(void);
  * rho_final, prim_res, dual_res, sum|x*|, trust_box) during thip_sqp_run,
  * up to `capacity` entries per problem (0 disables). */
 int thip_debug_trace(thip_ctx* ctx, int capacity);
-/* records [batch][capacity][10], counts [batch] */
+/* records [batch][capacity][THIP_TRACE_W], counts [batch].  One record per QP
+ * solve: [0] warm start, [1] rho at entry, [2] ADMM iterations, [3] status,
+ * [4] polish status, [5] rho at exit, [6] primal / [7] dual residual, [8] sum |x*|,
+ * [9] trust box size; then the trust-region step that QP served
+ * (BasicTrustRegionSQPResults::writeSolver, optimizers.cpp:533-547): [10] old
+ * exact merit, [11] new exact merit, [12] approx merit improve, [13] exact merit
+ * improve, [14] ratio, [15] decision (1 converged, 2 shrink, 3 accept; 0 none). */
+#define THIP_TRACE_W 16
 int thip_debug_get_trace(thip_ctx* ctx, double* records, int* counts);
 
 /* Linearised collision rows (config C) of every problem at trajectories x

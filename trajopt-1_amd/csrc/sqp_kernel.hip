@@ -3318,8 +3318,8 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
       c.s->prev_status = 0;
       if (c.s->trace && c.s->trace_n < c.s->trace_cap)
       {
-        double* rec = c.s->trace + 10 * c.s->trace_n++;
-        for (int i = 0; i < 10; ++i)
+        double* rec = c.s->trace + THIP_TRACE_W * c.s->trace_n++;
+        for (int i = 0; i < THIP_TRACE_W; ++i)
           rec[i] = 0;
         rec[3] = -1;
         rec[9] = c.s->trust;
@@ -3451,7 +3451,9 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
     xs = block_sum(c, xs);
     if (c.tid == 0 && c.s->trace_n < c.s->trace_cap)
     {
-      double* rec = c.s->trace + 10 * c.s->trace_n;
+      double* rec = c.s->trace + THIP_TRACE_W * c.s->trace_n;
+      for (int i = 10; i < THIP_TRACE_W; ++i)
+        rec[i] = 0;
       rec[0] = warm ? 1.0 : 0.0;
       rec[1] = c.s->rho0;
       rec[2] = iters;
@@ -3818,6 +3820,17 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
             c.s->trust *= P.trust_expand_ratio;
           }
           c.s->flag = decision;
+          if (c.s->trace && c.s->trace_n > 0 && c.s->trace_n == c.s->n_qp)  // (not after a full trace)
+          {
+            // the record of the QP this step solved (writeSolver's fields)
+            double* rec = c.s->trace + THIP_TRACE_W * (c.s->trace_n - 1);
+            rec[10] = old_merit;
+            rec[11] = new_merit;
+            rec[12] = approx;
+            rec[13] = exact;
+            rec[14] = ratio;
+            rec[15] = decision;
+          }
         }
         BSYNC();
         decision = c.s->flag;
@@ -3924,7 +3937,7 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
   sv.Nb = dyn + L.N * L.D * L.D;
   if (threadIdx.x == 0)
   {
-    ctl.trace = args.trace ? args.trace + (long long)b * args.trace_cap * 10 : nullptr;
+    ctl.trace = args.trace ? args.trace + (long long)b * args.trace_cap * THIP_TRACE_W : nullptr;
     ctl.trace_cap = args.trace_cap;
     ctl.trace_n = 0;
     ctl.prof = args.prof ? args.prof + (long long)b * kProfSlots : nullptr;

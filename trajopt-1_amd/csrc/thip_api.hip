@@ -1001,7 +1001,7 @@ int thip_debug_trace(thip_ctx* ctx, int capacity)
   if (capacity == 0)
     return THIP_OK;
   const size_t B = static_cast<size_t>(ctx->batch);
-  HIPCHK(ctx, hipMalloc(&ctx->d_trace, B * static_cast<size_t>(capacity) * 10 * sizeof(double)));
+  HIPCHK(ctx, hipMalloc(&ctx->d_trace, B * static_cast<size_t>(capacity) * THIP_TRACE_W * sizeof(double)));
   HIPCHK(ctx, hipMalloc(&ctx->d_trace_n, B * sizeof(int)));
   HIPCHK(ctx, hipMemset(ctx->d_trace_n, 0, B * sizeof(int)));
   return THIP_OK;
@@ -1113,7 +1113,7 @@ int thip_debug_get_trace(thip_ctx* ctx, double* records, int* counts)
     return THIP_E_INVALID;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   const size_t B = static_cast<size_t>(ctx->batch);
-  HIPCHK(ctx, hipMemcpy(records, ctx->d_trace, B * static_cast<size_t>(ctx->trace_cap) * 10 * sizeof(double),
+  HIPCHK(ctx, hipMemcpy(records, ctx->d_trace, B * static_cast<size_t>(ctx->trace_cap) * THIP_TRACE_W * sizeof(double),
                         hipMemcpyDeviceToHost));
   HIPCHK(ctx, hipMemcpy(counts, ctx->d_trace_n, B * sizeof(int), hipMemcpyDeviceToHost));
   return THIP_OK;

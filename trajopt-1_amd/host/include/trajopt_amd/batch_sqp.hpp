@@ -27,12 +27,16 @@ public:
   std::vector<sco::OptResults> optimize();
   // HIP-event duration of the last fused launch (ms).
   double lastKernelMs() const;
+  // Per-QP records of the next optimize() (thip_debug_trace, THIP_TRACE_W doubles each).
+  void enableTrace(int capacity);
+  std::vector<std::vector<double>> trace() const;  // [problem][n_records * THIP_TRACE_W]
   int batch() const { return static_cast<int>(probs_.size()); }
 
 private:
   void check(int rc, const char* what) const;
   std::vector<TrajOptProb::Ptr> probs_;
   struct thip_ctx* ctx_ = nullptr;
+  int trace_cap_ = 0;
 };
 
 // Per-problem drop-in for the reference's optimizer usage (SURVEY.md §8b tier i):

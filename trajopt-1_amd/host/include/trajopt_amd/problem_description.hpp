@@ -80,6 +80,11 @@ struct BasicTrustRegionSQPParameters
   double initial_merit_error_coeff = 10;
   bool inflate_constraints_individually = true;
   double trust_box_size = 1e-1;
+  // optimizers.hpp:127-129: with log_results, log_dir/trajopt_solver.log gets one
+  // writeSolver line per trust-region step (the vars / costs / constraints logs are not
+  // written: the device loop keeps no per-iteration copies of x and the term values)
+  bool log_results = false;
+  std::string log_dir = "/tmp";
 };
 }  // namespace sco
 

@@ -1,5 +1,7 @@
 #include "trajopt_amd/batch_sqp.hpp"
 
+#include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -98,6 +100,47 @@ std::vector<sco::OptResults> BatchTrustRegionSQP::optimize()
 
 double BatchTrustRegionSQP::lastKernelMs() const { return thip_last_kernel_ms(ctx_); }
 
+void BatchTrustRegionSQP::enableTrace(int capacity)
+{
+  check(thip_debug_trace(ctx_, capacity), "thip_debug_trace");
+  trace_cap_ = capacity;
+}
+
+std::vector<std::vector<double>> BatchTrustRegionSQP::trace() const
+{
+  const std::size_t B = static_cast<std::size_t>(batch()), W = THIP_TRACE_W;
+  std::vector<double> rec(B * static_cast<std::size_t>(trace_cap_) * W);
+  std::vector<int> cnt(B);
+  check(thip_debug_get_trace(ctx_, rec.data(), cnt.data()), "thip_debug_get_trace");
+  std::vector<std::vector<double>> out(B);
+  for (std::size_t b = 0; b < B; ++b)
+  {
+    const auto* p = rec.data() + b * static_cast<std::size_t>(trace_cap_) * W;
+    out[b].assign(p, p + static_cast<std::size_t>(std::min(cnt[b], trace_cap_)) * W);
+  }
+  return out;
+}
+
+// BasicTrustRegionSQPResults::writeSolver (optimizers.cpp:533-547), from the trace records
+static void writeSolverLog(const std::string& path, const std::vector<double>& rec)
+{
+  std::FILE* f = std::fopen(path.c_str(), "w");
+  if (!f)
+    throw std::runtime_error("BasicTrustRegionSQP: cannot open " + path);
+  bool header = true;
+  for (std::size_t k = 0; k + THIP_TRACE_W <= rec.size(); k += THIP_TRACE_W)
+  {
+    const double* r = rec.data() + k;
+    if (r[15] == 0)
+      continue;  // a QP without a merit evaluation (solver failure)
+    if (header)
+      std::fprintf(f, "%s,%s,%s,%s,%s,%s\n", "DESCRIPTION", "oldexact", "new_exact", "dapprox", "dexact", "ratio");
+    header = false;
+    std::fprintf(f, "%s,%10.3e,%10.3e,%10.3e,%10.3e,%10.3e\n", "Solver", r[10], r[11], r[12], r[13], r[14]);
+  }
+  std::fclose(f);
+}
+
 DblVec trajToDblVec(const std::vector<DblVec>& traj)
 {
   DblVec out;
@@ -185,7 +228,11 @@ sco::OptStatus BasicTrustRegionSQP::optimize()
     p->SetInitTraj(traj);
   }
   BatchTrustRegionSQP batch({ p }, device_);
+  if (param_.log_results)
+    batch.enableTrace(8192);
   results_ = batch.optimize()[0];
+  if (param_.log_results)
+    writeSolverLog(param_.log_dir + "/trajopt_solver.log", batch.trace()[0]);
   return results_.status;
 }
 }  // namespace trajopt

@@ -1,26 +1,41 @@
 // The reference's per-problem optimizer usage on the HIP path (planning_unit.cpp:83-124):
 //   ConstructProblem(pci) -> BasicTrustRegionSQP opt(prob); opt.initialize(...); opt.optimize()
-// usage: sqp_single problem.json   -> prints "status <s> iters <n> cost <c>" and the trajectory
+// usage: sqp_single [--log DIR] problem.json
+//   prints "status <s> iters <n> cost <c> fevals <f>" and the trajectory; with --log, the
+//   reference's log_results solver log in DIR/trajopt_solver.log
 #include <cstdio>
+#include <string>
 
 #include "trajopt_amd/batch_sqp.hpp"
 
 int main(int argc, char** argv)
 {
-  if (argc != 2)
+  std::string log_dir;
+  int a = 1;
+  if (argc == 4 && std::string(argv[1]) == "--log")
   {
-    std::fprintf(stderr, "usage: sqp_single problem.json\n");
+    log_dir = argv[2];
+    a = 3;
+  }
+  else if (argc != 2)
+  {
+    std::fprintf(stderr, "usage: sqp_single [--log DIR] problem.json\n");
     return 2;
   }
   try
   {
     const auto env = trajopt::Environment::makePR2();
-    trajopt::TrajOptProb::Ptr prob = trajopt::ConstructProblem(Json::parseFile(argv[1]), env);
+    trajopt::TrajOptProb::Ptr prob = trajopt::ConstructProblem(Json::parseFile(argv[a]), env);
     trajopt::BasicTrustRegionSQP opt(prob);
+    if (!log_dir.empty())
+    {
+      opt.getParameters().log_results = true;
+      opt.getParameters().log_dir = log_dir;
+    }
     opt.initialize(trajopt::trajToDblVec(prob->GetInitTraj()));
     const sco::OptStatus st = opt.optimize();
-    std::printf("status %s iters %d cost %.17g\n", sco::toString(st).c_str(), opt.results().n_sqp_iters,
-                opt.results().total_cost);
+    std::printf("status %s iters %d cost %.17g fevals %d\n", sco::toString(st).c_str(), opt.results().n_sqp_iters,
+                opt.results().total_cost, opt.results().n_func_evals);
     const int D = prob->GetNumDOF();
     for (std::size_t i = 0; i < opt.x().size(); ++i)
       std::printf("%.17g%c", opt.x()[i], (static_cast<int>(i) % D == D - 1) ? '\n' : ' ');

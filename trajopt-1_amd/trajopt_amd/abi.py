@@ -18,6 +18,7 @@ MAX_SPHERES = 32
 MAX_PRIMS = 16
 MAX_JPOS = 8
 MAX_JVX = 4
+TRACE_W = 16  # THIP_TRACE_W
 
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_CONTINUOUS, JOINT_PRISMATIC = 0, 1, 2, 3
 PRIM_SPHERE, PRIM_BOX, PRIM_CAPSULE = 0, 1, 2

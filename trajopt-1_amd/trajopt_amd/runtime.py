@@ -116,7 +116,7 @@ class BatchTrustRegionSQP:
         self._check(self.lib.thip_debug_trace(self.ctx, capacity), "thip_debug_trace")
 
     def get_trace(self):
-        rec = np.zeros((self.batch, self._trace_cap, 10))
+        rec = np.zeros((self.batch, self._trace_cap, abi.TRACE_W))
         cnt = (C.c_int * self.batch)()
         self._check(self.lib.thip_debug_get_trace(self.ctx, _dp(rec), cnt), "thip_debug_get_trace")
         return [rec[b, : cnt[b]] for b in range(self.batch)]
