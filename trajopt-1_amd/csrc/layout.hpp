@@ -237,6 +237,11 @@ struct KernelArgs
   int trace_cap;
   // diagnostics: per-problem phase cycle counters [batch][kProfSlots] (null = off)
   long long* prof;
+  // sqp_kernel: stage the uploaded inputs into the workspace at entry and gather
+  // the final trajectory at exit (null = skip); one launch per run
+  const double* stage_init;  // [batch][nx]
+  const double* stage_tgt;   // [batch][n_cart][12]
+  double* xout;              // [batch][nx]
 };
 
 constexpr int kHPack = 14;  // doubles per hinge row in A_HPK

@@ -3942,9 +3942,27 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
     ctl.trace_n = 0;
     ctl.prof = args.prof ? args.prof + (long long)b * kProfSlots : nullptr;
   }
+  if (args.stage_init)
+  {
+    // the uploaded inputs into this problem's (HBM-resident) INIT, X and TGT
+    for (int i = threadIdx.x; i < L.nx; i += kBlock)
+    {
+      const double v = args.stage_init[(long long)b * L.nx + i];
+      wsb[L.doff[A_INIT] + i] = v;
+      wsb[L.doff[A_X] + i] = v;
+    }
+    for (int i = threadIdx.x; i < L.n_cart * 12; i += kBlock)
+      wsb[L.doff[A_TGT] + i] = args.stage_tgt[(long long)b * L.n_cart * 12 + i];
+  }
   __syncthreads();
   const long long w0 = wall_clock64();
   sqp_optimize(c, sv);
+  if (args.xout)
+  {
+    __syncthreads();
+    for (int i = threadIdx.x; i < L.nx; i += kBlock)
+      args.xout[(long long)b * L.nx + i] = wsb[L.doff[A_X] + i];
+  }
   if (threadIdx.x == 0 && ctl.prof)
     ctl.prof[14] += wall_clock64() - w0;
   if (threadIdx.x == 0 && args.trace_n)

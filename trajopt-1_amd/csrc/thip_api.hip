@@ -787,6 +787,9 @@ static KernelArgs make_args(thip_ctx* ctx)
   a.trace_n = ctx->d_trace_n;
   a.trace_cap = ctx->trace_cap;
   a.prof = ctx->d_prof;
+  a.stage_init = nullptr;
+  a.stage_tgt = nullptr;
+  a.xout = nullptr;
   return a;
 }
 
@@ -875,14 +878,16 @@ int thip_sqp_run(thip_ctx* ctx)
     return ctx->err = "thip_sqp_run: call thip_upload first", THIP_E_STATE;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   KernelArgs a = make_args(ctx);
-  // re-stage the inputs: a run always starts from the uploaded initial trajectory
-  hipLaunchKernelGGL(stage_inputs_kernel, dim3(ctx->batch), dim3(kBlock), 0, ctx->stream, a, ctx->d_init, ctx->d_tgt);
+  // one launch: each workgroup re-stages its problem's uploaded inputs (a run always
+  // starts from the uploaded initial trajectory) and gathers its final trajectory, so
+  // no small kernels queue behind another batch's workgroups when batches overlap
+  a.stage_init = ctx->d_init;
+  a.stage_tgt = ctx->d_tgt;
+  a.xout = ctx->d_x;
   HIPCHK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
   hipLaunchKernelGGL(sqp_kernel, dim3(ctx->batch), dim3(kBlock), ctx->lds_bytes, ctx->stream, a);
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-  hipLaunchKernelGGL(gather_x_kernel, dim3(ctx->batch), dim3(kBlock), 0, ctx->stream, a, ctx->d_x);
-  HIPCHK(ctx, hipGetLastError());
   ctx->ran = true;
   return THIP_OK;
 }
