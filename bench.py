@@ -151,10 +151,13 @@ def main():
     from trajopt_amd.runtime import BatchTrustRegionSQP
 
     wl = sharding.rank_workload(args.config, args.batch, rank)
-    torch.cuda.set_device(local_rank)
+    # one GPU per rank; ranks beyond the visible GPUs share them (a rehearsal of the N > 1
+    # path on a smaller box -- the weak-scaling numbers are only meaningful with one GPU each)
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     # one torch stream per batch context, so that torch events bracket each launch on its own stream
     streams = [torch.cuda.Stream() for _ in range(max(1, args.inflight))]
-    solvers = [BatchTrustRegionSQP(wl, device=local_rank, stream=st.cuda_stream) for st in streams]
+    solvers = [BatchTrustRegionSQP(wl, device=device, stream=st.cuda_stream) for st in streams]
     for s in solvers:
         s.upload()
     solver = solvers[0]
