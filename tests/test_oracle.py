@@ -166,3 +166,21 @@ def test_cartpose_tolerance_golden(oracle_mod, golden):
     np.testing.assert_array_equal(jac, g["jac"])
     inside = (err == 0) & (np.abs(jac).sum(axis=-1) == 0)
     assert inside.sum() > 10 and (err != 0).sum() > 10
+
+
+def test_expr_ops_against_reference_build():
+    """The reference's own trajopt_sco/src/expr_ops.cpp, compiled from where it lies
+    into oracle/_ref (oracle/ref/Makefile), against the oracle's restatement: the same
+    driver prints exprMult / exprSquare / exprInc / exprDec / exprScale results for 200
+    seeded expressions from both; the outputs must be byte-identical."""
+    import subprocess
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    ref, orc = root / "oracle" / "_ref" / "expr_ops_ref", root / "oracle" / "build" / "expr_ops_orc"
+    if not ref.exists():
+        pytest.skip("oracle/_ref not built (/root/reference absent)")
+    a = subprocess.run([str(ref)], capture_output=True, text=True, timeout=60, check=True).stdout
+    b = subprocess.run([str(orc)], capture_output=True, text=True, timeout=60, check=True).stdout
+    assert a.count("\n") == 2200
+    assert a == b
