@@ -191,6 +191,12 @@ typedef struct thip_problem_desc {
   int cart_has_tol[THIP_MAX_CART];
   double cart_lower_tol[THIP_MAX_CART][6];
   double cart_upper_tol[THIP_MAX_CART][6];
+  /* 0: the target frame is the static chain root (the per-problem target offset
+   * is in the root frame).  > 0: DynamicCartPoseTermInfo (problem_description.cpp:
+   * 683-842, kinematic_terms.cpp:58-187): the target is this active chain link,
+   * the per-problem offset is in its frame, and the FD jacobian perturbs both
+   * frames. */
+  int cart_target_link[THIP_MAX_CART];
 
   /* JointPosTermInfo (problem_description.cpp:1097-1196).  Zero tolerances:
    * is_cnt 0 -> JointPosEqCost (quadratic, trajectory_costs.cpp:28-65),

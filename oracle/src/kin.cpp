@@ -151,9 +151,16 @@ void calcTransformError(const Iso3& t1, const Iso3& t2, double err[6])
 
 void calcJacobianTransformErrorDiff(const Iso3& target, const Iso3& source, const Iso3& source_pert, double err[6])
 {
-  const Iso3 ti = inverse(target);
-  const Iso3 pe = mul(ti, source);
-  const Iso3 ppe = mul(ti, source_pert);
+  calcJacobianTransformErrorDiff(target, target, source, source_pert, err);
+}
+
+// the 4-pose form [ext] used by DynamicCartPoseJacCalculator (kinematic_terms.cpp:170-177):
+// both frames perturbed, err2(target_pert^-1 source_pert) - err2(target^-1 source)
+void calcJacobianTransformErrorDiff(const Iso3& target, const Iso3& target_pert, const Iso3& source,
+                                    const Iso3& source_pert, double err[6])
+{
+  const Iso3 pe = mul(inverse(target), source);
+  const Iso3 ppe = mul(inverse(target_pert), source_pert);
   for (int i = 0; i < 3; ++i)
     err[i] = ppe.t[i] - pe.t[i];
   double r0[3], r1[3];
@@ -173,9 +180,15 @@ void calcJacobianTransformErrorDiff(const Iso3& target, const Iso3& source, cons
 void calcJacobianTransformErrorDiffTol(const Iso3& target, const Iso3& source, const Iso3& source_pert,
                                        const double* lower, const double* upper, double err[6])
 {
-  const Iso3 ti = inverse(target);
-  const Iso3 pe = mul(ti, source);
-  const Iso3 ppe = mul(ti, source_pert);
+  calcJacobianTransformErrorDiffTol(target, target, source, source_pert, lower, upper, err);
+}
+
+void calcJacobianTransformErrorDiffTol(const Iso3& target, const Iso3& target_pert, const Iso3& source,
+                                       const Iso3& source_pert, const double* lower, const double* upper,
+                                       double err[6])
+{
+  const Iso3 pe = mul(inverse(target), source);
+  const Iso3 ppe = mul(inverse(target_pert), source_pert);
   double e0[6], e1[6];
   for (int i = 0; i < 3; ++i)
   {

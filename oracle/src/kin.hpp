@@ -65,6 +65,11 @@ void calcJacobianTransformErrorDiff(const Iso3& target, const Iso3& source, cons
 void applyTolerances(double err[6], const double* lower, const double* upper, int n);
 void calcJacobianTransformErrorDiffTol(const Iso3& target, const Iso3& source, const Iso3& source_pert,
                                        const double* lower, const double* upper, double err[6]);
+void calcJacobianTransformErrorDiff(const Iso3& target, const Iso3& target_pert, const Iso3& source,
+                                    const Iso3& source_pert, double err[6]);
+void calcJacobianTransformErrorDiffTol(const Iso3& target, const Iso3& target_pert, const Iso3& source,
+                                       const Iso3& source_pert, const double* lower, const double* upper,
+                                       double err[6]);
 
 // link poses of the chain at q: out[n_links]
 void chainFwdKin(const thip_chain& chain, const double* q, std::vector<Iso3>& out);

@@ -478,6 +478,7 @@ void cartPoseIndices(const thip_problem_desc& d, int term, std::vector<int>& ind
 void setCartPoseTolerances(const thip_problem_desc& d, int term, CartPoseCalc& c)
 {
   c.has_tol = d.cart_has_tol[term] != 0;
+  c.target_link = d.cart_target_link[term];
   for (int i = 0; i < 6; ++i)
   {
     c.lower_tol[i] = d.cart_lower_tol[term][i];
@@ -492,7 +493,7 @@ DblVec CartPoseCalc::operator()(const DblVec& q) const
   std::vector<Iso3> fk;
   chainFwdKin(*chain, q.data(), fk);
   const Iso3 source_tf = mul(fk[static_cast<std::size_t>(source_link)], source_offset);
-  const Iso3 target_tf = mul(fk[0], target_offset);
+  const Iso3 target_tf = mul(fk[static_cast<std::size_t>(target_link)], target_offset);
   double err[6];
   calcTransformError(target_tf, source_tf, err);
   if (has_tol)
@@ -509,7 +510,7 @@ Mat CartPoseCalc::jac(const DblVec& q) const
   std::vector<Iso3> fk;
   chainFwdKin(*chain, q.data(), fk);
   const Iso3 source_tf = mul(fk[static_cast<std::size_t>(source_link)], source_offset);
-  const Iso3 target_tf = mul(fk[0], target_offset);
+  const Iso3 target_tf = mul(fk[static_cast<std::size_t>(target_link)], target_offset);
   Mat J(static_cast<int>(indices.size()), static_cast<int>(q.size()));
   DblVec qp = q;
   for (std::size_t i = 0; i < q.size(); ++i)
@@ -517,11 +518,13 @@ Mat CartPoseCalc::jac(const DblVec& q) const
     qp[i] = q[i] + eps;
     chainFwdKin(*chain, qp.data(), fk);
     const Iso3 sp = mul(fk[static_cast<std::size_t>(source_link)], source_offset);
+    // the static root frame does not move under the perturbation
+    const Iso3 tp = target_link > 0 ? mul(fk[static_cast<std::size_t>(target_link)], target_offset) : target_tf;
     double diff[6];
     if (has_tol)
-      calcJacobianTransformErrorDiffTol(target_tf, source_tf, sp, lower_tol, upper_tol, diff);
+      calcJacobianTransformErrorDiffTol(target_tf, tp, source_tf, sp, lower_tol, upper_tol, diff);
     else
-      calcJacobianTransformErrorDiff(target_tf, source_tf, sp, diff);
+      calcJacobianTransformErrorDiff(target_tf, tp, source_tf, sp, diff);
     for (std::size_t r = 0; r < indices.size(); ++r)
       J(static_cast<int>(r), static_cast<int>(i)) = diff[indices[r]] / eps;
     qp[i] = q[i];

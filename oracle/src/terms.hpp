@@ -40,6 +40,7 @@ struct CartPoseCalc
   Iso3 target_offset;  // target frame = chain root (static)
   std::vector<int> indices;
   bool has_tol = false;  // tolerance band (kinematic_terms.cpp:209-247, 319-339)
+  int target_link = 0;   // > 0: DynamicCartPose, the target is this active link (kinematic_terms.cpp:58-187)
   double lower_tol[6] = {}, upper_tol[6] = {};
   DblVec operator()(const DblVec& q) const;  // error
   Mat jac(const DblVec& q) const;            // forward-difference jacobian, eps = 1e-5

@@ -180,3 +180,17 @@ def test_joint_vel_tolerance_terms_lower_to_hinge_terms():
     assert d.n_jvx == 2
     assert (d.jvx_is_cnt[0], d.jvx_first_step[0], d.jvx_last_step[0]) == (0, 3, 4)
     assert (d.jvx_is_cnt[1], d.jvx_lower_tols[1][3], d.jvx_upper_tols[1][6]) == (1, -0.1, 0.2)
+
+
+def test_dynamic_cart_pose_lowering():
+    """DynamicCartPoseTermInfo (problem_description.cpp:683-842): both frames active; the
+    target link and its raw offset go to the descriptor; a static frame is rejected."""
+    term = {"type": "dynamic_cart_pose", "params": {"timestep": 3, "source_frame": "r_gripper_tool_frame",
+                                                     "target_frame": "r_upper_arm_roll_link",
+                                                     "target_frame_offset_xyz": [0.3, 0.0, 0.1]}}
+    d, _, tgt, _ = host.lower_json(_doc(costs=[term]))
+    assert d.n_cart == 1 and d.cart_target_link[0] > 0 and d.cart_source_link[0] > d.cart_target_link[0]
+    np.testing.assert_allclose(np.asarray(tgt).reshape(-1)[[3, 7, 11]], [0.3, 0.0, 0.1], atol=1e-15)
+    term["params"]["target_frame"] = "torso_lift_link"
+    with pytest.raises(host.HostError, match="are not both active links"):
+        host.lower_json(_doc(costs=[term]))

@@ -196,6 +196,23 @@ def test_cartpose_linearization_parity_tolerance(oracle_mod, cfg):
     np.testing.assert_allclose(jac, jo, rtol=0, atol=1e-9)
 
 
+def test_cartpose_linearization_parity_dynamic(oracle_mod):
+    """DynamicCartPose rows (both frames active, kinematic_terms.cpp:58-187): the
+    target is an arm link, the FD jacobian perturbs both frames."""
+    wl = problems.with_dynamic_target(problems.make_workload("B", 16))
+    rng = np.random.default_rng(13)
+    x = wl.init + rng.normal(0, 0.05, wl.init.shape)
+    s = BatchTrustRegionSQP(wl)
+    err, jac = s.linearize(x)
+    s.close()
+    eo, jo = oracle_mod.linearize(wl, x)
+    assert np.abs(eo).max() > 1e-3
+    # columns of joints upstream of the target link move both frames alike: zero there
+    assert np.abs(jo[..., :2]).max() < 1e-6
+    np.testing.assert_allclose(err, eo, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(jac, jo, rtol=0, atol=1e-9)
+
+
 def test_cartpose_linearization_golden_tolerance(golden):
     g = golden("cartpose_B_tol")
     wl = problems.with_cart_tolerances(problems.make_workload("B", g["x"].shape[0]))
@@ -561,6 +578,12 @@ def _variant(name):
             d.jvx_coeffs[1][j], d.jvx_targets[1][j] = 0.5, 0.02
             d.jvx_lower_tols[1][j], d.jvx_upper_tols[1][j] = -0.01, 0.01
         return wl
+    if name == "dynamic_cartpose_costs":
+        return problems.with_dynamic_target(problems.make_workload("B", 16, first_problem=70))
+    if name == "dynamic_cartpose_cnt_with_collision":
+        wl = problems.with_dynamic_target(problems.make_workload("C", 8, first_problem=70))
+        wl.desc.cart_is_cnt[5] = 1
+        return wl
     if name == "single_problem":
         return problems.make_workload("B", 1, first_problem=5)
     # other chains: 8 DoF with the prismatic torso_lift_joint first, and 6 DoF
@@ -589,7 +612,8 @@ VARIANTS = ["jointvel_only", "short_horizon", "two_fixed_steps", "position_only_
             "torso_arm_8dof_A", "torso_arm_8dof_B", "torso_arm_8dof_C", "torso_arm_8dof_jointpos", "arm_6dof_A",
             "arm_6dof_C", "discrete_fixed_both_ends_subrange", "discrete_two_waypoints",
             "discrete_with_static_hinges_8dof", "cartpose_tolerance_cost", "cartpose_tolerance_cnt",
-            "cartpose_tolerance_collision", "continuous_50_waypoints", "jointvel_cnt_band_with_cartpose"]
+            "cartpose_tolerance_collision", "continuous_50_waypoints", "jointvel_cnt_band_with_cartpose",
+            "dynamic_cartpose_costs", "dynamic_cartpose_cnt_with_collision"]
 
 
 @pytest.mark.parametrize("name", VARIANTS)

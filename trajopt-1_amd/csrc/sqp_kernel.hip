@@ -218,8 +218,12 @@ __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
     pose_load(So, c.d->cart_source_offset[k]);
     Pose Ss;
     pose_mul(S, So, Ss);
-    pose_load(Tb, ch.base_pose);
     pose_load(To, tgt + 12 * k);
+    const int tl = c.d->cart_target_link[k];
+    if (tl > 0)
+      chain_fk(ch, x + t * D, tl, Tb);  // DynamicCartPose: the active target link
+    else
+      pose_load(Tb, ch.base_pose);
     pose_mul(Tb, To, Tt);
     pose_inv(Tt, Ti);
     double* st = stage + 30 * k;
@@ -265,10 +269,22 @@ __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
       Ss.t[i] = st[9 + i];
       Ti.t[i] = st[21 + i];
     }
-    // calcJacobianTransformErrorDiff(target, source, source_perturbed)
+    // calcJacobianTransformErrorDiff(target, source, source_perturbed); DynamicCartPose:
+    // (target, target_perturbed, source, source_perturbed), kinematic_terms.cpp:170-177
     Pose pe, ppe;
     pose_mul(Ti, Ss, pe);
-    pose_mul(Ti, Sp, ppe);
+    const int tl = c.d->cart_target_link[k];
+    if (tl > 0)
+    {
+      Pose Tq, To, Tp, Tpi;
+      chain_fk(ch, q, tl, Tq);
+      pose_load(To, c.a(A_TGT) + 12 * k);
+      pose_mul(Tq, To, Tp);
+      pose_inv(Tp, Tpi);
+      pose_mul(Tpi, Sp, ppe);
+    }
+    else
+      pose_mul(Ti, Sp, ppe);
     double diff[6];
     if (c.d->cart_has_tol[k])
       transform_error_diff_tol(pe, ppe, c.d->cart_lower_tol[k], c.d->cart_upper_tol[k], diff);
@@ -1120,8 +1136,11 @@ __device__ void evaluate(Ctx& c, const double* x, double* costs, double* viols)
     chain_fk(ch, x + t * D, c.d->cart_source_link[k], S);
     pose_load(So, c.d->cart_source_offset[k]);
     pose_mul(S, So, Ss);
-    pose_load(Tb, ch.base_pose);
     pose_load(To, tgt + 12 * k);
+    if (c.d->cart_target_link[k] > 0)
+      chain_fk(ch, x + t * D, c.d->cart_target_link[k], Tb);  // DynamicCartPose
+    else
+      pose_load(Tb, ch.base_pose);
     pose_mul(Tb, To, Tt);
     pose_inv(Tt, Ti);
     double err[6];

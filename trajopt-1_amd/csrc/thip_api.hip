@@ -154,6 +154,8 @@ static int validate(const thip_problem_desc* d, std::string& why)
       return why = "CartPose timestep out of range", THIP_E_INVALID;
     if (d->cart_source_link[k] <= 0 || d->cart_source_link[k] >= ch.n_links)
       return why = "CartPose source frame must be an active chain link", THIP_E_INVALID;
+    if (d->cart_target_link[k] < 0 || d->cart_target_link[k] >= ch.n_links)
+      return why = "CartPose target link out of range (0: the static chain root)", THIP_E_INVALID;
   }
   if (d->n_jvx < 0 || d->n_jvx > THIP_MAX_JVX)
     return why = "n_jvx out of range", THIP_E_INVALID;

@@ -246,6 +246,17 @@ struct CartPoseTermInfo : public TermInfo
   void fromJson(ProblemConstructionInfo& pci, const Json::Value& v) override;
   void hatch(TrajOptProb& prob) override;
   static TermInfo::Ptr create() { return std::make_shared<CartPoseTermInfo>(); }
+
+protected:
+  bool dynamic_ = false;  // DynamicCartPoseTermInfo: both frames active
+};
+
+// problem_description.cpp:683-842: source and target both active links at one timestep
+// (DynamicCartPoseErrCalculator / DynamicCartPoseJacCalculator, kinematic_terms.cpp:58-187)
+struct DynamicCartPoseTermInfo : public CartPoseTermInfo
+{
+  DynamicCartPoseTermInfo() { dynamic_ = true; }
+  static TermInfo::Ptr create() { return std::make_shared<DynamicCartPoseTermInfo>(); }
 };
 
 // CollisionTermInfo (problem_description.cpp:1636-1858) with the

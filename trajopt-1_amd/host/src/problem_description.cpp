@@ -71,7 +71,6 @@ trajopt::TermInfo::Ptr makeUnsupported()
 {
   return std::make_shared<UnsupportedTermInfo>(kName);
 }
-constexpr char kDynCart[] = "dynamic_cart_pose";
 constexpr char kCartVel[] = "cart_vel";
 constexpr char kJointAcc[] = "joint_acc";
 constexpr char kJointJerk[] = "joint_jerk";
@@ -81,7 +80,7 @@ constexpr char kTotalTime[] = "total_time";
 void RegisterMakers()
 {
   gRegisteredMakers = true;  // first: RegisterMaker() below checks it
-  trajopt::TermInfo::RegisterMaker("dynamic_cart_pose", &makeUnsupported<kDynCart>);
+  trajopt::TermInfo::RegisterMaker("dynamic_cart_pose", &trajopt::DynamicCartPoseTermInfo::create);
   trajopt::TermInfo::RegisterMaker("cart_pose", &trajopt::CartPoseTermInfo::create);
   trajopt::TermInfo::RegisterMaker("cart_vel", &makeUnsupported<kCartVel>);
   trajopt::TermInfo::RegisterMaker("joint_pos", &trajopt::JointPosTermInfo::create);
@@ -588,9 +587,15 @@ void CartPoseTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value&
     throw std::runtime_error("invalid target frame: " + target_frame);
   const bool source_active = pci.kin->isActiveLinkId(source_frame);
   const bool target_active = pci.kin->isActiveLinkId(target_frame);
-  if (source_active && target_active)
+  if (dynamic_)
+  {
+    if (!(source_active && target_active))
+      throw std::runtime_error("source '" + source_frame + "' and target '" + target_frame +
+                               "' are not both active links");
+  }
+  else if (source_active && target_active)
     throw std::runtime_error("source '" + source_frame + "' and target '" + target_frame + "' are both active");
-  if (!source_active && !target_active)
+  else if (!source_active && !target_active)
     throw std::runtime_error("source '" + source_frame + "' and target '" + target_frame + "' are both static");
   const char* all_fields[] = { "timestep",
                                "pos_coeffs",
@@ -617,8 +622,8 @@ void CartPoseTermInfo::hatch(TrajOptProb& prob)
   // is_target_active_ (kinematic_terms.cpp:206, 213-247, 313-339): the error is
   // calcTransformError(static, active) and the jacobian perturbs the active frame either way,
   // so an active target lowers as the kernel's active frame with the source as the static one
-  const bool target_active = kin->isActiveLinkId(target_frame);
-  if (target_active == kin->isActiveLinkId(source_frame))
+  const bool target_active = kin->isActiveLinkId(target_frame) && !dynamic_;
+  if (!dynamic_ && target_active == kin->isActiveLinkId(source_frame))
     throw std::runtime_error("CartPoseTermInfo: source and target frames are both " +
                              std::string(target_active ? "active" : "static"));
   const std::string& active_frame = target_active ? target_frame : source_frame;
@@ -661,6 +666,8 @@ void CartPoseTermInfo::hatch(TrajOptProb& prob)
   }
   d.cart_is_cnt[k] = any(term_type & TermType::TT_COST) ? 0 : 1;
   d.cart_source_link[k] = kin->linkIndex(active_frame);
+  // DynamicCartPose: the target is an active link and its offset stays in that link's frame
+  d.cart_target_link[k] = dynamic_ ? kin->linkIndex(target_frame) : 0;
   for (int i = 0; i < 12; ++i)
     d.cart_source_offset[k][i] = active_offset[static_cast<std::size_t>(i)];
   for (int i = 0; i < 3; ++i)
@@ -671,7 +678,7 @@ void CartPoseTermInfo::hatch(TrajOptProb& prob)
   // per-problem static frame pose: the offset in the chain root frame (the kernel forms
   // base_pose * offset)
   Pose12 off = static_offset;
-  if (kin->linkIndex(static_frame) != 0)
+  if (!dynamic_ && kin->linkIndex(static_frame) != 0)
   {
     Pose12 base;
     std::copy(kin->chain.base_pose, kin->chain.base_pose + 12, base.begin());

@@ -114,6 +114,7 @@ class ProblemDesc(C.Structure):
         ("cart_has_tol", C.c_int * MAX_CART),
         ("cart_lower_tol", (C.c_double * 6) * MAX_CART),
         ("cart_upper_tol", (C.c_double * 6) * MAX_CART),
+        ("cart_target_link", C.c_int * MAX_CART),
         ("n_jpos", C.c_int),
         ("jpos_is_cnt", C.c_int * MAX_JPOS),
         ("jpos_first_step", C.c_int * MAX_JPOS),

@@ -34,7 +34,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import abi
-from .robots import PR2_TOOL_LINK, ROBOTS, chain_limits, fwd_kin
+from .robots import PR2_TOOL_LINK, ROBOTS, _to44, chain_limits, fwd_kin
 
 SEED_BASE = 20261015
 _MASK = (1 << 64) - 1
@@ -287,4 +287,22 @@ def with_cart_tolerances(wl, pos=0.02, rot=0.1, axes=range(6)):
             b = (pos if i < 3 else rot) if i in axes else 0.0
             d.cart_lower_tol[k][i] = -b
             d.cart_upper_tol[k][i] = b
+    return wl
+
+
+def with_dynamic_target(wl, link=3):
+    """Make every CartPose term of wl a DynamicCartPose term (both frames active,
+    DynamicCartPoseTermInfo, problem_description.cpp:683-842): the target is chain link
+    `link`, and each problem's target offset (in that link's frame) is the source
+    frame's pose relative to it along the problem's reference path, so the term holds
+    the tool at a fixed pose relative to the arm link."""
+    d = wl.desc
+    for k in range(d.n_cart):
+        d.cart_target_link[k] = link
+    for b in range(wl.batch):
+        for k in range(d.n_cart):
+            T = fwd_kin(d.chain, wl.q_ref[b, d.cart_step[k]])
+            src = T[d.cart_source_link[k]] @ _to44(list(d.cart_source_offset[k]))
+            rel = np.linalg.inv(T[link]) @ src
+            wl.targets[b, k] = rel[:3, :].reshape(12)
     return wl
