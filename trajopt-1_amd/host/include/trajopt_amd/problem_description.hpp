@@ -9,8 +9,8 @@
 //    TrajOptProb, instead of pushing sco::Cost objects; BatchTrustRegionSQP
 //    (batch_sqp.hpp) then solves many TrajOptProbs that share one structure.
 //  * The registered term types are the ones on the HIP path: joint_pos,
-//    joint_vel, cart_pose, collision.  The reference's other makers
-//    (dynamic_cart_pose, cart_vel, joint_acc, joint_jerk, total_time,
+//    joint_vel, cart_pose, dynamic_cart_pose, collision.  The reference's other
+//    makers (cart_vel, joint_acc, joint_jerk, total_time,
 //    problem_description.cpp:57-70) are registered too, and their hatch()
 //    throws "not supported on the HIP path" so a JSON that uses them fails
 //    loudly rather than silently dropping a term.
