@@ -62,6 +62,10 @@ def _doc(**over):
     return json.dumps(d)
 
 
+def _coll_pairs(pairs):
+    return {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 2, "pairs": pairs}
+
+
 @pytest.mark.parametrize(
     "text, needle",
     [
@@ -95,12 +99,37 @@ def _doc(**over):
         (_doc(init_info={"type": "given_traj", "data": [[0] * 7] * 4}), "given initialization traj has wrong length"),
         (_doc(init_info={"type": "bogus"}), "init_info did not have a valid type"),
         (_doc(basic_info={"n_steps": 5, "manip": "right_arm", "use_time": True}), "use_time"),
+        (_doc(costs=[{"type": "collision", "params": _coll_pairs([{"pair": ["table"]}])}]),
+         'expected true: it->isMember("link")'),
+        (_doc(costs=[{"type": "collision", "params": _coll_pairs([{"link": "r_forearm_link"}])}]),
+         'expected true: it->isMember("pair")'),
+        (_doc(costs=[{"type": "collision", "params": _coll_pairs([{"link": "r_forearm_link", "pair": []}])}]),
+         "wrong size: pair. expected > 0 got 0"),
+        (_doc(costs=[{"type": "collision", "params": _coll_pairs([{"link": "r_forearm_link", "pair": ["table"],
+                                                                    "dist_pen": 0.025}])}]),
+         "missing field: coeffs"),
+        (_doc(costs=[{"type": "collision", "params": _coll_pairs([{"link": "r_forearm_link", "pair": ["table"],
+                                                                    "coeffs": 10, "dist_pen": 0.025}])}]),
+         "per link-pair collision margins / coeffs (\"pairs\") that differ from the term's is not supported"),
     ],
 )
 def test_json_errors_match_reference(text, needle):
     with pytest.raises(host.HostError) as ei:
         host.lower_json(text)
     assert needle in str(ei.value), str(ei.value)
+
+
+def test_uniform_pairs_lower_to_the_term():
+    """A "pairs" override (problem_description.cpp:1686-1719) equal to the
+    term's coeffs / dist_pen changes no pair's margin or coefficient, so the
+    problem lowers exactly as without it."""
+    base = _doc(costs=[{"type": "collision", "params": {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 2}}])
+    same = _doc(costs=[{"type": "collision", "params": _coll_pairs(
+        [{"link": "r_forearm_link", "pair": ["table", "box"], "coeffs": 20, "dist_pen": 0.025}])}])
+    d0, i0, _, _ = host.lower_json(base)
+    d1, i1, _, _ = host.lower_json(same)
+    assert bytes(d0) == bytes(d1)
+    np.testing.assert_array_equal(i0, i1)
 
 
 def test_init_info_types():

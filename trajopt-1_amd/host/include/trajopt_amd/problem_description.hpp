@@ -271,7 +271,7 @@ struct CollisionTermInfo : public TermInfo
   double collision_margin_buffer = 0.5;
   double coeff = 20;             // CollisionCoeffData default
   double dist_pen = 0;           // collision margin
-  bool has_pairs = false;        // per link-pair margins / coeffs ("pairs")
+  bool has_pairs = false;        // a "pairs" override differing from coeff / dist_pen
   CollisionTermInfo() : TermInfo(TermType::TT_COST | TermType::TT_CNT) {}
   void fromJson(ProblemConstructionInfo& pci, const Json::Value& v) override;
   void hatch(TrajOptProb& prob) override;

@@ -714,7 +714,32 @@ void CollisionTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value
     throw std::runtime_error("CollisionTermInfo: invalid contact_test_type");
   json_marshal::childFromJson(params, coeff, "coeffs");
   json_marshal::childFromJson(params, dist_pen, "dist_pen");
-  has_pairs = params.isMember("pairs");
+  // problem_description.cpp:1686-1719: per link-pair overrides, validated as the reference does.
+  // An override equal to the term's own coeffs / dist_pen leaves every pair's margin and
+  // coefficient unchanged (CollisionCoeffData / CollisionMarginData defaults), so it lowers to
+  // the term-wide values; a differing one is refused in hatch().
+  has_pairs = false;
+  if (params.isMember("pairs"))
+  {
+    for (const Json::Value& it : params["pairs"])
+    {
+      if (!it.isMember("link"))
+        throw std::runtime_error("expected true: it->isMember(\"link\")");
+      std::string link;
+      json_marshal::childFromJson(it, link, "link");
+      if (!it.isMember("pair"))
+        throw std::runtime_error("expected true: it->isMember(\"pair\")");
+      std::vector<std::string> pair;
+      json_marshal::childFromJson(it, pair, "pair");
+      if (pair.empty())
+        throw std::runtime_error("wrong size: pair. expected > 0 got " + std::to_string(pair.size()));
+      double pair_coeffs = 20, pair_dist_pen = 0;
+      json_marshal::childFromJson(it, pair_coeffs, "coeffs");
+      json_marshal::childFromJson(it, pair_dist_pen, "dist_pen");
+      if (pair_coeffs != coeff || pair_dist_pen != dist_pen)
+        has_pairs = true;
+    }
+  }
   const char* all_fields[] = { "type",           "first_step",        "last_step",
                                "evaluator_type", "fixed_steps",       "contact_test_type",
                                "longest_valid_segment_length", "coeffs", "dist_pen", "pairs" };
@@ -732,7 +757,7 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
   if (contact_test_type != 2)
     unsupported("collision contact_test_type " + std::to_string(contact_test_type) + " (only ALL = 2)");
   if (has_pairs)
-    unsupported("per link-pair collision margins / coeffs (\"pairs\")");
+    unsupported("per link-pair collision margins / coeffs (\"pairs\") that differ from the term's");
   const auto env = prob.GetEnv();
   thip_problem_desc& d = prob.desc();
   if (d.coll_enabled)
