@@ -11,7 +11,7 @@ cost against a 10-primitive scene, 1024 problems per GPU.  `value` is SQP
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 1024]
 
-Batches in flight: the runtime keeps `--inflight` (default 2) batch contexts,
+Batches in flight: the runtime keeps `--inflight` (default 3) batch contexts,
 each with its own HIP stream, and submits step k to context k mod inflight,
 so the next batch's problems fill the CUs that the current batch's last
 (longest) problems leave idle.  Every step still solves a full batch of
@@ -127,7 +127,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1024, help="problems per GPU")
     ap.add_argument("--config", default="C")
-    ap.add_argument("--inflight", type=int, default=2, help="batch contexts (streams) in flight")
+    ap.add_argument("--inflight", type=int, default=3, help="batch contexts (streams) in flight")
     ap.add_argument("--cpu-problems", type=int, default=256)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")

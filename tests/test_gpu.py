@@ -732,7 +732,7 @@ def test_bench_json_line():
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in line, k
     assert line["value"] > 0 and line["n_gpus"] == 1 and line["dtype"] == "f64"
-    assert line["config"]["batches_in_flight"] == 2 and line["config"]["batch_latency_ms"] > 0
+    assert line["config"]["batches_in_flight"] == 3 and line["config"]["batch_latency_ms"] > 0
     rf = line["roofline"]
     assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and 0 < rf["frac"] == pytest.approx(rf["achieved"] / 8000.0)
     cb = line["cpu_baseline"]
