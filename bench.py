@@ -26,7 +26,10 @@ reported.
 Extra JSON objects:
   roofline      algorithmic HBM bytes of sqp_kernel (SURVEY.md §8d B_iter
                 model, counters read back from the device) / its HIP-event
-                duration, against the 8 TB/s HBM3E peak.
+                duration, against the 8 TB/s HBM3E peak; beside it the same
+                bytes over the timed region (achieved_per_step_gbs), the
+                PMC-measured traffic rate (measured_gbs) and what actually
+                limits the kernel (limiter).
   cpu_baseline  the oracle's CPU restatement (oracle/, "port") on a bounded
                 sample of the same problems, rank 0 at N=1 only.
 """
@@ -166,8 +169,14 @@ def main():
         for s in solvers:
             s.run()
     res = solver.download()[1] if args.warmup > 0 else None
-    # one batch alone (no other batch in flight): the per-batch latency
+    # one batch alone (no other batch in flight): the per-batch latency.  Every
+    # context's warmup launches must have drained first, else this launch shares
+    # the CUs with their tails
+    for s in solvers:
+        s.sync()
+    torch.cuda.synchronize()
     solver.run()
+    solver.sync()
     batch_latency_ms = solver.kernel_ms()
 
     def barrier():
@@ -213,6 +222,9 @@ def main():
     if rank == 0:
         value = iters_total * args.steps / elapsed
         achieved = bytes_local / (kms * 1e-3) / 1e9
+        # the same bytes over the whole timed region (all batches in flight
+        # together), and the PMC-measured HBM traffic over the launch duration
+        aggregate = bytes_local * args.steps / elapsed / 1e9  # rank 0's GPU
         wname = workload_name(wl, args.config, args.batch)
         traffic, traffic_src = measured_traffic(wname, args.batch)
         out = {
@@ -248,6 +260,11 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "measured_gbs": (traffic / (kms * 1e-3) / 1e9) if traffic else None,
+                "achieved_per_step_gbs": aggregate,
+                "limiter": "latency (serial block-tridiagonal KKT chain per ADMM iteration, one problem per CU); "
+                           "`achieved` is the SURVEY.md 8d streaming-byte model, measured HBM traffic is "
+                           "`measured_gbs` (working set LDS/register resident)",
                 "kernel_ms": kms,
                 "algorithmic_bytes_per_launch": bytes_local,
                 "model": model,

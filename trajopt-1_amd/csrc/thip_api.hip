@@ -745,17 +745,25 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     if ((e = hipMemcpy(ctx->d_jpt, jpt.data(), jpt.size() * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
       return fail(std::string("hipMemcpy(jpos targets): ") + hipGetErrorString(e));
   }
-  hipMemset(ctx->d_iws, 0, B * static_cast<size_t>(L.istride) * sizeof(int));
-  hipMemset(ctx->d_res, 0, B * sizeof(thip_result));
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
     return fail(std::string("hipStreamCreate: ") + hipGetErrorString(e));
   ctx->own_stream = true;
-  hipEventCreate(&ctx->ev0);
-  hipEventCreate(&ctx->ev1);
-  hipFuncSetAttribute(reinterpret_cast<const void*>(&sqp_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                      static_cast<int>(ctx->lds_bytes));
-  hipFuncSetAttribute(reinterpret_cast<const void*>(&linearize_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                      static_cast<int>(ctx->lds_lin_bytes));
+  // zeroed on the context's own (non-blocking) stream and waited for here: a
+  // non-blocking stream does not order against the null stream, and the
+  // caller may swap in its own stream (thip_set_stream) before the first run
+  if ((e = hipMemsetAsync(ctx->d_iws, 0, B * static_cast<size_t>(L.istride) * sizeof(int), ctx->stream)) !=
+          hipSuccess ||
+      (e = hipMemsetAsync(ctx->d_res, 0, B * sizeof(thip_result), ctx->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
+    return fail(std::string("hipMemsetAsync(workspace): ") + hipGetErrorString(e));
+  if ((e = hipEventCreate(&ctx->ev0)) != hipSuccess || (e = hipEventCreate(&ctx->ev1)) != hipSuccess)
+    return fail(std::string("hipEventCreate: ") + hipGetErrorString(e));
+  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sqp_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               static_cast<int>(ctx->lds_bytes))) != hipSuccess ||
+      (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&linearize_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ctx->lds_lin_bytes))) !=
+          hipSuccess)
+    return fail(std::string("hipFuncSetAttribute(dynamic LDS): ") + hipGetErrorString(e));
   *out = ctx;
   return THIP_OK;
 }
@@ -1010,7 +1018,10 @@ int thip_debug_trace(thip_ctx* ctx, int capacity)
   const size_t B = static_cast<size_t>(ctx->batch);
   HIPCHK(ctx, hipMalloc(&ctx->d_trace, B * static_cast<size_t>(capacity) * THIP_TRACE_W * sizeof(double)));
   HIPCHK(ctx, hipMalloc(&ctx->d_trace_n, B * sizeof(int)));
-  HIPCHK(ctx, hipMemset(ctx->d_trace_n, 0, B * sizeof(int)));
+  // ordered with the runs on the context's stream (non-blocking: the null
+  // stream would not order against it)
+  HIPCHK(ctx, hipMemsetAsync(ctx->d_trace_n, 0, B * sizeof(int), ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return THIP_OK;
 }
 
@@ -1099,7 +1110,8 @@ int thip_debug_profile(thip_ctx* ctx, int enable)
     return THIP_OK;
   const size_t n = static_cast<size_t>(ctx->batch) * kProfSlots;
   HIPCHK(ctx, hipMalloc(&ctx->d_prof, n * sizeof(long long)));
-  HIPCHK(ctx, hipMemset(ctx->d_prof, 0, n * sizeof(long long)));
+  HIPCHK(ctx, hipMemsetAsync(ctx->d_prof, 0, n * sizeof(long long), ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return THIP_OK;
 }
 

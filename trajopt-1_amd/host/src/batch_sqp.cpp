@@ -1,6 +1,7 @@
 #include "trajopt_amd/batch_sqp.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -117,6 +118,10 @@ std::vector<std::vector<double>> BatchTrustRegionSQP::trace() const
   {
     const auto* p = rec.data() + b * static_cast<std::size_t>(trace_cap_) * W;
     out[b].assign(p, p + static_cast<std::size_t>(std::min(cnt[b], trace_cap_)) * W);
+    // the device counts every record, also those past the capacity
+    if (cnt[b] > trace_cap_)
+      std::fprintf(stderr, "BatchTrustRegionSQP: trace of problem %zu truncated: %d of %d QP records kept\n", b,
+                   trace_cap_, cnt[b]);
   }
   return out;
 }
@@ -229,7 +234,17 @@ sco::OptStatus BasicTrustRegionSQP::optimize()
   }
   BatchTrustRegionSQP batch({ p }, device_);
   if (param_.log_results)
-    batch.enableTrace(8192);
+  {
+    // one record per QP solve: at most (penalty rounds) x (SQP iterations) x
+    // (trust-region tries per iteration); the box shrinks by trust_shrink_ratio
+    // per rejected try from at most trust_box_size * expand^max_iter down to
+    // min_trust_box_size
+    const double grow = param_.max_iter * std::log(std::max(param_.trust_expand_ratio, 1.0));
+    const double span = std::log(param_.trust_box_size / param_.min_trust_box_size) + grow;
+    const double tries = 2.0 + std::max(0.0, span / std::log(1.0 / param_.trust_shrink_ratio));
+    const double bound = (param_.max_merit_coeff_increases + 1.0) * param_.max_iter * tries;
+    batch.enableTrace(static_cast<int>(std::min(std::max(bound, 64.0), 1.0e6)));
+  }
   results_ = batch.optimize()[0];
   if (param_.log_results)
     writeSolverLog(param_.log_dir + "/trajopt_solver.log", batch.trace()[0]);

@@ -1,6 +1,7 @@
 // Minimal JSON parser / DOM (see json.hpp).
 #include "trajopt_amd/json.hpp"
 
+#include <charconv>
 #include <cmath>
 #include <cstdlib>
 #include <fstream>
@@ -115,16 +116,50 @@ private:
     fail(std::string("unexpected character '") + c + "'");
   }
 
+  // JSON number grammar (RFC 8259 6): -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?
+  // scanned first (jsoncpp rejects hex floats, "inf", ".5", "1."), then
+  // converted by std::from_chars, which ignores the C locale (strtod would
+  // read "0.5" as 0 under a comma-decimal LC_NUMERIC)
   Value number()
   {
-    const char* begin = s_.c_str() + pos_;
-    char* end = nullptr;
-    const double d = std::strtod(begin, &end);
-    if (end == begin)
+    const std::size_t start = pos_;
+    auto digit = [&](std::size_t p) { return p < s_.size() && s_[p] >= '0' && s_[p] <= '9'; };
+    std::size_t p = pos_;
+    if (p < s_.size() && s_[p] == '-')
+      ++p;
+    if (!digit(p))
       fail("invalid number");
-    pos_ += static_cast<std::size_t>(end - begin);
-    if (!std::isfinite(d))
+    if (s_[p] == '0')
+      ++p;
+    else
+      while (digit(p))
+        ++p;
+    if (p < s_.size() && s_[p] == '.')
+    {
+      ++p;
+      if (!digit(p))
+        fail("invalid number");
+      while (digit(p))
+        ++p;
+    }
+    if (p < s_.size() && (s_[p] == 'e' || s_[p] == 'E'))
+    {
+      ++p;
+      if (p < s_.size() && (s_[p] == '+' || s_[p] == '-'))
+        ++p;
+      if (!digit(p))
+        fail("invalid number");
+      while (digit(p))
+        ++p;
+    }
+    double d = 0.0;
+    const char* first = s_.data() + start;
+    const auto r = std::from_chars(first, s_.data() + p, d);
+    if (r.ec == std::errc::result_out_of_range || !std::isfinite(d))
       fail("number out of range");
+    if (r.ec != std::errc() || r.ptr != s_.data() + p)
+      fail("invalid number");
+    pos_ = p;
     return Value(d);
   }
 
