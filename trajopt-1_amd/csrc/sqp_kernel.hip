@@ -1672,15 +1672,15 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
       wave_sync();
       chol_inv_block(S, LI + t * DD, D, c.lane, bad);
       const double* Li = LI + t * DD;
-      if (k > 0)
-        for (int e = c.lane; e < DD; e += 64)
-        {
-          const int i = e / D, j = e % D;
-          double v = 0;
+      for (int e = c.lane; e < DD; e += 64)
+      {
+        const int i = e / D, j = e % D;
+        double v = 0;
+        if (k > 0)  // the half's first block has no coupling: zero (the segment's chain reads it)
           for (int q = 0; q <= i; ++q)
             v += Li[i * D + q] * Ls[q * D + j];
-          sv.M[t * DD + e] = v;
-        }
+        sv.M[t * DD + e] = v;
+      }
       wave_sync();
       if (!L.hinge)
         for (int e = c.lane; e < DD; e += 64)
@@ -2574,6 +2574,195 @@ __device__ void admm_step(Ctx& c, Solver& sv)
 // of admm_step() + reduced_solve(), so both paths give identical iterates.
 // State is written back to A_XA0/A_Z0/A_Y/A_DX/A_DY at the end of the segment
 // for the residual / termination / rho-update / polish code.
+// ---- fused twisted solve of the ADMM segment ------------------------------
+// K x = b with the twisted block factor (factor()), one pass per half on the
+// two chain waves, the factor's blocks in registers for the whole segment:
+//   forward   y_t = LI_t b_t - M_t y_{t-1}     (top half; bottom: y_{t+1})
+//   middle    y_m = LI_m b_m - M_m y_{m-1} - M'_m y_{m+1},  x_m = LI_m^T y_m
+//   backward  x_t = LI_t^T y_t - N_t x_{t+1}   (top half; bottom: x_{t-1})
+// Each step is one lane-level fma and one 3-level reduction: lane (i, k) =
+// (lane >> 3, lane & 7) holds one block element, the LI_t b_t and LI_t^T y_t
+// terms enter the same reduction as the chain term (computed off the serial
+// path), and the vector alternates between ROW layout (v[i] in octet i, from
+// octet_sum) and COL layout (v[k] at lane & 7 = k, from cross_octet_sum), so
+// no lane permutation sits on the serial path.  Steps of a half are indexed by
+// r = distance from the middle (t = m - 1 - r on wave 0, m + 1 + r on wave
+// 1): forward outputs are COL at even r, ROW at odd r; backward outputs the
+// opposite, which is the layout the forward pass left y_t in; the middle
+// reads y_{m-1}, y_{m+1}, b_m in COL layout, so both waves compute it
+// identically.  This replaces reduced_solve's four barrier-separated passes
+// (LI b, forward chain, LI^T y + middle, backward chain) by two.
+constexpr int kSegHalf = THIP_MAX_STEPS / 4;  // steps per half: N <= 32 on the segment
+static_assert(kSegHalf * 2 * 8 >= kBlock, "segment halves cover N <= 32");
+constexpr int kSegChunk = 8;  // blocks streamed from LDS per wait
+
+// Per-lane LDS addresses of the chain's block elements, fixed for a segment:
+// element (i, k) (ROW-output steps) or (k, i) (COL-output steps) of the block
+// at step r is at base + r * stride; lanes outside the D x D block read a zero.
+struct SegChain
+{
+  unsigned li_n, li_t, mf_n, mf_t, nb_n, nb_t;  // LDS byte addresses at r = 0
+  int stride;                                   // bytes per step (the block stride, signed by the half)
+  double mli, mm, mnb;                          // LI_m, M_m, M'_m elements (ROW output)
+  int R;                                        // steps in this wave's half (0 off the chain waves)
+};
+
+__device__ __forceinline__ unsigned lds_addr(const double* p)
+{
+  return (unsigned)(unsigned long)lds(p);
+}
+
+__device__ __forceinline__ void seg_chain_init(const Ctx& c, const Solver& sv, const double* zero, SegChain& ch)
+{
+  const int D = c.L.D, DD = D * D, N = c.L.N, m = c.L.tw_mid;
+  const int i = c.lane >> 3, k = c.lane & 7;
+  const bool act = (i < D) && (k < D);
+  const int offN = i * D + k, offT = k * D + i;
+  ch.R = (c.wave == 0) ? m : (c.wave == 1 ? N - 1 - m : 0);
+  const int t0 = (c.wave == 0) ? m - 1 : m + 1;  // r = 0
+  const int tdir = (c.wave == 0) ? -1 : 1;
+  ch.stride = act ? tdir * DD * 8 : 0;
+  const unsigned z = lds_addr(zero);
+  const unsigned li = lds_addr(c.a(A_LINV) + t0 * DD), mf = lds_addr(sv.M + t0 * DD), nb = lds_addr(sv.Nb + t0 * DD);
+  ch.li_n = act ? li + offN * 8 : z;
+  ch.li_t = act ? li + offT * 8 : z;
+  ch.mf_n = act ? mf + offN * 8 : z;
+  ch.mf_t = act ? mf + offT * 8 : z;
+  ch.nb_n = act ? nb + offN * 8 : z;
+  ch.nb_t = act ? nb + offT * 8 : z;
+  const lds_f64* LI = lds(c.a(A_LINV));
+  const lds_f64* M = lds(sv.M);
+  const lds_f64* Nb = lds(sv.Nb);
+  const bool top = m > 0, bot = N - 1 - m > 0;
+  ch.mli = act ? LI[m * DD + offN] : 0.0;
+  ch.mm = (act && top) ? M[m * DD + offN] : 0.0;
+  ch.mnb = (act && bot) ? Nb[m * DD + offN] : 0.0;
+}
+
+__device__ __forceinline__ double lds_at(unsigned a) { return *(const lds_f64*)(unsigned long)a; }
+
+// x = K^-1 b: b in BV (written by the segment's phase B), x into XV.  Ends with
+// every wave past a workgroup barrier; BV's rows m - 1 and m + 1 carry the
+// halves' y to the middle.  The blocks of kSegChunk steps are loaded, and
+// waited for once, before the chunk's serial steps (sched_barrier: left to
+// itself the scheduler sinks loads and their address arithmetic onto the
+// dependent steps).
+__device__ __forceinline__ void seg_chain_solve(const Ctx& c, const SegChain& ch, double* BVp, double* XVp,
+                                                long long& lap_fwd, long long& lap_bwd, long long* pf, long long& tq)
+{
+  const int D = c.L.D, N = c.L.N, m = c.L.tw_mid;
+  const int i = c.lane >> 3, k = c.lane & 7;
+  const int ic = (i < D) ? i : D - 1, kc = (k < D) ? k : D - 1;
+  lds_f64* BV = lds(BVp);
+  lds_f64* XV = lds(XVp);
+  const int R = __builtin_amdgcn_readfirstlane(ch.R);  // wave-uniform: guards are scalar branches
+  const int tdir = (c.wave == 0) ? -1 : 1;             // t = m + tdir * (1 + r)
+  // b of step r, in the lane's layout: COL-output steps (even r) take b[i], ROW (odd r) b[k]
+  const unsigned b0 = lds_addr(BVp + (m + tdir) * D);
+  const unsigned b_e = b0 + ic * 8, b_o = b0 + kc * 8;
+  const int bstride = tdir * D * 8;
+  double q[kSegHalf];
+  if (R > 0)
+  {
+    double y = 0.0;
+#pragma unroll
+    for (int r1 = kSegHalf - kSegChunk; r1 >= 0; r1 -= kSegChunk)
+    {
+      if (r1 >= R)
+        continue;
+      double li[kSegChunk], mf[kSegChunk], lb[kSegChunk];
+#pragma unroll
+      for (int u = 0; u < kSegChunk; ++u)
+      {
+        const int r = r1 + u;
+        const bool odd = r & 1;
+        li[u] = lds_at((odd ? ch.li_n : ch.li_t) + r * ch.stride);
+        mf[u] = lds_at((odd ? ch.mf_n : ch.mf_t) + r * ch.stride);
+        lb[u] = lds_at((odd ? b_o : b_e) + r * bstride);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = kSegChunk - 1; u >= 0; --u)
+        if (r1 + u < R)
+        {
+          const int r = r1 + u;
+          const double p = fma(-mf[u], y, li[u] * lb[u]);
+          y = (r & 1) ? octet_sum(p) : cross_octet_sum(p);
+          q[r] = li[u] * y;  // the backward step's LI^T y term
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // y_{m -+ 1} (COL layout) to the middle
+    if (i == 0 && k < D)
+      BV[(m + tdir) * D + k] = y;
+  }
+  BSYNC();
+  if (pf)
+  {
+    const long long tn = clock64();
+    lap_fwd += tn - tq;
+    tq = tn;
+  }
+  if (c.wave < 2)
+  {
+    const bool top = m > 0, bot = N - 1 - m > 0;
+    const double ym1 = top ? BV[(m - 1) * D + kc] : 0.0;
+    const double yp1 = bot ? BV[(m + 1) * D + kc] : 0.0;
+    const double bm = BV[m * D + kc];
+    const double p = fma(-ch.mnb, yp1, fma(-ch.mm, ym1, ch.mli * bm));
+    const double ym = octet_sum(p);           // ROW
+    double x = cross_octet_sum(ch.mli * ym);  // x_m, COL
+    if (c.wave == 0 && i == 0 && k < D)
+      XV[m * D + k] = x;
+#pragma unroll
+    for (int r1 = 0; r1 < kSegHalf; r1 += kSegChunk)
+    {
+      if (r1 >= R)
+        continue;
+      double nb[kSegChunk];
+#pragma unroll
+      for (int u = 0; u < kSegChunk; ++u)
+      {
+        const int r = r1 + u;
+        nb[u] = lds_at(((r & 1) ? ch.nb_t : ch.nb_n) + r * ch.stride);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      double xs[kSegChunk];
+#pragma unroll
+      for (int u = 0; u < kSegChunk; ++u)
+        if (r1 + u < R)
+        {
+          const int r = r1 + u;
+          const double p2 = fma(-nb[u], x, q[r]);
+          x = (r & 1) ? cross_octet_sum(p2) : octet_sum(p2);
+          xs[u] = x;
+        }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < kSegChunk; ++u)
+        if (r1 + u < R)
+        {
+          const int r = r1 + u;
+          const int t = m + tdir * (1 + r);
+          if (r & 1)
+          {
+            if (i == 0 && k < D)
+              XV[t * D + k] = xs[u];
+          }
+          else if (k == 0 && i < D)
+            XV[t * D + i] = xs[u];
+        }
+    }
+  }
+  BSYNC();
+  if (pf)
+  {
+    const long long tn = clock64();
+    lap_bwd += tn - tq;
+    tq = tn;
+  }
+}
+
 // rinv = 1 / rho, precomputed per segment (OSQP keeps rho_inv_vec)
 __device__ __forceinline__ void admm_row_update(double& z, double& y, double& dy, double zt, double rho, double rinv,
                                                 double lo, double up, double al)
@@ -2592,12 +2781,12 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
 {
   PROF(0);
   const Layout& L = c.L;
-  const int D = L.D, N = L.N, nx = L.nx, DD = D * D, nfr = L.n_fixed_rows, nr = L.n_rows;
+  const int D = L.D, N = L.N, nx = L.nx, nfr = L.n_fixed_rows, nr = L.n_rows;
   const thip_osqp_settings& os = c.d->osqp;
   const double sig = os.sigma, al = os.alpha;
   double *XA = c.a(A_XA0), *Z = c.a(A_Z0), *Y = c.a(A_Y), *DX = c.a(A_DX), *DY = c.a(A_DY);
   const double *Q = c.a(A_Q), *BS = c.a(A_BS), *RH = c.a(A_RHO), *Lo = c.a(A_L), *Up = c.a(A_U);
-  const double *FS = c.a(A_FS), *GS = c.a(A_GS), *WS = c.a(A_WS), *DG = c.a(A_DG), *LI = c.a(A_LINV);
+  const double *FS = c.a(A_FS), *GS = c.a(A_GS), *WS = c.a(A_WS), *DG = c.a(A_DG);
   double *MR = c.a(A_MR), *CV = c.a(A_CV), *YV = c.a(A_YV);
   // hinge rows (collision, config C): owned by h = tid + kBlock*j, state kept
   // in the planned arrays (LDS-resident under plan_lds_dynamic)
@@ -2749,7 +2938,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   int chp0[CS], chp1[CS], chp2[CS];  // hinge chunks of pair t-1: [chp0, chp1), of pair t: [chp1, chp2)
   double cq[CS], cbs[CS], clb[CS], cub[CS], crb[CS], cfs[CS], clf[CS], cuf[CS], crf[CS];
   double cx[CS], czb[CS], cyb[CS], czf[CS], cyf[CS], cdx[CS], cdyb[CS], cdyf[CS], crbi[CS], crfi[CS];
-  double cli[CS][THIP_MAX_DOF], cgs[CS][kMaxStepRows];
+  double cgs[CS][kMaxStepRows];
 #pragma unroll
   for (int u = 0; u < CS; ++u)
   {
@@ -2801,11 +2990,6 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
           crow[u][p] = r;
           cgs[u][p] = GS[r * D + i];
         }
-#pragma unroll
-      for (int k = 0; k < THIP_MAX_DOF; ++k)
-      {
-        cli[u][k] = (k <= i && k < D) ? LI[t * DD + i * D + k] : 0.0;
-      }
     }
     cdx[u] = cdyb[u] = cdyf[u] = 0.0;
   }
@@ -2862,6 +3046,12 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
     }
     adxn[u] = adxp[u] = adyr[u] = adybn[u] = adybp[u] = 0.0;
   }
+  // chain waves: the factor's blocks of their half, in registers
+  __shared__ double seg_zero;  // the chain's inactive lanes read this
+  if (c.tid == 0)
+    seg_zero = 0.0;
+  SegChain ch;
+  seg_chain_init(c, sv, &seg_zero, ch);
   BSYNC();
 
   // phase laps accumulate in registers and are flushed once per segment
@@ -2911,7 +3101,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       BSYNC();
     }
     SEG_LAP(lap17);
-    // B: waypoint right-hand sides, c_t = Linv_t b_t (octet gather in-wave)
+    // B: waypoint right-hand sides b -> YV
 #pragma unroll
     for (int u = 0; u < CS; ++u)
     {
@@ -2937,51 +3127,13 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
           for (int q = chp0[u]; q < chp1[u]; ++q)
             b += PARTl[q * 16 + D + j];
         }
-        lds(YV)[ccol[u]] = b;  // YV is free until the forward chain
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      if (cact[u])
-      {
-        const int i = (c.tid + kBlock * u) & 7;
-        const int base = ccol[u] - i;
-        double v0 = 0, v1 = 0;
-        // unconditional loads (in the LDS window), masked accumulation in two
-        // partial sums: no per-term branch, half the dependent adds
-#pragma unroll
-        for (int k = 0; k < THIP_MAX_DOF; ++k)
-        {
-          const double y = lds(YV)[base + k];
-          if (k & 1)
-            v1 = (k <= i) ? fma(cli[u][k], y, v1) : v1;
-          else
-            v0 = (k <= i) ? fma(cli[u][k], y, v0) : v0;
-        }
-        lds(CV)[ccol[u]] = v0 + v1;
+        lds(YV)[ccol[u]] = b;
       }
     }
     BSYNC();
     SEG_LAP(lap15);
-    twisted_forward(c, sv, CV, YV);
-    BSYNC();
-    SEG_LAP(lap9);
-    // d = LI^T y off the middle block; x_m by the last wave (no other thread
-    // touches CV[m])
-#pragma unroll
-    for (int u = 0; u < CS; ++u)
-      if (cact[u])
-      {
-        const int q = c.tid + kBlock * u;
-        if ((q >> 3) != L.tw_mid)
-          lds(CV)[ccol[u]] = twisted_dvalue(c, LI, YV, q >> 3, q & 7);
-      }
-    if (c.wave == kWaves - 1)
-      twisted_middle(c, sv, LI, CV, YV);
-    BSYNC();
-    SEG_LAP(lap16);
-    twisted_backward(c, sv, CV);
-    BSYNC();
-    SEG_LAP(lap10);
+    // x~ = K^-1 b into CV: forward halves, middle + backward halves
+    seg_chain_solve(c, ch, YV, CV, lap9, lap10, pf, tq);
     // E: back-substitution, z~ = A x~, relaxed updates
     const bool last = (iter == n_iter - 1);
 #pragma unroll

@@ -125,13 +125,14 @@ class BatchTrustRegionSQP:
                      "build_and_scale", "solve_rhs_diag", "fwd_chain", "bwd_chain", "aux_backsub", "qp_solve",
                      "sqp_total", "sqp_wall_ticks", "seg_B_rhs_linv", "seg_C2_linvT_middle",
                      "seg_hinge_gather", "seg_hinge_E", "coll_count_pass", "coll_rank_pass", "coll_rows", "coll_fk_substates",
-                     "unused23"]
+                     "seg_fwd_chain_w0", "chain_w0_loads", "chain_w0_serial", "chain_w0_stores",
+                     "unused27", "unused28", "unused29", "unused30", "unused31"]
 
     def enable_profile(self, on=True):
         self._check(self.lib.thip_debug_profile(self.ctx, 1 if on else 0), "thip_debug_profile")
 
     def get_profile(self):
-        out = np.zeros((self.batch, 24), dtype=np.int64)
+        out = np.zeros((self.batch, 32), dtype=np.int64)
         self._check(self.lib.thip_debug_get_profile(self.ctx, out.ctypes.data_as(C.POINTER(C.c_longlong))),
                     "thip_debug_get_profile")
         return out
