@@ -55,8 +55,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 def workload_name(wl, config, batch):
     terms = f"JointVel + {wl.desc.n_cart} CartPose ABS costs"
     if wl.desc.coll_enabled:
-        terms += f" + LVS-discrete collision cost ({wl.desc.n_prims}-primitive scene)"
-    return (f"config {config}: 7-DoF PR2 arm x {wl.n_steps} waypoints, {terms}, batch {batch} per GPU "
+        ev = {0: "LVS-discrete", 1: "LVS-continuous", 2: "discrete"}[wl.desc.coll_continuous]
+        terms += f" + {ev} collision cost ({wl.desc.n_prims}-primitive scene)"
+    robot = "14-DoF PR2 dual arm" if wl.n_dof == 14 else f"{wl.n_dof}-DoF PR2 arm"
+    return (f"config {config}: {robot} x {wl.n_steps} waypoints, {terms}, batch {batch} per GPU "
             "(BasicTrustRegionSQP + OSQP-semantics ADMM/polish)")
 
 

@@ -43,10 +43,10 @@
 extern "C" {
 #endif
 
-#define THIP_MAX_DOF 8
-#define THIP_MAX_LINKS 24
+#define THIP_MAX_DOF 16
+#define THIP_MAX_LINKS 32
 #define THIP_MAX_STEPS 64
-#define THIP_MAX_CART 64
+#define THIP_MAX_CART 128
 #define THIP_MAX_SPHERES 32
 #define THIP_MAX_PRIMS 16
 #define THIP_MAX_JPOS 8
@@ -91,16 +91,21 @@ extern "C" {
 #define THIP_PRIM_BOX 1
 #define THIP_PRIM_CAPSULE 2
 
-/* Serial kinematic chain (the tesseract JointGroup of the reference, restated):
- * link 0 is the chain root (static, world pose = base_pose); link k >= 1 hangs
- * off link k-1 through joint k with a fixed origin transform followed by the
- * joint motion about/along `joint_axis` (expressed in the joint frame). */
+/* Kinematic tree (the tesseract JointGroup of the reference, restated): link 0
+ * is the root (static, world pose = base_pose); link k >= 1 hangs off link
+ * parent[k] < k through joint k with a fixed origin transform followed by the
+ * joint motion about/along `joint_axis` (expressed in the joint frame).  A
+ * serial chain (the reference's right_arm / left_arm groups) has parent[k] =
+ * k - 1; a dual-arm group (both PR2 arms off torso_lift_link) branches at the
+ * root.  The segment's register-resident ADMM path takes n_dof <= 8; larger
+ * groups (up to THIP_MAX_DOF) run the generic block solve. */
 typedef struct thip_chain {
   int n_links;
   int n_dof;
   double base_pose[12];
   int joint_type[THIP_MAX_LINKS];
   int joint_dof[THIP_MAX_LINKS];          /* dof index for movable joints, -1 for fixed */
+  int parent[THIP_MAX_LINKS];             /* parent link of link k >= 1 (0 <= parent[k] < k) */
   double joint_origin[THIP_MAX_LINKS][12];
   double joint_axis[THIP_MAX_LINKS][3];
   double lower[THIP_MAX_DOF];             /* joint limits -> variable bounds */

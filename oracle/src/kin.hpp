@@ -2,7 +2,7 @@
 //
 // CPU restatement of the kinematics / pose-error arithmetic the reference
 // delegates to tesseract [ext, not under /root/reference]:
-//   JointGroup::calcFwdKin (serial chain, URDF joint semantics)
+//   JointGroup::calcFwdKin (kinematic tree, URDF joint semantics)
 //     call sites trajopt/src/kinematic_terms.cpp:255,355; collision_terms.cpp:882
 //   tesseract::common::calcTransformError, calcRotationalError(2),
 //   calcJacobianTransformErrorDiff, applyTolerances

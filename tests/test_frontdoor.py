@@ -39,9 +39,9 @@ def _expected_desc(wl):
     return ref
 
 
-@pytest.mark.parametrize("cfg", ["A", "B", "C", "J"])
+@pytest.mark.parametrize("cfg", ["A", "B", "C", "J", "E"])
 def test_json_lowering_matches_workload(cfg):
-    wl = problems.make_workload(cfg, 3)
+    wl = problems.make_workload(cfg, 3, n_steps=12 if cfg == "E" else None)
     exp = bytes(_expected_desc(wl))
     for b in range(wl.batch):
         text = host.workload_to_json(wl, b)
@@ -72,7 +72,7 @@ def _coll_pairs(pairs):
         ("{", "json:"),
         (json.dumps({"init_info": {"type": "stationary"}}), "Json missing required section basic_info!"),
         (json.dumps({"basic_info": {"n_steps": 5, "manip": "right_arm"}}), "Json missing required section init_info!"),
-        (_doc(basic_info={"n_steps": 5, "manip": "left_arm"}), "Manipulator does not exist: left_arm"),
+        (_doc(basic_info={"n_steps": 5, "manip": "full_body"}), "Manipulator does not exist: full_body"),
         (_doc(costs=[{"type": "foo", "params": {}}]), "failed to construct cost named foo"),
         (_doc(constraints=[{"type": "foo", "params": {}}]), "failed to construct constraint named foo"),
         (_doc(costs=[{"type": "joint_vel", "params": {"targets": [0], "bogus": 1}}]), "invalid field found: bogus"),

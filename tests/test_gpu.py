@@ -170,6 +170,22 @@ def test_fwd_kin_parity(oracle_mod, robot):
     np.testing.assert_allclose(poses, ref, rtol=0, atol=1e-13)
 
 
+def test_fwd_kin_parity_dual_arm_tree(oracle_mod):
+    """Config E's 14-DoF both_arms group (two branches off torso_lift_link):
+    every link's pose on the GPU against the oracle and the numpy FK."""
+    wl = problems.make_workload("E", 4, n_steps=6)
+    s = BatchTrustRegionSQP(wl)
+    poses = s.fwd_kin(wl.init)
+    s.close()
+    q = wl.init.reshape(-1, wl.n_dof)
+    ref = oracle_mod.fwd_kin(wl.desc.chain, q).reshape(poses.shape)
+    np.testing.assert_allclose(poses, ref, rtol=0, atol=1e-13)
+    T = robots.fwd_kin(wl.desc.chain, q[7])
+    for k in range(wl.desc.chain.n_links):
+        np.testing.assert_allclose(poses.reshape(-1, wl.desc.chain.n_links, 12)[7, k],
+                                   T[k][:3, :].reshape(12), rtol=0, atol=1e-12)
+
+
 def test_fwd_kin_golden(golden):
     g = golden("fk_pr2")
     wl = problems.make_workload("A", 16, n_steps=2)
@@ -329,6 +345,30 @@ def test_collision_rows_parity_continuous(oracle_mod):
     for b in range(wl.batch):
         _check_rows(rows[b], oracle_mod.collision_rows(wl, b, xo[b]), f"problem {b} (solution)", cc_atol=1e-12)
         _check_rows(rows_init[b], oracle_mod.collision_rows(wl, b, wl.init[b]), f"problem {b} (init)", cc_atol=1e-12)
+
+
+def test_collision_rows_parity_dual_arm(oracle_mod):
+    """Config E: LVS_CONTINUOUS contacts of both arms' spheres (links on two
+    branches of the tree; gradients through each arm's own joints) against
+    the oracle at the initial trajectory."""
+    wl = problems.make_workload("E", 8, n_steps=12)
+    wl.desc.coll_buffer = 0.3  # contacts within 0.325 m: every problem has some
+    s = BatchTrustRegionSQP(wl)
+    rows_init = s.collision_rows(wl.init)
+    s.close()
+    assert all(len(r) > 0 for r in rows_init)
+    for b in range(wl.batch):
+        _check_rows(rows_init[b], oracle_mod.collision_rows(wl, b, wl.init[b]), f"problem {b} (init)", cc_atol=1e-12)
+
+
+def test_sqp_parity_dual_arm_E(oracle_mod):
+    """Config E (BASELINE.json configs[4]): 14-DoF dual arm, 50 waypoints,
+    both tool frames tracked, LVS_CONTINUOUS collision -- the wide-block
+    (D > 8) solve path with the chain matrices in HBM."""
+    wl = problems.make_workload("E", 4)
+    x, res, tr = solve_gpu(wl, trace=4096)
+    assert all(r.flags == 0 for r in res)
+    check_parity(wl, oracle_mod, x, res, tr, label="E")
 
 
 def test_sqp_parity_collision_continuous(oracle_mod):

@@ -46,6 +46,32 @@ def test_fk_oracle_vs_numpy_other_chains(oracle_mod, robot):
         np.testing.assert_allclose(d, np.tile([0.0, 0.0, 0.1], (q.shape[0], 1)), atol=1e-12)
 
 
+def test_fk_oracle_vs_numpy_dual_arm_tree(oracle_mod):
+    """Config E's both_arms tree (left arm links 1-11, right arm 12-22, both
+    off torso_lift_link): oracle FK against the numpy FK, each tool frame
+    moved only by its own arm's joints, and the two arms mirror each other in
+    y at mirrored joint values."""
+    wl = problems.make_workload("E", 2, n_steps=5)
+    chain = wl.desc.chain
+    assert chain.n_dof == 14 and chain.n_links == 23 and chain.parent[12] == 0
+    q = wl.init.reshape(-1, wl.n_dof)
+    poses = oracle_mod.fwd_kin(chain, q)
+    for i in range(q.shape[0]):
+        ref = robots.fwd_kin(chain, q[i])
+        for k in range(chain.n_links):
+            np.testing.assert_allclose(poses[i, k], ref[k][:3, :].reshape(12), rtol=0, atol=1e-12)
+    q2 = q.copy()
+    q2[:, 7:] += 0.3  # right arm only
+    p2 = oracle_mod.fwd_kin(chain, q2)
+    np.testing.assert_array_equal(p2[:, 11], poses[:, 11])
+    assert np.abs(p2[:, 22] - poses[:, 22]).max() > 1e-3
+    z = np.zeros((1, 14))
+    z[0, [2, 9]] = 0.0  # upper arm rolls at zero, pans at zero: mirror images
+    pz = oracle_mod.fwd_kin(chain, z)[0]
+    np.testing.assert_allclose(pz[11][[3, 11]], pz[22][[3, 11]], atol=1e-14)
+    np.testing.assert_allclose(pz[11][7], -pz[22][7], atol=1e-14)
+
+
 @pytest.mark.parametrize("cfg", ["A", "B"])
 def test_cartpose_linearization_golden(oracle_mod, golden, cfg):
     g = golden(f"cartpose_{cfg}")

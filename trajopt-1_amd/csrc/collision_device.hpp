@@ -304,18 +304,24 @@ __device__ __forceinline__ int lvs_count(const double* q0, const double* q1, int
   return static_cast<int>(cnt);
 }
 
-// Geometric jacobian of chain link `link` at q (world frame, reference point =
-// link origin): J[6][D] row-major (linear rows 0-2, angular 3-5).
+// Geometric jacobian of link `link` at q (world frame, reference point =
+// link origin): J[6][D] row-major (linear rows 0-2, angular 3-5); columns of
+// joints off the link's path from the root are zero.
 __device__ inline void chain_jacobian(const thip_chain& ch, const double* q, int link, double* J)
 {
   const int D = ch.n_dof;
+  const unsigned path = chain_path(ch, link);
   Pose T[THIP_MAX_LINKS];
   pose_load(T[0], ch.base_pose);
+  int prev = 0;  // the path's previous link
   for (int k = 1; k <= link; ++k)
   {
+    if (!((path >> k) & 1u))
+      continue;
     Pose O, Tn;
     pose_load(O, ch.joint_origin[k]);
-    pose_mul(T[k - 1], O, Tn);
+    pose_mul(T[prev], O, Tn);
+    prev = k;
     const int type = ch.joint_type[k];
     if (type == THIP_JOINT_REVOLUTE || type == THIP_JOINT_CONTINUOUS)
     {
@@ -344,7 +350,7 @@ __device__ inline void chain_jacobian(const thip_chain& ch, const double* q, int
   for (int k = 1; k <= link; ++k)
   {
     const int type = ch.joint_type[k];
-    if (type == THIP_JOINT_FIXED)
+    if (type == THIP_JOINT_FIXED || !((path >> k) & 1u))
       continue;
     const double* ax = ch.joint_axis[k];
     double a[3];

@@ -1,7 +1,7 @@
 // Device kinematics and pose-error arithmetic (fp64, one thread per pose).
 //
 // GPU side of the tesseract arithmetic the reference calls
-// (trajopt/src/kinematic_terms.cpp:189-370): serial-chain FK, the
+// (trajopt/src/kinematic_terms.cpp:189-370): kinematic-tree FK, the
 // transform error target^-1 * source with the rotation-vector conventions of
 // tesseract's calcRotationalError / calcRotationalError2, and the
 // forward-difference error delta used by CartPoseJacCalculator.
@@ -75,13 +75,28 @@ __device__ __forceinline__ void rot_axis_angle(const double* ax, double ang, dou
   R[8] = ca2 * ax[2] + c;
 }
 
-// World pose of chain link `upto` at joint values q.
+// Links on the path root -> `link` (bit k set for link k >= 1): the joints
+// whose motion moves the link.  A serial chain has every link below `link`.
+__device__ __forceinline__ unsigned chain_path(const thip_chain& ch, int link)
+{
+  unsigned path = 0;
+  for (int k = link; k > 0; k = ch.parent[k])
+    path |= 1u << k;
+  return path;
+}
+
+// World pose of link `upto` at joint values q: the joints of its path from
+// the root, in order (parent[k] < k).
 __device__ inline void chain_fk(const thip_chain& ch, const double* q, int upto, Pose& out)
 {
+  static_assert(THIP_MAX_LINKS <= 32, "path mask");
+  const unsigned path = chain_path(ch, upto);
   Pose T;
   pose_load(T, ch.base_pose);
   for (int k = 1; k <= upto; ++k)
   {
+    if (!((path >> k) & 1u))
+      continue;
     Pose O, Tn;
     pose_load(O, ch.joint_origin[k]);
     pose_mul(T, O, Tn);

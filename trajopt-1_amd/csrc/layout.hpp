@@ -16,7 +16,7 @@ constexpr int kBlock = 256;  // threads per problem workgroup
 constexpr int kWaves = kBlock / 64;
 // dynamic LDS a problem may use (160 KB per CU on gfx950, one workgroup per
 // CU; the rest is the kernel's static LDS)
-constexpr long long kLdsBudgetBytes = 152 * 1024;
+constexpr long long kLdsBudgetBytes = 146 * 1024;
 // CartPose rows per waypoint the register-resident ADMM segment supports
 constexpr int kMaxStepRows = 8;
 // LVS sub-states per step pair the contact scan supports (sphere-center
@@ -68,6 +68,7 @@ enum DArr : int
   A_DG,      // diagonal of the aux block / x-col diagonal (n_cols)
   A_RE,      // effective rho of CartPose rows after aux elimination (n_rows)
   A_LINV,    // inverse Cholesky factor of the diagonal blocks (N*D*D)
+  A_CHM,     // wide blocks (D > 8): the chain matrices M, N in HBM (2*N*D*D; else unused)
   A_KB,      // assembled diagonal blocks (N*D*D)
   A_CV,      // block solve vectors (nx)
   A_YV,      // (nx)
@@ -161,6 +162,12 @@ struct Layout
   // lds_scratch doubles are the block-solve chain matrices / FK staging.
   int loff[A_COUNT];
   int lds_scratch;
+  // D > 8 (e.g. the 14-DoF dual arm): the block solve runs one lane per block
+  // row and its chain matrices M, N live in HBM (A_CHM), not in the LDS scratch
+  int wide;
+  // hinge chunk sums (A_HPART): lanes and doubles per chunk, >= 2 D (16 for
+  // the segment's D <= 8, 32 for wider blocks)
+  int part_w;
   int lds_doubles;
   int lds_budget;  // doubles of dynamic LDS the launch provides (dynamic plan)
   // register-resident ADMM segment (admm_segment): eligible when every

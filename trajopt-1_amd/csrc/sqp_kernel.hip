@@ -25,6 +25,9 @@ namespace thip
 {
 // ------------------------------------------------------------------ constants
 constexpr double kInf = 1e30;  // OSQP_INFTY
+// lane octets of the block solve: the chain layouts, the register-resident
+// ADMM segment and their unrolled per-dof loops take D <= kOct
+constexpr int kOct = 8;
 constexpr double kRhoMin = 1e-6, kRhoMax = 1e6, kRhoTol = 1e-4, kRhoEq = 1e3;
 constexpr double kMinScal = 1e-4, kMaxScal = 1e4;
 constexpr double kDivTol = 1.0 / kInf;
@@ -499,6 +502,8 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       int g = 0;
       for (int k = 1; k <= last_link; ++k)
       {
+        if (ch.parent[k] != k - 1)  // a branch of the tree: restart from the parent link's pose
+          chain_fk(ch, q, ch.parent[k], T);
         Pose O, Tn;
         pose_load(O, ch.joint_origin[k]);
         pose_mul(T, O, Tn);
@@ -1887,6 +1892,45 @@ __device__ __forceinline__ void block_chain(const double* Gp, const double* cvp,
   }
 }
 
+// The same recurrence for blocks wider than a lane octet (D > kOct, e.g.
+// the 14-DoF dual arm): lane i < D computes row i of each step from the
+// previous vector in LDS (out), one wave sync per step.
+__device__ __noinline__ void block_chain_wide(const double* Gp, const double* cvp, double* outp, int t0, int nsteps,
+                                              int dir, bool store_first, int D, int lane)
+{
+  const gbl_f64* G = gbl(Gp);  // HBM (Layout::wide)
+  const lds_f64* cv = lds(cvp);
+  lds_f64* out = lds(outp);
+  const int DD = D * D;
+  if (store_first && lane < D)
+    out[t0 * D + lane] = cv[t0 * D + lane];
+  wave_sync();
+  for (int s = 1; s <= nsteps; ++s)
+  {
+    const int t = t0 + dir * s, tp = t - dir;
+    double v = 0.0;
+    if (lane < D)
+    {
+      v = cv[t * D + lane];
+      for (int k = 0; k < D; ++k)
+        v -= G[t * DD + lane * D + k] * out[tp * D + k];
+    }
+    wave_sync();  // out may alias cv (backward pass, in place)
+    if (lane < D)
+      out[t * D + lane] = v;
+    wave_sync();
+  }
+}
+
+__device__ __forceinline__ void chain_any(const double* G, const double* cv, double* out, int t0, int nsteps, int dir,
+                                          bool store_first, int D, int lane, bool wide)
+{
+  if (wide)
+    block_chain_wide(G, cv, out, t0, nsteps, dir, store_first, D, lane);
+  else
+    block_chain(G, cv, out, t0, nsteps, dir, store_first, D, lane);
+}
+
 // Forward solve of the twisted factor: y = L^-1 b given c_t = LI_t b_t in
 // CV.  Wave 0 runs the top chain (t = 1..m-1), wave 1 the bottom chain
 // (t = N-2..m+1); the middle block is finished by twisted_middle().
@@ -1894,9 +1938,9 @@ __device__ __forceinline__ void twisted_forward(const Ctx& c, const Solver& sv, 
 {
   const int N = c.L.N, m = c.L.tw_mid;
   if (c.wave == 0)
-    block_chain(sv.M, CV, YV, 0, m - 1, +1, true, c.L.D, c.lane);
+    chain_any(sv.M, CV, YV, 0, m - 1, +1, true, c.L.D, c.lane, c.L.wide);
   else if (c.wave == 1 && N - 1 - m > 0)
-    block_chain(sv.M, CV, YV, N - 1, N - 2 - m, -1, true, c.L.D, c.lane);
+    chain_any(sv.M, CV, YV, N - 1, N - 2 - m, -1, true, c.L.D, c.lane, c.L.wide);
 }
 
 // Backward solve of the twisted factor, in place in CV (holding d_t =
@@ -1906,9 +1950,9 @@ __device__ __forceinline__ void twisted_backward(const Ctx& c, const Solver& sv,
 {
   const int N = c.L.N, m = c.L.tw_mid;
   if (c.wave == 0)
-    block_chain(sv.Nb, CV, CV, m, m, -1, false, c.L.D, c.lane);
+    chain_any(sv.Nb, CV, CV, m, m, -1, false, c.L.D, c.lane, c.L.wide);
   else if (c.wave == 1)
-    block_chain(sv.Nb, CV, CV, m, N - 1 - m, +1, false, c.L.D, c.lane);
+    chain_any(sv.Nb, CV, CV, m, N - 1 - m, +1, false, c.L.D, c.lane, c.L.wide);
 }
 
 // d_t[i] = (LI_t^T y_t)[i] for column (t, i), t != middle.
@@ -1917,11 +1961,18 @@ __device__ __forceinline__ double twisted_dvalue(const Ctx& c, const double* LIp
   const int D = c.L.D, DD = D * D;
   const lds_f64* LI = lds(LIp);
   const lds_f64* YV = lds(YVp);
+  if (c.L.wide)
+  {
+    double v = 0.0;
+    for (int k = i; k < D; ++k)
+      v += LI[t * DD + k * D + i] * YV[t * D + k];
+    return v;
+  }
   // unconditional loads from clamped indices, two accumulators (even / odd k):
   // no branch per term and half the dependent adds
   double v0 = 0, v1 = 0;
 #pragma unroll
-  for (int k = 0; k < THIP_MAX_DOF; ++k)
+  for (int k = 0; k < kOct; ++k)
   {
     const int kk = (k < D) ? k : D - 1;
     const double a = LI[t * DD + kk * D + i] * YV[t * D + kk];
@@ -1937,9 +1988,46 @@ __device__ __forceinline__ double twisted_dvalue(const Ctx& c, const double* LIp
 // The middle block of the twisted solve, by one whole wave in the chain's
 // octet layout: y_m = c_m - M_m y_{m-1} - M'_m y_{m+1} (octet reduction),
 // x_m = LI_m^T y_m (cross-octet reduction), written over c_m in CV.
+__device__ __noinline__ void twisted_middle_wide(const Ctx& c, const Solver& sv, const double* LIp, double* CVp,
+                                                double* YVp)
+{
+  const int D = c.L.D, DD = D * D, m = c.L.tw_mid, N = c.L.N, i = c.lane;
+  const lds_f64* LI = lds(LIp);
+  const gbl_f64* M = gbl(sv.M);  // HBM (Layout::wide)
+  const gbl_f64* Mb = gbl(sv.Nb);
+  lds_f64* CV = lds(CVp);
+  lds_f64* YV = lds(YVp);
+  if (i < D)
+  {
+    double s = 0.0;
+    for (int k = 0; k < D; ++k)
+    {
+      if (m > 0)
+        s += M[m * DD + i * D + k] * YV[(m - 1) * D + k];
+      if (N - 1 - m > 0)
+        s += Mb[m * DD + i * D + k] * YV[(m + 1) * D + k];
+    }
+    YV[m * D + i] = CV[m * D + i] - s;  // y_m (YV's middle row is not a chain output)
+  }
+  wave_sync();
+  if (i < D)
+  {
+    double x = 0.0;
+    for (int k = i; k < D; ++k)
+      x += LI[m * DD + k * D + i] * YV[m * D + k];
+    CV[m * D + i] = x;
+  }
+  wave_sync();
+}
+
 __device__ __forceinline__ void twisted_middle(const Ctx& c, const Solver& sv, const double* LIp, double* CVp,
                                                const double* YVp)
 {
+  if (c.L.wide)
+  {
+    twisted_middle_wide(c, sv, LIp, CVp, const_cast<double*>(YVp));
+    return;
+  }
   const int D = c.L.D, DD = D * D, m = c.L.tw_mid, N = c.L.N;
   const int i = c.lane >> 3, k = c.lane & 7;
   const bool act = (i < D) && (k < D);
@@ -2085,19 +2173,25 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   {
     // d = LI^T y off the middle block (all columns read before any write),
     // x_m at the middle block by the last wave
-    static_assert(THIP_MAX_STEPS * THIP_MAX_DOF <= 2 * kBlock, "two columns per thread");
+    constexpr int kCols = (THIP_MAX_STEPS * THIP_MAX_DOF + kBlock - 1) / kBlock;
     const int m = L.tw_mid;
-    const int c0 = c.tid, c1 = c.tid + kBlock;
-    const bool w0 = c0 < nx && c0 / D != m, w1 = c1 < nx && c1 / D != m;
-    const double d0 = w0 ? twisted_dvalue(c, LI, YV, c0 / D, c0 % D) : 0.0;
-    const double d1 = w1 ? twisted_dvalue(c, LI, YV, c1 / D, c1 % D) : 0.0;
+    double dv[kCols];
+#pragma unroll
+    for (int u = 0; u < kCols; ++u)
+    {
+      const int cu = c.tid + kBlock * u;
+      dv[u] = (cu < nx && cu / D != m) ? twisted_dvalue(c, LI, YV, cu / D, cu % D) : 0.0;
+    }
     if (c.wave == kWaves - 1)
       twisted_middle(c, sv, LI, CV, YV);
     BSYNC();
-    if (w0)
-      lds(CV)[c0] = d0;
-    if (w1)
-      lds(CV)[c1] = d1;
+#pragma unroll
+    for (int u = 0; u < kCols; ++u)
+    {
+      const int cu = c.tid + kBlock * u;
+      if (cu < nx && cu / D != m)
+        lds(CV)[cu] = dv[u];
+    }
   }
   BSYNC();
   PROF_LAP(8);
@@ -2213,7 +2307,7 @@ __device__ int build_hinge_chunks(Ctx& c)
 }
 
 // Row-parallel hinge share of A'v: A_HPART[q][k] = sum over chunk q of
-// HC[h][k] * v[hinge row h] (16 lanes per chunk, lane k = coefficient k).
+// HC[h][k] * v[hinge row h] (Layout::part_w lanes per chunk, lane k = coefficient k).
 // col_aty then adds the chunk sums of its two step pairs instead of looping
 // over every hinge row of them (a serial chain of loads per column).
 __device__ void hinge_chunk_sums(Ctx& c, const double* v, int nchk)
@@ -2222,9 +2316,9 @@ __device__ void hinge_chunk_sums(Ctx& c, const double* v, int nchk)
   const double* HC = c.a(A_HC);
   const int* CHK = reinterpret_cast<const int*>(c.a(A_HCHK));
   double* PART = c.a(A_HPART);
-  const int k = c.tid & 15;
+  const int pw = c.L.part_w, k = c.tid % pw;  // lanes per chunk: 2 D coefficients
   if (k < 2 * D)
-    for (int q = c.tid >> 4; q < nchk; q += kBlock / 16)
+    for (int q = c.tid / pw; q < nchk; q += kBlock / pw)
     {
       const int h0 = CHK[2 * q], h1 = CHK[2 * q + 1];
       double s0 = 0, s1 = 0;
@@ -2237,7 +2331,7 @@ __device__ void hinge_chunk_sums(Ctx& c, const double* v, int nchk)
         s0 = (h0 + i < h1) ? s0 + aa : s0;
         s1 = (h0 + i + 1 < h1) ? s1 + ab : s1;
       }
-      PART[q * 16 + k] = s0 + s1;
+      PART[q * pw + k] = s0 + s1;
     }
   BSYNC();
 }
@@ -2278,10 +2372,10 @@ __device__ __forceinline__ double col_aty(const Ctx& c, int col, const double* y
     {
       const double* PART = c.a(A_HPART);
       for (int q = c.s->hcp[t]; q < c.s->hcp[t + 1]; ++q)
-        v += PART[q * 16 + j];
+        v += PART[q * c.L.part_w + j];
       if (t > 0)
         for (int q = c.s->hcp[t - 1]; q < c.s->hcp[t]; ++q)
-          v += PART[q * 16 + D + j];
+          v += PART[q * c.L.part_w + D + j];
     }
     else if (c.s->n_h > 0)
     {
@@ -2894,7 +2988,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       // clamped indices (always in bounds), masked accumulation: the loads
       // of all terms are in flight together
 #pragma unroll
-      for (int k = 0; k < THIP_MAX_DOF; ++k)
+      for (int k = 0; k < kOct; ++k)
       {
         const int kk = (k < D) ? k : D - 1;
         const double a0 = HTP[kk * nhs + h], a1 = HTP[(D + kk) * nhs + h];
@@ -2996,7 +3090,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   // ---- abs-row owners
   bool aact[AS];
   int at[AS];
-  double arr[AS], alr[AS], aur[AS], awn[AS], awp[AS], adn[AS], adp[AS], adet[AS], ags[AS][THIP_MAX_DOF];
+  double arr[AS], alr[AS], aur[AS], awn[AS], awp[AS], adn[AS], adp[AS], adet[AS], ags[AS][kOct];
   double aqn[AS], aqp[AS], absn[AS], absp[AS], albn[AS], aubn[AS], arbn[AS], albp[AS], aubp[AS], arbp[AS];
   double axn[AS], axp[AS], azr[AS], ayr[AS], azbn[AS], aybn[AS], azbp[AS], aybp[AS];
   double adxn[AS], adxp[AS], adyr[AS], adybn[AS], adybp[AS];
@@ -3021,7 +3115,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
       adeti[u] = 1.0 / adet[u];
       arri[u] = 1.0 / arr[u];
 #pragma unroll
-      for (int j = 0; j < THIP_MAX_DOF; ++j)
+      for (int j = 0; j < kOct; ++j)
         ags[u][j] = (j < D) ? GS[a * D + j] : 0.0;
       aqn[u] = Q[ca];
       aqp[u] = Q[ca + 1];
@@ -3155,7 +3249,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
         const int t = at[u];
         double g0 = 0, g1 = 0;
 #pragma unroll
-        for (int j = 0; j < THIP_MAX_DOF; ++j)
+        for (int j = 0; j < kOct; ++j)
         {
           const double xv = lds(CV)[t * D + ((j < D) ? j : D - 1)];
           if (j & 1)
@@ -3682,7 +3776,7 @@ __device__ void plan_lds_dynamic(Ctx& c)
         case A_HPK: n = nh * kHPack; break;
         case A_HCT: n = (nh | 1) * 2 * D; break;
         case A_HCHK: n = nh / kHChunk + L.N + 1; break;
-        case A_HPART: n = (nh / kHChunk + L.N + 1) * 16; break;
+        case A_HPART: n = (nh / kHChunk + L.N + 1) * L.part_w; break;
         case A_GS: n = nab * D; break;
         case A_WS: n = nab * 2; break;
         case A_FS: n = L.n_fixed_rows; break;
@@ -4104,8 +4198,9 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
   c.scene = args.scene ? args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16 : nullptr;
   c.jpt = args.jpt + (long long)b * (L.n_jpos > 0 ? L.n_jpos : 1) * L.D;
   Solver sv;
-  sv.M = dyn;
-  sv.Nb = dyn + L.N * L.D * L.D;
+  // chain matrices: the LDS scratch, or HBM for wide blocks (Layout::wide)
+  sv.M = L.wide ? wsb + L.doff[A_CHM] : dyn;
+  sv.Nb = sv.M + L.N * L.D * L.D;
   if (threadIdx.x == 0)
   {
     ctl.trace = args.trace ? args.trace + (long long)b * args.trace_cap * THIP_TRACE_W : nullptr;

@@ -134,6 +134,8 @@ static int validate(const thip_problem_desc* d, std::string& why)
       return why = "bad joint type", THIP_E_INVALID;
     if (ty != THIP_JOINT_FIXED && (ch.joint_dof[k] < 0 || ch.joint_dof[k] >= ch.n_dof))
       return why = "bad joint dof index", THIP_E_INVALID;
+    if (ch.parent[k] < 0 || ch.parent[k] >= k)
+      return why = "bad parent link (links must be in tree order, 0 <= parent[k] < k)", THIP_E_INVALID;
   }
   if (d->n_fixed < 0 || d->n_fixed > THIP_MAX_STEPS)
     return why = "n_fixed out of range", THIP_E_INVALID;
@@ -518,6 +520,11 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   sizes[A_MR] = std::max(L.n_rows, 1) + L.h_cap;
   sizes[A_RE] = std::max(L.n_rows, 1);
   sizes[A_LINV] = sizes[A_KB] = NDD;
+  L.wide = (L.D > 8) ? 1 : 0;
+  if (const char* e = std::getenv("THIP_FORCE_WIDE"))  // diagnostic: the wide-block solve for any D
+    if (e[0] == '1')
+      L.wide = 1;
+  sizes[A_CHM] = L.wide ? 2 * NDD : 1;
   sizes[A_PB] = std::max(nc + m, nab * D);
   sizes[A_PS] = sizes[A_PR] = nc + m;
   sizes[A_HC0] = sizes[A_HC] = hc * 2 * D;
@@ -528,7 +535,8 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   sizes[A_HPK] = L.hinge ? hc * kHPack : 1;
   const long long nchk_cap = hc / kHChunk + L.N + 1;
   sizes[A_HCHK] = L.hinge ? nchk_cap : 1;
-  sizes[A_HPART] = L.hinge ? nchk_cap * 16 : 1;
+  L.part_w = (2 * L.D <= 16) ? 16 : 32;
+  sizes[A_HPART] = L.hinge ? nchk_cap * L.part_w : 1;
   sizes[A_HCT] = L.hinge ? 2 * D * (hc + 1) : 1;
   for (int k = 0; k < A_COUNT; ++k)
     if (sizes[k] < 0)
@@ -559,7 +567,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     ioff += (isizes[k] + 15) / 16 * 16;
   }
   L.istride = ioff;
-  const size_t lds_d = std::max<size_t>({ (size_t)(2 * NDD), (size_t)(30 * std::max(L.n_cart, 1)),
+  const size_t lds_d = std::max<size_t>({ (size_t)(L.wide ? 0 : 2 * NDD), (size_t)(30 * std::max(L.n_cart, 1)),
                                           (size_t)(L.n_costs + L.n_cnts + 2) });
   ctx->lds_lin_bytes = lds_d * sizeof(double);
   // LDS residency plan: the per-ADMM-iteration working set, hottest first,
@@ -589,7 +597,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     // one column slot (t, i) and one CartPose row per thread: N <= 32 and
     // n_abs <= 256; larger problems run the generic admm_step()
     // (collision problems: hinge rows are loop-owned inside the segment)
-    L.seg_ok = (max_step_rows <= kMaxStepRows && L.D <= 8 && L.N * 8 <= kBlock && L.n_abs <= kBlock) ? 1 : 0;
+    L.seg_ok = (max_step_rows <= kMaxStepRows && !L.wide && L.N * 8 <= kBlock && L.n_abs <= kBlock) ? 1 : 0;
     if (const char* e = std::getenv("THIP_NO_SEGMENT"))
       if (e[0] == '1')
         L.seg_ok = 0;

@@ -105,7 +105,7 @@ inline TermType operator|(TermType a, TermType b) { return TermType(static_cast<
 inline TermType operator&(TermType a, TermType b) { return TermType(static_cast<char>(a) & static_cast<char>(b)); }
 inline bool any(TermType t) { return static_cast<char>(t) != 0; }
 
-// tesseract JointGroup, restated for a serial chain
+// tesseract JointGroup, restated for a kinematic tree (thip_chain::parent)
 struct KinematicGroup
 {
   using ConstPtr = std::shared_ptr<const KinematicGroup>;
@@ -126,7 +126,7 @@ struct KinematicGroup
 
 struct CollisionSphere
 {
-  int link;           // chain link index
+  std::string link;   // robot link name
   double center[3];   // in the link frame
   double radius;
 };
@@ -147,9 +147,10 @@ public:
   std::vector<CollisionSphere> collision_spheres;      // robot collision model
   std::vector<std::array<double, 16>> scene;           // THIP_PRIM_* records
 
-  // PR2 right arm (group "right_arm": torso_lift_link -> r_gripper_tool_frame,
-  // joint data of trajopt_common/data/arm_around_table.urdf), zero state, the
-  // 14-sphere arm collision model of trajopt_amd/scene.py, empty scene.
+  // PR2 arms (groups "right_arm", "left_arm": torso_lift_link ->
+  // *_gripper_tool_frame, and "both_arms", joint data of
+  // trajopt_common/data/arm_around_table.urdf), zero state, the 14-sphere
+  // per-arm collision model of trajopt_amd/scene.py, empty scene.
   static Ptr makePR2();
 
 private:

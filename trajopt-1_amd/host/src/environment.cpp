@@ -1,9 +1,12 @@
-// Built-in environment: the PR2 right arm of the reference's test data
-// (trajopt_common/data/arm_around_table.urdf joints, pr2.srdf group
-// "right_arm": torso_lift_link -> r_gripper_tool_frame), the same numbers as
-// trajopt_amd/robots.py and the 14-sphere collision model of
+// Built-in environment: the PR2 arms of the reference's test data
+// (trajopt_common/data/arm_around_table.urdf joints; pr2.srdf groups
+// "right_arm" / "left_arm": torso_lift_link -> *_gripper_tool_frame, and
+// "both_arms", the two as one 14-joint tree), the same numbers as
+// trajopt_amd/robots.py, and the 14-sphere-per-arm collision model of
 // trajopt_amd/scene.py (PR2_ARM_SPHERES).
 #include <cmath>
+#include <string>
+#include <vector>
 
 #include "trajopt_amd/problem_description.hpp"
 
@@ -13,35 +16,51 @@ namespace
 {
 struct JointRow
 {
-  const char* joint;
-  const char* child;
+  std::string joint;
+  std::string child;
   int type;
   double xyz[3];
   double axis[3];
   double lower, upper;
 };
-}  // namespace
 
-Environment::Ptr Environment::makePR2()
+// One arm's joints, torso_lift_link -> *_gripper_tool_frame (11 joints, 7 movable).
+void armRows(bool left, std::vector<JointRow>& rows)
 {
   const double kPi4 = 4 * M_PI;
-  const JointRow rows[] = {
-    { "r_shoulder_pan_joint", "r_shoulder_pan_link", THIP_JOINT_REVOLUTE, { 0.0, -0.188, 0.0 }, { 0, 0, 1 },
-      -2.2853981634, 0.714601836603 },
-    { "r_shoulder_lift_joint", "r_shoulder_lift_link", THIP_JOINT_REVOLUTE, { 0.1, 0.0, 0.0 }, { 0, 1, 0 }, -0.5236,
-      1.3963 },
-    { "r_upper_arm_roll_joint", "r_upper_arm_roll_link", THIP_JOINT_REVOLUTE, { 0, 0, 0 }, { 1, 0, 0 }, -3.9, 0.8 },
-    { "r_upper_arm_joint", "r_upper_arm_link", THIP_JOINT_FIXED, { 0, 0, 0 }, { 0, 0, 0 }, 0, 0 },
-    { "r_elbow_flex_joint", "r_elbow_flex_link", THIP_JOINT_REVOLUTE, { 0.4, 0.0, 0.0 }, { 0, 1, 0 }, -2.3213, 0.0 },
-    { "r_forearm_roll_joint", "r_forearm_roll_link", THIP_JOINT_CONTINUOUS, { 0, 0, 0 }, { 1, 0, 0 }, -kPi4, kPi4 },
-    { "r_forearm_joint", "r_forearm_link", THIP_JOINT_FIXED, { 0, 0, 0 }, { 0, 0, 0 }, 0, 0 },
-    { "r_wrist_flex_joint", "r_wrist_flex_link", THIP_JOINT_REVOLUTE, { 0.321, 0.0, 0.0 }, { 0, 1, 0 }, -2.18, 0.0 },
-    { "r_wrist_roll_joint", "r_wrist_roll_link", THIP_JOINT_CONTINUOUS, { 0, 0, 0 }, { 1, 0, 0 }, -kPi4, kPi4 },
-    { "r_gripper_palm_joint", "r_gripper_palm_link", THIP_JOINT_FIXED, { 0, 0, 0 }, { 0, 0, 0 }, 0, 0 },
-    { "r_gripper_tool_joint", "r_gripper_tool_frame", THIP_JOINT_FIXED, { 0.18, 0.0, 0.0 }, { 0, 0, 0 }, 0, 0 },
-  };
+  const double y = left ? 0.188 : -0.188;
+  // l_shoulder_pan 2396-2402 / r 1479-1485; l_upper_arm_roll 2462-2468 / r 1545-1550
+  const double pan_lo = left ? -0.714601836603 : -2.2853981634, pan_hi = left ? 2.2853981634 : 0.714601836603;
+  const double roll_lo = left ? -0.8 : -3.9, roll_hi = left ? 3.9 : 0.8;
+  const char* p = left ? "l_" : "r_";
+  auto n = [&](const char* base) { return std::string(p) + base; };
+  rows.push_back({ n("shoulder_pan_joint"), n("shoulder_pan_link"), THIP_JOINT_REVOLUTE, { 0.0, y, 0.0 }, { 0, 0, 1 },
+                   pan_lo, pan_hi });
+  rows.push_back({ n("shoulder_lift_joint"), n("shoulder_lift_link"), THIP_JOINT_REVOLUTE, { 0.1, 0.0, 0.0 },
+                   { 0, 1, 0 }, -0.5236, 1.3963 });
+  rows.push_back({ n("upper_arm_roll_joint"), n("upper_arm_roll_link"), THIP_JOINT_REVOLUTE, { 0, 0, 0 }, { 1, 0, 0 },
+                   roll_lo, roll_hi });
+  rows.push_back({ n("upper_arm_joint"), n("upper_arm_link"), THIP_JOINT_FIXED, { 0, 0, 0 }, { 0, 0, 0 }, 0, 0 });
+  rows.push_back({ n("elbow_flex_joint"), n("elbow_flex_link"), THIP_JOINT_REVOLUTE, { 0.4, 0.0, 0.0 }, { 0, 1, 0 },
+                   -2.3213, 0.0 });
+  rows.push_back({ n("forearm_roll_joint"), n("forearm_roll_link"), THIP_JOINT_CONTINUOUS, { 0, 0, 0 }, { 1, 0, 0 },
+                   -kPi4, kPi4 });
+  rows.push_back({ n("forearm_joint"), n("forearm_link"), THIP_JOINT_FIXED, { 0, 0, 0 }, { 0, 0, 0 }, 0, 0 });
+  rows.push_back({ n("wrist_flex_joint"), n("wrist_flex_link"), THIP_JOINT_REVOLUTE, { 0.321, 0.0, 0.0 }, { 0, 1, 0 },
+                   -2.18, 0.0 });
+  rows.push_back({ n("wrist_roll_joint"), n("wrist_roll_link"), THIP_JOINT_CONTINUOUS, { 0, 0, 0 }, { 1, 0, 0 },
+                   -kPi4, kPi4 });
+  rows.push_back({ n("gripper_palm_joint"), n("gripper_palm_link"), THIP_JOINT_FIXED, { 0, 0, 0 }, { 0, 0, 0 }, 0, 0 });
+  rows.push_back({ n("gripper_tool_joint"), n("gripper_tool_frame"), THIP_JOINT_FIXED, { 0.18, 0.0, 0.0 },
+                   { 0, 0, 0 }, 0, 0 });
+}
+
+// A joint group of one or two arms off torso_lift_link (each arm a branch of
+// the tree rooted at the group's link 0).
+KinematicGroup makeGroup(const std::string& name, const std::vector<bool>& arms_left)
+{
   KinematicGroup g;
-  g.name = "right_arm";
+  g.name = name;
   thip_chain& c = g.chain;
   const double eye[12] = { 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0 };
   // world pose of torso_lift_link: base_footprint -> base_link (0, 0, 0.051) -> torso (-0.05, 0, 0.739675)
@@ -51,30 +70,39 @@ Environment::Ptr Environment::makePR2()
   c.base_pose[7] = 0.0;
   c.base_pose[11] = 0.051 + 0.739675;
   c.joint_dof[0] = -1;
+  c.parent[0] = 0;
   g.link_names.push_back("torso_lift_link");
   int dof = 0, k = 1;
-  for (const auto& r : rows)
+  for (const bool left : arms_left)
   {
-    c.joint_type[k] = r.type;
-    for (int i = 0; i < 12; ++i)
-      c.joint_origin[k][i] = eye[i];
-    c.joint_origin[k][3] = r.xyz[0];
-    c.joint_origin[k][7] = r.xyz[1];
-    c.joint_origin[k][11] = r.xyz[2];
-    if (r.type == THIP_JOINT_FIXED)
-      c.joint_dof[k] = -1;
-    else
+    std::vector<JointRow> rows;
+    armRows(left, rows);
+    int prev = 0;  // each arm hangs off the root
+    for (const auto& r : rows)
     {
-      c.joint_dof[k] = dof;
-      for (int i = 0; i < 3; ++i)
-        c.joint_axis[k][i] = r.axis[i];
-      c.lower[dof] = r.lower;
-      c.upper[dof] = r.upper;
-      g.joint_names.push_back(r.joint);
-      ++dof;
+      c.joint_type[k] = r.type;
+      c.parent[k] = prev;
+      for (int i = 0; i < 12; ++i)
+        c.joint_origin[k][i] = eye[i];
+      c.joint_origin[k][3] = r.xyz[0];
+      c.joint_origin[k][7] = r.xyz[1];
+      c.joint_origin[k][11] = r.xyz[2];
+      if (r.type == THIP_JOINT_FIXED)
+        c.joint_dof[k] = -1;
+      else
+      {
+        c.joint_dof[k] = dof;
+        for (int i = 0; i < 3; ++i)
+          c.joint_axis[k][i] = r.axis[i];
+        c.lower[dof] = r.lower;
+        c.upper[dof] = r.upper;
+        g.joint_names.push_back(r.joint);
+        ++dof;
+      }
+      g.link_names.push_back(r.child);
+      prev = k;
+      ++k;
     }
-    g.link_names.push_back(r.child);
-    ++k;
   }
   c.n_links = k;
   c.n_dof = dof;
@@ -84,18 +112,29 @@ Environment::Ptr Environment::makePR2()
   bl[11] = 0.051;
   g.static_frames["base_footprint"] = bf;
   g.static_frames["base_link"] = bl;
+  return g;
+}
+}  // namespace
 
+Environment::Ptr Environment::makePR2()
+{
   auto env = std::make_shared<Environment>();
-  env->addJointGroup(g);
-  // (link, center in the link frame, radius)
-  const CollisionSphere spheres[] = {
-    { 1, { 0.0, 0.0, 0.0 }, 0.09 },  { 1, { 0.1, 0.0, 0.0 }, 0.08 },  { 2, { 0.0, 0.0, 0.0 }, 0.08 },
-    { 2, { 0.1, 0.0, 0.0 }, 0.07 },  { 3, { 0.15, 0.0, 0.0 }, 0.07 }, { 3, { 0.3, 0.0, 0.0 }, 0.07 },
-    { 5, { 0.0, 0.0, 0.0 }, 0.07 },  { 5, { 0.08, 0.0, 0.0 }, 0.06 }, { 6, { 0.12, 0.0, 0.0 }, 0.06 },
-    { 6, { 0.24, 0.0, 0.0 }, 0.06 }, { 8, { 0.0, 0.0, 0.0 }, 0.06 },  { 8, { 0.08, 0.0, 0.0 }, 0.06 },
-    { 9, { 0.12, 0.0, 0.0 }, 0.06 }, { 9, { 0.18, 0.0, 0.0 }, 0.06 },
-  };
-  env->collision_spheres.assign(std::begin(spheres), std::end(spheres));
+  // pr2.srdf:12-17 left_arm / right_arm; both_arms = the two chains as one
+  // 14-joint group (left arm first), branching at torso_lift_link
+  env->addJointGroup(makeGroup("right_arm", { false }));
+  env->addJointGroup(makeGroup("left_arm", { true }));
+  env->addJointGroup(makeGroup("both_arms", { true, false }));
+  // 2 spheres per moving arm link (link, center in the link frame, radius),
+  // trajopt_amd/scene.py PR2_ARM_SPHERES; the left arm mirrors the right
+  const char* links[] = { "shoulder_pan_link", "shoulder_pan_link", "shoulder_lift_link", "shoulder_lift_link",
+                          "upper_arm_roll_link", "upper_arm_roll_link", "elbow_flex_link", "elbow_flex_link",
+                          "forearm_roll_link", "forearm_roll_link", "wrist_flex_link", "wrist_flex_link",
+                          "wrist_roll_link", "wrist_roll_link" };
+  const double cx[] = { 0.0, 0.1, 0.0, 0.1, 0.15, 0.3, 0.0, 0.08, 0.12, 0.24, 0.0, 0.08, 0.12, 0.18 };
+  const double rad[] = { 0.09, 0.08, 0.08, 0.07, 0.07, 0.07, 0.07, 0.06, 0.06, 0.06, 0.06, 0.06, 0.06, 0.06 };
+  for (const char* side : { "l_", "r_" })
+    for (int s = 0; s < 14; ++s)
+      env->collision_spheres.push_back({ std::string(side) + links[s], { cx[s], 0.0, 0.0 }, rad[s] });
   return env;
 }
 }  // namespace trajopt

@@ -197,10 +197,8 @@ int KinematicGroup::linkIndex(const std::string& link) const
 
 bool KinematicGroup::isActiveLinkId(const std::string& link) const
 {
-  const int k = linkIndex(link);
-  if (k < 0)
-    return false;
-  for (int i = 1; i <= k; ++i)
+  // moved by a joint on its path from the root
+  for (int i = linkIndex(link); i > 0; i = chain.parent[i])
     if (chain.joint_type[i] != THIP_JOINT_FIXED)
       return true;
   return false;
@@ -211,12 +209,14 @@ std::array<double, 12> KinematicGroup::staticWorldPose(const std::string& link) 
   const int k = linkIndex(link);
   if (k >= 0)
   {
-    for (int i = 1; i <= k; ++i)
-      if (chain.joint_type[i] != THIP_JOINT_FIXED)
-        throw std::runtime_error("staticWorldPose: link " + link + " is active");
+    if (isActiveLinkId(link))
+      throw std::runtime_error("staticWorldPose: link " + link + " is active");
+    std::vector<int> path;  // root -> link
+    for (int i = k; i > 0; i = chain.parent[i])
+      path.insert(path.begin(), i);
     Pose12 T;
     std::copy(chain.base_pose, chain.base_pose + 12, T.begin());
-    for (int i = 1; i <= k; ++i)
+    for (const int i : path)
     {
       Pose12 O;
       std::copy(chain.joint_origin[i], chain.joint_origin[i] + 12, O.begin());
@@ -770,8 +770,13 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
     if (a && b)
       throw std::runtime_error("Currently two adjacent fixed steps are not supported in collision term.");
   }
-  if (env->collision_spheres.empty() || static_cast<int>(env->collision_spheres.size()) > THIP_MAX_SPHERES)
-    unsupported("a collision model with " + std::to_string(env->collision_spheres.size()) + " spheres");
+  // the robot spheres on the group's links (the other robot links are outside the joint group)
+  std::vector<const CollisionSphere*> spheres;
+  for (const auto& cs : env->collision_spheres)
+    if (prob.GetKin()->linkIndex(cs.link) > 0)
+      spheres.push_back(&cs);
+  if (spheres.empty() || static_cast<int>(spheres.size()) > THIP_MAX_SPHERES)
+    unsupported("a collision model with " + std::to_string(spheres.size()) + " spheres");
   if (static_cast<int>(env->scene.size()) > THIP_MAX_PRIMS)
     unsupported("a scene of more than " + std::to_string(THIP_MAX_PRIMS) + " primitives");
   if (static_cast<int>(fixed_steps.size()) > THIP_MAX_STEPS)
@@ -790,11 +795,11 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
   // DISCRETE: SingleTimestepCollisionEvaluator per free waypoint (:1782-1796, :1842-1856)
   d.coll_continuous = (evaluator_type == 1) ? 2 : (evaluator_type >= 3) ? 1 : 0;
   d.coll_lvs = (evaluator_type == 3) ? 1.7976931348623157e308 : longest_valid_segment_length;
-  d.n_spheres = static_cast<int>(env->collision_spheres.size());
+  d.n_spheres = static_cast<int>(spheres.size());
   for (int s = 0; s < d.n_spheres; ++s)
   {
-    const CollisionSphere& cs = env->collision_spheres[static_cast<std::size_t>(s)];
-    d.sphere_link[s] = cs.link;
+    const CollisionSphere& cs = *spheres[static_cast<std::size_t>(s)];
+    d.sphere_link[s] = prob.GetKin()->linkIndex(cs.link);
     for (int i = 0; i < 3; ++i)
       d.sphere_center[s][i] = cs.center[i];
     d.sphere_radius[s] = cs.radius;

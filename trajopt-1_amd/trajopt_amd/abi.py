@@ -10,10 +10,10 @@ import ctypes as C
 import os
 from pathlib import Path
 
-MAX_DOF = 8
-MAX_LINKS = 24
+MAX_DOF = 16
+MAX_LINKS = 32
 MAX_STEPS = 64
-MAX_CART = 64
+MAX_CART = 128
 MAX_SPHERES = 32
 MAX_PRIMS = 16
 MAX_JPOS = 8
@@ -43,6 +43,7 @@ class Chain(C.Structure):
         ("base_pose", C.c_double * 12),
         ("joint_type", C.c_int * MAX_LINKS),
         ("joint_dof", C.c_int * MAX_LINKS),
+        ("parent", C.c_int * MAX_LINKS),
         ("joint_origin", _D12 * MAX_LINKS),
         ("joint_axis", _D3 * MAX_LINKS),
         ("lower", C.c_double * MAX_DOF),

@@ -106,12 +106,17 @@ def _quat_wxyz(R):
 
 
 def workload_to_json(wl, b: int) -> str:
-    """Problem b of a synthetic workload (configs A, B, C, J) in the
+    """Problem b of a synthetic workload (configs A, B, C, E, J) in the
     reference's TrajOptRequest JSON format: given_traj init, joint_vel cost,
     cart_pose terms with target_frame torso_lift_link and the target as
-    target_frame_offset, joint_pos terms, and the LVS_DISCRETE collision term."""
+    target_frame_offset, joint_pos terms, and the collision term (evaluator
+    LVS_DISCRETE, LVS_CONTINUOUS or DISCRETE).  Config E's 14-DoF chain is the
+    both_arms group, its tool frames links 11 (left) and 22 (right)."""
     d = wl.desc
     N, D = wl.n_steps, wl.n_dof
+    dual = d.chain.n_dof == 14 and d.chain.n_links == 23
+    manip = "both_arms" if dual else "right_arm"
+    tool_name = {11: "l_gripper_tool_frame", 22: "r_gripper_tool_frame"} if dual else {11: "r_gripper_tool_frame"}
     costs, cnts = [], []
     if d.jv_enabled:
         costs.append({"type": "joint_vel", "params": {
@@ -120,7 +125,8 @@ def workload_to_json(wl, b: int) -> str:
     for k in range(d.n_cart):
         T = np.asarray(wl.targets[b, k]).reshape(3, 4)
         term = {"type": "cart_pose", "params": {
-            "timestep": d.cart_step[k], "source_frame": "r_gripper_tool_frame", "target_frame": "torso_lift_link",
+            "timestep": d.cart_step[k], "source_frame": tool_name[d.cart_source_link[k]],
+            "target_frame": "torso_lift_link",
             "pos_coeffs": [d.cart_pos_coeffs[k][i] for i in range(3)],
             "rot_coeffs": [d.cart_rot_coeffs[k][i] for i in range(3)],
             "target_frame_offset_xyz": T[:, 3].tolist(), "target_frame_offset_wxyz": _quat_wxyz(T[:, :3])}}
@@ -134,13 +140,14 @@ def workload_to_json(wl, b: int) -> str:
         (cnts if d.jpos_is_cnt[k] else costs).append(term)
     if d.coll_enabled:
         term = {"type": "collision", "params": {
-            "coeffs": d.coll_coeff, "dist_pen": d.coll_margin, "evaluator_type": 2,
+            "coeffs": d.coll_coeff, "dist_pen": d.coll_margin,
+            "evaluator_type": {0: 2, 1: 4, 2: 1}[d.coll_continuous],
             "first_step": d.coll_first_step, "last_step": d.coll_last_step if d.coll_last_step >= 0 else N - 1,
             "fixed_steps": [d.coll_fixed_steps[i] for i in range(d.coll_n_fixed)],
             "longest_valid_segment_length": d.coll_lvs}}
         (cnts if d.coll_is_cnt else costs).append(term)
     doc = {
-        "basic_info": {"n_steps": N, "manip": "right_arm",
+        "basic_info": {"n_steps": N, "manip": manip,
                        "fixed_timesteps": [d.fixed_steps[i] for i in range(d.n_fixed)]},
         "costs": costs,
         "constraints": cnts,

@@ -25,6 +25,11 @@ Configs (BASELINE.json):
      *squared* error (trajectory_costs.cpp:162-171) while the model's is
      linear, so the trust region shrinks and the penalty loop runs out in the
      reference too (OPT_PENALTY_ITERATION_LIMIT).
+  E  14-DoF PR2 dual arm (robots.pr2_both_arms: both arms as one joint group,
+     a tree branching at torso_lift_link), 50 steps, JointVel cost, CartPose
+     ABS costs for both tool frames at t = 1..49, 10-primitive scene near the
+     reference path of either arm and the LVS_CONTINUOUS (swept-volume)
+     collision cost on 2 x 14 arm spheres (BASELINE.json configs[4]).
 """
 from __future__ import annotations
 
@@ -34,7 +39,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import abi
-from .robots import PR2_TOOL_LINK, ROBOTS, _to44, chain_limits, fwd_kin
+from .robots import PR2_BOTH_TOOL_LINKS, PR2_TOOL_LINK, ROBOTS, _to44, chain_limits, fwd_kin, pr2_both_arms
 
 SEED_BASE = 20261015
 _MASK = (1 << 64) - 1
@@ -148,6 +153,9 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
         N = n_steps or 30
     elif config == "J":
         N = n_steps or 10
+    elif config == "E":
+        N = n_steps or 50
+        robot = "both_arms"
     else:
         raise ValueError(f"unknown config {config}")
     d = base_desc(N, robot)
@@ -160,6 +168,12 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
         _add_cart(d, 0, N - 1, True, tool)
     elif config == "J":
         d.n_cart = 0
+    elif config == "E":
+        # both tool frames at every step after the first (cost_infos order: left, then right, per step)
+        d.n_cart = 2 * (N - 1)
+        for k, t in enumerate(range(1, N)):
+            for a, tl in enumerate(PR2_BOTH_TOOL_LINKS):
+                _add_cart(d, 2 * k + a, t, False, tl)
     else:
         d.n_cart = N - 1
         for k, t in enumerate(range(1, N)):
@@ -167,6 +181,10 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
     if config == "C":
         from .scene import add_collision_model
         add_collision_model(d, link_offset)
+    if config == "E":
+        from .scene import add_collision_model
+        add_collision_model(d, link_offsets=(0, PR2_BOTH_TOOL_LINKS[0]))
+        d.coll_continuous = 1  # LVS_CONTINUOUS (CastCollisionEvaluator)
     jpos_targets = None
     if config == "J":
         q_lo = np.where(types == abi.JOINT_CONTINUOUS, -math.pi, lo)
@@ -209,8 +227,8 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
             targets[b, 0] = _pose12_in_root(chain, q_ref[(N - 1) // 2], tool)
         else:
             for k in range(d.n_cart):
-                targets[b, k] = _pose12_in_root(chain, q_ref[d.cart_step[k]], tool)
-        if config == "C":
+                targets[b, k] = _pose12_in_root(chain, q_ref[d.cart_step[k]], d.cart_source_link[k])
+        if config in ("C", "E"):
             from .scene import make_scene
             scene[b] = make_scene(rng, chain, q_ref, d, link_offset)
     return Workload(config, d, init, targets, scene, q_refs, jpos_targets)

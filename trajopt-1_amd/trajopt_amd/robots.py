@@ -7,6 +7,15 @@ shoulder_lift 1513-1523, upper_arm_roll 1545-1550, elbow_flex 1702-1712,
 forearm_roll 1655-1664, wrist_flex 1779-1788, wrist_roll 1811-1820, tool
 1908-1911; base chain base_footprint->base_link 121-124, torso 735-744 with
 the torso joint at 0).  Continuous joints get +-4 pi variable bounds.
+
+PR2 both arms (config E, 14 DoF): the reference's left_arm and right_arm
+groups (pr2.srdf:12-17) as one joint group branching at torso_lift_link, left
+arm joints first (l_shoulder_pan 2396-2402, l_shoulder_lift 2430-2436,
+l_upper_arm_roll 2462-2468, l_elbow_flex 2619-2625, l_forearm_roll
+2572-2578, l_wrist_flex 2696-2702, l_wrist_roll 2728-2733, tool 2825-2828:
+the right arm mirrored in y, with its own limits).  The reference's SRDF has
+no 14-joint group (full_body adds the torso, pr2.srdf:54-70), so the group is
+named "both_arms" here.
 """
 from __future__ import annotations
 
@@ -38,6 +47,19 @@ PR2_RIGHT_ARM = [
     ("r_gripper_palm_joint", JOINT_FIXED, (0.0, 0.0, 0.0), None, None),
     ("r_gripper_tool_joint", JOINT_FIXED, (0.18, 0.0, 0.0), None, None),
 ]
+PR2_LEFT_ARM = [
+    ("l_shoulder_pan_joint", JOINT_REVOLUTE, (0.0, 0.188, 0.0), (0, 0, 1), (-0.714601836603, 2.2853981634)),
+    ("l_shoulder_lift_joint", JOINT_REVOLUTE, (0.1, 0.0, 0.0), (0, 1, 0), (-0.5236, 1.3963)),
+    ("l_upper_arm_roll_joint", JOINT_REVOLUTE, (0.0, 0.0, 0.0), (1, 0, 0), (-0.8, 3.9)),
+    ("l_upper_arm_joint", JOINT_FIXED, (0.0, 0.0, 0.0), None, None),
+    ("l_elbow_flex_joint", JOINT_REVOLUTE, (0.4, 0.0, 0.0), (0, 1, 0), (-2.3213, 0.0)),
+    ("l_forearm_roll_joint", JOINT_CONTINUOUS, (0.0, 0.0, 0.0), (1, 0, 0), (-4 * math.pi, 4 * math.pi)),
+    ("l_forearm_joint", JOINT_FIXED, (0.0, 0.0, 0.0), None, None),
+    ("l_wrist_flex_joint", JOINT_REVOLUTE, (0.321, 0.0, 0.0), (0, 1, 0), (-2.18, 0.0)),
+    ("l_wrist_roll_joint", JOINT_CONTINUOUS, (0.0, 0.0, 0.0), (1, 0, 0), (-4 * math.pi, 4 * math.pi)),
+    ("l_gripper_palm_joint", JOINT_FIXED, (0.0, 0.0, 0.0), None, None),
+    ("l_gripper_tool_joint", JOINT_FIXED, (0.18, 0.0, 0.0), None, None),
+]
 # world pose of torso_lift_link: base_footprint -> base_link (0,0,0.051) -> torso (-0.05,0,0.739675), q_torso = 0
 PR2_TORSO_WORLD = (-0.05, 0.0, 0.051 + 0.739675)
 PR2_TOOL_LINK = 11  # r_gripper_tool_frame
@@ -59,6 +81,13 @@ def pr2_torso_right_arm() -> Chain:
     return _chain(PR2_BASE_LINK_WORLD, [PR2_TORSO_JOINT] + PR2_RIGHT_ARM)
 
 
+def pr2_both_arms() -> Chain:
+    """14-DoF tree: links 1-11 the left arm (l_gripper_tool_frame = 11), links
+    12-22 the right arm (r_gripper_tool_frame = 22), both off the root."""
+    return _chain(PR2_TORSO_WORLD, PR2_LEFT_ARM + PR2_RIGHT_ARM,
+                  parents=[0] + list(range(1, 11)) + [0] + list(range(12, 22)))
+
+
 def pr2_right_arm_6dof() -> Chain:
     joints = [(n, JOINT_FIXED, xyz, None, None) if n == "r_wrist_roll_joint" else (n, t, xyz, ax, lim)
               for n, t, xyz, ax, lim in PR2_RIGHT_ARM]
@@ -69,12 +98,18 @@ ROBOTS = {
     "right_arm": (pr2_right_arm, PR2_TOOL_LINK, 0),
     "torso_right_arm": (pr2_torso_right_arm, PR2_TOOL_LINK + 1, 1),
     "right_arm_6dof": (pr2_right_arm_6dof, PR2_TOOL_LINK, 0),
+    "both_arms": (pr2_both_arms, 22, 0),  # config E; its CartPose terms use both tool links
 }
+# both_arms (config E): tool links of the two arms
+PR2_BOTH_TOOL_LINKS = (11, 22)
 
 
-def _chain(base_xyz, joints) -> Chain:
+def _chain(base_xyz, joints, parents=None) -> Chain:
+    """Joint k (1-based) attaches link k to link parents[k - 1] (default k - 1)."""
     c = Chain()
     c.n_links = len(joints) + 1
+    for k in range(1, c.n_links):
+        c.parent[k] = (k - 1) if parents is None else parents[k - 1]
     base = _pose(base_xyz)
     for i in range(12):
         c.base_pose[i] = base[i]
@@ -141,7 +176,7 @@ def fwd_kin(c: Chain, q):
     data generation only)."""
     T = [_to44(list(c.base_pose))]
     for k in range(1, c.n_links):
-        t = T[-1] @ _to44(list(c.joint_origin[k]))
+        t = T[c.parent[k]] @ _to44(list(c.joint_origin[k]))
         jt = c.joint_type[k]
         if jt in (JOINT_REVOLUTE, JOINT_CONTINUOUS):
             M = np.eye(4)

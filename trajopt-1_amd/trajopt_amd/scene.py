@@ -50,9 +50,21 @@ N_PRIMS = 10
 MARGIN, COEFF, BUFFER, LVS = 0.025, 20.0, 0.05, 0.05
 
 
-def add_collision_model(d: abi.ProblemDesc, link_offset: int = 0):
+def arm_spheres(link_offsets=(0,)):
+    """PR2_ARM_SPHERES once per arm, the arm's links shifted by its offset (both_arms: the left arm at
+    links 1-11, the right arm at 12-22, offsets (0, 11))."""
+    return [(link + off, c, r) for off in link_offsets for link, c, r in PR2_ARM_SPHERES]
+
+
+def desc_spheres(d: abi.ProblemDesc):
+    """The (link, center, radius) spheres of a descriptor."""
+    return [(d.sphere_link[s], tuple(d.sphere_center[s][i] for i in range(3)), d.sphere_radius[s])
+            for s in range(d.n_spheres)]
+
+
+def add_collision_model(d: abi.ProblemDesc, link_offset: int = 0, link_offsets=None):
     """LVS_DISCRETE collision cost over all step pairs, step 0 fixed.  link_offset shifts the sphere links
-    for chains with extra links before the arm (robots.ROBOTS)."""
+    for chains with extra links before the arm (robots.ROBOTS); link_offsets lists one offset per arm."""
     d.coll_enabled = 1
     d.coll_is_cnt = 0
     d.coll_first_step = 0
@@ -63,9 +75,10 @@ def add_collision_model(d: abi.ProblemDesc, link_offset: int = 0):
     d.coll_coeff = COEFF
     d.coll_buffer = BUFFER
     d.coll_lvs = LVS
-    d.n_spheres = len(PR2_ARM_SPHERES)
-    for s, (link, c, r) in enumerate(PR2_ARM_SPHERES):
-        d.sphere_link[s] = link + link_offset
+    spheres = arm_spheres(link_offsets if link_offsets is not None else (link_offset,))
+    d.n_spheres = len(spheres)
+    for s, (link, c, r) in enumerate(spheres):
+        d.sphere_link[s] = link
         for i in range(3):
             d.sphere_center[s][i] = c[i]
         d.sphere_radius[s] = r
@@ -89,22 +102,25 @@ def _rotation(rng):
     ])
 
 
-def sphere_centers(chain, q, link_offset: int = 0):
-    """World centers of the robot spheres at joint values q."""
+def sphere_centers(chain, q, link_offset: int = 0, spheres=None):
+    """World centers of the robot spheres at joint values q (spheres: (link, center, radius) with chain
+    link indices; default PR2_ARM_SPHERES shifted by link_offset)."""
     T = fwd_kin(chain, q)
-    return np.array([T[link + link_offset][:3, :3] @ np.array(c) + T[link + link_offset][:3, 3]
-                     for link, c, _ in PR2_ARM_SPHERES])
+    if spheres is None:
+        spheres = arm_spheres((link_offset,))
+    return np.array([T[link][:3, :3] @ np.array(c) + T[link][:3, 3] for link, c, _ in spheres])
 
 
 def make_scene(rng, chain, q_ref, d, link_offset: int = 0) -> np.ndarray:
-    """10 primitive records near the reference path of one problem."""
+    """10 primitive records near the reference path of one problem (near the descriptor's robot spheres)."""
     N = q_ref.shape[0]
     prims = np.zeros((N_PRIMS, 16))
-    path = [sphere_centers(chain, q_ref[t], link_offset) for t in range(N)]
-    radii = [r for _, _, r in PR2_ARM_SPHERES]
+    spheres = desc_spheres(d)
+    path = [sphere_centers(chain, q_ref[t], spheres=spheres) for t in range(N)]
+    radii = [r for _, _, r in spheres]
     for k in range(N_PRIMS):
         for _attempt in range(64):
-            rec = _draw_prim(rng, k, N, path)
+            rec = _draw_prim(rng, k, N, path, radii)
             if all(sphere_prim_distance(c[s], radii[s], rec)[0] > MARGIN + BUFFER
                    for c in path for s in range(len(radii))):
                 break
@@ -112,11 +128,11 @@ def make_scene(rng, chain, q_ref, d, link_offset: int = 0) -> np.ndarray:
     return prims
 
 
-def _draw_prim(rng, k, N, path):
+def _draw_prim(rng, k, N, path, radii):
     rec = np.zeros(16)
     if True:  # one placement draw
         t = min(int(rng.uniform() * N), N - 1)
-        s = min(int(rng.uniform() * len(PR2_ARM_SPHERES)), len(PR2_ARM_SPHERES) - 1)
+        s = min(int(rng.uniform() * len(radii)), len(radii) - 1)
         anchor = path[t][s]
         direction = _unit(rng)
         if k < 4:
@@ -131,7 +147,7 @@ def _draw_prim(rng, k, N, path):
             half = rng.uniform(0.05, 0.15)
             cap_r = rng.uniform(0.03, 0.06)
             bound = half + cap_r
-        center = anchor + direction * (PR2_ARM_SPHERES[s][2] + bound + rng.uniform(0.08, 0.2))
+        center = anchor + direction * (radii[s] + bound + rng.uniform(0.08, 0.2))
         if k < 4:
             rec[0] = abi.PRIM_SPHERE
             rec[1:4] = center
