@@ -37,7 +37,7 @@ print(f"shader clock ~{mhz:.0f} MHz; per problem: admm {admm.mean():.0f} (max {a
 slowest = int(np.argmax(pf[:, 14]))
 print(f"slowest problem {slowest}: {pf[slowest, 14] / 100:.0f} us wall, admm {admm[slowest]:.0f}")
 tot = pf[:, 13].sum()
-for k, name in [kv for kv in enumerate(BatchTrustRegionSQP.PROFILE_SLOTS) if kv[0] != 14 and not kv[1].startswith('unused')]:
+for k, name in [kv for kv in enumerate(BatchTrustRegionSQP.PROFILE_SLOTS) if kv[0] != 14 and not kv[1].startswith('unused') and not kv[1].startswith('n_')]:
     v = pf[:, k].sum()
     per_admm = v / admm.sum()
     print(f"  {k:2d} {name:<16} {100 * v / tot:6.1f}%   {per_admm:10.0f} cyc/admm-iter   "
@@ -52,3 +52,5 @@ for b in np.argsort(-pf[:, 14])[:4]:
     print(f"  problem {b}: {pf[b, 14] / 100:.0f} us, admm {admm[b]:.0f}, qp {qps[b]:.0f}, sqp {sqp[b]:.0f}, "
           f"mean hinge rows {nh_avg[b]:.0f}, contact rows {res[b].n_contact_rows}\n    {parts}")
 print(f"mean hinge rows per ADMM iteration (all): {nh_avg.mean():.1f}, max {nh_avg.max():.0f}")
+print(f"per QP: full primal-infeasibility checks {pf[:, 27].sum() / qps.sum():.2f}, "
+      f"full dual-infeasibility checks {pf[:, 28].sum() / qps.sum():.2f}, factorisations {pf[:, 29].sum() / qps.sum():.2f}")

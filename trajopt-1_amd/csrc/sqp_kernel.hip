@@ -137,13 +137,9 @@ struct ProfScope
 #define PROF_CAT(a, b) PROF_CAT2(a, b)
 #define PROF(slot) ProfScope PROF_CAT(prof_scope_, __LINE__)(c, slot)
 
-__device__ __forceinline__ double wave_max(double v)
-{
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-    v = fmax(v, __shfl_xor(v, o));
-  return v;
-}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v);
+__device__ __forceinline__ double wave_max(double v);
 __device__ __forceinline__ double wave_sum(double v)
 {
 #pragma unroll
@@ -176,6 +172,27 @@ __device__ void block_max(Ctx& c, double (&v)[K])
   for (int k = 0; k < K; ++k)
     v[k] = c.s->bc[k];
   BSYNC();
+}
+
+// two simultaneous block sums (wave_sum order per value)
+__device__ void block_sum2(Ctx& c, double& a, double& b)
+{
+  const double ra = wave_sum(a), rb = wave_sum(b);
+  if (c.lane == 0)
+  {
+    c.s->red[c.wave * 16] = ra;
+    c.s->red[c.wave * 16 + 1] = rb;
+  }
+  BSYNC();
+  double sa = 0, sb = 0;
+  for (int wv = 0; wv < kWaves; ++wv)
+  {
+    sa += c.s->red[wv * 16];
+    sb += c.s->red[wv * 16 + 1];
+  }
+  BSYNC();
+  a = sa;
+  b = sb;
 }
 
 __device__ double block_sum(Ctx& c, double v)
@@ -1755,6 +1772,8 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
     }
   }
   BSYNC();
+  if (c.tid == 0 && c.s->prof)
+    c.s->prof[29] += 1;  // factor calls (diagnostic count)
   const bool ok = (bad == 0);
   BSYNC();
   return ok;
@@ -1814,6 +1833,28 @@ __device__ __forceinline__ double cross_octet_sum(double v)
     const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
     const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
     v = __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+  }
+  return v;
+}
+
+// max over the wave: DPP / permlane exchanges in registers (the octet and
+// cross-octet patterns of the chain) instead of six ds_bpermute round trips;
+// max is exact, so the order is immaterial
+__device__ __forceinline__ double wave_max(double v)
+{
+  v = fmax(v, dpp_f64<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmax(v, dpp_f64<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fmax(v, dpp_f64<0x141>(v));  // row_half_mirror
+  v = fmax(v, dpp_f64<0x128>(v));  // row_ror:8
+  {
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+    v = fmax(__hiloint2double(hi[0], lo[0]), __hiloint2double(hi[1], lo[1]));
+  }
+  {
+    const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+    v = fmax(__hiloint2double(hi[0], lo[0]), __hiloint2double(hi[1], lo[1]));
   }
   return v;
 }
@@ -2442,6 +2483,11 @@ struct Norms
   double prim_res, dual_res;
   double zE, axE, qD, atyD, pxD;  // scaled-for-termination norms
   double pr, dr, z, ax, q, aty, px;  // raw (scaled-space) norms for rho estimate
+  // the infeasibility certificates' first tests (is_primal_infeasible /
+  // is_dual_infeasible), precomputed by the ADMM segment when inf_ready:
+  // max |E dy|, sum u (dy)+ + l (dy)- over the clipped delta y, max |D dx|, q'dx
+  int inf_ready;
+  double ndy, lhs, ndx, qdx;
 };
 
 __device__ void compute_residuals(Ctx& c, const double* x, const double* z, const double* y, Norms& nm)
@@ -2483,6 +2529,7 @@ __device__ void compute_residuals(Ctx& c, const double* x, const double* z, cons
     v[11] = fmax(v[11], fmax(fabs(Q[col]), fmax(fabs(aty), fabs(px))));
   }
   block_max<12>(c, v);
+  nm.inf_ready = 0;
   nm.prim_res = (c.m() > 0) ? v[0] : 0.0;
   nm.zE = v[1];
   nm.axE = v[2];
@@ -2499,6 +2546,8 @@ __device__ void compute_residuals(Ctx& c, const double* x, const double* z, cons
 
 __device__ bool is_primal_infeasible(Ctx& c, double eps)
 {
+  if (c.tid == 0 && c.s->prof)
+    c.s->prof[27] += 1;  // calls (diagnostic count)
   double* DY = c.a(A_DY);
   const double *Lo = c.a(A_L), *Up = c.a(A_U), *E = c.a(A_E), *DS = c.a(A_DS);
   double nv[1] = { 0 };
@@ -2535,6 +2584,8 @@ __device__ bool is_primal_infeasible(Ctx& c, double eps)
 
 __device__ bool is_dual_infeasible(Ctx& c, double eps)
 {
+  if (c.tid == 0 && c.s->prof)
+    c.s->prof[28] += 1;  // calls (diagnostic count)
   const double *DX = c.a(A_DX), *DS = c.a(A_DS), *Q = c.a(A_Q), *E = c.a(A_E), *Lo = c.a(A_L), *Up = c.a(A_U);
   double nv[1] = { 0 };
   FOR(col, c.nc()) nv[0] = fmax(nv[0], fabs(DS[col] * DX[col]));
@@ -2585,12 +2636,16 @@ __device__ bool check_termination(Ctx& c, const Norms& nm, bool approx)
     const double eps_prim = ea + er * fmax(nm.zE, nm.axE);
     if (nm.prim_res < eps_prim)
       prim_ok = true;
+    else if (nm.inf_ready && (!(nm.ndy > kDivTol) || !(nm.lhs < epi * nm.ndy)))
+      pinf = false;  // is_primal_infeasible's first two tests, from the segment
     else
       pinf = is_primal_infeasible(c, epi);
   }
   const double eps_dual = ea + er * (c.s->cinv * fmax(fmax(nm.qD, nm.atyD), nm.pxD));
   if (nm.dual_res < eps_dual)
     dual_ok = true;
+  else if (nm.inf_ready && (!(nm.ndx > kDivTol) || !(nm.qdx < c.s->c * edi * nm.ndx)))
+    dinf = false;  // is_dual_infeasible's first two tests, from the segment
   else
     dinf = is_dual_infeasible(c, edi);
   int st = 0;
@@ -2871,7 +2926,7 @@ __device__ __forceinline__ void admm_row_update(double& z, double& y, double& dy
 }
 
 template <int CS, int AS>
-__device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
+__device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
 {
   PROF(0);
   const Layout& L = c.L;
@@ -3303,6 +3358,174 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
     pf[17] += lap17;
     pf[18] += lap18;
   }
+  // residuals at the segment's last iterate (compute_residuals' quantities,
+  // with its arithmetic order), from the state in registers: x of the
+  // waypoint columns into YV and y of the CartPose / hinge rows into MR, one
+  // barrier, the hinge share of A'y as chunk sums (phase B's gather on y),
+  // then every owner's rows (A x - z) and columns (q + P x + A'y)
+  if (res)
+  {
+    PROF(1);
+#pragma unroll
+    for (int u = 0; u < CS; ++u)
+      if (cact[u])
+        lds(YV)[ccol[u]] = cx[u];
+#pragma unroll
+    for (int u = 0; u < AS; ++u)
+      if (aact[u])
+        MRl[c.tid + kBlock * u] = ayr[u];
+    for (int h = c.tid; h < nh; h += kBlock)
+      MRl[nr + h] = HPK[2 * nh + h];
+    BSYNC();
+    if (nh > 0)
+    {
+      if (hct_l)
+        hinge_gather_seg(lds(static_cast<const double*>(HCT)));
+      else
+        hinge_gather_seg(gbl(static_cast<const double*>(HCT)));
+      BSYNC();
+    }
+    const double *E = c.a(A_E), *DS = c.a(A_DS), *PD = c.a(A_PD), *PO = c.a(A_PO);
+    // v[12] = max |E dy| and v[13] = max |D dx| over the clipped delta y / delta x
+    // of the last iteration (is_primal_infeasible / is_dual_infeasible)
+    double v[14] = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
+    double lhs = 0.0, qdx = 0.0;
+    auto inf_row = [&](double dy, double lo, double up, double e) {
+      if (up > kInf * kMinScal)
+        dy = (lo < -kInf * kMinScal) ? 0.0 : fmin(dy, 0.0);
+      else if (lo < -kInf * kMinScal)
+        dy = fmax(dy, 0.0);
+      v[12] = fmax(v[12], fabs(e * dy));
+      lhs += up * fmax(dy, 0.0) + lo * fmin(dy, 0.0);
+    };
+    auto inf_col = [&](double dx, double q, double ds) {
+      v[13] = fmax(v[13], fabs(ds * dx));
+      qdx += q * dx;
+    };
+    auto row_terms = [&](double ax, double z, double e) {
+      const double pr = ax - z;
+      const double einv = 1.0 / e;
+      v[0] = fmax(v[0], fabs(einv * pr));
+      v[1] = fmax(v[1], fabs(einv * z));
+      v[2] = fmax(v[2], fabs(einv * ax));
+      v[3] = fmax(v[3], fabs(pr));
+      v[4] = fmax(v[4], fabs(z));
+      v[5] = fmax(v[5], fabs(ax));
+    };
+    auto col_terms = [&](double q, double px, double aty, double ds) {
+      const double dr = q + px + aty;
+      const double dinv = 1.0 / ds;
+      v[6] = fmax(v[6], fabs(dinv * dr));
+      v[7] = fmax(v[7], fabs(dinv * q));
+      v[8] = fmax(v[8], fabs(dinv * aty));
+      v[9] = fmax(v[9], fabs(dinv * px));
+      v[10] = fmax(v[10], fabs(dr));
+      v[11] = fmax(v[11], fmax(fabs(q), fmax(fabs(aty), fabs(px))));
+    };
+#pragma unroll
+    for (int u = 0; u < CS; ++u)
+      if (cact[u])
+      {
+        const int col = ccol[u], br = nr + col, t = col / D;
+        const double eb = E[br], ds = DS[col];
+        row_terms(cbs[u] * cx[u], czb[u], eb);
+        inf_row(cdyb[u], clb[u], cub[u], eb);
+        inf_col(cdx[u], cq[u], ds);
+        if (cfr[u] >= 0)
+        {
+          const double ef = E[cfr[u]];
+          row_terms(cfs[u] * cx[u], czf[u], ef);
+          inf_row(cdyf[u], clf[u], cuf[u], ef);
+        }
+        // col_px
+        double px = PD[col] * cx[u];
+        if (t < N - 1)
+          px += PO[col] * lds(YV)[col + D];
+        if (t > 0)
+          px += PO[col - D] * lds(YV)[col - D];
+        // col_aty (chunked)
+        double aty = cbs[u] * cyb[u];
+        if (cfr[u] >= 0)
+          aty += cfs[u] * cyf[u];
+#pragma unroll
+        for (int p = 0; p < kMaxStepRows; ++p)
+          if (p < cnrow[u])
+            aty += cgs[u][p] * MRl[crow[u][p]];
+        if (nh > 0)
+        {
+          const int j = (c.tid + kBlock * u) & 7;
+          for (int q = chp1[u]; q < chp2[u]; ++q)
+            aty += PARTl[q * 16 + j];
+          for (int q = chp0[u]; q < chp1[u]; ++q)
+            aty += PARTl[q * 16 + D + j];
+        }
+        col_terms(cq[u], px, aty, ds);
+      }
+#pragma unroll
+    for (int u = 0; u < AS; ++u)
+      if (aact[u])
+      {
+        const int a = c.tid + kBlock * u;
+        const int r = nfr + a, ca = nx + 2 * a, brn = nr + ca, brp = brn + 1;
+        const int t = at[u];
+        double ax = 0;
+#pragma unroll
+        for (int j = 0; j < kOct; ++j)
+          if (j < D)
+            ax += ags[u][j] * lds(YV)[t * D + j];
+        ax += awn[u] * axn[u] + awp[u] * axp[u];
+        const double er = E[r], en = E[brn], ep = E[brp], dn = DS[ca], dp = DS[ca + 1];
+        row_terms(ax, azr[u], er);
+        row_terms(absn[u] * axn[u], azbn[u], en);
+        row_terms(absp[u] * axp[u], azbp[u], ep);
+        col_terms(aqn[u], 0.0, absn[u] * aybn[u] + awn[u] * ayr[u], dn);
+        col_terms(aqp[u], 0.0, absp[u] * aybp[u] + awp[u] * ayr[u], dp);
+        inf_row(adyr[u], alr[u], aur[u], er);
+        inf_row(adybn[u], albn[u], aubn[u], en);
+        inf_row(adybp[u], albp[u], aubp[u], ep);
+        inf_col(adxn[u], aqn[u], dn);
+        inf_col(adxp[u], aqp[u], dp);
+      }
+    for (int h = c.tid; h < nh; h += kBlock)
+    {
+      const int rh = mb + 2 * h, col = ncb + h, t0 = static_cast<int>(HPK[12 * nh + h]);
+      const double xh = HPK[4 * nh + h], wh = HPK[7 * nh + h], bsh = HPK[8 * nh + h];
+      double ax = 0, ax1 = 0;
+      for (int k = 0; k < D; ++k)
+      {
+        ax += HC[h * 2 * D + k] * lds(YV)[t0 + k];
+        ax1 += HC[h * 2 * D + D + k] * lds(YV)[t0 + D + k];
+      }
+      ax = ax + ax1 + wh * xh;  // row_ax: hinge_dot + w h
+      const double e0 = E[rh], e1 = E[rh + 1], ds = DS[col];
+      row_terms(ax, HPK[h], e0);
+      row_terms(bsh * xh, HPK[nh + h], e1);
+      col_terms(HPK[9 * nh + h], 0.0, bsh * HPK[3 * nh + h] + wh * HPK[2 * nh + h], ds);
+      // (DY / DX of the last iteration, written by hinge_e)
+      inf_row(DY[rh], Lo[rh], Up[rh], e0);
+      inf_row(DY[rh + 1], Lo[rh + 1], Up[rh + 1], e1);
+      inf_col(DX[col], HPK[9 * nh + h], ds);
+    }
+    block_max<14>(c, v);
+    block_sum2(c, lhs, qdx);
+    res->inf_ready = 1;
+    res->ndy = v[12];
+    res->lhs = lhs;
+    res->ndx = v[13];
+    res->qdx = qdx;
+    res->prim_res = (c.m() > 0) ? v[0] : 0.0;
+    res->zE = v[1];
+    res->axE = v[2];
+    res->pr = v[3];
+    res->z = v[4];
+    res->ax = v[5];
+    res->dual_res = c.s->cinv * v[6];
+    res->qD = v[7];
+    res->atyD = v[8];
+    res->pxD = v[9];
+    res->dr = v[10];
+    res->q = v[11];
+  }
   // write back
 #pragma unroll
   for (int u = 0; u < CS; ++u)
@@ -3354,9 +3577,9 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter)
   BSYNC();
 }
 
-__device__ void admm_iterations(Ctx& c, Solver& sv, int n_iter)
+__device__ void admm_iterations(Ctx& c, Solver& sv, int n_iter, Norms* res)
 {
-  admm_segment<1, 1>(c, sv, n_iter);
+  admm_segment<1, 1>(c, sv, n_iter, res);
 }
 
 __device__ double rho_estimate(Ctx& c, const Norms& nm)
@@ -3597,7 +3820,7 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
                            (os.check_termination ? 4 * os.check_termination : 100) :
                            os.adaptive_rho_interval;
   Norms nm{};
-  bool can_check = false;
+  bool can_check = false, have_res = false;
   int it;
   bool fail = false;
   const int ct = os.check_termination;
@@ -3615,24 +3838,31 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
         stop = min(stop, (it + ct - 1) / ct * ct);
       if (os.adaptive_rho && interval)
         stop = min(stop, (it + interval - 1) / interval * interval);
-      admm_iterations(c, sv, stop - it + 1);
+      // the segment computes the residuals of its last iterate when they are needed
+      const bool want = (ct && stop % ct == 0) || (os.adaptive_rho && interval && stop % interval == 0);
+      admm_iterations(c, sv, stop - it + 1, want ? &nm : nullptr);
+      have_res = want;
       it = stop;
     }
     else
+    {
       admm_step(c, sv);
+      have_res = false;
+    }
     can_check = ct && (it % ct == 0);
     const int cur = c.s->cur;
     const double* xc = c.a(cur ? A_XA1 : A_XA0);
     const double* zc = c.a(cur ? A_Z1 : A_Z0);
     if (can_check)
     {
-      compute_residuals(c, xc, zc, Y, nm);
+      if (!have_res)
+        compute_residuals(c, xc, zc, Y, nm);
       if (check_termination(c, nm, false))
         break;
     }
     if (os.adaptive_rho && interval && (it % interval == 0))
     {
-      if (!can_check)
+      if (!can_check && !have_res)
         compute_residuals(c, xc, zc, Y, nm);
       const double rn = rho_estimate(c, nm);
       const double rho = c.s->rho;

@@ -126,7 +126,7 @@ class BatchTrustRegionSQP:
                      "sqp_total", "sqp_wall_ticks", "seg_B_rhs_linv", "seg_C2_linvT_middle",
                      "seg_hinge_gather", "seg_hinge_E", "coll_count_pass", "coll_rank_pass", "coll_rows", "coll_fk_substates",
                      "seg_fwd_chain_w0", "chain_w0_loads", "chain_w0_serial", "chain_w0_stores",
-                     "unused27", "unused28", "unused29", "unused30", "unused31"]
+                     "n_primal_inf_full", "n_dual_inf_full", "n_factor", "unused30", "unused31"]
 
     def enable_profile(self, on=True):
         self._check(self.lib.thip_debug_profile(self.ctx, 1 if on else 0), "thip_debug_profile")
