@@ -16,7 +16,7 @@ constexpr int kBlock = 256;  // threads per problem workgroup
 constexpr int kWaves = kBlock / 64;
 // dynamic LDS a problem may use (160 KB per CU on gfx950, one workgroup per
 // CU; the rest is the kernel's static LDS)
-constexpr long long kLdsBudgetBytes = 146 * 1024;
+constexpr long long kLdsBudgetBytes = 149 * 1024;
 // CartPose rows per waypoint the register-resident ADMM segment supports
 constexpr int kMaxStepRows = 8;
 // LVS sub-states per step pair the contact scan supports (sphere-center
@@ -162,6 +162,7 @@ struct Layout
   // lds_scratch doubles are the block-solve chain matrices / FK staging.
   int loff[A_COUNT];
   int lds_scratch;
+  int fac_off;  // doubles: factor()'s 4 D x D scratch blocks, inside lds_scratch
   // D > 8 (e.g. the 14-DoF dual arm): the block solve runs one lane per block
   // row and its chain matrices M, N live in HBM (A_CHM), not in the LDS scratch
   int wide;

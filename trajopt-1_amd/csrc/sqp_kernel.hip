@@ -81,6 +81,22 @@ struct Ctl
   int hcp[THIP_MAX_STEPS + 1];  // first hinge chunk of each step pair (admm_segment)
 };
 
+// The kinematic tree, copied into LDS at kernel entry (stage_chain): every
+// FK walk reads its joint origins, axes and types from here.  Read from the
+// descriptor in HBM they were FLAT loads with L2 latency at every joint of
+// every walk (sub-state FK of the contact scans, the CartPose jacobians).
+__shared__ thip_chain g_chain;
+
+__device__ __forceinline__ void stage_chain(const thip_problem_desc* d)
+{
+  static_assert(sizeof(thip_chain) % 4 == 0, "word copy");
+  const int* src = reinterpret_cast<const int*>(&d->chain);
+  int* dst = reinterpret_cast<int*>(&g_chain);
+  for (int w = threadIdx.x; w < static_cast<int>(sizeof(thip_chain) / 4); w += blockDim.x)
+    dst[w] = src[w];
+  __syncthreads();
+}
+
 struct Ctx
 {
   const Layout& L;
@@ -227,7 +243,7 @@ __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
   PROF(5);
   const Layout& L = c.L;
   const int D = L.D;
-  const thip_chain& ch = c.d->chain;
+  const thip_chain& ch = g_chain;
   double* stage = c.big;  // [n_cart][30]: source pose (12), target^-1 (12), err (6)
   const double* tgt = c.a(A_TGT);
   FOR(k, L.n_cart)
@@ -460,7 +476,7 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
   const CollStage& S = *c.cs;
   const Layout& L = c.L;
   const int D = L.D, ns = c.d->n_spheres, P = c.d->n_prims;
-  const thip_chain& ch = c.d->chain;
+  const thip_chain& ch = g_chain;
   const double margin = c.d->coll_margin, buffer = c.d->coll_buffer, coeff = c.d->coll_coeff;
   const double threshold = margin + buffer;  // contact distance after incrementCollisionMargin(buffer)
   double* SCR = c.a(A_CSCR) + (long long)c.wave * kSubCap * ns * 3;
@@ -563,66 +579,63 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       pf22[22] += clock64() - tfk0;
     if (PASS == 0)
     {
-      // counts and cost only: lane = (primitive, sphere), looping over the
-      // sub-states (the primitive and radius are loaded once per lane; the
-      // order of the candidates does not matter for a count and a sum)
+      // counts and cost only: lane = (sub-state, sphere), looping over the
+      // primitives, so every distance call of the wave is for one primitive
+      // (its type branch is uniform, its record a broadcast LDS read) and a
+      // lane loads its sphere centers once; the order of the candidates does
+      // not matter for a count and a sum
       double lcost = 0.0, lcount = 0.0;
-      for (int ps = c.lane; ps < P * ns; ps += 64)
+      const int nsi = ns * nseg;
+      for (int idx = c.lane; idx < nsi + 63; idx += 64)
       {
-        const int p = ps / ns, s = ps - p * ns;
-        double prim[16];
-        for (int e = 0; e < 16; ++e)
-          prim[e] = S.scene[16 * p + e];
+        if (__builtin_amdgcn_readfirstlane(idx - c.lane) >= nsi)
+          break;
+        const bool act = idx < nsi;
+        const int i = act ? idx / ns : 0, s = act ? idx - (idx / ns) * ns : 0;
         const double rad = S.rad[s];
-        constexpr int kU = 8;  // time indices per batch: their center loads are in flight together
-        for (int i0 = 0; i0 < nseg; i0 += kU)
+        double cx[3], cy[3];
         {
-          double cx[kU][3], cy[kU][3];
-#pragma unroll
-          for (int u = 0; u < kU; ++u)
+          const double* cp = SCR + (i * ns + s) * 3;
+          const double* cq = SCR + ((cont ? i + 1 : i) * ns + s) * 3;
+          for (int r = 0; r < 3; ++r)
           {
-            const int i = min(i0 + u, nseg - 1);  // clamped: always a valid address
-            const double* cp = SCR + (i * ns + s) * 3;
-            const double* cq = SCR + ((cont ? i + 1 : i) * ns + s) * 3;
-            for (int r = 0; r < 3; ++r)
-            {
-              cx[u][r] = cp[r];
-              cy[u][r] = cq[r];
-            }
+            cx[r] = cp[r];
+            cy[r] = cq[r];
           }
-#pragma unroll
-          for (int u = 0; u < kU; ++u)
+        }
+        for (int p = 0; p < P; ++p)
+        {
+          double prim[16];
+          for (int e = 0; e < 16; ++e)
+            prim[e] = S.scene[16 * p + e];
+          double dist = 0.0;
+          bool hit = false;
+          int cct = 3;  // CCType of the robot link: 1 Time0, 2 Time1, 3 Between
+          if (act)
           {
-            const int i = i0 + u;
-            double dist = 0.0;
-            bool hit = false;
-            int cct = 3;  // CCType of the robot link: 1 Time0, 2 Time1, 3 Between
-            if (i < nseg)
+            double n[3], pr[3];
+            if (cont)
             {
-              double n[3], pr[3];
-              if (cont)
+              if (swept_lower_bound(cx, cy, rad, prim) < threshold)
               {
-                if (swept_lower_bound(cx[u], cy[u], rad, prim) < threshold)
-                {
-                  double ts;
-                  swept_sphere_prim_distance(cx[u], cy[u], rad, prim, dist, n, pr, ts);
-                  hit = dist < threshold;
-                  cct = (i == 0 && ts == 0.0) ? 1 : ((i + 1 == last && ts == 1.0) ? 2 : 3);
-                }
-              }
-              else
-              {
-                sphere_prim_distance(cx[u], rad, prim, dist, n, pr);
+                double ts;
+                swept_sphere_prim_distance(cx, cy, rad, prim, dist, n, pr, ts);
                 hit = dist < threshold;
-                cct = (i == 0) ? 1 : ((i == last) ? 2 : 3);
+                cct = (i == 0 && ts == 0.0) ? 1 : ((i + 1 == last && ts == 1.0) ? 2 : 3);
               }
             }
-            hit = hit && !(dist > margin + buffer);
-            if (hit && (f0 || f1))
-              hit = (f0 && cct != 1) || (f1 && cct != 2);
-            lcount += hit ? 1.0 : 0.0;
-            lcost += hit ? fmax(margin - dist, 0.0) * coeff : 0.0;
+            else
+            {
+              sphere_prim_distance(cx, rad, prim, dist, n, pr);
+              hit = dist < threshold;
+              cct = (i == 0) ? 1 : ((i == last) ? 2 : 3);
+            }
           }
+          hit = hit && !(dist > margin + buffer);
+          if (hit && (f0 || f1))
+            hit = (f0 && cct != 1) || (f1 && cct != 2);
+          lcount += hit ? 1.0 : 0.0;
+          lcost += hit ? fmax(margin - dist, 0.0) * coeff : 0.0;
         }
       }
       const double cost = wave_sum(lcost);
@@ -993,7 +1006,7 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
     return;
   PROF(21);
   // rows: distance expression k + a_t.x_t + a_t+1.x_t+1 per contact
-  const thip_chain& ch = c.d->chain;
+  const thip_chain& ch = g_chain;
   const int* CONT = c.ia(I_CONT);
   const int* HT = c.ia(I_HT);
   const int* HKD = c.ia(I_HKIND);
@@ -1134,7 +1147,7 @@ __device__ void evaluate(Ctx& c, const double* x, double* costs, double* viols)
   PROF(6);
   const Layout& L = c.L;
   const int D = L.D;
-  const thip_chain& ch = c.d->chain;
+  const thip_chain& ch = g_chain;
   // JointVel: sum_{t,j} c_j (x_{t+1,j} - x_{t,j} - targ_j)^2
   double jv = 0;
   if (c.d->jv_enabled && !L.jv_ineq)
@@ -1664,8 +1677,10 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
   //   Lsub <- O LI_t^T (coupling into the next block), N_t = LI_t^T Lsub^T.
   // Bottom-half matrices are stored at their own waypoint index; the middle
   // stores M_m (top coupling) in M[m] and M'_m (bottom coupling) in Nb[m].
-  __shared__ double Sblk[2][THIP_MAX_DOF * THIP_MAX_DOF];
-  __shared__ double Lsub[2][THIP_MAX_DOF * THIP_MAX_DOF];
+  // per-half block and coupling scratch in the dynamic LDS after the chain
+  // scratch (Layout::fac_off, 4 D x D blocks)
+  double* const Sblk[2] = { c.big + L.fac_off, c.big + L.fac_off + D * D };
+  double* const Lsub[2] = { c.big + L.fac_off + 2 * D * D, c.big + L.fac_off + 3 * D * D };
   __shared__ int bad;
   const int m = L.tw_mid;
   const int DD = D * D;
@@ -3712,7 +3727,7 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   const Layout& L = c.L;
   const int nx = L.nx, D = L.D;
   const thip_osqp_settings& os = c.d->osqp;
-  const thip_chain& ch = c.d->chain;
+  const thip_chain& ch = g_chain;
   const double* X = c.a(A_X);
   double *Lo = c.a(A_L), *Up = c.a(A_U);
   const double *E = c.a(A_E), *GC = c.a(A_GC), *INIT = c.a(A_INIT), *DS = c.a(A_DS);
@@ -4038,7 +4053,7 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
   const thip_sqp_params& P = c.d->sqp;
   double *X = c.a(A_X), *XN = c.a(A_XN);
   double *COST = c.a(A_COST), *VIOL = c.a(A_VIOL), *NCOST = c.a(A_NCOST), *NVIOL = c.a(A_NVIOL), *MU = c.a(A_MU);
-  const thip_chain& ch = c.d->chain;
+  const thip_chain& ch = g_chain;
   // getClosestFeasiblePoint(x, 1e-3)
   FOR(col, nx)
   {
@@ -4414,6 +4429,7 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
   const int b = blockIdx.x;
   if (b >= args.batch)
     return;
+  stage_chain(args.desc);
   const Layout& L = args.L;
   // LDS residency plan (Layout::loff): hot QP arrays live in LDS for the
   // whole launch, the rest in this problem's HBM workspace
@@ -4504,6 +4520,7 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(KernelArgs args, cons
   const int b = blockIdx.x;
   if (b >= args.batch)
     return;
+  stage_chain(args.desc);
   const Layout& L = args.L;
   Ctx c(L, args.T, args.desc, args.ws + (long long)b * L.dstride, args.iws + (long long)b * L.istride, dyn, &ctl);
   c.scene = args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16;
@@ -4549,8 +4566,9 @@ __global__ __launch_bounds__(kBlock) void fwd_kin_kernel(KernelArgs args, const 
   const int b = blockIdx.x;
   if (b >= args.batch)
     return;
+  stage_chain(args.desc);
   const Layout& L = args.L;
-  const thip_chain& ch = args.desc->chain;
+  const thip_chain& ch = g_chain;
   for (int i = threadIdx.x; i < L.N * L.n_links; i += kBlock)
   {
     const int t = i / L.n_links, l = i % L.n_links;
@@ -4576,6 +4594,7 @@ __global__ __launch_bounds__(kBlock) void coll_rows_kernel(KernelArgs args, cons
   const int b = blockIdx.x;
   if (b >= args.batch)
     return;
+  stage_chain(args.desc);
   const Layout& L = args.L;
   Ctx c(L, args.T, args.desc, args.ws + (long long)b * L.dstride, args.iws + (long long)b * L.istride, nullptr,
         &ctl);

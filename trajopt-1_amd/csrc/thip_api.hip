@@ -578,6 +578,8 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
                           A_E,    A_DS,  A_RE, A_PB,  A_PS, A_PR };
     long long used = static_cast<long long>(lds_d);
     used = (used + 7) / 8 * 8;
+    L.fac_off = static_cast<int>(used);  // factor()'s 4 D x D blocks
+    used += (4LL * L.D * L.D + 7) / 8 * 8;
     L.lds_scratch = static_cast<int>(used);
     for (int k = 0; k < A_COUNT; ++k)
       L.loff[k] = -1;
