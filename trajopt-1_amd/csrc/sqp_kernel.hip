@@ -79,6 +79,8 @@ struct Ctl
   int flags;          // sticky THIP_FLAG_* of the run
   long long n_contact_rows, n_hinge_admm, n_substates;
   int hcp[THIP_MAX_STEPS + 1];  // first hinge chunk of each step pair (admm_segment)
+  int subcnt[THIP_MAX_STEPS];       // contact scan: LVS sub-states of each collision unit
+  int suboff[THIP_MAX_STEPS + 1];   // and their prefix (the batched sub-state FK)
 };
 
 // The kinematic tree, copied into LDS at kernel entry (stage_chain): every
@@ -470,6 +472,126 @@ __device__ void coll_stage(Ctx& c)
   BSYNC();
 }
 
+// World centers of every robot sphere at joint values q into dst[s * 3]: one
+// FK walk over the tree; each sphere group's link pose is the walk's prefix
+// (the same operations as chain_fk(.., link, ..)).
+__device__ __forceinline__ void sphere_centers_at(const CollStage& S, const thip_chain& ch, int ngr, const double* q,
+                                                  double* dst0)
+{
+  Pose T;
+  pose_load(T, ch.base_pose);
+  const int last_link = S.grp_link[ngr - 1];
+  int g = 0;
+  for (int k = 1; k <= last_link; ++k)
+  {
+    if (ch.parent[k] != k - 1)  // a branch of the tree: restart from the parent link's pose
+      chain_fk(ch, q, ch.parent[k], T);
+    Pose O, Tn;
+    pose_load(O, ch.joint_origin[k]);
+    pose_mul(T, O, Tn);
+    const int type = ch.joint_type[k];
+    if (type == THIP_JOINT_REVOLUTE || type == THIP_JOINT_CONTINUOUS)
+    {
+      Pose M;
+      rot_axis_angle(ch.joint_axis[k], q[ch.joint_dof[k]], M.r);
+      M.t[0] = M.t[1] = M.t[2] = 0;
+      pose_mul(Tn, M, T);
+    }
+    else if (type == THIP_JOINT_PRISMATIC)
+    {
+      Pose M;
+      const double v = q[ch.joint_dof[k]];
+      M.r[0] = M.r[4] = M.r[8] = 1;
+      M.r[1] = M.r[2] = M.r[3] = M.r[5] = M.r[6] = M.r[7] = 0;
+      M.t[0] = ch.joint_axis[k][0] * v;
+      M.t[1] = ch.joint_axis[k][1] * v;
+      M.t[2] = ch.joint_axis[k][2] * v;
+      pose_mul(Tn, M, T);
+    }
+    else
+      T = Tn;
+    for (; g < ngr && S.grp_link[g] == k; ++g)
+      for (int e = 0; e < S.grp_ns[g]; ++e)
+      {
+        const int s = S.sph_order[S.grp_s0[g] + e];
+        const double* cs = S.ctr + s * 3;
+        double* dst = dst0 + s * 3;
+        for (int r = 0; r < 3; ++r)
+          dst[r] = T.r[r * 3 + 0] * cs[0] + T.r[r * 3 + 1] * cs[1] + T.r[r * 3 + 2] * cs[2] + T.t[r];
+      }
+  }
+}
+
+// The LVS sub-states of every collision unit at x, their prefix in
+// Ctl::suboff, and -- when they number at most kWaves * kSubCap -- the sphere
+// centers of all of them computed by the whole workgroup at once into A_CSCR
+// (unit t's sub-state i at row suboff[t] + i).  A unit of one wave has ~5
+// sub-states, so a per-unit walk keeps ~5 of its 64 lanes busy.  Returns
+// whether the centers were computed (else each wave walks its own units).
+__device__ bool coll_substates_batched(Ctx& c, const double* x)
+{
+  const CollStage& S = *c.cs;
+  const Layout& L = c.L;
+  const int D = L.D, ns = c.d->n_spheres;
+  const bool single = L.coll_single != 0;
+  FOR(u, L.coll_last - L.coll_first)
+  {
+    const int t = L.coll_first + u;
+    int cnt = 0;
+    if (!(single && coll_fixed_step(c, t)))
+    {
+      const double* q0 = x + t * D;
+      cnt = single ? 1 : lvs_count(q0, x + (t + 1) * D, D, c.d->coll_lvs);
+      if (cnt > kSubCap)
+        cnt = 0;  // the unit's overflow is flagged by its wave
+    }
+    c.s->subcnt[t] = cnt;
+  }
+  BSYNC();
+  if (c.tid == 0)
+  {
+    int acc = 0;
+    for (int t = L.coll_first; t < L.coll_last; ++t)
+    {
+      c.s->suboff[t] = acc;
+      acc += c.s->subcnt[t];
+    }
+    c.s->suboff[L.coll_last] = acc;
+  }
+  BSYNC();
+  const int total = c.s->suboff[L.coll_last];
+  if (total > kWaves * kSubCap)
+    return false;
+  long long* pf22 = (c.tid == 0) ? c.s->prof : nullptr;
+  const long long tfk0 = pf22 ? clock64() : 0;
+  double* SCR = c.a(A_CSCR);
+  const thip_chain& ch = g_chain;
+  FOR(j, total)
+  {
+    // the unit holding sub-state j (binary search of the prefix)
+    int lo = L.coll_first, hi = L.coll_last - 1;
+    while (lo < hi)
+    {
+      const int mid = (lo + hi + 1) >> 1;
+      if (c.s->suboff[mid] <= j)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    const int t = lo, i = j - c.s->suboff[t], cnt = c.s->subcnt[t];
+    const double* q0 = x + t * D;
+    const double* q1 = single ? q0 : x + (t + 1) * D;
+    double q[THIP_MAX_DOF];
+    for (int k = 0; k < D; ++k)
+      q[k] = linspaced(cnt, q0[k], q1[k], i);
+    sphere_centers_at(S, ch, c.T.n_groups, q, SCR + (long long)j * ns * 3);
+  }
+  BSYNC();
+  if (pf22)
+    pf22[22] += clock64() - tfk0;
+  return true;
+}
+
 template <int PASS>
 __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
 {
@@ -479,7 +601,8 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
   const thip_chain& ch = g_chain;
   const double margin = c.d->coll_margin, buffer = c.d->coll_buffer, coeff = c.d->coll_coeff;
   const double threshold = margin + buffer;  // contact distance after incrementCollisionMargin(buffer)
-  double* SCR = c.a(A_CSCR) + (long long)c.wave * kSubCap * ns * 3;
+  const bool batched = coll_substates_batched(c, x);
+  double* SCRW = c.a(A_CSCR) + (long long)c.wave * kSubCap * ns * 3;
   int* PCNT = c.ia(I_PCNT);
   double* HCOST = c.a(A_HCOST);
   int* CONT = c.ia(I_CONT);
@@ -520,63 +643,26 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
     const bool cont = c.d->coll_continuous == 1;
     const int nseg = cont ? cnt - 1 : cnt;
     const int last = cnt - 1;
-    long long* pf22 = (c.tid == 0) ? c.s->prof : nullptr;
-    const long long tfk0 = pf22 ? clock64() : 0;
-    for (int isub = c.lane; isub < cnt; isub += 64)
+    // sphere centers of the unit's sub-states: computed by the batched walk,
+    // or here by this wave (one sub-state per lane)
+    const double* SCR = batched ? c.a(A_CSCR) + (long long)c.s->suboff[t] * ns * 3 : SCRW;
+    if (!batched)
     {
-      double q[THIP_MAX_DOF];
-      for (int j = 0; j < D; ++j)
-        q[j] = linspaced(cnt, q0[j], q1[j], isub);
-      // one FK walk up the chain; each group's link pose is the walk's prefix
-      // (the same operations as chain_fk(.., link, ..))
-      Pose T;
-      pose_load(T, ch.base_pose);
-      const int last_link = S.grp_link[ngr - 1];
-      int g = 0;
-      for (int k = 1; k <= last_link; ++k)
+      long long* pf22 = (c.tid == 0) ? c.s->prof : nullptr;
+      const long long tfk0 = pf22 ? clock64() : 0;
+      for (int isub = c.lane; isub < cnt; isub += 64)
       {
-        if (ch.parent[k] != k - 1)  // a branch of the tree: restart from the parent link's pose
-          chain_fk(ch, q, ch.parent[k], T);
-        Pose O, Tn;
-        pose_load(O, ch.joint_origin[k]);
-        pose_mul(T, O, Tn);
-        const int type = ch.joint_type[k];
-        if (type == THIP_JOINT_REVOLUTE || type == THIP_JOINT_CONTINUOUS)
-        {
-          Pose M;
-          rot_axis_angle(ch.joint_axis[k], q[ch.joint_dof[k]], M.r);
-          M.t[0] = M.t[1] = M.t[2] = 0;
-          pose_mul(Tn, M, T);
-        }
-        else if (type == THIP_JOINT_PRISMATIC)
-        {
-          Pose M;
-          const double v = q[ch.joint_dof[k]];
-          M.r[0] = M.r[4] = M.r[8] = 1;
-          M.r[1] = M.r[2] = M.r[3] = M.r[5] = M.r[6] = M.r[7] = 0;
-          M.t[0] = ch.joint_axis[k][0] * v;
-          M.t[1] = ch.joint_axis[k][1] * v;
-          M.t[2] = ch.joint_axis[k][2] * v;
-          pose_mul(Tn, M, T);
-        }
-        else
-          T = Tn;
-        for (; g < ngr && S.grp_link[g] == k; ++g)
-          for (int e = 0; e < S.grp_ns[g]; ++e)
-          {
-            const int s = S.sph_order[S.grp_s0[g] + e];
-            const double* cs = S.ctr + s * 3;
-            double* dst = SCR + (isub * ns + s) * 3;
-            for (int r = 0; r < 3; ++r)
-              dst[r] = T.r[r * 3 + 0] * cs[0] + T.r[r * 3 + 1] * cs[1] + T.r[r * 3 + 2] * cs[2] + T.t[r];
-          }
+        double q[THIP_MAX_DOF];
+        for (int j = 0; j < D; ++j)
+          q[j] = linspaced(cnt, q0[j], q1[j], isub);
+        sphere_centers_at(S, ch, ngr, q, SCRW + (long long)isub * ns * 3);
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (pf22)
+        pf22[22] += clock64() - tfk0;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (pf22)
-      pf22[22] += clock64() - tfk0;
     if (PASS == 0)
     {
       // counts and cost only: lane = (sub-state, sphere), looping over the
