@@ -112,6 +112,7 @@ enum IArr : int
   I_PCNT,      // contacts per step pair (N)
   I_HKIND,     // hinge row kind: 0 collision (margin - dist), 1 affine (static rows) (h_cap)
   I_HSLOT,     // affine hinge rows: merit slot (constraint) or -1 (cost, objective 1) (h_cap)
+  I_HBITS,     // contact scan: hit bit of every candidate of every unit, in the ContactResultMap order
   I_COUNT
 };
 

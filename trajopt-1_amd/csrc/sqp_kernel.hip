@@ -81,6 +81,8 @@ struct Ctl
   int hcp[THIP_MAX_STEPS + 1];  // first hinge chunk of each step pair (admm_segment)
   int subcnt[THIP_MAX_STEPS];       // contact scan: LVS sub-states of each collision unit
   int suboff[THIP_MAX_STEPS + 1];   // and their prefix (the batched sub-state FK)
+  int hboff[THIP_MAX_STEPS + 1];    // first I_HBITS word of each unit (batched scans)
+  int hbits_x;                      // the hit bits are those of the last count pass (batched)
 };
 
 // The kinematic tree, copied into LDS at kernel entry (stage_chain): every
@@ -449,6 +451,8 @@ struct CollStage
   int grp_s0[THIP_MAX_LINKS];
   int grp_link[THIP_MAX_LINKS];
   int sph_order[THIP_MAX_SPHERES];
+  int sph_grp[THIP_MAX_SPHERES];  // inverse of sph_order: group of sphere s
+  int sph_e[THIP_MAX_SPHERES];    // and its position in the group
 };
 
 __device__ void coll_stage(Ctx& c)
@@ -468,6 +472,12 @@ __device__ void coll_stage(Ctx& c)
     S.grp_ns[e] = c.T.grp_ns[e];
     S.grp_s0[e] = c.T.grp_s0[e];
     S.grp_link[e] = c.T.grp_link[e];
+    for (int k = 0; k < c.T.grp_ns[e]; ++k)
+    {
+      const int s = c.T.sph_order[c.T.grp_s0[e] + k];
+      S.sph_grp[s] = e;
+      S.sph_e[s] = k;
+    }
   }
   BSYNC();
 }
@@ -550,13 +560,19 @@ __device__ bool coll_substates_batched(Ctx& c, const double* x)
   BSYNC();
   if (c.tid == 0)
   {
-    int acc = 0;
+    const bool cont = c.d->coll_continuous == 1;
+    int acc = 0, wacc = 0;
     for (int t = L.coll_first; t < L.coll_last; ++t)
     {
       c.s->suboff[t] = acc;
-      acc += c.s->subcnt[t];
+      c.s->hboff[t] = wacc;
+      const int cnt = c.s->subcnt[t];
+      acc += cnt;
+      const int nseg = cont ? cnt - 1 : cnt;
+      wacc += (c.d->n_prims * (nseg > 0 ? nseg : 0) * ns + 63) / 64 * 2;  // whole 64-bit chunks
     }
     c.s->suboff[L.coll_last] = acc;
+    c.s->hboff[L.coll_last] = wacc;
   }
   BSYNC();
   const int total = c.s->suboff[L.coll_last];
@@ -601,7 +617,17 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
   const thip_chain& ch = g_chain;
   const double margin = c.d->coll_margin, buffer = c.d->coll_buffer, coeff = c.d->coll_coeff;
   const double threshold = margin + buffer;  // contact distance after incrementCollisionMargin(buffer)
-  const bool batched = coll_substates_batched(c, x);
+  // the rank pass at the point the count pass just scanned reads the hits it
+  // recorded (I_HBITS) instead of recomputing every candidate's distance
+  const bool use_bits = (PASS == 1) && c.s->hbits_x;
+  const bool batched = use_bits || coll_substates_batched(c, x);
+  if (PASS == 0)
+  {
+    BSYNC();  // every wave past its reads of the previous flag
+    if (c.tid == 0)
+      c.s->hbits_x = batched ? 1 : 0;
+  }
+  unsigned* const HBITS = reinterpret_cast<unsigned*>(c.ia(I_HBITS));
   double* SCRW = c.a(A_CSCR) + (long long)c.wave * kSubCap * ns * 3;
   int* PCNT = c.ia(I_PCNT);
   double* HCOST = c.a(A_HCOST);
@@ -646,6 +672,15 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
     // sphere centers of the unit's sub-states: computed by the batched walk,
     // or here by this wave (one sub-state per lane)
     const double* SCR = batched ? c.a(A_CSCR) + (long long)c.s->suboff[t] * ns * 3 : SCRW;
+    unsigned* const HB = batched ? HBITS + c.s->hboff[t] : nullptr;
+    if (PASS == 0 && HB)
+    {
+      for (int w = c.lane; w < c.s->hboff[t + 1] - c.s->hboff[t]; w += 64)
+        HB[w] = 0u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
     if (!batched)
     {
       long long* pf22 = (c.tid == 0) ? c.s->prof : nullptr;
@@ -722,6 +757,13 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
             hit = (f0 && cct != 1) || (f1 && cct != 2);
           lcount += hit ? 1.0 : 0.0;
           lcost += hit ? fmax(margin - dist, 0.0) * coeff : 0.0;
+          if (hit && HB)
+          {
+            // its index in the rank pass's (group, primitive, sub-state, sphere) order
+            const int g = S.sph_grp[s], gn = S.grp_ns[g];
+            const int cand = P * nseg * S.grp_s0[g] + (p * nseg + i) * gn + S.sph_e[s];
+            atomicOr(HB + (cand >> 5), 1u << (cand & 31));
+          }
         }
       }
       const double cost = wave_sum(lcost);
@@ -749,7 +791,30 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       bool hit = false;
       double dist = 0.0;
       int i = 0, s = 0, p = 0;
-      if (cand < total)
+      if (use_bits)
+      {
+        // the count pass's hits: 64 candidates = two words (each unit's bits
+        // start on a 64-bit boundary)
+        const unsigned w = HB[(c0 >> 5) + (c.lane >> 5)];
+        hit = (cand < total) && ((w >> (c.lane & 31)) & 1u);
+        if (hit)
+        {
+          int rem = cand, g = 0;
+          for (int gg = 0; gg + 1 < ngr; ++gg)
+          {
+            const int sz = P * nseg * S.grp_ns[gg];
+            const bool adv = (g == gg) && (rem >= sz);
+            rem = adv ? rem - sz : rem;
+            g = adv ? g + 1 : g;
+          }
+          const int gn = S.grp_ns[g];
+          p = rem / (nseg * gn);
+          const int r2 = rem % (nseg * gn);
+          i = r2 / gn;
+          s = S.sph_order[S.grp_s0[g] + r2 % gn];
+        }
+      }
+      else if (cand < total)
       {
         // flattened (group, primitive, sub-state, sphere) index; the group
         // walk is uniform, the selects per lane
