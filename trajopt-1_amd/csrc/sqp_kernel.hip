@@ -28,6 +28,9 @@ constexpr double kInf = 1e30;  // OSQP_INFTY
 // lane octets of the block solve: the chain layouts, the register-resident
 // ADMM segment and their unrolled per-dof loops take D <= kOct
 constexpr int kOct = 8;
+// iterations per thread issued together in the generic ADMM step's row and
+// column loops (loads of all of them before any store)
+constexpr int kGenU = 4;
 constexpr double kRhoMin = 1e-6, kRhoMax = 1e6, kRhoTol = 1e-4, kRhoEq = 1e3;
 constexpr double kMinScal = 1e-4, kMaxScal = 1e4;
 constexpr double kDivTol = 1.0 / kInf;
@@ -2025,6 +2028,27 @@ __device__ __forceinline__ double wave_max(double v)
   return v;
 }
 
+// sum_{k in [k0, k1)} a[k * sa] * b[k * sb], in order, for k1 <= THIP_MAX_DOF:
+// all loads issued first (clamped indices), masked accumulation
+template <int KMAX, typename AP, typename BP>
+__device__ __forceinline__ double masked_dot(AP a, int sa, BP b, int sb, int k0, int k1)
+{
+  double av[KMAX], bv[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+  {
+    const int kk = min(k, k1 - 1);
+    av[k] = a[kk * sa];
+    bv[k] = b[kk * sb];
+  }
+  double v = 0;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (k >= k0 && k < k1)
+      v += av[k] * bv[k];
+  return v;
+}
+
 // Block-bidiagonal recurrence v_t = c_t - G_t v_{t-1} (FWD, t = 1..N-1) or
 // v_t = c_t - G_t v_{t+1} (backward, t = N-2..0), run by one wave.  Lane
 // (i, k) = (lane >> 3, lane & 7) multiplies one element of the D x D block.
@@ -2100,8 +2124,13 @@ __device__ __forceinline__ void block_chain(const double* Gp, const double* cvp,
 }
 
 // The same recurrence for blocks wider than a lane octet (D > kOct, e.g.
-// the 14-DoF dual arm): lane i < D computes row i of each step from the
-// previous vector in LDS (out), one wave sync per step.
+// the 14-DoF dual arm), with the chain matrices in HBM (Layout::wide).  Lane
+// (i, q) = (lane >> 2, lane & 3) owns columns 4q..4q+3 of row i: a step is
+// four fmas against the previous vector (read back from LDS) and a two-level
+// quad reduction.  The blocks of kWideChunk steps are loaded into registers
+// before the chunk's serial steps, so the HBM latency is paid once per chunk
+// instead of once per step.
+constexpr int kWideChunk = 8;
 __device__ __noinline__ void block_chain_wide(const double* Gp, const double* cvp, double* outp, int t0, int nsteps,
                                               int dir, bool store_first, int D, int lane)
 {
@@ -2109,23 +2138,58 @@ __device__ __noinline__ void block_chain_wide(const double* Gp, const double* cv
   const lds_f64* cv = lds(cvp);
   lds_f64* out = lds(outp);
   const int DD = D * D;
-  if (store_first && lane < D)
-    out[t0 * D + lane] = cv[t0 * D + lane];
-  wave_sync();
-  for (int s = 1; s <= nsteps; ++s)
+  const int i = lane >> 2, q = lane & 3;
+  const bool row_ok = i < D;
+  const int ic = row_ok ? i : D - 1;
+  int kk[4];
+  bool kok[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
   {
-    const int t = t0 + dir * s, tp = t - dir;
-    double v = 0.0;
-    if (lane < D)
+    kok[e] = 4 * q + e < D;
+    kk[e] = kok[e] ? 4 * q + e : D - 1;  // clamped: every lane reads a valid address
+  }
+  if (store_first && q == 0 && row_ok)
+    out[t0 * D + i] = cv[t0 * D + i];
+  wave_sync();
+  for (int s0 = 1; s0 <= nsteps; s0 += kWideChunk)
+  {
+    double g[kWideChunk][4], cc[kWideChunk];
+#pragma unroll
+    for (int u = 0; u < kWideChunk; ++u)
     {
-      v = cv[t * D + lane];
-      for (int k = 0; k < D; ++k)
-        v -= G[t * DD + lane * D + k] * out[tp * D + k];
+      const int s = s0 + u;
+      const bool ok = s <= nsteps;
+      const int t = ok ? t0 + dir * s : t0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+      {
+        const double gv = G[t * DD + ic * D + kk[e]];
+        g[u][e] = (ok && row_ok && kok[e]) ? gv : 0.0;
+      }
+      // c_t enters the reduction on lane q == 0 of its row (out may alias cv
+      // in the backward pass: every c of the chunk is read before its step
+      // writes)
+      const double cvv = cv[t * D + ic];
+      cc[u] = (ok && row_ok && q == 0) ? cvv : 0.0;
     }
-    wave_sync();  // out may alias cv (backward pass, in place)
-    if (lane < D)
-      out[t * D + lane] = v;
-    wave_sync();
+#pragma unroll
+    for (int u = 0; u < kWideChunk; ++u)
+    {
+      const int s = s0 + u;
+      if (s > nsteps)
+        break;
+      const int t = t0 + dir * s, tp = t - dir;
+      double p = cc[u];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        p = fma(-g[u][e], out[tp * D + kk[e]], p);
+      p += dpp_f64<0xB1>(p);  // quad_perm [1,0,3,2]
+      p += dpp_f64<0x4E>(p);  // quad_perm [2,3,0,1]
+      if (q == 0 && row_ok)
+        out[t * D + i] = p;
+      wave_sync();
+    }
   }
 }
 
@@ -2169,12 +2233,7 @@ __device__ __forceinline__ double twisted_dvalue(const Ctx& c, const double* LIp
   const lds_f64* LI = lds(LIp);
   const lds_f64* YV = lds(YVp);
   if (c.L.wide)
-  {
-    double v = 0.0;
-    for (int k = i; k < D; ++k)
-      v += LI[t * DD + k * D + i] * YV[t * D + k];
-    return v;
-  }
+    return masked_dot<THIP_MAX_DOF>(LI + t * DD + i, D, YV + t * D, 1, i, D);
   // unconditional loads from clamped indices, two accumulators (even / odd k):
   // no branch per term and half the dependent adds
   double v0 = 0, v1 = 0;
@@ -2206,24 +2265,33 @@ __device__ __noinline__ void twisted_middle_wide(const Ctx& c, const Solver& sv,
   lds_f64* YV = lds(YVp);
   if (i < D)
   {
-    double s = 0.0;
-    for (int k = 0; k < D; ++k)
+    // all loads first (clamped), then the sum in the original order
+    const bool top = m > 0, bot = N - 1 - m > 0;
+    double mt[THIP_MAX_DOF], yt[THIP_MAX_DOF], mb[THIP_MAX_DOF], yb[THIP_MAX_DOF];
+#pragma unroll
+    for (int k = 0; k < THIP_MAX_DOF; ++k)
     {
-      if (m > 0)
-        s += M[m * DD + i * D + k] * YV[(m - 1) * D + k];
-      if (N - 1 - m > 0)
-        s += Mb[m * DD + i * D + k] * YV[(m + 1) * D + k];
+      const int kk = min(k, D - 1);
+      mt[k] = M[m * DD + i * D + kk];
+      yt[k] = YV[max(m - 1, 0) * D + kk];
+      mb[k] = Mb[m * DD + i * D + kk];
+      yb[k] = YV[min(m + 1, N - 1) * D + kk];
     }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < THIP_MAX_DOF; ++k)
+      if (k < D)
+      {
+        if (top)
+          s += mt[k] * yt[k];
+        if (bot)
+          s += mb[k] * yb[k];
+      }
     YV[m * D + i] = CV[m * D + i] - s;  // y_m (YV's middle row is not a chain output)
   }
   wave_sync();
   if (i < D)
-  {
-    double x = 0.0;
-    for (int k = i; k < D; ++k)
-      x += LI[m * DD + k * D + i] * YV[m * D + k];
-    CV[m * D + i] = x;
-  }
+    CV[m * D + i] = masked_dot<THIP_MAX_DOF>(LI + m * DD + i, D, YV + m * D, 1, i, D);
   wave_sync();
 }
 
@@ -2276,30 +2344,67 @@ __device__ __forceinline__ double hinge_gather(const double* HC, const double* m
   for (int q = h0; q < h1; q += kHChunk)
   {
     const int qe = min(q + kHChunk, h1);
-    double s0 = 0, s1 = 0;
-    for (int h = q; h < qe; h += 2)
+    // all loads of the chunk first (clamped rows), then the masked sums in
+    // the original order
+    double hc[kHChunk], mv[kHChunk];
+#pragma unroll
+    for (int i = 0; i < kHChunk; ++i)
     {
-      s0 += HC[h * stride + k] * mr[h];
-      if (h + 1 < qe)
-        s1 += HC[(h + 1) * stride + k] * mr[h + 1];
+      const int h = min(q + i, qe - 1);
+      hc[i] = HC[h * stride + k];
+      mv[i] = mr[h];
+    }
+    double s0 = 0, s1 = 0;
+#pragma unroll
+    for (int i = 0; i < kHChunk; i += 2)
+    {
+      if (q + i < qe)
+        s0 += hc[i] * mv[i];
+      if (q + i + 1 < qe)
+        s1 += hc[i + 1] * mv[i + 1];
     }
     b += s0 + s1;
   }
   return b;
 }
 
+// b + sum over the CSR entries p in [p0, p1) of GS[rows[p]][j] * MR[rows[p]],
+// in order; the row indices and values of four entries are loaded before
+// their products are summed (a serial chain of dependent loads otherwise)
+__device__ __forceinline__ double csr_row_gather(const int* rows, int p0, int p1, const double* GS, const double* MR,
+                                                 int D, int j, double b)
+{
+  for (int p = p0; p < p1; p += 4)
+  {
+    int rr[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      rr[u] = rows[min(p + u, p1 - 1)];
+    double g[4], mv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+    {
+      g[u] = GS[rr[u] * D + j];
+      mv[u] = MR[rr[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (p + u < p1)
+        b += g[u] * mv[u];
+  }
+  return b;
+}
+
+
 // a hinge row's distance-expression value a_t.x_t + a_t+1.x_t+1 (two
 // independent partial sums, one per waypoint); x points at x_t
 template <typename XP>
 __device__ __forceinline__ double hinge_dot(const double* hc, XP x, int D)
 {
-  double s0 = 0, s1 = 0;
-  for (int k = 0; k < D; ++k)
-  {
-    s0 += hc[k] * x[k];
-    s1 += hc[D + k] * x[D + k];
-  }
-  return s0 + s1;
+  // masked fixed-length sums (all loads in flight together), original order
+  if (D > kOct)
+    return masked_dot<THIP_MAX_DOF>(hc, 1, x, 1, 0, D) + masked_dot<THIP_MAX_DOF>(hc + D, 1, x + D, 1, 0, D);
+  return masked_dot<kOct>(hc, 1, x, 1, 0, D) + masked_dot<kOct>(hc + D, 1, x + D, 1, 0, D);
 }
 
 __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, const double* eta, double* out)
@@ -2318,29 +2423,62 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   const double *GS = c.a(A_GS), *WS = c.a(A_WS), *DG = c.a(A_DG), *LI = c.a(A_LINV), *BS = c.a(A_BS),
                *FS = c.a(A_FS);
   double *BX = c.a(A_BXW), *BA = c.a(A_BA), *MR = c.a(A_MR), *CV = c.a(A_CV), *YV = c.a(A_YV);
-  FOR(r, L.n_abs)
+  // kGenU rows per thread at once, every load before any store (see admm_step)
+  for (int r0 = c.tid; r0 < L.n_abs; r0 += kGenU * kBlock)
   {
-    const int ca = nx + 2 * r;
-    const double rr = rho_k(c, nfr + r, polish, delta);
-    const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
-    const double rn = BX[ca] + BS[ca] * eta[bound_row(L, ca)];
-    const double rp = BX[ca + 1] + BS[ca + 1] * eta[bound_row(L, ca + 1)];
-    const double det = dn * dp + rr * (dn * wp * wp + dp * wn * wn);
-    MR[r] = (eta[nfr + r] * dn * dp - rr * (wn * dp * rn + wp * dn * rp)) / det;
-    BA[ca] = rn;
-    BA[ca + 1] = rp;
+    double mr[kGenU], rnv[kGenU], rpv[kGenU];
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+    {
+      const int r = min(r0 + u * kBlock, L.n_abs - 1);
+      const int ca = nx + 2 * r;
+      const double rr = rho_k(c, nfr + r, polish, delta);
+      const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
+      const double rn = BX[ca] + BS[ca] * eta[bound_row(L, ca)];
+      const double rp = BX[ca + 1] + BS[ca + 1] * eta[bound_row(L, ca + 1)];
+      const double det = dn * dp + rr * (dn * wp * wp + dp * wn * wn);
+      mr[u] = (eta[nfr + r] * dn * dp - rr * (wn * dp * rn + wp * dn * rp)) / det;
+      rnv[u] = rn;
+      rpv[u] = rp;
+    }
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+    {
+      const int r = r0 + u * kBlock;
+      if (r >= L.n_abs)
+        break;
+      MR[r] = mr[u];
+      BA[nx + 2 * r] = rnv[u];
+      BA[nx + 2 * r + 1] = rpv[u];
+    }
   }
   const int nh = c.s->n_h;
-  FOR(h, nh)
+  for (int h0 = c.tid; h0 < nh; h0 += kGenU * kBlock)
   {
-    const int col = L.nc_base + h;
-    const double rr = rho_k(c, L.m_base + 2 * h, polish, delta);
-    const double dn = DG[col], w = c.a(A_HW)[h];
-    const double rn = BX[col] + BS[col] * eta[bound_row(L, col)];
-    MR[L.n_rows + h] = (eta[L.m_base + 2 * h] * dn - rr * w * rn) / (dn + rr * w * w);
-    BA[col] = rn;
+    double mr[kGenU], rnv[kGenU];
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+    {
+      const int h = min(h0 + u * kBlock, nh - 1);
+      const int col = L.nc_base + h;
+      const double rr = rho_k(c, L.m_base + 2 * h, polish, delta);
+      const double dn = DG[col], w = c.a(A_HW)[h];
+      const double rn = BX[col] + BS[col] * eta[bound_row(L, col)];
+      mr[u] = (eta[L.m_base + 2 * h] * dn - rr * w * rn) / (dn + rr * w * w);
+      rnv[u] = rn;
+    }
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+    {
+      const int h = h0 + u * kBlock;
+      if (h >= nh)
+        break;
+      MR[L.n_rows + h] = mr[u];
+      BA[L.nc_base + h] = rnv[u];
+    }
   }
   BSYNC();
+  PROF_LAP(23);
   FOR(col, nx)
   {
     const int t = col / D, j = col % D;
@@ -2348,11 +2486,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     const int f = c.T.fixed_of_step[t];
     if (f >= 0)
       b += FS[f * D + j] * eta[f * D + j];
-    for (int p = c.T.step_ptr[t]; p < c.T.step_ptr[t + 1]; ++p)
-    {
-      const int r = c.T.step_rows[p];
-      b += GS[r * D + j] * MR[r];
-    }
+    b = csr_row_gather(c.T.step_rows, c.T.step_ptr[t], c.T.step_ptr[t + 1], GS, MR, D, j, b);
     if (nh > 0)
     {
       const double* HC = c.a(A_HC);
@@ -2363,16 +2497,16 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     BX[col] = b;
   }
   BSYNC();
+  PROF_LAP(24);
   FOR(col, nx)
   {
     const int t = col / D, i = col % D;
-    double v = 0;
-    for (int k = 0; k <= i; ++k)
-      v += lds(LI)[t * DD + i * D + k] * BX[t * D + k];
+    const double v = L.wide ? masked_dot<THIP_MAX_DOF>(lds(LI) + t * DD + i * D, 1, BX + t * D, 1, 0, i + 1)
+                            : masked_dot<kOct>(lds(LI) + t * DD + i * D, 1, BX + t * D, 1, 0, i + 1);
     lds(CV)[col] = v;
   }
   BSYNC();
-  PROF_LAP(8);
+  PROF_LAP(25);
   // forward chains (twisted factor): y = L^-1 b
   twisted_forward(c, sv, CV, YV);
   BSYNC();
@@ -2401,37 +2535,65 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     }
   }
   BSYNC();
-  PROF_LAP(8);
+  PROF_LAP(26);
   // backward chains, in place: x lands in CV
   twisted_backward(c, sv, CV);
   BSYNC();
   PROF_LAP(10);
   FOR(col, nx) out[col] = CV[col];
   // aux back-substitution
-  FOR(r, L.n_abs)
+  for (int r0 = c.tid; r0 < L.n_abs; r0 += kGenU * kBlock)
   {
-    const int t = c.T.row_step[r];
-    const int ca = nx + 2 * r;
-    double g = 0;
-    for (int j = 0; j < D; ++j)
-      g += GS[r * D + j] * lds(CV)[t * D + j];
-    const double rr = rho_k(c, nfr + r, polish, delta);
-    const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
-    const double rn = BA[ca], rp = BA[ca + 1];
-    const double det = dn * dp + rr * (dn * wp * wp + dp * wn * wn);
-    const double cross = wp * rn - wn * rp;
-    const double h = eta[nfr + r] - rr * g;
-    out[ca] = (dp * rn + rr * wp * cross + wn * dp * h) / det;
-    out[ca + 1] = (dn * rp - rr * wn * cross + wp * dn * h) / det;
+    double on[kGenU], op[kGenU];
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+    {
+      const int r = min(r0 + u * kBlock, L.n_abs - 1);
+      const int t = c.T.row_step[r];
+      const int ca = nx + 2 * r;
+      const double g = L.wide ? masked_dot<THIP_MAX_DOF>(GS + r * D, 1, lds(CV) + t * D, 1, 0, D)
+                              : masked_dot<kOct>(GS + r * D, 1, lds(CV) + t * D, 1, 0, D);
+      const double rr = rho_k(c, nfr + r, polish, delta);
+      const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
+      const double rn = BA[ca], rp = BA[ca + 1];
+      const double det = dn * dp + rr * (dn * wp * wp + dp * wn * wn);
+      const double cross = wp * rn - wn * rp;
+      const double h = eta[nfr + r] - rr * g;
+      on[u] = (dp * rn + rr * wp * cross + wn * dp * h) / det;
+      op[u] = (dn * rp - rr * wn * cross + wp * dn * h) / det;
+    }
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+    {
+      const int r = r0 + u * kBlock;
+      if (r >= L.n_abs)
+        break;
+      out[nx + 2 * r] = on[u];
+      out[nx + 2 * r + 1] = op[u];
+    }
   }
-  FOR(h, nh)
+  for (int h0 = c.tid; h0 < nh; h0 += kGenU * kBlock)
   {
-    const int t = c.ia(I_HT)[h];
-    const double g = hinge_dot(c.a(A_HC) + h * 2 * D, lds(CV) + t * D, D);
-    const int col = L.nc_base + h;
-    const double rr = rho_k(c, L.m_base + 2 * h, polish, delta);
-    const double dn = DG[col], w = c.a(A_HW)[h];
-    out[col] = (BA[col] + w * (eta[L.m_base + 2 * h] - rr * g)) / (dn + rr * w * w);
+    double ov[kGenU];
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+    {
+      const int h = min(h0 + u * kBlock, nh - 1);
+      const int t = c.ia(I_HT)[h];
+      const double g = hinge_dot(c.a(A_HC) + h * 2 * D, lds(CV) + t * D, D);
+      const int col = L.nc_base + h;
+      const double rr = rho_k(c, L.m_base + 2 * h, polish, delta);
+      const double dn = DG[col], w = c.a(A_HW)[h];
+      ov[u] = (BA[col] + w * (eta[L.m_base + 2 * h] - rr * g)) / (dn + rr * w * w);
+    }
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+    {
+      const int h = h0 + u * kBlock;
+      if (h >= nh)
+        break;
+      out[L.nc_base + h] = ov[u];
+    }
   }
   BSYNC();
   PROF_LAP(11);
@@ -2845,31 +3007,128 @@ __device__ void admm_step(Ctx& c, Solver& sv)
   double* BX = c.a(A_BXW);
   const double *Q = c.a(A_Q), *RH = c.a(A_RHO), *Lo = c.a(A_L), *Up = c.a(A_U);
   double* ETA = c.a(A_PZ);  // eta = rho zp - y over all rows (scratch)
-  FOR(r, c.m()) ETA[r] = RH[r] * zp[r] - Y[r];
-  FOR(col, c.nc()) BX[col] = sig * xp[col] - Q[col];
+  long long* pf = (c.tid == 0) ? c.s->prof : nullptr;
+  long long tq = pf ? clock64() : 0;
+  // the generic step's loops run kGenU iterations per thread at once, all
+  // loads before any store: the arrays are generic pointers (LDS or HBM per
+  // the residency plan), so the compiler cannot hoist the next iteration's
+  // loads above this one's stores and each iteration paid a full memory
+  // round trip (config E: 14-DoF x 50 waypoints, ~4,300 rows)
+  const int m = c.m(), nc = c.nc();
+  for (int r0 = c.tid; r0 < m; r0 += kGenU * kBlock)
+  {
+    double e[kGenU];
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+    {
+      const int r = min(r0 + u * kBlock, m - 1);
+      e[u] = RH[r] * zp[r] - Y[r];
+    }
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+      if (r0 + u * kBlock < m)
+        ETA[r0 + u * kBlock] = e[u];
+  }
+  for (int c0 = c.tid; c0 < nc; c0 += kGenU * kBlock)
+  {
+    double e[kGenU];
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+    {
+      const int col = min(c0 + u * kBlock, nc - 1);
+      e[u] = sig * xp[col] - Q[col];
+    }
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+      if (c0 + u * kBlock < nc)
+        BX[c0 + u * kBlock] = e[u];
+  }
   BSYNC();
+  if (pf)
+    pf[30] += clock64() - tq;
   reduced_solve(c, sv, false, 0.0, ETA, XT);
-  // z tilde = A x tilde; updates
-  FOR(r, c.m())
+  if (pf)
+    tq = clock64();
+  // z tilde = A x tilde; updates.  One loop per row kind (CartPose / fixed
+  // rows, the columns' bound rows, hinge rows with their hinge variable's
+  // bound row), each straight-line: a loop over all rows diverged into every
+  // kind's branch in every wave and serialised their loads
+  auto update_rows = [&](int rb, int re, auto zt_of) {
+    for (int r0 = rb + c.tid; r0 < re; r0 += kGenU * kBlock)
+    {
+      double zt[kGenU], rh[kGenU], yv[kGenU], zv[kGenU], lo[kGenU], up[kGenU];
+#pragma unroll
+      for (int u = 0; u < kGenU; ++u)
+      {
+        const int r = min(r0 + u * kBlock, re - 1);  // clamped: every load valid
+        zt[u] = zt_of(r);
+        rh[u] = RH[r];
+        yv[u] = Y[r];
+        zv[u] = zp[r];
+        lo[u] = Lo[r];
+        up[u] = Up[r];
+      }
+#pragma unroll
+      for (int u = 0; u < kGenU; ++u)
+      {
+        const int r = r0 + u * kBlock;
+        if (r >= re)
+          break;
+        const double rho = rh[u];
+        double zr = (1.0 / rho) * yv[u];
+        zr = zr + al * zt[u];
+        zr = zr + (1.0 - al) * zv[u];
+        zr = fmin(fmax(zr, lo[u]), up[u]);
+        z[r] = zr;
+        const double dy = rho * (al * zt[u] + (1.0 - al) * zv[u] - zr);
+        DY[r] = dy;
+        Y[r] = yv[u] + dy;
+      }
+    }
+  };
+  const Layout& L = c.L;
+  update_rows(0, L.n_rows, [&](int r) { return row_ax(c, r, XT); });
   {
-    const double zt = row_ax(c, r, XT);
-    const double rho = RH[r];
-    double zr = (1.0 / rho) * Y[r];
-    zr = zr + al * zt;
-    zr = zr + (1.0 - al) * zp[r];
-    zr = fmin(fmax(zr, Lo[r]), Up[r]);
-    z[r] = zr;
-    const double dy = rho * (al * zt + (1.0 - al) * zp[r] - zr);
-    DY[r] = dy;
-    Y[r] += dy;
+    const double* BS = c.a(A_BS);
+    update_rows(L.n_rows, L.m_base, [&](int r) { return BS[r - L.n_rows] * XT[r - L.n_rows]; });
+    if (m > L.m_base)
+    {
+      // hinge row m_base + 2h: a_t.x_t + a_t+1.x_t+1 + w h; m_base + 2h + 1: the bound row of h
+      const double *HC = c.a(A_HC), *HW = c.a(A_HW);
+      const int* HT = c.ia(I_HT);
+      const int D = L.D;
+      update_rows(L.m_base, m, [&](int r) {
+        const int h2 = r - L.m_base, h = h2 >> 1, col = L.nc_base + h;
+        if (h2 & 1)
+          return BS[col] * XT[col];
+        return hinge_dot(HC + h * 2 * D, XT + HT[h] * D, D) + HW[h] * XT[col];
+      });
+    }
   }
-  FOR(col, c.nc())
+  for (int c0 = c.tid; c0 < nc; c0 += kGenU * kBlock)
   {
-    const double xv = al * XT[col] + (1.0 - al) * xp[col];
-    x[col] = xv;
-    DX[col] = xv - xp[col];
+    double xt[kGenU], xo[kGenU];
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+    {
+      const int col = min(c0 + u * kBlock, nc - 1);
+      xt[u] = XT[col];
+      xo[u] = xp[col];
+    }
+#pragma unroll
+    for (int u = 0; u < kGenU; ++u)
+    {
+      const int col = c0 + u * kBlock;
+      if (col >= nc)
+        break;
+      const double xv = al * xt[u] + (1.0 - al) * xo[u];
+      x[col] = xv;
+      DX[col] = xv - xo[u];
+    }
   }
   BSYNC();
+  if (pf)
+    pf[31] += clock64() - tq;
 }
 
 // ======================================================================

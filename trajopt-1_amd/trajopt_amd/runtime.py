@@ -125,8 +125,8 @@ class BatchTrustRegionSQP:
                      "build_and_scale", "solve_rhs_diag", "fwd_chain", "bwd_chain", "aux_backsub", "qp_solve",
                      "sqp_total", "sqp_wall_ticks", "seg_B_rhs_linv", "seg_C2_linvT_middle",
                      "seg_hinge_gather", "seg_hinge_E", "coll_count_pass", "coll_rank_pass", "coll_rows", "coll_fk_substates",
-                     "seg_fwd_chain_w0", "chain_w0_loads", "chain_w0_serial", "chain_w0_stores",
-                     "n_primal_inf_full", "n_dual_inf_full", "n_factor", "unused30", "unused31"]
+                     "gen_rhs_mr", "gen_rhs_cols", "gen_rhs_linv", "gen_dvalue_middle",
+                     "n_primal_inf_full", "n_dual_inf_full", "n_factor", "gen_pre", "gen_updates"]
 
     def enable_profile(self, on=True):
         self._check(self.lib.thip_debug_profile(self.ctx, 1 if on else 0), "thip_debug_profile")
