@@ -2028,8 +2028,9 @@ __device__ __forceinline__ double wave_max(double v)
   return v;
 }
 
-// sum_{k in [k0, k1)} a[k * sa] * b[k * sb], in order, for k1 <= THIP_MAX_DOF:
-// all loads issued first (clamped indices), masked accumulation
+// sum_{k in [k0, k1)} a[k * sa] * b[k * sb], in order, for k1 <= KMAX:
+// all loads issued first (clamped indices, finite operands), masked
+// accumulation
 template <int KMAX, typename AP, typename BP>
 __device__ __forceinline__ double masked_dot(AP a, int sa, BP b, int sb, int k0, int k1)
 {
@@ -2041,11 +2042,13 @@ __device__ __forceinline__ double masked_dot(AP a, int sa, BP b, int sb, int k0,
     av[k] = a[kk * sa];
     bv[k] = b[kk * sb];
   }
+  // masked terms add fma(a, 0, v) = v: the same sum, and no branch the
+  // compiler could sink the loads into (a guarded add compiled to one branch,
+  // one load and one full vmcnt wait per term)
   double v = 0;
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
-    if (k >= k0 && k < k1)
-      v += av[k] * bv[k];
+    v = fma(av[k], bv[k] * ((k >= k0 && k < k1) ? 1.0 : 0.0), v);
   return v;
 }
 
@@ -2141,14 +2144,18 @@ __device__ __noinline__ void block_chain_wide(const double* Gp, const double* cv
   const int i = lane >> 2, q = lane & 3;
   const bool row_ok = i < D;
   const int ic = row_ok ? i : D - 1;
+  // masks as multipliers on loaded values (finite), never as conditions: a
+  // guarded load compiled to a branch and a full vmcnt wait per load
   int kk[4];
-  bool kok[4];
+  double kmask[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e)
   {
-    kok[e] = 4 * q + e < D;
-    kk[e] = kok[e] ? 4 * q + e : D - 1;  // clamped: every lane reads a valid address
+    const bool kok = 4 * q + e < D;
+    kk[e] = kok ? 4 * q + e : D - 1;  // clamped: every lane reads a valid address
+    kmask[e] = kok ? 1.0 : 0.0;
   }
+  const double qmask = (q == 0) ? 1.0 : 0.0;
   if (store_first && q == 0 && row_ok)
     out[t0 * D + i] = cv[t0 * D + i];
   wave_sync();
@@ -2158,20 +2165,16 @@ __device__ __noinline__ void block_chain_wide(const double* Gp, const double* cv
 #pragma unroll
     for (int u = 0; u < kWideChunk; ++u)
     {
+      // steps past nsteps are never computed; rows i >= D are never stored
       const int s = s0 + u;
-      const bool ok = s <= nsteps;
-      const int t = ok ? t0 + dir * s : t0;
+      const int t = (s <= nsteps) ? t0 + dir * s : t0;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-      {
-        const double gv = G[t * DD + ic * D + kk[e]];
-        g[u][e] = (ok && row_ok && kok[e]) ? gv : 0.0;
-      }
+        g[u][e] = G[t * DD + ic * D + kk[e]];
       // c_t enters the reduction on lane q == 0 of its row (out may alias cv
       // in the backward pass: every c of the chunk is read before its step
       // writes)
-      const double cvv = cv[t * D + ic];
-      cc[u] = (ok && row_ok && q == 0) ? cvv : 0.0;
+      cc[u] = cv[t * D + ic] * qmask;
     }
 #pragma unroll
     for (int u = 0; u < kWideChunk; ++u)
@@ -2183,7 +2186,7 @@ __device__ __noinline__ void block_chain_wide(const double* Gp, const double* cv
       double p = cc[u];
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        p = fma(-g[u][e], out[tp * D + kk[e]], p);
+        p = fma(-g[u][e], out[tp * D + kk[e]] * kmask[e], p);
       p += dpp_f64<0xB1>(p);  // quad_perm [1,0,3,2]
       p += dpp_f64<0x4E>(p);  // quad_perm [2,3,0,1]
       if (q == 0 && row_ok)
@@ -2358,10 +2361,8 @@ __device__ __forceinline__ double hinge_gather(const double* HC, const double* m
 #pragma unroll
     for (int i = 0; i < kHChunk; i += 2)
     {
-      if (q + i < qe)
-        s0 += hc[i] * mv[i];
-      if (q + i + 1 < qe)
-        s1 += hc[i + 1] * mv[i + 1];
+      s0 = fma(hc[i], mv[i] * ((q + i < qe) ? 1.0 : 0.0), s0);  // masked: unchanged
+      s1 = fma(hc[i + 1], mv[i + 1] * ((q + i + 1 < qe) ? 1.0 : 0.0), s1);
     }
     b += s0 + s1;
   }
@@ -2389,8 +2390,7 @@ __device__ __forceinline__ double csr_row_gather(const int* rows, int p0, int p1
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (p + u < p1)
-        b += g[u] * mv[u];
+      b = fma(g[u], mv[u] * ((p + u < p1) ? 1.0 : 0.0), b);  // masked: b unchanged
   }
   return b;
 }
