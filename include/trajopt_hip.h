@@ -391,7 +391,7 @@ int thip_collision_rows(thip_ctx* ctx, const double* x, double* records, int cap
  * the slot list in sqp_kernel.hip).  enable = 0 frees them.  Counters
  * accumulate over runs until re-enabled. */
 int thip_debug_profile(thip_ctx* ctx, int enable);
-int thip_debug_get_profile(thip_ctx* ctx, long long* counters /* [batch][32] */);
+int thip_debug_get_profile(thip_ctx* ctx, long long* counters /* [batch][40] */);
 /* Diagnostics: workspace layout (array offsets in doubles / ints, and
  * dims = {N, D, nx, n_fixed_rows, n_abs, n_cols, n_rows, m, dstride, istride,
  * n_double_arrays, n_int_arrays}) and a copy of the device workspace. */

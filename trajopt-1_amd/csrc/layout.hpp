@@ -255,6 +255,6 @@ struct KernelArgs
 
 constexpr int kHPack = 14;  // doubles per hinge row in A_HPK
 constexpr int kHChunk = 8;  // hinge rows per gather chunk (rows of one step pair)
-constexpr int kProfSlots = 32;
+constexpr int kProfSlots = 40;
 
 }  // namespace thip

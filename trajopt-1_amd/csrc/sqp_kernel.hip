@@ -137,6 +137,21 @@ struct Ctx
 #define FOR(i, n) for (int i = c.tid; i < (n); i += kBlock)
 #define BSYNC() __syncthreads()
 
+// Arrays the residency plan always places in LDS (chain matrices, LINV, CV,
+// YV: thip_create rejects problems where they would not fit) are accessed
+// through LDS-typed pointers so the compiler emits ds_read/ds_write instead of
+// flat accesses (flat ops count on vmcnt and lgkmcnt, so every wait would also
+// drain outstanding stores).
+typedef __attribute__((address_space(3))) double lds_f64;
+__device__ __forceinline__ lds_f64* lds(double* p) { return (lds_f64*)p; }
+__device__ __forceinline__ const lds_f64* lds(const double* p) { return (const lds_f64*)p; }
+// HBM-resident arrays as global-address-space pointers: global_* instead of
+// FLAT instructions (a FLAT access also counts against lgkmcnt, so every LDS
+// wait would drain it too)
+typedef __attribute__((address_space(1))) double gbl_f64;
+__device__ __forceinline__ gbl_f64* gbl(double* p) { return (gbl_f64*)p; }
+__device__ __forceinline__ const gbl_f64* gbl(const double* p) { return (const gbl_f64*)p; }
+
 // Phase profiling (thip_debug_profile): shader-clock cycles accumulated per
 // slot by thread 0.  Slots: 0 admm_step, 1 residuals, 2 termination check,
 // 3 factor, 4 polish, 5 linearize, 6 evaluate, 7 build_and_scale,
@@ -1693,9 +1708,16 @@ __device__ __forceinline__ void wave_sync()
 
 // In-place lower Cholesky of the D x D block S (one wave; lane i owns row i),
 // then Li = L^-1 (lane j solves column j).  Flags `bad` if S is not positive
-// definite.
-__device__ __forceinline__ void chol_inv_block(double* S, double* Li, int D, int lane, int& bad)
+// definite.  S and Li are in LDS (factor()'s scratch and A_LINV, which the
+// residency plan always places in LDS).  The column solve runs over DM >= D
+// rows with compile-time indices, so its column stays in registers (indexed
+// with a runtime bound it was a private array in scratch memory: a scratch
+// round trip per term).
+template <int DM>
+__device__ __forceinline__ void chol_inv_block_t(double* Sp, double* Lip, int D, int lane, int& bad)
 {
+  lds_f64* S = lds(Sp);
+  lds_f64* Li = lds(Lip);
   for (int j = 0; j < D; ++j)
   {
     if (lane == j)
@@ -1724,24 +1746,180 @@ __device__ __forceinline__ void chol_inv_block(double* S, double* Li, int D, int
   if (lane < D)
   {
     const int j = lane;
-    double xcol[THIP_MAX_DOF];
-    for (int i = 0; i < D; ++i)
+    double xcol[DM];
+#pragma unroll
+    for (int i = 0; i < DM; ++i)
     {
-      double v = (i == j) ? 1.0 : 0.0;
-      for (int k = 0; k < i; ++k)
-        v -= S[i * D + k] * xcol[k];
-      xcol[i] = (i < j) ? 0.0 : v / S[i * D + i];
+      if (i < D)
+      {
+        double v = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < i; ++k)
+          v -= S[i * D + k] * xcol[k];
+        xcol[i] = (i < j) ? 0.0 : v / S[i * D + i];
+      }
+      else
+        xcol[i] = 0.0;
     }
-    for (int i = 0; i < D; ++i)
-      Li[i * D + j] = xcol[i];
+#pragma unroll
+    for (int i = 0; i < DM; ++i)
+      if (i < D)
+        Li[i * D + j] = xcol[i];
   }
   wave_sync();
+}
+
+__device__ __forceinline__ void chol_inv_block(double* S, double* Li, int D, int lane, int& bad)
+{
+  if (D > kOct)
+    chol_inv_block_t<THIP_MAX_DOF>(S, Li, D, lane, bad);
+  else
+    chol_inv_block_t<kOct>(S, Li, D, lane, bad);
+}
+
+// v + sum_{h in [h0, h1)} W[h] * (HC[h][a] * HC[h][b]), in order, 8 rows per
+// chunk with every load of the chunk issued first (masked rows add 0)
+__device__ __forceinline__ double hinge_outer_sum(const double* HC, const double* W, int stride, int a, int b, int h0,
+                                                  int h1, double v)
+{
+  for (int q = h0; q < h1; q += 8)
+  {
+    double w[8], p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+    {
+      const int h = min(q + u, h1 - 1);
+      w[u] = W[h];
+      p[u] = (HC[h * stride + a] * HC[h * stride + b]) * ((q + u < h1) ? 1.0 : 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v += w[u] * p[u];
+  }
+  return v;
+}
+
+// One half of the twisted block Cholesky (see factor()): wave 0 eliminates
+// waypoints 0..m-1, wave 1 waypoints N-1..m+1.  The block scratch S, the
+// coupling Ls and LI are LDS (typed: ds_read instead of FLAT); the inner
+// products run over DM >= D terms with clamped loads and masked terms, in the
+// order of the plain loops.
+template <int DM>
+__device__ __noinline__ void twisted_factor_half(Ctx& c, Solver& sv, const double* KB, double* LIp, const double* PO,
+                                                 double* Sp, double* Lsp, int& bad)
+{
+  const Layout& L = c.L;
+  const int D = L.D, N = L.N, DD = D * D, m = L.tw_mid, w = c.wave;
+  const int len = (w == 0) ? m : (N - 1 - m);
+  lds_f64* S = lds(Sp);
+  lds_f64* Ls = lds(Lsp);
+  for (int k = 0; k < len; ++k)
+  {
+    const int t = (w == 0) ? k : (N - 1 - k);
+    const int cpl = (w == 0) ? t : t - 1;  // PO index of the coupling to the next block
+    // the half's first block has no coupling (and Ls holds stale or
+    // uninitialised LDS then: never read, not even under a zero mask)
+    for (int e = c.lane; e < DD; e += 64)
+    {
+      const int i = e / D, j = e % D;
+      double v = KB[t * DD + e];
+      if (k > 0)
+      {
+        double a[DM], b[DM];
+#pragma unroll
+        for (int q = 0; q < DM; ++q)
+        {
+          const int qc = min(q, D - 1);
+          a[q] = Ls[i * D + qc];
+          b[q] = Ls[j * D + qc] * ((q < D) ? 1.0 : 0.0);
+        }
+#pragma unroll
+        for (int q = 0; q < DM; ++q)
+          v -= a[q] * b[q];
+      }
+      S[e] = v;
+    }
+    wave_sync();
+    chol_inv_block(Sp, LIp + t * DD, D, c.lane, bad);
+    const lds_f64* Li = lds(LIp) + t * DD;
+    for (int e = c.lane; e < DD; e += 64)
+    {
+      const int i = e / D, j = e % D;
+      double v = 0;  // zero for the half's first block (the segment's chain reads it)
+      if (k > 0)
+      {
+        double a[DM], b[DM];
+#pragma unroll
+        for (int q = 0; q < DM; ++q)
+        {
+          const int qc = min(q, D - 1);
+          a[q] = Li[i * D + qc];
+          b[q] = Ls[qc * D + j] * ((q <= i) ? 1.0 : 0.0);
+        }
+#pragma unroll
+        for (int q = 0; q < DM; ++q)
+          v += a[q] * b[q];
+      }
+      sv.M[t * DD + e] = v;
+    }
+    wave_sync();
+    if (!L.hinge)
+      for (int e = c.lane; e < DD; e += 64)
+      {
+        const int i = e / D, q = e % D;
+        Ls[e] = PO[cpl * D + i] * Li[q * D + i];
+      }
+    else
+    {
+      // Lsub[i][q] = sum_j K[i][j] LI_t[q][j] with K = K_{t+1,t} (top)
+      // or K_{t-1,t} = K_{t,t-1}^T (bottom)
+      const double* Kc = c.a(A_CPL) + cpl * DD;
+      for (int e = c.lane; e < DD; e += 64)
+      {
+        const int i = e / D, q = e % D;
+        double a[DM], b[DM];
+#pragma unroll
+        for (int j = 0; j < DM; ++j)
+        {
+          const int jc = min(j, D - 1);
+          a[j] = (w == 0) ? Kc[i * D + jc] : Kc[jc * D + i];
+          b[j] = Li[q * D + jc] * ((j <= q) ? 1.0 : 0.0);
+        }
+        double v = 0;
+#pragma unroll
+        for (int j = 0; j < DM; ++j)
+          v += a[j] * b[j];
+        Ls[e] = v;
+      }
+    }
+    wave_sync();
+    for (int e = c.lane; e < DD; e += 64)
+    {
+      const int i = e / D, j = e % D;
+      double a[DM], b[DM];
+#pragma unroll
+      for (int q = 0; q < DM; ++q)
+      {
+        const int qc = min(q, D - 1);
+        a[q] = Li[qc * D + i];
+        b[q] = Ls[j * D + qc] * ((q >= i && q < D) ? 1.0 : 0.0);
+      }
+      double v = 0;
+#pragma unroll
+      for (int q = 0; q < DM; ++q)
+        v += a[q] * b[q];
+      sv.Nb[t * DD + e] = v;
+    }
+    wave_sync();
+  }
 }
 
 // returns false if the reduced matrix is not positive definite
 __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delta)
 {
   PROF(3);
+  long long* pf = (c.tid == 0) ? c.s->prof : nullptr;
+  long long tq = pf ? clock64() : 0;
   const Layout& L = c.L;
   const int D = L.D, nx = L.nx, N = L.N;
   const double *PD = c.a(A_PD), *PO = c.a(A_PO), *BS = c.a(A_BS), *GS = c.a(A_GS), *WS = c.a(A_WS),
@@ -1788,20 +1966,35 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
         v += rho_k(c, fr, polish, delta) * (FS[fr] * FS[fr]);
       }
     }
-    for (int p = c.T.step_ptr[t]; p < c.T.step_ptr[t + 1]; ++p)
+    // the row sums in chunks of 8 rows, all loads of a chunk first (masked
+    // terms add fma(w, 0, v) = v): a loop of dependent loads otherwise
     {
-      const int r = c.T.step_rows[p];
-      v += RE[r] * (GS[r * D + i] * GS[r * D + j]);
+      const int p0 = c.T.step_ptr[t], p1 = c.T.step_ptr[t + 1];
+      for (int p = p0; p < p1; p += 8)
+      {
+        int rr[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          rr[u] = c.T.step_rows[min(p + u, p1 - 1)];
+        double w[8], a[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+        {
+          w[u] = RE[rr[u]];
+          a[u] = (GS[rr[u] * D + i] * GS[rr[u] * D + j]) * ((p + u < p1) ? 1.0 : 0.0);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          v += w[u] * a[u];
+      }
     }
     if (nh > 0)
     {
       const double *HC = c.a(A_HC), *HRE = c.a(A_HRE);
       const int* HP = c.ia(I_HPTR);
-      for (int h = HP[t]; h < HP[t + 1]; ++h)
-        v += HRE[h] * (HC[h * 2 * D + i] * HC[h * 2 * D + j]);
+      v = hinge_outer_sum(HC, HRE, 2 * D, i, j, HP[t], HP[t + 1], v);
       if (t > 0)
-        for (int h = HP[t - 1]; h < HP[t]; ++h)
-          v += HRE[h] * (HC[h * 2 * D + D + i] * HC[h * 2 * D + D + j]);
+        v = hinge_outer_sum(HC, HRE, 2 * D, D + i, D + j, HP[t - 1], HP[t], v);
     }
     KB[e] = v;
   }
@@ -1815,12 +2008,17 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
     {
       const int t = e / (D * D), i = (e / D) % D, j = e % D;
       double v = (i == j) ? PO[t * D + i] : 0.0;
-      for (int h = HP[t]; h < HP[t + 1]; ++h)
-        v += HRE[h] * (HC[h * 2 * D + D + i] * HC[h * 2 * D + j]);
+      v = hinge_outer_sum(HC, HRE, 2 * D, D + i, j, HP[t], HP[t + 1], v);
       CPL[e] = v;
     }
   }
   BSYNC();
+  if (pf)
+  {
+    const long long tn = clock64();
+    pf[32] += tn - tq;
+    tq = tn;
+  }
   // Twisted ("burn at both ends") block Cholesky.  Wave 0 eliminates the
   // waypoints 0..m-1 from the top, wave 1 eliminates N-1..m+1 from the bottom
   // (the same recurrence on the reversed block order; the JointVel couplings
@@ -1843,67 +2041,10 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
   BSYNC();
   if (c.wave < 2)
   {
-    const int w = c.wave;
-    const int len = (w == 0) ? m : (N - 1 - m);
-    double* S = Sblk[w];
-    double* Ls = Lsub[w];
-    for (int k = 0; k < len; ++k)
-    {
-      const int t = (w == 0) ? k : (N - 1 - k);
-      const int cpl = (w == 0) ? t : t - 1;  // PO index of the coupling to the next block
-      for (int e = c.lane; e < DD; e += 64)
-      {
-        const int i = e / D, j = e % D;
-        double v = KB[t * DD + e];
-        if (k > 0)
-          for (int q = 0; q < D; ++q)
-            v -= Ls[i * D + q] * Ls[j * D + q];
-        S[e] = v;
-      }
-      wave_sync();
-      chol_inv_block(S, LI + t * DD, D, c.lane, bad);
-      const double* Li = LI + t * DD;
-      for (int e = c.lane; e < DD; e += 64)
-      {
-        const int i = e / D, j = e % D;
-        double v = 0;
-        if (k > 0)  // the half's first block has no coupling: zero (the segment's chain reads it)
-          for (int q = 0; q <= i; ++q)
-            v += Li[i * D + q] * Ls[q * D + j];
-        sv.M[t * DD + e] = v;
-      }
-      wave_sync();
-      if (!L.hinge)
-        for (int e = c.lane; e < DD; e += 64)
-        {
-          const int i = e / D, q = e % D;
-          Ls[e] = PO[cpl * D + i] * Li[q * D + i];
-        }
-      else
-      {
-        // Lsub[i][q] = sum_j K[i][j] LI_t[q][j] with K = K_{t+1,t} (top)
-        // or K_{t-1,t} = K_{t,t-1}^T (bottom)
-        const double* Kc = c.a(A_CPL) + cpl * DD;
-        for (int e = c.lane; e < DD; e += 64)
-        {
-          const int i = e / D, q = e % D;
-          double v = 0;
-          for (int j = 0; j <= q; ++j)
-            v += ((w == 0) ? Kc[i * D + j] : Kc[j * D + i]) * Li[q * D + j];
-          Ls[e] = v;
-        }
-      }
-      wave_sync();
-      for (int e = c.lane; e < DD; e += 64)
-      {
-        const int i = e / D, j = e % D;
-        double v = 0;
-        for (int q = i; q < D; ++q)
-          v += Li[q * D + i] * Ls[j * D + q];
-        sv.Nb[t * DD + e] = v;
-      }
-      wave_sync();
-    }
+    if (D > kOct)
+      twisted_factor_half<THIP_MAX_DOF>(c, sv, KB, LI, PO, Sblk[c.wave], Lsub[c.wave], bad);
+    else
+      twisted_factor_half<kOct>(c, sv, KB, LI, PO, Sblk[c.wave], Lsub[c.wave], bad);
   }
   BSYNC();
   if (c.wave == 0)
@@ -1941,27 +2082,14 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
     }
   }
   BSYNC();
+  if (pf)
+    pf[33] += clock64() - tq;
   if (c.tid == 0 && c.s->prof)
     c.s->prof[29] += 1;  // factor calls (diagnostic count)
   const bool ok = (bad == 0);
   BSYNC();
   return ok;
 }
-
-// Arrays the residency plan always places in LDS (chain matrices, LINV, CV,
-// YV: thip_create rejects problems where they would not fit) are accessed
-// through LDS-typed pointers so the compiler emits ds_read/ds_write instead of
-// flat accesses (flat ops count on vmcnt and lgkmcnt, so every wait would also
-// drain outstanding stores).
-typedef __attribute__((address_space(3))) double lds_f64;
-__device__ __forceinline__ lds_f64* lds(double* p) { return (lds_f64*)p; }
-__device__ __forceinline__ const lds_f64* lds(const double* p) { return (const lds_f64*)p; }
-// HBM-resident arrays as global-address-space pointers: global_* instead of
-// FLAT instructions (a FLAT access also counts against lgkmcnt, so every LDS
-// wait would drain it too)
-typedef __attribute__((address_space(1))) double gbl_f64;
-__device__ __forceinline__ gbl_f64* gbl(double* p) { return (gbl_f64*)p; }
-__device__ __forceinline__ const gbl_f64* gbl(const double* p) { return (const gbl_f64*)p; }
 
 // is p (a generic pointer from the residency plan) inside this workgroup's
 // dynamic LDS?

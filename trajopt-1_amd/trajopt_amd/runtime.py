@@ -126,13 +126,15 @@ class BatchTrustRegionSQP:
                      "sqp_total", "sqp_wall_ticks", "seg_B_rhs_linv", "seg_C2_linvT_middle",
                      "seg_hinge_gather", "seg_hinge_E", "coll_count_pass", "coll_rank_pass", "coll_rows", "coll_fk_substates",
                      "gen_rhs_mr", "gen_rhs_cols", "gen_rhs_linv", "gen_dvalue_middle",
-                     "n_primal_inf_full", "n_dual_inf_full", "n_factor", "gen_pre", "gen_updates"]
+                     "n_primal_inf_full", "n_dual_inf_full", "n_factor", "gen_pre", "gen_updates",
+                     "factor_blocks", "factor_twisted", "unused34", "unused35", "unused36", "unused37", "unused38",
+                     "unused39"]
 
     def enable_profile(self, on=True):
         self._check(self.lib.thip_debug_profile(self.ctx, 1 if on else 0), "thip_debug_profile")
 
     def get_profile(self):
-        out = np.zeros((self.batch, 32), dtype=np.int64)
+        out = np.zeros((self.batch, 40), dtype=np.int64)
         self._check(self.lib.thip_debug_get_profile(self.ctx, out.ctypes.data_as(C.POINTER(C.c_longlong))),
                     "thip_debug_get_profile")
         return out
