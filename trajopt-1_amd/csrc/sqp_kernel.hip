@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <type_traits>
 
 #include "collision_device.hpp"
 #include "kin_device.hpp"
@@ -31,6 +32,11 @@ constexpr int kOct = 8;
 // iterations per thread issued together in the generic ADMM step's row and
 // column loops (loads of all of them before any store)
 constexpr int kGenU = 4;
+// ... sized to the loads an iteration issues: a wave tracks at most 63
+// outstanding vector-memory operations (vmcnt), beyond which the issue stalls
+constexpr int kGenULight = 8;  // a few loads per iteration (streaming vectors, bound rows)
+constexpr int kGenUHeavy = 2;  // a CartPose row's coefficients and x (~2 D + 8 loads)
+constexpr int kGenUHinge = 1;  // a hinge row's 2 D coefficients and 2 D x values
 constexpr double kRhoMin = 1e-6, kRhoMax = 1e6, kRhoTol = 1e-4, kRhoEq = 1e3;
 constexpr double kMinScal = 1e-4, kMaxScal = 1e4;
 constexpr double kDivTol = 1.0 / kInf;
@@ -2670,11 +2676,11 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   PROF_LAP(10);
   FOR(col, nx) out[col] = CV[col];
   // aux back-substitution
-  for (int r0 = c.tid; r0 < L.n_abs; r0 += kGenU * kBlock)
+  for (int r0 = c.tid; r0 < L.n_abs; r0 += kGenUHeavy * kBlock)
   {
-    double on[kGenU], op[kGenU];
+    double on[kGenUHeavy], op[kGenUHeavy];
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < kGenUHeavy; ++u)
     {
       const int r = min(r0 + u * kBlock, L.n_abs - 1);
       const int t = c.T.row_step[r];
@@ -2691,7 +2697,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       op[u] = (dn * rp - rr * wn * cross + wp * dn * h) / det;
     }
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < kGenUHeavy; ++u)
     {
       const int r = r0 + u * kBlock;
       if (r >= L.n_abs)
@@ -2700,11 +2706,11 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       out[nx + 2 * r + 1] = op[u];
     }
   }
-  for (int h0 = c.tid; h0 < nh; h0 += kGenU * kBlock)
+  for (int h0 = c.tid; h0 < nh; h0 += kGenUHinge * kBlock)
   {
-    double ov[kGenU];
+    double ov[kGenUHinge];
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < kGenUHinge; ++u)
     {
       const int h = min(h0 + u * kBlock, nh - 1);
       const int t = c.ia(I_HT)[h];
@@ -2715,7 +2721,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       ov[u] = (BA[col] + w * (eta[L.m_base + 2 * h] - rr * g)) / (dn + rr * w * w);
     }
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < kGenUHinge; ++u)
     {
       const int h = h0 + u * kBlock;
       if (h >= nh)
@@ -3143,31 +3149,31 @@ __device__ void admm_step(Ctx& c, Solver& sv)
   // loads above this one's stores and each iteration paid a full memory
   // round trip (config E: 14-DoF x 50 waypoints, ~4,300 rows)
   const int m = c.m(), nc = c.nc();
-  for (int r0 = c.tid; r0 < m; r0 += kGenU * kBlock)
+  for (int r0 = c.tid; r0 < m; r0 += kGenULight * kBlock)
   {
-    double e[kGenU];
+    double e[kGenULight];
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < kGenULight; ++u)
     {
       const int r = min(r0 + u * kBlock, m - 1);
       e[u] = RH[r] * zp[r] - Y[r];
     }
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < kGenULight; ++u)
       if (r0 + u * kBlock < m)
         ETA[r0 + u * kBlock] = e[u];
   }
-  for (int c0 = c.tid; c0 < nc; c0 += kGenU * kBlock)
+  for (int c0 = c.tid; c0 < nc; c0 += kGenULight * kBlock)
   {
-    double e[kGenU];
+    double e[kGenULight];
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < kGenULight; ++u)
     {
       const int col = min(c0 + u * kBlock, nc - 1);
       e[u] = sig * xp[col] - Q[col];
     }
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < kGenULight; ++u)
       if (c0 + u * kBlock < nc)
         BX[c0 + u * kBlock] = e[u];
   }
@@ -3181,12 +3187,13 @@ __device__ void admm_step(Ctx& c, Solver& sv)
   // rows, the columns' bound rows, hinge rows with their hinge variable's
   // bound row), each straight-line: a loop over all rows diverged into every
   // kind's branch in every wave and serialised their loads
-  auto update_rows = [&](int rb, int re, auto zt_of) {
-    for (int r0 = rb + c.tid; r0 < re; r0 += kGenU * kBlock)
+  auto update_rows = [&](int rb, int re, auto zt_of, auto unroll) {
+    constexpr int U = decltype(unroll)::value;  // rows per thread at once (see kGenU)
+    for (int r0 = rb + c.tid; r0 < re; r0 += U * kBlock)
     {
-      double zt[kGenU], rh[kGenU], yv[kGenU], zv[kGenU], lo[kGenU], up[kGenU];
+      double zt[U], rh[U], yv[U], zv[U], lo[U], up[U];
 #pragma unroll
-      for (int u = 0; u < kGenU; ++u)
+      for (int u = 0; u < U; ++u)
       {
         const int r = min(r0 + u * kBlock, re - 1);  // clamped: every load valid
         zt[u] = zt_of(r);
@@ -3197,7 +3204,7 @@ __device__ void admm_step(Ctx& c, Solver& sv)
         up[u] = Up[r];
       }
 #pragma unroll
-      for (int u = 0; u < kGenU; ++u)
+      for (int u = 0; u < U; ++u)
       {
         const int r = r0 + u * kBlock;
         if (r >= re)
@@ -3215,10 +3222,11 @@ __device__ void admm_step(Ctx& c, Solver& sv)
     }
   };
   const Layout& L = c.L;
-  update_rows(0, L.n_rows, [&](int r) { return row_ax(c, r, XT); });
+  update_rows(0, L.n_rows, [&](int r) { return row_ax(c, r, XT); }, std::integral_constant<int, kGenUHeavy>());
   {
     const double* BS = c.a(A_BS);
-    update_rows(L.n_rows, L.m_base, [&](int r) { return BS[r - L.n_rows] * XT[r - L.n_rows]; });
+    update_rows(L.n_rows, L.m_base, [&](int r) { return BS[r - L.n_rows] * XT[r - L.n_rows]; },
+                std::integral_constant<int, kGenULight>());
     if (m > L.m_base)
     {
       // hinge row m_base + 2h: a_t.x_t + a_t+1.x_t+1 + w h; m_base + 2h + 1: the bound row of h
@@ -3230,21 +3238,21 @@ __device__ void admm_step(Ctx& c, Solver& sv)
         if (h2 & 1)
           return BS[col] * XT[col];
         return hinge_dot(HC + h * 2 * D, XT + HT[h] * D, D) + HW[h] * XT[col];
-      });
+      }, std::integral_constant<int, kGenUHinge>());
     }
   }
-  for (int c0 = c.tid; c0 < nc; c0 += kGenU * kBlock)
+  for (int c0 = c.tid; c0 < nc; c0 += kGenULight * kBlock)
   {
-    double xt[kGenU], xo[kGenU];
+    double xt[kGenULight], xo[kGenULight];
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < kGenULight; ++u)
     {
       const int col = min(c0 + u * kBlock, nc - 1);
       xt[u] = XT[col];
       xo[u] = xp[col];
     }
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < kGenULight; ++u)
     {
       const int col = c0 + u * kBlock;
       if (col >= nc)
