@@ -4155,6 +4155,59 @@ __device__ double rho_estimate(Ctx& c, const Norms& nm)
 }
 
 // polish: returns nothing; updates x/z/y buffers on success
+// Loops of the generic (non-segment) code: U iterations per thread at once,
+// the loads of all of them (ld) before any store (st), see kGenU.
+template <int U, typename LD, typename ST>
+__device__ __forceinline__ void gen_loop(const Ctx& c, int b, int e, LD ld, ST st)
+{
+  for (int i0 = b + c.tid; i0 < e; i0 += U * kBlock)
+  {
+    decltype(ld(0)) v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld(min(i0 + u * kBlock, e - 1));  // clamped: every load valid
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+    {
+      const int i = i0 + u * kBlock;
+      if (i >= e)
+        break;
+      st(i, v[u]);
+    }
+  }
+}
+
+// (A x)_r for every row, one straight-line loop per row kind (as the ADMM
+// update): ld(r, ax) gathers the row's other operands, st(r, value) stores
+template <typename LD, typename ST>
+__device__ __forceinline__ void gen_rows_ax(const Ctx& c, const double* x, LD ld, ST st)
+{
+  const Layout& L = c.L;
+  const int m = c.m(), D = L.D;
+  const double* BS = c.a(A_BS);
+  gen_loop<kGenUHeavy>(c, 0, L.n_rows, [&](int r) { return ld(r, row_ax(c, r, x)); }, st);
+  gen_loop<kGenULight>(c, L.n_rows, L.m_base, [&](int r) { return ld(r, BS[r - L.n_rows] * x[r - L.n_rows]); }, st);
+  if (m > L.m_base)
+  {
+    const double *HC = c.a(A_HC), *HW = c.a(A_HW);
+    const int* HT = c.ia(I_HT);
+    gen_loop<kGenUHinge>(c, L.m_base, m,
+                         [&](int r) {
+                           const int h2 = r - L.m_base, h = h2 >> 1, col = L.nc_base + h;
+                           const double ax = (h2 & 1) ? BS[col] * x[col]
+                                                      : hinge_dot(HC + h * 2 * D, x + HT[h] * D, D) + HW[h] * x[col];
+                           return ld(r, ax);
+                         },
+                         st);
+  }
+}
+
+struct RowV
+{
+  double ax, a, b, d, e;
+  int act;
+};
+
 __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
 {
   PROF(4);
@@ -4166,15 +4219,19 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
   double* Y = c.a(A_Y);
   const double *Lo = c.a(A_L), *Up = c.a(A_U), *Q = c.a(A_Q);
   int* ACT = c.ia(I_ACT);
-  FOR(r, c.m())
-  {
-    int f = 0;
-    if (z[r] - Lo[r] < -Y[r])
-      f = -1;
-    else if (Up[r] - z[r] < Y[r])
-      f = 1;
-    ACT[r] = f;
-  }
+  const int m = c.m();
+  // (the loops below are the plain per-row / per-column loops of OSQP's
+  // polish, in the loads-first form of gen_loop / gen_rows_ax)
+  gen_loop<kGenULight>(
+      c, 0, m, [&](int r) { return RowV{ 0.0, z[r], Lo[r], Up[r], Y[r], 0 }; },
+      [&](int r, const RowV& v) {
+        int f = 0;
+        if (v.a - v.b < -v.e)
+          f = -1;
+        else if (v.d - v.a < v.e)
+          f = 1;
+        ACT[r] = f;
+      });
   BSYNC();
   if (!factor(c, sv, delta, true, delta))
   {
@@ -4187,19 +4244,20 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
   double *PB = c.a(A_PB), *PS = c.a(A_PS), *PR = c.a(A_PR), *PZ = c.a(A_PZ);
   double *BX = c.a(A_BXW), *XT = c.a(A_XT);
   const int nc = c.nc();
-  FOR(col, nc)
-  {
-    PB[col] = -Q[col];
-    PR[col] = -Q[col];
-    PS[col] = 0.0;
-  }
-  FOR(r, c.m())
-  {
-    const double b = (ACT[r] < 0) ? Lo[r] : ((ACT[r] > 0) ? Up[r] : 0.0);
-    PB[nc + r] = b;
-    PR[nc + r] = b;
-    PS[nc + r] = 0.0;
-  }
+  gen_loop<kGenULight>(c, 0, nc, [&](int col) { return Q[col]; },
+                       [&](int col, double q) {
+                         PB[col] = -q;
+                         PR[col] = -q;
+                         PS[col] = 0.0;
+                       });
+  gen_loop<kGenULight>(
+      c, 0, m, [&](int r) { return RowV{ 0.0, Lo[r], Up[r], 0.0, 0.0, ACT[r] }; },
+      [&](int r, const RowV& v) {
+        const double b = (v.act < 0) ? v.a : ((v.act > 0) ? v.b : 0.0);
+        PB[nc + r] = b;
+        PR[nc + r] = b;
+        PS[nc + r] = 0.0;
+      });
   BSYNC();
   // OSQP 1.0 polish: one solve with the delta-regularised KKT, then exactly
   // polish_refine_iter iterative-refinement steps on the unregularised KKT.
@@ -4208,40 +4266,53 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
   // waypoint-block normal equations), so the same step count reproduces
   // OSQP's polished point, including when 3 steps leave it inexact.
   const int max_refine = os.polish_refine_iter;
+  const int nchk = (c.s->n_h > 0) ? build_hinge_chunks(c) : 0;
   for (int it = 0; it <= max_refine; ++it)
   {
     // solve K_delta d = PR  (rhs_x + A_act' r_y / delta), d_y = (A_act d_x - r_y) / delta
     double* eta = PZ;  // r_y / delta on active rows
-    FOR(r, c.m()) eta[r] = (ACT[r] != 0) ? PR[nc + r] / delta : 0.0;
-    FOR(col, nc) BX[col] = PR[col];
+    gen_loop<kGenULight>(
+        c, 0, m, [&](int r) { return RowV{ 0.0, PR[nc + r], 0.0, 0.0, 0.0, ACT[r] }; },
+        [&](int r, const RowV& v) { eta[r] = (v.act != 0) ? v.a / delta : 0.0; });
+    gen_loop<kGenULight>(c, 0, nc, [&](int col) { return PR[col]; }, [&](int col, double v) { BX[col] = v; });
     BSYNC();
     reduced_solve(c, sv, true, delta, eta, XT);
-    FOR(col, nc) PS[col] += XT[col];
-    FOR(r, c.m())
-    {
-      if (ACT[r] != 0)
-        PS[nc + r] += (row_ax(c, r, XT) - PR[nc + r]) / delta;
-    }
+    gen_loop<kGenULight>(
+        c, 0, nc, [&](int col) { return RowV{ 0.0, PS[col], XT[col], 0.0, 0.0, 0 }; },
+        [&](int col, const RowV& v) { PS[col] = v.a + v.b; });
+    gen_rows_ax(
+        c, XT, [&](int r, double ax) { return RowV{ ax, PR[nc + r], PS[nc + r], 0.0, 0.0, ACT[r] }; },
+        [&](int r, const RowV& v) {
+          if (v.act != 0)
+            PS[nc + r] = v.b + (v.ax - v.a) / delta;
+        });
     BSYNC();
     if (it == max_refine)
       break;
-    // residual of the unregularised KKT: PR = PB - K [x; y]
-    FOR(col, nc) PR[col] = PB[col] - col_px(c, col, PS) - col_aty(c, col, PS + nc);
-    FOR(r, c.m()) PR[nc + r] = (ACT[r] != 0) ? PB[nc + r] - row_ax(c, r, PS) : 0.0;
+    // residual of the unregularised KKT: PR = PB - K [x; y] (the hinge share of
+    // A'y from row-parallel chunk sums, as compute_residuals)
+    if (nchk > 0)
+      hinge_chunk_sums(c, PS + nc, nchk);
+    gen_loop<kGenUHeavy>(
+        c, 0, nc, [&](int col) { return PB[col] - col_px(c, col, PS) - col_aty(c, col, PS + nc, nchk > 0); },
+        [&](int col, double v) { PR[col] = v; });
+    gen_rows_ax(
+        c, PS, [&](int r, double ax) { return RowV{ ax, PB[nc + r], 0.0, 0.0, 0.0, ACT[r] }; },
+        [&](int r, const RowV& v) { PR[nc + r] = (v.act != 0) ? v.a - v.ax : 0.0; });
     BSYNC();
   }
   // polished point: x, z = A x, y (active) -> normal cone projection
   double* pz = PZ;
   double* py = PR + nc;  // reuse
-  FOR(r, c.m())
-  {
-    const double zr = row_ax(c, r, PS);
-    const double yr = (ACT[r] != 0) ? PS[nc + r] : 0.0;
-    const double tv = zr + yr;
-    const double zc = fmin(fmax(tv, Lo[r]), Up[r]);
-    pz[r] = zc;
-    py[r] = tv - zc;
-  }
+  gen_rows_ax(
+      c, PS, [&](int r, double ax) { return RowV{ ax, PS[nc + r], Lo[r], Up[r], 0.0, ACT[r] }; },
+      [&](int r, const RowV& v) {
+        const double yr = (v.act != 0) ? v.a : 0.0;
+        const double tv = v.ax + yr;
+        const double zc = fmin(fmax(tv, v.b), v.d);
+        pz[r] = zc;
+        py[r] = tv - zc;
+      });
   BSYNC();
   Norms pn;
   compute_residuals(c, PS, pz, py, pn);
@@ -4250,12 +4321,13 @@ __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
                   (pn.dual_res < nm.dual_res && nm.prim_res < 1e-10);
   if (ok)
   {
-    FOR(col, nc) x[col] = PS[col];
-    FOR(r, c.m())
-    {
-      z[r] = pz[r];
-      Y[r] = py[r];
-    }
+    gen_loop<kGenULight>(c, 0, nc, [&](int col) { return PS[col]; }, [&](int col, double v) { x[col] = v; });
+    gen_loop<kGenULight>(
+        c, 0, m, [&](int r) { return RowV{ 0.0, pz[r], py[r], 0.0, 0.0, 0 }; },
+        [&](int r, const RowV& v) {
+          z[r] = v.a;
+          Y[r] = v.b;
+        });
     nm.prim_res = pn.prim_res;
     nm.dual_res = pn.dual_res;
   }
