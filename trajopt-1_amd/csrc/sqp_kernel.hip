@@ -2904,6 +2904,59 @@ __device__ __forceinline__ double col_aty(const Ctx& c, int col, const double* y
   return v;
 }
 
+// Loops of the generic (non-segment) code: U iterations per thread at once,
+// the loads of all of them (ld) before any store (st), see kGenU.
+template <int U, typename LD, typename ST>
+__device__ __forceinline__ void gen_loop(const Ctx& c, int b, int e, LD ld, ST st)
+{
+  for (int i0 = b + c.tid; i0 < e; i0 += U * kBlock)
+  {
+    decltype(ld(0)) v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld(min(i0 + u * kBlock, e - 1));  // clamped: every load valid
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+    {
+      const int i = i0 + u * kBlock;
+      if (i >= e)
+        break;
+      st(i, v[u]);
+    }
+  }
+}
+
+// (A x)_r for every row, one straight-line loop per row kind (as the ADMM
+// update): ld(r, ax) gathers the row's other operands, st(r, value) stores
+template <typename LD, typename ST>
+__device__ __forceinline__ void gen_rows_ax(const Ctx& c, const double* x, LD ld, ST st)
+{
+  const Layout& L = c.L;
+  const int m = c.m(), D = L.D;
+  const double* BS = c.a(A_BS);
+  gen_loop<kGenUHeavy>(c, 0, L.n_rows, [&](int r) { return ld(r, row_ax(c, r, x)); }, st);
+  gen_loop<kGenULight>(c, L.n_rows, L.m_base, [&](int r) { return ld(r, BS[r - L.n_rows] * x[r - L.n_rows]); }, st);
+  if (m > L.m_base)
+  {
+    const double *HC = c.a(A_HC), *HW = c.a(A_HW);
+    const int* HT = c.ia(I_HT);
+    gen_loop<kGenUHinge>(c, L.m_base, m,
+                         [&](int r) {
+                           const int h2 = r - L.m_base, h = h2 >> 1, col = L.nc_base + h;
+                           const double ax = (h2 & 1) ? BS[col] * x[col]
+                                                      : hinge_dot(HC + h * 2 * D, x + HT[h] * D, D) + HW[h] * x[col];
+                           return ld(r, ax);
+                         },
+                         st);
+  }
+}
+
+struct RowV
+{
+  double ax, a, b, d, e;
+  int act;
+};
+
 // ======================================================================
 // OSQP solve on the structured QP (one workgroup)
 // ======================================================================
@@ -3012,23 +3065,25 @@ __device__ bool is_primal_infeasible(Ctx& c, double eps)
     c.s->prof[27] += 1;  // calls (diagnostic count)
   double* DY = c.a(A_DY);
   const double *Lo = c.a(A_L), *Up = c.a(A_U), *E = c.a(A_E), *DS = c.a(A_DS);
+  const int m = c.m();
   double nv[1] = { 0 };
-  FOR(r, c.m())
-  {
-    double dy = DY[r];
-    if (Up[r] > kInf * kMinScal)
-      dy = (Lo[r] < -kInf * kMinScal) ? 0.0 : fmin(dy, 0.0);
-    else if (Lo[r] < -kInf * kMinScal)
-      dy = fmax(dy, 0.0);
-    DY[r] = dy;
-    nv[0] = fmax(nv[0], fabs(E[r] * dy));
-  }
+  double lhs = 0;  // this thread's rows in FOR order, as the plain loop
+  gen_loop<kGenULight>(
+      c, 0, m, [&](int r) { return RowV{ 0.0, DY[r], Up[r], Lo[r], E[r], 0 }; },
+      [&](int r, const RowV& v) {
+        double dy = v.a;
+        if (v.b > kInf * kMinScal)
+          dy = (v.d < -kInf * kMinScal) ? 0.0 : fmin(dy, 0.0);
+        else if (v.d < -kInf * kMinScal)
+          dy = fmax(dy, 0.0);
+        DY[r] = dy;
+        nv[0] = fmax(nv[0], fabs(v.e * dy));
+        lhs += v.b * fmax(dy, 0.0) + v.d * fmin(dy, 0.0);
+      });
   block_max<1>(c, nv);
   const double ndy = nv[0];
   if (!(ndy > kDivTol))
     return false;
-  double lhs = 0;
-  FOR(r, c.m()) lhs += Up[r] * fmax(DY[r], 0.0) + Lo[r] * fmin(DY[r], 0.0);
   lhs = block_sum(c, lhs);
   if (!(lhs < eps * ndy))
     return false;
@@ -3039,7 +3094,9 @@ __device__ bool is_primal_infeasible(Ctx& c, double eps)
     BSYNC();  // DY rewritten above
     hinge_chunk_sums(c, DY, build_hinge_chunks(c));
   }
-  FOR(col, c.nc()) av[0] = fmax(av[0], fabs((1.0 / DS[col]) * col_aty(c, col, DY, chunked)));
+  gen_loop<kGenUHeavy>(
+      c, 0, c.nc(), [&](int col) { return (1.0 / DS[col]) * col_aty(c, col, DY, chunked); },
+      [&](int, double v) { av[0] = fmax(av[0], fabs(v)); });
   block_max<1>(c, av);
   return av[0] < eps * ndy;
 }
@@ -3050,29 +3107,36 @@ __device__ bool is_dual_infeasible(Ctx& c, double eps)
     c.s->prof[28] += 1;  // calls (diagnostic count)
   const double *DX = c.a(A_DX), *DS = c.a(A_DS), *Q = c.a(A_Q), *E = c.a(A_E), *Lo = c.a(A_L), *Up = c.a(A_U);
   double nv[1] = { 0 };
-  FOR(col, c.nc()) nv[0] = fmax(nv[0], fabs(DS[col] * DX[col]));
+  double qdx = 0;  // this thread's columns in FOR order, as the plain loop
+  gen_loop<kGenULight>(
+      c, 0, c.nc(), [&](int col) { return RowV{ 0.0, DS[col], DX[col], Q[col], 0.0, 0 }; },
+      [&](int, const RowV& v) {
+        nv[0] = fmax(nv[0], fabs(v.a * v.b));
+        qdx += v.d * v.b;
+      });
   block_max<1>(c, nv);
   const double ndx = nv[0];
   const double cs = c.s->c;
   if (!(ndx > kDivTol))
     return false;
-  double qdx = 0;
-  FOR(col, c.nc()) qdx += Q[col] * DX[col];
   qdx = block_sum(c, qdx);
   if (!(qdx < cs * eps * ndx))
     return false;
   double pv[1] = { 0 };
-  FOR(col, c.nc()) pv[0] = fmax(pv[0], fabs((1.0 / DS[col]) * col_px(c, col, DX)));
+  gen_loop<kGenULight>(
+      c, 0, c.nc(), [&](int col) { return (1.0 / DS[col]) * col_px(c, col, DX); },
+      [&](int, double v) { pv[0] = fmax(pv[0], fabs(v)); });
   block_max<1>(c, pv);
   if (!(pv[0] < cs * eps * ndx))
     return false;
   double bad[1] = { 0 };
-  FOR(r, c.m())
-  {
-    const double adx = (1.0 / E[r]) * row_ax(c, r, DX);
-    if (((Up[r] < kInf * kMinScal) && (adx > eps * ndx)) || ((Lo[r] > -kInf * kMinScal) && (adx < -eps * ndx)))
-      bad[0] = 1.0;
-  }
+  gen_rows_ax(
+      c, DX, [&](int r, double ax) { return RowV{ ax, E[r], Up[r], Lo[r], 0.0, 0 }; },
+      [&](int, const RowV& v) {
+        const double adx = (1.0 / v.a) * v.ax;
+        if (((v.b < kInf * kMinScal) && (adx > eps * ndx)) || ((v.d > -kInf * kMinScal) && (adx < -eps * ndx)))
+          bad[0] = 1.0;
+      });
   block_max<1>(c, bad);
   return bad[0] == 0.0;
 }
@@ -4155,59 +4219,6 @@ __device__ double rho_estimate(Ctx& c, const Norms& nm)
 }
 
 // polish: returns nothing; updates x/z/y buffers on success
-// Loops of the generic (non-segment) code: U iterations per thread at once,
-// the loads of all of them (ld) before any store (st), see kGenU.
-template <int U, typename LD, typename ST>
-__device__ __forceinline__ void gen_loop(const Ctx& c, int b, int e, LD ld, ST st)
-{
-  for (int i0 = b + c.tid; i0 < e; i0 += U * kBlock)
-  {
-    decltype(ld(0)) v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld(min(i0 + u * kBlock, e - 1));  // clamped: every load valid
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-    {
-      const int i = i0 + u * kBlock;
-      if (i >= e)
-        break;
-      st(i, v[u]);
-    }
-  }
-}
-
-// (A x)_r for every row, one straight-line loop per row kind (as the ADMM
-// update): ld(r, ax) gathers the row's other operands, st(r, value) stores
-template <typename LD, typename ST>
-__device__ __forceinline__ void gen_rows_ax(const Ctx& c, const double* x, LD ld, ST st)
-{
-  const Layout& L = c.L;
-  const int m = c.m(), D = L.D;
-  const double* BS = c.a(A_BS);
-  gen_loop<kGenUHeavy>(c, 0, L.n_rows, [&](int r) { return ld(r, row_ax(c, r, x)); }, st);
-  gen_loop<kGenULight>(c, L.n_rows, L.m_base, [&](int r) { return ld(r, BS[r - L.n_rows] * x[r - L.n_rows]); }, st);
-  if (m > L.m_base)
-  {
-    const double *HC = c.a(A_HC), *HW = c.a(A_HW);
-    const int* HT = c.ia(I_HT);
-    gen_loop<kGenUHinge>(c, L.m_base, m,
-                         [&](int r) {
-                           const int h2 = r - L.m_base, h = h2 >> 1, col = L.nc_base + h;
-                           const double ax = (h2 & 1) ? BS[col] * x[col]
-                                                      : hinge_dot(HC + h * 2 * D, x + HT[h] * D, D) + HW[h] * x[col];
-                           return ld(r, ax);
-                         },
-                         st);
-  }
-}
-
-struct RowV
-{
-  double ax, a, b, d, e;
-  int act;
-};
-
 __device__ void polish(Ctx& c, Solver& sv, Norms& nm)
 {
   PROF(4);
