@@ -2378,12 +2378,12 @@ __device__ __forceinline__ double twisted_dvalue(const Ctx& c, const double* LIp
   for (int k = 0; k < kOct; ++k)
   {
     const int kk = (k < D) ? k : D - 1;
-    const double a = LI[t * DD + kk * D + i] * YV[t * D + kk];
-    const bool use = (k >= i) && (k < D);
+    // masked by a 0/1 multiplier, not a select (see masked_dot)
+    const double a = LI[t * DD + kk * D + i] * (YV[t * D + kk] * (((k >= i) && (k < D)) ? 1.0 : 0.0));
     if (k & 1)
-      v1 = use ? v1 + a : v1;
+      v1 += a;
     else
-      v0 = use ? v0 + a : v0;
+      v0 += a;
   }
   return v0 + v1;
 }
@@ -2829,10 +2829,11 @@ __device__ void hinge_chunk_sums(Ctx& c, const double* v, int nchk)
       for (int i = 0; i < kHChunk; i += 2)
       {
         const int ha = min(h0 + i, h1 - 1), hb = min(h0 + i + 1, h1 - 1);
-        const double aa = HC[ha * 2 * D + k] * v[mb + 2 * ha];
-        const double ab = HC[hb * 2 * D + k] * v[mb + 2 * hb];
-        s0 = (h0 + i < h1) ? s0 + aa : s0;
-        s1 = (h0 + i + 1 < h1) ? s1 + ab : s1;
+        // masked by 0/1 multipliers, not selects (see masked_dot)
+        const double aa = HC[ha * 2 * D + k] * (v[mb + 2 * ha] * ((h0 + i < h1) ? 1.0 : 0.0));
+        const double ab = HC[hb * 2 * D + k] * (v[mb + 2 * hb] * ((h0 + i + 1 < h1) ? 1.0 : 0.0));
+        s0 += aa;
+        s1 += ab;
       }
       PART[q * pw + k] = s0 + s1;
     }
@@ -3647,8 +3648,9 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
           const int ha = min(h0 + i, h1 - 1), hb = min(h0 + i + 1, h1 - 1);  // in bounds
           const double aa = HTP[k * nhs + ha], ma = MRl[nr + ha];
           const double ab = HTP[k * nhs + hb], mb2 = MRl[nr + hb];
-          s0 = (h0 + i < h1) ? s0 + aa * ma : s0;
-          s1 = (h0 + i + 1 < h1) ? s1 + ab * mb2 : s1;
+          // masked by 0/1 multipliers, not selects (see masked_dot)
+          s0 += aa * (ma * ((h0 + i < h1) ? 1.0 : 0.0));
+          s1 += ab * (mb2 * ((h0 + i + 1 < h1) ? 1.0 : 0.0));
         }
         PARTlw[q * 16 + k] = s0 + s1;
       }
@@ -3673,8 +3675,9 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
         const int kk = (k < D) ? k : D - 1;
         const double a0 = HTP[kk * nhs + h], a1 = HTP[(D + kk) * nhs + h];
         const double x0 = lds(CV)[t0 + kk], x1 = lds(CV)[t0 + D + kk];
-        g0 = (k < D) ? g0 + a0 * x0 : g0;
-        g1 = (k < D) ? g1 + a1 * x1 : g1;
+        const double mk = (k < D) ? 1.0 : 0.0;  // a 0/1 multiplier, not a select (see masked_dot)
+        g0 += a0 * (x0 * mk);
+        g1 += a1 * (x1 * mk);
       }
       const double g = g0 + g1;
       const double av = (rn + w * (eta - rho_s * g)) * deni;
@@ -3932,10 +3935,11 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
         for (int j = 0; j < kOct; ++j)
         {
           const double xv = lds(CV)[t * D + ((j < D) ? j : D - 1)];
+          const double xm = xv * ((j < D) ? 1.0 : 0.0);  // a 0/1 multiplier, not a select
           if (j & 1)
-            g1 = (j < D) ? g1 + ags[u][j] * xv : g1;
+            g1 += ags[u][j] * xm;
           else
-            g0 = (j < D) ? g0 + ags[u][j] * xv : g0;
+            g0 += ags[u][j] * xm;
         }
         const double g = g0 + g1;
         const double dn = adn[u], dp = adp[u], wn = awn[u], wp = awp[u], rr = arr[u];
