@@ -4099,9 +4099,8 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
         const int t = at[u];
         double ax = 0;
 #pragma unroll
-        for (int j = 0; j < kOct; ++j)
-          if (j < D)
-            ax += ags[u][j] * lds(YV)[t * D + j];
+        for (int j = 0; j < kOct; ++j)  // 0/1 multiplier, not a guard (see masked_dot)
+          ax += ags[u][j] * (lds(YV)[t * D + min(j, D - 1)] * ((j < D) ? 1.0 : 0.0));
         ax += awn[u] * axn[u] + awp[u] * axp[u];
         const double er = E[r], en = E[brn], ep = E[brp], dn = DS[ca], dp = DS[ca + 1];
         row_terms(ax, azr[u], er);
