@@ -955,3 +955,20 @@ def test_contact_capacity_overflow_fails_loudly():
     over = [r for r in res if r.flags & 1]
     assert over, "expected at least one problem over 4 contacts"
     assert all(r.status == 4 for r in over)
+
+
+@pytest.mark.parametrize("cfg,B", [("B", 32), ("C", 32)])
+def test_sqp_parity_generic_step(oracle_mod, cfg, B, monkeypatch):
+    """The generic ADMM step (admm_step + reduced_solve: loads-first loops, masked
+    products, per-row-kind updates) on problems the register-resident segment
+    would otherwise run (THIP_NO_SEGMENT=1, read by thip_create): same parity bar
+    against the oracle, and the same outcomes as the segment path."""
+    wl = problems.make_workload(cfg, B)
+    x_seg, res_seg, _ = solve_gpu(wl)
+    monkeypatch.setenv("THIP_NO_SEGMENT", "1")
+    x, res, tr = solve_gpu(wl, trace=2048)
+    monkeypatch.delenv("THIP_NO_SEGMENT")
+    check_parity(wl, oracle_mod, x, res, tr, label=f"{cfg}-generic")
+    same = sum(int(a.status == b.status and np.abs(xa - xb).max() <= TOL_X)
+               for a, b, xa, xb in zip(res, res_seg, x, x_seg))
+    assert same >= 0.85 * B, f"{cfg}: generic step and segment agree on {same} of {B} problems"

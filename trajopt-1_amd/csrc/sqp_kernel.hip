@@ -3188,7 +3188,10 @@ __device__ bool check_termination(Ctx& c, const Norms& nm, bool approx)
   return st != 0;
 }
 
-__device__ void admm_step(Ctx& c, Solver& sv)
+// pre_ready: ETA and BX already hold this step's rho zp - y and sigma xp - q
+// (the previous admm_step computed them from its new iterate, with rho
+// unchanged since); every step leaves them ready for the next one
+__device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
 {
   PROF(0);
   const thip_osqp_settings& os = c.d->osqp;
@@ -3214,7 +3217,7 @@ __device__ void admm_step(Ctx& c, Solver& sv)
   // loads above this one's stores and each iteration paid a full memory
   // round trip (config E: 14-DoF x 50 waypoints, ~4,300 rows)
   const int m = c.m(), nc = c.nc();
-  for (int r0 = c.tid; r0 < m; r0 += kGenULight * kBlock)
+  for (int r0 = c.tid; r0 < (pre_ready ? 0 : m); r0 += kGenULight * kBlock)
   {
     double e[kGenULight];
 #pragma unroll
@@ -3228,7 +3231,7 @@ __device__ void admm_step(Ctx& c, Solver& sv)
       if (r0 + u * kBlock < m)
         ETA[r0 + u * kBlock] = e[u];
   }
-  for (int c0 = c.tid; c0 < nc; c0 += kGenULight * kBlock)
+  for (int c0 = c.tid; c0 < (pre_ready ? 0 : nc); c0 += kGenULight * kBlock)
   {
     double e[kGenULight];
 #pragma unroll
@@ -3282,7 +3285,9 @@ __device__ void admm_step(Ctx& c, Solver& sv)
         z[r] = zr;
         const double dy = rho * (al * zt[u] + (1.0 - al) * zv[u] - zr);
         DY[r] = dy;
-        Y[r] = yv[u] + dy;
+        const double yn = yv[u] + dy;
+        Y[r] = yn;
+        ETA[r] = rho * zr - yn;  // the next step's rho zp - y (same expression)
       }
     }
   };
@@ -3308,13 +3313,14 @@ __device__ void admm_step(Ctx& c, Solver& sv)
   }
   for (int c0 = c.tid; c0 < nc; c0 += kGenULight * kBlock)
   {
-    double xt[kGenULight], xo[kGenULight];
+    double xt[kGenULight], xo[kGenULight], qv[kGenULight];
 #pragma unroll
     for (int u = 0; u < kGenULight; ++u)
     {
       const int col = min(c0 + u * kBlock, nc - 1);
       xt[u] = XT[col];
       xo[u] = xp[col];
+      qv[u] = Q[col];
     }
 #pragma unroll
     for (int u = 0; u < kGenULight; ++u)
@@ -3325,6 +3331,7 @@ __device__ void admm_step(Ctx& c, Solver& sv)
       const double xv = al * xt[u] + (1.0 - al) * xo[u];
       x[col] = xv;
       DX[col] = xv - xo[u];
+      BX[col] = sig * xv - qv[u];  // the next step's sigma xp - q (same expression)
     }
   }
   BSYNC();
@@ -4474,6 +4481,7 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   // the segment addresses MR, the hinge chunk table and chunk sums as LDS
   const bool seg = L.seg_ok && lds_resident(c, c.a(A_MR)) &&
                    (c.s->n_h == 0 || (lds_resident(c, c.a(A_HCHK)) && lds_resident(c, c.a(A_HPART))));
+  bool pre_ready = false;  // admm_step's ETA / BX (cleared when rho changes)
   for (it = 1; it <= os.max_iter; ++it)
   {
     if (seg)
@@ -4493,7 +4501,8 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
     }
     else
     {
-      admm_step(c, sv);
+      admm_step(c, sv, pre_ready);
+      pre_ready = true;
       have_res = false;
     }
     can_check = ct && (it % ct == 0);
@@ -4530,6 +4539,7 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
             RH[r] = kRhoEq * nr;
         }
         BSYNC();
+        pre_ready = false;  // ETA = rho zp - y changes with rho
         if (!factor(c, sv, os.sigma, false, 0.0))
         {
           fail = true;
