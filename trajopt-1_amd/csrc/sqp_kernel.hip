@@ -3299,16 +3299,44 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
                 std::integral_constant<int, kGenULight>());
     if (m > L.m_base)
     {
-      // hinge row m_base + 2h: a_t.x_t + a_t+1.x_t+1 + w h; m_base + 2h + 1: the bound row of h
+      // hinge row m_base + 2h: a_t.x_t + a_t+1.x_t+1 + w h; m_base + 2h + 1:
+      // the bound row of h.  One thread per hinge variable updates both rows
+      // (a loop over the rows alternated the two kinds lane by lane)
       const double *HC = c.a(A_HC), *HW = c.a(A_HW);
       const int* HT = c.ia(I_HT);
-      const int D = L.D;
-      update_rows(L.m_base, m, [&](int r) {
-        const int h2 = r - L.m_base, h = h2 >> 1, col = L.nc_base + h;
-        if (h2 & 1)
-          return BS[col] * XT[col];
-        return hinge_dot(HC + h * 2 * D, XT + HT[h] * D, D) + HW[h] * XT[col];
-      }, std::integral_constant<int, kGenUHinge>());
+      const int D = L.D, nh = (m - L.m_base) >> 1;
+      for (int h = c.tid; h < nh; h += kBlock)
+      {
+        const int col = L.nc_base + h, r0 = L.m_base + 2 * h;
+        const double xh = XT[col];
+        const double zt2[2] = { hinge_dot(HC + h * 2 * D, XT + HT[h] * D, D) + HW[h] * xh, BS[col] * xh };
+        double rh[2], yv[2], zv[2], lo[2], up[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+        {
+          rh[u] = RH[r0 + u];
+          yv[u] = Y[r0 + u];
+          zv[u] = zp[r0 + u];
+          lo[u] = Lo[r0 + u];
+          up[u] = Up[r0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+        {
+          const int r = r0 + u;
+          const double rho = rh[u];
+          double zr = (1.0 / rho) * yv[u];
+          zr = zr + al * zt2[u];
+          zr = zr + (1.0 - al) * zv[u];
+          zr = fmin(fmax(zr, lo[u]), up[u]);
+          z[r] = zr;
+          const double dy = rho * (al * zt2[u] + (1.0 - al) * zv[u] - zr);
+          DY[r] = dy;
+          const double yn = yv[u] + dy;
+          Y[r] = yn;
+          ETA[r] = rho * zr - yn;
+        }
+      }
     }
   }
   for (int c0 = c.tid; c0 < nc; c0 += kGenULight * kBlock)
