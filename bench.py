@@ -241,7 +241,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (splitmix64 seeds 20261015+b, PR2 right arm; SURVEY.md §8d)",
+            "data": "synthetic (splitmix64 seeds 20261015+b, PR2 %s; SURVEY.md §8d)"
+                    % ("both arms" if wl.n_dof == 14 else "right arm"),
             "config": {
                 "workload": wname,
                 "batch_per_gpu": args.batch,
