@@ -105,24 +105,98 @@ def measured_traffic(workload_name, batch):
     return best[1]["hbm_bytes_per_launch"], best[0]
 
 
+def host_cpus():
+    """(CPUs this process may use, host nproc, CPU model, cgroup CPU quota).
+    The usable count is the scheduler affinity capped by the cgroup quota
+    (cpu.max), so a container that sees the whole machine but is limited to a
+    share of it reports the share."""
+    nproc = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = nproc
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+            usable = max(1, min(usable, int(quota)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, nproc, model, quota
+
+
 def cpu_baseline(config, n_problems, threads):
-    """Oracle (CPU restatement of the reference path) on a bounded sample."""
+    """The oracle (CPU restatement of the reference path) timed on a bounded
+    sample of the same problems: its -O3 FMA build for the host's ISA level
+    (oracle/Makefile liboracle_fast_*), one problem per thread on every CPU the
+    process may use, plus the one-thread latency of one problem."""
     sys.path.insert(0, str(ROOT))
     from oracle import oracle  # checker / baseline only
 
-    wl = problems.make_workload(config, n_problems)
+    usable, nproc, model, quota = host_cpus()
+    threads = usable if threads <= 0 else threads
+    n = n_problems if n_problems > 0 else min(1024, max(128, 2 * threads))
+    wl = problems.make_workload(config, n)
     t0 = time.perf_counter()
-    _, res = oracle.solve(wl, n_threads=threads)
+    _, res = oracle.solve(wl, n_threads=threads, variant="fast")
     dt = time.perf_counter() - t0
     iters = sum(r.n_sqp_iters for r in res)
+    one = problems.make_workload(config, 1)
+    t1 = time.perf_counter()
+    _, r1 = oracle.solve(one, n_threads=1, variant="fast")
+    lat = time.perf_counter() - t1
     return {
         "value": iters / dt,
         "unit": "SQP iters/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"first {n_problems} problems of the same workload (seeds 20261015+b), "
-                  f"{iters} SQP iterations in {dt:.1f} s, one problem per thread",
+        "sample": f"first {n} problems of the same workload (seeds 20261015+b), {iters} SQP iterations in "
+                  f"{dt:.1f} s, one problem per thread on {threads} threads",
+        "build": oracle.variant_path("fast").name + " (g++ -O3 -ffp-contract=fast, x86-64-v3/v4 by host ISA)",
+        "host_nproc": nproc,
+        "host_cpu_model": model,
+        "cgroup_cpu_quota": quota,
+        "single_problem_latency_s": lat,
+        "single_problem_sqp_iters": r1[0].n_sqp_iters,
+        "single_thread_sqp_iters_per_s": r1[0].n_sqp_iters / lat,
     }
+
+
+def latency_model(config):
+    """The newest committed critical-path model of the kernel (profiles/*_latency_<config>.json,
+    tools/latency_model.py): cycles per ADMM iteration on the serial path against the measured."""
+    best = None
+    for p in sorted((ROOT / "profiles").glob(f"*_latency_{config}.json")):
+        try:
+            best = json.loads(p.read_text()) | {"source": p.name}
+        except (OSError, ValueError):
+            continue
+    return best
+
+
+def pmc_evidence(config):
+    """The newest committed counter summary of sqp_kernel (profiles/*_pmc_<config>.json,
+    tools/pmc_latency.sh): where the wave cycles go."""
+    best = None
+    for p in sorted((ROOT / "profiles").glob(f"*_pmc_{config}.json")):
+        try:
+            d = json.loads(p.read_text())
+        except (OSError, ValueError):
+            continue
+        if "wave_cycle_split" in d:
+            best = {"source": p.name, "wave_cycle_split": d["wave_cycle_split"],
+                    "lds_bank_conflict_share": d.get("lds_bank_conflict_share"),
+                    "measured_hbm_gbs": d.get("measured_hbm_gbs")}
+    return best
 
 
 def main():
@@ -133,8 +207,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1024, help="problems per GPU")
     ap.add_argument("--config", default="C")
     ap.add_argument("--inflight", type=int, default=3, help="batch contexts (streams) in flight")
-    ap.add_argument("--cpu-problems", type=int, default=256)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-problems", type=int, default=0, help="0: max(128, 2 x threads), at most 1024")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this process may use")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -255,7 +329,13 @@ def main():
                 "batch_latency_ms": batch_latency_ms,
             },
             "roofline": {
-                "bound": "hbm",
+                # what limits the kernel: the serial block-tridiagonal KKT chains and
+                # barriers of every ADMM iteration (one 256-thread problem per CU; wave
+                # cycles mostly parked on s_waitcnt / barriers, see `pmc`).  `achieved` /
+                # `frac` are the SURVEY.md 8d streaming-byte model against HBM peak, as
+                # the metric asks; the working set is LDS/register resident, so the
+                # measured HBM traffic (`traffic`, `measured_gbs`) is far below it.
+                "bound": "latency",
                 "kernel": "thip::sqp_kernel",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
@@ -265,9 +345,8 @@ def main():
                 "traffic_source": traffic_src,
                 "measured_gbs": (traffic / (kms * 1e-3) / 1e9) if traffic else None,
                 "achieved_per_step_gbs": aggregate,
-                "limiter": "latency (serial block-tridiagonal KKT chain per ADMM iteration, one problem per CU); "
-                           "`achieved` is the SURVEY.md 8d streaming-byte model, measured HBM traffic is "
-                           "`measured_gbs` (working set LDS/register resident)",
+                "latency": latency_model(args.config),
+                "pmc": pmc_evidence(args.config),
                 "kernel_ms": kms,
                 "algorithmic_bytes_per_launch": bytes_local,
                 "model": model,

@@ -43,6 +43,11 @@
 extern "C" {
 #endif
 
+/* ABI version of the structs below: thip_create rejects a descriptor whose
+ * abi_version differs (a caller compiled against another layout).  3: the
+ * descriptor carries abi_version, thip_chain.is_tree, thip_sqp_params.max_time. */
+#define THIP_ABI_VERSION 3
+
 #define THIP_MAX_DOF 16
 #define THIP_MAX_LINKS 32
 #define THIP_MAX_STEPS 64
@@ -97,15 +102,18 @@ extern "C" {
  * joint motion about/along `joint_axis` (expressed in the joint frame).  A
  * serial chain (the reference's right_arm / left_arm groups) has parent[k] =
  * k - 1; a dual-arm group (both PR2 arms off torso_lift_link) branches at the
- * root.  The segment's register-resident ADMM path takes n_dof <= 8; larger
- * groups (up to THIP_MAX_DOF) run the generic block solve. */
+ * root.  `parent` is read only when is_tree = 1: a zero-initialised chain is a
+ * serial chain (parent[k] = k - 1), never a star.  The segment's
+ * register-resident ADMM path takes n_dof <= 8; larger groups (up to
+ * THIP_MAX_DOF) run the generic block solve. */
 typedef struct thip_chain {
   int n_links;
   int n_dof;
+  int is_tree;                            /* 0: serial chain (parent[] ignored); 1: tree, parent[] used */
   double base_pose[12];
   int joint_type[THIP_MAX_LINKS];
   int joint_dof[THIP_MAX_LINKS];          /* dof index for movable joints, -1 for fixed */
-  int parent[THIP_MAX_LINKS];             /* parent link of link k >= 1 (0 <= parent[k] < k) */
+  int parent[THIP_MAX_LINKS];             /* is_tree: parent link of link k >= 1 (0 <= parent[k] < k) */
   double joint_origin[THIP_MAX_LINKS][12];
   double joint_axis[THIP_MAX_LINKS][3];
   double lower[THIP_MAX_DOF];             /* joint limits -> variable bounds */
@@ -128,6 +136,10 @@ typedef struct thip_sqp_params {
   double initial_merit_error_coeff; /* 10 */
   int inflate_constraints_individually; /* 1 */
   double trust_box_size;            /* 0.1 */
+  double max_time;                  /* seconds, DBL_MAX = no limit (optimizers.hpp:117): checked at the
+                                       top of every SQP iteration against the problem's own clock (its
+                                       workgroup's start); past it the run ends with OPT_TIME_LIMIT, or
+                                       OPT_CONVERGED when no constraint is violated (optimizers.cpp:739-753) */
 } thip_sqp_params;
 
 /* OSQP settings as configured by OSQPModelConfig::setDefaultOSQPSettings
@@ -157,6 +169,7 @@ typedef struct thip_osqp_settings {
  * (initial trajectory, CartPose target poses, scene primitives) is uploaded
  * separately, batched. */
 typedef struct thip_problem_desc {
+  int abi_version;  /* THIP_ABI_VERSION */
   int n_steps;
   thip_chain chain;
 
@@ -396,6 +409,15 @@ int thip_debug_get_profile(thip_ctx* ctx, long long* counters /* [batch][40] */)
  * dims = {N, D, nx, n_fixed_rows, n_abs, n_cols, n_rows, m, dstride, istride,
  * n_double_arrays, n_int_arrays}) and a copy of the device workspace. */
 int thip_debug_layout(thip_ctx* ctx, long long* doff, long long* ioff, long long* dims);
+/* Diagnostics: force a solve path for every context created after the call
+ * (process-wide; 0 restores the automatic choice).  THIP_DEBUG_NO_SEGMENT runs
+ * the generic ADMM step instead of the register-resident segment,
+ * THIP_DEBUG_FORCE_WIDE the wide-block (D > 8) solve for any D.  Same
+ * results to the parity bar; for tests and profiling only (the product path
+ * never reads the environment). */
+#define THIP_DEBUG_NO_SEGMENT 1
+#define THIP_DEBUG_FORCE_WIDE 2
+int thip_debug_set_path(int flags);
 int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws);
 
 #ifdef __cplusplus

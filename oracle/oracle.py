@@ -23,7 +23,32 @@ from trajopt_amd import abi  # noqa: E402
 
 LIB = ROOT / "build" / "liboracle.so"
 KAT = ROOT / "build" / "kat"
-_lib = None
+_libs = {}
+
+
+def _has_avx512():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("flags"):
+                    return " avx512f " in ln + " "
+    except OSError:
+        pass
+    return False
+
+
+def variant_path(variant="exact"):
+    """exact: the parity checker (no FMA contraction).  fast: the same sources at
+    -O3 with FMA contraction for the highest x86-64 ISA level this host runs
+    (v4 with AVX-512, else v3) -- the timed CPU baseline, and a second rounding
+    of the same algorithm for the parity gate's stability proofs."""
+    if variant == "exact":
+        return LIB
+    if variant == "fast":
+        return ROOT / "build" / ("liboracle_fast_v4.so" if _has_avx512() else "liboracle_fast_v3.so")
+    if variant == "san":
+        return ROOT / "build" / "liboracle_san.so"
+    raise ValueError(variant)
 
 
 def build(quiet=True):
@@ -35,12 +60,12 @@ def build(quiet=True):
         print(out.stdout)
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not LIB.exists():
+def lib(variant="exact"):
+    if variant not in _libs:
+        path = variant_path(variant)
+        if not path.exists():
             build()
-        L = C.CDLL(str(LIB))
+        L = C.CDLL(str(path))
         P = C.POINTER
         dp = P(C.c_double)
         L.oracle_solve_batch.argtypes = [P(abi.ProblemDesc), C.c_int, dp, dp, dp, dp, dp, P(abi.Result), C.c_int]
@@ -56,8 +81,8 @@ def lib():
         assert L.oracle_sizeof_desc() == C.sizeof(abi.ProblemDesc), "descriptor layout mismatch"
         L.oracle_sizeof_result.restype = C.c_int
         assert L.oracle_sizeof_result() == C.sizeof(abi.Result), "result layout mismatch (rebuild the oracle)"
-        _lib = L
-    return _lib
+        _libs[variant] = L
+    return _libs[variant]
 
 
 def _dp(a):
@@ -73,10 +98,10 @@ def _jpos(wl, b=None):
     return np.ascontiguousarray(jt if b is None else jt[b], dtype=np.float64)
 
 
-def solve(wl, n_threads=1):
+def solve(wl, n_threads=1, variant="exact"):
     """BasicTrustRegionSQP::optimize for every problem of the workload.
     Returns (x [B,N,D], list of abi.Result)."""
-    L = lib()
+    L = lib(variant)
     B = wl.batch
     init = np.ascontiguousarray(wl.init, dtype=np.float64)
     tg = np.ascontiguousarray(wl.targets, dtype=np.float64) if wl.targets.size else None

@@ -230,7 +230,7 @@ void chainFwdKin(const thip_chain& chain, const double* q, std::vector<Iso3>& ou
   out[0] = Iso3::from12(chain.base_pose);
   for (int k = 1; k < chain.n_links; ++k)
   {
-    Iso3 t = mul(out[static_cast<std::size_t>(chain.parent[k])], Iso3::from12(chain.joint_origin[k]));
+    Iso3 t = mul(out[static_cast<std::size_t>(parentOf(chain, k))], Iso3::from12(chain.joint_origin[k]));
     const int type = chain.joint_type[k];
     if (type == THIP_JOINT_REVOLUTE || type == THIP_JOINT_CONTINUOUS)
       t = mul(t, axisAngle(chain.joint_axis[k], q[chain.joint_dof[k]]));
@@ -256,7 +256,7 @@ void chainJacobian(const thip_chain& chain, const double* q, int link, double* J
   // the joints on the link's path from the root (a tree: other branches do
   // not move it)
   std::vector<char> on_path(static_cast<std::size_t>(chain.n_links), 0);
-  for (int k = link; k > 0; k = chain.parent[k])
+  for (int k = link; k > 0; k = parentOf(chain, k))
     on_path[static_cast<std::size_t>(k)] = 1;
   for (int k = 1; k <= link; ++k)
   {

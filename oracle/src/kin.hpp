@@ -20,6 +20,10 @@
 
 namespace orc
 {
+// parent link of k >= 1: thip_chain.parent when the chain is a tree, else k - 1
+// (a zero-initialised chain is serial, include/trajopt_hip.h)
+inline int parentOf(const thip_chain& c, int k) { return c.is_tree ? c.parent[k] : k - 1; }
+
 struct Iso3
 {
   // row-major R (3x3) and t

@@ -1,5 +1,6 @@
 // ORACLE — test infrastructure only (see sco_expr.hpp header).
 // Restatement of trajopt_sco modelling + OSQPModel + BasicTrustRegionSQP.
+#include <chrono>
 #include "sco.hpp"
 
 #include <algorithm>
@@ -944,6 +945,7 @@ OptStatus BasicTrustRegionSQP::optimize()
     throw std::runtime_error("you forgot to initialize!");
   results_.x = prob_->getClosestFeasiblePoint(results_.x);
   OptStatus retval = INVALID;
+  const auto start_time = std::chrono::steady_clock::now();
 
   auto evalCosts = [&](const DblVec& x) {
     DblVec out(costs.size());
@@ -962,6 +964,16 @@ OptStatus BasicTrustRegionSQP::optimize()
   {
     for (int iter = 1;; ++iter)
     {
+      // time limit (optimizers.cpp:739-753): checked before the iteration body runs
+      const double elapsed_time =
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - start_time).count() / 1000.0;
+      if (elapsed_time > param_.max_time)
+      {
+        retval = OPT_TIME_LIMIT;
+        if (results_.cnt_viols.empty() || vecMax(results_.cnt_viols) < param_.cnt_tolerance)
+          retval = OPT_CONVERGED;
+        goto cleanup;
+      }
       ++results_.n_sqp_iters;
       if (results_.cost_vals.empty() && results_.cnt_viols.empty())
       {

@@ -385,6 +385,7 @@ struct BasicTrustRegionSQPParameters
   double initial_merit_error_coeff = 10;
   bool inflate_constraints_individually = true;
   double trust_box_size = 1e-1;
+  double max_time = 1.7976931348623157e308;  // optimizers.hpp:117
 };
 
 class BasicTrustRegionSQP

@@ -50,6 +50,7 @@ BasicTrustRegionSQPParameters toSqpParams(const thip_sqp_params& p)
   o.initial_merit_error_coeff = p.initial_merit_error_coeff;
   o.inflate_constraints_individually = p.inflate_constraints_individually != 0;
   o.trust_box_size = p.trust_box_size;
+  o.max_time = p.max_time;
   return o;
 }
 

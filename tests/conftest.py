@@ -37,3 +37,21 @@ def golden():
         return dict(np.load(d / f"{name}.npz"))
 
     return load
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """Write the parity gate's per-check table (tests/parity.py RECORDS) to
+    gpurun_out/parity_table.json (DESIGN.md §5 is regenerated from it)."""
+    try:
+        import parity
+    except ImportError:
+        return
+    if not parity.RECORDS:
+        return
+    import json
+
+    out = REPO / "gpurun_out"
+    out.mkdir(exist_ok=True)
+    strict, total = parity.pooled()
+    (out / "parity_table.json").write_text(json.dumps(
+        {"records": parity.RECORDS, "pooled_strict": strict, "pooled_total": total}, indent=1) + "\n")

@@ -225,10 +225,22 @@ def test_dynamic_cart_pose_lowering():
         host.lower_json(_doc(costs=[term]))
 
 
-@pytest.mark.parametrize("bad", ["0x10", ".5", "1.", "-", "01", "1e", "+1", "Infinity", "NaN", "1e999"])
+@pytest.mark.parametrize("text,value", [("1.", 1.0), ("-", 0.0), ("01", 1.0), ("-.5", -0.5), ("2.5e-1", 0.25),
+                                        ("-0", 0.0), ("18446744073709551616", 18446744073709551616.0)])
+def test_json_number_loose_forms(text, value):
+    """Number tokens the reference's Json::Reader accepts beyond RFC 8259
+    (jsoncpp Reader::readNumber scans each part possibly empty, decodeNumber
+    reads '-' and digits as an integer, decodeDouble the rest)."""
+    doc = _doc(costs=[{"type": "joint_vel", "params": {"targets": [0], "coeffs": ["X"]}}]).replace('"X"', text)
+    d, _, _, _ = host.lower_json(doc)
+    assert d.jv_coeffs[0] == value
+
+
+@pytest.mark.parametrize("bad", ["0x10", ".5", "1e", "+1", "Infinity", "NaN", "1e999", "-e5", "1e+"])
 def test_json_number_grammar(bad):
-    """Numbers outside RFC 8259's grammar are rejected, as jsoncpp rejects them
-    (the parser used to take strtod's hex floats and leading dots)."""
+    """Number tokens the reference's Json::Reader rejects: a hex prefix, a
+    leading '.' or '+', a non-numeric word, an exponent without digits, a
+    double out of range."""
     text = _doc(basic_info={"n_steps": 5, "manip": "right_arm", "dt_lower_lim": "X"}).replace('"X"', bad)
     with pytest.raises(host.HostError) as ei:
         host.lower_json(text)

@@ -1,26 +1,14 @@
 """GPU parity tests (MI355X): the HIP path through the C-ABI against the oracle.
 
 Bar (BASELINE.json north_star): converged trajectories within 1e-5 absolute
-of the CPU path with identical OptStatus and constraint-satisfied flags.
-
-Every problem must have identical status and flag.  A problem whose
-trajectory differs by more than 1e-5 passes only if its per-QP traces show
-the documented mechanism (DESIGN.md "Parity"): the two paths agree until a QP
-whose returned point is an unpolished ADMM iterate on at least one side
-(polish failed or skipped), i.e. a point defined only to OSQP's eps_abs = 1e-4;
-from there rounding-level differences in the ADMM iterates legitimately
-select different SQP paths.  The second accepted mechanism is a trust-region
-decision flip: a QP returns the same polished point on both sides (to 1e-7
-relative) and the accept/shrink ratio computed from it falls on different
-sides of its threshold.  Such problems must still reach the same status,
-flags and a total cost within 2 %, and they may not exceed 15 % of a batch of
-32 or more problems.
-
-A problem whose status or flag differs passes only if the oracle itself is
-unstable on it at rounding level: rerun from the same initial trajectory
-perturbed by 1e-13 (interior waypoints), the oracle reaches the GPU's status
-and flag.  Such a problem's SQP outcome is not a function of its inputs at
-double precision, on either side; it counts against the 15 % as well.
+of the CPU path with identical OptStatus and constraint-satisfied flags.  The
+gate is tests/parity.py: a problem that misses the bar passes only with a
+per-problem proof that the oracle itself does not determine its outcome at
+double precision (its reruns under a second rounding of the same algorithm
+and under 1e-13 / 1e-12 input perturbations reach the GPU's outcome, or
+spread beyond 1e-5).  Batches of 32 or more must meet the bar strictly on
+85 % of their problems, and the pooled strict fraction over all checks is
+bounded in test_zz_pooled_strict_fraction.
 """
 import json
 import subprocess
@@ -29,12 +17,11 @@ import sys
 import numpy as np
 import pytest
 
-from trajopt_amd import abi, problems, robots
+from parity import RECORDS, TOL_X, check_parity, pooled
+from trajopt_amd import abi, problems, robots, sharding
 from trajopt_amd.runtime import BatchTrustRegionSQP, HipError
 
 pytestmark = pytest.mark.gpu
-
-TOL_X = 1e-5
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -54,109 +41,6 @@ def solve_gpu(wl, trace=0):
     tr = s.get_trace() if trace else None
     s.close()
     return x, res, tr
-
-
-def _first_split(tg, to):
-    n = min(len(tg), len(to))
-    for k in range(n):
-        a, o = tg[k], to[k]
-        if a[3] != o[3] or abs(a[8] - o[8]) > 1e-6 * max(1.0, abs(o[8])):
-            return k
-    return n
-
-
-def _perturbed_oracle_runs(wl, oracle_mod, seeds=(1, 2, 3, 4, 5), amp=1e-13):
-    """The oracle rerun from `amp`-perturbed initial trajectories: [(x, results)] per seed."""
-    runs = []
-    for seed in seeds:
-        wp = wl.slice(0, wl.batch)
-        rng = np.random.default_rng(seed)
-        wp.init[:, 1:] += rng.normal(0.0, amp, wp.init[:, 1:].shape)
-        runs.append(oracle_mod.solve(wp, n_threads=16))
-    return runs
-
-
-class _PerturbedOutcomes:
-    """(status, flag) per problem of the oracle rerun from rounding-level
-    perturbed initial trajectories (1e-13, then 1e-12; seeds 1..20), run
-    lazily: on a chaotic problem (a penalty loop that stalls, QPs returned at
-    ADMM accuracy) the reference's own outcome flips under such
-    perturbations in a few seeds out of 20, so a status that differs from the
-    unperturbed oracle's is accepted only if the oracle itself reaches it."""
-
-    SCHEDULE = [(1e-13, s) for s in range(1, 21)] + [(1e-12, s) for s in range(1, 21)]
-
-    def __init__(self, wl, oracle_mod, tol):
-        self.wl, self.oracle_mod, self.tol = wl, oracle_mod, tol
-        self.done = 0
-        self.out = [set() for _ in range(wl.batch)]
-
-    def reaches(self, b, outcome):
-        while outcome not in self.out[b] and self.done < len(self.SCHEDULE):
-            amp, seed = self.SCHEDULE[self.done]
-            self.done += 1
-            for _, rp in _perturbed_oracle_runs(self.wl, self.oracle_mod, (seed,), amp):
-                for bb in range(self.wl.batch):
-                    self.out[bb].add((rp[bb].status, rp[bb].max_cnt_viol < self.tol))
-        return outcome in self.out[b]
-
-
-def check_parity(wl, oracle_mod, x, res, tr=None, min_strict=0.85, label=""):
-    xo, ro = oracle_mod.solve(wl, n_threads=16)
-    tol = wl.desc.sqp.cnt_tolerance
-    B = wl.batch
-    bad, chaotic, perturbed = [], [], None
-    for b in range(B):
-        fg, fo = res[b].max_cnt_viol < tol, ro[b].max_cnt_viol < tol
-        if res[b].status != ro[b].status or fg != fo:
-            if perturbed is None:
-                perturbed = _PerturbedOutcomes(wl, oracle_mod, tol)
-            assert perturbed.reaches(b, (res[b].status, fg)), (
-                f"{label} problem {b}: status {res[b].status} vs {ro[b].status}, constraint flag {fg} vs {fo}; "
-                f"perturbed oracle runs reach {sorted(perturbed.out[b])}")
-            chaotic.append(b)
-            continue
-        if np.abs(x[b] - xo[b]).max() > TOL_X:
-            bad.append(b)
-    strict = 1.0 - (len(bad) + len(chaotic)) / B
-    if B >= 32:  # the fraction bound is only meaningful on a real batch
-        assert strict >= min_strict, f"{label}: only {strict:.2%} of problems within {TOL_X}: {bad} {chaotic}"
-    if not bad:
-        return
-    if tr is None:
-        _, _, tr = solve_gpu(wl, trace=2048)
-    runs = None
-    for b in bad:
-        _, _, to = oracle_mod.solve_trace(wl, b, cap=2048)
-        tg = tr[b]
-        k = _first_split(tg, to)
-        unpolished = [j for j in range(0, min(k + 1, len(tg), len(to)))
-                      if (tg[j][3] == 1 and tg[j][4] != 1) or (to[j][3] == 1 and to[j][4] != 1)
-                      or tg[j][3] != 1 or to[j][3] != 1]
-        # second mechanism: a trust-region decision flip.  QP k-1 returned the
-        # same polished point on both sides (sum|x*| within 1e-7 relative) and
-        # the next QP starts from a different trust box: the accept/shrink
-        # ratio (optimizers.cpp:865-880), a quotient of small differences of
-        # merit values, fell on different sides of its threshold.
-        flip = (0 < k < min(len(tg), len(to)) and abs(tg[k - 1][8] - to[k - 1][8]) <= 1e-7 * max(1.0, abs(to[k - 1][8]))
-                and tg[k][9] != to[k][9])
-        assert unpolished or flip, (f"{label} problem {b}: trajectories differ by "
-                                    f"{np.abs(x[b] - xo[b]).max():.2e} but every QP up to the split ({k}) was "
-                                    f"polished on both sides and no trust-region decision flipped")
-        cg, co = res[b].total_cost, ro[b].total_cost
-        if abs(cg - co) <= 0.02 * max(1.0, abs(co)):
-            continue
-        # the oracle itself is not reproducible on this problem: its own reruns from
-        # 1e-13-perturbed inputs disagree beyond the 1e-5 bar, and the GPU's cost lies
-        # within the range those reruns reach (+-2 %)
-        if runs is None:
-            runs = _perturbed_oracle_runs(wl, oracle_mod)
-        spread = max(np.abs(xr[b] - xo[b]).max() for xr, _ in runs)
-        costs = [co] + [rr[b].total_cost for _, rr in runs]
-        lo, hi = min(costs), max(costs)
-        assert spread > TOL_X and lo - 0.02 * max(1.0, abs(lo)) <= cg <= hi + 0.02 * max(1.0, abs(hi)), (
-            f"{label} problem {b}: cost {cg} vs {co}; perturbed oracle reruns spread {spread:.1e}, "
-            f"costs [{lo}, {hi}]")
 
 
 # ------------------------------------------------------------------ kinematics
@@ -295,8 +179,8 @@ def test_sqp_golden_fixtures(golden, oracle_mod):
 @pytest.mark.parametrize("cfg,B", [("A", 64), ("B", 32)])
 def test_sqp_parity(oracle_mod, cfg, B):
     wl = problems.make_workload(cfg, B)
-    x, res, tr = solve_gpu(wl, trace=2048)
-    check_parity(wl, oracle_mod, x, res, tr, label=cfg)
+    x, res, _ = solve_gpu(wl)
+    check_parity(wl, oracle_mod, x, res, label=cfg)
 
 
 # ------------------------------------------------------------------ collision (config C)
@@ -366,20 +250,26 @@ def test_sqp_parity_dual_arm_E(oracle_mod):
     both tool frames tracked, LVS_CONTINUOUS collision -- the wide-block
     (D > 8) solve path with the chain matrices in HBM."""
     wl = problems.make_workload("E", 4)
-    x, res, tr = solve_gpu(wl, trace=4096)
+    x, res, _ = solve_gpu(wl)
     assert all(r.flags == 0 for r in res)
-    check_parity(wl, oracle_mod, x, res, tr, label="E")
+    xo, ro = oracle_mod.solve(wl, n_threads=16)
+    # strict on these four: same status, x within the bar, the same SQP path
+    for b in range(wl.batch):
+        assert res[b].status == ro[b].status, b
+        assert np.abs(x[b] - xo[b]).max() <= TOL_X, (b, np.abs(x[b] - xo[b]).max())
+        assert (res[b].n_sqp_iters, res[b].n_qp_solves) == (ro[b].n_sqp_iters, ro[b].n_qp_solves), b
+    check_parity(wl, oracle_mod, x, res, label="E", oracle=(xo, ro))
 
 
 def test_sqp_parity_collision_continuous(oracle_mod):
     wl = _continuous(problems.make_workload("C", 32, first_problem=200))
-    x, res, tr = solve_gpu(wl, trace=2048)
+    x, res, _ = solve_gpu(wl)
     assert all(r.flags == 0 for r in res)
-    check_parity(wl, oracle_mod, x, res, tr, label="C-continuous")
+    check_parity(wl, oracle_mod, x, res, label="C-continuous")
     wl = _continuous(problems.make_workload("C", 8, first_problem=300))
     wl.desc.coll_is_cnt = 1
-    x, res, tr = solve_gpu(wl, trace=2048)
-    check_parity(wl, oracle_mod, x, res, tr, label="C-continuous-cnt")
+    x, res, _ = solve_gpu(wl)
+    check_parity(wl, oracle_mod, x, res, label="C-continuous-cnt")
 
 
 def _single(wl):
@@ -409,15 +299,15 @@ def test_collision_rows_parity_discrete(oracle_mod):
 
 def test_sqp_parity_collision_discrete(oracle_mod):
     wl = _single(problems.make_workload("C", 32, first_problem=400))
-    x, res, tr = solve_gpu(wl, trace=2048)
+    x, res, _ = solve_gpu(wl)
     assert all(r.flags == 0 for r in res)
     assert all(r.n_costs == 1 + 29 + (wl.n_steps - 1) for r in res)
-    check_parity(wl, oracle_mod, x, res, tr, label="C-discrete")
+    check_parity(wl, oracle_mod, x, res, label="C-discrete")
     wl = _single(problems.make_workload("C", 8, first_problem=500))
     wl.desc.coll_is_cnt = 1
-    x, res, tr = solve_gpu(wl, trace=2048)
+    x, res, _ = solve_gpu(wl)
     assert all(r.n_cnts == wl.n_steps - 1 for r in res)
-    check_parity(wl, oracle_mod, x, res, tr, label="C-discrete-cnt")
+    check_parity(wl, oracle_mod, x, res, label="C-discrete-cnt")
 
 
 def test_collision_rows_golden_discrete(golden):
@@ -457,9 +347,9 @@ def test_sqp_parity_collision(oracle_mod, golden):
     np.testing.assert_array_equal([r.status for r in res], g["status"])
     assert np.abs(x - g["x"]).max() <= TOL_X
     wl = problems.make_workload("C", 32)
-    x, res, tr = solve_gpu(wl, trace=2048)
+    x, res, _ = solve_gpu(wl)
     assert all(r.flags == 0 for r in res)
-    check_parity(wl, oracle_mod, x, res, tr, label="C")
+    check_parity(wl, oracle_mod, x, res, label="C")
 
 
 def test_sqp_parity_collision_constraint(oracle_mod):
@@ -468,10 +358,10 @@ def test_sqp_parity_collision_constraint(oracle_mod):
     merit coefficients, violations counted in the penalty loop."""
     wl = problems.make_workload("C", 32, first_problem=64)
     wl.desc.coll_is_cnt = 1
-    x, res, tr = solve_gpu(wl, trace=2048)
+    x, res, _ = solve_gpu(wl)
     assert all(r.flags == 0 for r in res)
     assert all(r.n_cnts == wl.n_steps - 1 for r in res)
-    check_parity(wl, oracle_mod, x, res, tr, label="C-cnt")
+    check_parity(wl, oracle_mod, x, res, label="C-cnt")
 
 
 def _variant(name):
@@ -675,11 +565,11 @@ VARIANTS = ["jointvel_only", "short_horizon", "two_fixed_steps", "position_only_
 @pytest.mark.parametrize("name", VARIANTS)
 def test_sqp_parity_variants(oracle_mod, name):
     wl = _variant(name)
-    x, res, tr = solve_gpu(wl, trace=2048)
+    x, res, _ = solve_gpu(wl)
     # without polishing every QP returns an ADMM iterate: the paths agree
     # only to the ADMM accuracy, so the trajectory bar does not apply
     min_strict = 0.0 if name in ("no_polish", "admm_iteration_cap") else 0.85
-    check_parity(wl, oracle_mod, x, res, tr, min_strict=min_strict, label=name)
+    check_parity(wl, oracle_mod, x, res, min_strict=min_strict, label=name)
 
 
 def test_sqp_iteration_cap_status():
@@ -692,70 +582,92 @@ def test_sqp_iteration_cap_status():
     assert [r.status for r in res] == [0] * 4 and all(r.n_sqp_iters == 3 for r in res)
 
 
+def test_max_time_zero_ends_before_the_first_iteration(oracle_mod):
+    """BasicTrustRegionSQPParameters::max_time (optimizers.cpp:739-753): with 0 the
+    check at the top of the first SQP iteration fires before any evaluation, so
+    the constraint violations are still empty and the status is OPT_CONVERGED;
+    x is the closest feasible point of the start (optimizers.cpp:725)."""
+    wl = problems.make_workload("A", 8)
+    wl.desc.sqp.max_time = 0.0
+    x, res, _ = solve_gpu(wl)
+    xo, ro = oracle_mod.solve(wl, n_threads=8)
+    for b in range(wl.batch):
+        assert res[b].status == ro[b].status == 0
+        assert res[b].n_sqp_iters == ro[b].n_sqp_iters == 0 and res[b].n_qp_solves == 0
+        assert res[b].total_cost == ro[b].total_cost == 0.0
+    np.testing.assert_allclose(x, xo, rtol=0, atol=1e-15)
+
+
+def test_max_time_limits_the_run():
+    """A time limit shorter than the solves: problems end with OPT_TIME_LIMIT
+    (constraints violated) or OPT_CONVERGED (none violated), never after more
+    SQP iterations than the unlimited run."""
+    wl = problems.make_workload("A", 64)
+    _, free, _ = solve_gpu(wl)
+    wl.desc.sqp.max_time = 2e-4
+    _, res, _ = solve_gpu(wl)
+    assert any(r.status == 3 for r in res)
+    assert all(r.status in (0, 3) or r.n_sqp_iters == f.n_sqp_iters for r, f in zip(res, free))
+    assert all(r.n_sqp_iters <= f.n_sqp_iters for r, f in zip(res, free))
+    for r in res:
+        if r.status == 3:
+            assert r.max_cnt_viol >= wl.desc.sqp.cnt_tolerance
+
+
 # ------------------------------------------------------------------ full size
-def test_full_batch_properties_and_sampled_parity(oracle_mod):
-    """BASELINE config at full size (1024 problems): size-independent
-    properties on every problem, oracle parity on a sample of 32."""
-    wl = problems.make_workload("B", 1024)
-    s = BatchTrustRegionSQP(wl)
+def _full_size_properties(wl, s):
+    """Bitwise-identical reruns, joint limits, the fixed timestep, statuses, counters."""
     x1, r1 = s.optimize()
     x2, r2 = s.optimize()
-    s.close()
-    # determinism: bitwise identical reruns
     np.testing.assert_array_equal(x1, x2)
     assert [r.n_admm_iters for r in r1] == [r.n_admm_iters for r in r2]
+    assert [r.n_contact_rows for r in r1] == [r.n_contact_rows for r in r2]
     lo, hi, _ = robots.chain_limits(wl.desc.chain)
     # trust-box bounds are clamped to the joint limits; a QP point is feasible
     # to OSQP's tolerance (eps_abs = 1e-4 when it is an unpolished iterate)
     viol = max(float(np.max(lo - x1)), float(np.max(x1 - hi)), 0.0)
     assert viol <= 1e-4, viol
     np.testing.assert_allclose(x1[:, 0], wl.init[:, 0], rtol=0, atol=1e-6)  # fixed timestep rows
-    assert all(r.status in (0, 1, 2) for r in r1)
-    assert all(r.n_sqp_iters >= 1 and r.n_qp_solves >= r.n_sqp_iters for r in r1)
-    sample = list(range(16)) + list(range(1008, 1024))
-    sub = problems.make_workload("B", 16)
-    sub2 = problems.make_workload("B", 16, first_problem=1008)
-    xo1, ro1 = oracle_mod.solve(sub, n_threads=16)
-    xo2, ro2 = oracle_mod.solve(sub2, n_threads=16)
-    xo = np.concatenate([xo1, xo2])
-    ro = ro1 + ro2
-    within = 0
-    for k, b in enumerate(sample):
-        assert r1[b].status == ro[k].status
-        within += np.abs(x1[b] - xo[k]).max() <= TOL_X
-    assert within >= 0.85 * len(sample)
-
-
-def test_full_batch_collision_properties_and_sampled_parity(oracle_mod):
-    """The bench workload (config C, 1024 problems, LVS-discrete collision):
-    bitwise reruns, joint limits, the fixed timestep, no contact-capacity overflow,
-    consistent collision counters on every problem; oracle parity on a sample of 32."""
-    wl = problems.make_workload("C", 1024)
-    s = BatchTrustRegionSQP(wl)
-    x1, r1 = s.optimize()
-    x2, r2 = s.optimize()
-    s.close()
-    np.testing.assert_array_equal(x1, x2)
-    assert [r.n_admm_iters for r in r1] == [r.n_admm_iters for r in r2]
-    assert [r.n_contact_rows for r in r1] == [r.n_contact_rows for r in r2]
-    lo, hi, _ = robots.chain_limits(wl.desc.chain)
-    viol = max(float(np.max(lo - x1)), float(np.max(x1 - hi)), 0.0)
-    assert viol <= 1e-4, viol
-    np.testing.assert_allclose(x1[:, 0], wl.init[:, 0], rtol=0, atol=1e-6)
     assert all(r.flags == 0 for r in r1)
     assert all(r.status in (0, 1, 2) for r in r1)
-    assert all(r.n_substates >= 2 * (wl.n_steps - 1) * r.n_sqp_iters for r in r1)
-    assert sum(r.n_contact_rows for r in r1) > 0
-    sample = list(range(16)) + list(range(1008, 1024))
-    xo1, ro1 = oracle_mod.solve(problems.make_workload("C", 16), n_threads=16)
-    xo2, ro2 = oracle_mod.solve(problems.make_workload("C", 16, first_problem=1008), n_threads=16)
-    xo = np.concatenate([xo1, xo2])
-    ro = ro1 + ro2
-    within = 0
-    for k, b in enumerate(sample):
-        assert r1[b].status == ro[k].status
-        within += np.abs(x1[b] - xo[k]).max() <= TOL_X
-    assert within >= 0.85 * len(sample)
+    assert all(r.n_sqp_iters >= 1 and r.n_qp_solves >= r.n_sqp_iters for r in r1)
+    if wl.desc.coll_enabled:
+        assert sum(r.n_contact_rows for r in r1) > 0
+        if wl.desc.coll_continuous != 2:
+            assert all(r.n_substates >= 2 * (wl.n_steps - 1) * r.n_sqp_iters for r in r1)
+    return x1, r1
+
+
+@pytest.mark.timeout(1500)
+@pytest.mark.parametrize("cfg,rank", [("B", 0), ("C", 0), ("C", 7)])
+def test_full_batch_every_problem(oracle_mod, cfg, rank):
+    """1024 problems per GPU, every problem against the oracle under the strict
+    gate: config B, the bench workload (config C), and rank 7's shard of config D
+    (configs[3]: 8192 problems over 8 GPUs, seeds 7168-8191, the per-GPU
+    workload of the last rank)."""
+    wl = sharding.rank_workload(cfg, 1024, rank)
+    s = BatchTrustRegionSQP(wl)
+    x, res = _full_size_properties(wl, s)
+    s.close()
+    label = f"{cfg}-1024" if rank == 0 else f"D-rank{rank}-1024"
+    check_parity(wl, oracle_mod, x, res, label=label, min_strict=0.9)
+
+
+@pytest.mark.timeout(1500)
+def test_full_batch_E_512(oracle_mod):
+    """Config E at one GPU's share of configs[4] (4096 problems over 8 GPUs):
+    512 problems of the 14-DoF dual arm, 50 waypoints, LVS_CONTINUOUS.
+    Properties on every problem, the strict gate on 32 problems spread over the
+    batch."""
+    wl = problems.make_workload("E", 512)
+    s = BatchTrustRegionSQP(wl)
+    x, res = _full_size_properties(wl, s)
+    s.close()
+    from parity import subset
+
+    idx = np.arange(0, 512, 16)
+    sub = subset(wl, idx)
+    check_parity(sub, oracle_mod, x[idx], [res[i] for i in idx], label="E-512-sample32", min_strict=0.9)
 
 
 def test_devices_stream_interop():
@@ -790,47 +702,48 @@ def test_bench_json_line():
     assert line["value"] > 0 and line["n_gpus"] == 1 and line["dtype"] == "f64"
     assert line["config"]["batches_in_flight"] == 3 and line["config"]["batch_latency_ms"] > 0
     rf = line["roofline"]
-    assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and 0 < rf["frac"] == pytest.approx(rf["achieved"] / 8000.0)
+    assert rf["bound"] == "latency" and rf["peak"] == 8000.0 and 0 < rf["frac"] == pytest.approx(rf["achieved"] / 8000.0)
     cb = line["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
+    assert cb["host_nproc"] >= 1 and cb["single_problem_latency_s"] > 0
 
 
 def test_joint_pos_reference_unit(oracle_mod):
     """joint_costs_unit.cpp:63-150 (equality_jointPos) on the HIP path: the
     reference's EXPECTs plus parity with the oracle."""
     wl = problems.make_reference_unit("joint_pos_eq", 4)
-    x, res, tr = solve_gpu(wl, trace=512)
+    x, res, _ = solve_gpu(wl)
     for b in range(wl.batch):
         assert res[b].status == 0
         assert np.abs(x[b, 0]).max() < 1e-4
         assert np.abs(x[b, 1:] + 0.1).max() < 0.01
-    check_parity(wl, oracle_mod, x, res, tr, label="joint_pos_eq")
+    check_parity(wl, oracle_mod, x, res, label="joint_pos_eq")
 
 
 def test_joint_pos_ineq_reference_unit(oracle_mod):
     """joint_costs_unit.cpp:152-262 (inequality_jointPos): hinge rows of
     JointPosIneqConstraint / JointPosIneqCost on the HIP path."""
     wl = problems.make_reference_unit("joint_pos_ineq", 4)
-    x, res, tr = solve_gpu(wl, trace=512)
+    x, res, _ = solve_gpu(wl)
     for b in range(wl.batch):
         assert res[b].status == 0
         for i in list(range(0, 5)) + list(range(6, 10)):
             assert (x[b, i] < 0.2 + 1e-4).all() and (x[b, i] > -0.1 - 1e-4).all()
-    check_parity(wl, oracle_mod, x, res, tr, label="joint_pos_ineq")
+    check_parity(wl, oracle_mod, x, res, label="joint_pos_ineq")
 
 
 def test_joint_vel_ineq_reference_unit(oracle_mod):
     """joint_costs_unit.cpp:354-463 (inequality_jointVel): a JointVelIneqConstraint
     and two JointVelIneqCost terms (three JointVel terms, static hinge rows)."""
     wl = problems.make_reference_unit("joint_vel_ineq", 4)
-    x, res, tr = solve_gpu(wl, trace=512)
+    x, res, _ = solve_gpu(wl)
     N = wl.n_steps
     for b in range(wl.batch):
         assert res[b].n_cnts == 1 and res[b].n_costs == 2
         v = np.diff(x[b], axis=0)
         for i in list(range(0, N // 2)) + list(range(N // 2 + 1, N - 1)):
             assert (v[i] < 0.2 + 1e-4).all() and (v[i] > -0.1 - 1e-4).all()
-    check_parity(wl, oracle_mod, x, res, tr, label="joint_vel_ineq")
+    check_parity(wl, oracle_mod, x, res, label="joint_vel_ineq")
 
 
 def test_joint_pos_per_problem_targets():
@@ -957,18 +870,33 @@ def test_contact_capacity_overflow_fails_loudly():
     assert all(r.status == 4 for r in over)
 
 
-@pytest.mark.parametrize("cfg,B", [("B", 32), ("C", 32)])
-def test_sqp_parity_generic_step(oracle_mod, cfg, B, monkeypatch):
+@pytest.mark.parametrize("cfg,B,path", [("B", 32, abi.DEBUG_NO_SEGMENT), ("C", 32, abi.DEBUG_NO_SEGMENT),
+                                         ("B", 32, abi.DEBUG_FORCE_WIDE), ("C", 32, abi.DEBUG_FORCE_WIDE)])
+def test_sqp_parity_forced_paths(oracle_mod, cfg, B, path, hip):
     """The generic ADMM step (admm_step + reduced_solve: loads-first loops, masked
-    products, per-row-kind updates) on problems the register-resident segment
-    would otherwise run (THIP_NO_SEGMENT=1, read by thip_create): same parity bar
-    against the oracle, and the same outcomes as the segment path."""
+    products, per-row-kind updates) and the wide-block solve (block_chain_wide,
+    twisted_middle_wide, chain matrices in HBM: config E's path) on problems the
+    register-resident segment would otherwise run (thip_debug_set_path): the
+    same parity gate against the oracle, and the same outcomes as the segment."""
     wl = problems.make_workload(cfg, B)
     x_seg, res_seg, _ = solve_gpu(wl)
-    monkeypatch.setenv("THIP_NO_SEGMENT", "1")
-    x, res, tr = solve_gpu(wl, trace=2048)
-    monkeypatch.delenv("THIP_NO_SEGMENT")
-    check_parity(wl, oracle_mod, x, res, tr, label=f"{cfg}-generic")
+    assert hip.thip_debug_set_path(path) == 0
+    try:
+        x, res, _ = solve_gpu(wl)
+    finally:
+        hip.thip_debug_set_path(0)
+    name = {abi.DEBUG_NO_SEGMENT: "generic", abi.DEBUG_FORCE_WIDE: "wide"}[path]
+    check_parity(wl, oracle_mod, x, res, label=f"{cfg}-{name}")
     same = sum(int(a.status == b.status and np.abs(xa - xb).max() <= TOL_X)
                for a, b, xa, xb in zip(res, res_seg, x, x_seg))
-    assert same >= 0.85 * B, f"{cfg}: generic step and segment agree on {same} of {B} problems"
+    assert same >= 0.85 * B, f"{cfg}: {name} path and segment agree on {same} of {B} problems"
+
+
+def test_zz_pooled_strict_fraction():
+    """Pooled over every parity check of the session that carries a fraction
+    bound: at least 93 % of all problems meet the bar strictly (the rest carry
+    a per-problem proof of oracle instability)."""
+    strict, total = pooled()
+    if total < 200:
+        pytest.skip(f"only {total} problems checked in this session")
+    assert strict >= 0.93 * total, f"pooled strict fraction {strict}/{total}"

@@ -126,6 +126,8 @@ enum ShKind : int
 
 struct Layout
 {
+  // sqp.max_time in wall_clock64() ticks (LLONG_MAX: no limit)
+  long long max_ticks;
   int N, D, nx;
   int n_links;
   int n_fixed, n_fixed_rows;

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <climits>
 #include <type_traits>
 
 #include "collision_device.hpp"
@@ -76,6 +77,7 @@ struct Ctl
   double prim_res, dual_res;
   int flag;
   int can_check;
+  int time_up;  // the max_time check of this SQP iteration fired
   // diagnostics
   double* trace;
   int trace_cap, trace_n;
@@ -4754,11 +4756,35 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
   bool have_prev_setup = false;
   bool first_eval = true;
   int retval = THIP_OPT_INVALID;
+  // cost / violation values before the first evaluation: an empty OptResults
+  // (a time limit can end the run before it, optimizers.cpp:739-753)
+  FOR(i, L.n_costs) COST[i] = 0.0;
+  FOR(i, L.n_cnts) VIOL[i] = 0.0;
+  const long long t_start = wall_clock64();
   for (int mi = 0; mi < P.max_merit_coeff_increases; ++mi)
   {
     bool goto_penalty = false, goto_cleanup = false;
     for (int iter = 1;; ++iter)
     {
+      // time limit (optimizers.cpp:739-753), before the iteration body: the
+      // problem's own clock since sqp_optimize began
+      if (L.max_ticks != LLONG_MAX)
+      {
+        if (c.tid == 0)
+          c.s->time_up = (wall_clock64() - t_start) > L.max_ticks ? 1 : 0;
+        BSYNC();
+        if (c.s->time_up)
+        {
+          retval = THIP_OPT_TIME_LIMIT;
+          double vm = -INFINITY;
+          for (int i = 0; i < L.n_cnts; ++i)
+            vm = fmax(vm, VIOL[i]);
+          if (first_eval || L.n_cnts == 0 || vm < P.cnt_tolerance)
+            retval = THIP_OPT_CONVERGED;
+          goto_cleanup = true;
+          break;
+        }
+      }
       if (c.tid == 0)
         c.s->n_sqp++;
       if (first_eval)

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -95,6 +97,7 @@ void thip_default_sqp_params(thip_sqp_params* p)
   p->initial_merit_error_coeff = 10;
   p->inflate_constraints_individually = 1;
   p->trust_box_size = 1e-1;
+  p->max_time = DBL_MAX;  // optimizers.hpp:117
 }
 
 void thip_default_osqp_settings(thip_osqp_settings* s)
@@ -118,8 +121,23 @@ void thip_default_osqp_settings(thip_osqp_settings* s)
   s->polish_refine_iter = 3;
 }
 
+// thip_debug_set_path: diagnostic solve-path overrides for contexts created afterwards
+static int g_debug_path = 0;
+
+int thip_debug_set_path(int flags)
+{
+  if (flags & ~(THIP_DEBUG_NO_SEGMENT | THIP_DEBUG_FORCE_WIDE))
+    return THIP_E_INVALID;
+  g_debug_path = flags;
+  return THIP_OK;
+}
+
 static int validate(const thip_problem_desc* d, std::string& why)
 {
+  if (d->abi_version != THIP_ABI_VERSION)
+    return why = "descriptor abi_version " + std::to_string(d->abi_version) + " != THIP_ABI_VERSION " +
+                 std::to_string(THIP_ABI_VERSION) + " (caller built against another trajopt_hip.h)",
+           THIP_E_INVALID;
   const thip_chain& ch = d->chain;
   if (ch.n_dof <= 0 || ch.n_dof > THIP_MAX_DOF)
     return why = "n_dof out of range", THIP_E_INVALID;
@@ -134,7 +152,7 @@ static int validate(const thip_problem_desc* d, std::string& why)
       return why = "bad joint type", THIP_E_INVALID;
     if (ty != THIP_JOINT_FIXED && (ch.joint_dof[k] < 0 || ch.joint_dof[k] >= ch.n_dof))
       return why = "bad joint dof index", THIP_E_INVALID;
-    if (ch.parent[k] < 0 || ch.parent[k] >= k)
+    if (ch.is_tree && (ch.parent[k] < 0 || ch.parent[k] >= k))
       return why = "bad parent link (links must be in tree order, 0 <= parent[k] < k)", THIP_E_INVALID;
   }
   if (d->n_fixed < 0 || d->n_fixed > THIP_MAX_STEPS)
@@ -223,6 +241,12 @@ static int validate(const thip_problem_desc* d, std::string& why)
                  THIP_E_INVALID;
   if (d->coll_enabled && (d->coll_max_contacts < 0 || d->coll_max_contacts > THIP_MAX_CONTACTS))
     return why = "collision: coll_max_contacts out of range", THIP_E_INVALID;
+  if (!(d->sqp.max_time >= 0))
+    return why = "sqp.max_time must be >= 0 (DBL_MAX: no limit)", THIP_E_INVALID;
+  if (!(d->sqp.trust_shrink_ratio > 0 && d->sqp.trust_shrink_ratio < 1) || !(d->sqp.min_trust_box_size > 0) ||
+      !(d->sqp.trust_box_size > 0))
+    return why = "sqp: need 0 < trust_shrink_ratio < 1, min_trust_box_size > 0 and trust_box_size > 0",
+           THIP_E_INVALID;
   if (d->osqp.check_termination < 0 || d->osqp.max_iter < 1 || d->osqp.scaling < 0)
     return why = "bad OSQP settings", THIP_E_INVALID;
   return THIP_OK;
@@ -245,6 +269,9 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   ctx->device = device;
   ctx->batch = batch;
   ctx->desc = *desc;
+  if (!ctx->desc.chain.is_tree)  // serial chain: parent[] is not read from the caller
+    for (int k = 0; k < THIP_MAX_LINKS; ++k)
+      ctx->desc.chain.parent[k] = k > 0 ? k - 1 : 0;
   const thip_problem_desc& d = ctx->desc;
   Layout& L = ctx->L;
   L.N = d.n_steps;
@@ -521,9 +548,8 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   sizes[A_RE] = std::max(L.n_rows, 1);
   sizes[A_LINV] = sizes[A_KB] = NDD;
   L.wide = (L.D > 8) ? 1 : 0;
-  if (const char* e = std::getenv("THIP_FORCE_WIDE"))  // diagnostic: the wide-block solve for any D
-    if (e[0] == '1')
-      L.wide = 1;
+  if (g_debug_path & THIP_DEBUG_FORCE_WIDE)  // diagnostic: the wide-block solve for any D
+    L.wide = 1;
   sizes[A_CHM] = L.wide ? 2 * NDD : 1;
   sizes[A_PB] = std::max(nc + m, nab * D);
   sizes[A_PS] = sizes[A_PR] = nc + m;
@@ -606,9 +632,8 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     // n_abs <= 256; larger problems run the generic admm_step()
     // (collision problems: hinge rows are loop-owned inside the segment)
     L.seg_ok = (max_step_rows <= kMaxStepRows && !L.wide && L.N * 8 <= kBlock && L.n_abs <= kBlock) ? 1 : 0;
-    if (const char* e = std::getenv("THIP_NO_SEGMENT"))
-      if (e[0] == '1')
-        L.seg_ok = 0;
+    if (g_debug_path & THIP_DEBUG_NO_SEGMENT)  // diagnostic: the generic ADMM step
+      L.seg_ok = 0;
     L.seg_slots = 1;
     L.tw_mid = L.N / 2;
     if (L.loff[A_LINV] < 0 || L.loff[A_CV] < 0 || L.loff[A_YV] < 0)
@@ -640,6 +665,14 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess)
     return fail(std::string("hipSetDevice: ") + hipGetErrorString(e));
+  {
+    // BasicTrustRegionSQPParameters::max_time (seconds) in wall_clock64() ticks
+    int rate_khz = 0;
+    if ((e = hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device)) != hipSuccess || rate_khz <= 0)
+      return fail("hipDeviceGetAttribute(WallClockRate) failed");
+    const double ticks = d.sqp.max_time * 1e3 * static_cast<double>(rate_khz);
+    L.max_ticks = (ticks >= 9.0e18) ? LLONG_MAX : (ticks <= 0 ? 0LL : static_cast<long long>(ticks));
+  }
   if (ctx->lds_lin_bytes > 60 * 1024)
     return fail("problem too large for the LDS-resident block solve");
   // tables

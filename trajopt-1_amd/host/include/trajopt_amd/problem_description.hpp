@@ -61,8 +61,8 @@ struct OptResults
   int flags{ 0 };
 };
 
-// optimizers.hpp:92-135 (numeric members; max_time is accepted and ignored:
-// the device loop has no wall clock)
+// optimizers.hpp:92-135 (numeric members; max_time is checked on the device at
+// the top of every SQP iteration against the problem's own clock)
 struct BasicTrustRegionSQPParameters
 {
   double improve_ratio_threshold = 0.25;

@@ -224,6 +224,11 @@ sco::OptStatus BasicTrustRegionSQP::optimize()
   q.initial_merit_error_coeff = param_.initial_merit_error_coeff;
   q.inflate_constraints_individually = param_.inflate_constraints_individually ? 1 : 0;
   q.trust_box_size = param_.trust_box_size;
+  q.max_time = param_.max_time;
+  if (!(param_.trust_shrink_ratio > 0 && param_.trust_shrink_ratio < 1) || !(param_.min_trust_box_size > 0) ||
+      !(param_.trust_box_size > 0) || !(param_.trust_expand_ratio > 0))
+    throw std::runtime_error("BasicTrustRegionSQP: need 0 < trust_shrink_ratio < 1, trust_expand_ratio > 0, "
+                             "min_trust_box_size > 0 and trust_box_size > 0");
   if (!x0_.empty())
   {
     const int N = p->GetNumSteps(), D = p->GetNumDOF();
@@ -243,7 +248,8 @@ sco::OptStatus BasicTrustRegionSQP::optimize()
     const double span = std::log(param_.trust_box_size / param_.min_trust_box_size) + grow;
     const double tries = 2.0 + std::max(0.0, span / std::log(1.0 / param_.trust_shrink_ratio));
     const double bound = (param_.max_merit_coeff_increases + 1.0) * param_.max_iter * tries;
-    batch.enableTrace(static_cast<int>(std::min(std::max(bound, 64.0), 1.0e6)));
+    // (a non-finite bound -- absurd parameters -- takes the fixed cap)
+    batch.enableTrace(static_cast<int>(std::isfinite(bound) ? std::min(std::max(bound, 64.0), 1.0e6) : 1.0e6));
   }
   results_ = batch.optimize()[0];
   if (param_.log_results)

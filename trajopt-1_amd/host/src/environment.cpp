@@ -71,6 +71,7 @@ KinematicGroup makeGroup(const std::string& name, const std::vector<bool>& arms_
   c.base_pose[11] = 0.051 + 0.739675;
   c.joint_dof[0] = -1;
   c.parent[0] = 0;
+  c.is_tree = arms_left.size() > 1 ? 1 : 0;
   g.link_names.push_back("torso_lift_link");
   int dof = 0, k = 1;
   for (const bool left : arms_left)

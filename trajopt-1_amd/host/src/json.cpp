@@ -116,10 +116,14 @@ private:
     fail(std::string("unexpected character '") + c + "'");
   }
 
-  // JSON number grammar (RFC 8259 6): -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?
-  // scanned first (jsoncpp rejects hex floats, "inf", ".5", "1."), then
-  // converted by std::from_chars, which ignores the C locale (strtod would
-  // read "0.5" as 0 under a comma-decimal LC_NUMERIC)
+  // Number tokens as the reference's parser reads them (Json::Reader,
+  // trajopt/test/trajopt_test_utils.hpp:14; jsoncpp Reader::readNumber /
+  // decodeNumber / decodeDouble): an optional '-', digits, an optional '.' and
+  // digits, an optional exponent, each part possibly empty.  A token of only
+  // '-' and digits is an integer ("01" -> 1, "-" -> 0); any other token must
+  // convert as a whole to a finite double ("1." -> 1, "-.5" -> -0.5; "1e",
+  // "1e999" fail).  The conversion is std::from_chars, which ignores the C
+  // locale (strtod would read "0.5" as 0 under a comma-decimal LC_NUMERIC).
   Value number()
   {
     const std::size_t start = pos_;
@@ -127,38 +131,52 @@ private:
     std::size_t p = pos_;
     if (p < s_.size() && s_[p] == '-')
       ++p;
-    if (!digit(p))
-      fail("invalid number");
-    if (s_[p] == '0')
+    const std::size_t int0 = p;
+    while (digit(p))
       ++p;
-    else
-      while (digit(p))
-        ++p;
+    bool integral = true;
     if (p < s_.size() && s_[p] == '.')
     {
+      integral = false;
       ++p;
-      if (!digit(p))
-        fail("invalid number");
       while (digit(p))
         ++p;
     }
     if (p < s_.size() && (s_[p] == 'e' || s_[p] == 'E'))
     {
+      integral = false;
       ++p;
       if (p < s_.size() && (s_[p] == '+' || s_[p] == '-'))
         ++p;
-      if (!digit(p))
-        fail("invalid number");
       while (digit(p))
         ++p;
     }
-    double d = 0.0;
     const char* first = s_.data() + start;
-    const auto r = std::from_chars(first, s_.data() + p, d);
-    if (r.ec == std::errc::result_out_of_range || !std::isfinite(d))
-      fail("number out of range");
-    if (r.ec != std::errc() || r.ptr != s_.data() + p)
-      fail("invalid number");
+    const char* last = s_.data() + p;
+    double d = 0.0;
+    if (integral)
+    {
+      unsigned long long u = 0;
+      const auto r = std::from_chars(s_.data() + int0, last, u);
+      if (int0 == p)
+        u = 0;  // "-": jsoncpp decodes an empty digit run as 0
+      else if (r.ec == std::errc::result_out_of_range)
+        integral = false;  // beyond 64 bits: jsoncpp falls back to decodeDouble
+      if (integral)
+      {
+        d = static_cast<double>(u);
+        if (s_[start] == '-')
+          d = -d;
+      }
+    }
+    if (!integral)
+    {
+      const auto r = std::from_chars(first, last, d);
+      if (r.ec == std::errc::result_out_of_range || !std::isfinite(d))
+        fail("number out of range");
+      if (r.ec != std::errc() || r.ptr != last)
+        fail("invalid number");
+    }
     pos_ = p;
     return Value(d);
   }

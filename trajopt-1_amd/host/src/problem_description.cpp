@@ -198,7 +198,7 @@ int KinematicGroup::linkIndex(const std::string& link) const
 bool KinematicGroup::isActiveLinkId(const std::string& link) const
 {
   // moved by a joint on its path from the root
-  for (int i = linkIndex(link); i > 0; i = chain.parent[i])
+  for (int i = linkIndex(link); i > 0; i = chain.is_tree ? chain.parent[i] : i - 1)
     if (chain.joint_type[i] != THIP_JOINT_FIXED)
       return true;
   return false;
@@ -212,7 +212,7 @@ std::array<double, 12> KinematicGroup::staticWorldPose(const std::string& link) 
     if (isActiveLinkId(link))
       throw std::runtime_error("staticWorldPose: link " + link + " is active");
     std::vector<int> path;  // root -> link
-    for (int i = k; i > 0; i = chain.parent[i])
+    for (int i = k; i > 0; i = chain.is_tree ? chain.parent[i] : i - 1)
       path.insert(path.begin(), i);
     Pose12 T;
     std::copy(chain.base_pose, chain.base_pose + 12, T.begin());
@@ -839,6 +839,7 @@ TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci)
   prob->env_ = pci.env;
   thip_problem_desc& d = prob->desc_;
   std::memset(&d, 0, sizeof(d));
+  d.abi_version = THIP_ABI_VERSION;
   d.n_steps = n_steps;
   d.chain = pci.kin->chain;
   const int n_dof = pci.kin->numJoints();
@@ -897,6 +898,7 @@ TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci)
   d.sqp.initial_merit_error_coeff = o.initial_merit_error_coeff;
   d.sqp.inflate_constraints_individually = o.inflate_constraints_individually ? 1 : 0;
   d.sqp.trust_box_size = o.trust_box_size;
+  d.sqp.max_time = o.max_time;
   d.osqp = pci.osqp;
 
   for (const auto& ci : pci.cost_infos)

@@ -10,6 +10,7 @@ import ctypes as C
 import os
 from pathlib import Path
 
+ABI_VERSION = 3  # THIP_ABI_VERSION
 MAX_DOF = 16
 MAX_LINKS = 32
 MAX_STEPS = 64
@@ -19,6 +20,7 @@ MAX_PRIMS = 16
 MAX_JPOS = 8
 MAX_JVX = 4
 TRACE_W = 16  # THIP_TRACE_W
+DEBUG_NO_SEGMENT, DEBUG_FORCE_WIDE = 1, 2  # thip_debug_set_path flags
 
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_CONTINUOUS, JOINT_PRISMATIC = 0, 1, 2, 3
 PRIM_SPHERE, PRIM_BOX, PRIM_CAPSULE = 0, 1, 2
@@ -40,6 +42,7 @@ class Chain(C.Structure):
     _fields_ = [
         ("n_links", C.c_int),
         ("n_dof", C.c_int),
+        ("is_tree", C.c_int),
         ("base_pose", C.c_double * 12),
         ("joint_type", C.c_int * MAX_LINKS),
         ("joint_dof", C.c_int * MAX_LINKS),
@@ -67,6 +70,7 @@ class SqpParams(C.Structure):
         ("initial_merit_error_coeff", C.c_double),
         ("inflate_constraints_individually", C.c_int),
         ("trust_box_size", C.c_double),
+        ("max_time", C.c_double),
     ]
 
 
@@ -94,6 +98,7 @@ class OsqpSettings(C.Structure):
 
 class ProblemDesc(C.Structure):
     _fields_ = [
+        ("abi_version", C.c_int),
         ("n_steps", C.c_int),
         ("chain", Chain),
         ("n_fixed", C.c_int),
@@ -153,6 +158,10 @@ class ProblemDesc(C.Structure):
         ("osqp", OsqpSettings),
     ]
 
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.abi_version = ABI_VERSION
+
 
 class Result(C.Structure):
     _fields_ = [
@@ -191,6 +200,7 @@ def default_sqp_params() -> SqpParams:
     p.initial_merit_error_coeff = 10
     p.inflate_constraints_individually = 1
     p.trust_box_size = 1e-1
+    p.max_time = 1.7976931348623157e308
     return p
 
 
@@ -273,6 +283,8 @@ def _declare(lib):
     lib.thip_debug_profile.restype = C.c_int
     lib.thip_debug_get_profile.argtypes = [vp, P(C.c_longlong)]
     lib.thip_debug_get_profile.restype = C.c_int
+    lib.thip_debug_set_path.argtypes = [C.c_int]
+    lib.thip_debug_set_path.restype = C.c_int
     lib.thip_sizeof_desc.argtypes = []
     lib.thip_sizeof_desc.restype = C.c_int
     lib.thip_sizeof_result.argtypes = []

@@ -108,6 +108,7 @@ def _chain(base_xyz, joints, parents=None) -> Chain:
     """Joint k (1-based) attaches link k to link parents[k - 1] (default k - 1)."""
     c = Chain()
     c.n_links = len(joints) + 1
+    c.is_tree = 0 if parents is None else 1
     for k in range(1, c.n_links):
         c.parent[k] = (k - 1) if parents is None else parents[k - 1]
     base = _pose(base_xyz)
