@@ -420,6 +420,45 @@ int thip_debug_layout(thip_ctx* ctx, long long* doff, long long* ioff, long long
 int thip_debug_set_path(int flags);
 int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws);
 
+/* ------------------------------------------------------------- Generic QP
+ * OSQP 1.0 on an arbitrary sparse QP
+ *     minimise 1/2 x'Px + q'x   subject to   l <= A x <= u
+ * with OSQPModel's settings and warm start (sco::OSQPModel::optimize,
+ * trajopt_sco/src/osqp_interface.cpp:283-615): the QP backend of
+ * sco::GpuModel (trajopt-1_amd/host/include/trajopt_sco/gpu_model.hpp), which
+ * is the sco::Model a non-lowerable OptProb (custom terms, JointAcc /
+ * JointJerk terms, the reference's small-problem tests) is solved with.  A
+ * thip_qp holds one sparsity pattern -- P upper-triangular CSC (n x n), A CSC
+ * (m x n) -- for `batch` QPs whose values differ; one workgroup per QP, dense
+ * quasi-definite LDL^T of the KKT, so n + m <= THIP_QP_MAX_KKT. */
+#define THIP_QP_MAX_KKT 4096
+typedef struct thip_qp thip_qp;
+typedef struct thip_qp_info {
+  int status;        /* OSQP 1.0 status value (1 solved, 2 solved inaccurate, 3/4 primal infeasible
+                        (inaccurate), 5/6 dual infeasible (inaccurate), 7 max iter, 9 non-convex);
+                        -1: setup failed (see setup_error) */
+  int setup_error;   /* osqp_setup error code when status = -1 (1 data validation, 4 KKT
+                        factorisation, 5 non-convex) */
+  int polish_status; /* 1 polished, -1 polish failed, 0 not run */
+  int iter;          /* ADMM iterations */
+  double rho;        /* rho at exit (the warm start of the next solve) */
+  double prim_res;
+  double dual_res;
+} thip_qp_info;
+/* Pattern (host arrays, copied): P_colptr[n+1], P_rowind[nnz_P] (rows <= column),
+ * A_colptr[n+1], A_rowind[nnz_A]. */
+int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_rowind, const int* A_colptr,
+                   const int* A_rowind, int batch, thip_qp** out);
+/* Solve every QP (synchronous; host arrays): P_values [batch][nnz_P], q [batch][n],
+ * A_values [batch][nnz_A], l, u [batch][m] (+-1e30 = infinite); warm_x [batch][n],
+ * warm_y [batch][m] (both or neither), warm_rho [batch] (or NULL: settings->rho);
+ * out: x [batch][n], y [batch][m] (may be NULL), info [batch]. */
+int thip_qp_solve(thip_qp* qp, const double* P_values, const double* q, const double* A_values, const double* l,
+                  const double* u, const thip_osqp_settings* settings, const double* warm_x, const double* warm_y,
+                  const double* warm_rho, double* x, double* y, thip_qp_info* info);
+void thip_qp_destroy(thip_qp* qp);
+const char* thip_qp_last_error(thip_qp* qp); /* NULL: the last thip_qp_create failure */
+
 #ifdef __cplusplus
 }
 #endif

@@ -85,6 +85,17 @@ def lib(variant="exact"):
     return _libs[variant]
 
 
+def set_jitter(jac_abs=0.0, kkt_rel=0.0, sol_rel=0.0, seed=0, variant="exact"):
+    """Rounding jitter of the next solves (oracle/src/jitter.hpp): +-jac_abs on
+    every FD Jacobian entry, a relative +-kkt_rel on every KKT solution entry, a
+    relative +-sol_rel on every returned QP solution; all 0 turns it off.  Test
+    infrastructure: the parity gate's stability proofs."""
+    L = lib(variant)
+    L.oracle_set_jitter.argtypes = [C.c_double, C.c_double, C.c_double, C.c_ulonglong]
+    L.oracle_set_jitter.restype = None
+    L.oracle_set_jitter(float(jac_abs), float(kkt_rel), float(sol_rel), int(seed))
+
+
 def _dp(a):
     if a is None:
         return None
@@ -127,7 +138,7 @@ def solve_trace(wl, b, cap=2048):
     sc = np.ascontiguousarray(wl.scene[b], dtype=np.float64) if wl.scene.size else None
     x = np.zeros_like(init)
     res = abi.Result()
-    rec = np.zeros((cap, 10))
+    rec = np.zeros((cap, 12))
     n = L.oracle_solve_trace(C.byref(wl.desc), _dp(init), _dp(tg), _dp(sc), _dp(_jpos(wl, b)), _dp(x), C.byref(res),
                              _dp(rec), cap)
     if n < 0:

@@ -12,6 +12,7 @@
 
 #include "collision.hpp"
 #include "terms.hpp"
+#include "jitter.hpp"
 
 using namespace orc;
 
@@ -20,9 +21,10 @@ namespace
 thread_local std::string g_err;
 
 void solveOne(const thip_problem_desc* d, const double* init, const double* targets, const double* scene,
-              const double* jpos_targets, double* out_x, thip_result* res)
+              const double* jpos_targets, double* out_x, thip_result* res, int problem = 0)
 {
   const int N = d->n_steps, D = d->chain.n_dof;
+  jitterSeed(static_cast<std::uint64_t>(problem));
   TrajProblem tp = constructProblem(*d, init, targets, scene, jpos_targets);
   BasicTrustRegionSQP opt(tp.prob);
   opt.getParameters() = toSqpParams(d->sqp);
@@ -52,6 +54,15 @@ extern "C" {
 
 const char* oracle_last_error() { return g_err.c_str(); }
 
+// Rounding jitter for the parity gate's stability proofs (jitter.hpp); 0, 0 = off.
+void oracle_set_jitter(double jac_abs, double kkt_rel, double sol_rel, unsigned long long seed)
+{
+  g_jitter.jac_abs = jac_abs;
+  g_jitter.kkt_rel = kkt_rel;
+  g_jitter.sol_rel = sol_rel;
+  g_jitter.seed = seed;
+}
+
 // BasicTrustRegionSQP::optimize over a batch, problems spread over n_threads.
 int oracle_solve_batch(const thip_problem_desc* d, int batch, const double* init, const double* targets,
                        const double* scene, const double* jpos_targets, double* out_x, thip_result* res,
@@ -73,7 +84,7 @@ int oracle_solve_batch(const thip_problem_desc* d, int batch, const double* init
         solveOne(d, init + static_cast<std::size_t>(b) * N * D,
                  targets ? targets + static_cast<std::size_t>(b) * d->n_cart * 12 : nullptr,
                  scene ? scene + static_cast<std::size_t>(b) * d->n_prims * 16 : nullptr,
-                 jpos_targets ? jpos_targets + static_cast<std::size_t>(b) * d->n_jpos * D : nullptr, out_x + static_cast<std::size_t>(b) * N * D, res ? res + b : nullptr);
+                 jpos_targets ? jpos_targets + static_cast<std::size_t>(b) * d->n_jpos * D : nullptr, out_x + static_cast<std::size_t>(b) * N * D, res ? res + b : nullptr, b);
       }
       catch (const std::exception& e)
       {
@@ -139,7 +150,8 @@ int oracle_linearize(const thip_problem_desc* d, int batch, const double* x, con
 }
 
 // one problem with a per-QP trace: rec[cap][10] =
-// (warm, rho0, iters, status, polish, rho1, prim_res, dual_res, sum|x|, trust_box); returns #records
+// (warm, rho0, iters, status, polish, rho1, prim_res, dual_res, sum|x|, trust_box, tie_cleanup,
+// tie_polish); returns #records
 int oracle_solve_trace(const thip_problem_desc* d, const double* init, const double* targets, const double* scene,
                        const double* jpos_targets, double* out_x, thip_result* res, double* rec, int cap)
 {
@@ -164,7 +176,8 @@ int oracle_solve_trace(const thip_problem_desc* d, const double* init, const dou
       res->n_admm_iters = opt.results().n_admm_iters;
     }
     const int n = std::min<int>(cap, static_cast<int>(tr.size()));
-    std::memcpy(rec, tr.data(), sizeof(double) * 10 * static_cast<std::size_t>(n));
+    static_assert(sizeof(OSQPModel::Trace) == 12 * sizeof(double), "trace record layout");
+    std::memcpy(rec, tr.data(), sizeof(double) * 12 * static_cast<std::size_t>(n));
     return n;
   }
   catch (const std::exception& e)

@@ -1,6 +1,7 @@
 // ORACLE — test infrastructure only (see sco_expr.hpp header).
 // OSQP 1.0.0 restatement; see osqp_restated.hpp for provenance.
 #include "osqp_restated.hpp"
+#include "jitter.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -553,6 +554,9 @@ void OsqpSolver::update_xz_tilde()
   // direct KKT solve, stores the solution in sol_
   std::copy(xz_tilde_.begin(), xz_tilde_.end(), sol_.begin());
   ldl_.solve(sol_.data());
+  if (g_jitter.kkt_rel > 0)  // parity-gate rounding jitter (jitter.hpp)
+    for (auto& v : sol_)
+      v *= 1.0 + g_jitter.kkt_rel * jitterU();
   for (OsqpInt j = 0; j < n; ++j)
     xz_tilde_[j] = sol_[j];
   for (OsqpInt r = 0; r < m; ++r)
@@ -821,6 +825,7 @@ int OsqpSolver::solve()
     cold_start();
   status_val = OSQP_UNSOLVED;
   status_polish = 0;
+  polish_margin = 1e300;
   bool can_check = false;
   OsqpInt it;
   for (it = 1; it <= settings_.max_iter; ++it)
@@ -880,8 +885,13 @@ void OsqpSolver::polish()
   // form_Ared: active set guess, rows kept in original order
   std::vector<int> flag(static_cast<std::size_t>(m), 0);  // -1 lower, +1 upper, 0 inactive
   std::vector<OsqpInt> act;
+  polish_margin = 1e300;
   for (OsqpInt r = 0; r < m; ++r)
   {
+    if (l_[r] > -OSQP_INFTY * OSQP_MIN_SCALING)
+      polish_margin = std::min(polish_margin, std::fabs((z_[r] - l_[r]) + y_[r]));
+    if (u_[r] < OSQP_INFTY * OSQP_MIN_SCALING)
+      polish_margin = std::min(polish_margin, std::fabs((u_[r] - z_[r]) - y_[r]));
     if (z_[r] - l_[r] < -y_[r])
       flag[r] = -1;
     else if (u_[r] - z_[r] < y_[r])
@@ -965,6 +975,9 @@ void OsqpSolver::polish()
     rhs[n + k] = (flag[act[k]] < 0) ? l_[act[k]] : u_[act[k]];
   sol = rhs;
   plsh.solve(sol.data());
+  if (g_jitter.kkt_rel > 0)
+    for (auto& v : sol)
+      v *= 1.0 + g_jitter.kkt_rel * jitterU();
   // iterative refinement on the unregularised KKT
   for (int itr = 0; itr < settings_.polish_refine_iter; ++itr)
   {
@@ -1022,6 +1035,9 @@ void OsqpSolver::store_solution()
   {
     for (std::size_t j = 0; j < n; ++j)
       sol_x[j] = (settings_.scaling > 0) ? D_[j] * x_[j] : x_[j];
+    if (g_jitter.sol_rel > 0)  // parity-gate rounding jitter (jitter.hpp)
+      for (std::size_t j = 0; j < n; ++j)
+        sol_x[j] *= 1.0 + g_jitter.sol_rel * jitterU();
     for (std::size_t r = 0; r < m; ++r)
       sol_y[r] = (settings_.scaling > 0) ? cinv_ * (E_[r] * y_[r]) : y_[r];
   }

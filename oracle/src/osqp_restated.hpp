@@ -120,6 +120,7 @@ public:
   OsqpInt iter = 0;
   double prim_res = 0, dual_res = 0;
   int rho_updates = 0;
+  double polish_margin = 0;  // smallest margin of the last polish's active-set comparisons
   const OsqpSettings& settings() const { return settings_; }
 
 private:

@@ -371,7 +371,7 @@ CvxOptStatus OSQPModel::optimize()
   catch (const std::exception&)
   {
     if (trace)
-      trace->push_back({ 0, 0, 0, -1, 0, 0, 0, 0, 0, trace_trust });
+      trace->push_back({ 0, 0, 0, -1, 0, 0, 0, 0, 0, trace_trust, trace_tie_cleanup, 0 });
     return CVX_FAILED;
   }
   const double rho0 = ws_->settings().rho;
@@ -384,7 +384,8 @@ CvxOptStatus OSQPModel::optimize()
       xs += std::fabs(v);
     trace->push_back({ last_warm_started ? 1.0 : 0.0, rho0, static_cast<double>(ws_->iter),
                        static_cast<double>(ws_->status_val), static_cast<double>(ws_->status_polish),
-                       ws_->settings().rho, ws_->prim_res, ws_->dual_res, xs, trace_trust });
+                       ws_->settings().rho, ws_->prim_res, ws_->dual_res, xs, trace_trust, trace_tie_cleanup,
+                       ws_->polish_margin });
   }
   last_osqp_status = ws_->status_val;
   last_polish_status = ws_->status_polish;
@@ -984,6 +985,7 @@ OptStatus BasicTrustRegionSQP::optimize()
       bool converged_inner = false;
       bool failed = false;
       {
+        t_cleanup_margin = 1e300;
         std::vector<ConvexObjective::Ptr> cost_models(costs.size());
         for (std::size_t i = 0; i < costs.size(); ++i)
           cost_models[i] = costs[i]->convex(results_.x, model_.get());
@@ -1004,6 +1006,8 @@ OptStatus BasicTrustRegionSQP::optimize()
         for (auto& c : cnt_cost_models)
           exprInc(objective, c->quad_);
         model_->setObjective(objective);
+        if (osqp_model)
+          osqp_model->trace_tie_cleanup = t_cleanup_margin;
 
         int qp_solver_failures = 0;
         while (param_.trust_box_size >= param_.min_trust_box_size)

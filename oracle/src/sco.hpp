@@ -117,9 +117,12 @@ public:
   struct Trace
   {
     double warm, rho0, iters, status, polish, rho1, prim, dual, xsum, trust;
+    double tie_cleanup;  // smallest | |J| - 1e-7 | of the linearisation this QP solves (cleanupAff)
+    double tie_polish;   // smallest margin of polish's active-set comparisons (1e300 if no polish)
   };
   std::vector<Trace>* trace = nullptr;
   double trace_trust = 0;
+  double trace_tie_cleanup = 1e300;
   long long admm_iters_total = 0;
   int last_osqp_status = 0;
   int last_polish_status = 0;

@@ -233,9 +233,20 @@ inline QuadExpr exprSquare(const AffExpr& a)
   return out;
 }
 
+// smallest | |c| - 1e-7 | cleanupAff has compared since the last reset: how close
+// a linearisation's sparsity pattern (the warm-start test, quirk Q2) came to a
+// tie (tests/parity.py's threshold-tie evidence; infinity after a reset)
+inline thread_local double t_cleanup_margin = 1e300;
+
 inline AffExpr cleanupAff(const AffExpr& a)
 {
   AffExpr out;
+  for (std::size_t i = 0; i < a.size(); ++i)
+  {
+    const double m = std::fabs(std::fabs(a.coeffs[i]) - 1e-7);
+    if (m < t_cleanup_margin)
+      t_cleanup_margin = m;
+  }
   for (std::size_t i = 0; i < a.size(); ++i)
     if (std::fabs(a.coeffs[i]) > 1e-7)
     {

@@ -1,5 +1,6 @@
 // ORACLE — test infrastructure only (see sco_expr.hpp header).
 #include "terms.hpp"
+#include "jitter.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -527,7 +528,11 @@ Mat CartPoseCalc::jac(const DblVec& q) const
     else
       calcJacobianTransformErrorDiff(target_tf, tp, source_tf, sp, diff);
     for (std::size_t r = 0; r < indices.size(); ++r)
+    {
       J(static_cast<int>(r), static_cast<int>(i)) = diff[indices[r]] / eps;
+      if (g_jitter.jac_abs > 0)  // parity-gate rounding jitter (jitter.hpp)
+        J(static_cast<int>(r), static_cast<int>(i)) += g_jitter.jac_abs * jitterU();
+    }
     qp[i] = q[i];
   }
   return J;

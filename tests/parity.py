@@ -9,10 +9,15 @@ the reference algorithm itself does not determine its outcome at double
 precision.  The proof reruns the oracle on the problem under rounding-level
 changes that leave the mathematics untouched:
   * the oracle's second build (oracle/Makefile `liboracle_fast_*`: the same
-    sources at -O3 with FMA contraction), i.e. the same algorithm with
-    different rounding -- exactly what differs between the GPU and the oracle;
+    sources at -O3 with FMA contraction): the same algorithm, another rounding;
+  * rounding jitter (oracle/src/jitter.hpp), re-drawing the noise that the
+    GPU's different operation order puts into the quantities the algorithm
+    thresholds: +-3e-10 on every forward-difference CartPose Jacobian entry
+    (GPU and oracle agree to 1.5e-10 there, tools/mask_probe.py), a relative
+    1e-14 on every KKT solve and 1e-10 on every returned QP solution (the
+    polished points agree to ~5e-11 relative, per-QP traces);
   * the initial trajectory perturbed by 1e-13, then 1e-12 (interior
-    waypoints, seeded normal noise), on both builds.
+    waypoints, seeded normal noise).
 The rerun "cloud" is grown lazily, only for the problems that miss the bar,
 and the problem is excused iff
   (reach)   some rerun reaches the GPU's outcome: same status, same flag and
@@ -34,12 +39,14 @@ import numpy as np
 TOL_X = 1e-5
 COST_RTOL = 0.02
 
-# (build, perturbation amplitude, seed); amplitude 0: the unperturbed inputs
-SCHEDULE = ([("fast", 0.0, 0)]
-            + [("exact", 1e-13, s) for s in range(1, 9)]
-            + [("fast", 1e-13, s) for s in range(1, 5)]
-            + [("exact", 1e-12, s) for s in range(1, 9)]
-            + [("fast", 1e-12, s) for s in range(1, 5)])
+# (build, input perturbation amplitude, rounding jitter on, seed)
+JITTER = (3e-10, 1e-14, 1e-10)  # FD Jacobian (absolute), KKT solve, QP solution (relative)
+SCHEDULE = ([("fast", 0.0, False, 0)]
+            + [("exact", 0.0, True, s) for s in range(1, 9)]
+            + [("exact", 1e-13, False, s) for s in range(1, 5)]
+            + [("fast", 0.0, True, s) for s in range(1, 5)]
+            + [("exact", 1e-12, False, s) for s in range(1, 5)]
+            + [("exact", 1e-13, True, s) for s in range(9, 13)])
 
 RECORDS: list[dict] = []
 
@@ -97,11 +104,18 @@ class Cloud:
         """Run the next schedule entry on the pending problems; False when exhausted."""
         if self.k >= len(SCHEDULE) or not pending:
             return False
-        build, amp, seed = SCHEDULE[self.k]
+        build, amp, jit, seed = SCHEDULE[self.k]
         self.k += 1
         sub = perturbed(subset(self.wl, pending), amp, seed)
-        x, res = oracle_solve(sub, self.oracle_mod, self.threads, variant=build)
-        progress(f"cloud run {self.k}/{len(SCHEDULE)} ({build}, {amp:g}, seed {seed}) on {len(pending)} problems")
+        if jit:
+            self.oracle_mod.set_jitter(*JITTER, seed=seed, variant=build)
+        try:
+            x, res = oracle_solve(sub, self.oracle_mod, self.threads, variant=build)
+        finally:
+            if jit:
+                self.oracle_mod.set_jitter(0.0, 0.0, 0.0, seed=0, variant=build)
+        progress(f"cloud run {self.k}/{len(SCHEDULE)} ({build}, input {amp:g}, jitter {jit}, seed {seed}) "
+                 f"on {len(pending)} problems")
         tol = self.wl.desc.sqp.cnt_tolerance
         for j, b in enumerate(pending):
             self.members[b].append((x[j], res[j].status, res[j].max_cnt_viol < tol, res[j].total_cost))

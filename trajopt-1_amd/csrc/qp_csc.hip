@@ -1,0 +1,1218 @@
+// Generic sparse QP solve with OSQP 1.0 semantics on gfx950 (the GpuModel
+// backend of trajopt_sco::Model, include/trajopt_hip.h "Generic QP").
+//
+// The reference solves every convexified QP with OSQP 1.0 through
+// sco::OSQPModel (trajopt_sco/src/osqp_interface.cpp:283-615).  This kernel
+// runs that algorithm for a batch of QPs that share one sparsity pattern, one
+// 256-thread workgroup per QP:
+//   * modified Ruiz equilibration + cost scaling (settings.scaling passes);
+//   * the rho vector (equality rows x1e3, free rows rho_min);
+//   * the quasi-definite KKT [P + sigma I, A'; A, -diag(1/rho)] factored as a
+//     dense LDL^T in the QP's HBM workspace (no pivoting: a quasi-definite
+//     matrix factors under any symmetric order; the pivot signs give OSQP's
+//     convexity check) and solved forward / diagonal / backward with the
+//     solve vector in LDS;
+//   * ADMM with over-relaxation, termination on unscaled inf-norm residuals
+//     every check_termination iterations, primal / dual infeasibility
+//     certificates, iteration-based adaptive rho (refactorisation);
+//   * polishing: active set from (z, y), the delta-regularised reduced KKT,
+//     polish_refine_iter refinements on the unregularised one, OSQP's
+//     acceptance test;
+//   * warm start of (x, y, rho) as OSQPModel::createOrUpdateSolver passes it.
+// The structured trajectory QPs of a TrajOptProb batch do not come here: they
+// run sqp_kernel's block-tridiagonal path.  This path serves arbitrary
+// sco::Model users (custom terms, JointAcc / JointJerk terms, the reference's
+// small-problem and solver-interface tests): the dense factor bounds the KKT
+// dimension n + m at THIP_QP_MAX_KKT.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/trajopt_hip.h"
+
+namespace thip_qp_dev
+{
+constexpr int kQB = 256;
+constexpr double kInf = 1e30;             // OSQP_INFTY
+constexpr double kRhoMin = 1e-6, kRhoMax = 1e6, kRhoTol = 1e-4, kRhoEq = 1e3;
+constexpr double kMinScaling = 1e-4, kMaxScaling = 1e4;
+constexpr double kDivTol = 1.0 / kInf;
+
+// OSQP 1.0 status values (osqp_api_constants.h)
+enum : int
+{
+  SOLVED = 1,
+  SOLVED_INACCURATE = 2,
+  PRIMAL_INFEASIBLE = 3,
+  PRIMAL_INFEASIBLE_INACCURATE = 4,
+  DUAL_INFEASIBLE = 5,
+  DUAL_INFEASIBLE_INACCURATE = 6,
+  MAX_ITER_REACHED = 7,
+  NON_CVX = 9,
+  UNSOLVED = 11,
+};
+
+// workspace arrays per QP (doubles), sizes n / m / nnz / N = n + m / N*N
+enum Arr : int
+{
+  W_PX, W_AX, W_Q, W_L, W_U, W_D, W_DI, W_E, W_EI, W_TD, W_TE, W_RHO, W_RHOI, W_CT,
+  W_X, W_XP, W_Z, W_ZP, W_Y, W_DX, W_DY, W_XT, W_AXV, W_PXV, W_ATY, W_RP, W_RD, W_T1, W_T2,
+  W_PXS, W_PZS, W_PYS, W_RHS, W_RES, W_FLG, W_RMAP, W_K, W_KT, W_COUNT
+};
+
+struct QpPattern
+{
+  int n, m, nnz_p, nnz_a, N;  // N = n + m: the KKT dimension
+  // P upper triangular CSC and its rows (entries (j, c >= j) of row j -> index into P values)
+  const int *Pp, *Pi, *Prp, *Prj, *Prmap;
+  // A CSC and its rows (-> index into A values)
+  const int *Ap, *Ai, *Arp, *Arj, *Armap;
+  long long off[W_COUNT];
+  long long stride;
+};
+
+struct QpArgs
+{
+  QpPattern pat;
+  thip_osqp_settings s;
+  const double *Pv, *qv, *Av, *lv, *uv;       // [batch][...]
+  const double *x_ws, *y_ws, *rho_ws;         // warm start (null = cold)
+  double *x_out, *y_out;                      // [batch][n], [batch][m]
+  thip_qp_info* info;                         // [batch]
+  double* ws;                                 // [batch][stride]
+  int batch;
+};
+
+struct Sh
+{
+  double red[kQB / 64];
+  double c, cinv, rho;
+  double prim_res, dual_res;
+  int status, polish, iter, npos, fail, nred;
+};
+
+#define QFOR(i, n) for (int i = static_cast<int>(threadIdx.x); i < (n); i += kQB)
+
+__device__ __forceinline__ double wave_max(double v)
+{
+  for (int o = 32; o > 0; o >>= 1)
+    v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v)
+{
+  for (int o = 32; o > 0; o >>= 1)
+    v += __shfl_xor(v, o);
+  return v;
+}
+__device__ double bmax(Sh& sh, double v)
+{
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0)
+    sh.red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = sh.red[0];
+  for (int w = 1; w < kQB / 64; ++w)
+    r = fmax(r, sh.red[w]);
+  return r;
+}
+__device__ double bsum(Sh& sh, double v)
+{
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0)
+    sh.red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = sh.red[0];
+  for (int w = 1; w < kQB / 64; ++w)
+    r += sh.red[w];
+  return r;
+}
+__device__ double norm_inf(Sh& sh, const double* v, int n)
+{
+  double a = 0;
+  QFOR(i, n) a = fmax(a, fabs(v[i]));
+  return bmax(sh, a);
+}
+__device__ double scaled_norm_inf(Sh& sh, const double* s, const double* v, int n)
+{
+  double a = 0;
+  QFOR(i, n) a = fmax(a, fabs(s[i] * v[i]));
+  return bmax(sh, a);
+}
+__device__ __forceinline__ double limit_scaling(double a)
+{
+  a = a < kMinScaling ? 1.0 : a;
+  return a > kMaxScaling ? kMaxScaling : a;
+}
+
+struct Qp
+{
+  const QpPattern& p;
+  const thip_osqp_settings& s;
+  double* w;
+  Sh& sh;
+  double* lv;  // LDS solve vector [N]
+  int n, m;
+  __device__ double* a(int k) const { return w + p.off[k]; }
+};
+
+// y = A x (rows), y = A' x (columns), y = P x (full symmetric from the upper triangle)
+__device__ void a_mul(const Qp& q, const double* x, double* y)
+{
+  const double* AX = q.a(W_AX);
+  QFOR(r, q.m)
+  {
+    double v = 0;
+    for (int e = q.p.Arp[r]; e < q.p.Arp[r + 1]; ++e)
+      v += AX[q.p.Armap[e]] * x[q.p.Arj[e]];
+    y[r] = v;
+  }
+}
+__device__ void at_mul(const Qp& q, const double* x, double* y)
+{
+  const double* AX = q.a(W_AX);
+  QFOR(j, q.n)
+  {
+    double v = 0;
+    for (int e = q.p.Ap[j]; e < q.p.Ap[j + 1]; ++e)
+      v += AX[e] * x[q.p.Ai[e]];
+    y[j] = v;
+  }
+}
+__device__ void p_mul(const Qp& q, const double* x, double* y)
+{
+  const double* PX = q.a(W_PX);
+  QFOR(j, q.n)
+  {
+    double v = 0;
+    for (int e = q.p.Pp[j]; e < q.p.Pp[j + 1]; ++e)  // (i, j), i <= j
+      v += PX[e] * x[q.p.Pi[e]];
+    for (int e = q.p.Prp[j]; e < q.p.Prp[j + 1]; ++e)  // (j, c), c > j
+      if (q.p.Prj[e] != j)
+        v += PX[q.p.Prmap[e]] * x[q.p.Prj[e]];
+    y[j] = v;
+  }
+}
+
+// inf-norm of the full symmetric P's columns
+__device__ void p_col_norm(const Qp& q, double* out)
+{
+  const double* PX = q.a(W_PX);
+  QFOR(j, q.n)
+  {
+    double v = 0;
+    for (int e = q.p.Pp[j]; e < q.p.Pp[j + 1]; ++e)
+      v = fmax(v, fabs(PX[e]));
+    for (int e = q.p.Prp[j]; e < q.p.Prp[j + 1]; ++e)
+      v = fmax(v, fabs(PX[q.p.Prmap[e]]));
+    out[j] = v;
+  }
+}
+
+// modified Ruiz equilibration (OSQP scale_data)
+__device__ void scale_data(Qp& q)
+{
+  const int n = q.n, m = q.m;
+  double *PX = q.a(W_PX), *AX = q.a(W_AX), *Q = q.a(W_Q), *D = q.a(W_D), *E = q.a(W_E), *TD = q.a(W_TD),
+         *TE = q.a(W_TE);
+  if (threadIdx.x == 0)
+    q.sh.c = 1.0;
+  QFOR(j, n) D[j] = 1.0;
+  QFOR(r, m) E[r] = 1.0;
+  __syncthreads();
+  for (int it = 0; it < q.s.scaling; ++it)
+  {
+    p_col_norm(q, TD);
+    __syncthreads();
+    QFOR(j, n)
+    {
+      double v = 0;
+      for (int e = q.p.Ap[j]; e < q.p.Ap[j + 1]; ++e)
+        v = fmax(v, fabs(AX[e]));
+      TD[j] = 1.0 / sqrt(limit_scaling(fmax(TD[j], v)));
+    }
+    QFOR(r, m)
+    {
+      double v = 0;
+      for (int e = q.p.Arp[r]; e < q.p.Arp[r + 1]; ++e)
+        v = fmax(v, fabs(AX[q.p.Armap[e]]));
+      TE[r] = 1.0 / sqrt(limit_scaling(v));
+    }
+    __syncthreads();
+    QFOR(j, n)
+    for (int e = q.p.Pp[j]; e < q.p.Pp[j + 1]; ++e)
+      PX[e] = (PX[e] * TD[q.p.Pi[e]]) * TD[j];
+    QFOR(j, n)
+    for (int e = q.p.Ap[j]; e < q.p.Ap[j + 1]; ++e)
+      AX[e] = (AX[e] * TE[q.p.Ai[e]]) * TD[j];
+    QFOR(j, n)
+    {
+      Q[j] *= TD[j];
+      D[j] *= TD[j];
+    }
+    QFOR(r, m) E[r] *= TE[r];
+    __syncthreads();
+    // cost normalisation
+    p_col_norm(q, TD);
+    __syncthreads();
+    double s = 0;
+    QFOR(j, n) s += TD[j];
+    s = bsum(q.sh, s);
+    double c_temp = (n > 0) ? s / static_cast<double>(n) : 0.0;
+    const double qn = limit_scaling(norm_inf(q.sh, Q, n));
+    c_temp = fmax(c_temp, qn);
+    c_temp = 1.0 / limit_scaling(c_temp);
+    QFOR(j, n)
+    for (int e = q.p.Pp[j]; e < q.p.Pp[j + 1]; ++e)
+      PX[e] *= c_temp;
+    QFOR(j, n) Q[j] *= c_temp;
+    if (threadIdx.x == 0)
+      q.sh.c *= c_temp;
+    __syncthreads();
+  }
+  double *DI = q.a(W_DI), *EI = q.a(W_EI), *L = q.a(W_L), *U = q.a(W_U);
+  QFOR(j, n) DI[j] = 1.0 / D[j];
+  QFOR(r, m)
+  {
+    EI[r] = 1.0 / E[r];
+    L[r] *= E[r];
+    U[r] *= E[r];
+  }
+  if (threadIdx.x == 0)
+    q.sh.cinv = 1.0 / q.sh.c;
+  __syncthreads();
+}
+
+__device__ void set_rho_vec(Qp& q)
+{
+  double *L = q.a(W_L), *U = q.a(W_U), *RHO = q.a(W_RHO), *RHOI = q.a(W_RHOI), *CT = q.a(W_CT);
+  const double rho = q.sh.rho;
+  QFOR(r, q.m)
+  {
+    double ct, rv;
+    if (L[r] < -kInf * kMinScaling && U[r] > kInf * kMinScaling)
+    {
+      ct = -1;
+      rv = kRhoMin;
+    }
+    else if (U[r] - L[r] < kRhoTol)
+    {
+      ct = 1;
+      rv = kRhoEq * rho;
+    }
+    else
+    {
+      ct = 0;
+      rv = rho;
+    }
+    CT[r] = ct;
+    RHO[r] = rv;
+    RHOI[r] = 1.0 / rv;
+  }
+  __syncthreads();
+}
+
+// dense LDL^T of the N x N symmetric matrix K (lower triangle, row-major, in
+// place: D on the diagonal, L strictly below); KT gets L^T row-major for the
+// forward solve.  sh.npos = positive pivots, sh.fail = 1 on a zero / non-finite pivot.
+__device__ void ldl_factor(Qp& q, double* K, double* KT, int N)
+{
+  if (threadIdx.x == 0)
+  {
+    q.sh.npos = 0;
+    q.sh.fail = 0;
+  }
+  __syncthreads();
+  for (int k = 0; k < N; ++k)
+  {
+    const double d = K[(long long)k * N + k];
+    if (d == 0.0 || !isfinite(d))
+    {
+      if (threadIdx.x == 0)
+        q.sh.fail = 1;
+      __syncthreads();
+      return;
+    }
+    if (threadIdx.x == 0 && d > 0)
+      q.sh.npos++;
+    const int T = N - k - 1;
+    const double dinv = 1.0 / d;
+    QFOR(ii, T)
+    {
+      const long long i = k + 1 + ii;
+      K[i * N + k] *= dinv;
+    }
+    __syncthreads();
+    // trailing update K[i][j] -= L[i][k] d L[j][k], k < j <= i
+    const long long TT = (long long)T * T;
+    for (long long e = threadIdx.x; e < TT; e += kQB)
+    {
+      const int ii = static_cast<int>(e / T), jj = static_cast<int>(e - (long long)ii * T);
+      if (jj <= ii)
+      {
+        const long long i = k + 1 + ii, j = k + 1 + jj;
+        K[i * N + j] -= (K[i * N + k] * d) * K[j * N + k];
+      }
+    }
+    __syncthreads();
+  }
+  // L^T rows for the forward solve
+  const long long NN = (long long)N * N;
+  for (long long e = threadIdx.x; e < NN; e += kQB)
+  {
+    const long long i = e / N, j = e - i * N;
+    if (j < i)
+      KT[j * N + i] = K[e];
+  }
+  __syncthreads();
+}
+
+// in place solve K v = b with v in LDS (lv[0..N))
+__device__ void ldl_solve(Qp& q, const double* K, const double* KT, int N, double* v)
+{
+  __syncthreads();
+  for (int k = 0; k < N; ++k)
+  {
+    const double vk = v[k];
+    const double* row = KT + (long long)k * N;
+    QFOR(ii, N - k - 1)
+    {
+      const int i = k + 1 + ii;
+      v[i] -= row[i] * vk;
+    }
+    __syncthreads();
+  }
+  QFOR(i, N) v[i] /= K[(long long)i * N + i];
+  __syncthreads();
+  for (int i = N - 1; i > 0; --i)
+  {
+    const double vi = v[i];
+    const double* row = K + (long long)i * N;
+    QFOR(j, i) v[j] -= row[j] * vi;
+    __syncthreads();
+  }
+}
+
+// KKT [P + sigma I, A'; A, -diag(1/rho)] (lower triangle)
+__device__ void build_kkt(Qp& q)
+{
+  const int n = q.n, m = q.m, N = n + m;
+  double *K = q.a(W_K), *PX = q.a(W_PX), *AX = q.a(W_AX), *RHOI = q.a(W_RHOI);
+  const long long NN = (long long)N * N;
+  for (long long e = threadIdx.x; e < NN; e += kQB)
+    K[e] = 0.0;
+  __syncthreads();
+  QFOR(j, n)
+  for (int e = q.p.Pp[j]; e < q.p.Pp[j + 1]; ++e)
+    K[(long long)j * N + q.p.Pi[e]] = PX[e];  // (i, j) upper -> (j, i) lower
+  QFOR(j, n)
+  for (int e = q.p.Ap[j]; e < q.p.Ap[j + 1]; ++e)
+    K[(long long)(n + q.p.Ai[e]) * N + j] = AX[e];
+  __syncthreads();
+  QFOR(j, n) K[(long long)j * N + j] += q.s.sigma;
+  QFOR(r, m) K[(long long)(n + r) * N + (n + r)] = -RHOI[r];
+  __syncthreads();
+}
+
+__device__ double prim_res(Qp& q, const double* x, const double* z)
+{
+  double *AXV = q.a(W_AXV), *RP = q.a(W_RP);
+  a_mul(q, x, AXV);
+  __syncthreads();
+  QFOR(r, q.m) RP[r] = AXV[r] - z[r];
+  __syncthreads();
+  return q.s.scaling > 0 ? scaled_norm_inf(q.sh, q.a(W_EI), RP, q.m) : norm_inf(q.sh, RP, q.m);
+}
+
+__device__ double dual_res(Qp& q, const double* x, const double* y)
+{
+  double *PXV = q.a(W_PXV), *ATY = q.a(W_ATY), *RD = q.a(W_RD), *Q = q.a(W_Q);
+  p_mul(q, x, PXV);
+  if (q.m > 0)
+    at_mul(q, y, ATY);
+  __syncthreads();
+  QFOR(j, q.n) RD[j] = (q.m > 0) ? (Q[j] + PXV[j]) + ATY[j] : Q[j] + PXV[j];
+  __syncthreads();
+  return q.s.scaling > 0 ? q.sh.cinv * scaled_norm_inf(q.sh, q.a(W_DI), RD, q.n) : norm_inf(q.sh, RD, q.n);
+}
+
+__device__ bool primal_infeasible(Qp& q, double eps)
+{
+  double *L = q.a(W_L), *U = q.a(W_U), *DY = q.a(W_DY), *T1 = q.a(W_T1);
+  QFOR(r, q.m)
+  {
+    if (U[r] > kInf * kMinScaling)
+      DY[r] = (L[r] < -kInf * kMinScaling) ? 0.0 : fmin(DY[r], 0.0);
+    else if (L[r] < -kInf * kMinScaling)
+      DY[r] = fmax(DY[r], 0.0);
+  }
+  __syncthreads();
+  const double ndy = q.s.scaling > 0 ? scaled_norm_inf(q.sh, q.a(W_E), DY, q.m) : norm_inf(q.sh, DY, q.m);
+  if (!(ndy > kDivTol))
+    return false;
+  double lhs = 0;
+  QFOR(r, q.m) lhs += U[r] * fmax(DY[r], 0.0) + L[r] * fmin(DY[r], 0.0);
+  lhs = bsum(q.sh, lhs);
+  if (!(lhs < eps * ndy))
+    return false;
+  at_mul(q, DY, T1);
+  __syncthreads();
+  if (q.s.scaling > 0)
+  {
+    const double* DI = q.a(W_DI);
+    QFOR(j, q.n) T1[j] *= DI[j];
+    __syncthreads();
+  }
+  return norm_inf(q.sh, T1, q.n) < eps * ndy;
+}
+
+__device__ bool dual_infeasible(Qp& q, double eps)
+{
+  double *DX = q.a(W_DX), *Q = q.a(W_Q), *T1 = q.a(W_T1), *T2 = q.a(W_T2), *L = q.a(W_L), *U = q.a(W_U);
+  double ndx, cs;
+  if (q.s.scaling > 0)
+  {
+    ndx = scaled_norm_inf(q.sh, q.a(W_D), DX, q.n);
+    cs = q.sh.c;
+  }
+  else
+  {
+    ndx = norm_inf(q.sh, DX, q.n);
+    cs = 1.0;
+  }
+  if (!(ndx > kDivTol))
+    return false;
+  double qdx = 0;
+  QFOR(j, q.n) qdx += Q[j] * DX[j];
+  qdx = bsum(q.sh, qdx);
+  if (!(qdx < cs * eps * ndx))
+    return false;
+  p_mul(q, DX, T1);
+  __syncthreads();
+  if (q.s.scaling > 0)
+  {
+    const double* DI = q.a(W_DI);
+    QFOR(j, q.n) T1[j] *= DI[j];
+    __syncthreads();
+  }
+  if (!(norm_inf(q.sh, T1, q.n) < cs * eps * ndx))
+    return false;
+  a_mul(q, DX, T2);
+  __syncthreads();
+  if (q.s.scaling > 0)
+  {
+    const double* EI = q.a(W_EI);
+    QFOR(r, q.m) T2[r] *= EI[r];
+    __syncthreads();
+  }
+  double bad = 0;
+  QFOR(r, q.m)
+  if (((U[r] < kInf * kMinScaling) && (T2[r] > eps * ndx)) || ((L[r] > -kInf * kMinScaling) && (T2[r] < -eps * ndx)))
+    bad = 1;
+  return bmax(q.sh, bad) == 0.0;
+}
+
+// check_termination (OSQP 1.0): sets sh.status, returns true when done
+__device__ bool check_termination(Qp& q, bool approximate)
+{
+  double eps_abs = q.s.eps_abs, eps_rel = q.s.eps_rel, eps_pi = q.s.eps_prim_inf, eps_di = q.s.eps_dual_inf;
+  if (approximate)
+  {
+    eps_abs *= 10;
+    eps_rel *= 10;
+    eps_pi *= 10;
+    eps_di *= 10;
+  }
+  bool prim_ok = false, dual_ok = false, prim_inf = false, dual_inf = false;
+  const bool sc = q.s.scaling > 0;
+  if (q.m == 0)
+    prim_ok = true;
+  else
+  {
+    const double* EI = q.a(W_EI);
+    const double mr = sc ? fmax(scaled_norm_inf(q.sh, EI, q.a(W_Z), q.m), scaled_norm_inf(q.sh, EI, q.a(W_AXV), q.m))
+                         : fmax(norm_inf(q.sh, q.a(W_Z), q.m), norm_inf(q.sh, q.a(W_AXV), q.m));
+    const double eps_prim = eps_abs + eps_rel * mr;
+    if (q.sh.prim_res < eps_prim)
+      prim_ok = true;
+    else
+      prim_inf = primal_infeasible(q, eps_pi);
+  }
+  double mr;
+  if (sc)
+  {
+    const double* DI = q.a(W_DI);
+    mr = scaled_norm_inf(q.sh, DI, q.a(W_Q), q.n);
+    mr = fmax(mr, scaled_norm_inf(q.sh, DI, q.a(W_ATY), q.n));
+    mr = fmax(mr, scaled_norm_inf(q.sh, DI, q.a(W_PXV), q.n));
+    mr *= q.sh.cinv;
+  }
+  else
+    mr = fmax(fmax(norm_inf(q.sh, q.a(W_Q), q.n), norm_inf(q.sh, q.a(W_ATY), q.n)), norm_inf(q.sh, q.a(W_PXV), q.n));
+  const double eps_dual = eps_abs + eps_rel * mr;
+  if (q.sh.dual_res < eps_dual)
+    dual_ok = true;
+  else
+    dual_inf = dual_infeasible(q, eps_di);
+  int st = 0;
+  if (prim_ok && dual_ok)
+    st = approximate ? SOLVED_INACCURATE : SOLVED;
+  else if (prim_inf)
+    st = approximate ? PRIMAL_INFEASIBLE_INACCURATE : PRIMAL_INFEASIBLE;
+  else if (dual_inf)
+    st = approximate ? DUAL_INFEASIBLE_INACCURATE : DUAL_INFEASIBLE;
+  __syncthreads();
+  if (threadIdx.x == 0 && st)
+    q.sh.status = st;
+  __syncthreads();
+  return st != 0;
+}
+
+// adaptive rho: estimate, and refactor when it moved by more than the tolerance.
+// Returns false when the refactorisation is not quasi-definite (OSQP_NON_CVX).
+__device__ bool adapt_rho(Qp& q)
+{
+  double pr = norm_inf(q.sh, q.a(W_RP), q.m);
+  double dr = norm_inf(q.sh, q.a(W_RD), q.n);
+  const double prn = fmax(norm_inf(q.sh, q.a(W_Z), q.m), norm_inf(q.sh, q.a(W_AXV), q.m));
+  pr /= (prn + kDivTol);
+  double drn = fmax(norm_inf(q.sh, q.a(W_Q), q.n), norm_inf(q.sh, q.a(W_ATY), q.n));
+  drn = fmax(drn, norm_inf(q.sh, q.a(W_PXV), q.n));
+  dr /= (drn + kDivTol);
+  double est = q.sh.rho * sqrt(pr / (dr + kDivTol));
+  est = fmin(fmax(est, kRhoMin), kRhoMax);
+  if (!(est > q.sh.rho * q.s.adaptive_rho_tolerance || est < q.sh.rho / q.s.adaptive_rho_tolerance))
+    return true;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    q.sh.rho = fmin(fmax(est, kRhoMin), kRhoMax);
+  __syncthreads();
+  double *RHO = q.a(W_RHO), *RHOI = q.a(W_RHOI), *CT = q.a(W_CT);
+  QFOR(r, q.m)
+  {
+    if (CT[r] == 0.0)
+    {
+      RHO[r] = q.sh.rho;
+      RHOI[r] = 1.0 / q.sh.rho;
+    }
+    else if (CT[r] == 1.0)
+    {
+      RHO[r] = kRhoEq * q.sh.rho;
+      RHOI[r] = 1.0 / RHO[r];
+    }
+  }
+  __syncthreads();
+  build_kkt(q);
+  ldl_factor(q, q.a(W_K), q.a(W_KT), q.n + q.m);
+  return !q.sh.fail && q.sh.npos >= q.n;
+}
+
+__device__ void polish(Qp& q)
+{
+  const int n = q.n, m = q.m;
+  double *Z = q.a(W_Z), *Y = q.a(W_Y), *L = q.a(W_L), *U = q.a(W_U), *FLG = q.a(W_FLG), *RMAP = q.a(W_RMAP);
+  QFOR(r, m)
+  {
+    double f = 0;
+    if (Z[r] - L[r] < -Y[r])
+      f = -1;
+    else if (U[r] - Z[r] < Y[r])
+      f = 1;
+    FLG[r] = f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+  {
+    int k = 0;
+    for (int r = 0; r < m; ++r)
+      RMAP[r] = (FLG[r] != 0.0) ? k++ : -1;
+    q.sh.nred = k;
+  }
+  __syncthreads();
+  const int mred = q.sh.nred, N = n + mred;
+  // reduced KKT [P + delta I, Ared'; Ared, -delta I]
+  double *K = q.a(W_K), *KT = q.a(W_KT), *PX = q.a(W_PX), *AX = q.a(W_AX);
+  const long long NN = (long long)N * N;
+  for (long long e = threadIdx.x; e < NN; e += kQB)
+    K[e] = 0.0;
+  __syncthreads();
+  QFOR(j, n)
+  for (int e = q.p.Pp[j]; e < q.p.Pp[j + 1]; ++e)
+    K[(long long)j * N + q.p.Pi[e]] = PX[e];
+  QFOR(j, n)
+  for (int e = q.p.Ap[j]; e < q.p.Ap[j + 1]; ++e)
+  {
+    const int k = static_cast<int>(RMAP[q.p.Ai[e]]);
+    if (k >= 0)
+      K[(long long)(n + k) * N + j] = AX[e];
+  }
+  __syncthreads();
+  QFOR(j, n) K[(long long)j * N + j] += q.s.delta;
+  QFOR(k, mred) K[(long long)(n + k) * N + (n + k)] = -q.s.delta;
+  __syncthreads();
+  ldl_factor(q, K, KT, N);
+  if (q.sh.fail || q.sh.npos < n)
+  {
+    if (threadIdx.x == 0)
+      q.sh.polish = -1;
+    __syncthreads();
+    return;
+  }
+  double *RHS = q.a(W_RHS), *RES = q.a(W_RES), *Q = q.a(W_Q), *T1 = q.a(W_T1), *T2 = q.a(W_T2);
+  double* v = q.lv;
+  QFOR(j, n) RHS[j] = -Q[j];
+  QFOR(r, m)
+  {
+    const int k = static_cast<int>(RMAP[r]);
+    if (k >= 0)
+      RHS[n + k] = (FLG[r] < 0) ? L[r] : U[r];
+  }
+  __syncthreads();
+  QFOR(i, N) v[i] = RHS[i];
+  ldl_solve(q, K, KT, N, v);
+  double* SOL = q.a(W_RD) /* n */;
+  double* SOLY = q.a(W_RP) /* >= mred */;
+  QFOR(j, n) SOL[j] = v[j];
+  QFOR(k, mred) SOLY[k] = v[n + k];
+  __syncthreads();
+  for (int itr = 0; itr < q.s.polish_refine_iter; ++itr)
+  {
+    // RES = RHS - [P, Ared'; Ared, 0] sol
+    p_mul(q, SOL, T1);
+    QFOR(j, n)
+    {
+      double t = 0;
+      for (int e = q.p.Ap[j]; e < q.p.Ap[j + 1]; ++e)
+      {
+        const int k = static_cast<int>(RMAP[q.p.Ai[e]]);
+        if (k >= 0)
+          t += AX[e] * SOLY[k];
+      }
+      T2[j] = t;
+    }
+    QFOR(r, m)
+    {
+      const int k = static_cast<int>(RMAP[r]);
+      if (k >= 0)
+      {
+        double t = 0;
+        for (int e = q.p.Arp[r]; e < q.p.Arp[r + 1]; ++e)
+          t += AX[q.p.Armap[e]] * SOL[q.p.Arj[e]];
+        RES[n + k] = RHS[n + k] - t;
+      }
+    }
+    __syncthreads();
+    QFOR(j, n) RES[j] = (RHS[j] - T1[j]) - T2[j];
+    __syncthreads();
+    QFOR(i, N) v[i] = RES[i];
+    ldl_solve(q, K, KT, N, v);
+    QFOR(j, n) SOL[j] += v[j];
+    QFOR(k, mred) SOLY[k] += v[n + k];
+    __syncthreads();
+  }
+  double *PXS = q.a(W_PXS), *PZS = q.a(W_PZS), *PYS = q.a(W_PYS);
+  QFOR(j, n) PXS[j] = SOL[j];
+  __syncthreads();
+  a_mul(q, PXS, PZS);
+  __syncthreads();
+  QFOR(r, m)
+  {
+    const int k = static_cast<int>(RMAP[r]);
+    const double py = (k >= 0) ? SOLY[k] : 0.0;
+    const double t = PZS[r] + py;
+    PZS[r] = fmin(fmax(t, L[r]), U[r]);
+    PYS[r] = t - PZS[r];
+  }
+  __syncthreads();
+  const double pr0 = q.sh.prim_res, dr0 = q.sh.dual_res;
+  const double pp = (m > 0) ? prim_res(q, PXS, PZS) : 0.0;
+  const double pd = dual_res(q, PXS, PYS);
+  const bool ok = (pp < pr0 && pd < dr0) || (pp < pr0 && dr0 < 1e-10) || (pd < dr0 && pr0 < 1e-10);
+  __syncthreads();
+  if (ok)
+  {
+    double *X = q.a(W_X);
+    QFOR(j, n) X[j] = PXS[j];
+    QFOR(r, m)
+    {
+      Z[r] = PZS[r];
+      Y[r] = PYS[r];
+    }
+  }
+  if (threadIdx.x == 0)
+  {
+    q.sh.polish = ok ? 1 : -1;
+    if (ok)
+    {
+      q.sh.prim_res = pp;
+      q.sh.dual_res = pd;
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kQB) void qp_csc_kernel(QpArgs args)
+{
+  extern __shared__ double lv[];
+  __shared__ Sh sh;
+  const int b = blockIdx.x;
+  if (b >= args.batch)
+    return;
+  const QpPattern& P = args.pat;
+  const int n = P.n, m = P.m;
+  Qp q{ P, args.s, args.ws + (long long)b * P.stride, sh, lv, n, m };
+  // data (scaled in place)
+  {
+    double *PX = q.a(W_PX), *AX = q.a(W_AX), *Q = q.a(W_Q), *L = q.a(W_L), *U = q.a(W_U);
+    QFOR(e, P.nnz_p) PX[e] = args.Pv[(long long)b * P.nnz_p + e];
+    QFOR(e, P.nnz_a) AX[e] = args.Av[(long long)b * P.nnz_a + e];
+    QFOR(j, n) Q[j] = args.qv[(long long)b * n + j];
+    QFOR(r, m)
+    {
+      L[r] = args.lv[(long long)b * m + r];
+      U[r] = args.uv[(long long)b * m + r];
+    }
+  }
+  if (threadIdx.x == 0)
+  {
+    sh.c = sh.cinv = 1.0;
+    sh.rho = args.rho_ws ? args.rho_ws[b] : args.s.rho;
+    sh.rho = fmin(fmax(sh.rho, kRhoMin), kRhoMax);
+    sh.status = UNSOLVED;
+    sh.polish = 0;
+    sh.iter = 0;
+    sh.prim_res = sh.dual_res = 0;
+  }
+  __syncthreads();
+  if (args.s.scaling > 0)
+    scale_data(q);
+  else
+  {
+    QFOR(j, n) q.a(W_D)[j] = q.a(W_DI)[j] = 1.0;
+    QFOR(r, m) q.a(W_E)[r] = q.a(W_EI)[r] = 1.0;
+    __syncthreads();
+  }
+  set_rho_vec(q);
+  build_kkt(q);
+  ldl_factor(q, q.a(W_K), q.a(W_KT), n + m);
+  thip_qp_info* info = args.info + b;
+  if (q.sh.fail || q.sh.npos < n)
+  {
+    // osqp_setup fails: OSQP_LINSYS_SOLVER_INIT_ERROR / OSQP_NONCVX_ERROR
+    if (threadIdx.x == 0)
+    {
+      info->status = -1;
+      info->setup_error = q.sh.fail ? 4 : 5;
+      info->polish_status = 0;
+      info->iter = 0;
+      info->rho = sh.rho;
+      info->prim_res = info->dual_res = 0;
+    }
+    return;
+  }
+  double *X = q.a(W_X), *XP = q.a(W_XP), *Z = q.a(W_Z), *ZP = q.a(W_ZP), *Y = q.a(W_Y), *DX = q.a(W_DX),
+         *DY = q.a(W_DY), *XT = q.a(W_XT), *Q = q.a(W_Q), *L = q.a(W_L), *U = q.a(W_U), *RHO = q.a(W_RHO),
+         *RHOI = q.a(W_RHOI);
+  // warm start (osqp_warm_start: x / D, y / E * c, z = A x) or cold start
+  if (args.x_ws && args.y_ws)
+  {
+    const double *DI = q.a(W_DI), *EI = q.a(W_EI);
+    const bool sc = args.s.scaling > 0;
+    QFOR(j, n) X[j] = sc ? args.x_ws[(long long)b * n + j] * DI[j] : args.x_ws[(long long)b * n + j];
+    QFOR(r, m) Y[r] = sc ? (args.y_ws[(long long)b * m + r] * EI[r]) * sh.c : args.y_ws[(long long)b * m + r];
+    __syncthreads();
+    a_mul(q, X, Z);
+  }
+  else
+  {
+    QFOR(j, n) X[j] = 0.0;
+    QFOR(r, m) Z[r] = Y[r] = 0.0;
+  }
+  __syncthreads();
+  int interval = args.s.adaptive_rho_interval;
+  if (args.s.adaptive_rho == 1 && interval == 0)
+    interval = args.s.check_termination ? 4 * args.s.check_termination : 100;
+  const int N = n + m;
+  const double alpha = args.s.alpha, sigma = args.s.sigma;
+  bool can_check = false;
+  bool noncvx = false;
+  int it;
+  for (it = 1; it <= args.s.max_iter; ++it)
+  {
+    // (x_prev, z_prev) <- (x, z): OSQP swaps the buffers; x and z are overwritten below
+    QFOR(j, n) XP[j] = X[j];
+    QFOR(r, m) ZP[r] = Z[r];
+    __syncthreads();
+    QFOR(j, n) XT[j] = sigma * XP[j] - Q[j];
+    QFOR(r, m) XT[n + r] = ZP[r] - RHOI[r] * Y[r];
+    __syncthreads();
+    QFOR(i, N) lv[i] = XT[i];
+    ldl_solve(q, q.a(W_K), q.a(W_KT), N, lv);
+    QFOR(j, n) XT[j] = lv[j];
+    QFOR(r, m) XT[n + r] += RHOI[r] * lv[n + r];
+    __syncthreads();
+    QFOR(j, n)
+    {
+      X[j] = alpha * XT[j] + (1.0 - alpha) * XP[j];
+      DX[j] = X[j] - XP[j];
+    }
+    QFOR(r, m)
+    {
+      double zr = RHOI[r] * Y[r];
+      zr = zr + alpha * XT[n + r];
+      zr = zr + (1.0 - alpha) * ZP[r];
+      Z[r] = fmin(fmax(zr, L[r]), U[r]);
+      DY[r] = RHO[r] * (alpha * XT[n + r] + (1.0 - alpha) * ZP[r] - Z[r]);
+      Y[r] += DY[r];
+    }
+    __syncthreads();
+    can_check = args.s.check_termination && (it % args.s.check_termination == 0);
+    const bool adapt_now = args.s.adaptive_rho && interval && (it % interval == 0);
+    bool done = false;
+    if (can_check || adapt_now)
+    {
+      const double pr = (m > 0) ? prim_res(q, X, Z) : 0.0;
+      const double dr = dual_res(q, X, Y);
+      if (threadIdx.x == 0)
+      {
+        sh.iter = it;
+        sh.prim_res = pr;
+        sh.dual_res = dr;
+      }
+      __syncthreads();
+      if (can_check)
+        done = check_termination(q, false);
+      if (!done && adapt_now && !adapt_rho(q))
+      {
+        noncvx = true;
+        break;
+      }
+    }
+    if (done)
+      break;
+  }
+  if (noncvx)
+  {
+    if (threadIdx.x == 0)
+      sh.status = NON_CVX;
+    __syncthreads();
+  }
+  else
+  {
+    if (!can_check)
+    {
+      // the last iterate was not checked: compute and test it
+      const double pr = (m > 0) ? prim_res(q, X, Z) : 0.0;
+      const double dr = dual_res(q, X, Y);
+      if (threadIdx.x == 0)
+      {
+        sh.iter = it - 1;
+        sh.prim_res = pr;
+        sh.dual_res = dr;
+      }
+      __syncthreads();
+      check_termination(q, false);
+    }
+    if (sh.status == UNSOLVED && !check_termination(q, true))
+    {
+      if (threadIdx.x == 0)
+        sh.status = MAX_ITER_REACHED;
+      __syncthreads();
+    }
+    if (args.s.polishing && sh.status == SOLVED)
+      polish(q);
+  }
+  // store_solution (unscaled), NaN on infeasibility
+  const int st = sh.status;
+  const bool inf = st == PRIMAL_INFEASIBLE || st == PRIMAL_INFEASIBLE_INACCURATE || st == DUAL_INFEASIBLE ||
+                   st == DUAL_INFEASIBLE_INACCURATE;
+  const double *D = q.a(W_D), *E = q.a(W_E);
+  const bool sc = args.s.scaling > 0;
+  QFOR(j, n) args.x_out[(long long)b * n + j] = inf ? NAN : (sc ? D[j] * X[j] : X[j]);
+  QFOR(r, m) args.y_out[(long long)b * m + r] = inf ? NAN : (sc ? sh.cinv * (E[r] * Y[r]) : Y[r]);
+  if (threadIdx.x == 0)
+  {
+    info->status = st;
+    info->setup_error = 0;
+    info->polish_status = sh.polish;
+    info->iter = sh.iter;
+    info->rho = sh.rho;
+    info->prim_res = sh.prim_res;
+    info->dual_res = sh.dual_res;
+  }
+}
+}  // namespace thip_qp_dev
+
+using namespace thip_qp_dev;
+
+struct thip_qp
+{
+  int device = 0, batch = 0, n = 0, m = 0, nnz_p = 0, nnz_a = 0;
+  QpPattern pat{};
+  int* d_idx = nullptr;
+  double* d_ws = nullptr;
+  double *d_in = nullptr, *d_out = nullptr;
+  thip_qp_info* d_info = nullptr;
+  long long in_doubles = 0;
+  size_t lds = 0;
+  std::string err;
+};
+
+static std::string g_qp_create_err;
+
+extern "C" {
+
+int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_rowind, const int* A_colptr,
+                   const int* A_rowind, int batch, thip_qp** out)
+{
+  if (!out || n <= 0 || m < 0 || batch <= 0 || !P_colptr || !A_colptr)
+  {
+    g_qp_create_err = "thip_qp_create: bad arguments";
+    return THIP_E_INVALID;
+  }
+  if (n + m > THIP_QP_MAX_KKT)
+  {
+    g_qp_create_err = "thip_qp_create: n + m = " + std::to_string(n + m) + " exceeds THIP_QP_MAX_KKT (" +
+                      std::to_string(THIP_QP_MAX_KKT) + ")";
+    return THIP_E_INVALID;
+  }
+  const int np = P_colptr[n], na = A_colptr[n];
+  if (P_colptr[0] != 0 || A_colptr[0] != 0 || np < 0 || na < 0)
+  {
+    g_qp_create_err = "thip_qp_create: bad column pointers";
+    return THIP_E_INVALID;
+  }
+  for (int j = 0; j < n; ++j)
+  {
+    if (P_colptr[j + 1] < P_colptr[j] || A_colptr[j + 1] < A_colptr[j])
+    {
+      g_qp_create_err = "thip_qp_create: column pointers must not decrease";
+      return THIP_E_INVALID;
+    }
+    for (int e = P_colptr[j]; e < P_colptr[j + 1]; ++e)
+      if (P_rowind[e] < 0 || P_rowind[e] > j)
+      {
+        g_qp_create_err = "thip_qp_create: P must be upper triangular CSC";
+        return THIP_E_INVALID;
+      }
+    for (int e = A_colptr[j]; e < A_colptr[j + 1]; ++e)
+      if (A_rowind[e] < 0 || A_rowind[e] >= m)
+      {
+        g_qp_create_err = "thip_qp_create: A row index out of range";
+        return THIP_E_INVALID;
+      }
+  }
+  auto* q = new thip_qp();
+  q->device = device;
+  q->batch = batch;
+  q->n = n;
+  q->m = m;
+  q->nnz_p = np;
+  q->nnz_a = na;
+  // rows of P's upper triangle and of A (pattern -> value index maps)
+  std::vector<int> prp(n + 1, 0), prj(np), prm(np), arp(m + 1, 0), arj(na), arm(na);
+  for (int j = 0; j < n; ++j)
+    for (int e = P_colptr[j]; e < P_colptr[j + 1]; ++e)
+      prp[P_rowind[e] + 1]++;
+  for (int j = 0; j < n; ++j)
+    prp[j + 1] += prp[j];
+  {
+    std::vector<int> nx(prp.begin(), prp.end() - 1);
+    for (int j = 0; j < n; ++j)
+      for (int e = P_colptr[j]; e < P_colptr[j + 1]; ++e)
+      {
+        const int k = nx[P_rowind[e]]++;
+        prj[k] = j;
+        prm[k] = e;
+      }
+  }
+  for (int e = 0; e < na; ++e)
+    arp[A_rowind[e] + 1]++;
+  for (int r = 0; r < m; ++r)
+    arp[r + 1] += arp[r];
+  {
+    std::vector<int> nx(arp.begin(), arp.end() - 1);
+    for (int j = 0; j < n; ++j)
+      for (int e = A_colptr[j]; e < A_colptr[j + 1]; ++e)
+      {
+        const int k = nx[A_rowind[e]]++;
+        arj[k] = j;
+        arm[k] = e;
+      }
+  }
+  std::vector<int> idx;
+  auto push = [&](const int* v, int len) {
+    const size_t o = idx.size();
+    idx.insert(idx.end(), v, v + len);
+    idx.push_back(0);
+    return o;
+  };
+  const size_t oPp = push(P_colptr, n + 1), oPi = push(P_rowind, np), oPrp = push(prp.data(), n + 1),
+               oPrj = push(prj.data(), np), oPrm = push(prm.data(), np), oAp = push(A_colptr, n + 1),
+               oAi = push(A_rowind, na), oArp = push(arp.data(), m + 1), oArj = push(arj.data(), na),
+               oArm = push(arm.data(), na);
+  const long long N = n + m;
+  long long sizes[W_COUNT];
+  sizes[W_PX] = std::max(np, 1);
+  sizes[W_AX] = std::max(na, 1);
+  sizes[W_Q] = sizes[W_D] = sizes[W_DI] = sizes[W_TD] = sizes[W_X] = sizes[W_XP] = sizes[W_DX] = n;
+  sizes[W_PXV] = sizes[W_ATY] = sizes[W_RD] = sizes[W_T1] = sizes[W_PXS] = n;
+  const long long mm = std::max(m, 1);
+  sizes[W_L] = sizes[W_U] = sizes[W_E] = sizes[W_EI] = sizes[W_TE] = sizes[W_RHO] = sizes[W_RHOI] = sizes[W_CT] = mm;
+  sizes[W_Z] = sizes[W_ZP] = sizes[W_Y] = sizes[W_DY] = sizes[W_AXV] = sizes[W_RP] = sizes[W_T2] = mm;
+  sizes[W_PZS] = sizes[W_PYS] = sizes[W_FLG] = sizes[W_RMAP] = mm;
+  sizes[W_XT] = sizes[W_RHS] = sizes[W_RES] = N;
+  sizes[W_K] = sizes[W_KT] = N * N;
+  long long off = 0;
+  for (int k = 0; k < W_COUNT; ++k)
+  {
+    q->pat.off[k] = off;
+    off += (sizes[k] + 31) / 32 * 32;
+  }
+  q->pat.stride = off;
+  q->pat.n = n;
+  q->pat.m = m;
+  q->pat.nnz_p = np;
+  q->pat.nnz_a = na;
+  q->pat.N = static_cast<int>(N);
+  q->in_doubles = (long long)np + na + n + 2LL * m;
+  q->lds = static_cast<size_t>(N) * sizeof(double);
+  auto fail = [&](const std::string& msg) {
+    g_qp_create_err = msg;
+    thip_qp_destroy(q);
+    return THIP_E_HIP;
+  };
+  hipError_t e;
+  if ((e = hipSetDevice(device)) != hipSuccess)
+    return fail(std::string("hipSetDevice: ") + hipGetErrorString(e));
+  if ((e = hipMalloc(&q->d_idx, idx.size() * sizeof(int))) != hipSuccess ||
+      (e = hipMalloc(&q->d_ws, static_cast<size_t>(q->pat.stride) * batch * sizeof(double))) != hipSuccess ||
+      (e = hipMalloc(&q->d_in, static_cast<size_t>(q->in_doubles + 2LL * n + m + 1) * batch * sizeof(double))) !=
+          hipSuccess ||
+      (e = hipMalloc(&q->d_out, static_cast<size_t>(n + m) * batch * sizeof(double))) != hipSuccess ||
+      (e = hipMalloc(&q->d_info, sizeof(thip_qp_info) * batch)) != hipSuccess)
+    return fail(std::string("hipMalloc: ") + hipGetErrorString(e));
+  if ((e = hipMemcpy(q->d_idx, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)
+    return fail(std::string("hipMemcpy: ") + hipGetErrorString(e));
+  q->pat.Pp = q->d_idx + oPp;
+  q->pat.Pi = q->d_idx + oPi;
+  q->pat.Prp = q->d_idx + oPrp;
+  q->pat.Prj = q->d_idx + oPrj;
+  q->pat.Prmap = q->d_idx + oPrm;
+  q->pat.Ap = q->d_idx + oAp;
+  q->pat.Ai = q->d_idx + oAi;
+  q->pat.Arp = q->d_idx + oArp;
+  q->pat.Arj = q->d_idx + oArj;
+  q->pat.Armap = q->d_idx + oArm;
+  *out = q;
+  return THIP_OK;
+}
+
+int thip_qp_solve(thip_qp* q, const double* P_values, const double* qvec, const double* A_values, const double* l,
+                  const double* u, const thip_osqp_settings* settings, const double* warm_x, const double* warm_y,
+                  const double* warm_rho, double* x, double* y, thip_qp_info* info)
+{
+  if (!q || !P_values || !qvec || !A_values || !l || !u || !settings || !x || !info)
+    return THIP_E_INVALID;
+  const int n = q->n, m = q->m, B = q->batch;
+  if (settings->max_iter < 1 || settings->check_termination < 0 || settings->scaling < 0 ||
+      !(settings->alpha > 0 && settings->alpha < 2) || !(settings->sigma > 0) || !(settings->rho > 0) ||
+      !(settings->delta > 0))
+  {
+    q->err = "thip_qp_solve: bad OSQP settings";
+    return THIP_E_INVALID;
+  }
+  // osqp_setup's validate_data: l <= u (a failing problem is reported, not solved)
+  std::vector<int> bad(static_cast<size_t>(B), 0);
+  for (int b = 0; b < B; ++b)
+    for (int r = 0; r < m; ++r)
+      if (!(l[(long long)b * m + r] <= u[(long long)b * m + r]))
+        bad[static_cast<size_t>(b)] = 1;
+  hipError_t e;
+  if ((e = hipSetDevice(q->device)) != hipSuccess)
+  {
+    q->err = std::string("hipSetDevice: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  // inputs packed into one device buffer
+  const size_t np = static_cast<size_t>(q->nnz_p) * B, na = static_cast<size_t>(q->nnz_a) * B;
+  const size_t nn = static_cast<size_t>(n) * B, mm = static_cast<size_t>(m) * B;
+  double* d = q->d_in;
+  double *dP = d, *dA = dP + np, *dq = dA + na, *dl = dq + nn, *du = dl + mm, *dxw = du + mm, *dyw = dxw + nn,
+         *drw = dyw + mm;
+  auto h2d = [&](double* dst, const double* src, size_t cnt) {
+    if (cnt && (e = hipMemcpy(dst, src, cnt * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+      return false;
+    return true;
+  };
+  const bool ws = warm_x && warm_y;
+  if (!h2d(dP, P_values, np) || !h2d(dA, A_values, na) || !h2d(dq, qvec, nn) || !h2d(dl, l, mm) || !h2d(du, u, mm) ||
+      (ws && (!h2d(dxw, warm_x, nn) || !h2d(dyw, warm_y, mm))) || (warm_rho && !h2d(drw, warm_rho, B)))
+  {
+    q->err = std::string("hipMemcpy: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  QpArgs a{};
+  a.pat = q->pat;
+  a.s = *settings;
+  a.Pv = dP;
+  a.Av = dA;
+  a.qv = dq;
+  a.lv = dl;
+  a.uv = du;
+  a.x_ws = ws ? dxw : nullptr;
+  a.y_ws = ws ? dyw : nullptr;
+  a.rho_ws = warm_rho ? drw : nullptr;
+  a.x_out = q->d_out;
+  a.y_out = q->d_out + nn;
+  a.info = q->d_info;
+  a.ws = q->d_ws;
+  a.batch = B;
+  hipLaunchKernelGGL(qp_csc_kernel, dim3(B), dim3(kQB), q->lds, nullptr, a);
+  if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess)
+  {
+    q->err = std::string("qp_csc_kernel: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  std::vector<thip_qp_info> hinfo(static_cast<size_t>(B));
+  if ((e = hipMemcpy(x, q->d_out, nn * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess ||
+      (y && m && (e = hipMemcpy(y, q->d_out + nn, mm * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess) ||
+      (e = hipMemcpy(hinfo.data(), q->d_info, sizeof(thip_qp_info) * B, hipMemcpyDeviceToHost)) != hipSuccess)
+  {
+    q->err = std::string("hipMemcpy: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  for (int b = 0; b < B; ++b)
+  {
+    info[b] = hinfo[static_cast<size_t>(b)];
+    if (bad[static_cast<size_t>(b)])
+    {
+      info[b].status = -1;
+      info[b].setup_error = 1;  // OSQP_DATA_VALIDATION_ERROR
+    }
+  }
+  return THIP_OK;
+}
+
+void thip_qp_destroy(thip_qp* q)
+{
+  if (!q)
+    return;
+  hipFree(q->d_idx);
+  hipFree(q->d_ws);
+  hipFree(q->d_in);
+  hipFree(q->d_out);
+  hipFree(q->d_info);
+  delete q;
+}
+
+const char* thip_qp_last_error(thip_qp* q) { return q ? q->err.c_str() : g_qp_create_err.c_str(); }
+
+}  // extern "C"

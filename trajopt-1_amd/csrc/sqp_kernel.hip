@@ -78,6 +78,10 @@ struct Ctl
   int flag;
   int can_check;
   int time_up;  // the max_time check of this SQP iteration fired
+  // OSQPModel sparsity fingerprint of the last QP setup (pattern_fingerprint)
+  unsigned long long fp_hash;
+  int fp_n, fp_m;
+  long long fp_nnz;
   // diagnostics
   double* trace;
   int trace_cap, trace_n;
@@ -4717,6 +4721,95 @@ __device__ void plan_lds_dynamic(Ctx& c)
 // ======================================================================
 // The SQP driver kernel: BasicTrustRegionSQP::optimize per workgroup
 // ======================================================================
+// OSQPModel's sparsity test (osqp_interface.cpp:199-201, 268-271, quirk Q2):
+// the constraint matrix A counts as unchanged when n, m and nnz are equal and
+// the first n + 1 BYTES of its 64-bit column pointers and the first nnz BYTES
+// of its 64-bit row indices are equal -- a byte count used as an element
+// count, so only a prefix of the pattern (about the first n / 8 column pointers
+// and nnz / 8 row indices: the early waypoints) is ever compared.  This walks
+// A in OSQPModel's CSC order (x columns waypoint-major, then the aux columns
+// of the abs rows, then the hinge columns; rows fixed < abs < hinge < the
+// identity block) and hashes exactly the compared prefix, byte-masked where a
+// count ends inside a 64-bit element.  Thread 0 of the workgroup; the result is
+// (n, m, nnz, hash) in the control block's fp_* fields.
+__device__ __forceinline__ unsigned long long fp_mix(unsigned long long h, unsigned long long v)
+{
+  h ^= v + 0x9E3779B97F4A7C15ULL + (h << 6) + (h >> 2);
+  return h * 0xBF58476D1CE4E5B9ULL;
+}
+
+__device__ void pattern_fingerprint(Ctx& c, unsigned long long& hash, int& n_out, int& m_out, long long& nnz_out)
+{
+  const Layout& L = c.L;
+  const int D = L.D, nx = L.nx, nh = c.s->n_h, n = c.nc();
+  const int *mask = c.ia(I_MASK), *HP = c.ia(I_HPTR), *HM = c.ia(I_HMASK);
+  const int* fos = c.T.fixed_of_step;
+  long long nnz = (long long)L.n_fixed_rows + 2LL * L.n_abs + nh + n;
+  for (int r = 0; r < L.n_abs; ++r)
+    nnz += __popc(mask[r]);
+  for (int h = 0; h < nh; ++h)
+    nnz += __popc(HM[h]);
+  const long long row_hinge0 = L.n_rows, row_ident0 = (long long)L.n_rows + nh;
+  // byte prefixes: p[0..(n+1)/8) whole + (n+1)%8 low bytes of the next; same for i with nnz
+  const long long kp = (n + 1) / 8, kpr = (n + 1) % 8, ki = nnz / 8, kir = nnz % 8;
+  auto low = [](unsigned long long v, long long bytes) {
+    return bytes >= 8 ? v : (v & ((1ULL << (8 * bytes)) - 1ULL));
+  };
+  unsigned long long h = 0x6A09E667F3BCC908ULL;
+  long long ptr = 0, e = 0;  // column pointer value, entry counter
+  auto entry = [&](long long row) {
+    if (e < ki)
+      h = fp_mix(h, (unsigned long long)row);
+    else if (e == ki && kir)
+      h = fp_mix(h, low((unsigned long long)row, kir) ^ 0x5555ULL);
+    ++e;
+  };
+  for (int col = 0; col <= n; ++col)
+  {
+    if (col < kp)
+      h = fp_mix(h, (unsigned long long)ptr);
+    else if (col == kp && kpr)
+      h = fp_mix(h, low((unsigned long long)ptr, kpr) ^ 0xAAAAULL);
+    if (col == n || (col >= kp && e > ki))
+      break;
+    const long long e0 = e;
+    if (col < nx)
+    {
+      const int t = col / D, j = col % D;
+      if (fos[t] >= 0)
+        entry((long long)fos[t] * D + j);
+      for (int q = c.T.step_ptr[t]; q < c.T.step_ptr[t + 1]; ++q)
+      {
+        const int r = c.T.step_rows[q];
+        if ((mask[r] >> j) & 1)
+          entry(L.n_fixed_rows + r);
+      }
+      if (L.hinge)
+      {
+        // hinge rows of step pair t - 1 (waypoint t is its second half) then of pair t
+        if (t > 0)
+          for (int hh = HP[t - 1]; hh < HP[t]; ++hh)
+            if ((HM[hh] >> (D + j)) & 1)
+              entry(row_hinge0 + hh);
+        if (t < L.N - 1)
+          for (int hh = HP[t]; hh < HP[t + 1]; ++hh)
+            if ((HM[hh] >> j) & 1)
+              entry(row_hinge0 + hh);
+      }
+    }
+    else if (col < L.nc_base)
+      entry(L.n_fixed_rows + (col - nx) / 2);  // neg / pos of abs row (col - nx) / 2
+    else
+      entry(row_hinge0 + (col - L.nc_base));   // the hinge variable of hinge row col - nc_base
+    entry(row_ident0 + col);                    // identity block (variable bounds)
+    ptr += e - e0;
+  }
+  hash = h;
+  n_out = n;
+  m_out = c.m();
+  nnz_out = nnz;
+}
+
 __device__ void sqp_optimize(Ctx& c, Solver& sv)
 {
   PROF(13);
@@ -4801,24 +4894,23 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
       if (L.hinge)
         plan_lds_dynamic(c);
       build_and_scale(c);
-      // pattern of A (jacobian drops) vs previous QP setup
-      double diff[1] = { 0 };
-      FOR(r, L.n_abs) if (mask[r] != pmask[r]) diff[0] = 1.0;
-      if (L.hinge)
+      // pattern of A vs the previous QP setup, as OSQPModel tests it (quirk Q2)
+      BSYNC();
+      if (c.tid == 0)
       {
-        // hinge rows: same count, start steps and kept coefficients
-        // (OSQPModel compares the CSC pattern of A bytewise)
-        const int nh = c.s->n_h;
-        if (nh != c.s->n_h_prev)
-          diff[0] = 1.0;
-        else
-        {
-          const int *HT = c.ia(I_HT), *HM = c.ia(I_HMASK), *PHT = c.ia(I_PHT), *PHM = c.ia(I_PHMASK);
-          FOR(h, nh) if (HT[h] != PHT[h] || HM[h] != PHM[h]) diff[0] = 1.0;
-        }
+        unsigned long long fh;
+        int fn, fm;
+        long long fz;
+        pattern_fingerprint(c, fh, fn, fm, fz);
+        c.s->flag = (fn == c.s->fp_n && fm == c.s->fp_m && fz == c.s->fp_nnz && fh == c.s->fp_hash) ? 1 : 0;
+        c.s->fp_n = fn;
+        c.s->fp_m = fm;
+        c.s->fp_nnz = fz;
+        c.s->fp_hash = fh;
       }
-      block_max<1>(c, diff);
-      bool pattern_equal = have_prev_setup && diff[0] == 0.0;
+      BSYNC();
+      bool pattern_equal = have_prev_setup && c.s->flag == 1;
+      BSYNC();
       FOR(r, L.n_abs) pmask[r] = mask[r];
       if (L.hinge)
       {
