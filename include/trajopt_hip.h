@@ -56,6 +56,7 @@ extern "C" {
 #define THIP_MAX_PRIMS 16
 #define THIP_MAX_JPOS 8
 #define THIP_MAX_JVX 4
+#define THIP_MAX_JDT 8
 #define THIP_MAX_CONTACTS 131072
 
 /* error codes */
@@ -248,6 +249,25 @@ typedef struct thip_problem_desc {
   double jvx_targets[THIP_MAX_JVX][THIP_MAX_DOF];
   double jvx_upper_tols[THIP_MAX_JVX][THIP_MAX_DOF];
   double jvx_lower_tols[THIP_MAX_JVX][THIP_MAX_DOF];
+
+  /* Joint-derivative terms the fused sqp_kernel does not lower (the generic
+   * path runs them: sco::BasicTrustRegionSQP on the host with the GpuModel):
+   * order 1 JointVelEqConstraint (trajectory_costs.cpp:376-424), order 2
+   * JointAcc{Eq,Ineq}{Cost,Constraint} (:502-753), order 3 JointJerk (:756-1016),
+   * zero tolerances -> Eq forms.  Steps after the hatch clamping
+   * (problem_description.cpp:1412-1533, 1534-1640).  Costs follow every other
+   * cost term but collision, constraints every other constraint but collision.
+   * thip_create rejects a descriptor with n_jdt > 0; it is the lowered record
+   * the oracle reads. */
+  int n_jdt;
+  int jdt_order[THIP_MAX_JDT];
+  int jdt_is_cnt[THIP_MAX_JDT];
+  int jdt_first_step[THIP_MAX_JDT];
+  int jdt_last_step[THIP_MAX_JDT];
+  double jdt_coeffs[THIP_MAX_JDT][THIP_MAX_DOF];
+  double jdt_targets[THIP_MAX_JDT][THIP_MAX_DOF];
+  double jdt_upper_tols[THIP_MAX_JDT][THIP_MAX_DOF];
+  double jdt_lower_tols[THIP_MAX_JDT][THIP_MAX_DOF];
 
   /* CollisionTermInfo, LVS_DISCRETE or LVS_CONTINUOUS, cost or constraint
    * (collision_terms.cpp:737-1161,1267-1386):

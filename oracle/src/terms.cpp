@@ -538,6 +538,264 @@ Mat CartPoseCalc::jac(const DblVec& q) const
   return J;
 }
 
+// ------------------------------------------------------------ JointVel cnt / JointAcc / JointJerk
+// JointVelEqConstraint (trajectory_costs.cpp:376-424), JointAcc{Eq,Ineq}{Cost,
+// Constraint} (:502-753), JointJerk{...} (:756-1016): the k-th forward difference
+// of the trajectory (stencils [-1 1], [1 -2 1], [-1 3 -3 1], expressions built in
+// the ctors' exprInc order), minus the target, per (step, joint), i-major.
+// value(): Eigen's diffAxis0 applied k times (repeated differences), summed
+// column-major.
+struct JointDiffData
+{
+  std::vector<VarVector> rows;
+  DblVec coeffs, targets, upper, lower;
+  int order = 2, first = 0, last = 0;
+  static const double* stencil(int order)
+  {
+    static const double s1[] = { -1, 1 }, s2[] = { 1, -2, 1 }, s3[] = { -1, 3, -3, 1 };
+    return order == 1 ? s1 : order == 2 ? s2 : s3;
+  }
+  int count() const { return last - order - first + 1; }  // steps i = first .. last - order
+  AffExpr diffExpr(int i, std::size_t j) const
+  {
+    AffExpr d;
+    const double* st = stencil(order);
+    for (int k = 0; k <= order; ++k)
+      exprInc(d, exprMult(rows[static_cast<std::size_t>(i + k)][j], st[k]));
+    exprDec(d, targets[j]);
+    return d;
+  }
+  // (diffAxis0^order(traj block) - targets)[i - first][j]
+  double diffValue(const DblVec& x, int i, std::size_t j) const
+  {
+    double v[4];
+    for (int k = 0; k <= order; ++k)
+      v[k] = rows[static_cast<std::size_t>(i + k)][j].value(x);
+    for (int o = 0; o < order; ++o)
+      for (int k = 0; k < order - o; ++k)
+        v[k] = v[k + 1] - v[k];
+    return v[0] - targets[j];
+  }
+  AffExprVector ineqExprs() const
+  {
+    AffExprVector out;
+    for (int i = first; i <= last - order; ++i)
+      for (std::size_t j = 0; j < coeffs.size(); ++j)
+      {
+        const AffExpr d = diffExpr(i, j);
+        AffExpr up, lo;
+        exprInc(up, upper[j]);  // -(upper_tol - (d - targ)) * coeff
+        exprDec(up, d);
+        exprScale(up, -coeffs[j]);
+        out.push_back(up);
+        exprInc(lo, lower[j]);  // (lower_tol - (d - targ)) * coeff
+        exprDec(lo, d);
+        exprScale(lo, coeffs[j]);
+        out.push_back(lo);
+      }
+    return out;
+  }
+  VarVector vars() const
+  {
+    VarVector v;
+    for (auto& r : rows)
+      v.insert(v.end(), r.begin(), r.end());
+    return v;
+  }
+  void check(const char* what) const
+  {
+    if (((last - order) - first) < 0)
+      throw std::runtime_error(std::string(what) + ", trajectory is too short!");
+  }
+};
+
+class JointDiffEqCost : public Cost
+{
+public:
+  explicit JointDiffEqCost(JointDiffData d) : Cost(d.order == 2 ? "JointAccEq" : "JointJerkEq"), d_(std::move(d))
+  {
+    d_.check(d_.order == 2 ? "JointAccEqCost" : "JointJerkEqCost");
+    for (int i = d_.first; i <= d_.last - d_.order; ++i)
+      for (std::size_t j = 0; j < d_.coeffs.size(); ++j)
+        exprInc(expr_, exprMult(exprSquare(d_.diffExpr(i, j)), d_.coeffs[j]));
+  }
+  double value(const DblVec& x) override
+  {
+    double s = 0;
+    for (std::size_t j = 0; j < d_.coeffs.size(); ++j)
+      for (int i = d_.first; i <= d_.last - d_.order; ++i)
+      {
+        const double v = d_.diffValue(x, i, j);
+        s += (v * v) * d_.coeffs[j];
+      }
+    return s;
+  }
+  ConvexObjective::Ptr convex(const DblVec&, Model* model) override
+  {
+    auto out = std::make_shared<ConvexObjective>(model);
+    out->addQuadExpr(expr_);
+    return out;
+  }
+  VarVector getVars() override { return d_.vars(); }
+
+private:
+  JointDiffData d_;
+  QuadExpr expr_;
+};
+
+// hinge form: upper/lower rows; value sums pospart of both blocks column-major
+class JointDiffIneqCost : public Cost
+{
+public:
+  explicit JointDiffIneqCost(JointDiffData d) : Cost(d.order == 2 ? "JointAccIneq" : "JointJerkIneq"), d_(std::move(d))
+  {
+    d_.check(d_.order == 2 ? "JointAccIneqCost" : "JointJerkIneqCost");
+    exprs_ = d_.ineqExprs();
+  }
+  double value(const DblVec& x) override
+  {
+    double s1 = 0, s2 = 0;
+    for (std::size_t j = 0; j < d_.coeffs.size(); ++j)
+      for (int i = d_.first; i <= d_.last - d_.order; ++i)
+      {
+        const double v = d_.diffValue(x, i, j);
+        s1 += std::fmax((v - d_.upper[j]) * d_.coeffs[j], 0.0);
+      }
+    for (std::size_t j = 0; j < d_.coeffs.size(); ++j)
+      for (int i = d_.first; i <= d_.last - d_.order; ++i)
+      {
+        const double v = d_.diffValue(x, i, j);
+        s2 += std::fmax(((v * -1) + d_.lower[j]) * d_.coeffs[j], 0.0);
+      }
+    return s1 + s2;
+  }
+  ConvexObjective::Ptr convex(const DblVec&, Model* model) override
+  {
+    auto out = std::make_shared<ConvexObjective>(model);
+    for (const AffExpr& e : exprs_)
+      out->addHinge(e, 1);
+    return out;
+  }
+  VarVector getVars() override { return d_.vars(); }
+  const AffExprVector& exprs() const { return exprs_; }
+  DblVec values(const DblVec& x) const
+  {
+    // [diff1 | diff2] flattened column-major, pospart (the IneqConstraint value)
+    DblVec out;
+    for (int blk = 0; blk < 2; ++blk)
+      for (std::size_t j = 0; j < d_.coeffs.size(); ++j)
+        for (int i = d_.first; i <= d_.last - d_.order; ++i)
+        {
+          const double v = d_.diffValue(x, i, j);
+          const double e = blk == 0 ? (v - d_.upper[j]) * d_.coeffs[j] : ((v * -1) + d_.lower[j]) * d_.coeffs[j];
+          out.push_back(std::fmax(e, 0.0));
+        }
+    return out;
+  }
+
+private:
+  JointDiffData d_;
+  AffExprVector exprs_;
+};
+
+class JointDiffEqConstraint : public Constraint
+{
+public:
+  explicit JointDiffEqConstraint(JointDiffData d)
+    : Constraint(d.order == 1 ? "JointVelEq" : d.order == 2 ? "JointAccEq" : "JointJerkEq"), d_(std::move(d))
+  {
+    d_.check(d_.order == 1 ? "JointVelEqConstraint" : d_.order == 2 ? "JointAccEqConstraint" : "JointJerkEqConstraint");
+    for (int i = d_.first; i <= d_.last - d_.order; ++i)
+      for (std::size_t j = 0; j < d_.coeffs.size(); ++j)
+        exprs_.push_back(exprMult(d_.diffExpr(i, j), d_.coeffs[j]));
+  }
+  ConstraintType type() override { return EQ; }
+  // quirk Q3: the value is the SQUARED difference times the coefficient (column-major)
+  DblVec value(const DblVec& x) override
+  {
+    DblVec out;
+    for (std::size_t j = 0; j < d_.coeffs.size(); ++j)
+      for (int i = d_.first; i <= d_.last - d_.order; ++i)
+      {
+        const double v = d_.diffValue(x, i, j);
+        out.push_back((v * v) * d_.coeffs[j]);
+      }
+    return out;
+  }
+  ConvexConstraints::Ptr convex(const DblVec&, Model* model) override
+  {
+    auto out = std::make_shared<ConvexConstraints>(model);
+    for (const AffExpr& e : exprs_)
+      out->addEqCnt(e);
+    return out;
+  }
+  VarVector getVars() override { return d_.vars(); }
+
+private:
+  JointDiffData d_;
+  AffExprVector exprs_;
+};
+
+class JointDiffIneqConstraint : public Constraint
+{
+public:
+  explicit JointDiffIneqConstraint(JointDiffData d)
+    : Constraint(d.order == 2 ? "JointAccIneq" : "JointJerkIneq"), rows_(std::move(d))
+  {
+  }
+  ConstraintType type() override { return INEQ; }
+  DblVec value(const DblVec& x) override { return rows_.values(x); }
+  ConvexConstraints::Ptr convex(const DblVec&, Model* model) override
+  {
+    auto out = std::make_shared<ConvexConstraints>(model);
+    for (const AffExpr& e : rows_.exprs())
+      out->addIneqCnt(e);
+    return out;
+  }
+  VarVector getVars() override { return rows_.getVars(); }
+
+private:
+  JointDiffIneqCost rows_;
+};
+
+void addJointDiffTerm(TrajProblem& tp, const std::vector<VarVector>& rows, const thip_problem_desc& d, int k)
+{
+  const int D = d.chain.n_dof;
+  JointDiffData jd;
+  jd.rows = rows;
+  jd.order = d.jdt_order[k];
+  jd.first = d.jdt_first_step[k];
+  jd.last = d.jdt_last_step[k];
+  jd.coeffs.assign(d.jdt_coeffs[k], d.jdt_coeffs[k] + D);
+  jd.targets.assign(d.jdt_targets[k], d.jdt_targets[k] + D);
+  jd.upper.assign(d.jdt_upper_tols[k], d.jdt_upper_tols[k] + D);
+  jd.lower.assign(d.jdt_lower_tols[k], d.jdt_lower_tols[k] + D);
+  bool zero = true;
+  for (int j = 0; j < D; ++j)
+    zero = zero && std::fabs(jd.upper[static_cast<std::size_t>(j)]) < 1e-5 &&
+           std::fabs(jd.lower[static_cast<std::size_t>(j)]) < 1e-5;
+  if (jd.order < 1 || jd.order > 3)
+    throw std::runtime_error("jdt_order must be 1, 2 or 3");
+  if (d.jdt_is_cnt[k])
+  {
+    if (zero)
+      tp.prob->addConstraint(std::make_shared<JointDiffEqConstraint>(jd));
+    else if (jd.order == 1)
+      throw std::runtime_error("a JointVel tolerance constraint is a jvx term");
+    else
+      tp.prob->addConstraint(std::make_shared<JointDiffIneqConstraint>(jd));
+  }
+  else
+  {
+    if (jd.order == 1)
+      throw std::runtime_error("JointVel costs are jv / jvx terms");
+    if (zero)
+      tp.prob->addCost(std::make_shared<JointDiffEqCost>(jd));
+    else
+      tp.prob->addCost(std::make_shared<JointDiffIneqCost>(jd));
+  }
+}
+
 // ------------------------------------------------------------ construction
 TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj, const double* cart_targets,
                              const double* scene, const double* jpos_targets)
@@ -651,6 +909,9 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
       tp.prob->addCost(std::make_shared<JointVelIneqCost>(rows, dv(d.jvx_coeffs[x]), dv(d.jvx_targets[x]),
                                                           dv(d.jvx_upper_tols[x]), dv(d.jvx_lower_tols[x]), f, l));
     }
+  for (int k = 0; k < d.n_jdt; ++k)
+    if (!d.jdt_is_cnt[k])
+      addJointDiffTerm(tp, rows, d, k);
   if (d.coll_enabled && !d.coll_is_cnt)
     addCollisionTerms(tp, rows, d, scene);
   // cnt_infos: CartPose constraints, collision constraint
@@ -674,6 +935,9 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
       tp.prob->addConstraint(std::make_shared<JointVelIneqConstraint>(
           rows, dv(d.jvx_coeffs[x]), dv(d.jvx_targets[x]), dv(d.jvx_upper_tols[x]), dv(d.jvx_lower_tols[x]), f, l));
     }
+  for (int k = 0; k < d.n_jdt; ++k)
+    if (d.jdt_is_cnt[k])
+      addJointDiffTerm(tp, rows, d, k);
   if (d.coll_enabled && d.coll_is_cnt)
     addCollisionTerms(tp, rows, d, scene);
   return tp;

@@ -189,6 +189,10 @@ static int validate(const thip_problem_desc* d, std::string& why)
                    "a term with zero tolerances goes in jv_*",
              THIP_E_INVALID;
   }
+  if (d->n_jdt != 0)
+    return why = "JointAcc / JointJerk terms and JointVel equality constraints are not lowered into the batched "
+                 "kernel: solve such a problem with sco::BasicTrustRegionSQP (the generic path, GpuModel)",
+           THIP_E_INVALID;
   if (d->n_jpos < 0 || d->n_jpos > THIP_MAX_JPOS)
     return why = "n_jpos out of range", THIP_E_INVALID;
   for (int k = 0; k < d->n_jpos; ++k)

@@ -19,6 +19,7 @@ MAX_SPHERES = 32
 MAX_PRIMS = 16
 MAX_JPOS = 8
 MAX_JVX = 4
+MAX_JDT = 8
 TRACE_W = 16  # THIP_TRACE_W
 DEBUG_NO_SEGMENT, DEBUG_FORCE_WIDE = 1, 2  # thip_debug_set_path flags
 
@@ -137,6 +138,15 @@ class ProblemDesc(C.Structure):
         ("jvx_targets", (C.c_double * MAX_DOF) * MAX_JVX),
         ("jvx_upper_tols", (C.c_double * MAX_DOF) * MAX_JVX),
         ("jvx_lower_tols", (C.c_double * MAX_DOF) * MAX_JVX),
+        ("n_jdt", C.c_int),
+        ("jdt_order", C.c_int * MAX_JDT),
+        ("jdt_is_cnt", C.c_int * MAX_JDT),
+        ("jdt_first_step", C.c_int * MAX_JDT),
+        ("jdt_last_step", C.c_int * MAX_JDT),
+        ("jdt_coeffs", (C.c_double * MAX_DOF) * MAX_JDT),
+        ("jdt_targets", (C.c_double * MAX_DOF) * MAX_JDT),
+        ("jdt_upper_tols", (C.c_double * MAX_DOF) * MAX_JDT),
+        ("jdt_lower_tols", (C.c_double * MAX_DOF) * MAX_JDT),
         ("coll_enabled", C.c_int),
         ("coll_is_cnt", C.c_int),
         ("coll_first_step", C.c_int),
