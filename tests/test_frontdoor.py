@@ -79,9 +79,13 @@ def _coll_pairs(pairs):
         (_doc(costs=[{"type": "joint_vel", "params": {}}]), "missing field: targets"),
         (_doc(costs=[{"type": "joint_vel", "params": {"targets": [0, 0]}}]),
          "wrong number of JointVelTermInfo targets. expected 7 got 2"),
-        (_doc(costs=[{"type": "joint_acc", "params": {}}]), "term type 'joint_acc' is not supported on the HIP path"),
-        (_doc(constraints=[{"type": "joint_vel", "params": {"targets": [0]}}]),
-         "JointVelTermInfo as an equality constraint (JointVelEqConstraint) is not supported"),
+        (_doc(costs=[{"type": "joint_acc", "params": {}}]), "missing field: targets"),
+        (_doc(costs=[{"type": "joint_jerk", "params": {"targets": [0], "use_time": False}}]),
+         "invalid field found: use_time"),
+        (_doc(costs=[{"type": "joint_acc", "params": {"targets": [0, 0]}}]),
+         "wrong number of JointAccTermInfo targets. expected 7 got 2"),
+        (_doc(costs=[{"type": "joint_jerk", "params": {"targets": [0], "first_step": 1, "last_step": 1}}]),
+         "too short"),
         (_doc(costs=[{"type": "collision", "params": {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 0}}]),
          "collision evaluator_type 0 (DISCRETE = 1, LVS_DISCRETE = 2, CONTINUOUS = 3, LVS_CONTINUOUS = 4 are) "
          "is not supported"),

@@ -16,7 +16,8 @@ class BatchTrustRegionSQP
 public:
   // Checks that every problem shares problem 0's structure (steps, chain,
   // terms, parameters, scene size) and allocates the device workspace.
-  explicit BatchTrustRegionSQP(std::vector<TrajOptProb::Ptr> probs, int device = 0);
+  explicit BatchTrustRegionSQP(const std::vector<TrajOptProb::Ptr>& probs, int device = 0);
+  explicit BatchTrustRegionSQP(std::vector<LoweredProblem> probs, int device = 0);
   ~BatchTrustRegionSQP();
   BatchTrustRegionSQP(const BatchTrustRegionSQP&) = delete;
   BatchTrustRegionSQP& operator=(const BatchTrustRegionSQP&) = delete;
@@ -33,40 +34,30 @@ public:
   int batch() const { return static_cast<int>(probs_.size()); }
 
 private:
+  void init(int device);
   void check(int rc, const char* what) const;
-  std::vector<TrajOptProb::Ptr> probs_;
+  std::vector<LoweredProblem> probs_;
   struct thip_ctx* ctx_ = nullptr;
   int trace_cap_ = 0;
 };
 
 // Per-problem drop-in for the reference's optimizer usage (SURVEY.md §8b tier i):
-//   sco::BasicTrustRegionSQP opt(prob);            optimizers.hpp:142-194
+//   BasicTrustRegionSQP opt(prob);                 optimizers.hpp:142-194
 //   opt.initialize(trajToDblVec(prob->GetInitTraj()));
 //   opt.optimize();                                optimizers.cpp:699-991
 //   getTraj(opt.x(), ...), opt.results()           (planning_unit.cpp:83-124)
-// The problem runs as a batch of one on the device; parameters set here
-// replace the problem's opt_info for this run.
-class BasicTrustRegionSQP
+// sco::BasicTrustRegionSQP with the problem's own opt_info as the parameters
+// and the HIP device of both paths (the fused kernel for a lowerable problem,
+// the GpuModel's QPs otherwise).
+class BasicTrustRegionSQP : public sco::BasicTrustRegionSQP
 {
 public:
-  explicit BasicTrustRegionSQP(TrajOptProb::Ptr prob, int device = 0);
-  void setProblem(TrajOptProb::Ptr prob);
-  void setParameters(const sco::BasicTrustRegionSQPParameters& param) { param_ = param; }
-  const sco::BasicTrustRegionSQPParameters& getParameters() const { return param_; }
-  sco::BasicTrustRegionSQPParameters& getParameters() { return param_; }
-  // x: the trajectory row-major [step][dof] (trajToDblVec); size n_steps * n_dof
-  void initialize(const DblVec& x);
-  sco::OptStatus optimize();
-  const DblVec& x() const { return results_.x; }
-  const sco::OptResults& results() const { return results_; }
-
-private:
-  TrajOptProb::Ptr prob_;
-  int device_;
-  sco::BasicTrustRegionSQPParameters param_;
-  DblVec x0_;
-  sco::OptResults results_;
+  explicit BasicTrustRegionSQP(const TrajOptProb::Ptr& prob, int device = 0);
 };
+
+// Upper bound on the per-QP trace records of one problem under param (the
+// native path's trajopt_solver.log)
+int traceCapacity(const sco::BasicTrustRegionSQPParameters& param);
 
 // trajopt/src/utils.cpp:13-24: the trajectory as one row-major vector
 DblVec trajToDblVec(const std::vector<DblVec>& traj);

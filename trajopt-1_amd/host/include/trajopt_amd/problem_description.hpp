@@ -3,16 +3,18 @@
 // ConstructProblem, trajopt/include/trajopt/problem_description.hpp:30-260)
 // restated in C++ over the C-ABI of include/trajopt_hip.h.
 //
-// Differences from the reference, all forced by what the HIP path lowers:
-//  * hatch() lowers a term into the batch-shared structure (thip_problem_desc)
-//    and the problem's own data (targets, initial trajectory) of a
-//    TrajOptProb, instead of pushing sco::Cost objects; BatchTrustRegionSQP
-//    (batch_sqp.hpp) then solves many TrajOptProbs that share one structure.
-//  * The registered term types are the ones on the HIP path: joint_pos,
-//    joint_vel, cart_pose, dynamic_cart_pose, collision.  The reference's other
-//    makers (cart_vel, joint_acc, joint_jerk, total_time,
-//    problem_description.cpp:57-70) are registered too, and their hatch()
-//    throws "not supported on the HIP path" so a JSON that uses them fails
+// TrajOptProb is a sco::OptProb (trajopt_sco/modeling.hpp): hatch() pushes
+// sco::Cost / sco::Constraint objects with prob.addCost / addConstraint, as the
+// reference does, so user TermInfos plug in unchanged.  The built-in terms
+// also lower themselves into the batch-shared structure (thip_problem_desc) and
+// the problem's own data (targets, initial trajectory); a problem whose every
+// term lowered runs the fused sqp_kernel (BatchTrustRegionSQP, batch_sqp.hpp,
+// or sco::BasicTrustRegionSQP as a batch of one), any other runs
+// sco::BasicTrustRegionSQP's host loop with each QP on the GPU (GpuModel).
+//  * Registered term types: joint_pos, joint_vel, joint_acc, joint_jerk,
+//    cart_pose, dynamic_cart_pose, collision.  cart_vel and total_time
+//    (problem_description.cpp:57-70) are registered too and their hatch()
+//    throws "not supported on the HIP path", so a JSON that uses them fails
 //    loudly rather than silently dropping a term.
 //  * Environment / KinematicGroup stand in for tesseract's Environment and
 //    JointGroup (which are out of scope): a serial chain with link and joint
@@ -27,71 +29,18 @@
 #include <vector>
 
 #include "trajopt_amd/json.hpp"
+#include "trajopt_amd/trajectory_costs.hpp"
 #include "trajopt_hip.h"
+#include "trajopt_sco/gpu_model.hpp"
+#include "trajopt_sco/modeling.hpp"
+#include "trajopt_sco/optimizers.hpp"
 
-namespace sco
-{
-// trajopt_sco/include/trajopt_sco/optimizers.hpp:25-33
-enum OptStatus : int
-{
-  OPT_CONVERGED,
-  OPT_SCO_ITERATION_LIMIT,
-  OPT_PENALTY_ITERATION_LIMIT,
-  OPT_TIME_LIMIT,
-  OPT_FAILED,
-  INVALID
-};
-std::string toString(OptStatus status);
-
-using DblVec = std::vector<double>;
-using IntVec = std::vector<int>;
-
-// optimizers.hpp:40-59 (+ the counters the HIP path reports)
-struct OptResults
-{
-  DblVec x;
-  OptStatus status{ INVALID };
-  double total_cost{ 0 };
-  DblVec cost_vals;  // not reported per term by the batch kernel (empty)
-  DblVec cnt_viols;  // idem
-  int n_func_evals{ 0 }, n_qp_solves{ 0 };
-  int n_sqp_iters{ 0 };
-  long long n_admm_iters{ 0 };
-  double max_cnt_viol{ 0 };
-  int flags{ 0 };
-};
-
-// optimizers.hpp:92-135 (numeric members; max_time is checked on the device at
-// the top of every SQP iteration against the problem's own clock)
-struct BasicTrustRegionSQPParameters
-{
-  double improve_ratio_threshold = 0.25;
-  double min_trust_box_size = 1e-4;
-  double min_approx_improve = 1e-4;
-  double min_approx_improve_frac = -1.7976931348623157e308;
-  int max_iter = 50;
-  double trust_shrink_ratio = 0.1;
-  double trust_expand_ratio = 1.5;
-  double cnt_tolerance = 1e-4;
-  double max_merit_coeff_increases = 5;
-  int max_qp_solver_failures = 3;
-  double merit_coeff_increase_ratio = 10;
-  double max_time = 1.7976931348623157e308;
-  double initial_merit_error_coeff = 10;
-  bool inflate_constraints_individually = true;
-  double trust_box_size = 1e-1;
-  // optimizers.hpp:127-129: with log_results, log_dir/trajopt_solver.log gets one
-  // writeSolver line per trust-region step (the vars / costs / constraints logs are not
-  // written: the device loop keeps no per-iteration copies of x and the term values)
-  bool log_results = false;
-  std::string log_dir = "/tmp";
-};
-}  // namespace sco
 
 namespace trajopt
 {
 using sco::DblVec;
 using sco::IntVec;
+struct ProblemConstructionInfo;
 
 // problem_description.hpp:30-60
 enum class TermType : char
@@ -234,6 +183,29 @@ struct JointVelTermInfo : public TermInfo
   static TermInfo::Ptr create() { return std::make_shared<JointVelTermInfo>(); }
 };
 
+// JointAccTermInfo / JointJerkTermInfo (problem_description.cpp:1393-1640): not
+// lowered into the batched kernel; their hatch() adds the JointAcc / JointJerk
+// cost or constraint objects (trajectory_costs.hpp) and records the term in the
+// descriptor's jdt table (the oracle's input)
+struct JointAccTermInfo : public TermInfo
+{
+  DblVec coeffs, targets, upper_tols, lower_tols;
+  int first_step = 0, last_step = -1;
+  JointAccTermInfo() : TermInfo(TermType::TT_COST | TermType::TT_CNT | TermType::TT_USE_TIME) {}
+  void fromJson(ProblemConstructionInfo& pci, const Json::Value& v) override;
+  void hatch(TrajOptProb& prob) override;
+  static TermInfo::Ptr create() { return std::make_shared<JointAccTermInfo>(); }
+};
+struct JointJerkTermInfo : public TermInfo
+{
+  DblVec coeffs, targets, upper_tols, lower_tols;
+  int first_step = 0, last_step = -1;
+  JointJerkTermInfo() : TermInfo(TermType::TT_COST | TermType::TT_CNT | TermType::TT_USE_TIME) {}
+  void fromJson(ProblemConstructionInfo& pci, const Json::Value& v) override;
+  void hatch(TrajOptProb& prob) override;
+  static TermInfo::Ptr create() { return std::make_shared<JointJerkTermInfo>(); }
+};
+
 // CartPoseTermInfo (problem_description.hpp:353-387); poses are 3x4 row-major
 struct CartPoseTermInfo : public TermInfo
 {
@@ -302,12 +274,29 @@ private:
   void readInitInfo(const Json::Value& v);
 };
 
-// The lowered problem: batch-shared structure + this problem's data.
-class TrajOptProb
+// The lowered form of one problem: the batch-shared structure and the
+// per-problem data the batched kernel uploads (thip_upload).
+struct LoweredProblem
+{
+  thip_problem_desc desc{};
+  std::vector<double> init;          // [n_steps * n_dof] row-major
+  std::vector<double> cart_targets;  // [n_cart][12] target-frame offsets in the chain root
+  std::vector<double> jpos_targets;  // [n_jpos][n_dof]
+  std::vector<double> scene;         // [n_prims][16]
+};
+
+// problem_description.hpp:69-108: the trajectory variables, the terms hatched
+// into them (sco::OptProb), and the lowered form the batched kernel runs.
+class TrajOptProb : public sco::OptProb, public std::enable_shared_from_this<TrajOptProb>
 {
 public:
   using Ptr = std::shared_ptr<TrajOptProb>;
 
+  TrajOptProb(int n_steps, const ProblemConstructionInfo& pci);
+  sco::VarVector GetVarRow(int i, int start_col, int num_col) { return traj_vars_.rblock(i, start_col, num_col); }
+  sco::VarVector GetVarRow(int i) { return traj_vars_.row(i); }
+  sco::Var& GetVar(int i, int j) { return traj_vars_.at(i, j); }
+  VarArray& GetVars() { return traj_vars_; }
   int GetNumSteps() const { return desc_.n_steps; }
   int GetNumDOF() const { return desc_.chain.n_dof; }
   KinematicGroup::ConstPtr GetKin() const { return kin_; }
@@ -322,6 +311,20 @@ public:
   std::vector<double> jpos_targets;  // [n_jpos][D]
   std::vector<double> scene;         // [n_prims][16]
 
+  // a built-in hatch() adds its lowered terms through these (counted), a user
+  // TermInfo through addCost / addConstraint (not lowered)
+  void addLoweredCost(sco::Cost::Ptr c);
+  void addLoweredConstraint(sco::Constraint::Ptr c);
+  // every cost and constraint lowered into desc() (the batched kernel runs it)
+  bool lowerable() const;
+  std::string unloweredTerms() const;  // names of the terms the kernel does not run
+  // the lowered form with the current initial trajectory
+  LoweredProblem lowered() const;
+  // sco::BasicTrustRegionSQP asks first: a lowerable problem runs sqp_kernel as a batch of one
+  bool solveNative(const sco::BasicTrustRegionSQPParameters& param, const DblVec& x0,
+                   sco::OptResults& results) override;
+  int device = 0;  // HIP device of the native path
+
   friend TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci);
 
 private:
@@ -329,6 +332,8 @@ private:
   std::vector<DblVec> init_;
   KinematicGroup::ConstPtr kin_;
   Environment::ConstPtr env_;
+  VarArray traj_vars_;
+  std::vector<const void*> lowered_;  // the lowered Cost / Constraint objects
 };
 
 TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci);

@@ -52,6 +52,10 @@ public:
   void writeToFile(const std::string& fname) const override;  // osqp_interface.cpp:621-640
   VarVector getVars() const override;
 
+  // HIP device of the following solves
+  void setDevice(int device);
+  int device() const { return config_.device; }
+
   // diagnostics of the last solve
   const thip_qp_info& lastInfo() const { return info_; }
   long long admmItersTotal() const { return admm_total_; }

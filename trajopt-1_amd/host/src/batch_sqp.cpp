@@ -12,28 +12,111 @@ namespace trajopt
 namespace
 {
 // The structure of a lowered problem: its descriptor with the per-problem
-// default targets cleared (they travel in TrajOptProb::jpos_targets).
-thip_problem_desc structureOf(const TrajOptProb& p)
+// default targets cleared (they travel in LoweredProblem::jpos_targets).
+thip_problem_desc structureOf(const LoweredProblem& p)
 {
-  thip_problem_desc d = p.desc();
+  thip_problem_desc d = p.desc;
   for (auto& row : d.jpos_targets)
     for (double& v : row)
       v = 0.0;
   return d;
 }
+
+std::vector<LoweredProblem> lowerAll(const std::vector<TrajOptProb::Ptr>& probs)
+{
+  std::vector<LoweredProblem> out;
+  out.reserve(probs.size());
+  for (const auto& p : probs)
+  {
+    if (!p)
+      throw std::runtime_error("BatchTrustRegionSQP: null problem");
+    if (!p->lowerable())
+      throw std::runtime_error("BatchTrustRegionSQP: the batched kernel does not run " + p->unloweredTerms() +
+                               "; solve such a problem with sco::BasicTrustRegionSQP (the generic path)");
+    out.push_back(p->lowered());
+  }
+  return out;
+}
+
+void copyParams(const sco::BasicTrustRegionSQPParameters& p, thip_sqp_params& q)
+{
+  q.improve_ratio_threshold = p.improve_ratio_threshold;
+  q.min_trust_box_size = p.min_trust_box_size;
+  q.min_approx_improve = p.min_approx_improve;
+  q.min_approx_improve_frac = p.min_approx_improve_frac;
+  q.max_iter = p.max_iter;
+  q.trust_shrink_ratio = p.trust_shrink_ratio;
+  q.trust_expand_ratio = p.trust_expand_ratio;
+  q.cnt_tolerance = p.cnt_tolerance;
+  q.max_merit_coeff_increases = p.max_merit_coeff_increases;
+  q.max_qp_solver_failures = p.max_qp_solver_failures;
+  q.merit_coeff_increase_ratio = p.merit_coeff_increase_ratio;
+  q.initial_merit_error_coeff = p.initial_merit_error_coeff;
+  q.inflate_constraints_individually = p.inflate_constraints_individually ? 1 : 0;
+  q.trust_box_size = p.trust_box_size;
+  q.max_time = p.max_time;
+}
+
+void paramsFrom(const thip_sqp_params& q, sco::BasicTrustRegionSQPParameters& p)
+{
+  p.improve_ratio_threshold = q.improve_ratio_threshold;
+  p.min_trust_box_size = q.min_trust_box_size;
+  p.min_approx_improve = q.min_approx_improve;
+  p.min_approx_improve_frac = q.min_approx_improve_frac;
+  p.max_iter = q.max_iter;
+  p.trust_shrink_ratio = q.trust_shrink_ratio;
+  p.trust_expand_ratio = q.trust_expand_ratio;
+  p.cnt_tolerance = q.cnt_tolerance;
+  p.max_merit_coeff_increases = q.max_merit_coeff_increases;
+  p.max_qp_solver_failures = q.max_qp_solver_failures;
+  p.merit_coeff_increase_ratio = q.merit_coeff_increase_ratio;
+  p.initial_merit_error_coeff = q.initial_merit_error_coeff;
+  p.inflate_constraints_individually = q.inflate_constraints_individually != 0;
+  p.trust_box_size = q.trust_box_size;
+  p.max_time = q.max_time;
+}
+
+// BasicTrustRegionSQPResults::writeSolver (optimizers.cpp:533-547), from the trace records
+void writeSolverLog(const std::string& path, const std::vector<double>& rec)
+{
+  std::FILE* f = std::fopen(path.c_str(), "w");
+  if (!f)
+    throw std::runtime_error("BasicTrustRegionSQP: cannot open " + path);
+  bool header = true;
+  for (std::size_t k = 0; k + THIP_TRACE_W <= rec.size(); k += THIP_TRACE_W)
+  {
+    const double* r = rec.data() + k;
+    if (r[15] == 0)
+      continue;  // a QP without a merit evaluation (solver failure)
+    if (header)
+      std::fprintf(f, "%s,%s,%s,%s,%s,%s\n", "DESCRIPTION", "oldexact", "new_exact", "dapprox", "dexact", "ratio");
+    header = false;
+    std::fprintf(f, "%s,%10.3e,%10.3e,%10.3e,%10.3e,%10.3e\n", "Solver", r[10], r[11], r[12], r[13], r[14]);
+  }
+  std::fclose(f);
+}
 }  // namespace
 
-BatchTrustRegionSQP::BatchTrustRegionSQP(std::vector<TrajOptProb::Ptr> probs, int device) : probs_(std::move(probs))
+// ------------------------------------------------------------ BatchTrustRegionSQP
+BatchTrustRegionSQP::BatchTrustRegionSQP(const std::vector<TrajOptProb::Ptr>& probs, int device)
+  : probs_(lowerAll(probs))
+{
+  init(device);
+}
+
+BatchTrustRegionSQP::BatchTrustRegionSQP(std::vector<LoweredProblem> probs, int device) : probs_(std::move(probs))
+{
+  init(device);
+}
+
+void BatchTrustRegionSQP::init(int device)
 {
   if (probs_.empty())
     throw std::runtime_error("BatchTrustRegionSQP: empty batch");
-  for (const auto& p : probs_)
-    if (!p)
-      throw std::runtime_error("BatchTrustRegionSQP: null problem");
-  const thip_problem_desc d0 = structureOf(*probs_[0]);
+  const thip_problem_desc d0 = structureOf(probs_[0]);
   for (std::size_t b = 1; b < probs_.size(); ++b)
   {
-    const thip_problem_desc db = structureOf(*probs_[b]);
+    const thip_problem_desc db = structureOf(probs_[b]);
     if (std::memcmp(&d0, &db, sizeof(d0)) != 0)
       throw std::runtime_error("BatchTrustRegionSQP: problem " + std::to_string(b) +
                                " does not share problem 0's structure (steps, chain, terms, parameters and scene "
@@ -56,17 +139,16 @@ void BatchTrustRegionSQP::setStream(void* stream) { check(thip_set_stream(ctx_, 
 
 std::vector<sco::OptResults> BatchTrustRegionSQP::optimize()
 {
-  const thip_problem_desc& d = probs_[0]->desc();
+  const thip_problem_desc& d = probs_[0].desc;
   const int B = batch(), N = d.n_steps, D = d.chain.n_dof;
   std::vector<double> init, tgt, jpt, scene;
   init.reserve(static_cast<std::size_t>(B) * N * D);
   for (const auto& p : probs_)
   {
-    for (const auto& row : p->GetInitTraj())
-      init.insert(init.end(), row.begin(), row.end());
-    tgt.insert(tgt.end(), p->cart_targets.begin(), p->cart_targets.end());
-    jpt.insert(jpt.end(), p->jpos_targets.begin(), p->jpos_targets.end());
-    scene.insert(scene.end(), p->scene.begin(), p->scene.end());
+    init.insert(init.end(), p.init.begin(), p.init.end());
+    tgt.insert(tgt.end(), p.cart_targets.begin(), p.cart_targets.end());
+    jpt.insert(jpt.end(), p.jpos_targets.begin(), p.jpos_targets.end());
+    scene.insert(scene.end(), p.scene.begin(), p.scene.end());
   }
   if (init.size() != static_cast<std::size_t>(B) * N * D ||
       tgt.size() != static_cast<std::size_t>(B) * d.n_cart * 12 ||
@@ -126,24 +208,66 @@ std::vector<std::vector<double>> BatchTrustRegionSQP::trace() const
   return out;
 }
 
-// BasicTrustRegionSQPResults::writeSolver (optimizers.cpp:533-547), from the trace records
-static void writeSolverLog(const std::string& path, const std::vector<double>& rec)
+// ------------------------------------------------------------ the native path of one problem
+int traceCapacity(const sco::BasicTrustRegionSQPParameters& param)
 {
-  std::FILE* f = std::fopen(path.c_str(), "w");
-  if (!f)
-    throw std::runtime_error("BasicTrustRegionSQP: cannot open " + path);
-  bool header = true;
-  for (std::size_t k = 0; k + THIP_TRACE_W <= rec.size(); k += THIP_TRACE_W)
+  // one record per QP solve: at most (penalty rounds) x (SQP iterations) x
+  // (trust-region tries per iteration); the box shrinks by trust_shrink_ratio
+  // per rejected try from at most trust_box_size * expand^max_iter down to
+  // min_trust_box_size
+  const double grow = param.max_iter * std::log(std::max(param.trust_expand_ratio, 1.0));
+  const double span = std::log(param.trust_box_size / param.min_trust_box_size) + grow;
+  const double tries = 2.0 + std::max(0.0, span / std::log(1.0 / param.trust_shrink_ratio));
+  const double bound = (param.max_merit_coeff_increases + 1.0) * param.max_iter * tries;
+  // (a non-finite bound -- absurd parameters -- takes the fixed cap)
+  return static_cast<int>(std::isfinite(bound) ? std::min(std::max(bound, 64.0), 1.0e6) : 1.0e6);
+}
+
+bool TrajOptProb::solveNative(const sco::BasicTrustRegionSQPParameters& param, const DblVec& x0,
+                              sco::OptResults& results)
+{
+  if (!lowerable())
+    return false;
+  if (!(param.trust_shrink_ratio > 0 && param.trust_shrink_ratio < 1) || !(param.min_trust_box_size > 0) ||
+      !(param.trust_box_size > 0) || !(param.trust_expand_ratio > 0))
+    throw std::runtime_error("BasicTrustRegionSQP: need 0 < trust_shrink_ratio < 1, trust_expand_ratio > 0, "
+                             "min_trust_box_size > 0 and trust_box_size > 0");
+  const int N = GetNumSteps(), D = GetNumDOF();
+  if (x0.size() != static_cast<std::size_t>(N) * static_cast<std::size_t>(D))
+    throw std::runtime_error("BasicTrustRegionSQP: expected " + std::to_string(N * D) + " initial values, got " +
+                             std::to_string(x0.size()));
+  // fixed timesteps are linear equalities to ConstructProblem's initial trajectory
+  // (problem_description.cpp:489-510); the kernel pins them to the uploaded start,
+  // so a start that moves a fixed step would change the problem: refuse it
+  for (int f = 0; f < desc_.n_fixed; ++f)
   {
-    const double* r = rec.data() + k;
-    if (r[15] == 0)
-      continue;  // a QP without a merit evaluation (solver failure)
-    if (header)
-      std::fprintf(f, "%s,%s,%s,%s,%s,%s\n", "DESCRIPTION", "oldexact", "new_exact", "dapprox", "dexact", "ratio");
-    header = false;
-    std::fprintf(f, "%s,%10.3e,%10.3e,%10.3e,%10.3e,%10.3e\n", "Solver", r[10], r[11], r[12], r[13], r[14]);
+    const int t = desc_.fixed_steps[f];
+    for (int j = 0; j < D; ++j)
+      if (x0[static_cast<std::size_t>(t * D + j)] != init_[static_cast<std::size_t>(t)][static_cast<std::size_t>(j)])
+        throw std::runtime_error("BasicTrustRegionSQP::initialize: fixed timestep " + std::to_string(t) +
+                                 " differs from the problem's initial trajectory");
   }
-  std::fclose(f);
+  LoweredProblem lp = lowered();
+  lp.init = x0;
+  copyParams(param, lp.desc.sqp);
+  BatchTrustRegionSQP batch(std::vector<LoweredProblem>{ std::move(lp) }, device);
+  if (param.log_results)
+    batch.enableTrace(traceCapacity(param));
+  results = batch.optimize()[0];
+  if (param.log_results)
+    writeSolverLog(param.log_dir + "/trajopt_solver.log", batch.trace()[0]);
+  return true;
+}
+
+// ------------------------------------------------------------ BasicTrustRegionSQP
+BasicTrustRegionSQP::BasicTrustRegionSQP(const TrajOptProb::Ptr& prob, int device)
+  : sco::BasicTrustRegionSQP(prob)
+{
+  prob->device = device;
+  if (auto* gm = dynamic_cast<sco::GpuModel*>(prob->getModel().get()))
+    gm->setDevice(device);
+  // the problem's own parameters (ProblemConstructionInfo::opt_info) are the defaults
+  paramsFrom(prob->desc().sqp, param_);
 }
 
 DblVec trajToDblVec(const std::vector<DblVec>& traj)
@@ -152,108 +276,5 @@ DblVec trajToDblVec(const std::vector<DblVec>& traj)
   for (const auto& row : traj)
     out.insert(out.end(), row.begin(), row.end());
   return out;
-}
-
-BasicTrustRegionSQP::BasicTrustRegionSQP(TrajOptProb::Ptr prob, int device) : device_(device)
-{
-  setProblem(std::move(prob));
-}
-
-void BasicTrustRegionSQP::setProblem(TrajOptProb::Ptr prob)
-{
-  if (!prob)
-    throw std::runtime_error("BasicTrustRegionSQP: null problem");
-  prob_ = std::move(prob);
-  // the problem's own parameters (ProblemConstructionInfo::opt_info) are the defaults
-  const thip_sqp_params& q = prob_->desc().sqp;
-  param_.improve_ratio_threshold = q.improve_ratio_threshold;
-  param_.min_trust_box_size = q.min_trust_box_size;
-  param_.min_approx_improve = q.min_approx_improve;
-  param_.min_approx_improve_frac = q.min_approx_improve_frac;
-  param_.max_iter = q.max_iter;
-  param_.trust_shrink_ratio = q.trust_shrink_ratio;
-  param_.trust_expand_ratio = q.trust_expand_ratio;
-  param_.cnt_tolerance = q.cnt_tolerance;
-  param_.max_merit_coeff_increases = q.max_merit_coeff_increases;
-  param_.max_qp_solver_failures = q.max_qp_solver_failures;
-  param_.merit_coeff_increase_ratio = q.merit_coeff_increase_ratio;
-  param_.initial_merit_error_coeff = q.initial_merit_error_coeff;
-  param_.inflate_constraints_individually = q.inflate_constraints_individually != 0;
-  param_.trust_box_size = q.trust_box_size;
-  x0_.clear();
-  results_ = sco::OptResults{};
-}
-
-void BasicTrustRegionSQP::initialize(const DblVec& x)
-{
-  const std::size_t n = static_cast<std::size_t>(prob_->GetNumSteps()) * static_cast<std::size_t>(prob_->GetNumDOF());
-  if (x.size() != n)
-    throw std::runtime_error("BasicTrustRegionSQP::initialize: expected " + std::to_string(n) + " values, got " +
-                             std::to_string(x.size()));
-  // fixed timesteps are linear equalities to ConstructProblem's initial trajectory
-  // (problem_description.cpp:489-510); the device path pins them to the uploaded start,
-  // so a start that moves a fixed step would change the problem: refuse it
-  const thip_problem_desc& d = prob_->desc();
-  const int D = prob_->GetNumDOF();
-  for (int f = 0; f < d.n_fixed; ++f)
-  {
-    const int t = d.fixed_steps[f];
-    for (int j = 0; j < D; ++j)
-      if (x[static_cast<std::size_t>(t * D + j)] != prob_->GetInitTraj()[static_cast<std::size_t>(t)][static_cast<std::size_t>(j)])
-        throw std::runtime_error("BasicTrustRegionSQP::initialize: fixed timestep " + std::to_string(t) +
-                                 " differs from the problem's initial trajectory");
-  }
-  x0_ = x;
-}
-
-sco::OptStatus BasicTrustRegionSQP::optimize()
-{
-  auto p = std::make_shared<TrajOptProb>(*prob_);
-  thip_sqp_params& q = p->desc().sqp;
-  q.improve_ratio_threshold = param_.improve_ratio_threshold;
-  q.min_trust_box_size = param_.min_trust_box_size;
-  q.min_approx_improve = param_.min_approx_improve;
-  q.min_approx_improve_frac = param_.min_approx_improve_frac;
-  q.max_iter = param_.max_iter;
-  q.trust_shrink_ratio = param_.trust_shrink_ratio;
-  q.trust_expand_ratio = param_.trust_expand_ratio;
-  q.cnt_tolerance = param_.cnt_tolerance;
-  q.max_merit_coeff_increases = param_.max_merit_coeff_increases;
-  q.max_qp_solver_failures = param_.max_qp_solver_failures;
-  q.merit_coeff_increase_ratio = param_.merit_coeff_increase_ratio;
-  q.initial_merit_error_coeff = param_.initial_merit_error_coeff;
-  q.inflate_constraints_individually = param_.inflate_constraints_individually ? 1 : 0;
-  q.trust_box_size = param_.trust_box_size;
-  q.max_time = param_.max_time;
-  if (!(param_.trust_shrink_ratio > 0 && param_.trust_shrink_ratio < 1) || !(param_.min_trust_box_size > 0) ||
-      !(param_.trust_box_size > 0) || !(param_.trust_expand_ratio > 0))
-    throw std::runtime_error("BasicTrustRegionSQP: need 0 < trust_shrink_ratio < 1, trust_expand_ratio > 0, "
-                             "min_trust_box_size > 0 and trust_box_size > 0");
-  if (!x0_.empty())
-  {
-    const int N = p->GetNumSteps(), D = p->GetNumDOF();
-    std::vector<DblVec> traj(static_cast<std::size_t>(N));
-    for (int t = 0; t < N; ++t)
-      traj[static_cast<std::size_t>(t)].assign(x0_.begin() + t * D, x0_.begin() + (t + 1) * D);
-    p->SetInitTraj(traj);
-  }
-  BatchTrustRegionSQP batch({ p }, device_);
-  if (param_.log_results)
-  {
-    // one record per QP solve: at most (penalty rounds) x (SQP iterations) x
-    // (trust-region tries per iteration); the box shrinks by trust_shrink_ratio
-    // per rejected try from at most trust_box_size * expand^max_iter down to
-    // min_trust_box_size
-    const double grow = param_.max_iter * std::log(std::max(param_.trust_expand_ratio, 1.0));
-    const double span = std::log(param_.trust_box_size / param_.min_trust_box_size) + grow;
-    const double tries = 2.0 + std::max(0.0, span / std::log(1.0 / param_.trust_shrink_ratio));
-    const double bound = (param_.max_merit_coeff_increases + 1.0) * param_.max_iter * tries;
-    // (a non-finite bound -- absurd parameters -- takes the fixed cap)
-    batch.enableTrace(static_cast<int>(std::isfinite(bound) ? std::min(std::max(bound, 64.0), 1.0e6) : 1.0e6));
-  }
-  results_ = batch.optimize()[0];
-  if (param_.log_results)
-    writeSolverLog(param_.log_dir + "/trajopt_solver.log", batch.trace()[0]);
-  return results_.status;
 }
 }  // namespace trajopt

@@ -10,6 +10,8 @@
 #include <iostream>
 #include <stdexcept>
 
+#include "trajopt_sco/expr_ops.hpp"
+
 namespace
 {
 bool gRegisteredMakers = false;
@@ -72,8 +74,6 @@ trajopt::TermInfo::Ptr makeUnsupported()
   return std::make_shared<UnsupportedTermInfo>(kName);
 }
 constexpr char kCartVel[] = "cart_vel";
-constexpr char kJointAcc[] = "joint_acc";
-constexpr char kJointJerk[] = "joint_jerk";
 constexpr char kTotalTime[] = "total_time";
 
 // problem_description.cpp:57-70
@@ -85,8 +85,8 @@ void RegisterMakers()
   trajopt::TermInfo::RegisterMaker("cart_vel", &makeUnsupported<kCartVel>);
   trajopt::TermInfo::RegisterMaker("joint_pos", &trajopt::JointPosTermInfo::create);
   trajopt::TermInfo::RegisterMaker("joint_vel", &trajopt::JointVelTermInfo::create);
-  trajopt::TermInfo::RegisterMaker("joint_acc", &makeUnsupported<kJointAcc>);
-  trajopt::TermInfo::RegisterMaker("joint_jerk", &makeUnsupported<kJointJerk>);
+  trajopt::TermInfo::RegisterMaker("joint_acc", &trajopt::JointAccTermInfo::create);
+  trajopt::TermInfo::RegisterMaker("joint_jerk", &trajopt::JointJerkTermInfo::create);
   trajopt::TermInfo::RegisterMaker("collision", &trajopt::CollisionTermInfo::create);
   trajopt::TermInfo::RegisterMaker("total_time", &makeUnsupported<kTotalTime>);
 }
@@ -171,18 +171,106 @@ double linspaced(int size, double low, double high, int i)
     return (i == 0) ? low : high - double(size1 - i) * step;
   return (i == size1) ? high : low + double(i) * step;
 }
-}  // namespace
 
-namespace sco
+bool allZero(const trajopt::DblVec& v)
 {
-std::string toString(OptStatus status)
-{
-  static const char* names[] = { "OPT_CONVERGED",   "OPT_SCO_ITERATION_LIMIT", "OPT_PENALTY_ITERATION_LIMIT",
-                                 "OPT_TIME_LIMIT", "OPT_FAILED",              "INVALID" };
-  const int i = static_cast<int>(status);
-  return (i >= 0 && i <= 5) ? names[i] : "INVALID";
+  return std::all_of(v.begin(), v.end(), [](double a) { return doubleEquals(a, 0.); });
 }
-}  // namespace sco
+
+// the JointVel / JointAcc / JointJerk step clamping of the reference's hatch()
+// (problem_description.cpp:1227-1243, 1423-1440, 1545-1562): `span` steps are needed
+// for one difference
+void clampSteps(int n_steps, int order, int& first, int& last)
+{
+  if (last <= -1)
+    last = n_steps - 1;
+  if ((n_steps - (order + 1)) <= first)
+    first = n_steps - (order + 1);
+  if ((n_steps - 1) <= last)
+    last = n_steps - 1;
+  if (last == first)
+    last += (order == 1) ? 1 : (order == 2) ? 2 : 4;
+  if (last < first)
+    std::swap(first, last);
+}
+
+trajopt::JointDiffSpec diffSpec(trajopt::TrajOptProb& prob, int order, const trajopt::DblVec& coeffs,
+                                const trajopt::DblVec& targets, const trajopt::DblVec& upper,
+                                const trajopt::DblVec& lower, int first, int last)
+{
+  trajopt::JointDiffSpec s;
+  s.vars = prob.GetVars();
+  s.coeffs = coeffs;
+  s.targets = targets;
+  s.upper_tols = upper;
+  s.lower_tols = lower;
+  s.order = order;
+  s.first_step = first;
+  s.last_step = last;
+  return s;
+}
+
+// the host cost / constraint object of a joint-difference term (trajectory_costs.hpp)
+void addJointDiffObjects(trajopt::TrajOptProb& prob, const trajopt::JointDiffSpec& s, bool is_cost, bool zero_tols,
+                         const std::string& name, bool lowered)
+{
+  if (is_cost)
+  {
+    sco::Cost::Ptr c = zero_tols ? sco::Cost::Ptr(std::make_shared<trajopt::JointDiffEqCost>(s, name))
+                                 : sco::Cost::Ptr(std::make_shared<trajopt::JointDiffIneqCost>(s, name));
+    if (lowered)
+      prob.addLoweredCost(c);
+    else
+      prob.addCost(c);
+  }
+  else
+  {
+    sco::Constraint::Ptr c = zero_tols
+                                 ? sco::Constraint::Ptr(std::make_shared<trajopt::JointDiffEqConstraint>(s, name))
+                                 : sco::Constraint::Ptr(std::make_shared<trajopt::JointDiffIneqConstraint>(s, name));
+    if (lowered)
+      prob.addLoweredConstraint(c);
+    else
+      prob.addConstraint(c);
+  }
+}
+
+// a JointVel equality constraint / JointAcc / JointJerk term: the descriptor's jdt
+// table (the oracle's input; the batched kernel refuses it) and the host object
+void addJointDiffTerm(trajopt::TrajOptProb& prob, int order, bool is_cost, const trajopt::DblVec& coeffs,
+                      const trajopt::DblVec& targets, const trajopt::DblVec& upper, const trajopt::DblVec& lower,
+                      int first, int last, const std::string& name)
+{
+  thip_problem_desc& d = prob.desc();
+  if (d.n_jdt >= THIP_MAX_JDT)
+    unsupported("more than " + std::to_string(THIP_MAX_JDT) + " JointVel-constraint / JointAcc / JointJerk terms");
+  if (first < 0 || last > prob.GetNumSteps() - 1)
+    throw std::runtime_error(name + ": the trajectory is too short for a difference of order " +
+                             std::to_string(order) + " over steps " + std::to_string(first) + ".." +
+                             std::to_string(last));
+  const int k = d.n_jdt++;
+  d.jdt_order[k] = order;
+  d.jdt_is_cnt[k] = is_cost ? 0 : 1;
+  d.jdt_first_step[k] = first;
+  d.jdt_last_step[k] = last;
+  for (std::size_t j = 0; j < coeffs.size(); ++j)
+  {
+    d.jdt_coeffs[k][j] = coeffs[j];
+    d.jdt_targets[k][j] = targets[j];
+    d.jdt_upper_tols[k][j] = upper[j];
+    d.jdt_lower_tols[k][j] = lower[j];
+  }
+  addJointDiffObjects(prob, diffSpec(prob, order, coeffs, targets, upper, lower, first, last), is_cost,
+                      allZero(upper) && allZero(lower), name, false);
+}
+
+sco::ModelConfig::ConstPtr modelConfig(const trajopt::ProblemConstructionInfo& pci)
+{
+  auto c = std::make_shared<sco::GpuModelConfig>();
+  c->settings = pci.osqp;
+  return c;
+}
+}  // namespace
 
 namespace trajopt
 {
@@ -486,6 +574,8 @@ void JointPosTermInfo::hatch(TrajOptProb& prob)
     d.jpos_targets[k][j] = 0.0;  // per problem: TrajOptProb::jpos_targets
     prob.jpos_targets.push_back(targets[j]);
   }
+  addJointDiffObjects(prob, diffSpec(prob, 0, coeffs, targets, upper_tols, lower_tols, first_step, last_step),
+                      !d.jpos_is_cnt[k], allZero(upper_tols) && allZero(lower_tols), name, true);
 }
 
 // ------------------------------------------------------------ JointVel
@@ -505,8 +595,9 @@ void JointVelTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value&
   ensure_only_members(params, all_fields, sizeof(all_fields) / sizeof(char*));
 }
 
-// problem_description.cpp:1216-1391 (the step clamping itself is applied by
-// thip_create on the raw first/last steps, identically)
+// problem_description.cpp:1216-1391.  The kernel lowers the costs and the
+// tolerance constraint (thip_create clamps the raw steps as below); an equality
+// constraint goes to the jdt table and runs on the generic path.
 void JointVelTermInfo::hatch(TrajOptProb& prob)
 {
   const auto n_dof = static_cast<unsigned>(prob.GetNumDOF());
@@ -516,18 +607,24 @@ void JointVelTermInfo::hatch(TrajOptProb& prob)
     upper_tols = DblVec(n_dof, 0);
   if (lower_tols.empty())
     lower_tols = DblVec(n_dof, 0);
+  int first = first_step, last = last_step;
+  clampSteps(prob.GetNumSteps(), 1, first, last);
   checkParameterSize(coeffs, n_dof, "JointVelTermInfo coeffs", true);
   checkParameterSize(targets, n_dof, "JointVelTermInfo targets", true);
   checkParameterSize(upper_tols, n_dof, "JointVelTermInfo upper_tols", true);
   checkParameterSize(lower_tols, n_dof, "JointVelTermInfo lower_tols", true);
   if (any(term_type & TermType::TT_USE_TIME))
     unsupported("JointVelTermInfo with use_time");
-  // doubleEquals(tol, 0) (problem_description.cpp:1249-1252): zero tolerances -> the Eq forms
-  bool zero_tols = true;
-  for (unsigned j = 0; j < n_dof; ++j)
-    zero_tols = zero_tols && doubleEquals(upper_tols[j], 0.) && doubleEquals(lower_tols[j], 0.);
+  // doubleEquals(tol, 0) (problem_description.cpp:1254-1257): zero tolerances -> the Eq forms
+  const bool zero_tols = allZero(upper_tols) && allZero(lower_tols);
   const bool is_cost = any(term_type & TermType::TT_COST);
+  const JointDiffSpec spec = diffSpec(prob, 1, coeffs, targets, upper_tols, lower_tols, first, last);
   thip_problem_desc& d = prob.desc();
+  if (!is_cost && zero_tols)
+  {
+    addJointDiffTerm(prob, 1, false, coeffs, targets, upper_tols, lower_tols, first, last, name);
+    return;
+  }
   if (!zero_tols && (!is_cost || d.jv_enabled))
   {
     // JointVelIneqConstraint, or a further JointVelIneqCost: two hinge rows per (step, joint)
@@ -544,10 +641,9 @@ void JointVelTermInfo::hatch(TrajOptProb& prob)
       d.jvx_upper_tols[x][j] = upper_tols[j];
       d.jvx_lower_tols[x][j] = lower_tols[j];
     }
+    addJointDiffObjects(prob, spec, is_cost, false, name, true);
     return;
   }
-  if (!is_cost)
-    unsupported("JointVelTermInfo as an equality constraint (JointVelEqConstraint)");
   if (d.jv_enabled)
     unsupported("more than one JointVel cost without tolerances");
   d.jv_enabled = 1;
@@ -560,6 +656,79 @@ void JointVelTermInfo::hatch(TrajOptProb& prob)
     d.jv_upper_tols[j] = upper_tols[j];  // nonzero: JointVelIneqCost
     d.jv_lower_tols[j] = lower_tols[j];
   }
+  addJointDiffObjects(prob, spec, true, zero_tols, name, true);
+}
+
+// ------------------------------------------------------------ JointAcc / JointJerk
+namespace
+{
+void readJointDiffParams(ProblemConstructionInfo& pci, const Json::Value& v, const char* what, bool allow_use_time,
+                         DblVec& coeffs, DblVec& targets, DblVec& upper_tols, DblVec& lower_tols, int& first_step,
+                         int& last_step)
+{
+  if (!v.isMember("params"))
+    throw std::runtime_error(std::string(what) + ": missing params");
+  const Json::Value& params = v["params"];
+  const auto n_dof = static_cast<std::size_t>(pci.kin->numJoints());
+  json_marshal::childFromJson(params, targets, "targets");
+  json_marshal::childFromJson(params, coeffs, "coeffs", DblVec(n_dof, 1));
+  json_marshal::childFromJson(params, upper_tols, "upper_tols", DblVec(n_dof, 0));
+  json_marshal::childFromJson(params, lower_tols, "lower_tols", DblVec(n_dof, 0));
+  json_marshal::childFromJson(params, first_step, "first_step", 0);
+  json_marshal::childFromJson(params, last_step, "last_step", pci.basic_info.n_steps - 1);
+  // (JointJerkTermInfo's list has no "use_time", problem_description.cpp:1530)
+  const char* all_fields[] = { "coeffs", "first_step", "last_step", "targets", "lower_tols", "upper_tols", "use_time" };
+  ensure_only_members(params, all_fields, allow_use_time ? 7 : 6);
+}
+
+// problem_description.cpp:1412-1512 / 1534-1634
+void hatchJointDiff(TrajOptProb& prob, TermType term_type, int order, const char* what, const std::string& name,
+                    DblVec& coeffs, DblVec& targets, DblVec& upper_tols, DblVec& lower_tols, int& first_step,
+                    int& last_step)
+{
+  const auto n_dof = static_cast<unsigned>(prob.GetNumDOF());
+  if (coeffs.empty())
+    coeffs = DblVec(n_dof, 1);
+  if (upper_tols.empty())
+    upper_tols = DblVec(n_dof, 0);
+  if (lower_tols.empty())
+    lower_tols = DblVec(n_dof, 0);
+  clampSteps(prob.GetNumSteps(), order, first_step, last_step);
+  const std::string w(what);
+  checkParameterSize(coeffs, n_dof, w + " coeffs", true);
+  checkParameterSize(targets, n_dof, w + " targets", true);
+  checkParameterSize(upper_tols, n_dof, w + " upper_tols", true);
+  checkParameterSize(lower_tols, n_dof, w + " lower_tols", true);
+  if (any(term_type & TermType::TT_USE_TIME))
+  {
+    // the reference logs and adds nothing
+    std::cerr << w << ": Use time version of this term has not been defined.\n";
+    return;
+  }
+  addJointDiffTerm(prob, order, any(term_type & TermType::TT_COST), coeffs, targets, upper_tols, lower_tols,
+                   first_step, last_step, name);
+}
+}  // namespace
+
+void JointAccTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value& v)
+{
+  readJointDiffParams(pci, v, "JointAccTermInfo", true, coeffs, targets, upper_tols, lower_tols, first_step,
+                      last_step);
+}
+void JointAccTermInfo::hatch(TrajOptProb& prob)
+{
+  hatchJointDiff(prob, term_type, 2, "JointAccTermInfo", name, coeffs, targets, upper_tols, lower_tols, first_step,
+                 last_step);
+}
+void JointJerkTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value& v)
+{
+  readJointDiffParams(pci, v, "JointJerkTermInfo", false, coeffs, targets, upper_tols, lower_tols, first_step,
+                      last_step);
+}
+void JointJerkTermInfo::hatch(TrajOptProb& prob)
+{
+  hatchJointDiff(prob, term_type, 3, "JointJerkTermInfo", name, coeffs, targets, upper_tols, lower_tols, first_step,
+                 last_step);
 }
 
 // ------------------------------------------------------------ CartPose
@@ -685,6 +854,10 @@ void CartPoseTermInfo::hatch(TrajOptProb& prob)
     off = poseMul(poseInv(base), poseMul(kin->staticWorldPose(static_frame), static_offset));
   }
   prob.cart_targets.insert(prob.cart_targets.end(), off.begin(), off.end());
+  if (d.cart_is_cnt[k])
+    prob.addLoweredConstraint(std::make_shared<DeviceOnlyConstraint>(name, sco::EQ));
+  else
+    prob.addLoweredCost(std::make_shared<DeviceOnlyCost>(name));
 }
 
 // ------------------------------------------------------------ Collision
@@ -807,6 +980,10 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
   d.n_prims = static_cast<int>(env->scene.size());
   for (const auto& p : env->scene)
     prob.scene.insert(prob.scene.end(), p.begin(), p.end());
+  if (d.coll_is_cnt)
+    prob.addLoweredConstraint(std::make_shared<DeviceOnlyConstraint>(name, sco::INEQ));
+  else
+    prob.addLoweredCost(std::make_shared<DeviceOnlyCost>(name));
 }
 
 // ------------------------------------------------------------ ConstructProblem
@@ -834,14 +1011,8 @@ TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci)
   if (n_steps < 2 || n_steps > THIP_MAX_STEPS)
     throw std::runtime_error("n_steps must be in [2, " + std::to_string(THIP_MAX_STEPS) + "]");
 
-  auto prob = std::make_shared<TrajOptProb>();
-  prob->kin_ = pci.kin;
-  prob->env_ = pci.env;
+  auto prob = std::make_shared<TrajOptProb>(n_steps, pci);
   thip_problem_desc& d = prob->desc_;
-  std::memset(&d, 0, sizeof(d));
-  d.abi_version = THIP_ABI_VERSION;
-  d.n_steps = n_steps;
-  d.chain = pci.kin->chain;
   const int n_dof = pci.kin->numJoints();
 
   // initial trajectory
@@ -879,6 +1050,10 @@ TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci)
     if (t < 0 || t >= n_steps)
       throw std::runtime_error("Fixed timestep index is outside the bounds of the initial trajectory.");
     d.fixed_steps[d.n_fixed++] = t;
+    for (int j = 0; j < n_dof; ++j)
+      prob->addLinearConstraint(
+          sco::exprSub(sco::AffExpr(prob->GetVar(t, j)), init[static_cast<std::size_t>(t)][static_cast<std::size_t>(j)]),
+          sco::EQ);
   }
 
   // optimizer parameters: BasicTrustRegionSQP(prob) takes them from the caller
@@ -906,6 +1081,71 @@ TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci)
   for (const auto& ci : pci.cnt_infos)
     ci->hatch(*prob);
   return prob;
+}
+
+// ------------------------------------------------------------ TrajOptProb
+// problem_description.cpp:557-598: the j_i_j variables with the joint limits as bounds
+TrajOptProb::TrajOptProb(int n_steps, const ProblemConstructionInfo& pci)
+  : sco::OptProb(sco::ModelType::OSQP, modelConfig(pci)), kin_(pci.kin), env_(pci.env)
+{
+  if (!kin_)
+    throw std::runtime_error("TrajOptProb: pci.kin is null");
+  const int n_dof = kin_->numJoints();
+  std::memset(&desc_, 0, sizeof(desc_));
+  desc_.abi_version = THIP_ABI_VERSION;
+  desc_.n_steps = n_steps;
+  desc_.chain = kin_->chain;
+  std::vector<std::string> names;
+  DblVec lb, ub;
+  for (int i = 0; i < n_steps; ++i)
+    for (int j = 0; j < n_dof; ++j)
+    {
+      names.push_back("j_" + std::to_string(i) + "_" + std::to_string(j));
+      lb.push_back(kin_->chain.lower[j]);
+      ub.push_back(kin_->chain.upper[j]);
+    }
+  traj_vars_.n_rows = n_steps;
+  traj_vars_.n_cols = n_dof;
+  traj_vars_.data = createVariables(names, lb, ub);
+}
+
+void TrajOptProb::addLoweredCost(sco::Cost::Ptr c)
+{
+  lowered_.push_back(c.get());
+  addCost(std::move(c));
+}
+
+void TrajOptProb::addLoweredConstraint(sco::Constraint::Ptr c)
+{
+  lowered_.push_back(c.get());
+  addConstraint(std::move(c));
+}
+
+std::string TrajOptProb::unloweredTerms() const
+{
+  std::string out;
+  auto note = [&](const std::string& n) { out += (out.empty() ? "" : ", ") + ("'" + n + "'"); };
+  for (const auto& c : costs_)
+    if (std::find(lowered_.begin(), lowered_.end(), c.get()) == lowered_.end())
+      note(c->name());
+  for (const auto& c : getConstraints())
+    if (std::find(lowered_.begin(), lowered_.end(), c.get()) == lowered_.end())
+      note(c->name());
+  return out;
+}
+
+bool TrajOptProb::lowerable() const { return desc_.n_jdt == 0 && unloweredTerms().empty(); }
+
+LoweredProblem TrajOptProb::lowered() const
+{
+  LoweredProblem lp;
+  lp.desc = desc_;
+  for (const auto& row : init_)
+    lp.init.insert(lp.init.end(), row.begin(), row.end());
+  lp.cart_targets = cart_targets;
+  lp.jpos_targets = jpos_targets;
+  lp.scene = scene;
+  return lp;
 }
 
 TrajOptProb::Ptr ConstructProblem(const Json::Value& root, const Environment::ConstPtr& env)

@@ -69,6 +69,16 @@ GpuModel::~GpuModel()
   thip_qp_destroy(qp_);
 }
 
+void GpuModel::setDevice(int device)
+{
+  if (device == config_.device)
+    return;
+  thip_qp_destroy(qp_);
+  qp_ = nullptr;
+  qp_Pp_.clear();
+  config_.device = device;
+}
+
 Var GpuModel::addVar(const std::string& name)
 {
   std::scoped_lock lock(mutex_);
