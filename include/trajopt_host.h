@@ -39,6 +39,17 @@ int thost_lower_json(const char* json_text, const double* scene, int n_prims, th
 int thost_solve_json_batch(const char* const* json_texts, int batch, const double* scenes, int n_prims, int device,
                            double* x, thip_result* results, char* err, int err_len);
 
+/* ConstructProblem for one JSON problem and trajopt::BasicTrustRegionSQP
+ * (sco::BasicTrustRegionSQP with the problem's opt_info) on HIP device
+ * `device`, as the reference's planning code runs one problem
+ * (optimizers.cpp:699-991): a problem whose every term lowered into the
+ * batched kernel runs it as a batch of one (*native = 1); one with terms the
+ * kernel does not lower (JointAcc / JointJerk, JointVel equality constraints)
+ * runs the SQP loop on the host with every QP on the GPU (GpuModel,
+ * *native = 0).  x: [n_steps][n_dof]; result and native may be NULL. */
+int thost_solve_json(const char* json_text, const double* scene, int n_prims, int device, double* x,
+                     thip_result* result, int* native, char* err, int err_len);
+
 #ifdef __cplusplus
 }
 #endif

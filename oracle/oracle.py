@@ -96,6 +96,27 @@ def set_jitter(jac_abs=0.0, kkt_rel=0.0, sol_rel=0.0, seed=0, variant="exact"):
     L.oracle_set_jitter(float(jac_abs), float(kkt_rel), float(sol_rel), int(seed))
 
 
+SCO_CASES = {0: "setup_problem", 1: "ExprMult_test2", 2: "ExprMult_test3", 3: "QuadraticSeparable",
+             4: "QuadraticNonseparable", 5: "TP1", 6: "TP3", 7: "TP6", 8: "TP7"}
+
+
+def sco_case(case_id, variant="exact"):
+    """One of the reference's trajopt_sco unit problems (src/sco_cases.cpp) on the
+    oracle's OSQPModel / BasicTrustRegionSQP -> dict(x, status, n_qp, n_sqp,
+    n_vars_after, n_admm)."""
+    L = lib(variant)
+    L.oracle_sco_case.argtypes = [C.c_int, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_int),
+                                  C.POINTER(C.c_longlong)]
+    L.oracle_sco_case.restype = C.c_int
+    x = np.zeros(8)
+    counts = (C.c_int * 5)()
+    admm = C.c_longlong(0)
+    if L.oracle_sco_case(case_id, _dp(x), 8, counts, C.byref(admm)) != 0:
+        raise RuntimeError(f"oracle_sco_case({case_id}) failed")
+    return {"x": x[: counts[0]].copy(), "status": counts[1], "n_qp": counts[2], "n_sqp": counts[3],
+            "n_vars_after": counts[4], "n_admm": admm.value}
+
+
 def _dp(a):
     if a is None:
         return None

@@ -1119,9 +1119,15 @@ int thip_qp_solve(thip_qp* q, const double* P_values, const double* qvec, const 
                   const double* u, const thip_osqp_settings* settings, const double* warm_x, const double* warm_y,
                   const double* warm_rho, double* x, double* y, thip_qp_info* info)
 {
-  if (!q || !P_values || !qvec || !A_values || !l || !u || !settings || !x || !info)
+  if (!q)
     return THIP_E_INVALID;
   const int n = q->n, m = q->m, B = q->batch;
+  // (an empty P -- a linear objective -- or an empty A may come with NULL values)
+  if ((!P_values && q->nnz_p) || !qvec || (!A_values && q->nnz_a) || (m && (!l || !u)) || !settings || !x || !info)
+  {
+    q->err = "thip_qp_solve: null argument";
+    return THIP_E_INVALID;
+  }
   if (settings->max_iter < 1 || settings->check_termination < 0 || settings->scaling < 0 ||
       !(settings->alpha > 0 && settings->alpha < 2) || !(settings->sigma > 0) || !(settings->rho > 0) ||
       !(settings->delta > 0))

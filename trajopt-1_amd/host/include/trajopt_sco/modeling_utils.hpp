@@ -61,6 +61,12 @@ public:
 
 // num_diff.cpp: forward differences (f(x + eps e_i) - f(x)) / eps
 Mat calcForwardNumJac(const VectorOfVector& f, const DblVec& x, double epsilon);
+DblVec calcForwardNumGrad(const ScalarOfVector& f, const DblVec& x, double epsilon);
+// num_diff.cpp:70-105: central gradient + diagonal Hessian; forward gradient + symmetrised
+// forward Jacobian of it
+void calcGradAndDiagHess(const ScalarOfVector& f, const DblVec& x, double epsilon, double& y, DblVec& grad,
+                         DblVec& hess);
+void calcGradHess(const ScalarOfVector& f, const DblVec& x, double epsilon, double& y, DblVec& grad, Mat& hess);
 
 enum PenaltyType : std::uint8_t
 {
@@ -71,6 +77,23 @@ enum PenaltyType : std::uint8_t
 
 // modeling_utils.cpp:31-39: constant = y - dydx . x, cleanupAff
 AffExpr affFromValGrad(double y, const DblVec& x, const DblVec& dydx, const VarVector& vars);
+
+// modeling_utils.cpp:41-117: a scalar cost, convexified by its numerical
+// gradient and the positive part of its (diagonal or full) numerical Hessian
+class CostFromFunc : public Cost
+{
+public:
+  CostFromFunc(ScalarOfVector::Ptr f, VarVector vars, const std::string& name, bool full_hessian = false);
+  double value(const DblVec& x) override;
+  ConvexObjective::Ptr convex(const DblVec& x, Model* model) override;
+  VarVector getVars() override { return vars_; }
+
+protected:
+  ScalarOfVector::Ptr f_;
+  VarVector vars_;
+  bool full_hessian_;
+  double epsilon_{ DEFAULT_EPSILON };
+};
 
 class CostFromErrFunc : public Cost
 {

@@ -66,6 +66,44 @@ int thost_lower_json(const char* json_text, const double* scene, int n_prims, th
   }
 }
 
+int thost_solve_json(const char* json_text, const double* scene, int n_prims, int device, double* x,
+                     thip_result* result, int* native, char* err, int err_len)
+{
+  try
+  {
+    if (!x)
+      throw std::runtime_error("thost_solve_json: null x");
+    auto prob = construct(json_text, scene, n_prims);
+    const bool lowered = prob->lowerable();
+    trajopt::BasicTrustRegionSQP opt(prob, device);
+    opt.initialize(trajopt::trajToDblVec(prob->GetInitTraj()));
+    opt.optimize();
+    const sco::OptResults& r = opt.results();
+    std::copy(r.x.begin(), r.x.end(), x);
+    if (result)
+    {
+      std::memset(result, 0, sizeof(*result));
+      result->status = static_cast<int>(r.status);
+      result->n_sqp_iters = r.n_sqp_iters;
+      result->n_qp_solves = r.n_qp_solves;
+      result->n_func_evals = r.n_func_evals;
+      result->n_admm_iters = r.n_admm_iters;
+      result->total_cost = r.total_cost;
+      result->max_cnt_viol = r.max_cnt_viol;
+      result->flags = r.flags;
+    }
+    if (native)
+      *native = lowered ? 1 : 0;
+    setErr(err, err_len, "");
+    return 0;
+  }
+  catch (const std::exception& e)
+  {
+    setErr(err, err_len, e.what());
+    return -1;
+  }
+}
+
 int thost_solve_json_batch(const char* const* json_texts, int batch, const double* scenes, int n_prims, int device,
                            double* x, thip_result* results, char* err, int err_len)
 {

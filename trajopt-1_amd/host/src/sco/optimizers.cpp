@@ -9,6 +9,7 @@
 #include <stdexcept>
 
 #include "trajopt_sco/expr_ops.hpp"
+#include "trajopt_sco/gpu_model.hpp"
 
 namespace sco
 {
@@ -397,6 +398,8 @@ cleanup:
   results_.status = retval;
   results_.total_cost = vecSum(results_.cost_vals);
   results_.max_cnt_viol = results_.cnt_viols.empty() ? 0.0 : vecMax(results_.cnt_viols);
+  if (const auto* gm = dynamic_cast<const GpuModel*>(model_.get()))
+    results_.n_admm_iters = gm->admmItersTotal();
   callCallbacks();
   for (std::FILE* f : { log_solver, log_vars, log_costs, log_cnts })
     if (f)

@@ -39,6 +39,9 @@ def load_host():
         L.thost_solve_json_batch.argtypes = [C.POINTER(C.c_char_p), C.c_int, dp, C.c_int, C.c_int, dp,
                                              C.POINTER(abi.Result), C.c_char_p, C.c_int]
         L.thost_solve_json_batch.restype = C.c_int
+        L.thost_solve_json.argtypes = [C.c_char_p, dp, C.c_int, C.c_int, dp, C.POINTER(abi.Result),
+                                       C.POINTER(C.c_int), C.c_char_p, C.c_int]
+        L.thost_solve_json.restype = C.c_int
         _host = L
     return _host
 
@@ -83,6 +86,25 @@ def solve_json_batch(texts, scenes=None, device=0):
     if rc != 0:
         raise HostError(err.value.decode())
     return x, list(res)
+
+
+def solve_json(text: str, scene=None, device=0):
+    """-> (x [N, D], abi.Result, native) through trajopt::BasicTrustRegionSQP:
+    native is True when the problem ran the fused kernel as a batch of one,
+    False when it ran the host SQP loop with the GpuModel's QPs."""
+    L = load_host()
+    desc, _, _, _ = lower_json(text, scene)
+    N, D = desc.n_steps, desc.chain.n_dof
+    sc = None if scene is None or len(scene) == 0 else np.ascontiguousarray(scene, dtype=np.float64)
+    n_prims = 0 if sc is None else sc.shape[0]
+    x = np.zeros((N, D))
+    res = abi.Result()
+    native = C.c_int(-1)
+    err = C.create_string_buffer(4096)
+    rc = L.thost_solve_json(text.encode(), _dp(sc), n_prims, device, _dp(x), C.byref(res), C.byref(native), err, 4096)
+    if rc != 0:
+        raise HostError(err.value.decode())
+    return x, res, bool(native.value)
 
 
 def _quat_wxyz(R):
