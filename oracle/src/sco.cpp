@@ -261,7 +261,8 @@ bool OSQPModel::updateObjective(bool check_sparsity)
   {
     eq = true;
     eq = eq && std::memcmp(P_.p.data(), P.p.data(), static_cast<std::size_t>(P_.n) + 1) == 0;
-    eq = eq && std::memcmp(P_.i.data(), P.i.data(), static_cast<std::size_t>(P_.nnz())) == 0;
+    // (an empty P compares equal; memcmp is not called on its null data)
+    eq = eq && (P_.nnz() == 0 || std::memcmp(P_.i.data(), P.i.data(), static_cast<std::size_t>(P_.nnz())) == 0);
   }
   n_ = n;
   P_ = std::move(P);

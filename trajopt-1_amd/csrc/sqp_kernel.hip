@@ -3410,7 +3410,8 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
 // (LI b, forward chain, LI^T y + middle, backward chain) by two.
 constexpr int kSegHalf = THIP_MAX_STEPS / 4;  // steps per half: N <= 32 on the segment
 static_assert(kSegHalf * 2 * 8 >= kBlock, "segment halves cover N <= 32");
-constexpr int kSegChunk = 8;  // blocks streamed from LDS per wait
+constexpr int kSegGroup = 4;  // forward steps whose blocks are loaded one group ahead
+static_assert(kSegHalf % kSegGroup == 0 && kSegHalf % 8 == 0, "chain groups");
 
 // Per-lane LDS addresses of the chain's block elements, fixed for a segment:
 // element (i, k) (ROW-output steps) or (k, i) (COL-output steps) of the block
@@ -3418,6 +3419,7 @@ constexpr int kSegChunk = 8;  // blocks streamed from LDS per wait
 struct SegChain
 {
   unsigned li_n, li_t, mf_n, mf_t, nb_n, nb_t;  // LDS byte addresses at r = 0
+  unsigned zero;                                // LDS byte address of a 0.0
   int stride;                                   // bytes per step (the block stride, signed by the half)
   double mli, mm, mnb;                          // LI_m, M_m, M'_m elements (ROW output)
   int R;                                        // steps in this wave's half (0 off the chain waves)
@@ -3439,6 +3441,7 @@ __device__ __forceinline__ void seg_chain_init(const Ctx& c, const Solver& sv, c
   const int tdir = (c.wave == 0) ? -1 : 1;
   ch.stride = act ? tdir * DD * 8 : 0;
   const unsigned z = lds_addr(zero);
+  ch.zero = z;
   const unsigned li = lds_addr(c.a(A_LINV) + t0 * DD), mf = lds_addr(sv.M + t0 * DD), nb = lds_addr(sv.Nb + t0 * DD);
   ch.li_n = act ? li + offN * 8 : z;
   ch.li_t = act ? li + offT * 8 : z;
@@ -3459,10 +3462,14 @@ __device__ __forceinline__ double lds_at(unsigned a) { return *(const lds_f64*)(
 
 // x = K^-1 b: b in BV (written by the segment's phase B), x into XV.  Ends with
 // every wave past a workgroup barrier; BV's rows m - 1 and m + 1 carry the
-// halves' y to the middle.  The blocks of kSegChunk steps are loaded, and
-// waited for once, before the chunk's serial steps (sched_barrier: left to
-// itself the scheduler sinks loads and their address arithmetic onto the
-// dependent steps).
+// halves' y to the middle.
+// Both halves run kSegHalf steps with no branches: the steps r >= R of a
+// shorter half read zero blocks (address `zero`) and produce exact zeros, so
+// y enters the first real step as 0 (the recurrence's start) and the real
+// steps' arithmetic is unchanged.  Forward: the blocks of the next group of
+// kSegGroup steps are loaded while the current group runs, in consumption
+// order (the LDS returns in order, so each step waits only for its own three
+// loads).  Backward: one load per step, all issued up front.
 __device__ __forceinline__ void seg_chain_solve(const Ctx& c, const SegChain& ch, double* BVp, double* XVp,
                                                 long long& lap_fwd, long long& lap_bwd, long long* pf, long long& tq)
 {
@@ -3471,45 +3478,50 @@ __device__ __forceinline__ void seg_chain_solve(const Ctx& c, const SegChain& ch
   const int ic = (i < D) ? i : D - 1, kc = (k < D) ? k : D - 1;
   lds_f64* BV = lds(BVp);
   lds_f64* XV = lds(XVp);
-  const int R = __builtin_amdgcn_readfirstlane(ch.R);  // wave-uniform: guards are scalar branches
+  const int R = __builtin_amdgcn_readfirstlane(ch.R);  // wave-uniform
   const int tdir = (c.wave == 0) ? -1 : 1;             // t = m + tdir * (1 + r)
   // b of step r, in the lane's layout: COL-output steps (even r) take b[i], ROW (odd r) b[k]
   const unsigned b0 = lds_addr(BVp + (m + tdir) * D);
   const unsigned b_e = b0 + ic * 8, b_o = b0 + kc * 8;
   const int bstride = tdir * D * 8;
+  const unsigned zero = ch.zero;
   double q[kSegHalf];
-  if (R > 0)
+  if (c.wave < 2)
   {
+    double li[kSegHalf], mf[kSegHalf], lb[kSegHalf];
+    auto load = [&](int r) {
+      const bool on = r < R;
+      const bool odd = r & 1;
+      li[r] = lds_at(on ? (odd ? ch.li_n : ch.li_t) + r * ch.stride : zero);
+      mf[r] = lds_at(on ? (odd ? ch.mf_n : ch.mf_t) + r * ch.stride : zero);
+      lb[r] = lds_at(on ? (odd ? b_o : b_e) + r * bstride : zero);
+    };
     double y = 0.0;
 #pragma unroll
-    for (int r1 = kSegHalf - kSegChunk; r1 >= 0; r1 -= kSegChunk)
-    {
-      if (r1 >= R)
-        continue;
-      double li[kSegChunk], mf[kSegChunk], lb[kSegChunk];
+    for (int u = 0; u < kSegGroup; ++u)
+      load(kSegHalf - 1 - u);
 #pragma unroll
-      for (int u = 0; u < kSegChunk; ++u)
+    for (int g = 0; g < kSegHalf / kSegGroup; ++g)
+    {
+      if (g + 1 < kSegHalf / kSegGroup)
       {
-        const int r = r1 + u;
-        const bool odd = r & 1;
-        li[u] = lds_at((odd ? ch.li_n : ch.li_t) + r * ch.stride);
-        mf[u] = lds_at((odd ? ch.mf_n : ch.mf_t) + r * ch.stride);
-        lb[u] = lds_at((odd ? b_o : b_e) + r * bstride);
+#pragma unroll
+        for (int u = 0; u < kSegGroup; ++u)
+          load(kSegHalf - 1 - kSegGroup * (g + 1) - u);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int u = kSegChunk - 1; u >= 0; --u)
-        if (r1 + u < R)
-        {
-          const int r = r1 + u;
-          const double p = fma(-mf[u], y, li[u] * lb[u]);
-          y = (r & 1) ? octet_sum(p) : cross_octet_sum(p);
-          q[r] = li[u] * y;  // the backward step's LI^T y term
-        }
+      for (int u = 0; u < kSegGroup; ++u)
+      {
+        const int r = kSegHalf - 1 - kSegGroup * g - u;
+        const double p = fma(-mf[r], y, li[r] * lb[r]);
+        y = (r & 1) ? octet_sum(p) : cross_octet_sum(p);
+        q[r] = li[r] * y;  // the backward step's LI^T y term
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     // y_{m -+ 1} (COL layout) to the middle
-    if (i == 0 && k < D)
+    if (R > 0 && i == 0 && k < D)
       BV[(m + tdir) * D + k] = y;
   }
   BSYNC();
@@ -3521,54 +3533,46 @@ __device__ __forceinline__ void seg_chain_solve(const Ctx& c, const SegChain& ch
   }
   if (c.wave < 2)
   {
+    // the middle's operands first: the LDS returns in order
     const bool top = m > 0, bot = N - 1 - m > 0;
-    const double ym1 = top ? BV[(m - 1) * D + kc] : 0.0;
-    const double yp1 = bot ? BV[(m + 1) * D + kc] : 0.0;
+    const double ym1 = BV[(top ? m - 1 : m) * D + kc];
+    const double yp1 = BV[(bot ? m + 1 : m) * D + kc];
     const double bm = BV[m * D + kc];
+    __builtin_amdgcn_sched_barrier(0);
+    double nb[kSegHalf];
+#pragma unroll
+    for (int r = 0; r < kSegHalf; ++r)
+      nb[r] = lds_at(r < R ? ((r & 1) ? ch.nb_t : ch.nb_n) + r * ch.stride : zero);
+    __builtin_amdgcn_sched_barrier(0);
+    // (mm / mnb are 0 on a missing half: the reads above stay in bounds)
     const double p = fma(-ch.mnb, yp1, fma(-ch.mm, ym1, ch.mli * bm));
     const double ym = octet_sum(p);           // ROW
     double x = cross_octet_sum(ch.mli * ym);  // x_m, COL
     if (c.wave == 0 && i == 0 && k < D)
       XV[m * D + k] = x;
+    __builtin_amdgcn_sched_barrier(0);
+    double xs[kSegHalf];
 #pragma unroll
-    for (int r1 = 0; r1 < kSegHalf; r1 += kSegChunk)
+    for (int r = 0; r < kSegHalf; ++r)
     {
-      if (r1 >= R)
-        continue;
-      double nb[kSegChunk];
-#pragma unroll
-      for (int u = 0; u < kSegChunk; ++u)
-      {
-        const int r = r1 + u;
-        nb[u] = lds_at(((r & 1) ? ch.nb_t : ch.nb_n) + r * ch.stride);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      double xs[kSegChunk];
-#pragma unroll
-      for (int u = 0; u < kSegChunk; ++u)
-        if (r1 + u < R)
-        {
-          const int r = r1 + u;
-          const double p2 = fma(-nb[u], x, q[r]);
-          x = (r & 1) ? cross_octet_sum(p2) : octet_sum(p2);
-          xs[u] = x;
-        }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int u = 0; u < kSegChunk; ++u)
-        if (r1 + u < R)
-        {
-          const int r = r1 + u;
-          const int t = m + tdir * (1 + r);
-          if (r & 1)
-          {
-            if (i == 0 && k < D)
-              XV[t * D + k] = xs[u];
-          }
-          else if (k == 0 && i < D)
-            XV[t * D + i] = xs[u];
-        }
+      const double p2 = fma(-nb[r], x, q[r]);
+      x = (r & 1) ? cross_octet_sum(p2) : octet_sum(p2);
+      xs[r] = x;
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < kSegHalf; ++r)
+      if (r < R)
+      {
+        const int t = m + tdir * (1 + r);
+        if (r & 1)
+        {
+          if (i == 0 && k < D)
+            XV[t * D + k] = xs[r];
+        }
+        else if (k == 0 && i < D)
+          XV[t * D + i] = xs[r];
+      }
   }
   BSYNC();
   if (pf)
