@@ -17,6 +17,17 @@ constexpr int kWaves = kBlock / 64;
 // dynamic LDS a problem may use (160 KB per CU on gfx950, one workgroup per
 // CU; the rest is the kernel's static LDS)
 constexpr long long kLdsBudgetBytes = 149 * 1024;
+// ADMM-segment chain pack (A_CPK), per half h (0: top, 1: bottom) and chain
+// step r (distance from the middle block), in the lane order the octet chain
+// reads it, zero past the half's length and outside the D x D block:
+//   kCpkLM   [2][16][64][2]  (LI, M) pairs of the forward pass (16 B per lane)
+//   kCpkNB   [2][16][64]     N' blocks of the backward pass
+//   kCpkB    [2][16][8]      right-hand side of the forward pass
+//   kCpkBM   [8]             right-hand side of the middle block
+//   kCpkYM   [2][8]          the halves' last y, handed to the middle
+constexpr int kCpkSteps = 16;
+constexpr int kCpkLM = 0, kCpkNB = kCpkLM + 2 * kCpkSteps * 64 * 2, kCpkB = kCpkNB + 2 * kCpkSteps * 64,
+              kCpkBM = kCpkB + 2 * kCpkSteps * 8, kCpkYM = kCpkBM + 8, kCpk = kCpkYM + 16;
 // CartPose rows per waypoint the register-resident ADMM segment supports
 constexpr int kMaxStepRows = 8;
 // LVS sub-states per step pair the contact scan supports (sphere-center
@@ -94,6 +105,7 @@ enum DArr : int
   A_HCHK,    // hinge chunk table: (first row, end row) int pairs, one double per chunk
   A_HPART,   // hinge chunk partial sums [n_chunks][16]
   A_HCT,     // ADMM-segment copy of A_HC, field-major [2D][n_h | 1] (odd stride: no LDS bank conflicts)
+  A_CPK,     // ADMM-segment chain pack (kCpk doubles, N <= 32 and D <= 8; see seg_chain_solve)
   A_COUNT
 };
 

@@ -3408,122 +3408,156 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
 // reads y_{m-1}, y_{m+1}, b_m in COL layout, so both waves compute it
 // identically.  This replaces reduced_solve's four barrier-separated passes
 // (LI b, forward chain, LI^T y + middle, backward chain) by two.
-constexpr int kSegHalf = THIP_MAX_STEPS / 4;  // steps per half: N <= 32 on the segment
-static_assert(kSegHalf * 2 * 8 >= kBlock, "segment halves cover N <= 32");
-constexpr int kSegGroup = 4;  // forward steps whose blocks are loaded one group ahead
-static_assert(kSegHalf % kSegGroup == 0 && kSegHalf % 8 == 0, "chain groups");
+static_assert(kCpkSteps * 2 * 8 >= kBlock, "segment halves cover N <= 32");
 
-// Per-lane LDS addresses of the chain's block elements, fixed for a segment:
-// element (i, k) (ROW-output steps) or (k, i) (COL-output steps) of the block
-// at step r is at base + r * stride; lanes outside the D x D block read a zero.
+// The middle block's elements in the lane's layout (ROW output), fixed for a
+// segment, and the half's length.
 struct SegChain
 {
-  unsigned li_n, li_t, mf_n, mf_t, nb_n, nb_t;  // LDS byte addresses at r = 0
-  unsigned zero;                                // LDS byte address of a 0.0
-  int stride;                                   // bytes per step (the block stride, signed by the half)
-  double mli, mm, mnb;                          // LI_m, M_m, M'_m elements (ROW output)
-  int R;                                        // steps in this wave's half (0 off the chain waves)
+  double mli, mm, mnb;  // LI_m, M_m, M'_m elements
+  int R;                // steps in this wave's half (0 off the chain waves)
+  int D, m, lane, wave;
+  lds_f64* P;           // the chain pack (A_CPK)
+  lds_f64* XV;          // x out (A_CV)
 };
 
-__device__ __forceinline__ unsigned lds_addr(const double* p)
-{
-  return (unsigned)(unsigned long)lds(p);
-}
-
-__device__ __forceinline__ void seg_chain_init(const Ctx& c, const Solver& sv, const double* zero, SegChain& ch)
+// Fill the chain pack (layout.hpp kCpk*) from the factor's blocks: step r of
+// half h is waypoint t = m - 1 - r (h = 0) or m + 1 + r (h = 1); lane (i, k)
+// of a COL-output step (even r) holds element (k, i) of LI_t and M_t, of a
+// ROW-output step (odd r) element (i, k); the backward block N'_t the other
+// way round.  Entries past the half's length, outside the D x D block, and the
+// right-hand-side slots are zero.  All threads; ends with a barrier.
+__device__ void seg_chain_pack(const Ctx& c, const Solver& sv, SegChain& ch)
 {
   const int D = c.L.D, DD = D * D, N = c.L.N, m = c.L.tw_mid;
-  const int i = c.lane >> 3, k = c.lane & 7;
-  const bool act = (i < D) && (k < D);
-  const int offN = i * D + k, offT = k * D + i;
-  ch.R = (c.wave == 0) ? m : (c.wave == 1 ? N - 1 - m : 0);
-  const int t0 = (c.wave == 0) ? m - 1 : m + 1;  // r = 0
-  const int tdir = (c.wave == 0) ? -1 : 1;
-  ch.stride = act ? tdir * DD * 8 : 0;
-  const unsigned z = lds_addr(zero);
-  ch.zero = z;
-  const unsigned li = lds_addr(c.a(A_LINV) + t0 * DD), mf = lds_addr(sv.M + t0 * DD), nb = lds_addr(sv.Nb + t0 * DD);
-  ch.li_n = act ? li + offN * 8 : z;
-  ch.li_t = act ? li + offT * 8 : z;
-  ch.mf_n = act ? mf + offN * 8 : z;
-  ch.mf_t = act ? mf + offT * 8 : z;
-  ch.nb_n = act ? nb + offN * 8 : z;
-  ch.nb_t = act ? nb + offT * 8 : z;
+  lds_f64* P = lds(c.a(A_CPK));
   const lds_f64* LI = lds(c.a(A_LINV));
   const lds_f64* M = lds(sv.M);
   const lds_f64* Nb = lds(sv.Nb);
-  const bool top = m > 0, bot = N - 1 - m > 0;
-  ch.mli = act ? LI[m * DD + offN] : 0.0;
-  ch.mm = (act && top) ? M[m * DD + offN] : 0.0;
-  ch.mnb = (act && bot) ? Nb[m * DD + offN] : 0.0;
+  const int Rh[2] = { m, N - 1 - m };
+  for (int e = c.tid; e < 2 * kCpkSteps * 64; e += kBlock)
+  {
+    const int h = e / (kCpkSteps * 64), r = (e / 64) % kCpkSteps, lane = e & 63;
+    const int i = lane >> 3, k = lane & 7;
+    double li = 0.0, mf = 0.0, nb = 0.0;
+    if (r < Rh[h] && i < D && k < D)
+    {
+      const int t = (h == 0) ? m - 1 - r : m + 1 + r;
+      const int offN = t * DD + i * D + k, offT = t * DD + k * D + i;
+      li = LI[(r & 1) ? offN : offT];
+      mf = M[(r & 1) ? offN : offT];
+      nb = Nb[(r & 1) ? offT : offN];
+    }
+    P[kCpkLM + 2 * e] = li;
+    P[kCpkLM + 2 * e + 1] = mf;
+    P[kCpkNB + e] = nb;
+  }
+  for (int e = c.tid; e < kCpk - kCpkB; e += kBlock)
+    P[kCpkB + e] = 0.0;
+  {
+    const int i = c.lane >> 3, k = c.lane & 7;
+    const bool act = (i < D) && (k < D);
+    const int offN = i * D + k;
+    ch.R = (c.wave < 2) ? Rh[c.wave] : 0;
+    ch.D = D;
+    ch.m = m;
+    ch.lane = c.lane;
+    ch.wave = c.wave;
+    ch.P = P;
+    ch.XV = lds(c.a(A_CV));
+    const bool top = m > 0, bot = N - 1 - m > 0;
+    ch.mli = act ? LI[m * DD + offN] : 0.0;
+    ch.mm = (act && top) ? M[m * DD + offN] : 0.0;
+    ch.mnb = (act && bot) ? Nb[m * DD + offN] : 0.0;
+  }
+  BSYNC();
 }
 
-__device__ __forceinline__ double lds_at(unsigned a) { return *(const lds_f64*)(unsigned long)a; }
-
-// x = K^-1 b: b in BV (written by the segment's phase B), x into XV.  Ends with
-// every wave past a workgroup barrier; BV's rows m - 1 and m + 1 carry the
-// halves' y to the middle.
-// Both halves run kSegHalf steps with no branches: the steps r >= R of a
-// shorter half read zero blocks (address `zero`) and produce exact zeros, so
-// y enters the first real step as 0 (the recurrence's start) and the real
-// steps' arithmetic is unchanged.  Forward: the blocks of the next group of
-// kSegGroup steps are loaded while the current group runs, in consumption
-// order (the LDS returns in order, so each step waits only for its own three
-// loads).  Backward: one load per step, all issued up front.
-__device__ __forceinline__ void seg_chain_solve(const Ctx& c, const SegChain& ch, double* BVp, double* XVp,
-                                                long long& lap_fwd, long long& lap_bwd, long long* pf, long long& tq)
+// the pack slot of column (t, i)'s right-hand side (phase B writes it there)
+__device__ __forceinline__ int seg_b_slot(int t, int i, int m)
 {
-  const int D = c.L.D, N = c.L.N, m = c.L.tw_mid;
-  const int i = c.lane >> 3, k = c.lane & 7;
+  if (t < m)
+    return kCpkB + (m - 1 - t) * 8 + i;
+  if (t > m)
+    return kCpkB + kCpkSteps * 8 + (t - m - 1) * 8 + i;
+  return kCpkBM + i;
+}
+
+// x = K^-1 b: b in the pack (phase B), x into XV.  Ends with every wave past a
+// workgroup barrier.  Both halves run kCpkSteps steps with no branches: the
+// steps r >= R of a shorter half read zero blocks and a zero right-hand side
+// and produce exact zeros, so y enters the first real step as 0 (the
+// recurrence's start) and the real steps' arithmetic is unchanged.  Every load
+// is one LDS instruction from a per-lane base with an immediate offset (the
+// pack's lane order), and the forward pass loads the (LI, M) pair of a step
+// as one 16-byte read; the next group of kSegGroup steps is loaded while the
+// current group runs.
+constexpr int kSegGroup = 4;
+static_assert(kCpkSteps % kSegGroup == 0, "chain groups");
+typedef __attribute__((ext_vector_type(2))) double dbl2;
+typedef __attribute__((address_space(3))) dbl2 lds_dbl2;
+
+__device__ __forceinline__ void seg_chain_solve(const SegChain& ch, long long& lap_fwd, long long& lap_bwd,
+                                                long long* pf, long long& tq, long long& own_fwd, long long& own_bwd)
+{
+  const int D = ch.D, m = ch.m, lane = ch.lane, wave = ch.wave;
+  const int i = lane >> 3, k = lane & 7;
   const int ic = (i < D) ? i : D - 1, kc = (k < D) ? k : D - 1;
-  lds_f64* BV = lds(BVp);
-  lds_f64* XV = lds(XVp);
+  lds_f64* P = ch.P;
+  lds_f64* XV = ch.XV;
   const int R = __builtin_amdgcn_readfirstlane(ch.R);  // wave-uniform
-  const int tdir = (c.wave == 0) ? -1 : 1;             // t = m + tdir * (1 + r)
-  // b of step r, in the lane's layout: COL-output steps (even r) take b[i], ROW (odd r) b[k]
-  const unsigned b0 = lds_addr(BVp + (m + tdir) * D);
-  const unsigned b_e = b0 + ic * 8, b_o = b0 + kc * 8;
-  const int bstride = tdir * D * 8;
-  const unsigned zero = ch.zero;
-  double q[kSegHalf];
-  if (c.wave < 2)
+  const int h = (wave == 1) ? 1 : 0;
+  const int tdir = (wave == 0) ? -1 : 1;               // t = m + tdir * (1 + r)
+  double q[kCpkSteps];
+  double y = 0.0;
+  if (wave < 2)
   {
-    double li[kSegHalf], mf[kSegHalf], lb[kSegHalf];
+    const lds_dbl2* LMp = (const lds_dbl2*)(P + kCpkLM + h * kCpkSteps * 128) + lane;  // + r * 64
+    const lds_f64* Be = P + kCpkB + h * kCpkSteps * 8 + ic;                              // + r * 8, even r
+    const lds_f64* Bo = P + kCpkB + h * kCpkSteps * 8 + kc;                              // odd r
+    dbl2 lm[kCpkSteps];
+    double lb[kCpkSteps];
     auto load = [&](int r) {
-      const bool on = r < R;
-      const bool odd = r & 1;
-      li[r] = lds_at(on ? (odd ? ch.li_n : ch.li_t) + r * ch.stride : zero);
-      mf[r] = lds_at(on ? (odd ? ch.mf_n : ch.mf_t) + r * ch.stride : zero);
-      lb[r] = lds_at(on ? (odd ? b_o : b_e) + r * bstride : zero);
+      lm[r] = LMp[r * 64];
+      lb[r] = (r & 1) ? Bo[r * 8] : Be[r * 8];
     };
-    double y = 0.0;
 #pragma unroll
     for (int u = 0; u < kSegGroup; ++u)
-      load(kSegHalf - 1 - u);
+      load(kCpkSteps - 1 - u);
 #pragma unroll
-    for (int g = 0; g < kSegHalf / kSegGroup; ++g)
+    for (int g = 0; g < kCpkSteps / kSegGroup; ++g)
     {
-      if (g + 1 < kSegHalf / kSegGroup)
+      if (g + 1 < kCpkSteps / kSegGroup)
       {
 #pragma unroll
         for (int u = 0; u < kSegGroup; ++u)
-          load(kSegHalf - 1 - kSegGroup * (g + 1) - u);
+          load(kCpkSteps - 1 - kSegGroup * (g + 1) - u);
+      }
+      // the LI_t b_t products of the group, off the serial path
+      double lib[kSegGroup];
+#pragma unroll
+      for (int u = 0; u < kSegGroup; ++u)
+      {
+        const int r = kCpkSteps - 1 - kSegGroup * g - u;
+        lib[u] = lm[r].x * lb[r];
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < kSegGroup; ++u)
       {
-        const int r = kSegHalf - 1 - kSegGroup * g - u;
-        const double p = fma(-mf[r], y, li[r] * lb[r]);
+        const int r = kCpkSteps - 1 - kSegGroup * g - u;
+        const double p = fma(-lm[r].y, y, lib[u]);
         y = (r & 1) ? octet_sum(p) : cross_octet_sum(p);
-        q[r] = li[r] * y;  // the backward step's LI^T y term
+        q[r] = lm[r].x * y;  // the backward step's LI^T y term
       }
       __builtin_amdgcn_sched_barrier(0);
     }
     // y_{m -+ 1} (COL layout) to the middle
-    if (R > 0 && i == 0 && k < D)
-      BV[(m + tdir) * D + k] = y;
+    if (i == 0 && k < D)
+      P[kCpkYM + h * 8 + k] = y;
   }
+  if (pf)
+    own_fwd += clock64() - tq;  // wave 0's own forward half, without the barrier
   BSYNC();
   if (pf)
   {
@@ -3531,29 +3565,29 @@ __device__ __forceinline__ void seg_chain_solve(const Ctx& c, const SegChain& ch
     lap_fwd += tn - tq;
     tq = tn;
   }
-  if (c.wave < 2)
+  if (wave < 2)
   {
-    // the middle's operands first: the LDS returns in order
-    const bool top = m > 0, bot = N - 1 - m > 0;
-    const double ym1 = BV[(top ? m - 1 : m) * D + kc];
-    const double yp1 = BV[(bot ? m + 1 : m) * D + kc];
-    const double bm = BV[m * D + kc];
+    // the middle's operands first: the LDS returns in order (a missing half
+    // has a zero hand-off slot and a zero M_m / M'_m)
+    const double ym1 = P[kCpkYM + kc];
+    const double yp1 = P[kCpkYM + 8 + kc];
+    const double bm = P[kCpkBM + kc];
     __builtin_amdgcn_sched_barrier(0);
-    double nb[kSegHalf];
+    const lds_f64* NBp = P + kCpkNB + h * kCpkSteps * 64 + lane;  // + r * 64
+    double nb[kCpkSteps];
 #pragma unroll
-    for (int r = 0; r < kSegHalf; ++r)
-      nb[r] = lds_at(r < R ? ((r & 1) ? ch.nb_t : ch.nb_n) + r * ch.stride : zero);
+    for (int r = 0; r < kCpkSteps; ++r)
+      nb[r] = NBp[r * 64];
     __builtin_amdgcn_sched_barrier(0);
-    // (mm / mnb are 0 on a missing half: the reads above stay in bounds)
     const double p = fma(-ch.mnb, yp1, fma(-ch.mm, ym1, ch.mli * bm));
     const double ym = octet_sum(p);           // ROW
     double x = cross_octet_sum(ch.mli * ym);  // x_m, COL
-    if (c.wave == 0 && i == 0 && k < D)
+    if (wave == 0 && i == 0 && k < D)
       XV[m * D + k] = x;
     __builtin_amdgcn_sched_barrier(0);
-    double xs[kSegHalf];
+    double xs[kCpkSteps];
 #pragma unroll
-    for (int r = 0; r < kSegHalf; ++r)
+    for (int r = 0; r < kCpkSteps; ++r)
     {
       const double p2 = fma(-nb[r], x, q[r]);
       x = (r & 1) ? cross_octet_sum(p2) : octet_sum(p2);
@@ -3561,7 +3595,7 @@ __device__ __forceinline__ void seg_chain_solve(const Ctx& c, const SegChain& ch
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < kSegHalf; ++r)
+    for (int r = 0; r < kCpkSteps; ++r)
       if (r < R)
       {
         const int t = m + tdir * (1 + r);
@@ -3574,6 +3608,8 @@ __device__ __forceinline__ void seg_chain_solve(const Ctx& c, const SegChain& ch
           XV[t * D + i] = xs[r];
       }
   }
+  if (pf)
+    own_bwd += clock64() - tq;
   BSYNC();
   if (pf)
   {
@@ -3600,6 +3636,10 @@ template <int CS, int AS>
 __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
 {
   PROF(0);
+  // the Ctx fields the iterations use, in registers: the Ctx itself lives in
+  // private memory and is re-read with dependent FLAT loads after every store
+  // the compiler cannot prove does not alias it
+  const int tid = c.tid;
   const Layout& L = c.L;
   const int D = L.D, N = L.N, nx = L.nx, nfr = L.n_fixed_rows, nr = L.n_rows;
   const thip_osqp_settings& os = c.d->osqp;
@@ -3622,7 +3662,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
   // inequalities (u finite, l = -inf; bound row l = 0, u = +inf), so their
   // rho is the scalar rho (set_rho_vec) and only the finite bounds are kept.
   const double rho_s = c.s->rho, rho_si = 1.0 / rho_s;
-  for (int h = c.tid; h < nh; h += kBlock)
+  for (int h = tid; h < nh; h += kBlock)
   {
     const int rh = mb + 2 * h, rb = rh + 1, col = ncb + h;
     HP_(0) = Z[rh];
@@ -3650,7 +3690,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
   int* CHK = reinterpret_cast<int*>(c.a(A_HCHK));
   double* PART = c.a(A_HPART);
   const int nchk = build_hinge_chunks(c);
-  if (c.tid == 0)
+  if (tid == 0)
     c.s->cur = 0;
   // MR, the chunk table and the chunk sums are LDS-resident (qp_solve checks
   // it): ds_* instructions.  The pack and HCT are LDS-resident when the QP's
@@ -3665,7 +3705,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
   const bool pk_l = lds_resident(c, HPK), hct_l = lds_resident(c, HCT);
   // phase A, hinge rows: multipliers MR_h; rn, eta kept in the pack
   auto hinge_a = [&](auto PKP) {
-    for (int h = c.tid; h < nh; h += kBlock)
+    for (int h = tid; h < nh; h += kBlock)
     {
       const double zh = PKP[h], zb = PKP[nh + h], yh = PKP[2 * nh + h], yb = PKP[3 * nh + h];
       const double xa = PKP[4 * nh + h], dn = PKP[6 * nh + h], w = PKP[7 * nh + h], bs = PKP[8 * nh + h];
@@ -3680,10 +3720,10 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
   // phase B': hinge-row share of the waypoint rhs, row-parallel: 16 lanes
   // per chunk, lane k sums HC[h][k] * MR_h over the chunk's rows
   auto hinge_gather_seg = [&](auto HTP) {
-    const int k = c.tid & 15;
+    const int k = tid & 15;
     if (k < 2 * D)
 #pragma unroll 2
-      for (int q = c.tid >> 4; q < nchk; q += kBlock / 16)
+      for (int q = tid >> 4; q < nchk; q += kBlock / 16)
       {
         const int h0 = CHKl[2 * q], h1 = CHKl[2 * q + 1];
         double s0 = 0, s1 = 0;
@@ -3703,7 +3743,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
   // phase E, hinge rows: hinge variable, z~ = A x~, relaxed z/y/x updates
   // (admm_row_update with the infinite bound dropped)
   auto hinge_e = [&](auto PKP, auto HTP, bool last) {
-    for (int h = c.tid; h < nh; h += kBlock)
+    for (int h = tid; h < nh; h += kBlock)
     {
       // every pack field is read before any store (the stores could alias
       // them as far as the compiler knows)
@@ -3764,7 +3804,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
 #pragma unroll
   for (int u = 0; u < CS; ++u)
   {
-    const int q = c.tid + kBlock * u;
+    const int q = tid + kBlock * u;
     const int t = q >> 3, i = q & 7;
     cact[u] = (t < N) && (i < D);
     cfr[u] = -1;
@@ -3826,7 +3866,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
 #pragma unroll
   for (int u = 0; u < AS; ++u)
   {
-    const int a = c.tid + kBlock * u;
+    const int a = tid + kBlock * u;
     aact[u] = a < L.n_abs;
     if (aact[u])
     {
@@ -3868,19 +3908,23 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
     }
     adxn[u] = adxp[u] = adyr[u] = adybn[u] = adybp[u] = 0.0;
   }
-  // chain waves: the factor's blocks of their half, in registers
-  __shared__ double seg_zero;  // the chain's inactive lanes read this
-  if (c.tid == 0)
-    seg_zero = 0.0;
+  // the chain pack of this factorisation (ends with a barrier)
   SegChain ch;
-  seg_chain_init(c, sv, &seg_zero, ch);
-  BSYNC();
+  seg_chain_pack(c, sv, ch);
+  int cbslot[CS];  // pack slot of each owned column's right-hand side
+#pragma unroll
+  for (int u = 0; u < CS; ++u)
+  {
+    const int q = tid + kBlock * u;
+    cbslot[u] = seg_b_slot(q >> 3, q & 7, L.tw_mid);
+  }
+  lds_f64* const CPKl = lds(c.a(A_CPK));
 
   // phase laps accumulate in registers and are flushed once per segment
   // (a global read-modify-write per lap would stall wave 0 inside the loop)
-  long long* pf = (c.tid == 0) ? c.s->prof : nullptr;
+  long long* pf = (tid == 0) ? c.s->prof : nullptr;
   long long tq = pf ? clock64() : 0;
-  long long lap8 = 0, lap9 = 0, lap10 = 0, lap11 = 0, lap15 = 0, lap16 = 0, lap17 = 0, lap18 = 0;
+  long long lap8 = 0, lap9 = 0, lap10 = 0, lap11 = 0, lap15 = 0, lap16 = 0, lap17 = 0, lap18 = 0, lap34 = 0;
 #define SEG_LAP(acc)                  \
   if (pf)                             \
   {                                   \
@@ -3903,7 +3947,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
         arn[u] = bxn + absn[u] * ebn;
         arp[u] = bxp + absp[u] * ebp;
         const double dn = adn[u], dp = adp[u], wn = awn[u], wp = awp[u], rr = arr[u];
-        MRl[c.tid + kBlock * u] = (aeta[u] * dn * dp - rr * (wn * dp * arn[u] + wp * dn * arp[u])) * adeti[u];
+        MRl[tid + kBlock * u] = (aeta[u] * dn * dp - rr * (wn * dp * arn[u] + wp * dn * arp[u])) * adeti[u];
       }
     if (nh > 0)
     {
@@ -3943,19 +3987,19 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
             b += cgs[u][p] * MRl[crow[u][p]];
         if (nh > 0)
         {
-          const int j = (c.tid + kBlock * u) & 7;
+          const int j = (tid + kBlock * u) & 7;
           for (int q = chp1[u]; q < chp2[u]; ++q)
             b += PARTl[q * 16 + j];
           for (int q = chp0[u]; q < chp1[u]; ++q)
             b += PARTl[q * 16 + D + j];
         }
-        lds(YV)[ccol[u]] = b;
+        CPKl[cbslot[u]] = b;
       }
     }
     BSYNC();
     SEG_LAP(lap15);
     // x~ = K^-1 b into CV: forward halves, middle + backward halves
-    seg_chain_solve(c, ch, YV, CV, lap9, lap10, pf, tq);
+    seg_chain_solve(ch, lap9, lap10, pf, tq, lap16, lap34);
     // E: back-substitution, z~ = A x~, relaxed updates
     const bool last = (iter == n_iter - 1);
 #pragma unroll
@@ -4029,6 +4073,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
     pf[11] += lap11;
     pf[15] += lap15;
     pf[16] += lap16;
+    pf[34] += lap34;
     pf[17] += lap17;
     pf[18] += lap18;
   }
@@ -4047,8 +4092,8 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
 #pragma unroll
     for (int u = 0; u < AS; ++u)
       if (aact[u])
-        MRl[c.tid + kBlock * u] = ayr[u];
-    for (int h = c.tid; h < nh; h += kBlock)
+        MRl[tid + kBlock * u] = ayr[u];
+    for (int h = tid; h < nh; h += kBlock)
       MRl[nr + h] = HPK[2 * nh + h];
     BSYNC();
     if (nh > 0)
@@ -4127,7 +4172,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
             aty += cgs[u][p] * MRl[crow[u][p]];
         if (nh > 0)
         {
-          const int j = (c.tid + kBlock * u) & 7;
+          const int j = (tid + kBlock * u) & 7;
           for (int q = chp1[u]; q < chp2[u]; ++q)
             aty += PARTl[q * 16 + j];
           for (int q = chp0[u]; q < chp1[u]; ++q)
@@ -4139,7 +4184,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
     for (int u = 0; u < AS; ++u)
       if (aact[u])
       {
-        const int a = c.tid + kBlock * u;
+        const int a = tid + kBlock * u;
         const int r = nfr + a, ca = nx + 2 * a, brn = nr + ca, brp = brn + 1;
         const int t = at[u];
         double ax = 0;
@@ -4159,7 +4204,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
         inf_col(adxn[u], aqn[u], dn);
         inf_col(adxp[u], aqp[u], dp);
       }
-    for (int h = c.tid; h < nh; h += kBlock)
+    for (int h = tid; h < nh; h += kBlock)
     {
       const int rh = mb + 2 * h, col = ncb + h, t0 = static_cast<int>(HPK[12 * nh + h]);
       const double xh = HPK[4 * nh + h], wh = HPK[7 * nh + h], bsh = HPK[8 * nh + h];
@@ -4221,7 +4266,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
   for (int u = 0; u < AS; ++u)
     if (aact[u])
     {
-      const int a = c.tid + kBlock * u;
+      const int a = tid + kBlock * u;
       const int r = nfr + a, ca = nx + 2 * a, brn = nr + ca, brp = brn + 1;
       XA[ca] = axn[u];
       XA[ca + 1] = axp[u];
@@ -4237,7 +4282,7 @@ __device__ void admm_segment(Ctx& c, Solver& sv, int n_iter, Norms* res)
       Y[brp] = aybp[u];
       DY[brp] = adybp[u];
     }
-  for (int h = c.tid; h < nh; h += kBlock)
+  for (int h = tid; h < nh; h += kBlock)
   {
     const int rh = mb + 2 * h;
     Z[rh] = HP_(0);
@@ -4517,7 +4562,7 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   bool fail = false;
   const int ct = os.check_termination;
   // the segment addresses MR, the hinge chunk table and chunk sums as LDS
-  const bool seg = L.seg_ok && lds_resident(c, c.a(A_MR)) &&
+  const bool seg = L.seg_ok && lds_resident(c, c.a(A_MR)) && lds_resident(c, c.a(A_CPK)) &&
                    (c.s->n_h == 0 || (lds_resident(c, c.a(A_HCHK)) && lds_resident(c, c.a(A_HPART))));
   bool pre_ready = false;  // admm_step's ETA / BX (cleared when rho changes)
   for (it = 1; it <= os.max_iter; ++it)
@@ -4683,7 +4728,7 @@ __device__ void plan_lds_dynamic(Ctx& c)
     const long long NDD = (long long)L.N * D * D, nab = L.n_abs > 0 ? L.n_abs : 1;
     // the ADMM segment's working set first (chains, rhs, multipliers, the
     // hinge-row pack and coefficients), then the rest as in the host plan
-    const int order[] = { A_LINV, A_CV, A_YV, A_MR, A_HPART, A_HCHK, A_HCT, A_HPK, A_HC, A_BXW, A_BA, A_HW, A_HRE, A_DG, A_GS, A_WS,
+    const int order[] = { A_LINV, A_CV, A_YV, A_CPK, A_MR, A_HPART, A_HCHK, A_HCT, A_HPK, A_HC, A_BXW, A_BA, A_HW, A_HRE, A_DG, A_GS, A_WS,
                           A_FS,   A_BS, A_XA0, A_XA1, A_Z0, A_Z1, A_Y, A_XT, A_PZ, A_RHO, A_L,  A_U,  A_Q,
                           A_DX,   A_DY, A_PD,  A_PO,  A_E,  A_DS, A_RE, A_CPL, A_PB, A_PS, A_PR };
     long long used = L.lds_scratch;
@@ -4693,6 +4738,7 @@ __device__ void plan_lds_dynamic(Ctx& c)
       switch (k)
       {
         case A_LINV: case A_CPL: n = NDD; break;
+        case A_CPK: n = (L.loff[A_CPK] >= 0) ? kCpk : 0; break;  // the host plan's offset
         case A_CV: case A_YV: case A_PD: case A_PO: n = nx; break;
         case A_MR: n = L.n_rows + nh; break;
         case A_RE: n = L.n_rows; break;

@@ -568,6 +568,9 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   L.part_w = (2 * L.D <= 16) ? 16 : 32;
   sizes[A_HPART] = L.hinge ? nchk_cap * L.part_w : 1;
   sizes[A_HCT] = L.hinge ? 2 * D * (hc + 1) : 1;
+  // the segment's chain pack: narrow blocks and N <= 32 only (the segment's domain)
+  const bool cpk = !L.wide && L.N * 8 <= kBlock && L.N <= 2 * kCpkSteps;
+  sizes[A_CPK] = cpk ? kCpk : 1;
   for (int k = 0; k < A_COUNT; ++k)
     if (sizes[k] < 0)
     {
@@ -609,7 +612,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   // LDS residency plan: the per-ADMM-iteration working set, hottest first,
   // until the budget of one workgroup per CU is used; the rest stays in HBM.
   {
-    const int order[] = { A_LINV, A_CV,  A_YV, A_BXW, A_BA, A_MR, A_DG, A_GS, A_WS, A_FS, A_BS, A_XA0, A_XA1,
+    const int order[] = { A_LINV, A_CV,  A_YV, A_CPK, A_BXW, A_BA, A_MR, A_DG, A_GS, A_WS, A_FS, A_BS, A_XA0, A_XA1,
                           A_Z0,   A_Z1,  A_Y,  A_XT,  A_PZ, A_RHO, A_L, A_U,  A_Q,  A_DX, A_DY, A_PD,  A_PO,
                           A_E,    A_DS,  A_RE, A_PB,  A_PS, A_PR };
     long long used = static_cast<long long>(lds_d);
@@ -635,7 +638,10 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     // one column slot (t, i) and one CartPose row per thread: N <= 32 and
     // n_abs <= 256; larger problems run the generic admm_step()
     // (collision problems: hinge rows are loop-owned inside the segment)
-    L.seg_ok = (max_step_rows <= kMaxStepRows && !L.wide && L.N * 8 <= kBlock && L.n_abs <= kBlock) ? 1 : 0;
+    L.seg_ok = (max_step_rows <= kMaxStepRows && !L.wide && L.N * 8 <= kBlock && L.n_abs <= kBlock && cpk &&
+                L.loff[A_CPK] >= 0)
+                   ? 1
+                   : 0;
     if (g_debug_path & THIP_DEBUG_NO_SEGMENT)  // diagnostic: the generic ADMM step
       L.seg_ok = 0;
     L.seg_slots = 1;
@@ -653,7 +659,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
       // actual contact count (plan_lds_dynamic, same priority order, so
       // LINV/CV/YV keep their offsets); the launch provides the whole budget
       for (int k = 0; k < A_COUNT; ++k)
-        if (k != A_LINV && k != A_CV && k != A_YV)
+        if (k != A_LINV && k != A_CV && k != A_YV && k != A_CPK)
           L.loff[k] = -1;
       ctx->lds_bytes = static_cast<size_t>(budget) * sizeof(double);
       L.lds_doubles = static_cast<int>(budget);

@@ -123,11 +123,11 @@ class BatchTrustRegionSQP:
 
     PROFILE_SLOTS = ["admm_step", "residuals", "termination", "factor", "polish", "linearize", "evaluate",
                      "build_and_scale", "solve_rhs_diag", "fwd_chain", "bwd_chain", "aux_backsub", "qp_solve",
-                     "sqp_total", "sqp_wall_ticks", "seg_B_rhs_linv", "seg_C2_linvT_middle",
+                     "sqp_total", "sqp_wall_ticks", "seg_B_rhs_linv", "fwd_wave0_own",
                      "seg_hinge_gather", "seg_hinge_E", "coll_count_pass", "coll_rank_pass", "coll_rows", "coll_fk_substates",
                      "gen_rhs_mr", "gen_rhs_cols", "gen_rhs_linv", "gen_dvalue_middle",
                      "n_primal_inf_full", "n_dual_inf_full", "n_factor", "gen_pre", "gen_updates",
-                     "factor_blocks", "factor_twisted", "unused34", "unused35", "unused36", "unused37", "unused38",
+                     "factor_blocks", "factor_twisted", "bwd_wave0_own", "unused35", "unused36", "unused37", "unused38",
                      "unused39"]
 
     def enable_profile(self, on=True):
