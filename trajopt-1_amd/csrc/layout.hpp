@@ -181,6 +181,10 @@ struct Layout
   // D > 8 (e.g. the 14-DoF dual arm): the block solve runs one lane per block
   // row and its chain matrices M, N live in HBM (A_CHM), not in the LDS scratch
   int wide;
+  // the chain matrices M, N in HBM (A_CHM) for narrow blocks too: collision
+  // problems on the ADMM segment, whose chain runs from the pack (A_CPK), so
+  // the LDS they would take holds hinge-row data instead
+  int chm_hbm;
   // hinge chunk sums (A_HPART): lanes and doubles per chunk, >= 2 D (16 for
   // the segment's D <= 8, 32 for wider blocks)
   int part_w;

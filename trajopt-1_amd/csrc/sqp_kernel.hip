@@ -2205,10 +2205,10 @@ constexpr int kChainChunk = 8;
 
 // v_t = c_t - G_t v_{t-dir} for t = t0 + dir, ..., t0 + dir * nsteps, from
 // v_{t0} = c_{t0} (written to out[t0] if store_first).
-__device__ __forceinline__ void block_chain(const double* Gp, const double* cvp, double* outp, int t0, int nsteps,
-                                            int dir, bool store_first, int D, int lane)
+template <typename GP>
+__device__ __forceinline__ void block_chain(GP G, const double* cvp, double* outp, int t0, int nsteps, int dir,
+                                            bool store_first, int D, int lane)
 {
-  const lds_f64* G = lds(Gp);
   const lds_f64* cv = lds(cvp);
   lds_f64* out = lds(outp);
   const int i = lane >> 3, k = lane & 7;
@@ -2336,13 +2336,16 @@ __device__ __noinline__ void block_chain_wide(const double* Gp, const double* cv
   }
 }
 
+// the chain matrices in LDS, or in HBM (Layout::wide, Layout::chm_hbm)
 __device__ __forceinline__ void chain_any(const double* G, const double* cv, double* out, int t0, int nsteps, int dir,
-                                          bool store_first, int D, int lane, bool wide)
+                                          bool store_first, int D, int lane, bool wide, bool chm_hbm)
 {
   if (wide)
     block_chain_wide(G, cv, out, t0, nsteps, dir, store_first, D, lane);
+  else if (chm_hbm)
+    block_chain(gbl(G), cv, out, t0, nsteps, dir, store_first, D, lane);
   else
-    block_chain(G, cv, out, t0, nsteps, dir, store_first, D, lane);
+    block_chain(lds(G), cv, out, t0, nsteps, dir, store_first, D, lane);
 }
 
 // Forward solve of the twisted factor: y = L^-1 b given c_t = LI_t b_t in
@@ -2352,9 +2355,9 @@ __device__ __forceinline__ void twisted_forward(const Ctx& c, const Solver& sv, 
 {
   const int N = c.L.N, m = c.L.tw_mid;
   if (c.wave == 0)
-    chain_any(sv.M, CV, YV, 0, m - 1, +1, true, c.L.D, c.lane, c.L.wide);
+    chain_any(sv.M, CV, YV, 0, m - 1, +1, true, c.L.D, c.lane, c.L.wide, c.L.chm_hbm);
   else if (c.wave == 1 && N - 1 - m > 0)
-    chain_any(sv.M, CV, YV, N - 1, N - 2 - m, -1, true, c.L.D, c.lane, c.L.wide);
+    chain_any(sv.M, CV, YV, N - 1, N - 2 - m, -1, true, c.L.D, c.lane, c.L.wide, c.L.chm_hbm);
 }
 
 // Backward solve of the twisted factor, in place in CV (holding d_t =
@@ -2364,9 +2367,9 @@ __device__ __forceinline__ void twisted_backward(const Ctx& c, const Solver& sv,
 {
   const int N = c.L.N, m = c.L.tw_mid;
   if (c.wave == 0)
-    chain_any(sv.Nb, CV, CV, m, m, -1, false, c.L.D, c.lane, c.L.wide);
+    chain_any(sv.Nb, CV, CV, m, m, -1, false, c.L.D, c.lane, c.L.wide, c.L.chm_hbm);
   else if (c.wave == 1)
-    chain_any(sv.Nb, CV, CV, m, N - 1 - m, +1, false, c.L.D, c.lane, c.L.wide);
+    chain_any(sv.Nb, CV, CV, m, N - 1 - m, +1, false, c.L.D, c.lane, c.L.wide, c.L.chm_hbm);
 }
 
 // d_t[i] = (LI_t^T y_t)[i] for column (t, i), t != middle.
@@ -2438,21 +2441,15 @@ __device__ __noinline__ void twisted_middle_wide(const Ctx& c, const Solver& sv,
   wave_sync();
 }
 
-__device__ __forceinline__ void twisted_middle(const Ctx& c, const Solver& sv, const double* LIp, double* CVp,
-                                               const double* YVp)
+template <typename MP>
+__device__ __forceinline__ void twisted_middle_narrow(const Ctx& c, MP M, MP Mb, const double* LIp, double* CVp,
+                                                      const double* YVp)
 {
-  if (c.L.wide)
-  {
-    twisted_middle_wide(c, sv, LIp, CVp, const_cast<double*>(YVp));
-    return;
-  }
   const int D = c.L.D, DD = D * D, m = c.L.tw_mid, N = c.L.N;
   const int i = c.lane >> 3, k = c.lane & 7;
   const bool act = (i < D) && (k < D);
   const lds_f64* LI = lds(LIp);
   const lds_f64* YV = lds(YVp);
-  const lds_f64* M = lds(sv.M);
-  const lds_f64* Mb = lds(sv.Nb);
   lds_f64* CV = lds(CVp);
   double p = 0.0;
   if (act)
@@ -2469,6 +2466,19 @@ __device__ __forceinline__ void twisted_middle(const Ctx& c, const Solver& sv, c
   wave_sync();
   if (i == 0 && k < D)
     CV[m * D + k] = xm;
+}
+
+__device__ __forceinline__ void twisted_middle(const Ctx& c, const Solver& sv, const double* LIp, double* CVp,
+                                               const double* YVp)
+{
+  if (c.L.wide)
+    twisted_middle_wide(c, sv, LIp, CVp, const_cast<double*>(YVp));
+  else if (c.L.chm_hbm)
+    twisted_middle_narrow(c, gbl(static_cast<const double*>(sv.M)), gbl(static_cast<const double*>(sv.Nb)), LIp, CVp,
+                          YVp);
+  else
+    twisted_middle_narrow(c, lds(static_cast<const double*>(sv.M)), lds(static_cast<const double*>(sv.Nb)), LIp, CVp,
+                          YVp);
 }
 
 // Solve K [x; aux] = r + A' eta, with r (n_cols) in A_BXW (overwritten) and
@@ -3432,8 +3442,8 @@ __device__ void seg_chain_pack(const Ctx& c, const Solver& sv, SegChain& ch)
   const int D = c.L.D, DD = D * D, N = c.L.N, m = c.L.tw_mid;
   lds_f64* P = lds(c.a(A_CPK));
   const lds_f64* LI = lds(c.a(A_LINV));
-  const lds_f64* M = lds(sv.M);
-  const lds_f64* Nb = lds(sv.Nb);
+  const double* M = sv.M;  // LDS or HBM (Layout::chm_hbm): generic loads, once per segment
+  const double* Nb = sv.Nb;
   const int Rh[2] = { m, N - 1 - m };
   for (int e = c.tid; e < 2 * kCpkSteps * 64; e += kBlock)
   {
@@ -5283,7 +5293,7 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
   c.jpt = args.jpt + (long long)b * (L.n_jpos > 0 ? L.n_jpos : 1) * L.D;
   Solver sv;
   // chain matrices: the LDS scratch, or HBM for wide blocks (Layout::wide)
-  sv.M = L.wide ? wsb + L.doff[A_CHM] : dyn;
+  sv.M = (L.wide || L.chm_hbm) ? wsb + L.doff[A_CHM] : dyn;
   sv.Nb = sv.M + L.N * L.D * L.D;
   if (threadIdx.x == 0)
   {

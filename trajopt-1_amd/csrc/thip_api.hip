@@ -554,7 +554,8 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   L.wide = (L.D > 8) ? 1 : 0;
   if (g_debug_path & THIP_DEBUG_FORCE_WIDE)  // diagnostic: the wide-block solve for any D
     L.wide = 1;
-  sizes[A_CHM] = L.wide ? 2 * NDD : 1;
+  L.chm_hbm = (!L.wide && L.hinge && L.N * 8 <= kBlock && L.N <= 2 * kCpkSteps) ? 1 : 0;
+  sizes[A_CHM] = (L.wide || L.chm_hbm) ? 2 * NDD : 1;
   sizes[A_PB] = std::max(nc + m, nab * D);
   sizes[A_PS] = sizes[A_PR] = nc + m;
   sizes[A_HC0] = sizes[A_HC] = hc * 2 * D;
@@ -606,7 +607,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     ioff += (isizes[k] + 15) / 16 * 16;
   }
   L.istride = ioff;
-  const size_t lds_d = std::max<size_t>({ (size_t)(L.wide ? 0 : 2 * NDD), (size_t)(30 * std::max(L.n_cart, 1)),
+  const size_t lds_d = std::max<size_t>({ (size_t)((L.wide || L.chm_hbm) ? 0 : 2 * NDD), (size_t)(30 * std::max(L.n_cart, 1)),
                                           (size_t)(L.n_costs + L.n_cnts + 2) });
   ctx->lds_lin_bytes = lds_d * sizeof(double);
   // LDS residency plan: the per-ADMM-iteration working set, hottest first,
