@@ -39,6 +39,13 @@ int thost_lower_json(const char* json_text, const double* scene, int n_prims, th
 int thost_solve_json_batch(const char* const* json_texts, int batch, const double* scenes, int n_prims, int device,
                            double* x, thip_result* results, char* err, int err_len);
 
+/* thost_solve_json_batch sharded over n_devices HIP devices of this process
+ * (trajopt::MultiDeviceBatchSQP: contiguous shards, sizes differing by at most
+ * one, all shards running concurrently; a device may be listed more than once). */
+int thost_solve_json_batch_multi(const char* const* json_texts, int batch, const double* scenes, int n_prims,
+                                 const int* devices, int n_devices, double* x, thip_result* results, char* err,
+                                 int err_len);
+
 /* ConstructProblem for one JSON problem and trajopt::BasicTrustRegionSQP
  * (sco::BasicTrustRegionSQP with the problem's opt_info) on HIP device
  * `device`, as the reference's planning code runs one problem

@@ -283,3 +283,18 @@ print(repr(desc.jv_coeffs[0]))
     p = subprocess.run([sys.executable, "-c", code, str(root)], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr
     assert p.stdout.strip().splitlines()[-1] == "0.5", p.stdout
+
+
+def test_multi_device_needs_devices(built):
+    """thost_solve_json_batch_multi refuses an empty device list before any HIP
+    call (runs without a GPU)."""
+    import ctypes as C
+
+    L = host.load_host()
+    text = _doc().encode()
+    arr = (C.c_char_p * 1)(text)
+    x = np.zeros(5 * 7)
+    err = C.create_string_buffer(512)
+    rc = L.thost_solve_json_batch_multi(arr, 1, None, 0, (C.c_int * 1)(0), 0,
+                                        x.ctypes.data_as(C.POINTER(C.c_double)), None, err, 512)
+    assert rc == -1 and "no devices" in err.value.decode()

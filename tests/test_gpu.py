@@ -814,6 +814,26 @@ def test_frontdoor_reference_planning_config(oracle_mod):
     check_parity(wl, oracle_mod, x, res, label="arm_around_table")
 
 
+def test_frontdoor_multi_device_shards():
+    """trajopt::MultiDeviceBatchSQP (thost_solve_json_batch_multi): a batch in
+    contiguous shards on several device entries -- here three contexts on the
+    box's one GPU, each on its own stream, all submitted before any is
+    collected -- returns bit for bit the single-context batch, in order, with
+    shard sizes differing by at most one (an entry beyond the batch size gets
+    nothing)."""
+    from trajopt_amd import host
+
+    wl = problems.make_workload("B", 37)
+    texts = [host.workload_to_json(wl, b) for b in range(37)]
+    x1, r1 = host.solve_json_batch(texts)
+    x3, r3 = host.solve_json_batch(texts, devices=[0, 0, 0])
+    np.testing.assert_array_equal(x1, x3)
+    assert [(a.status, a.n_sqp_iters, a.n_qp_solves, a.total_cost) for a in r1] == \
+        [(a.status, a.n_sqp_iters, a.n_qp_solves, a.total_cost) for a in r3]
+    x2, _ = host.solve_json_batch(texts[:2], devices=[0, 0, 0])  # one entry idle
+    np.testing.assert_array_equal(x2, x1[:2])
+
+
 def test_frontdoor_cli(tmp_path):
     from trajopt_amd import host
 

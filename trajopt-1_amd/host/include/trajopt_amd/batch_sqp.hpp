@@ -26,6 +26,10 @@ public:
   void setStream(void* stream);
   // Upload, run every problem's SQP loop, download.
   std::vector<sco::OptResults> optimize();
+  // optimize() in two halves: submit() uploads and queues the fused kernel on
+  // the context's stream and returns; collect() waits for it and downloads.
+  void submit();
+  std::vector<sco::OptResults> collect();
   // HIP-event duration of the last fused launch (ms).
   double lastKernelMs() const;
   // Per-QP records of the next optimize() (thip_debug_trace, THIP_TRACE_W doubles each).
@@ -39,6 +43,25 @@ private:
   std::vector<LoweredProblem> probs_;
   struct thip_ctx* ctx_ = nullptr;
   int trace_cap_ = 0;
+};
+
+// One batch sharded over several HIP devices of this process (SURVEY.md §8e:
+// the problems are independent, so there is no collective): contiguous shards
+// whose sizes differ by at most one, one BatchTrustRegionSQP per device entry
+// (a device may be listed more than once: several contexts on their own
+// streams), every shard submitted before any is collected, so the devices run
+// concurrently.  Results come back in the batch's order.
+class MultiDeviceBatchSQP
+{
+public:
+  MultiDeviceBatchSQP(const std::vector<TrajOptProb::Ptr>& probs, const std::vector<int>& devices);
+  std::vector<sco::OptResults> optimize();
+  // problems per device entry (0 for an entry beyond the batch size)
+  const std::vector<int>& shardSizes() const { return sizes_; }
+
+private:
+  std::vector<std::unique_ptr<BatchTrustRegionSQP>> shards_;
+  std::vector<int> sizes_;
 };
 
 // Per-problem drop-in for the reference's optimizer usage (SURVEY.md §8b tier i):

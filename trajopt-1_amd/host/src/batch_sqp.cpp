@@ -4,6 +4,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <iterator>
+#include <memory>
 #include <stdexcept>
 #include <string>
 
@@ -139,6 +141,12 @@ void BatchTrustRegionSQP::setStream(void* stream) { check(thip_set_stream(ctx_, 
 
 std::vector<sco::OptResults> BatchTrustRegionSQP::optimize()
 {
+  submit();
+  return collect();
+}
+
+void BatchTrustRegionSQP::submit()
+{
   const thip_problem_desc& d = probs_[0].desc;
   const int B = batch(), N = d.n_steps, D = d.chain.n_dof;
   std::vector<double> init, tgt, jpt, scene;
@@ -160,7 +168,13 @@ std::vector<sco::OptResults> BatchTrustRegionSQP::optimize()
   if (d.n_jpos > 0)
     check(thip_upload_joint_targets(ctx_, jpt.data()), "thip_upload_joint_targets");
   check(thip_sqp_run(ctx_), "thip_sqp_run");
-  std::vector<double> x(init.size());
+}
+
+std::vector<sco::OptResults> BatchTrustRegionSQP::collect()
+{
+  const thip_problem_desc& d = probs_[0].desc;
+  const int B = batch(), N = d.n_steps, D = d.chain.n_dof;
+  std::vector<double> x(static_cast<std::size_t>(B) * N * D);
   std::vector<thip_result> res(static_cast<std::size_t>(B));
   check(thip_download(ctx_, x.data(), res.data()), "thip_download");
   std::vector<sco::OptResults> out(static_cast<std::size_t>(B));
@@ -177,6 +191,41 @@ std::vector<sco::OptResults> BatchTrustRegionSQP::optimize()
     o.n_admm_iters = r.n_admm_iters;
     o.max_cnt_viol = r.max_cnt_viol;
     o.flags = r.flags;
+  }
+  return out;
+}
+
+// ------------------------------------------------------------ MultiDeviceBatchSQP
+MultiDeviceBatchSQP::MultiDeviceBatchSQP(const std::vector<TrajOptProb::Ptr>& probs, const std::vector<int>& devices)
+{
+  if (devices.empty())
+    throw std::runtime_error("MultiDeviceBatchSQP: no devices");
+  if (probs.empty())
+    throw std::runtime_error("MultiDeviceBatchSQP: empty batch");
+  const std::vector<LoweredProblem> all = lowerAll(probs);
+  const std::size_t B = all.size(), W = devices.size();
+  std::size_t lo = 0;
+  for (std::size_t r = 0; r < W; ++r)
+  {
+    const std::size_t n = B / W + (r < B % W ? 1 : 0);  // shard r: [lo, lo + n)
+    sizes_.push_back(static_cast<int>(n));
+    if (n == 0)
+      continue;
+    std::vector<LoweredProblem> part(all.begin() + static_cast<long>(lo), all.begin() + static_cast<long>(lo + n));
+    shards_.push_back(std::make_unique<BatchTrustRegionSQP>(std::move(part), devices[r]));
+    lo += n;
+  }
+}
+
+std::vector<sco::OptResults> MultiDeviceBatchSQP::optimize()
+{
+  for (auto& s : shards_)
+    s->submit();
+  std::vector<sco::OptResults> out;
+  for (auto& s : shards_)
+  {
+    std::vector<sco::OptResults> r = s->collect();
+    out.insert(out.end(), std::make_move_iterator(r.begin()), std::make_move_iterator(r.end()));
   }
   return out;
 }

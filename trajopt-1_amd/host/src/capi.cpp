@@ -107,15 +107,24 @@ int thost_solve_json(const char* json_text, const double* scene, int n_prims, in
 int thost_solve_json_batch(const char* const* json_texts, int batch, const double* scenes, int n_prims, int device,
                            double* x, thip_result* results, char* err, int err_len)
 {
+  return thost_solve_json_batch_multi(json_texts, batch, scenes, n_prims, &device, 1, x, results, err, err_len);
+}
+
+int thost_solve_json_batch_multi(const char* const* json_texts, int batch, const double* scenes, int n_prims,
+                                 const int* devices, int n_devices, double* x, thip_result* results, char* err,
+                                 int err_len)
+{
   try
   {
     if (!json_texts || batch <= 0 || !x)
       throw std::runtime_error("thost_solve_json_batch: bad arguments");
+    if (!devices || n_devices <= 0)
+      throw std::runtime_error("thost_solve_json_batch_multi: no devices");
     std::vector<trajopt::TrajOptProb::Ptr> probs;
     for (int b = 0; b < batch; ++b)
       probs.push_back(construct(json_texts[b], scenes ? scenes + static_cast<std::size_t>(b) * n_prims * 16 : nullptr,
                                 n_prims));
-    trajopt::BatchTrustRegionSQP opt(probs, device);
+    trajopt::MultiDeviceBatchSQP opt(probs, std::vector<int>(devices, devices + n_devices));
     const auto res = opt.optimize();
     for (int b = 0; b < batch; ++b)
     {

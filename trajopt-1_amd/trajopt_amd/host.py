@@ -39,6 +39,9 @@ def load_host():
         L.thost_solve_json_batch.argtypes = [C.POINTER(C.c_char_p), C.c_int, dp, C.c_int, C.c_int, dp,
                                              C.POINTER(abi.Result), C.c_char_p, C.c_int]
         L.thost_solve_json_batch.restype = C.c_int
+        L.thost_solve_json_batch_multi.argtypes = [C.POINTER(C.c_char_p), C.c_int, dp, C.c_int, C.POINTER(C.c_int),
+                                                   C.c_int, dp, C.POINTER(abi.Result), C.c_char_p, C.c_int]
+        L.thost_solve_json_batch_multi.restype = C.c_int
         L.thost_solve_json.argtypes = [C.c_char_p, dp, C.c_int, C.c_int, dp, C.POINTER(abi.Result),
                                        C.POINTER(C.c_int), C.c_char_p, C.c_int]
         L.thost_solve_json.restype = C.c_int
@@ -70,8 +73,9 @@ def lower_json(text: str, scene=None):
     return desc, init, tgt, jpt
 
 
-def solve_json_batch(texts, scenes=None, device=0):
-    """-> (x [B, N, D], list of abi.Result) through trajopt::BatchTrustRegionSQP."""
+def solve_json_batch(texts, scenes=None, device=0, devices=None):
+    """-> (x [B, N, D], list of abi.Result) through trajopt::BatchTrustRegionSQP, or
+    trajopt::MultiDeviceBatchSQP over `devices` (a list of HIP device ids)."""
     L = load_host()
     B = len(texts)
     desc, _, _, _ = lower_json(texts[0], None if scenes is None else scenes[0])
@@ -82,7 +86,9 @@ def solve_json_batch(texts, scenes=None, device=0):
     x = np.zeros((B, N, D))
     res = (abi.Result * B)()
     err = C.create_string_buffer(4096)
-    rc = L.thost_solve_json_batch(arr, B, _dp(sc), n_prims, device, _dp(x), res, err, 4096)
+    devs = [device] if devices is None else list(devices)
+    dv = (C.c_int * max(1, len(devs)))(*devs)
+    rc = L.thost_solve_json_batch_multi(arr, B, _dp(sc), n_prims, dv, len(devs), _dp(x), res, err, 4096)
     if rc != 0:
         raise HostError(err.value.decode())
     return x, list(res)
