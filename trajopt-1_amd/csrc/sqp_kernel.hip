@@ -2568,24 +2568,37 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     pf[slot] += tn - tq;        \
     tq = tn;                    \
   }
+  // the Ctx / Layout / Tables values the loops use, in registers (the Ctx
+  // lives in private memory and would be re-read with dependent FLAT loads
+  // after every store the compiler cannot prove does not alias it)
+  const int tid = c.tid;
   const Layout& L = c.L;
-  const int D = L.D, nx = L.nx, DD = D * D, nfr = L.n_fixed_rows;
+  const int D = L.D, nx = L.nx, DD = D * D, nfr = L.n_fixed_rows, n_abs = L.n_abs, n_rows = L.n_rows;
+  const int nc_base = L.nc_base, m_base = L.m_base;
+  const bool wide = L.wide;
   const double *GS = c.a(A_GS), *WS = c.a(A_WS), *DG = c.a(A_DG), *LI = c.a(A_LINV), *BS = c.a(A_BS),
                *FS = c.a(A_FS);
   double *BX = c.a(A_BXW), *BA = c.a(A_BA), *MR = c.a(A_MR), *CV = c.a(A_CV), *YV = c.a(A_YV);
+  const double *RHO = c.a(A_RHO), *HW = c.a(A_HW), *HC = c.a(A_HC);
+  const int *ACT = c.ia(I_ACT), *HT = c.ia(I_HT), *HP = c.ia(I_HPTR);
+  const int *fixed_of_step = c.T.fixed_of_step, *step_ptr = c.T.step_ptr, *step_rows = c.T.step_rows,
+            *row_step = c.T.row_step;
+  // rho_k() and bound_row() on the hoisted values (same expressions)
+  auto rho_l = [&](int r) { return !polish ? RHO[r] : (ACT[r] != 0 ? 1.0 / delta : 0.0); };
+  auto brow = [&](int col) { return col < nc_base ? n_rows + col : m_base + 2 * (col - nc_base) + 1; };
   // kGenU rows per thread at once, every load before any store (see admm_step)
-  for (int r0 = c.tid; r0 < L.n_abs; r0 += kGenU * kBlock)
+  for (int r0 = tid; r0 < n_abs; r0 += kGenU * kBlock)
   {
     double mr[kGenU], rnv[kGenU], rpv[kGenU];
 #pragma unroll
     for (int u = 0; u < kGenU; ++u)
     {
-      const int r = min(r0 + u * kBlock, L.n_abs - 1);
+      const int r = min(r0 + u * kBlock, n_abs - 1);
       const int ca = nx + 2 * r;
-      const double rr = rho_k(c, nfr + r, polish, delta);
+      const double rr = rho_l(nfr + r);
       const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
-      const double rn = BX[ca] + BS[ca] * eta[bound_row(L, ca)];
-      const double rp = BX[ca + 1] + BS[ca + 1] * eta[bound_row(L, ca + 1)];
+      const double rn = BX[ca] + BS[ca] * eta[brow(ca)];
+      const double rp = BX[ca + 1] + BS[ca + 1] * eta[brow(ca + 1)];
       const double det = dn * dp + rr * (dn * wp * wp + dp * wn * wn);
       mr[u] = (eta[nfr + r] * dn * dp - rr * (wn * dp * rn + wp * dn * rp)) / det;
       rnv[u] = rn;
@@ -2595,7 +2608,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     for (int u = 0; u < kGenU; ++u)
     {
       const int r = r0 + u * kBlock;
-      if (r >= L.n_abs)
+      if (r >= n_abs)
         break;
       MR[r] = mr[u];
       BA[nx + 2 * r] = rnv[u];
@@ -2603,18 +2616,18 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     }
   }
   const int nh = c.s->n_h;
-  for (int h0 = c.tid; h0 < nh; h0 += kGenU * kBlock)
+  for (int h0 = tid; h0 < nh; h0 += kGenU * kBlock)
   {
     double mr[kGenU], rnv[kGenU];
 #pragma unroll
     for (int u = 0; u < kGenU; ++u)
     {
       const int h = min(h0 + u * kBlock, nh - 1);
-      const int col = L.nc_base + h;
-      const double rr = rho_k(c, L.m_base + 2 * h, polish, delta);
-      const double dn = DG[col], w = c.a(A_HW)[h];
-      const double rn = BX[col] + BS[col] * eta[bound_row(L, col)];
-      mr[u] = (eta[L.m_base + 2 * h] * dn - rr * w * rn) / (dn + rr * w * w);
+      const int col = nc_base + h;
+      const double rr = rho_l(m_base + 2 * h);
+      const double dn = DG[col], w = HW[h];
+      const double rn = BX[col] + BS[col] * eta[brow(col)];
+      mr[u] = (eta[m_base + 2 * h] * dn - rr * w * rn) / (dn + rr * w * w);
       rnv[u] = rn;
     }
 #pragma unroll
@@ -2623,35 +2636,33 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       const int h = h0 + u * kBlock;
       if (h >= nh)
         break;
-      MR[L.n_rows + h] = mr[u];
-      BA[L.nc_base + h] = rnv[u];
+      MR[n_rows + h] = mr[u];
+      BA[nc_base + h] = rnv[u];
     }
   }
   BSYNC();
   PROF_LAP(23);
-  FOR(col, nx)
+  for (int col = tid; col < nx; col += kBlock)
   {
     const int t = col / D, j = col % D;
-    double b = BX[col] + BS[col] * eta[bound_row(L, col)];
-    const int f = c.T.fixed_of_step[t];
+    double b = BX[col] + BS[col] * eta[brow(col)];
+    const int f = fixed_of_step[t];
     if (f >= 0)
       b += FS[f * D + j] * eta[f * D + j];
-    b = csr_row_gather(c.T.step_rows, c.T.step_ptr[t], c.T.step_ptr[t + 1], GS, MR, D, j, b);
+    b = csr_row_gather(step_rows, step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
     if (nh > 0)
     {
-      const double* HC = c.a(A_HC);
-      const int* HP = c.ia(I_HPTR);
-      b = hinge_gather(HC, MR + L.n_rows, 2 * D, j, HP[t], HP[t + 1], b);
-      b = hinge_gather(HC, MR + L.n_rows, 2 * D, D + j, t > 0 ? HP[t - 1] : HP[t], HP[t], b);
+      b = hinge_gather(HC, MR + n_rows, 2 * D, j, HP[t], HP[t + 1], b);
+      b = hinge_gather(HC, MR + n_rows, 2 * D, D + j, t > 0 ? HP[t - 1] : HP[t], HP[t], b);
     }
     BX[col] = b;
   }
   BSYNC();
   PROF_LAP(24);
-  FOR(col, nx)
+  for (int col = tid; col < nx; col += kBlock)
   {
     const int t = col / D, i = col % D;
-    const double v = L.wide ? masked_dot<THIP_MAX_DOF>(lds(LI) + t * DD + i * D, 1, BX + t * D, 1, 0, i + 1)
+    const double v = wide ? masked_dot<THIP_MAX_DOF>(lds(LI) + t * DD + i * D, 1, BX + t * D, 1, 0, i + 1)
                             : masked_dot<kOct>(lds(LI) + t * DD + i * D, 1, BX + t * D, 1, 0, i + 1);
     lds(CV)[col] = v;
   }
@@ -2670,7 +2681,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
 #pragma unroll
     for (int u = 0; u < kCols; ++u)
     {
-      const int cu = c.tid + kBlock * u;
+      const int cu = tid + kBlock * u;
       dv[u] = (cu < nx && cu / D != m) ? twisted_dvalue(c, LI, YV, cu / D, cu % D) : 0.0;
     }
     if (c.wave == kWaves - 1)
@@ -2679,7 +2690,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
 #pragma unroll
     for (int u = 0; u < kCols; ++u)
     {
-      const int cu = c.tid + kBlock * u;
+      const int cu = tid + kBlock * u;
       if (cu < nx && cu / D != m)
         lds(CV)[cu] = dv[u];
     }
@@ -2690,20 +2701,21 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   twisted_backward(c, sv, CV);
   BSYNC();
   PROF_LAP(10);
-  FOR(col, nx) out[col] = CV[col];
+  for (int col = tid; col < nx; col += kBlock)
+    out[col] = CV[col];
   // aux back-substitution
-  for (int r0 = c.tid; r0 < L.n_abs; r0 += kGenUHeavy * kBlock)
+  for (int r0 = tid; r0 < n_abs; r0 += kGenUHeavy * kBlock)
   {
     double on[kGenUHeavy], op[kGenUHeavy];
 #pragma unroll
     for (int u = 0; u < kGenUHeavy; ++u)
     {
-      const int r = min(r0 + u * kBlock, L.n_abs - 1);
-      const int t = c.T.row_step[r];
+      const int r = min(r0 + u * kBlock, n_abs - 1);
+      const int t = row_step[r];
       const int ca = nx + 2 * r;
-      const double g = L.wide ? masked_dot<THIP_MAX_DOF>(GS + r * D, 1, lds(CV) + t * D, 1, 0, D)
+      const double g = wide ? masked_dot<THIP_MAX_DOF>(GS + r * D, 1, lds(CV) + t * D, 1, 0, D)
                               : masked_dot<kOct>(GS + r * D, 1, lds(CV) + t * D, 1, 0, D);
-      const double rr = rho_k(c, nfr + r, polish, delta);
+      const double rr = rho_l(nfr + r);
       const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
       const double rn = BA[ca], rp = BA[ca + 1];
       const double det = dn * dp + rr * (dn * wp * wp + dp * wn * wn);
@@ -2716,25 +2728,25 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     for (int u = 0; u < kGenUHeavy; ++u)
     {
       const int r = r0 + u * kBlock;
-      if (r >= L.n_abs)
+      if (r >= n_abs)
         break;
       out[nx + 2 * r] = on[u];
       out[nx + 2 * r + 1] = op[u];
     }
   }
-  for (int h0 = c.tid; h0 < nh; h0 += kGenUHinge * kBlock)
+  for (int h0 = tid; h0 < nh; h0 += kGenUHinge * kBlock)
   {
     double ov[kGenUHinge];
 #pragma unroll
     for (int u = 0; u < kGenUHinge; ++u)
     {
       const int h = min(h0 + u * kBlock, nh - 1);
-      const int t = c.ia(I_HT)[h];
-      const double g = hinge_dot(c.a(A_HC) + h * 2 * D, lds(CV) + t * D, D);
-      const int col = L.nc_base + h;
-      const double rr = rho_k(c, L.m_base + 2 * h, polish, delta);
-      const double dn = DG[col], w = c.a(A_HW)[h];
-      ov[u] = (BA[col] + w * (eta[L.m_base + 2 * h] - rr * g)) / (dn + rr * w * w);
+      const int t = HT[h];
+      const double g = hinge_dot(HC + h * 2 * D, lds(CV) + t * D, D);
+      const int col = nc_base + h;
+      const double rr = rho_l(m_base + 2 * h);
+      const double dn = DG[col], w = HW[h];
+      ov[u] = (BA[col] + w * (eta[m_base + 2 * h] - rr * g)) / (dn + rr * w * w);
     }
 #pragma unroll
     for (int u = 0; u < kGenUHinge; ++u)
@@ -2742,7 +2754,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       const int h = h0 + u * kBlock;
       if (h >= nh)
         break;
-      out[L.nc_base + h] = ov[u];
+      out[nc_base + h] = ov[u];
     }
   }
   BSYNC();
@@ -3210,12 +3222,13 @@ __device__ bool check_termination(Ctx& c, const Norms& nm, bool approx)
 __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
 {
   PROF(0);
+  const int tid = c.tid;  // (the Ctx values the loops use, in registers: see reduced_solve)
   const thip_osqp_settings& os = c.d->osqp;
   const double sig = os.sigma, al = os.alpha;
   // swap buffers
   const int cur = c.s->cur ^ 1;
   BSYNC();
-  if (c.tid == 0)
+  if (tid == 0)
     c.s->cur = cur;
   double* x = c.a(cur ? A_XA1 : A_XA0);
   const double* xp = c.a(cur ? A_XA0 : A_XA1);
@@ -3225,7 +3238,7 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
   double* BX = c.a(A_BXW);
   const double *Q = c.a(A_Q), *RH = c.a(A_RHO), *Lo = c.a(A_L), *Up = c.a(A_U);
   double* ETA = c.a(A_PZ);  // eta = rho zp - y over all rows (scratch)
-  long long* pf = (c.tid == 0) ? c.s->prof : nullptr;
+  long long* pf = (tid == 0) ? c.s->prof : nullptr;
   long long tq = pf ? clock64() : 0;
   // the generic step's loops run kGenU iterations per thread at once, all
   // loads before any store: the arrays are generic pointers (LDS or HBM per
@@ -3233,7 +3246,7 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
   // loads above this one's stores and each iteration paid a full memory
   // round trip (config E: 14-DoF x 50 waypoints, ~4,300 rows)
   const int m = c.m(), nc = c.nc();
-  for (int r0 = c.tid; r0 < (pre_ready ? 0 : m); r0 += kGenULight * kBlock)
+  for (int r0 = tid; r0 < (pre_ready ? 0 : m); r0 += kGenULight * kBlock)
   {
     double e[kGenULight];
 #pragma unroll
@@ -3247,7 +3260,7 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
       if (r0 + u * kBlock < m)
         ETA[r0 + u * kBlock] = e[u];
   }
-  for (int c0 = c.tid; c0 < (pre_ready ? 0 : nc); c0 += kGenULight * kBlock)
+  for (int c0 = tid; c0 < (pre_ready ? 0 : nc); c0 += kGenULight * kBlock)
   {
     double e[kGenULight];
 #pragma unroll
@@ -3273,7 +3286,7 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
   // kind's branch in every wave and serialised their loads
   auto update_rows = [&](int rb, int re, auto zt_of, auto unroll) {
     constexpr int U = decltype(unroll)::value;  // rows per thread at once (see kGenU)
-    for (int r0 = rb + c.tid; r0 < re; r0 += U * kBlock)
+    for (int r0 = rb + tid; r0 < re; r0 += U * kBlock)
     {
       double zt[U], rh[U], yv[U], zv[U], lo[U], up[U];
 #pragma unroll
@@ -3308,22 +3321,40 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
     }
   };
   const Layout& L = c.L;
-  update_rows(0, L.n_rows, [&](int r) { return row_ax(c, r, XT); }, std::integral_constant<int, kGenUHeavy>());
+  const int D = L.D, nx = L.nx, nfr = L.n_fixed_rows, n_rows = L.n_rows, m_base = L.m_base, nc_base = L.nc_base;
+  const double *FS = c.a(A_FS), *GS = c.a(A_GS), *WS = c.a(A_WS), *BS = c.a(A_BS);
+  const int *row_step = c.T.row_step, *fixed_steps = c.d->fixed_steps;
+  // row_ax() for the fixed and CartPose rows, on the hoisted values (same expressions)
+  auto row_ax_l = [&](int r) {
+    if (r < nfr)
+    {
+      const int slot = r / D, j = r % D;
+      return FS[r] * XT[fixed_steps[slot] * D + j];
+    }
+    const int a = r - nfr;
+    const int t = row_step[a];
+    double v = 0;
+    for (int j = 0; j < D; ++j)
+      v += GS[a * D + j] * XT[t * D + j];
+    const int ca = nx + 2 * a;
+    v += WS[2 * a] * XT[ca] + WS[2 * a + 1] * XT[ca + 1];
+    return v;
+  };
+  update_rows(0, n_rows, row_ax_l, std::integral_constant<int, kGenUHeavy>());
   {
-    const double* BS = c.a(A_BS);
-    update_rows(L.n_rows, L.m_base, [&](int r) { return BS[r - L.n_rows] * XT[r - L.n_rows]; },
+    update_rows(n_rows, m_base, [&](int r) { return BS[r - n_rows] * XT[r - n_rows]; },
                 std::integral_constant<int, kGenULight>());
-    if (m > L.m_base)
+    if (m > m_base)
     {
       // hinge row m_base + 2h: a_t.x_t + a_t+1.x_t+1 + w h; m_base + 2h + 1:
       // the bound row of h.  One thread per hinge variable updates both rows
       // (a loop over the rows alternated the two kinds lane by lane)
       const double *HC = c.a(A_HC), *HW = c.a(A_HW);
       const int* HT = c.ia(I_HT);
-      const int D = L.D, nh = (m - L.m_base) >> 1;
-      for (int h = c.tid; h < nh; h += kBlock)
+      const int nh = (m - m_base) >> 1;
+      for (int h = tid; h < nh; h += kBlock)
       {
-        const int col = L.nc_base + h, r0 = L.m_base + 2 * h;
+        const int col = nc_base + h, r0 = m_base + 2 * h;
         const double xh = XT[col];
         const double zt2[2] = { hinge_dot(HC + h * 2 * D, XT + HT[h] * D, D) + HW[h] * xh, BS[col] * xh };
         double rh[2], yv[2], zv[2], lo[2], up[2];
@@ -3355,7 +3386,7 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
       }
     }
   }
-  for (int c0 = c.tid; c0 < nc; c0 += kGenULight * kBlock)
+  for (int c0 = tid; c0 < nc; c0 += kGenULight * kBlock)
   {
     double xt[kGenULight], xo[kGenULight], qv[kGenULight];
 #pragma unroll
