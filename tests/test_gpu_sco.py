@@ -96,3 +96,65 @@ def test_joint_terms_single_problem(sco_lib, oracle_mod, name):
     assert check(x) == [], (name, check(x))
     wl = joint_terms.workload(text, host)
     check_parity(wl, oracle_mod, x[None], [res], label=f"json-{name}", min_strict=0.0)
+
+
+def run_diag(L, mode, log_dir=None):
+    L.sco_case_diag.argtypes = [C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_char_p,
+                                C.c_int]
+    L.sco_case_diag.restype = C.c_int
+    x = np.zeros(2)
+    counts = (C.c_int * 3)()
+    err = C.create_string_buffer(2048)
+    rc = L.sco_case_diag(mode, 0, None if log_dir is None else str(log_dir).encode(),
+                         x.ctypes.data_as(C.POINTER(C.c_double)), counts, err, 2048)
+    assert rc == 0, err.value.decode()
+    return x, counts[0], counts[1], counts[2]
+
+
+def test_generic_path_logs(sco_lib, tmp_path):
+    """log_results on the generic path (TP1): the reference's four CSV logs
+    (optimizers.cpp:533-647, opened at :712-730, written per trust-region step at
+    :858-871): the solver log's DESCRIPTION header and one `Solver` line per
+    solved QP, the variable names and values, and the per-term cost / constraint
+    lines with their four columns per term."""
+    x, status, n_qp, _ = run_diag(sco_lib, 0, tmp_path)
+    assert status == 0
+    solver = (tmp_path / "trajopt_solver.log").read_text().splitlines()
+    assert solver[0] == "DESCRIPTION,oldexact,new_exact,dapprox,dexact,ratio"
+    assert sum(l.startswith("Solver,") for l in solver) == n_qp and len(solver) == n_qp + 1
+    assert all(len(l.split(",")) == 6 for l in solver)
+    vars_ = (tmp_path / "trajopt_vars.log").read_text().splitlines()
+    assert vars_[0] == "NAMES,x_0,x_1" and all(l.startswith("VALUES,") for l in vars_[1:]) and len(vars_) == n_qp + 1
+    assert all(len([float(v) for v in l.split(",")[1:]]) == 2 for l in vars_[1:])  # each step's new x
+    costs = (tmp_path / "trajopt_costs.log").read_text().splitlines()
+    assert costs[0] == "COST NAMES,f,f,f,f" and costs[1] == "DESCRIPTION,oldexact,dapprox,dexact,ratio"
+    assert all(l.startswith("COSTS,") and len(l.split(",")) == 5 for l in costs[2:]) and len(costs) == n_qp + 2
+    cnts = (tmp_path / "trajopt_constraints.log").read_text().splitlines()
+    assert cnts[0] == "CONSTRAINT NAMES,g,g,g,g" and cnts[1] == "DESCRIPTION,oldexact,dapprox,dexact,ratio"
+    assert all(l.startswith("CONSTRAINTS,") and len(l.split(",")) == 5 for l in cnts[2:])
+
+
+def test_generic_path_time_limit(sco_lib):
+    """max_time = 0: the limit is checked before the first convexification
+    (optimizers.cpp:739-753); with no constraint values yet the status is
+    OPT_CONVERGED (the reference's rule), x is the start, no QP was solved."""
+    x, status, n_qp, n_sqp = run_diag(sco_lib, 1)
+    assert (status, n_qp, n_sqp) == (0, 0, 0)
+    np.testing.assert_array_equal(x, [-2.0, 1.0])
+
+
+def test_generic_path_qp_failure_writes_lp(sco_lib):
+    """An infeasible QP (x0 >= 1 and x0 <= 0 as model constraints): every solve
+    fails, the model is dumped to /tmp/fail.lp (OSQPModel::writeToFile,
+    osqp_interface.cpp:621-640, called at optimizers.cpp:817-842) and the run
+    ends OPT_FAILED: two shrinks, one retry at the minimum trust box, and the
+    fourth failure ends the run (max_qp_solver_failures = 3)."""
+    import os
+
+    lp = "/tmp/fail.lp"
+    if os.path.exists(lp):
+        os.remove(lp)
+    _, status, n_qp, _ = run_diag(sco_lib, 2)
+    assert status == 4 and n_qp == 4  # OPT_FAILED
+    text = open(lp).read()
+    assert "Minimize" in text and "Subject To" in text and "Bounds" in text and text.rstrip().endswith("End")

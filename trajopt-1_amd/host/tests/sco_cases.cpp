@@ -174,9 +174,92 @@ CaseOut sqpCase(int id, int device)
   o.n_admm = solver.results().n_admm_iters;
   return o;
 }
+
+// TP1 (case 5) with the optimizer's logs, a time limit, or a QP that cannot be
+// solved: the reference's diagnostics on the generic path.
+//   mode 0: log_results into log_dir (optimizers.cpp:533-647 formats)
+//   mode 1: max_time = 0 (optimizers.cpp:739-753: the limit is checked before
+//           the first convexification)
+//   mode 2: an infeasible linear constraint pair (x0 >= 1 and x0 <= 0): every
+//           QP fails, /tmp/fail.lp is written (optimizers.cpp:817-842) and the
+//           run ends OPT_FAILED after max_qp_solver_failures
+CaseOut diagCase(int mode, int device, const char* log_dir)
+{
+  auto prob = makeProblem(2, device);
+  prob->addCost(std::make_shared<CostFromFunc>(
+      ScalarOfVector::construct([](const DblVec& x) { return 1 * sq(x[1] - sq(x[0])) + sq(1 - x[0]); }),
+      prob->getVars(), "f", true));
+  prob->addConstraint(std::make_shared<ConstraintFromErrFunc>(
+      VectorOfVector::construct([](const DblVec& x) { return DblVec{ -1.5 - x[1] }; }), prob->getVars(), DblVec(),
+      INEQ, "g"));
+  if (mode == 2)
+  {
+    const Var x0 = prob->getVars()[0];
+    AffExpr ge;  // 1 - x0 <= 0
+    ge.constant = 1;
+    ge.coeffs = { -1 };
+    ge.vars = { x0 };
+    prob->addLinearConstraint(ge, INEQ);
+    prob->addLinearConstraint(AffExpr(x0), INEQ);  // x0 <= 0
+  }
+  BasicTrustRegionSQP solver(prob);
+  BasicTrustRegionSQPParameters p;
+  p.max_iter = 1000;
+  p.min_trust_box_size = 1e-5;
+  p.min_approx_improve = 1e-10;
+  p.initial_merit_error_coeff = 1;
+  if (mode == 0)
+  {
+    p.log_results = true;
+    p.log_dir = log_dir;
+  }
+  if (mode == 1)
+    p.max_time = 0.0;
+  solver.setParameters(p);
+  solver.initialize({ -2, 1 });
+  CaseOut o;
+  o.status = solver.optimize();
+  o.x = solver.x();
+  o.n_qp = solver.results().n_qp_solves;
+  o.n_sqp = solver.results().n_sqp_iters;
+  return o;
+}
+}  // namespace
+
+namespace
+{
+void setErr(char* err, int err_len, const char* what)
+{
+  if (err && err_len > 0)
+  {
+    const std::size_t n = std::min<std::size_t>(std::strlen(what), static_cast<std::size_t>(err_len - 1));
+    std::memcpy(err, what, n);
+    err[n] = '\0';
+  }
+}
 }  // namespace
 
 extern "C" {
+// counts[3] = {status, n_qp_solves, n_sqp_iters}; x: [2]
+int sco_case_diag(int mode, int device, const char* log_dir, double* x, int* counts, char* err, int err_len)
+{
+  try
+  {
+    const CaseOut o = diagCase(mode, device, log_dir ? log_dir : "/tmp");
+    x[0] = o.x[0];
+    x[1] = o.x[1];
+    counts[0] = o.status;
+    counts[1] = o.n_qp;
+    counts[2] = o.n_sqp;
+    return 0;
+  }
+  catch (const std::exception& e)
+  {
+    setErr(err, err_len, e.what());
+    return -1;
+  }
+}
+
 // x: [cap]; counts[5] = {n_x, status, n_qp_solves, n_sqp_iters, n_vars_after}
 int sco_case_run(int id, int device, double* x, int cap, int* counts, long long* n_admm, char* err, int err_len)
 {
