@@ -45,8 +45,9 @@ extern "C" {
 
 /* ABI version of the structs below: thip_create rejects a descriptor whose
  * abi_version differs (a caller compiled against another layout).  3: the
- * descriptor carries abi_version, thip_chain.is_tree, thip_sqp_params.max_time. */
-#define THIP_ABI_VERSION 3
+ * descriptor carries abi_version, thip_chain.is_tree, thip_sqp_params.max_time.
+ * 4: use_time, fixed dofs, time JointVel.  5: TotalTime. */
+#define THIP_ABI_VERSION 5
 
 #define THIP_MAX_DOF 16
 #define THIP_MAX_LINKS 32
@@ -57,6 +58,8 @@ extern "C" {
 #define THIP_MAX_JPOS 8
 #define THIP_MAX_JVX 4
 #define THIP_MAX_JDT 8
+#define THIP_MAX_JVT 4
+#define THIP_MAX_TTT 2
 #define THIP_MAX_CONTACTS 131072
 
 /* error codes */
@@ -268,6 +271,41 @@ typedef struct thip_problem_desc {
   double jdt_targets[THIP_MAX_JDT][THIP_MAX_DOF];
   double jdt_upper_tols[THIP_MAX_JDT][THIP_MAX_DOF];
   double jdt_lower_tols[THIP_MAX_JDT][THIP_MAX_DOF];
+
+  /* Time parameterisation (basic_info.use_time, problem_description.cpp:557-598,
+   * 372-379): one more variable per waypoint, dt_i in [dt_lower, dt_upper]
+   * after the waypoint's joints, initialised to init_dt; and the time-
+   * parameterised JointVel terms (JointVelTermInfo::hatch with TT_USE_TIME,
+   * :1263-1344): per joint j a TrajOptCostFromErrFunc / ConstraintFromErrFunc
+   * over (x_j[first..last], dt[first..last]) with JointVelErrCalculator /
+   * JointVelJacCalculator (kinematic_terms.cpp:434-475), SQUARED or HINGE
+   * (costs) / EQ or INEQ (constraints) by the tolerances, steps clamped as
+   * the JointVel hatch.  Costs follow the jdt costs, constraints the jdt
+   * constraints.  basic_info.fixed_dofs (:528-546): joint columns pinned to
+   * the initial trajectory at every step that is not a fixed timestep.
+   * thip_create rejects use_time, n_jvt, n_ttt > 0 and n_fixed_dofs > 0 (the generic
+   * path runs them); they are the lowered record the oracle reads. */
+  int use_time;
+  double dt_lower, dt_upper, init_dt;
+  int n_fixed_dofs;
+  int fixed_dofs[THIP_MAX_DOF];
+  int n_jvt;
+  int jvt_is_cnt[THIP_MAX_JVT];
+  int jvt_first_step[THIP_MAX_JVT];
+  int jvt_last_step[THIP_MAX_JVT];
+  double jvt_coeffs[THIP_MAX_JVT][THIP_MAX_DOF];
+  double jvt_targets[THIP_MAX_JVT][THIP_MAX_DOF];
+  double jvt_upper_tols[THIP_MAX_JVT][THIP_MAX_DOF];
+  double jvt_lower_tols[THIP_MAX_JVT][THIP_MAX_DOF];
+  /* TotalTimeTermInfo (problem_description.cpp:1860-1913): sum over steps 1..N-1
+   * of 1/x[i][W-1] (the last variable column: dt with use_time) minus limit,
+   * TimeCostCalculator / TimeCostJacCalculator (kinematic_terms.cpp:579-591);
+   * SQUARED / EQ when limit is 0, else HINGE / INEQ.  Costs follow the time
+   * JointVel costs, constraints the time JointVel constraints. */
+  int n_ttt;
+  int ttt_is_cnt[THIP_MAX_TTT];
+  double ttt_coeff[THIP_MAX_TTT];
+  double ttt_limit[THIP_MAX_TTT];
 
   /* CollisionTermInfo, LVS_DISCRETE or LVS_CONTINUOUS, cost or constraint
    * (collision_terms.cpp:737-1161,1267-1386):

@@ -139,7 +139,8 @@ def solve(wl, n_threads=1, variant="exact"):
     tg = np.ascontiguousarray(wl.targets, dtype=np.float64) if wl.targets.size else None
     sc = np.ascontiguousarray(wl.scene, dtype=np.float64) if wl.scene.size else None
     jt = _jpos(wl)
-    x = np.zeros_like(init)
+    # [B][N][D], and the dt column after the joints with use_time
+    x = np.zeros((B, init.shape[1], init.shape[2] + (1 if wl.desc.use_time else 0)))
     res = (abi.Result * B)()
     rc = L.oracle_solve_batch(C.byref(wl.desc), B, _dp(init), _dp(tg), _dp(sc), _dp(jt), _dp(x), res, n_threads)
     if rc != 0:

@@ -31,7 +31,8 @@ void solveOne(const thip_problem_desc* d, const double* init, const double* targ
   opt.initialize(tp.init);
   opt.optimize();
   const OptResults& r = opt.results();
-  std::memcpy(out_x, r.x.data(), sizeof(double) * static_cast<std::size_t>(N * D));
+  // [n_steps][n_dof (+ dt with use_time)]
+  std::memcpy(out_x, r.x.data(), sizeof(double) * static_cast<std::size_t>(N * (D + (d->use_time ? 1 : 0))));
   if (res)
   {
     std::memset(res, 0, sizeof(*res));
@@ -84,7 +85,8 @@ int oracle_solve_batch(const thip_problem_desc* d, int batch, const double* init
         solveOne(d, init + static_cast<std::size_t>(b) * N * D,
                  targets ? targets + static_cast<std::size_t>(b) * d->n_cart * 12 : nullptr,
                  scene ? scene + static_cast<std::size_t>(b) * d->n_prims * 16 : nullptr,
-                 jpos_targets ? jpos_targets + static_cast<std::size_t>(b) * d->n_jpos * D : nullptr, out_x + static_cast<std::size_t>(b) * N * D, res ? res + b : nullptr, b);
+                 jpos_targets ? jpos_targets + static_cast<std::size_t>(b) * d->n_jpos * D : nullptr,
+                 out_x + static_cast<std::size_t>(b) * N * (D + (d->use_time ? 1 : 0)), res ? res + b : nullptr, b);
       }
       catch (const std::exception& e)
       {

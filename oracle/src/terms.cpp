@@ -796,6 +796,103 @@ void addJointDiffTerm(TrajProblem& tp, const std::vector<VarVector>& rows, const
   }
 }
 
+// ------------------------------------------------------------ time-parameterised JointVel
+// JointVelErrCalculator (kinematic_terms.cpp:434-449) over v = (x_first..x_last,
+// dt_first..dt_last): vel_i = (x_{i+1} - x_i) * dt_{i+1}; the error is
+// [-(upper - (vel - target)); lower - (vel - target)]
+static DblVec jointVelTimeErr(const DblVec& v, double target, double upper, double lower)
+{
+  const int half = static_cast<int>(v.size() / 2), nv = half - 1;
+  DblVec out(static_cast<std::size_t>(2 * nv));
+  for (int i = 0; i < nv; ++i)
+  {
+    const double vel = (v[static_cast<std::size_t>(i + 1)] - v[static_cast<std::size_t>(i)]) *
+                       v[static_cast<std::size_t>(half + i + 1)];
+    out[static_cast<std::size_t>(i)] = -(upper - (vel - target));
+    out[static_cast<std::size_t>(nv + i)] = lower - (vel - target);
+  }
+  return out;
+}
+
+// JointVelJacCalculator (kinematic_terms.cpp:451-475)
+static Mat jointVelTimeJac(const DblVec& v)
+{
+  const int n = static_cast<int>(v.size()), half = n / 2, nv = half - 1;
+  Mat J(2 * nv, n);
+  for (int i = 0; i < nv; ++i)
+  {
+    const int ti = i + half + 1;
+    J(i, i) = -1.0 * v[static_cast<std::size_t>(ti)];
+    J(i, i + 1) = 1.0 * v[static_cast<std::size_t>(ti)];
+    J(i, ti) = v[static_cast<std::size_t>(i + 1)] - v[static_cast<std::size_t>(i)];
+  }
+  for (int i = 0; i < nv; ++i)
+    for (int c = 0; c < n; ++c)
+      J(nv + i, c) = -J(i, c);
+  return J;
+}
+
+// JointVelTermInfo::hatch with TT_USE_TIME (problem_description.cpp:1263-1344):
+// one term per joint over (x_j, dt) on steps [first, last] (already clamped)
+void addJointVelTimeTerm(TrajProblem& tp, const thip_problem_desc& d, int k)
+{
+  const int D = d.chain.n_dof, W = tp.n_cols;
+  const int first = d.jvt_first_step[k], last = d.jvt_last_step[k];
+  const int nv = last - first;
+  bool zero = true;
+  for (int j = 0; j < D; ++j)
+    zero = zero && std::fabs(d.jvt_upper_tols[k][j]) < 1e-5 && std::fabs(d.jvt_lower_tols[k][j]) < 1e-5;
+  for (int j = 0; j < D; ++j)
+  {
+    VarVector vars;
+    for (int i = first; i <= last; ++i)
+      vars.push_back(tp.traj_vars[static_cast<std::size_t>(i * W + j)]);
+    for (int i = first; i <= last; ++i)
+      vars.push_back(tp.traj_vars[static_cast<std::size_t>(i * W + D)]);
+    const double targ = d.jvt_targets[k][j], up = d.jvt_upper_tols[k][j], lo = d.jvt_lower_tols[k][j];
+    VectorOfVector f = [targ, up, lo](const DblVec& v) { return jointVelTimeErr(v, targ, up, lo); };
+    MatrixOfVector dfdx = [](const DblVec& v) { return jointVelTimeJac(v); };
+    const DblVec coeffs(static_cast<std::size_t>(nv * 2), d.jvt_coeffs[k][j]);
+    const std::string name = "joint_vel_time_" + std::to_string(k) + "_j" + std::to_string(j);
+    if (!d.jvt_is_cnt[k])
+      tp.prob->addCost(std::make_shared<CostFromErrFunc>(f, dfdx, vars, coeffs, zero ? SQUARED : HINGE, name));
+    else
+      tp.prob->addConstraint(std::make_shared<ConstraintFromErrFunc>(f, dfdx, vars, coeffs, zero ? EQ : INEQ, name));
+  }
+}
+
+// ------------------------------------------------------------ TotalTime
+// TotalTimeTermInfo::hatch (problem_description.cpp:1872-1913) over the last
+// variable column of steps 1..N-1; TimeCostCalculator / TimeCostJacCalculator
+// (kinematic_terms.cpp:579-591): sum(1/v) - limit, d/dv = -1/v^2
+void addTotalTimeTerm(TrajProblem& tp, const thip_problem_desc& d, int k)
+{
+  const int N = tp.n_steps, W = tp.n_cols;
+  VarVector vars;
+  for (int i = 1; i < N; ++i)
+    vars.push_back(tp.traj_vars[static_cast<std::size_t>(i * W + W - 1)]);
+  const double limit = d.ttt_limit[k];
+  VectorOfVector f = [limit](const DblVec& v) {
+    double s = 0;
+    for (double x : v)
+      s += 1.0 / x;
+    return DblVec{ s - limit };
+  };
+  MatrixOfVector dfdx = [](const DblVec& v) {
+    Mat J(1, static_cast<int>(v.size()));
+    for (int c = 0; c < static_cast<int>(v.size()); ++c)
+      J(0, c) = -1.0 / (v[static_cast<std::size_t>(c)] * v[static_cast<std::size_t>(c)]);
+    return J;
+  };
+  const bool zero = std::fabs(limit) < 1e-5;  // doubleEquals(limit, 0)
+  const DblVec coeffs{ d.ttt_coeff[k] };
+  const std::string name = "total_time_" + std::to_string(k);
+  if (!d.ttt_is_cnt[k])
+    tp.prob->addCost(std::make_shared<CostFromErrFunc>(f, dfdx, vars, coeffs, zero ? SQUARED : HINGE, name));
+  else
+    tp.prob->addConstraint(std::make_shared<ConstraintFromErrFunc>(f, dfdx, vars, coeffs, zero ? EQ : INEQ, name));
+}
+
 // ------------------------------------------------------------ construction
 TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj, const double* cart_targets,
                              const double* scene, const double* jpos_targets)
@@ -808,22 +905,40 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
   tp.n_steps = N;
   tp.n_dof = D;
   tp.prob = std::make_shared<OptProb>(toOsqpSettings(d.osqp));
-  // TrajOptProb ctor: variables j_i_j with joint-limit bounds (problem_description.cpp:557-598)
+  // TrajOptProb ctor: variables j_i_j with joint-limit bounds, and with use_time
+  // dt_i in [dt_lower, dt_upper] after each waypoint's joints
+  // (problem_description.cpp:557-598); generateInitTraj appends the constant
+  // init dt column (:372-379)
+  const int ut = d.use_time ? 1 : 0, W = D + ut;
+  tp.n_cols = W;
   std::vector<std::string> names;
   DblVec lb, ub;
   for (int i = 0; i < N; ++i)
+  {
     for (int j = 0; j < D; ++j)
     {
       names.push_back("j_" + std::to_string(i) + "_" + std::to_string(j));
       lb.push_back(d.chain.lower[j]);
       ub.push_back(d.chain.upper[j]);
     }
+    if (ut)
+    {
+      names.push_back("dt_" + std::to_string(i));
+      lb.push_back(d.dt_lower);
+      ub.push_back(d.dt_upper);
+    }
+  }
   tp.traj_vars = tp.prob->createVariables(names, lb, ub);
-  tp.init.assign(init_traj, init_traj + N * D);
-  std::vector<VarVector> rows(static_cast<std::size_t>(N));
+  for (int i = 0; i < N; ++i)
+  {
+    tp.init.insert(tp.init.end(), init_traj + i * D, init_traj + (i + 1) * D);
+    if (ut)
+      tp.init.push_back(d.init_dt);
+  }
+  std::vector<VarVector> rows(static_cast<std::size_t>(N));  // the joint variables of each waypoint
   for (int i = 0; i < N; ++i)
     rows[static_cast<std::size_t>(i)] =
-        VarVector(tp.traj_vars.begin() + i * D, tp.traj_vars.begin() + (i + 1) * D);
+        VarVector(tp.traj_vars.begin() + i * W, tp.traj_vars.begin() + i * W + D);
 
   // fixed timesteps: persistent linear equalities (problem_description.cpp:489-510)
   for (int f = 0; f < d.n_fixed; ++f)
@@ -833,6 +948,23 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
       tp.prob->addLinearConstraint(exprSub(AffExpr(rows[static_cast<std::size_t>(t)][static_cast<std::size_t>(j)]),
                                            init_traj[t * D + j]),
                                    EQ);
+  }
+  // fixed dofs: the joint pinned to the initial trajectory at every step that is
+  // not a fixed timestep (problem_description.cpp:528-546)
+  for (int k = 0; k < d.n_fixed_dofs; ++k)
+  {
+    const int j = d.fixed_dofs[k];
+    for (int i = 0; i < N; ++i)
+    {
+      bool fixed = false;
+      for (int f = 0; f < d.n_fixed; ++f)
+        fixed = fixed || d.fixed_steps[f] == i;
+      if (fixed)
+        continue;
+      tp.prob->addLinearConstraint(exprSub(AffExpr(rows[static_cast<std::size_t>(i)][static_cast<std::size_t>(j)]),
+                                           AffExpr(init_traj[i * D + j])),
+                                   EQ);
+    }
   }
 
   // cost_infos: JointVel, CartPose costs, collision cost
@@ -912,6 +1044,12 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
   for (int k = 0; k < d.n_jdt; ++k)
     if (!d.jdt_is_cnt[k])
       addJointDiffTerm(tp, rows, d, k);
+  for (int k = 0; k < d.n_jvt; ++k)
+    if (!d.jvt_is_cnt[k])
+      addJointVelTimeTerm(tp, d, k);
+  for (int k = 0; k < d.n_ttt; ++k)
+    if (!d.ttt_is_cnt[k])
+      addTotalTimeTerm(tp, d, k);
   if (d.coll_enabled && !d.coll_is_cnt)
     addCollisionTerms(tp, rows, d, scene);
   // cnt_infos: CartPose constraints, collision constraint
@@ -938,6 +1076,12 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
   for (int k = 0; k < d.n_jdt; ++k)
     if (d.jdt_is_cnt[k])
       addJointDiffTerm(tp, rows, d, k);
+  for (int k = 0; k < d.n_jvt; ++k)
+    if (d.jvt_is_cnt[k])
+      addJointVelTimeTerm(tp, d, k);
+  for (int k = 0; k < d.n_ttt; ++k)
+    if (d.ttt_is_cnt[k])
+      addTotalTimeTerm(tp, d, k);
   if (d.coll_enabled && d.coll_is_cnt)
     addCollisionTerms(tp, rows, d, scene);
   return tp;

@@ -22,8 +22,8 @@ namespace orc
 struct TrajProblem
 {
   OptProb::Ptr prob;
-  std::vector<Var> traj_vars;  // [n_steps * n_dof]
-  int n_steps = 0, n_dof = 0;
+  std::vector<Var> traj_vars;  // [n_steps * (n_dof + use_time)]: per step the joints, then dt (use_time)
+  int n_steps = 0, n_dof = 0, n_cols = 0;
   DblVec init;
 };
 

@@ -36,11 +36,15 @@ pytestmark = pytest.mark.skipif(not _have_asan(), reason="no libasan / libubsan 
 def built():
     import __graft_entry__
 
+    import fcntl
+
     __graft_entry__.build()
     jobs = str(min(8, os.cpu_count() or 1))
-    subprocess.run(["make", "-C", str(HOST), "-j", jobs, "san"], check=True, capture_output=True, text=True)
-    subprocess.run(["make", "-C", str(REPO / "oracle"), "-j", jobs, "build/kat_san"], check=True,
-                   capture_output=True, text=True)
+    with open(REPO / ".build.lock", "w") as lock:  # (parallel pytest workers)
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        subprocess.run(["make", "-C", str(HOST), "-j", jobs, "san"], check=True, capture_output=True, text=True)
+        subprocess.run(["make", "-C", str(REPO / "oracle"), "-j", jobs, "build/kat_san"], check=True,
+                       capture_output=True, text=True)
 
 
 def _run(cmd):

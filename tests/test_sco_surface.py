@@ -48,7 +48,7 @@ def test_oracle_sco_cases_meet_reference_assertions(oracle_mod, case):
 def test_joint_term_kats(built, oracle_mod, name):
     text, check = joint_terms.PROBLEMS[name]
     wl = joint_terms.workload(text, host)
-    assert (wl.desc.n_jdt == 0) == (name in joint_terms.LOWERABLE)
+    assert joint_terms.lowerable(wl.desc) == (name in joint_terms.LOWERABLE)
     x, res = oracle_mod.solve(wl)
     assert res[0].status == 0, (name, res[0].status)
     assert check(x[0]) == [], (name, check(x[0]))
@@ -85,3 +85,44 @@ def test_generic_path_refuses_device_only_terms(built):
     with pytest.raises(host.HostError) as ei:
         host.solve_json(json.dumps(doc))
     assert "evaluated by the batched GPU kernel only" in str(ei.value)
+
+
+def test_time_and_fixed_dof_lowering(built):
+    """use_time adds the dt column (TrajOptProb ctor, problem_description.cpp:557-598)
+    with the init dt appended (:372-379); time JointVel terms fill the jvt table
+    with the JointVel clamping; TotalTime and fixed dofs fill theirs."""
+    text, _ = joint_terms.PROBLEMS["inequality_jointVel_time"]
+    d, init, _, _ = host.lower_json(text)
+    assert d.use_time == 1 and (d.dt_lower, d.dt_upper) == (0.01234, 3.5678)
+    assert abs(d.init_dt - (3.5678 - 0.01234)) < 1e-15
+    assert init.shape == (joint_terms.STEPS, 7) and d.n_jdt == 0
+    assert d.n_jvt == 3 and [d.jvt_is_cnt[k] for k in range(3)] == [0, 0, 1]
+    assert [(d.jvt_first_step[k], d.jvt_last_step[k]) for k in range(3)] == [(0, 4), (5, 9), (0, 9)]
+    text, _ = joint_terms.PROBLEMS["equality_jointVel_time"]
+    d, _, _, _ = host.lower_json(text)
+    assert (d.jvt_first_step[1], d.jvt_last_step[1]) == (0, 1)  # last == first -> first + 1
+    text, _ = joint_terms.PROBLEMS["total_time_cnt"]
+    d, _, _, _ = host.lower_json(text)
+    assert d.n_ttt == 1 and d.ttt_is_cnt[0] == 1 and d.ttt_limit[0] == 5.8 and d.ttt_coeff[0] == 1.0
+    text, _ = joint_terms.PROBLEMS["fixed_dofs"]
+    d, _, _, _ = host.lower_json(text)
+    assert d.n_fixed_dofs == 2 and list(d.fixed_dofs)[:2] == [2, 5] and d.use_time == 0
+
+
+@pytest.mark.parametrize("edit, msg", [
+    (lambda doc: doc["basic_info"].update(use_time=True), "No terms use time"),
+    (lambda doc: doc["basic_info"].update(fixed_dofs=[7]), "greater than the number of DOF"),
+    (lambda doc: doc["costs"].append({"type": "total_time", "params": {"coeff": 1, "limit": 1, "bogus": 0}}),
+     "bogus"),
+])
+def test_time_front_door_errors(built, edit, msg):
+    """ConstructProblem's use_time consistency checks (problem_description.cpp:419-456)
+    and the fixed-dof range check (:515-520); TotalTime's params whitelist (:1868)."""
+    import json
+
+    doc = json.loads(joint_terms.PROBLEMS["equality_jointVel"][0])
+    edit(doc)
+    with pytest.raises(host.HostError) as ei:
+        host.lower_json(json.dumps(doc))
+    assert msg in str(ei.value)
+

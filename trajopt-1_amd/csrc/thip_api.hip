@@ -193,6 +193,11 @@ static int validate(const thip_problem_desc* d, std::string& why)
     return why = "JointAcc / JointJerk terms and JointVel equality constraints are not lowered into the batched "
                  "kernel: solve such a problem with sco::BasicTrustRegionSQP (the generic path, GpuModel)",
            THIP_E_INVALID;
+  if (d->use_time != 0 || d->n_jvt != 0 || d->n_ttt != 0 || d->n_fixed_dofs != 0)
+    return why = "time-parameterised problems (use_time, JointVel terms with use_time, TotalTime) and fixed dofs are not "
+                 "lowered into the batched kernel: solve such a problem with sco::BasicTrustRegionSQP (the generic "
+                 "path, GpuModel)",
+           THIP_E_INVALID;
   if (d->n_jpos < 0 || d->n_jpos > THIP_MAX_JPOS)
     return why = "n_jpos out of range", THIP_E_INVALID;
   for (int k = 0; k < d->n_jpos; ++k)

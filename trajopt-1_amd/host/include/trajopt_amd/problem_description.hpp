@@ -183,6 +183,10 @@ struct JointVelTermInfo : public TermInfo
   static TermInfo::Ptr create() { return std::make_shared<JointVelTermInfo>(); }
 };
 
+// (JointVelTermInfo with use_time: per joint a CostFromErrFunc / ConstraintFromErrFunc
+// over (x_j, dt) with the JointVelErrCalculator / JointVelJacCalculator error and
+// jacobian, recorded in the descriptor's jvt table; the generic path runs it.)
+
 // JointAccTermInfo / JointJerkTermInfo (problem_description.cpp:1393-1640): not
 // lowered into the batched kernel; their hatch() adds the JointAcc / JointJerk
 // cost or constraint objects (trajectory_costs.hpp) and records the term in the
@@ -204,6 +208,17 @@ struct JointJerkTermInfo : public TermInfo
   void fromJson(ProblemConstructionInfo& pci, const Json::Value& v) override;
   void hatch(TrajOptProb& prob) override;
   static TermInfo::Ptr create() { return std::make_shared<JointJerkTermInfo>(); }
+};
+
+// TotalTimeTermInfo (problem_description.hpp:623-633): the sum of 1/dt over steps
+// 1..N-1 against a limit (generic path)
+struct TotalTimeTermInfo : public TermInfo
+{
+  double coeff = 1, limit = 1;
+  TotalTimeTermInfo() : TermInfo(TermType::TT_COST | TermType::TT_CNT | TermType::TT_USE_TIME) {}
+  void fromJson(ProblemConstructionInfo& pci, const Json::Value& v) override;
+  void hatch(TrajOptProb& prob) override;
+  static TermInfo::Ptr create() { return std::make_shared<TotalTimeTermInfo>(); }
 };
 
 // CartPoseTermInfo (problem_description.hpp:353-387); poses are 3x4 row-major
@@ -296,11 +311,14 @@ public:
   sco::VarVector GetVarRow(int i, int start_col, int num_col) { return traj_vars_.rblock(i, start_col, num_col); }
   sco::VarVector GetVarRow(int i) { return traj_vars_.row(i); }
   sco::Var& GetVar(int i, int j) { return traj_vars_.at(i, j); }
-  VarArray& GetVars() { return traj_vars_; }
+  VarArray& GetVars() { return traj_vars_; }  // [n_steps][n_dof (+ dt with use_time)]
+  VarArray& GetJointVars() { return joint_vars_; }  // the joint columns (vars.block(0, 0, rows, n_dof))
+  bool GetHasTime() const { return desc_.use_time != 0; }
   int GetNumSteps() const { return desc_.n_steps; }
   int GetNumDOF() const { return desc_.chain.n_dof; }
   KinematicGroup::ConstPtr GetKin() const { return kin_; }
   Environment::ConstPtr GetEnv() const { return env_; }
+  // rows of n_dof joint values, plus the dt column with use_time (generateInitTraj)
   const std::vector<DblVec>& GetInitTraj() const { return init_; }
   void SetInitTraj(const std::vector<DblVec>& x) { init_ = x; }
 
@@ -332,7 +350,7 @@ private:
   std::vector<DblVec> init_;
   KinematicGroup::ConstPtr kin_;
   Environment::ConstPtr env_;
-  VarArray traj_vars_;
+  VarArray traj_vars_, joint_vars_;
   std::vector<const void*> lowered_;  // the lowered Cost / Constraint objects
 };
 

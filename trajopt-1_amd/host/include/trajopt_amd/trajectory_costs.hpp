@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "trajopt_sco/modeling.hpp"
+#include "trajopt_sco/modeling_utils.hpp"
 
 namespace trajopt
 {
@@ -100,6 +101,16 @@ private:
   JointDiffIneqCost rows_;
   bool clamp_;  // JointPosIneqConstraint returns the raw block, the others pospart
 };
+
+// JointVelErrCalculator / JointVelJacCalculator (kinematic_terms.cpp:434-475):
+// over v = (x_first..x_last, dt_first..dt_last), vel_i = (x_{i+1} - x_i) dt_{i+1},
+// error [-(upper - (vel - target)); lower - (vel - target)] and its jacobian
+sco::VectorOfVector::Ptr jointVelTimeErr(double target, double upper_tol, double lower_tol);
+sco::MatrixOfVector::Ptr jointVelTimeJac();
+// TimeCostCalculator / TimeCostJacCalculator (kinematic_terms.cpp:579-591):
+// sum(1/v) - limit and its row -1/v^2
+sco::VectorOfVector::Ptr totalTimeErr(double limit);
+sco::MatrixOfVector::Ptr totalTimeJac();
 
 // A term lowered into the batched kernel whose exact value / convexification
 // needs the device (CartPose FK and finite differences, collision signed

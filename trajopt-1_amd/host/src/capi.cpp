@@ -46,11 +46,10 @@ int thost_lower_json(const char* json_text, const double* scene, int n_prims, th
     auto prob = construct(json_text, scene, n_prims);
     if (desc)
       *desc = prob->desc();
-    if (init)
+    if (init)  // the joint columns
     {
-      double* o = init;
-      for (const auto& row : prob->GetInitTraj())
-        o = std::copy(row.begin(), row.end(), o);
+      const trajopt::LoweredProblem lp = prob->lowered();
+      std::copy(lp.init.begin(), lp.init.end(), init);
     }
     if (cart_targets)
       std::copy(prob->cart_targets.begin(), prob->cart_targets.end(), cart_targets);

@@ -74,7 +74,6 @@ trajopt::TermInfo::Ptr makeUnsupported()
   return std::make_shared<UnsupportedTermInfo>(kName);
 }
 constexpr char kCartVel[] = "cart_vel";
-constexpr char kTotalTime[] = "total_time";
 
 // problem_description.cpp:57-70
 void RegisterMakers()
@@ -88,7 +87,7 @@ void RegisterMakers()
   trajopt::TermInfo::RegisterMaker("joint_acc", &trajopt::JointAccTermInfo::create);
   trajopt::TermInfo::RegisterMaker("joint_jerk", &trajopt::JointJerkTermInfo::create);
   trajopt::TermInfo::RegisterMaker("collision", &trajopt::CollisionTermInfo::create);
-  trajopt::TermInfo::RegisterMaker("total_time", &makeUnsupported<kTotalTime>);
+  trajopt::TermInfo::RegisterMaker("total_time", &trajopt::TotalTimeTermInfo::create);
 }
 
 bool iequals(const std::string& a, const std::string& b)
@@ -199,7 +198,7 @@ trajopt::JointDiffSpec diffSpec(trajopt::TrajOptProb& prob, int order, const tra
                                 const trajopt::DblVec& lower, int first, int last)
 {
   trajopt::JointDiffSpec s;
-  s.vars = prob.GetVars();
+  s.vars = prob.GetJointVars();
   s.coeffs = coeffs;
   s.targets = targets;
   s.upper_tols = upper;
@@ -613,11 +612,46 @@ void JointVelTermInfo::hatch(TrajOptProb& prob)
   checkParameterSize(targets, n_dof, "JointVelTermInfo targets", true);
   checkParameterSize(upper_tols, n_dof, "JointVelTermInfo upper_tols", true);
   checkParameterSize(lower_tols, n_dof, "JointVelTermInfo lower_tols", true);
-  if (any(term_type & TermType::TT_USE_TIME))
-    unsupported("JointVelTermInfo with use_time");
   // doubleEquals(tol, 0) (problem_description.cpp:1254-1257): zero tolerances -> the Eq forms
   const bool zero_tols = allZero(upper_tols) && allZero(lower_tols);
   const bool is_cost = any(term_type & TermType::TT_COST);
+  if (any(term_type & TermType::TT_USE_TIME))
+  {
+    // :1263-1344: per joint, the (x_j, dt) columns of steps [first, last]
+    thip_problem_desc& d = prob.desc();
+    if (!prob.GetHasTime())
+      throw std::runtime_error("A term is using time and basic_info is not set correctly. Try basic_info.use_time = "
+                               "true");
+    if (d.n_jvt >= THIP_MAX_JVT)
+      unsupported("more than " + std::to_string(THIP_MAX_JVT) + " time-parameterised JointVel terms");
+    const int k = d.n_jvt++;
+    d.jvt_is_cnt[k] = is_cost ? 0 : 1;
+    d.jvt_first_step[k] = first;
+    d.jvt_last_step[k] = last;
+    const int nv = last - first, D = prob.GetNumDOF();
+    for (unsigned j = 0; j < n_dof; ++j)
+    {
+      d.jvt_coeffs[k][j] = coeffs[j];
+      d.jvt_targets[k][j] = targets[j];
+      d.jvt_upper_tols[k][j] = upper_tols[j];
+      d.jvt_lower_tols[k][j] = lower_tols[j];
+      sco::VarVector vars;
+      for (int i = first; i <= last; ++i)
+        vars.push_back(prob.GetVar(i, static_cast<int>(j)));
+      for (int i = first; i <= last; ++i)
+        vars.push_back(prob.GetVar(i, D));
+      const DblVec c(static_cast<std::size_t>(2 * nv), coeffs[j]);
+      const std::string nm = name + "_j" + std::to_string(j);
+      auto f = jointVelTimeErr(targets[j], upper_tols[j], lower_tols[j]);
+      if (is_cost)
+        prob.addCost(std::make_shared<sco::CostFromErrFunc>(f, jointVelTimeJac(), vars, c,
+                                                            zero_tols ? sco::SQUARED : sco::HINGE, nm));
+      else
+        prob.addConstraint(std::make_shared<sco::ConstraintFromErrFunc>(f, jointVelTimeJac(), vars, c,
+                                                                        zero_tols ? sco::EQ : sco::INEQ, nm));
+    }
+    return;
+  }
   const JointDiffSpec spec = diffSpec(prob, 1, coeffs, targets, upper_tols, lower_tols, first, last);
   thip_problem_desc& d = prob.desc();
   if (!is_cost && zero_tols)
@@ -729,6 +763,45 @@ void JointJerkTermInfo::hatch(TrajOptProb& prob)
 {
   hatchJointDiff(prob, term_type, 3, "JointJerkTermInfo", name, coeffs, targets, upper_tols, lower_tols, first_step,
                  last_step);
+}
+
+// ------------------------------------------------------------ TotalTime
+// problem_description.cpp:1860-1870
+void TotalTimeTermInfo::fromJson(ProblemConstructionInfo&, const Json::Value& v)
+{
+  if (!v.isMember("params"))
+    throw std::runtime_error("TotalTimeTermInfo: missing params");
+  const Json::Value& params = v["params"];
+  json_marshal::childFromJson(params, coeff, "coeff", 1.0);
+  json_marshal::childFromJson(params, limit, "limit", 1.0);
+  const char* all_fields[] = { "coeff", "limit" };
+  ensure_only_members(params, all_fields, sizeof(all_fields) / sizeof(char*));
+}
+
+// :1872-1913: the last variable column (dt with use_time) of steps 1..N-1
+void TotalTimeTermInfo::hatch(TrajOptProb& prob)
+{
+  thip_problem_desc& d = prob.desc();
+  if (d.n_ttt >= THIP_MAX_TTT)
+    unsupported("more than " + std::to_string(THIP_MAX_TTT) + " TotalTime terms");
+  const bool is_cost = any(term_type & TermType::TT_COST);
+  if (!is_cost && !any(term_type & TermType::TT_CNT))
+    throw std::runtime_error("A valid term type was not specified in TotalTimeTermInfo");
+  const int k = d.n_ttt++;
+  d.ttt_is_cnt[k] = is_cost ? 0 : 1;
+  d.ttt_coeff[k] = coeff;
+  d.ttt_limit[k] = limit;
+  const VarArray& tv = prob.GetVars();
+  sco::VarVector vars;
+  for (int i = 1; i < prob.GetNumSteps(); ++i)
+    vars.push_back(tv(i, tv.n_cols - 1));
+  const bool zero = std::fabs(limit) < 1e-5;  // doubleEquals(limit, 0)
+  if (is_cost)
+    prob.addCost(std::make_shared<sco::CostFromErrFunc>(totalTimeErr(limit), totalTimeJac(), vars, DblVec{ coeff },
+                                                        zero ? sco::SQUARED : sco::HINGE, name));
+  else
+    prob.addConstraint(std::make_shared<sco::ConstraintFromErrFunc>(totalTimeErr(limit), totalTimeJac(), vars,
+                                                                    DblVec{ coeff }, zero ? sco::EQ : sco::INEQ, name));
 }
 
 // ------------------------------------------------------------ CartPose
@@ -994,18 +1067,35 @@ TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci)
   const int n_steps = bi.n_steps;
   if (!pci.kin)
     throw std::runtime_error("ConstructProblem: pci.kin is null");
+  // problem_description.cpp:419-453
+  bool use_time = false;
   for (const auto& ci : pci.cost_infos)
-    if (!any(ci->getSupportedTypes() & TermType::TT_COST) ||
-        (any(ci->term_type & TermType::TT_USE_TIME) && !any(ci->getSupportedTypes() & TermType::TT_USE_TIME)))
-      throw std::runtime_error(ci->name + " is not a supported cost type");
+  {
+    if (!any(ci->getSupportedTypes() & TermType::TT_COST))
+      throw std::runtime_error(ci->name + " is only a constraint, but you listed it as a cost");
+    if (any(ci->term_type & TermType::TT_USE_TIME))
+    {
+      use_time = true;
+      if (!any(ci->getSupportedTypes() & TermType::TT_USE_TIME))
+        throw std::runtime_error(ci->name + " does not support time, but you listed it as a using time");
+    }
+  }
   for (const auto& ci : pci.cnt_infos)
-    if (!any(ci->getSupportedTypes() & TermType::TT_CNT) ||
-        (any(ci->term_type & TermType::TT_USE_TIME) && !any(ci->getSupportedTypes() & TermType::TT_USE_TIME)))
-      throw std::runtime_error(ci->name + " is not a supported constraint type");
-  if (bi.use_time)
-    unsupported("use_time (the 1/dt column)");
-  if (!bi.fixed_dofs.empty())
-    unsupported("basic_info.fixed_dofs");
+  {
+    if (!any(ci->getSupportedTypes() & TermType::TT_CNT))
+      throw std::runtime_error(ci->name + " is only a cost, but you listed it as a constraint");
+    if (any(ci->term_type & TermType::TT_USE_TIME))
+    {
+      use_time = true;
+      if (!any(ci->getSupportedTypes() & TermType::TT_USE_TIME))
+        throw std::runtime_error(ci->name + " does not support time, but you listed it as a using time");
+    }
+  }
+  if (use_time && !bi.use_time)
+    throw std::runtime_error("A term is using time and basic_info is not set correctly. Try basic_info.use_time = "
+                             "true");
+  if (!use_time && bi.use_time)
+    throw std::runtime_error("No terms use time and basic_info is not set correctly. Try basic_info.use_time = false");
   if (!iequals(bi.convex_solver, "OSQP") && !iequals(bi.convex_solver, "AUTO_SOLVER"))
     unsupported("convex_solver " + bi.convex_solver);
   if (n_steps < 2 || n_steps > THIP_MAX_STEPS)
@@ -1040,7 +1130,18 @@ TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci)
   for (const auto& row : init)
     if (static_cast<int>(row.size()) != n_dof)
       throw std::runtime_error("initial trajectory row has the wrong number of dofs");
+  // with use_time, the constant init dt column (problem_description.cpp:372-379)
+  if (bi.use_time)
+    for (auto& row : init)
+      row.push_back(pci.init_info.dt);
   prob->init_ = init;
+  d.use_time = bi.use_time ? 1 : 0;
+  if (bi.use_time)  // (zero otherwise: the descriptor of a problem without time is unchanged)
+  {
+    d.dt_lower = bi.dt_lower_lim;
+    d.dt_upper = bi.dt_upper_lim;
+    d.init_dt = pci.init_info.dt;
+  }
 
   // fixed timesteps (problem_description.cpp:489-510)
   if (bi.fixed_timesteps.size() > THIP_MAX_STEPS)
@@ -1054,6 +1155,25 @@ TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci)
       prob->addLinearConstraint(
           sco::exprSub(sco::AffExpr(prob->GetVar(t, j)), init[static_cast<std::size_t>(t)][static_cast<std::size_t>(j)]),
           sco::EQ);
+  }
+  // fixed dofs (:528-546): the joint pinned to the initial trajectory at every
+  // step that is not a fixed timestep
+  if (bi.fixed_dofs.size() > THIP_MAX_DOF)
+    throw std::runtime_error("too many fixed dofs");
+  for (int dof : bi.fixed_dofs)
+  {
+    // (the reference tests n_dof < dof; a dof equal to n_dof would index past the joints)
+    if (dof < 0 || dof >= n_dof)
+      throw std::runtime_error("DOF(aka Joint) indice is greater than the number of DOF available.");
+    d.fixed_dofs[d.n_fixed_dofs++] = dof;
+    for (int i = 0; i < n_steps; ++i)
+    {
+      if (std::find(bi.fixed_timesteps.begin(), bi.fixed_timesteps.end(), i) != bi.fixed_timesteps.end())
+        continue;
+      prob->addLinearConstraint(sco::exprSub(sco::AffExpr(prob->GetVar(i, dof)),
+                                             sco::AffExpr(init[static_cast<std::size_t>(i)][static_cast<std::size_t>(dof)])),
+                                sco::EQ);
+    }
   }
 
   // optimizer parameters: BasicTrustRegionSQP(prob) takes them from the caller
@@ -1095,18 +1215,33 @@ TrajOptProb::TrajOptProb(int n_steps, const ProblemConstructionInfo& pci)
   desc_.abi_version = THIP_ABI_VERSION;
   desc_.n_steps = n_steps;
   desc_.chain = kin_->chain;
+  desc_.use_time = pci.basic_info.use_time ? 1 : 0;
+  const int W = n_dof + desc_.use_time;
   std::vector<std::string> names;
   DblVec lb, ub;
   for (int i = 0; i < n_steps; ++i)
+  {
     for (int j = 0; j < n_dof; ++j)
     {
       names.push_back("j_" + std::to_string(i) + "_" + std::to_string(j));
       lb.push_back(kin_->chain.lower[j]);
       ub.push_back(kin_->chain.upper[j]);
     }
+    if (desc_.use_time)
+    {
+      names.push_back("dt_" + std::to_string(i));
+      lb.push_back(pci.basic_info.dt_lower_lim);
+      ub.push_back(pci.basic_info.dt_upper_lim);
+    }
+  }
   traj_vars_.n_rows = n_steps;
-  traj_vars_.n_cols = n_dof;
+  traj_vars_.n_cols = W;
   traj_vars_.data = createVariables(names, lb, ub);
+  joint_vars_.n_rows = n_steps;
+  joint_vars_.n_cols = n_dof;
+  for (int i = 0; i < n_steps; ++i)
+    for (int j = 0; j < n_dof; ++j)
+      joint_vars_.data.push_back(traj_vars_(i, j));
 }
 
 void TrajOptProb::addLoweredCost(sco::Cost::Ptr c)
@@ -1134,14 +1269,18 @@ std::string TrajOptProb::unloweredTerms() const
   return out;
 }
 
-bool TrajOptProb::lowerable() const { return desc_.n_jdt == 0 && unloweredTerms().empty(); }
+bool TrajOptProb::lowerable() const
+{
+  return desc_.n_jdt == 0 && desc_.n_jvt == 0 && desc_.n_ttt == 0 && !desc_.use_time && desc_.n_fixed_dofs == 0 &&
+         unloweredTerms().empty();
+}
 
 LoweredProblem TrajOptProb::lowered() const
 {
   LoweredProblem lp;
   lp.desc = desc_;
-  for (const auto& row : init_)
-    lp.init.insert(lp.init.end(), row.begin(), row.end());
+  for (const auto& row : init_)  // the joint columns
+    lp.init.insert(lp.init.end(), row.begin(), row.begin() + GetNumDOF());
   lp.cart_targets = cart_targets;
   lp.jpos_targets = jpos_targets;
   lp.scene = scene;

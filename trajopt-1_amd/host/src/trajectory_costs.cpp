@@ -207,6 +207,60 @@ sco::ConvexConstraints::Ptr JointDiffIneqConstraint::convex(const DblVec&, sco::
   return out;
 }
 
+sco::VectorOfVector::Ptr jointVelTimeErr(double target, double upper_tol, double lower_tol)
+{
+  return sco::VectorOfVector::construct([target, upper_tol, lower_tol](const DblVec& v) {
+    const std::size_t half = v.size() / 2, nv = half - 1;
+    DblVec out(2 * nv);
+    for (std::size_t i = 0; i < nv; ++i)
+    {
+      const double vel = (v[i + 1] - v[i]) * v[half + i + 1];
+      out[i] = -(upper_tol - (vel - target));
+      out[nv + i] = lower_tol - (vel - target);
+    }
+    return out;
+  });
+}
+
+sco::MatrixOfVector::Ptr jointVelTimeJac()
+{
+  return sco::MatrixOfVector::construct([](const DblVec& v) {
+    const int n = static_cast<int>(v.size()), half = n / 2, nv = half - 1;
+    sco::Mat J(2 * nv, n);
+    for (int i = 0; i < nv; ++i)
+    {
+      const int ti = i + half + 1;  // the dt of the velocity's second waypoint
+      J(i, i) = -1.0 * v[static_cast<std::size_t>(ti)];
+      J(i, i + 1) = 1.0 * v[static_cast<std::size_t>(ti)];
+      J(i, ti) = v[static_cast<std::size_t>(i + 1)] - v[static_cast<std::size_t>(i)];
+    }
+    for (int i = 0; i < nv; ++i)  // the bottom half: the negative velocities
+      for (int c = 0; c < n; ++c)
+        J(nv + i, c) = -J(i, c);
+    return J;
+  });
+}
+
+sco::VectorOfVector::Ptr totalTimeErr(double limit)
+{
+  return sco::VectorOfVector::construct([limit](const DblVec& v) {
+    double s = 0;
+    for (const double x : v)
+      s += 1.0 / x;
+    return DblVec{ s - limit };
+  });
+}
+
+sco::MatrixOfVector::Ptr totalTimeJac()
+{
+  return sco::MatrixOfVector::construct([](const DblVec& v) {
+    sco::Mat J(1, static_cast<int>(v.size()));
+    for (int c = 0; c < static_cast<int>(v.size()); ++c)
+      J(0, c) = -1.0 / (v[static_cast<std::size_t>(c)] * v[static_cast<std::size_t>(c)]);
+    return J;
+  });
+}
+
 double DeviceOnlyCost::value(const DblVec&)
 {
   throw std::runtime_error("term '" + name_ +

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 from pathlib import Path
 
-ABI_VERSION = 3  # THIP_ABI_VERSION
+ABI_VERSION = 5  # THIP_ABI_VERSION
 MAX_DOF = 16
 MAX_LINKS = 32
 MAX_STEPS = 64
@@ -20,6 +20,8 @@ MAX_PRIMS = 16
 MAX_JPOS = 8
 MAX_JVX = 4
 MAX_JDT = 8
+MAX_JVT = 4
+MAX_TTT = 2
 TRACE_W = 16  # THIP_TRACE_W
 DEBUG_NO_SEGMENT, DEBUG_FORCE_WIDE = 1, 2  # thip_debug_set_path flags
 
@@ -147,6 +149,24 @@ class ProblemDesc(C.Structure):
         ("jdt_targets", (C.c_double * MAX_DOF) * MAX_JDT),
         ("jdt_upper_tols", (C.c_double * MAX_DOF) * MAX_JDT),
         ("jdt_lower_tols", (C.c_double * MAX_DOF) * MAX_JDT),
+        ("use_time", C.c_int),
+        ("dt_lower", C.c_double),
+        ("dt_upper", C.c_double),
+        ("init_dt", C.c_double),
+        ("n_fixed_dofs", C.c_int),
+        ("fixed_dofs", C.c_int * MAX_DOF),
+        ("n_jvt", C.c_int),
+        ("jvt_is_cnt", C.c_int * MAX_JVT),
+        ("jvt_first_step", C.c_int * MAX_JVT),
+        ("jvt_last_step", C.c_int * MAX_JVT),
+        ("jvt_coeffs", (C.c_double * MAX_DOF) * MAX_JVT),
+        ("jvt_targets", (C.c_double * MAX_DOF) * MAX_JVT),
+        ("jvt_upper_tols", (C.c_double * MAX_DOF) * MAX_JVT),
+        ("jvt_lower_tols", (C.c_double * MAX_DOF) * MAX_JVT),
+        ("n_ttt", C.c_int),
+        ("ttt_is_cnt", C.c_int * MAX_TTT),
+        ("ttt_coeff", C.c_double * MAX_TTT),
+        ("ttt_limit", C.c_double * MAX_TTT),
         ("coll_enabled", C.c_int),
         ("coll_is_cnt", C.c_int),
         ("coll_first_step", C.c_int),

@@ -100,7 +100,7 @@ def solve_json(text: str, scene=None, device=0):
     False when it ran the host SQP loop with the GpuModel's QPs."""
     L = load_host()
     desc, _, _, _ = lower_json(text, scene)
-    N, D = desc.n_steps, desc.chain.n_dof
+    N, D = desc.n_steps, desc.chain.n_dof + (1 if desc.use_time else 0)  # (+ the dt column)
     sc = None if scene is None or len(scene) == 0 else np.ascontiguousarray(scene, dtype=np.float64)
     n_prims = 0 if sc is None else sc.shape[0]
     x = np.zeros((N, D))
