@@ -210,6 +210,9 @@ def main():
     ap.add_argument("--cpu-problems", type=int, default=0, help="0: max(128, 2 x threads), at most 1024")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this process may use")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--diag-util", action="store_true",
+                    help="diagnostic: per-problem cycle/wall counters over the timed steps (phase timers on; "
+                         "~1 %% slower) -> CU utilisation and shader clock on stderr")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -259,6 +262,9 @@ def main():
         if world > 1:
             dist.barrier()
 
+    if args.diag_util:
+        for s in solvers:
+            s.enable_profile(True)  # zeroed counters, accumulated over the timed launches
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -278,6 +284,13 @@ def main():
     # every timed launch, bracketed on its own stream (stage + sqp_kernel + gather; the
     # sqp_kernel share of a launch is > 97 % in profiles/*_kernel_stats.csv)
     kernel_ms = [a.elapsed_time(b) for a, b in events]
+    if args.diag_util:
+        pf = np.concatenate([s.get_profile() for s in solvers]).astype(np.float64)
+        n_cu = torch.cuda.get_device_properties(device).multi_processor_count
+        busy = pf[:, 14].sum() * 1e-8  # problem wall time, 10 ns units (s_memrealtime)
+        print(f"diag-util: {n_cu} CUs busy {100 * busy / (n_cu * elapsed):.1f} % of {elapsed:.2f} s; "
+              f"shader clock {pf[:, 13].sum() / pf[:, 14].sum() * 100:.0f} MHz; mean problem "
+              f"{busy / (len(solvers) and args.steps * wl.batch) * 1e3:.1f} ms", file=sys.stderr)
     x_last, res_last = solver.download()
     for s in solvers[1:min(len(solvers), args.steps)]:  # the contexts that ran a timed step
         _, r2 = s.download()

@@ -51,9 +51,11 @@ int thost_solve_json_batch_multi(const char* const* json_texts, int batch, const
  * `device`, as the reference's planning code runs one problem
  * (optimizers.cpp:699-991): a problem whose every term lowered into the
  * batched kernel runs it as a batch of one (*native = 1); one with terms the
- * kernel does not lower (JointAcc / JointJerk, JointVel equality constraints)
- * runs the SQP loop on the host with every QP on the GPU (GpuModel,
- * *native = 0).  x: [n_steps][n_dof]; result and native may be NULL. */
+ * kernel does not lower (JointAcc / JointJerk, JointVel equality constraints,
+ * time-parameterised JointVel, TotalTime, fixed dofs) runs the SQP loop on the
+ * host with every QP on the GPU (GpuModel, *native = 0).
+ * x: [n_steps][n_dof (+ 1: the dt column with basic_info.use_time)];
+ * result and native may be NULL. */
 int thost_solve_json(const char* json_text, const double* scene, int n_prims, int device, double* x,
                      thip_result* result, int* native, char* err, int err_len);
 

@@ -2,6 +2,7 @@
 
     python tools/phase_profile.py B 1024
 """
+import os
 import sys
 import time
 
@@ -11,6 +12,7 @@ import numpy as np
 from trajopt_amd import problems
 from trajopt_amd.runtime import BatchTrustRegionSQP
 
+os.makedirs("gpurun_out", exist_ok=True)
 cfg = sys.argv[1] if len(sys.argv) > 1 else "B"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 wl = problems.make_workload(cfg, B)
@@ -34,6 +36,8 @@ print(f"LVS sub-state passes per problem {subs.mean():.0f}; per scan call and st
 mhz = pf[:, 13].sum() / pf[:, 14].sum() * 100.0
 print(f"shader clock ~{mhz:.0f} MHz; per problem: admm {admm.mean():.0f} (max {admm.max():.0f}), "
       f"qp {qps.mean():.1f}, sqp {sqp.mean():.1f}")
+# per-problem wall time (10 ns units) for the dispatch simulation (tools/dispatch_sim.py)
+np.save(f"gpurun_out/pp_{cfg}_{B}_wall.npy", pf[:, 14])
 slowest = int(np.argmax(pf[:, 14]))
 print(f"slowest problem {slowest}: {pf[slowest, 14] / 100:.0f} us wall, admm {admm[slowest]:.0f}")
 tot = pf[:, 13].sum()
