@@ -653,6 +653,28 @@ def test_full_batch_every_problem(oracle_mod, cfg, rank):
     check_parity(wl, oracle_mod, x, res, label=label, min_strict=0.9)
 
 
+def test_dynamic_problem_assignment_matches_static(monkeypatch):
+    """Batches larger than the resident slots run persistent workgroups that take
+    problems from a counter (KernelArgs::work); the results are bitwise those of
+    the one-workgroup-per-problem mapping, run after run (the counter resets
+    itself at the end of each launch)."""
+    wl = problems.make_workload("A", 600)
+    s = BatchTrustRegionSQP(wl)
+    x1, r1 = s.optimize()
+    x2, r2 = s.optimize()  # a second launch on the same counter
+    s.close()
+    monkeypatch.setenv("THIP_STATIC_DISPATCH", "1")
+    s = BatchTrustRegionSQP(wl)
+    x0, r0 = s.optimize()
+    s.close()
+    np.testing.assert_array_equal(x1, x0)
+    np.testing.assert_array_equal(x2, x0)
+    for a, b, c in zip(r0, r1, r2):
+        assert (a.status, a.n_sqp_iters, a.n_admm_iters, a.total_cost) == (b.status, b.n_sqp_iters, b.n_admm_iters,
+                                                                             b.total_cost)
+        assert (b.n_admm_iters, b.total_cost) == (c.n_admm_iters, c.total_cost)
+
+
 @pytest.mark.timeout(1500)
 def test_full_batch_E_512(oracle_mod):
     """Config E at one GPU's share of configs[4] (4096 problems over 8 GPUs):

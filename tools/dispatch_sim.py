@@ -51,6 +51,12 @@ def simulate(dur, steps, inflight, cus=256, order=None):
     return t_end
 
 
+def simulate_xcd(dur, steps, inflight, cus=256, xcds=8):
+    """The same with the grid dealt round-robin over `xcds` dies (workgroup i runs
+    on die i % xcds, cus / xcds CUs each): the slowest die ends the run."""
+    return max(simulate(dur[x::xcds], steps, inflight, cus // xcds) for x in range(xcds))
+
+
 def main():
     dur = np.load(sys.argv[1]).astype(np.float64) * 1e-8  # seconds
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
@@ -60,7 +66,9 @@ def main():
           f"work / {cus} CUs = {bound * 1e3:.0f} ms per batch")
     for inflight in (1, 2, 3, 4, 6, 8, steps):
         t = simulate(dur, steps, inflight, cus)
-        print(f"  {inflight:2d} in flight: {t / steps * 1e3:7.0f} ms/step ({bound * steps / t * 100:5.1f} % of the bound)")
+        tx = simulate_xcd(dur, steps, inflight, cus)
+        print(f"  {inflight:2d} in flight: {t / steps * 1e3:7.0f} ms/step ({bound * steps / t * 100:5.1f} % of the bound); "
+              f"grid dealt over 8 XCDs: {tx / steps * 1e3:7.0f} ms/step ({bound * steps / tx * 100:5.1f} %)")
 
 
 if __name__ == "__main__":

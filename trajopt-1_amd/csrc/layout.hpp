@@ -269,6 +269,11 @@ struct KernelArgs
   const double* stage_init;  // [batch][nx]
   const double* stage_tgt;   // [batch][n_cart][12]
   double* xout;              // [batch][nx]
+  // dynamic problem assignment (null = workgroup b solves problem b): the grid
+  // holds one workgroup per resident slot and each workgroup takes the next
+  // problem from work[0] until the batch is exhausted; the last workgroup to
+  // finish (work[1]) resets both to 0 for the next launch on the stream
+  int* work;
 };
 
 constexpr int kHPack = 14;  // doubles per hinge row in A_HPK

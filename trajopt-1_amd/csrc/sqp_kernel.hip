@@ -5301,24 +5301,62 @@ done:
   BSYNC();
 }
 
+__device__ __forceinline__ void solve_problem(const KernelArgs& args, int b, double* dyn, Ctl& ctl,
+                                              double** ptab, CollStage& cstage);
+
 __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
 {
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ Ctl ctl;
-  const int b = blockIdx.x;
-  if (b >= args.batch)
-    return;
-  stage_chain(args.desc);
-  const Layout& L = args.L;
+  __shared__ int next_problem;
   // LDS residency plan (Layout::loff): hot QP arrays live in LDS for the
   // whole launch, the rest in this problem's HBM workspace
   __shared__ double* ptab[A_COUNT];
+  __shared__ CollStage cstage;
+  if (!args.work && static_cast<int>(blockIdx.x) >= args.batch)
+    return;
+  stage_chain(args.desc);
+  const Layout& L = args.L;
+  // One problem per workgroup (args.work null), or a persistent workgroup per
+  // resident slot taking problems in order from the launch's counter: the
+  // grid is dealt round-robin over the XCDs, so with a static mapping each
+  // die solves a fixed eighth of the batch and the die with the heaviest
+  // eighth ends the launch; with the counter, a die that finishes its
+  // problems early takes more.  Every problem is still solved by one
+  // workgroup from its own inputs, so results do not depend on the mapping.
+  for (int b = blockIdx.x;;)
+  {
+    if (args.work)
+    {
+      __syncthreads();  // the previous problem is done with next_problem
+      if (threadIdx.x == 0)
+        next_problem = atomicAdd(&args.work[0], 1);
+      __syncthreads();
+      b = __builtin_amdgcn_readfirstlane(next_problem);
+      if (b >= args.batch)
+        break;
+    }
+    solve_problem(args, b, dyn, ctl, ptab, cstage);
+    if (!args.work)
+      return;
+  }
+  // the last workgroup out resets the counters for the stream's next launch
+  if (threadIdx.x == 0 && atomicAdd(&args.work[1], 1) == static_cast<int>(gridDim.x) - 1)
+  {
+    atomicExch(&args.work[0], 0);
+    atomicExch(&args.work[1], 0);
+  }
+}
+
+__device__ __forceinline__ void solve_problem(const KernelArgs& args, int b, double* dyn, Ctl& ctl,
+                                              double** ptab, CollStage& cstage)
+{
+  const Layout& L = args.L;
   double* wsb = args.ws + (long long)b * L.dstride;
   for (int k = threadIdx.x; k < A_COUNT; k += kBlock)
     ptab[k] = L.loff[k] >= 0 ? dyn + L.loff[k] : wsb + L.doff[k];
   Ctx c(L, args.T, args.desc, wsb, args.iws + (long long)b * L.istride, dyn, &ctl, ptab);
   c.ptab_w = L.hinge ? ptab : nullptr;
-  __shared__ CollStage cstage;
   c.cs = &cstage;
   c.scene = args.scene ? args.scene + (long long)b * (args.desc->n_prims > 0 ? args.desc->n_prims : 1) * 16 : nullptr;
   c.jpt = args.jpt + (long long)b * (L.n_jpos > 0 ? L.n_jpos : 1) * L.D;

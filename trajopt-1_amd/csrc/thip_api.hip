@@ -58,6 +58,8 @@ struct thip_ctx
   bool ran = false;
   size_t lds_bytes = 0;      // sqp_kernel: scratch + LDS-resident arrays
   size_t lds_lin_bytes = 0;  // linearize_kernel: scratch only
+  int* d_work = nullptr;     // sqp_kernel's problem counter (KernelArgs::work); null: static mapping
+  int grid = 0;              // sqp_kernel workgroups (resident slots, or the batch)
   std::string err;
 };
 
@@ -829,6 +831,26 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ctx->lds_lin_bytes))) !=
           hipSuccess)
     return fail(std::string("hipFuncSetAttribute(dynamic LDS): ") + hipGetErrorString(e));
+  // dynamic problem assignment: one persistent workgroup per resident slot
+  // (KernelArgs::work), unless THIP_STATIC_DISPATCH is set
+  ctx->grid = batch;
+  if (!std::getenv("THIP_STATIC_DISPATCH"))
+  {
+    int per_cu = 0, n_cu = 0;
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&sqp_kernel), kBlock,
+                                                          ctx->lds_bytes)) != hipSuccess ||
+        (e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
+      return fail(std::string("occupancy query: ") + hipGetErrorString(e));
+    const long long slots = static_cast<long long>(std::max(per_cu, 1)) * std::max(n_cu, 1);
+    if (slots < batch)
+    {
+      if ((e = hipMalloc(&ctx->d_work, 2 * sizeof(int))) != hipSuccess ||
+          (e = hipMemsetAsync(ctx->d_work, 0, 2 * sizeof(int), ctx->stream)) != hipSuccess ||
+          (e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
+        return fail(std::string("work counter: ") + hipGetErrorString(e));
+      ctx->grid = static_cast<int>(slots);
+    }
+  }
   *out = ctx;
   return THIP_OK;
 }
@@ -865,6 +887,7 @@ static KernelArgs make_args(thip_ctx* ctx)
   a.stage_init = nullptr;
   a.stage_tgt = nullptr;
   a.xout = nullptr;
+  a.work = nullptr;
   return a;
 }
 
@@ -959,8 +982,10 @@ int thip_sqp_run(thip_ctx* ctx)
   a.stage_init = ctx->d_init;
   a.stage_tgt = ctx->d_tgt;
   a.xout = ctx->d_x;
+  a.work = ctx->d_work;
   HIPCHK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-  hipLaunchKernelGGL(sqp_kernel, dim3(ctx->batch), dim3(kBlock), ctx->lds_bytes, ctx->stream, a);
+  hipLaunchKernelGGL(sqp_kernel, dim3(ctx->d_work ? ctx->grid : ctx->batch), dim3(kBlock), ctx->lds_bytes,
+                     ctx->stream, a);
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
   ctx->ran = true;
@@ -1216,6 +1241,7 @@ void thip_destroy(thip_ctx* ctx)
   hipFree(ctx->d_ws);
   hipFree(ctx->d_iws);
   hipFree(ctx->d_res);
+  hipFree(ctx->d_work);
   hipFree(ctx->d_init);
   hipFree(ctx->d_tgt);
   hipFree(ctx->d_scene);
