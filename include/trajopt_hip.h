@@ -517,6 +517,32 @@ int thip_qp_solve(thip_qp* qp, const double* P_values, const double* q, const do
 void thip_qp_destroy(thip_qp* qp);
 const char* thip_qp_last_error(thip_qp* qp); /* NULL: the last thip_qp_create failure */
 
+/* Resident workspace (update in place).  The OSQP 1.0 solver object of every QP
+ * of the batch stays on the device between calls, as OsqpEigen::Solver keeps it
+ * for trajopt_sqp::OSQPEigenSolver (the QPSolver of the trajopt_sqp front end,
+ * trajopt_optimizers/trajopt_sqp/src/osqp_eigen_solver.cpp:73-320, driven by
+ * TrustRegionSQPSolver::stepSQPSolver, trust_region_sqp_solver.cpp:202-260):
+ * after thip_qp_setup, only the vectors / values that changed are sent, the
+ * scaling, rho vector, KKT factor and ADMM iterates persist.  Host arrays,
+ * [batch][...], synchronous.  info->status is -1 with setup_error set when a
+ * call fails (1 data validation: l > u, the update is rejected; 4 / 5 the
+ * refactorisation failed / is not quasi-definite: the workspace is gone, the
+ * next call must be thip_qp_setup), 0 otherwise (thip_qp_solve_resident:
+ * the OSQP status). */
+/* osqp_setup: Ruiz scaling, rho vector, KKT factor; x = z = y = 0 */
+int thip_qp_setup(thip_qp* qp, const double* P_values, const double* q, const double* A_values, const double* l,
+                  const double* u, const thip_osqp_settings* settings, thip_qp_info* info);
+/* osqp_update_data_vec: q and / or (l, u) (NULL = unchanged); the rho vector follows the
+ * constraint types, refactored only when a type changed */
+int thip_qp_update_vec(thip_qp* qp, const double* q, const double* l, const double* u, thip_qp_info* info);
+/* osqp_update_data_mat: all values of P and / or A (same pattern; NULL = unchanged):
+ * unscale, replace, rescale, refactor */
+int thip_qp_update_mat(thip_qp* qp, const double* P_values, const double* A_values, thip_qp_info* info);
+/* osqp_warm_start: x and / or y (unscaled; NULL = unchanged), z = A x; turns warm starting on */
+int thip_qp_warm_start(thip_qp* qp, const double* x, const double* y);
+/* osqp_solve from the kept iterates (warm_starting) or from zero: x [batch][n], y [batch][m] (may be NULL) */
+int thip_qp_solve_resident(thip_qp* qp, double* x, double* y, thip_qp_info* info);
+
 #ifdef __cplusplus
 }
 #endif

@@ -237,3 +237,21 @@ def run_kats():
         build()
     p = subprocess.run([str(KAT)], capture_output=True, text=True)
     return p.returncode, p.stdout
+
+
+def tsqp_solve(spec, variant="exact"):
+    """The trajopt_sqp front end (src/trajopt_sqp.cpp: TrustRegionSQPSolver over
+    TrajOptQPProblem with OSQPEigenSolver's update-in-place QP) on one
+    trajopt_amd.tsqp.Spec -> (x [n_nodes, n_dof], tsqp.Result)."""
+    from trajopt_amd import tsqp  # the spec layout (include/trajopt_host.h)
+
+    L = lib(variant)
+    if not hasattr(L, "_tsqp_ready"):
+        L.oracle_tsqp_solve.argtypes = [C.POINTER(tsqp.Spec), C.POINTER(C.c_double), C.POINTER(tsqp.Result)]
+        L.oracle_tsqp_solve.restype = C.c_int
+        L._tsqp_ready = True
+    x = np.zeros((spec.n_nodes, spec.n_dof))
+    res = tsqp.Result()
+    if L.oracle_tsqp_solve(C.byref(spec), _dp(x), C.byref(res)) != 0:
+        raise RuntimeError("oracle_tsqp_solve: " + L.oracle_last_error().decode())
+    return x, res

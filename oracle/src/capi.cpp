@@ -412,3 +412,32 @@ int oracle_sizeof_desc() { return static_cast<int>(sizeof(thip_problem_desc)); }
 int oracle_sizeof_result() { return static_cast<int>(sizeof(thip_result)); }
 
 }  // extern "C"
+
+// trajopt_sqp front end (trajopt_sqp.hpp): x [n_nodes][n_dof]
+#include "trajopt_sqp.hpp"
+extern "C" int oracle_tsqp_solve(const tsqp_spec* spec, double* x, tsqp_result* result)
+{
+  try
+  {
+    const orc::tsqp::Result r = orc::tsqp::solve(*spec);
+    std::memcpy(x, r.x.data(), sizeof(double) * r.x.size());
+    if (result)
+    {
+      std::memset(result, 0, sizeof(*result));
+      result->status = r.status;
+      result->overall_iteration = r.overall_iteration;
+      result->penalty_iteration = r.penalty_iteration;
+      result->qp_setups = r.qp_setups;
+      result->qp_updates = r.qp_updates;
+      result->qp_solves = r.qp_solves;
+      result->admm_iters = r.admm_iters;
+      result->best_exact_merit = r.best_exact_merit;
+    }
+    return 0;
+  }
+  catch (const std::exception& e)
+  {
+    g_err = e.what();
+    return -1;
+  }
+}

@@ -355,6 +355,109 @@ void OsqpSolver::scale_data()
   }
 }
 
+// OSQP 1.0 unscale_data: P <- cinv Dinv P Dinv, q <- Dinv (cinv q), A <- Einv A Dinv,
+// l <- Einv l, u <- Einv u
+void OsqpSolver::unscale_data()
+{
+  for (OsqpInt j = 0; j < P_.n; ++j)
+    for (OsqpInt p = P_.p[j]; p < P_.p[j + 1]; ++p)
+      P_.x[p] = ((P_.x[p] * cinv_) * Dinv_[P_.i[p]]) * Dinv_[j];
+  for (OsqpInt j = 0; j < n_; ++j)
+    q_[j] = (q_[j] * cinv_) * Dinv_[j];
+  for (OsqpInt j = 0; j < A_.n; ++j)
+    for (OsqpInt p = A_.p[j]; p < A_.p[j + 1]; ++p)
+      A_.x[p] = (A_.x[p] * Einv_[A_.i[p]]) * Dinv_[j];
+  for (OsqpInt r = 0; r < m_; ++r)
+  {
+    l_[r] = l_[r] * Einv_[r];
+    u_[r] = u_[r] * Einv_[r];
+  }
+}
+
+// OSQP 1.0 update_rho_vec: the rows whose constraint type changed get the rho
+// of their new type; refactor only if one did
+int OsqpSolver::update_rho_vec()
+{
+  bool changed = false;
+  for (OsqpInt i = 0; i < m_; ++i)
+  {
+    int ct;
+    double rv;
+    if (l_[i] < -OSQP_INFTY * OSQP_MIN_SCALING && u_[i] > OSQP_INFTY * OSQP_MIN_SCALING)
+    {
+      ct = -1;
+      rv = OSQP_RHO_MIN;
+    }
+    else if (u_[i] - l_[i] < OSQP_RHO_TOL)
+    {
+      ct = 1;
+      rv = OSQP_RHO_EQ_OVER_RHO_INEQ * settings_.rho;
+    }
+    else
+    {
+      ct = 0;
+      rv = settings_.rho;
+    }
+    if (constr_type_[i] != ct)
+    {
+      constr_type_[i] = ct;
+      rho_vec_[i] = rv;
+      rho_inv_vec_[i] = 1.0 / rv;
+      kkt_.x[kkt_rho_diag_[i]] = -rho_inv_vec_[i];
+      changed = true;
+    }
+  }
+  if (!changed)
+    return 0;
+  const int npos = ldl_.refactor(kkt_);
+  if (npos < 0)
+    return 4;
+  return (npos < n_) ? 5 : 0;
+}
+
+int OsqpSolver::update_data_vec(const double* q, const double* l, const double* u)
+{
+  if (l && u)
+    for (OsqpInt i = 0; i < m_; ++i)
+      if (l[i] > u[i])
+        return 1;  // OSQP_DATA_VALIDATION_ERROR, data unchanged
+  const bool sc = settings_.scaling > 0;
+  if (q)
+    for (OsqpInt j = 0; j < n_; ++j)
+      q_[j] = sc ? (D_[j] * q[j]) * c_ : q[j];
+  if (l && u)
+  {
+    for (OsqpInt i = 0; i < m_; ++i)
+    {
+      l_[i] = sc ? E_[i] * l[i] : l[i];
+      u_[i] = sc ? E_[i] * u[i] : u[i];
+    }
+    return update_rho_vec();
+  }
+  return 0;
+}
+
+int OsqpSolver::update_data_mat(const double* Px, const double* Ax)
+{
+  const bool sc = settings_.scaling > 0;
+  if (sc)
+    unscale_data();
+  if (Px)
+    std::copy(Px, Px + P_.nnz(), P_.x.begin());
+  if (Ax)
+    std::copy(Ax, Ax + A_.nnz(), A_.x.begin());
+  if (sc)
+    scale_data();
+  At_ = csc_transpose(A_);
+  // linsys update_matrices: the KKT values with the current rho vector
+  const int e = build_and_factor_kkt();
+  if (e == 1)
+    return 4;
+  if (e == 2)
+    return 5;
+  return 0;
+}
+
 void OsqpSolver::set_rho_vec()
 {
   settings_.rho = std::min(std::max(settings_.rho, OSQP_RHO_MIN), OSQP_RHO_MAX);

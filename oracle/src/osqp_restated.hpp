@@ -112,6 +112,13 @@ public:
             const OsqpSettings& settings);
   int warm_start(const double* x, const double* y);
   int solve();
+  // OSQP 1.0 update-in-place API (the resident solver object OsqpEigen keeps for
+  // trajopt_sqp::OSQPEigenSolver): osqp_update_data_vec (q and / or l, u; NULL =
+  // unchanged; the rho vector follows the constraint types, refactored only
+  // when one changed) and osqp_update_data_mat (all P / A values, same pattern:
+  // unscale_data, replace, scale_data, refactor).  0 or an OSQP error code.
+  int update_data_vec(const double* q, const double* l, const double* u);
+  int update_data_mat(const double* Px, const double* Ax);
 
   // unscaled solution
   std::vector<double> sol_x, sol_y;
@@ -145,6 +152,8 @@ private:
   OsqpSettings settings_;
 
   void scale_data();
+  void unscale_data();
+  int update_rho_vec();
   void set_rho_vec();
   int build_and_factor_kkt();
   int update_rho(double rho_new);

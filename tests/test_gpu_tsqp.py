@@ -1,0 +1,130 @@
+"""GPU tests of the trajopt_sqp front end: the product --
+trajopt_sqp::TrustRegionSQPSolver over a TrajOptQPProblem with the QP in
+thip_qp's resident GPU workspace (GpuQPSolver: set up once, then updated in
+place) -- against the oracle's restatement with OSQP's update-in-place calls
+(oracle/src/trajopt_sqp.cpp), on the reference's joint optimisation units and
+seeded trajectory problems: identical status and iteration counts, the same
+number of setups and in-place updates, trajectories within 1e-5."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import tsqp_cases
+from trajopt_amd import abi, tsqp
+
+pytestmark = pytest.mark.gpu
+TOL_X = 1e-5
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    abi.load_hip()
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need an AMD GPU"
+
+
+def _compare(spec, oracle_mod):
+    x, r = tsqp.solve(spec)
+    xo, ro = oracle_mod.tsqp_solve(spec)
+    assert tsqp.STATUS[r.status] == tsqp.STATUS[ro.status]
+    assert (r.overall_iteration, r.penalty_iteration) == (ro.overall_iteration, ro.penalty_iteration)
+    assert (r.qp_setups, r.qp_updates, r.qp_solves) == (ro.qp_setups, ro.qp_updates, ro.qp_solves)
+    dx = float(np.abs(x - xo).max())
+    assert dx <= TOL_X, dx
+    return x, r, ro
+
+
+@pytest.mark.parametrize("name", list(tsqp_cases.reference_units()))
+def test_reference_units(gpu, oracle_mod, name):
+    spec, expect = tsqp_cases.reference_units()[name]
+    x, r, _ = _compare(spec, oracle_mod)
+    assert tsqp.STATUS[r.status] == "SQP_CONVERGED"
+    assert r.qp_setups == 1  # one device setup, later convexifications in place
+    flat = x.reshape(-1)
+    for sl, val, tol in expect:  # the reference's EXPECT_NEAR values
+        assert np.all(np.abs(flat[sl] - val) <= tol), (name, flat[sl], val)
+
+
+@pytest.mark.parametrize("kind,seed", tsqp_cases.SYNTHETIC)
+def test_synthetic_parity(gpu, oracle_mod, kind, seed):
+    _, r, _ = _compare(tsqp_cases.synthetic(kind, seed), oracle_mod)
+    assert r.qp_setups == 1 and r.qp_updates >= 1
+
+
+def _qp_lib():
+    L = abi.load_hip()
+    P = C.POINTER
+    dp, ip = P(C.c_double), P(C.c_int)
+    L.thip_qp_create.argtypes = [C.c_int, C.c_int, C.c_int, ip, ip, ip, ip, C.c_int, P(C.c_void_p)]
+    L.thip_qp_solve.argtypes = [C.c_void_p, dp, dp, dp, dp, dp, P(abi.OsqpSettings), dp, dp, dp, dp, dp, C.c_void_p]
+    L.thip_qp_setup.argtypes = [C.c_void_p, dp, dp, dp, dp, dp, P(abi.OsqpSettings), C.c_void_p]
+    L.thip_qp_update_vec.argtypes = [C.c_void_p, dp, dp, dp, C.c_void_p]
+    L.thip_qp_update_mat.argtypes = [C.c_void_p, dp, dp, C.c_void_p]
+    L.thip_qp_warm_start.argtypes = [C.c_void_p, dp, dp]
+    L.thip_qp_solve_resident.argtypes = [C.c_void_p, dp, dp, C.c_void_p]
+    L.thip_qp_destroy.argtypes = [C.c_void_p]
+    return L
+
+
+def test_resident_setup_equals_one_shot(gpu):
+    """thip_qp_setup + thip_qp_solve_resident from a cold start is osqp_setup +
+    osqp_solve: bitwise the one-shot thip_qp_solve; an in-place update of q, l, u
+    and the A values followed by a resident solve stays a valid OSQP solve of the
+    new data (KKT residuals at the tolerance)."""
+    L = _qp_lib()
+    rng = np.random.default_rng(7)
+    n, m0 = 12, 8
+    M = rng.normal(size=(n, n))
+    Pd = M @ M.T + np.eye(n)
+    Pu = np.triu(Pd)
+    A = np.vstack([rng.normal(size=(m0, n)) * (rng.random((m0, n)) < 0.5), np.eye(n)])
+    m = A.shape[0]
+
+    def csc(Mx):
+        p, i, x = [0], [], []
+        for j in range(Mx.shape[1]):
+            nz = np.nonzero(Mx[:, j])[0]
+            i += list(nz)
+            x += list(Mx[nz, j])
+            p.append(len(i))
+        return (np.array(p, dtype=np.int32), np.array(i, dtype=np.int32), np.array(x, dtype=np.float64))
+
+    Pp, Pi, Px = csc(Pu)
+    Ap, Ai, Ax = csc(A)
+    q = rng.normal(size=n)
+    lo = np.concatenate([rng.uniform(-1, 0, m0), np.full(n, -2.0)])
+    up = np.concatenate([rng.uniform(0, 1, m0), np.full(n, 2.0)])
+    s = abi.OsqpSettings()
+    abi.load_hip().thip_default_osqp_settings(C.byref(s))
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))  # noqa: E731
+    h = C.c_void_p()
+    assert L.thip_qp_create(0, n, m, ip(Pp), ip(Pi), ip(Ap), ip(Ai), 1, C.byref(h)) == 0
+    info = (C.c_byte * 64)()
+    x1, y1 = np.zeros(n), np.zeros(m)
+    assert L.thip_qp_solve(h, dp(Px), dp(q), dp(Ax), dp(lo), dp(up), C.byref(s), None, None, None, dp(x1), dp(y1),
+                           info) == 0
+    x2, y2 = np.zeros(n), np.zeros(m)
+    assert L.thip_qp_setup(h, dp(Px), dp(q), dp(Ax), dp(lo), dp(up), C.byref(s), info) == 0
+    assert L.thip_qp_solve_resident(h, dp(x2), dp(y2), info) == 0
+    assert np.array_equal(x1, x2) and np.array_equal(y1, y2)
+    # in place: new q, bounds and A values, then the warm-started resident solve
+    q2 = q + 0.1 * rng.normal(size=n)
+    Ax2 = Ax * (1 + 0.05 * rng.normal(size=Ax.shape))
+    lo2, up2 = lo - 0.1, up + 0.1
+    assert L.thip_qp_update_vec(h, dp(q2), None, None, info) == 0
+    assert L.thip_qp_update_mat(h, None, dp(Ax2), info) == 0
+    assert L.thip_qp_update_vec(h, None, dp(lo2), dp(up2), info) == 0
+    x3, y3 = np.zeros(n), np.zeros(m)
+    assert L.thip_qp_solve_resident(h, dp(x3), dp(y3), info) == 0
+    # A with the new CSC values
+    A2 = np.zeros_like(A)
+    for j in range(n):
+        for e in range(Ap[j], Ap[j + 1]):
+            A2[Ai[e], j] = Ax2[e]
+    r_prim = np.abs(np.clip(A2 @ x3, lo2, up2) - A2 @ x3).max()
+    r_dual = np.abs(Pd @ x3 + q2 + A2.T @ y3).max()
+    assert r_prim < 1e-4 and r_dual < 1e-4, (r_prim, r_dual)
+    L.thip_qp_destroy(h)

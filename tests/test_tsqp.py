@@ -1,0 +1,67 @@
+"""CPU tests of the trajopt_sqp front end: the oracle's
+restatement of TrustRegionSQPSolver / TrajOptQPProblem / OSQPEigenSolver
+(oracle/src/trajopt_sqp.cpp) pinned by the reference's own joint optimisation
+units, and the product's problem construction (thost_tsqp_solve) rejecting bad
+input with the reference's messages before any GPU work."""
+import numpy as np
+import pytest
+
+import tsqp_cases
+from trajopt_amd import tsqp
+
+
+@pytest.mark.parametrize("name", list(tsqp_cases.reference_units()))
+def test_oracle_reference_units(oracle_mod, name):
+    spec, expect = tsqp_cases.reference_units()[name]
+    x, res = oracle_mod.tsqp_solve(spec)
+    assert tsqp.STATUS[res.status] == "SQP_CONVERGED"
+    flat = x.reshape(-1)
+    for sl, val, tol in expect:
+        assert np.all(np.abs(flat[sl] - val) <= tol), (name, flat[sl], val)
+    # one QP setup, every later convexification applied in place
+    assert res.qp_setups == 1
+
+
+@pytest.mark.parametrize("kind,seed", tsqp_cases.SYNTHETIC[::4])
+def test_oracle_synthetic_runs(oracle_mod, kind, seed):
+    spec = tsqp_cases.synthetic(kind, seed)
+    x, res = oracle_mod.tsqp_solve(spec)
+    assert np.all(np.isfinite(x))
+    assert res.qp_setups == 1 and res.qp_updates >= 1  # the pattern persists across convexifications
+    if kind == "penalty":
+        assert tsqp.STATUS[res.status] in ("SQP_PENALTY_ITERATION_LIMIT", "SQP_ITERATION_LIMIT")
+    else:
+        assert tsqp.STATUS[res.status] == "SQP_CONVERGED"
+    if kind == "bounded":
+        lo = np.frombuffer(spec.var_lower, dtype=np.float64)[:7]
+        up = np.frombuffer(spec.var_upper, dtype=np.float64)[:7]
+        assert np.all(x >= lo - 1e-6) and np.all(x <= up + 1e-6)
+
+
+def _expect_error(spec, text):
+    with pytest.raises(Exception) as e:
+        tsqp.solve(spec)
+    assert text in str(e.value)
+
+
+def test_product_argument_checks():
+    D = 7
+    # the reference's constructor errors, raised before any QP is built
+    s = tsqp.make_spec(np.zeros((3, D)), [dict(kind=tsqp.JOINT_ACC, penalty=tsqp.SQUARED, first=0, last=2,
+                                                lower=[0.0] * D)])
+    _expect_error(s, "JointAccelConstraint requires a minimum of four position variables!")
+    s = tsqp.make_spec(np.zeros((5, D)), [dict(kind=tsqp.JOINT_JERK, penalty=tsqp.SQUARED, first=0, last=4,
+                                                lower=[0.0] * D)])
+    _expect_error(s, "JointJerkConstraint requires a minimum of six position variables!")
+    s = tsqp.make_spec(np.zeros((3, D)), [dict(kind=tsqp.JOINT_VEL, penalty=tsqp.SQUARED, first=0, last=2,
+                                                coeffs=[-1.0], lower=[0.0] * D)])
+    _expect_error(s, "coeff must be greater than zero.")
+    # penalty kinds check the bound types (trajopt_qp_problem.cpp:417-474)
+    s = tsqp.make_spec(np.zeros((2, D)), [dict(kind=tsqp.JOINT_POS, penalty=tsqp.SQUARED, first=0,
+                                                lower=[0.0] * D, upper=[1.0] * D)])
+    _expect_error(s, "squared cost must have equality bounds!")
+    s = tsqp.make_spec(np.zeros((2, D)), [dict(kind=tsqp.JOINT_POS, penalty=tsqp.HINGE, first=0,
+                                                lower=[0.0] * D, upper=[0.0] * D)])
+    _expect_error(s, "hinge cost must have inequality bounds!")
+    s = tsqp.make_spec(np.zeros((2, D)), [dict(kind=tsqp.JOINT_POS, first=3, lower=[0.0] * D)])
+    _expect_error(s, "term nodes out of range")

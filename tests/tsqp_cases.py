@@ -1,0 +1,92 @@
+"""Problems of the trajopt_sqp front end (tsqp_spec): the reference's joint
+optimisation units (trajopt_optimizers/trajopt_sqp/test/joint_{position,velocity,
+acceleration,jerk}_optimization_unit.cpp, with their EXPECT_NEAR values) and
+seeded trajectory problems that exercise every penalty kind, variable bounds,
+the merit-coefficient loop and many in-place QP updates."""
+import numpy as np
+
+from trajopt_amd import tsqp
+
+D = 7
+REF_OSQP = dict(adaptive_rho=0)  # the units' setAdaptiveRho(false)
+
+
+def pos(node, target, coeff=5.0, upper=None):
+    lo = list(np.broadcast_to(target, D).astype(float))
+    up = lo if upper is None else list(np.broadcast_to(upper, D).astype(float))
+    return dict(kind=tsqp.JOINT_POS, penalty=tsqp.CONSTRAINT, first=node, coeffs=[coeff] * D, lower=lo, upper=up)
+
+
+def reference_units():
+    """name -> (spec, expected [(slice of x, value, tol)])"""
+    out = {}
+    # joint_position_optimization_unit.cpp:54-101
+    s = tsqp.make_spec(np.zeros((2, D)), [pos(0, 0.0, 1.0), pos(1, 1.0, 1.0)], osqp=REF_OSQP)
+    out["joint_position"] = (s, [(slice(0, 7), 0.0, 1e-5), (slice(7, 14), 1.0, 1e-5)])
+    # joint_velocity_optimization_unit.cpp:60-126
+    init = np.vstack([np.zeros(D), np.full(D, 10.0), np.full(D, 10.0)])
+    s = tsqp.make_spec(init, [pos(0, 0.0), pos(2, 10.0),
+                              dict(kind=tsqp.JOINT_VEL, penalty=tsqp.SQUARED, first=0, last=2, coeffs=[1.0],
+                                   lower=[0.0] * D)], osqp=REF_OSQP)
+    out["joint_velocity"] = (s, [(slice(0, 7), 0.0, 1e-3), (slice(7, 14), 5.0, 1e-1), (slice(14, 21), 10.0, 1e-3)])
+    # joint_acceleration_optimization_unit.cpp:60-128
+    init = np.vstack([np.zeros(D)] + [np.full(D, 10.0)] * 3)
+    s = tsqp.make_spec(init, [pos(0, 0.0), pos(3, 10.0),
+                              dict(kind=tsqp.JOINT_ACC, penalty=tsqp.SQUARED, first=0, last=3, coeffs=[1.0],
+                                   lower=[0.0] * D)], osqp=REF_OSQP)
+    out["joint_acceleration"] = (s, [(slice(0, 7), 0.0, 1e-5), (slice(7, 14), 3.333, 1e-1),
+                                     (slice(14, 21), 6.666, 1e-1), (slice(21, 28), 10.0, 1e-5)])
+    # joint_jerk_optimization_unit.cpp:60-135
+    init = np.vstack([np.zeros(D)] + [np.full(D, (i / 5.0) * (10 + 0.01)) for i in range(1, 5)] +
+                     [np.full(D, 10.0)])
+    s = tsqp.make_spec(init, [pos(0, 0.0), pos(5, 10.0),
+                              dict(kind=tsqp.JOINT_JERK, penalty=tsqp.SQUARED, first=0, last=5, coeffs=[1.0],
+                                   lower=[0.0] * D)], osqp=REF_OSQP)
+    out["joint_jerk"] = (s, [(slice(0, 7), 0.0, 1e-5), (slice(7, 14), 2.0, 1e-1), (slice(14, 21), 4.0, 1e-1),
+                             (slice(21, 28), 6.0, 1e-1), (slice(28, 35), 8.0, 1e-1), (slice(35, 42), 10.0, 1e-5)])
+    return out
+
+
+def synthetic(kind, seed, n=20):
+    """Seeded trajectory problems (splitmix-free numpy Generator, seed = 20261015 + seed)."""
+    rng = np.random.default_rng(20261015 + seed)
+    q0 = rng.uniform(-1.0, 1.0, D)
+    q1 = q0 + rng.uniform(-1.5, 1.5, D)
+    init = np.linspace(q0, q1, n) + rng.normal(0.0, 0.05, (n, D))
+    init[0], init[-1] = q0, q1
+    mid = n // 2
+    span = dict(first=0, last=n - 1)
+    if kind == "smooth":
+        # start / goal constraints, squared velocity and acceleration costs, a hinge
+        # cost keeping the middle node inside a box
+        lo = init[mid] - 0.05
+        terms = [pos(0, q0), pos(n - 1, q1),
+                 dict(kind=tsqp.JOINT_VEL, penalty=tsqp.SQUARED, coeffs=[1.0], lower=[0.0] * D, **span),
+                 dict(kind=tsqp.JOINT_ACC, penalty=tsqp.SQUARED, coeffs=[0.5], lower=[0.0] * D, **span),
+                 dict(kind=tsqp.JOINT_POS, penalty=tsqp.HINGE, first=mid, coeffs=[10.0] * D, lower=list(lo),
+                      upper=list(lo + 0.1))]
+        return tsqp.make_spec(init, terms)
+    if kind == "absolute":
+        # absolute velocity cost (slack pairs), jerk squared cost, start / goal
+        terms = [pos(0, q0), pos(n - 1, q1),
+                 dict(kind=tsqp.JOINT_VEL, penalty=tsqp.ABSOLUTE, coeffs=[2.0], lower=[0.0] * D, **span),
+                 dict(kind=tsqp.JOINT_JERK, penalty=tsqp.SQUARED, coeffs=[0.1], lower=[0.0] * D, **span)]
+        return tsqp.make_spec(init, terms)
+    if kind == "bounded":
+        # variable bounds that bind, a velocity target, an interior position constraint
+        vl, vu = np.minimum(q0, q1) - 0.1, np.maximum(q0, q1) + 0.1
+        terms = [pos(0, q0), pos(n - 1, q1), pos(mid, 0.5 * (q0 + q1) + 0.05),
+                 dict(kind=tsqp.JOINT_VEL, penalty=tsqp.SQUARED, coeffs=list(rng.uniform(0.5, 2.0, D)),
+                      lower=list(rng.uniform(-0.05, 0.05, D)), **span)]
+        return tsqp.make_spec(init, terms, var_lower=vl, var_upper=vu)
+    if kind == "penalty":
+        # a zero-velocity equality constraint that conflicts with the goal: the
+        # merit coefficients grow until the penalty-iteration limit
+        terms = [pos(0, q0), pos(n - 1, q1),
+                 dict(kind=tsqp.JOINT_VEL, penalty=tsqp.CONSTRAINT, coeffs=[1.0], lower=[0.0] * D, **span),
+                 dict(kind=tsqp.JOINT_ACC, penalty=tsqp.SQUARED, coeffs=[1.0], lower=[0.0] * D, **span)]
+        return tsqp.make_spec(init, terms)
+    raise ValueError(kind)
+
+
+SYNTHETIC = [(k, s) for k in ("smooth", "absolute", "bounded", "penalty") for s in range(4)]

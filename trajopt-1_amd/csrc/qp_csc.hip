@@ -62,7 +62,29 @@ enum Arr : int
 {
   W_PX, W_AX, W_Q, W_L, W_U, W_D, W_DI, W_E, W_EI, W_TD, W_TE, W_RHO, W_RHOI, W_CT,
   W_X, W_XP, W_Z, W_ZP, W_Y, W_DX, W_DY, W_XT, W_AXV, W_PXV, W_ATY, W_RP, W_RD, W_T1, W_T2,
-  W_PXS, W_PZS, W_PYS, W_RHS, W_RES, W_FLG, W_RMAP, W_K, W_KT, W_COUNT
+  W_PXS, W_PZS, W_PYS, W_RHS, W_RES, W_FLG, W_RMAP, W_K, W_KT, W_SC, W_COUNT
+};
+// W_SC: the scalars a resident workspace keeps between launches (thip_qp_setup ...
+// thip_qp_solve_resident): cost scaling c and 1/c, the current rho, setup ok, and
+// whether the ADMM KKT factor in W_K must be rebuilt (polish factors its reduced
+// KKT in the same storage; OSQP keeps a separate polish factor)
+enum : int
+{
+  SC_C = 0,
+  SC_CINV,
+  SC_RHO,
+  SC_OK,
+  SC_KKT_DIRTY,
+  SC_COUNT
+};
+// resident-workspace operations (qp_resident_kernel), OSQP 1.0 API calls
+enum : int
+{
+  OP_SETUP = 0,    // osqp_setup
+  OP_UPDATE_VEC,   // osqp_update_data_vec
+  OP_UPDATE_MAT,   // osqp_update_data_mat
+  OP_WARM_START,   // osqp_warm_start
+  OP_SOLVE,        // osqp_solve
 };
 
 struct QpPattern
@@ -758,84 +780,18 @@ __device__ void polish(Qp& q)
   __syncthreads();
 }
 
-__global__ __launch_bounds__(kQB) void qp_csc_kernel(QpArgs args)
+// osqp_solve from the current iterates (X, Z, Y in the scaled space): ADMM
+// with termination / infeasibility checks and adaptive rho, polish, then the
+// unscaled solution and info of problem b.  Shared by the one-shot kernel and
+// the resident workspace.
+__device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
 {
-  extern __shared__ double lv[];
-  __shared__ Sh sh;
-  const int b = blockIdx.x;
-  if (b >= args.batch)
-    return;
-  const QpPattern& P = args.pat;
-  const int n = P.n, m = P.m;
-  Qp q{ P, args.s, args.ws + (long long)b * P.stride, sh, lv, n, m };
-  // data (scaled in place)
-  {
-    double *PX = q.a(W_PX), *AX = q.a(W_AX), *Q = q.a(W_Q), *L = q.a(W_L), *U = q.a(W_U);
-    QFOR(e, P.nnz_p) PX[e] = args.Pv[(long long)b * P.nnz_p + e];
-    QFOR(e, P.nnz_a) AX[e] = args.Av[(long long)b * P.nnz_a + e];
-    QFOR(j, n) Q[j] = args.qv[(long long)b * n + j];
-    QFOR(r, m)
-    {
-      L[r] = args.lv[(long long)b * m + r];
-      U[r] = args.uv[(long long)b * m + r];
-    }
-  }
-  if (threadIdx.x == 0)
-  {
-    sh.c = sh.cinv = 1.0;
-    sh.rho = args.rho_ws ? args.rho_ws[b] : args.s.rho;
-    sh.rho = fmin(fmax(sh.rho, kRhoMin), kRhoMax);
-    sh.status = UNSOLVED;
-    sh.polish = 0;
-    sh.iter = 0;
-    sh.prim_res = sh.dual_res = 0;
-  }
-  __syncthreads();
-  if (args.s.scaling > 0)
-    scale_data(q);
-  else
-  {
-    QFOR(j, n) q.a(W_D)[j] = q.a(W_DI)[j] = 1.0;
-    QFOR(r, m) q.a(W_E)[r] = q.a(W_EI)[r] = 1.0;
-    __syncthreads();
-  }
-  set_rho_vec(q);
-  build_kkt(q);
-  ldl_factor(q, q.a(W_K), q.a(W_KT), n + m);
-  thip_qp_info* info = args.info + b;
-  if (q.sh.fail || q.sh.npos < n)
-  {
-    // osqp_setup fails: OSQP_LINSYS_SOLVER_INIT_ERROR / OSQP_NONCVX_ERROR
-    if (threadIdx.x == 0)
-    {
-      info->status = -1;
-      info->setup_error = q.sh.fail ? 4 : 5;
-      info->polish_status = 0;
-      info->iter = 0;
-      info->rho = sh.rho;
-      info->prim_res = info->dual_res = 0;
-    }
-    return;
-  }
+  Sh& sh = q.sh;
+  double* lv = q.lv;
+  const int n = q.n, m = q.m;
   double *X = q.a(W_X), *XP = q.a(W_XP), *Z = q.a(W_Z), *ZP = q.a(W_ZP), *Y = q.a(W_Y), *DX = q.a(W_DX),
          *DY = q.a(W_DY), *XT = q.a(W_XT), *Q = q.a(W_Q), *L = q.a(W_L), *U = q.a(W_U), *RHO = q.a(W_RHO),
          *RHOI = q.a(W_RHOI);
-  // warm start (osqp_warm_start: x / D, y / E * c, z = A x) or cold start
-  if (args.x_ws && args.y_ws)
-  {
-    const double *DI = q.a(W_DI), *EI = q.a(W_EI);
-    const bool sc = args.s.scaling > 0;
-    QFOR(j, n) X[j] = sc ? args.x_ws[(long long)b * n + j] * DI[j] : args.x_ws[(long long)b * n + j];
-    QFOR(r, m) Y[r] = sc ? (args.y_ws[(long long)b * m + r] * EI[r]) * sh.c : args.y_ws[(long long)b * m + r];
-    __syncthreads();
-    a_mul(q, X, Z);
-  }
-  else
-  {
-    QFOR(j, n) X[j] = 0.0;
-    QFOR(r, m) Z[r] = Y[r] = 0.0;
-  }
-  __syncthreads();
   int interval = args.s.adaptive_rho_interval;
   if (args.s.adaptive_rho == 1 && interval == 0)
     interval = args.s.check_termination ? 4 * args.s.check_termination : 100;
@@ -948,6 +904,342 @@ __global__ __launch_bounds__(kQB) void qp_csc_kernel(QpArgs args)
     info->dual_res = sh.dual_res;
   }
 }
+
+__global__ __launch_bounds__(kQB) void qp_csc_kernel(QpArgs args)
+{
+  extern __shared__ double lv[];
+  __shared__ Sh sh;
+  const int b = blockIdx.x;
+  if (b >= args.batch)
+    return;
+  const QpPattern& P = args.pat;
+  const int n = P.n, m = P.m;
+  Qp q{ P, args.s, args.ws + (long long)b * P.stride, sh, lv, n, m };
+  // data (scaled in place)
+  {
+    double *PX = q.a(W_PX), *AX = q.a(W_AX), *Q = q.a(W_Q), *L = q.a(W_L), *U = q.a(W_U);
+    QFOR(e, P.nnz_p) PX[e] = args.Pv[(long long)b * P.nnz_p + e];
+    QFOR(e, P.nnz_a) AX[e] = args.Av[(long long)b * P.nnz_a + e];
+    QFOR(j, n) Q[j] = args.qv[(long long)b * n + j];
+    QFOR(r, m)
+    {
+      L[r] = args.lv[(long long)b * m + r];
+      U[r] = args.uv[(long long)b * m + r];
+    }
+  }
+  if (threadIdx.x == 0)
+  {
+    sh.c = sh.cinv = 1.0;
+    sh.rho = args.rho_ws ? args.rho_ws[b] : args.s.rho;
+    sh.rho = fmin(fmax(sh.rho, kRhoMin), kRhoMax);
+    sh.status = UNSOLVED;
+    sh.polish = 0;
+    sh.iter = 0;
+    sh.prim_res = sh.dual_res = 0;
+  }
+  __syncthreads();
+  if (args.s.scaling > 0)
+    scale_data(q);
+  else
+  {
+    QFOR(j, n) q.a(W_D)[j] = q.a(W_DI)[j] = 1.0;
+    QFOR(r, m) q.a(W_E)[r] = q.a(W_EI)[r] = 1.0;
+    __syncthreads();
+  }
+  set_rho_vec(q);
+  build_kkt(q);
+  ldl_factor(q, q.a(W_K), q.a(W_KT), n + m);
+  thip_qp_info* info = args.info + b;
+  if (q.sh.fail || q.sh.npos < n)
+  {
+    // osqp_setup fails: OSQP_LINSYS_SOLVER_INIT_ERROR / OSQP_NONCVX_ERROR
+    if (threadIdx.x == 0)
+    {
+      info->status = -1;
+      info->setup_error = q.sh.fail ? 4 : 5;
+      info->polish_status = 0;
+      info->iter = 0;
+      info->rho = sh.rho;
+      info->prim_res = info->dual_res = 0;
+    }
+    return;
+  }
+  // warm start (osqp_warm_start: x / D, y / E * c, z = A x) or cold start
+  double *X = q.a(W_X), *Z = q.a(W_Z), *Y = q.a(W_Y);
+  if (args.x_ws && args.y_ws)
+  {
+    const double *DI = q.a(W_DI), *EI = q.a(W_EI);
+    const bool sc = args.s.scaling > 0;
+    QFOR(j, n) X[j] = sc ? args.x_ws[(long long)b * n + j] * DI[j] : args.x_ws[(long long)b * n + j];
+    QFOR(r, m) Y[r] = sc ? (args.y_ws[(long long)b * m + r] * EI[r]) * sh.c : args.y_ws[(long long)b * m + r];
+    __syncthreads();
+    a_mul(q, X, Z);
+  }
+  else
+  {
+    QFOR(j, n) X[j] = 0.0;
+    QFOR(r, m) Z[r] = Y[r] = 0.0;
+  }
+  __syncthreads();
+  admm_solve(q, args, b, info);
+}
+
+// ---------------------------------------------------------------------------
+// Resident workspace (update in place): the OSQP 1.0 solver object kept on the
+// device between calls, as OsqpEigen::Solver keeps it for trajopt_sqp's
+// OSQPEigenSolver (trajopt_optimizers/trajopt_sqp/src/osqp_eigen_solver.cpp:
+// 73-320, trust_region_sqp_solver.cpp:202-260).  One launch per API call:
+//   OP_SETUP       osqp_setup: data, Ruiz scaling, rho vector, KKT factor, x = z = y = 0
+//   OP_UPDATE_VEC  osqp_update_data_vec: q <- c (D q_new); l, u <- E l_new, E u_new, then
+//                  the constraint types (rho vector) and a refactorisation only when a
+//                  type changed (update_rho_vec)
+//   OP_UPDATE_MAT  osqp_update_data_mat: unscale_data, new P / A values (same pattern),
+//                  scale_data (q, l, u ride along through unscale and rescale), refactor
+//   OP_WARM_START  osqp_warm_start: x / D, z = A x, c y / E
+//   OP_SOLVE       osqp_solve: from the kept iterates (warm_starting) or from zero
+// The scaled data, scaling, rho vector, iterates and factor stay in the QP's
+// HBM workspace; c, 1/c and rho in W_SC.  Only the changed vectors cross the bus.
+__device__ void resident_refactor(Qp& q)
+{
+  build_kkt(q);
+  ldl_factor(q, q.a(W_K), q.a(W_KT), q.n + q.m);
+}
+
+// OSQP unscale_data: P <- cinv Dinv P Dinv, q <- Dinv (cinv q), A <- Einv A Dinv, l, u <- Einv l, Einv u
+__device__ void unscale_data(Qp& q)
+{
+  const int n = q.n, m = q.m;
+  double *PX = q.a(W_PX), *AX = q.a(W_AX), *Q = q.a(W_Q), *L = q.a(W_L), *U = q.a(W_U);
+  const double *DI = q.a(W_DI), *EI = q.a(W_EI);
+  const double cinv = q.sh.cinv;
+  QFOR(j, n)
+  for (int e = q.p.Pp[j]; e < q.p.Pp[j + 1]; ++e)
+    PX[e] = ((PX[e] * cinv) * DI[q.p.Pi[e]]) * DI[j];
+  QFOR(j, n) Q[j] = (Q[j] * cinv) * DI[j];
+  QFOR(j, n)
+  for (int e = q.p.Ap[j]; e < q.p.Ap[j + 1]; ++e)
+    AX[e] = (AX[e] * EI[q.p.Ai[e]]) * DI[j];
+  QFOR(r, m)
+  {
+    L[r] = L[r] * EI[r];
+    U[r] = U[r] * EI[r];
+  }
+  __syncthreads();
+}
+
+__device__ void set_unit_scaling(Qp& q)
+{
+  QFOR(j, q.n) q.a(W_D)[j] = q.a(W_DI)[j] = 1.0;
+  QFOR(r, q.m) q.a(W_E)[r] = q.a(W_EI)[r] = 1.0;
+  if (threadIdx.x == 0)
+    q.sh.c = q.sh.cinv = 1.0;
+  __syncthreads();
+}
+
+__device__ void report_setup_error(Qp& q, thip_qp_info* info, int code)
+{
+  if (threadIdx.x == 0)
+  {
+    info->status = -1;
+    info->setup_error = code;
+    info->polish_status = 0;
+    info->iter = 0;
+    info->rho = q.sh.rho;
+    info->prim_res = info->dual_res = 0;
+  }
+}
+
+__global__ __launch_bounds__(kQB) void qp_resident_kernel(QpArgs args, int op)
+{
+  extern __shared__ double lv[];
+  __shared__ Sh sh;
+  const int b = blockIdx.x;
+  if (b >= args.batch)
+    return;
+  const QpPattern& P = args.pat;
+  const int n = P.n, m = P.m;
+  Qp q{ P, args.s, args.ws + (long long)b * P.stride, sh, lv, n, m };
+  double* SC = q.a(W_SC);
+  thip_qp_info* info = args.info + b;
+  const bool sc = args.s.scaling > 0;
+  if (threadIdx.x == 0)
+  {
+    sh.c = (op == OP_SETUP) ? 1.0 : SC[SC_C];
+    sh.cinv = (op == OP_SETUP) ? 1.0 : SC[SC_CINV];
+    sh.rho = (op == OP_SETUP) ? fmin(fmax(args.s.rho, kRhoMin), kRhoMax) : SC[SC_RHO];
+    sh.status = UNSOLVED;
+    sh.polish = 0;
+    sh.iter = 0;
+    sh.prim_res = sh.dual_res = 0;
+    sh.fail = 0;
+    sh.npos = n;
+  }
+  __syncthreads();
+  double *PX = q.a(W_PX), *AX = q.a(W_AX), *Q = q.a(W_Q), *L = q.a(W_L), *U = q.a(W_U);
+  double *X = q.a(W_X), *Z = q.a(W_Z), *Y = q.a(W_Y);
+  const double *D = q.a(W_D), *E = q.a(W_E);
+  bool ok = true;
+  int err = 0;
+  if (op == OP_SETUP)
+  {
+    QFOR(e, P.nnz_p) PX[e] = args.Pv[(long long)b * P.nnz_p + e];
+    QFOR(e, P.nnz_a) AX[e] = args.Av[(long long)b * P.nnz_a + e];
+    QFOR(j, n) Q[j] = args.qv[(long long)b * n + j];
+    QFOR(r, m)
+    {
+      L[r] = args.lv[(long long)b * m + r];
+      U[r] = args.uv[(long long)b * m + r];
+    }
+    __syncthreads();
+    if (sc)
+      scale_data(q);
+    else
+      set_unit_scaling(q);
+    set_rho_vec(q);
+    resident_refactor(q);
+    ok = !sh.fail && sh.npos >= n;
+    err = sh.fail ? 4 : 5;
+    QFOR(j, n) X[j] = 0.0;
+    QFOR(r, m) Z[r] = Y[r] = 0.0;
+    if (threadIdx.x == 0)
+    {
+      SC[SC_OK] = ok ? 1.0 : 0.0;
+      SC[SC_KKT_DIRTY] = 0.0;
+    }
+  }
+  else if (op == OP_UPDATE_VEC)
+  {
+    if (args.qv)
+      QFOR(j, n) Q[j] = sc ? (D[j] * args.qv[(long long)b * n + j]) * sh.c : args.qv[(long long)b * n + j];
+    if (args.lv)
+    {
+      QFOR(r, m)
+      {
+        L[r] = sc ? E[r] * args.lv[(long long)b * m + r] : args.lv[(long long)b * m + r];
+        U[r] = sc ? E[r] * args.uv[(long long)b * m + r] : args.uv[(long long)b * m + r];
+      }
+      __syncthreads();
+      // update_rho_vec: rows whose constraint type changed get their rho; a
+      // refactorisation only if one did
+      double *RHO = q.a(W_RHO), *RHOI = q.a(W_RHOI), *CT = q.a(W_CT);
+      double changed = 0;
+      QFOR(r, m)
+      {
+        double ct, rv;
+        if (L[r] < -kInf * kMinScaling && U[r] > kInf * kMinScaling)
+        {
+          ct = -1;
+          rv = kRhoMin;
+        }
+        else if (U[r] - L[r] < kRhoTol)
+        {
+          ct = 1;
+          rv = kRhoEq * sh.rho;
+        }
+        else
+        {
+          ct = 0;
+          rv = sh.rho;
+        }
+        if (CT[r] != ct)
+        {
+          CT[r] = ct;
+          RHO[r] = rv;
+          RHOI[r] = 1.0 / rv;
+          changed = 1;
+        }
+      }
+      if (bmax(sh, changed) != 0.0)
+      {
+        resident_refactor(q);
+        ok = !sh.fail && sh.npos >= n;
+        err = sh.fail ? 4 : 5;
+        if (threadIdx.x == 0)
+          SC[SC_KKT_DIRTY] = 0.0;
+      }
+    }
+  }
+  else if (op == OP_UPDATE_MAT)
+  {
+    if (sc)
+      unscale_data(q);
+    if (args.Pv)
+      QFOR(e, P.nnz_p) PX[e] = args.Pv[(long long)b * P.nnz_p + e];
+    if (args.Av)
+      QFOR(e, P.nnz_a) AX[e] = args.Av[(long long)b * P.nnz_a + e];
+    __syncthreads();
+    if (sc)
+      scale_data(q);
+    resident_refactor(q);
+    ok = !sh.fail && sh.npos >= n;
+    err = sh.fail ? 4 : 5;
+    if (threadIdx.x == 0)
+      SC[SC_KKT_DIRTY] = 0.0;
+  }
+  else if (op == OP_WARM_START)
+  {
+    const double *DI = q.a(W_DI), *EI = q.a(W_EI);
+    if (args.x_ws)
+    {
+      QFOR(j, n) X[j] = sc ? args.x_ws[(long long)b * n + j] * DI[j] : args.x_ws[(long long)b * n + j];
+      __syncthreads();
+      a_mul(q, X, Z);
+    }
+    if (args.y_ws)
+      QFOR(r, m) Y[r] = sc ? (args.y_ws[(long long)b * m + r] * EI[r]) * sh.c : args.y_ws[(long long)b * m + r];
+  }
+  else  // OP_SOLVE
+  {
+    if (SC[SC_OK] == 0.0)
+    {
+      report_setup_error(q, info, 4);
+      return;
+    }
+    if (SC[SC_KKT_DIRTY] != 0.0)
+    {
+      resident_refactor(q);  // the same factor OSQP kept
+      if (threadIdx.x == 0)
+        SC[SC_KKT_DIRTY] = 0.0;
+    }
+    if (!args.s.warm_starting)
+    {
+      QFOR(j, n) X[j] = 0.0;
+      QFOR(r, m) Z[r] = Y[r] = 0.0;
+    }
+    __syncthreads();
+    admm_solve(q, args, b, info);
+    if (threadIdx.x == 0)
+    {
+      if (sh.polish != 0)
+        SC[SC_KKT_DIRTY] = 1.0;  // polish factored its reduced KKT over W_K
+      SC[SC_RHO] = sh.rho;
+    }
+    return;
+  }
+  __syncthreads();
+  if (!ok)
+  {
+    report_setup_error(q, info, err);
+    if (threadIdx.x == 0)
+      SC[SC_OK] = 0.0;
+  }
+  else if (threadIdx.x == 0)
+  {
+    info->status = 0;
+    info->setup_error = 0;
+    info->polish_status = 0;
+    info->iter = 0;
+    info->rho = sh.rho;
+    info->prim_res = info->dual_res = 0;
+  }
+  if (threadIdx.x == 0)
+  {
+    SC[SC_C] = sh.c;
+    SC[SC_CINV] = sh.cinv;
+    SC[SC_RHO] = sh.rho;
+  }
+}
+
 }  // namespace thip_qp_dev
 
 using namespace thip_qp_dev;
@@ -963,6 +1255,9 @@ struct thip_qp
   long long in_doubles = 0;
   size_t lds = 0;
   std::string err;
+  // resident workspace (thip_qp_setup ...): the settings of its setup
+  thip_osqp_settings rs{};
+  bool resident = false;
 };
 
 static std::string g_qp_create_err;
@@ -1070,6 +1365,7 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
   sizes[W_PZS] = sizes[W_PYS] = sizes[W_FLG] = sizes[W_RMAP] = mm;
   sizes[W_XT] = sizes[W_RHS] = sizes[W_RES] = N;
   sizes[W_K] = sizes[W_KT] = N * N;
+  sizes[W_SC] = SC_COUNT;
   long long off = 0;
   for (int k = 0; k < W_COUNT; ++k)
   {
@@ -1165,6 +1461,7 @@ int thip_qp_solve(thip_qp* q, const double* P_values, const double* qvec, const 
     q->err = std::string("hipMemcpy: ") + hipGetErrorString(e);
     return THIP_E_HIP;
   }
+  q->resident = false;  // the one-shot solve reuses the workspace
   QpArgs a{};
   a.pat = q->pat;
   a.s = *settings;
@@ -1205,6 +1502,213 @@ int thip_qp_solve(thip_qp* q, const double* P_values, const double* qvec, const 
     }
   }
   return THIP_OK;
+}
+
+// ---- resident workspace (update in place) --------------------------------
+static bool qp_settings_ok(thip_qp* q, const thip_osqp_settings* settings)
+{
+  if (settings->max_iter < 1 || settings->check_termination < 0 || settings->scaling < 0 ||
+      !(settings->alpha > 0 && settings->alpha < 2) || !(settings->sigma > 0) || !(settings->rho > 0) ||
+      !(settings->delta > 0))
+  {
+    q->err = "bad OSQP settings";
+    return false;
+  }
+  return true;
+}
+
+// one resident operation over the batch: inputs (any may be null) to the
+// device, the launch, outputs back
+static int qp_resident(thip_qp* q, int op, const double* P_values, const double* qvec, const double* A_values,
+                       const double* l, const double* u, const double* x_in, const double* y_in, double* x,
+                       double* y, thip_qp_info* info)
+{
+  const int n = q->n, m = q->m, B = q->batch;
+  hipError_t e;
+  if ((e = hipSetDevice(q->device)) != hipSuccess)
+  {
+    q->err = std::string("hipSetDevice: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  const size_t np = static_cast<size_t>(q->nnz_p) * B, na = static_cast<size_t>(q->nnz_a) * B;
+  const size_t nn = static_cast<size_t>(n) * B, mm = static_cast<size_t>(m) * B;
+  double* d = q->d_in;
+  double *dP = d, *dA = dP + np, *dq = dA + na, *dl = dq + nn, *du = dl + mm, *dxw = du + mm, *dyw = dxw + nn;
+  auto h2d = [&](double* dst, const double* src, size_t cnt) {
+    if (src && cnt && (e = hipMemcpy(dst, src, cnt * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+      return false;
+    return true;
+  };
+  if (!h2d(dP, P_values, np) || !h2d(dA, A_values, na) || !h2d(dq, qvec, nn) || !h2d(dl, l, mm) || !h2d(du, u, mm) ||
+      !h2d(dxw, x_in, nn) || !h2d(dyw, y_in, mm))
+  {
+    q->err = std::string("hipMemcpy: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  QpArgs a{};
+  a.pat = q->pat;
+  a.s = q->rs;
+  a.Pv = P_values ? dP : nullptr;
+  a.Av = A_values ? dA : nullptr;
+  a.qv = qvec ? dq : nullptr;
+  a.lv = l ? dl : nullptr;
+  a.uv = u ? du : nullptr;
+  a.x_ws = x_in ? dxw : nullptr;
+  a.y_ws = y_in ? dyw : nullptr;
+  a.rho_ws = nullptr;
+  a.x_out = q->d_out;
+  a.y_out = q->d_out + nn;
+  a.info = q->d_info;
+  a.ws = q->d_ws;
+  a.batch = B;
+  hipLaunchKernelGGL(qp_resident_kernel, dim3(B), dim3(kQB), q->lds, nullptr, a, op);
+  if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess)
+  {
+    q->err = std::string("qp_resident_kernel: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  if (op == OP_SOLVE && ((x && (e = hipMemcpy(x, q->d_out, nn * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess) ||
+                         (y && m && (e = hipMemcpy(y, q->d_out + nn, mm * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess)))
+  {
+    q->err = std::string("hipMemcpy: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  if (info && (op != OP_WARM_START) &&
+      (e = hipMemcpy(info, q->d_info, sizeof(thip_qp_info) * B, hipMemcpyDeviceToHost)) != hipSuccess)
+  {
+    q->err = std::string("hipMemcpy: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  return THIP_OK;
+}
+
+// osqp_setup's / osqp_update_data_vec's validate: l <= u for every row of every QP
+static bool bounds_ok(const thip_qp* q, const double* l, const double* u)
+{
+  const long long mm = static_cast<long long>(q->m) * q->batch;
+  for (long long r = 0; r < mm; ++r)
+    if (!(l[r] <= u[r]))
+      return false;
+  return true;
+}
+
+static void fail_info(thip_qp* q, thip_qp_info* info, int code)
+{
+  for (int b = 0; b < q->batch; ++b)
+  {
+    info[b] = thip_qp_info{};
+    info[b].status = -1;
+    info[b].setup_error = code;
+  }
+}
+
+int thip_qp_setup(thip_qp* q, const double* P_values, const double* qvec, const double* A_values, const double* l,
+                  const double* u, const thip_osqp_settings* settings, thip_qp_info* info)
+{
+  if (!q)
+    return THIP_E_INVALID;
+  if ((!P_values && q->nnz_p) || !qvec || (!A_values && q->nnz_a) || (q->m && (!l || !u)) || !settings || !info)
+  {
+    q->err = "thip_qp_setup: null argument";
+    return THIP_E_INVALID;
+  }
+  if (!qp_settings_ok(q, settings))
+  {
+    q->err = "thip_qp_setup: " + q->err;
+    return THIP_E_INVALID;
+  }
+  q->rs = *settings;
+  q->resident = true;
+  if (q->m && !bounds_ok(q, l, u))
+  {
+    // OSQP_DATA_VALIDATION_ERROR: no workspace
+    q->resident = false;
+    fail_info(q, info, 1);
+    return THIP_OK;
+  }
+  const int rc = qp_resident(q, OP_SETUP, P_values, qvec, A_values, l, u, nullptr, nullptr, nullptr, nullptr, info);
+  if (rc == THIP_OK)
+    for (int b = 0; b < q->batch; ++b)
+      if (info[b].status == -1)
+        q->resident = false;
+  return rc;
+}
+
+int thip_qp_update_vec(thip_qp* q, const double* qvec, const double* l, const double* u, thip_qp_info* info)
+{
+  if (!q)
+    return THIP_E_INVALID;
+  if (!q->resident)
+  {
+    q->err = "thip_qp_update_vec: no resident workspace (thip_qp_setup first)";
+    return THIP_E_STATE;
+  }
+  if (!info || (!l) != (!u))
+  {
+    q->err = "thip_qp_update_vec: l and u go together; info is required";
+    return THIP_E_INVALID;
+  }
+  if (l && q->m && !bounds_ok(q, l, u))
+  {
+    fail_info(q, info, 1);  // rejected, the workspace keeps its data
+    return THIP_OK;
+  }
+  return qp_resident(q, OP_UPDATE_VEC, nullptr, qvec, nullptr, q->m ? l : nullptr, q->m ? u : nullptr, nullptr,
+                     nullptr, nullptr, nullptr, info);
+}
+
+int thip_qp_update_mat(thip_qp* q, const double* P_values, const double* A_values, thip_qp_info* info)
+{
+  if (!q)
+    return THIP_E_INVALID;
+  if (!q->resident)
+  {
+    q->err = "thip_qp_update_mat: no resident workspace (thip_qp_setup first)";
+    return THIP_E_STATE;
+  }
+  if (!info)
+  {
+    q->err = "thip_qp_update_mat: info is required";
+    return THIP_E_INVALID;
+  }
+  const int rc = qp_resident(q, OP_UPDATE_MAT, q->nnz_p ? P_values : nullptr, nullptr, q->nnz_a ? A_values : nullptr,
+                             nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, info);
+  if (rc == THIP_OK)
+    for (int b = 0; b < q->batch; ++b)
+      if (info[b].status == -1)
+        q->resident = false;
+  return rc;
+}
+
+int thip_qp_warm_start(thip_qp* q, const double* x, const double* y)
+{
+  if (!q)
+    return THIP_E_INVALID;
+  if (!q->resident)
+  {
+    q->err = "thip_qp_warm_start: no resident workspace (thip_qp_setup first)";
+    return THIP_E_STATE;
+  }
+  q->rs.warm_starting = 1;  // osqp_warm_start turns warm starting on
+  return qp_resident(q, OP_WARM_START, nullptr, nullptr, nullptr, nullptr, nullptr, x, q->m ? y : nullptr, nullptr,
+                     nullptr, nullptr);
+}
+
+int thip_qp_solve_resident(thip_qp* q, double* x, double* y, thip_qp_info* info)
+{
+  if (!q)
+    return THIP_E_INVALID;
+  if (!q->resident)
+  {
+    q->err = "thip_qp_solve_resident: no resident workspace (thip_qp_setup first)";
+    return THIP_E_STATE;
+  }
+  if (!x || !info)
+  {
+    q->err = "thip_qp_solve_resident: null argument";
+    return THIP_E_INVALID;
+  }
+  return qp_resident(q, OP_SOLVE, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, x, y, info);
 }
 
 void thip_qp_destroy(thip_qp* q)

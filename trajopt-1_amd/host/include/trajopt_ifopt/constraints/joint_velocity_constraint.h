@@ -1,0 +1,2 @@
+#pragma once
+#include "trajopt_ifopt/constraints/joint_constraints.h"

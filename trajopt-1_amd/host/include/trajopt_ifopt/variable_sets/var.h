@@ -1,0 +1,2 @@
+#pragma once
+#include "trajopt_ifopt/variable_sets/nodes_variables.h"
