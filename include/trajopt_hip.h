@@ -470,11 +470,14 @@ int thip_debug_layout(thip_ctx* ctx, long long* doff, long long* ioff, long long
 /* Diagnostics: force a solve path for every context created after the call
  * (process-wide; 0 restores the automatic choice).  THIP_DEBUG_NO_SEGMENT runs
  * the generic ADMM step instead of the register-resident segment,
- * THIP_DEBUG_FORCE_WIDE the wide-block (D > 8) solve for any D.  Same
+ * THIP_DEBUG_FORCE_WIDE the wide-block (D > 8) solve for any D,
+ * THIP_DEBUG_NO_BRANCH one block solve over all dofs of a tree whose terms
+ * never couple its branches (the dual arm splits into two 7-dof solves).  Same
  * results to the parity bar; for tests and profiling only (the product path
  * never reads the environment). */
 #define THIP_DEBUG_NO_SEGMENT 1
 #define THIP_DEBUG_FORCE_WIDE 2
+#define THIP_DEBUG_NO_BRANCH 4  /* one block solve over all dofs even when the terms split the tree */
 int thip_debug_set_path(int flags);
 int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws);
 

@@ -247,8 +247,9 @@ def test_collision_rows_parity_dual_arm(oracle_mod):
 
 def test_sqp_parity_dual_arm_E(oracle_mod):
     """Config E (BASELINE.json configs[4]): 14-DoF dual arm, 50 waypoints,
-    both tool frames tracked, LVS_CONTINUOUS collision -- the wide-block
-    (D > 8) solve path with the chain matrices in HBM."""
+    both tool frames tracked, LVS_CONTINUOUS collision -- no term touches both
+    arms, so the block solve splits into two 7-dof branches (Layout::nbr), each
+    with its own twisted factorisation on two waves."""
     wl = problems.make_workload("E", 4)
     x, res, _ = solve_gpu(wl)
     assert all(r.flags == 0 for r in res)
@@ -932,6 +933,25 @@ def test_sqp_parity_forced_paths(oracle_mod, cfg, B, path, hip):
     same = sum(int(a.status == b.status and np.abs(xa - xb).max() <= TOL_X)
                for a, b, xa, xb in zip(res, res_seg, x, x_seg))
     assert same >= 0.85 * B, f"{cfg}: {name} path and segment agree on {same} of {B} problems"
+
+
+def test_sqp_parity_dual_arm_E_unsplit(oracle_mod, hip):
+    """Config E through the single 14-dof wide-block solve (THIP_DEBUG_NO_BRANCH:
+    block_chain_wide, twisted_middle_wide, chain matrices in HBM) against the
+    oracle and against the default two-branch solve."""
+    wl = problems.make_workload("E", 8)
+    x_br, res_br, _ = solve_gpu(wl)
+    assert hip.thip_debug_set_path(abi.DEBUG_NO_BRANCH) == 0
+    try:
+        x, res, _ = solve_gpu(wl)
+    finally:
+        hip.thip_debug_set_path(0)
+    xo, ro = oracle_mod.solve(wl, n_threads=16)
+    for xs, rs, name in ((x, res, "E-unsplit"), (x_br, res_br, "E-branches")):
+        assert all(r.flags == 0 for r in rs)
+        check_parity(wl, oracle_mod, xs, rs, label=name, oracle=(xo, ro))
+    same = sum(int(a.status == b.status and np.abs(xa - xb).max() <= TOL_X) for a, b, xa, xb in zip(res, res_br, x, x_br))
+    assert same >= 7, f"unsplit and two-branch solves agree on {same} of 8 problems"
 
 
 def test_zz_pooled_strict_fraction():

@@ -197,7 +197,35 @@ struct Layout
   int seg_slots;
   // middle block of the twisted block factorisation (N / 2)
   int tw_mid;
+  // Branches of the block solve.  A kinematic tree whose terms never touch two
+  // branches (a dual arm: each CartPose term and each collision sphere moves the
+  // dofs of one arm only) has a reduced KKT matrix that is block diagonal over
+  // the branches' dof ranges, so the block-tridiagonal solve splits into nbr
+  // independent chains of sN / nbr blocks of sD = D / nbr dofs: solve block
+  // b * N + t is waypoint t's dofs [b sD, (b + 1) sD) (the dofs of a branch
+  // are contiguous).  Each branch gets its own twisted factorisation (top half
+  // on wave 2b, bottom half on wave 2b + 1).  nbr = 1: sD = D, sN = N.
+  int nbr;
+  int sD;
+  int sN;
 };
+
+// the solve-layout index of column col (t, j): block b * N + t, row j - b sD
+__host__ __device__ __forceinline__ int solve_index(const Layout& L, int col)
+{
+  if (L.nbr == 1)
+    return col;
+  const int t = col / L.D, j = col - t * L.D, b = j / L.sD;
+  return (b * L.N + t) * L.sD + (j - b * L.sD);
+}
+// the column of solve-layout index v
+__host__ __device__ __forceinline__ int solve_column(const Layout& L, int v)
+{
+  if (L.nbr == 1)
+    return v;
+  const int T = v / L.sD, i = v - T * L.sD, b = T / L.N, t = T - b * L.N;
+  return t * L.D + b * L.sD + i;
+}
 
 // shared (batch-wide) tables, device resident
 struct Tables

@@ -1821,14 +1821,17 @@ __device__ __noinline__ void twisted_factor_half(Ctx& c, Solver& sv, const doubl
                                                  double* Sp, double* Lsp, int& bad)
 {
   const Layout& L = c.L;
-  const int D = L.D, N = L.N, DD = D * D, m = L.tw_mid, w = c.wave;
-  const int len = (w == 0) ? m : (N - 1 - m);
+  // the solve layout's blocks (Layout::nbr): wave 2b runs branch b's top half,
+  // wave 2b + 1 its bottom half
+  const int D = L.sD, N = L.N, DD = D * D, m = L.tw_mid, half = c.wave & 1, base = (c.wave >> 1) * N;
+  const int len = (half == 0) ? m : (N - 1 - m);
+  const bool use_cpl = L.hinge || L.nbr > 1;
   lds_f64* S = lds(Sp);
   lds_f64* Ls = lds(Lsp);
   for (int k = 0; k < len; ++k)
   {
-    const int t = (w == 0) ? k : (N - 1 - k);
-    const int cpl = (w == 0) ? t : t - 1;  // PO index of the coupling to the next block
+    const int t = base + ((half == 0) ? k : (N - 1 - k));
+    const int cpl = (half == 0) ? t : t - 1;  // coupling block to the next block of the half
     // the half's first block has no coupling (and Ls holds stale or
     // uninitialised LDS then: never read, not even under a zero mask)
     for (int e = c.lane; e < DD; e += 64)
@@ -1875,7 +1878,7 @@ __device__ __noinline__ void twisted_factor_half(Ctx& c, Solver& sv, const doubl
       sv.M[t * DD + e] = v;
     }
     wave_sync();
-    if (!L.hinge)
+    if (!use_cpl)
       for (int e = c.lane; e < DD; e += 64)
       {
         const int i = e / D, q = e % D;
@@ -1894,7 +1897,7 @@ __device__ __noinline__ void twisted_factor_half(Ctx& c, Solver& sv, const doubl
         for (int j = 0; j < DM; ++j)
         {
           const int jc = min(j, D - 1);
-          a[j] = (w == 0) ? Kc[i * D + jc] : Kc[jc * D + i];
+          a[j] = (half == 0) ? Kc[i * D + jc] : Kc[jc * D + i];
           b[j] = Li[q * D + jc] * ((j <= q) ? 1.0 : 0.0);
         }
         double v = 0;
@@ -1963,10 +1966,14 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
     c.a(A_HRE)[h] = rr * dn / (dn + rr * w * w);
   }
   BSYNC();
-  // diagonal blocks
-  FOR(e, N * D * D)
+  // diagonal blocks, in the solve layout (Layout::nbr): block T = b N + t holds
+  // waypoint t's dofs [b sD, (b + 1) sD); the other branches' entries of the
+  // waypoint block are exact zeros (no term touches two branches)
+  const int sD = L.sD, sDD = sD * sD;
+  FOR(e, L.sN * sDD)
   {
-    const int t = e / (D * D), i = (e / D) % D, j = e % D;
+    const int T = e / sDD, bi = T / N, t = T - bi * N;
+    const int i = bi * sD + (e / sD) % sD, j = bi * sD + e % sD;  // dofs of the waypoint block
     double v = 0;
     if (i == j)
     {
@@ -2010,17 +2017,25 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
     }
     KB[e] = v;
   }
-  if (L.hinge)
+  if (L.hinge || L.nbr > 1)
   {
-    // dense couplings K_{t+1,t} = diag(PO_t) + sum_h rho_eff a_t+1 a_t^T
+    // dense couplings K_{t+1,t} = diag(PO_t) + sum_h rho_eff a_t+1 a_t^T, per
+    // solve block (T, T + 1) of one branch (block N - 1 of a branch couples to
+    // nothing; its entry is unused)
     double* CPL = c.a(A_CPL);
     const double *HC = c.a(A_HC), *HRE = c.a(A_HRE);
     const int* HP = c.ia(I_HPTR);
-    FOR(e, (N - 1) * D * D)
+    FOR(e, (L.sN - 1) * sDD)
     {
-      const int t = e / (D * D), i = (e / D) % D, j = e % D;
-      double v = (i == j) ? PO[t * D + i] : 0.0;
-      v = hinge_outer_sum(HC, HRE, 2 * D, D + i, j, HP[t], HP[t + 1], v);
+      const int T = e / sDD, bi = T / N, t = T - bi * N;
+      const int il = (e / sD) % sD, jl = e % sD, i = bi * sD + il, j = bi * sD + jl;
+      double v = 0.0;
+      if (t < N - 1)
+      {
+        v = (i == j) ? PO[t * D + i] : 0.0;
+        if (nh > 0)
+          v = hinge_outer_sum(HC, HRE, 2 * D, D + i, j, HP[t], HP[t + 1], v);
+      }
       CPL[e] = v;
     }
   }
@@ -2043,54 +2058,59 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
   // stores M_m (top coupling) in M[m] and M'_m (bottom coupling) in Nb[m].
   // per-half block and coupling scratch in the dynamic LDS after the chain
   // scratch (Layout::fac_off, 4 D x D blocks)
-  double* const Sblk[2] = { c.big + L.fac_off, c.big + L.fac_off + D * D };
-  double* const Lsub[2] = { c.big + L.fac_off + 2 * D * D, c.big + L.fac_off + 3 * D * D };
+  // per-wave block and coupling scratch in the dynamic LDS after the chain
+  // scratch (Layout::fac_off, 4 D x D >= 4 nbr sD x sD doubles): wave w's block
+  // Sblk(w), its coupling Lsub(w)
+  auto Sblk = [&](int w) { return c.big + L.fac_off + w * sDD; };
+  auto Lsub = [&](int w) { return c.big + L.fac_off + (2 * L.nbr + w) * sDD; };
   __shared__ int bad;
   const int m = L.tw_mid;
-  const int DD = D * D;
   if (c.tid == 0)
     bad = 0;
   BSYNC();
-  if (c.wave < 2)
+  if (c.wave < 2 * L.nbr)
   {
-    if (D > kOct)
-      twisted_factor_half<THIP_MAX_DOF>(c, sv, KB, LI, PO, Sblk[c.wave], Lsub[c.wave], bad);
+    if (sD > kOct)
+      twisted_factor_half<THIP_MAX_DOF>(c, sv, KB, LI, PO, Sblk(c.wave), Lsub(c.wave), bad);
     else
-      twisted_factor_half<kOct>(c, sv, KB, LI, PO, Sblk[c.wave], Lsub[c.wave], bad);
+      twisted_factor_half<kOct>(c, sv, KB, LI, PO, Sblk(c.wave), Lsub(c.wave), bad);
   }
   BSYNC();
-  if (c.wave == 0)
+  if ((c.wave & 1) == 0 && c.wave < 2 * L.nbr)
   {
+    // the middle block of branch b: both halves' Schur complements
+    const int bi = c.wave >> 1, mb = bi * N + m;
     const bool top = m > 0, bot = (N - 1 - m) > 0;
-    double* S = Sblk[0];
-    for (int e = c.lane; e < DD; e += 64)
+    double* S = Sblk(c.wave);
+    const double *Lt = Lsub(c.wave), *Lb = Lsub(c.wave + 1);
+    for (int e = c.lane; e < sDD; e += 64)
     {
-      const int i = e / D, j = e % D;
-      double v = KB[m * DD + e];
+      const int i = e / sD, j = e % sD;
+      double v = KB[mb * sDD + e];
       if (top)
-        for (int q = 0; q < D; ++q)
-          v -= Lsub[0][i * D + q] * Lsub[0][j * D + q];
+        for (int q = 0; q < sD; ++q)
+          v -= Lt[i * sD + q] * Lt[j * sD + q];
       if (bot)
-        for (int q = 0; q < D; ++q)
-          v -= Lsub[1][i * D + q] * Lsub[1][j * D + q];
+        for (int q = 0; q < sD; ++q)
+          v -= Lb[i * sD + q] * Lb[j * sD + q];
       S[e] = v;
     }
     wave_sync();
-    chol_inv_block(S, LI + m * DD, D, c.lane, bad);
-    const double* Li = LI + m * DD;
-    for (int e = c.lane; e < DD; e += 64)
+    chol_inv_block(S, LI + mb * sDD, sD, c.lane, bad);
+    const double* Li = LI + mb * sDD;
+    for (int e = c.lane; e < sDD; e += 64)
     {
-      const int i = e / D, j = e % D;
+      const int i = e / sD, j = e % sD;
       double vt = 0, vb = 0;
       for (int q = 0; q <= i; ++q)
       {
-        vt += Li[i * D + q] * Lsub[0][q * D + j];
-        vb += Li[i * D + q] * Lsub[1][q * D + j];
+        vt += Li[i * sD + q] * Lt[q * sD + j];
+        vb += Li[i * sD + q] * Lb[q * sD + j];
       }
       if (top)
-        sv.M[m * DD + e] = vt;
+        sv.M[mb * sDD + e] = vt;
       if (bot)
-        sv.Nb[m * DD + e] = vb;
+        sv.Nb[mb * sDD + e] = vb;
     }
   }
   BSYNC();
@@ -2353,29 +2373,37 @@ __device__ __forceinline__ void chain_any(const double* G, const double* cv, dou
 // (t = N-2..m+1); the middle block is finished by twisted_middle().
 __device__ __forceinline__ void twisted_forward(const Ctx& c, const Solver& sv, double* CV, double* YV)
 {
-  const int N = c.L.N, m = c.L.tw_mid;
-  if (c.wave == 0)
-    chain_any(sv.M, CV, YV, 0, m - 1, +1, true, c.L.D, c.lane, c.L.wide, c.L.chm_hbm);
-  else if (c.wave == 1 && N - 1 - m > 0)
-    chain_any(sv.M, CV, YV, N - 1, N - 2 - m, -1, true, c.L.D, c.lane, c.L.wide, c.L.chm_hbm);
+  // solve layout (Layout::nbr): branch b's blocks b N .. b N + N - 1, its top
+  // half on wave 2b, its bottom half on wave 2b + 1
+  const Layout& L = c.L;
+  const int N = L.N, m = L.tw_mid, half = c.wave & 1, base = (c.wave >> 1) * N;
+  if (c.wave >= 2 * L.nbr)
+    return;
+  if (half == 0)
+    chain_any(sv.M, CV, YV, base, m - 1, +1, true, L.sD, c.lane, L.wide, L.chm_hbm);
+  else if (N - 1 - m > 0)
+    chain_any(sv.M, CV, YV, base + N - 1, N - 2 - m, -1, true, L.sD, c.lane, L.wide, L.chm_hbm);
 }
 
 // Backward solve of the twisted factor, in place in CV (holding d_t =
 // LI_t^T y_t and x_m at the middle): top chain x_t = d_t - N_t x_{t+1} on
-// wave 0, bottom chain x_t = d_t - N'_t x_{t-1} on wave 1.
+// wave 0, bottom chain x_t = d_t - N'_t x_{t-1} on wave 1 (per branch: 2b, 2b + 1).
 __device__ __forceinline__ void twisted_backward(const Ctx& c, const Solver& sv, double* CV)
 {
-  const int N = c.L.N, m = c.L.tw_mid;
-  if (c.wave == 0)
-    chain_any(sv.Nb, CV, CV, m, m, -1, false, c.L.D, c.lane, c.L.wide, c.L.chm_hbm);
-  else if (c.wave == 1)
-    chain_any(sv.Nb, CV, CV, m, N - 1 - m, +1, false, c.L.D, c.lane, c.L.wide, c.L.chm_hbm);
+  const Layout& L = c.L;
+  const int N = L.N, m = L.tw_mid, half = c.wave & 1, base = (c.wave >> 1) * N;
+  if (c.wave >= 2 * L.nbr)
+    return;
+  if (half == 0)
+    chain_any(sv.Nb, CV, CV, base + m, m, -1, false, L.sD, c.lane, L.wide, L.chm_hbm);
+  else
+    chain_any(sv.Nb, CV, CV, base + m, N - 1 - m, +1, false, L.sD, c.lane, L.wide, L.chm_hbm);
 }
 
 // d_t[i] = (LI_t^T y_t)[i] for column (t, i), t != middle.
 __device__ __forceinline__ double twisted_dvalue(const Ctx& c, const double* LIp, const double* YVp, int t, int i)
 {
-  const int D = c.L.D, DD = D * D;
+  const int D = c.L.sD, DD = D * D;  // solve block t (Layout::nbr)
   const lds_f64* LI = lds(LIp);
   const lds_f64* YV = lds(YVp);
   if (c.L.wide)
@@ -2443,9 +2471,9 @@ __device__ __noinline__ void twisted_middle_wide(const Ctx& c, const Solver& sv,
 
 template <typename MP>
 __device__ __forceinline__ void twisted_middle_narrow(const Ctx& c, MP M, MP Mb, const double* LIp, double* CVp,
-                                                      const double* YVp)
+                                                      const double* YVp, int branch)
 {
-  const int D = c.L.D, DD = D * D, m = c.L.tw_mid, N = c.L.N;
+  const int D = c.L.sD, DD = D * D, N = c.L.N, mloc = c.L.tw_mid, m = branch * N + mloc;
   const int i = c.lane >> 3, k = c.lane & 7;
   const bool act = (i < D) && (k < D);
   const lds_f64* LI = lds(LIp);
@@ -2454,9 +2482,9 @@ __device__ __forceinline__ void twisted_middle_narrow(const Ctx& c, MP M, MP Mb,
   double p = 0.0;
   if (act)
   {
-    if (m > 0)
+    if (mloc > 0)
       p = M[m * DD + i * D + k] * YV[(m - 1) * D + k];
-    if (N - 1 - m > 0)
+    if (N - 1 - mloc > 0)
       p += Mb[m * DD + i * D + k] * YV[(m + 1) * D + k];
   }
   const double s = octet_sum(p);
@@ -2468,17 +2496,18 @@ __device__ __forceinline__ void twisted_middle_narrow(const Ctx& c, MP M, MP Mb,
     CV[m * D + k] = xm;
 }
 
+// the middle block of branch `branch` (wide blocks: one branch)
 __device__ __forceinline__ void twisted_middle(const Ctx& c, const Solver& sv, const double* LIp, double* CVp,
-                                               const double* YVp)
+                                               const double* YVp, int branch)
 {
   if (c.L.wide)
     twisted_middle_wide(c, sv, LIp, CVp, const_cast<double*>(YVp));
   else if (c.L.chm_hbm)
     twisted_middle_narrow(c, gbl(static_cast<const double*>(sv.M)), gbl(static_cast<const double*>(sv.Nb)), LIp, CVp,
-                          YVp);
+                          YVp, branch);
   else
     twisted_middle_narrow(c, lds(static_cast<const double*>(sv.M)), lds(static_cast<const double*>(sv.Nb)), LIp, CVp,
-                          YVp);
+                          YVp, branch);
 }
 
 // Solve K [x; aux] = r + A' eta, with r (n_cols) in A_BXW (overwritten) and
@@ -2573,7 +2602,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   // after every store the compiler cannot prove does not alias it)
   const int tid = c.tid;
   const Layout& L = c.L;
-  const int D = L.D, nx = L.nx, DD = D * D, nfr = L.n_fixed_rows, n_abs = L.n_abs, n_rows = L.n_rows;
+  const int D = L.D, nx = L.nx, nfr = L.n_fixed_rows, n_abs = L.n_abs, n_rows = L.n_rows;
   const int nc_base = L.nc_base, m_base = L.m_base;
   const bool wide = L.wide;
   const double *GS = c.a(A_GS), *WS = c.a(A_WS), *DG = c.a(A_DG), *LI = c.a(A_LINV), *BS = c.a(A_BS),
@@ -2659,12 +2688,16 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   }
   BSYNC();
   PROF_LAP(24);
-  for (int col = tid; col < nx; col += kBlock)
+  // c = LI b per solve block (Layout::nbr): solve index v is row i of block T,
+  // branch bi's part of waypoint t
+  const int sD = L.sD, sDD = sD * sD, N = L.N, nbr = L.nbr;
+  for (int v = tid; v < nx; v += kBlock)
   {
-    const int t = col / D, i = col % D;
-    const double v = wide ? masked_dot<THIP_MAX_DOF>(lds(LI) + t * DD + i * D, 1, BX + t * D, 1, 0, i + 1)
-                            : masked_dot<kOct>(lds(LI) + t * DD + i * D, 1, BX + t * D, 1, 0, i + 1);
-    lds(CV)[col] = v;
+    const int T = v / sD, i = v - T * sD, bi = T / N, t = T - bi * N;
+    const double* bt = BX + t * D + bi * sD;
+    const double cv = wide ? masked_dot<THIP_MAX_DOF>(lds(LI) + T * sDD + i * sD, 1, bt, 1, 0, i + 1)
+                           : masked_dot<kOct>(lds(LI) + T * sDD + i * sD, 1, bt, 1, 0, i + 1);
+    lds(CV)[v] = cv;
   }
   BSYNC();
   PROF_LAP(25);
@@ -2678,31 +2711,47 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     constexpr int kCols = (THIP_MAX_STEPS * THIP_MAX_DOF + kBlock - 1) / kBlock;
     const int m = L.tw_mid;
     double dv[kCols];
+    auto off_middle = [&](int cu) { return cu < nx && (cu / sD) % N != m; };
 #pragma unroll
     for (int u = 0; u < kCols; ++u)
     {
       const int cu = tid + kBlock * u;
-      dv[u] = (cu < nx && cu / D != m) ? twisted_dvalue(c, LI, YV, cu / D, cu % D) : 0.0;
+      dv[u] = off_middle(cu) ? twisted_dvalue(c, LI, YV, cu / sD, cu % sD) : 0.0;
     }
-    if (c.wave == kWaves - 1)
-      twisted_middle(c, sv, LI, CV, YV);
+    if (c.wave >= kWaves - nbr)  // the last nbr waves: one middle block each
+      twisted_middle(c, sv, LI, CV, YV, c.wave - (kWaves - nbr));
     BSYNC();
 #pragma unroll
     for (int u = 0; u < kCols; ++u)
     {
       const int cu = tid + kBlock * u;
-      if (cu < nx && cu / D != m)
+      if (off_middle(cu))
         lds(CV)[cu] = dv[u];
     }
   }
   BSYNC();
   PROF_LAP(26);
-  // backward chains, in place: x lands in CV
+  // backward chains, in place: x lands in CV (solve layout)
   twisted_backward(c, sv, CV);
   BSYNC();
   PROF_LAP(10);
-  for (int col = tid; col < nx; col += kBlock)
-    out[col] = CV[col];
+  // x in column order: in CV itself, or (branches) gathered into YV for the
+  // row products below
+  const double* XC = CV;
+  if (nbr > 1)
+  {
+    for (int col = tid; col < nx; col += kBlock)
+    {
+      const double xv = lds(CV)[solve_index(L, col)];
+      out[col] = xv;
+      lds(YV)[col] = xv;
+    }
+    BSYNC();
+    XC = YV;
+  }
+  else
+    for (int col = tid; col < nx; col += kBlock)
+      out[col] = CV[col];
   // aux back-substitution
   for (int r0 = tid; r0 < n_abs; r0 += kGenUHeavy * kBlock)
   {
@@ -2713,8 +2762,8 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       const int r = min(r0 + u * kBlock, n_abs - 1);
       const int t = row_step[r];
       const int ca = nx + 2 * r;
-      const double g = wide ? masked_dot<THIP_MAX_DOF>(GS + r * D, 1, lds(CV) + t * D, 1, 0, D)
-                              : masked_dot<kOct>(GS + r * D, 1, lds(CV) + t * D, 1, 0, D);
+      const double g = (D > kOct) ? masked_dot<THIP_MAX_DOF>(GS + r * D, 1, lds(XC) + t * D, 1, 0, D)
+                                  : masked_dot<kOct>(GS + r * D, 1, lds(XC) + t * D, 1, 0, D);
       const double rr = rho_l(nfr + r);
       const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
       const double rn = BA[ca], rp = BA[ca + 1];
@@ -2742,7 +2791,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     {
       const int h = min(h0 + u * kBlock, nh - 1);
       const int t = HT[h];
-      const double g = hinge_dot(HC + h * 2 * D, lds(CV) + t * D, D);
+      const double g = hinge_dot(HC + h * 2 * D, lds(XC) + t * D, D);
       const int col = nc_base + h;
       const double rr = rho_l(m_base + 2 * h);
       const double dn = DG[col], w = HW[h];
@@ -4766,7 +4815,7 @@ __device__ void plan_lds_dynamic(Ctx& c)
   {
     const Layout& L = c.L;
     const long long nx = L.nx, nc = c.nc(), m = c.m(), nh = c.s->n_h, D = L.D;
-    const long long NDD = (long long)L.N * D * D, nab = L.n_abs > 0 ? L.n_abs : 1;
+    const long long NDD = (long long)L.sN * L.sD * L.sD, nab = L.n_abs > 0 ? L.n_abs : 1;
     // the ADMM segment's working set first (chains, rhs, multipliers, the
     // hinge-row pack and coefficients), then the rest as in the host plan
     const int order[] = { A_LINV, A_CV, A_YV, A_CPK, A_MR, A_HPART, A_HCHK, A_HCT, A_HPK, A_HC, A_BXW, A_BA, A_HW, A_HRE, A_DG, A_GS, A_WS,
@@ -5363,7 +5412,7 @@ __device__ __forceinline__ void solve_problem(const KernelArgs& args, int b, dou
   Solver sv;
   // chain matrices: the LDS scratch, or HBM for wide blocks (Layout::wide)
   sv.M = (L.wide || L.chm_hbm) ? wsb + L.doff[A_CHM] : dyn;
-  sv.Nb = sv.M + L.N * L.D * L.D;
+  sv.Nb = sv.M + L.sN * L.sD * L.sD;
   if (threadIdx.x == 0)
   {
     ctl.trace = args.trace ? args.trace + (long long)b * args.trace_cap * THIP_TRACE_W : nullptr;

@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 #include <cstdlib>
+#include <functional>
 
 #include "layout.hpp"
 
@@ -128,7 +129,7 @@ static int g_debug_path = 0;
 
 int thip_debug_set_path(int flags)
 {
-  if (flags & ~(THIP_DEBUG_NO_SEGMENT | THIP_DEBUG_FORCE_WIDE))
+  if (flags & ~(THIP_DEBUG_NO_SEGMENT | THIP_DEBUG_FORCE_WIDE | THIP_DEBUG_NO_BRANCH))
     return THIP_E_INVALID;
   g_debug_path = flags;
   return THIP_OK;
@@ -557,17 +558,73 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   sizes[A_ZT] = sizes[A_DY] = sizes[A_AX] = sizes[A_PRV] = sizes[A_SOLY] = sizes[A_PZ] = m;
   sizes[A_MR] = std::max(L.n_rows, 1) + L.h_cap;
   sizes[A_RE] = std::max(L.n_rows, 1);
-  sizes[A_LINV] = sizes[A_KB] = NDD;
-  L.wide = (L.D > 8) ? 1 : 0;
+  // branches of the block solve (Layout::nbr): the dofs split into groups no
+  // term couples -- every CartPose term joins the dofs on the root paths of its
+  // source (and dynamic target) link, every collision sphere those of its link;
+  // joint-space terms touch single dofs.  Two contiguous groups of <= 8 dofs
+  // each (the dual arm) solve as two independent narrow block chains.
+  L.nbr = 1;
+  L.sD = L.D;
+  if (L.D > 8 && d.chain.is_tree && !(g_debug_path & (THIP_DEBUG_NO_BRANCH | THIP_DEBUG_FORCE_WIDE)))
+  {
+    std::vector<int> uf(static_cast<size_t>(L.D));
+    for (int k = 0; k < L.D; ++k)
+      uf[static_cast<size_t>(k)] = k;
+    std::function<int(int)> root = [&](int a) {
+      return uf[static_cast<size_t>(a)] == a ? a : (uf[static_cast<size_t>(a)] = root(uf[static_cast<size_t>(a)]));
+    };
+    auto join_path = [&](int link, int& first) {
+      for (int k = link; k > 0 && k < d.chain.n_links; k = d.chain.parent[k])
+      {
+        const int dof = d.chain.joint_dof[k];
+        if (dof < 0)
+          continue;
+        if (first < 0)
+          first = dof;
+        else
+          uf[static_cast<size_t>(root(dof))] = root(first);
+      }
+    };
+    for (int c = 0; c < d.n_cart; ++c)
+    {
+      int first = -1;
+      join_path(d.cart_source_link[c], first);
+      if (d.cart_target_link[c] > 0)
+        join_path(d.cart_target_link[c], first);
+    }
+    if (d.coll_enabled)
+      for (int s2 = 0; s2 < d.n_spheres; ++s2)
+      {
+        int first = -1;
+        join_path(d.sphere_link[s2], first);
+      }
+    const int half = L.D / 2;
+    bool split = (L.D % 2 == 0) && half <= 8 && root(0) != root(half);
+    for (int k = 0; k < L.D && split; ++k)
+      split = root(k) == root(k < half ? 0 : half);
+    if (split)
+    {
+      L.nbr = 2;
+      L.sD = half;
+    }
+  }
+  L.sN = L.nbr * L.N;
+  const long long sNDD = (long long)L.sN * L.sD * L.sD;
+  sizes[A_LINV] = sizes[A_KB] = sNDD;
+  L.wide = (L.sD > 8) ? 1 : 0;
   if (g_debug_path & THIP_DEBUG_FORCE_WIDE)  // diagnostic: the wide-block solve for any D
     L.wide = 1;
-  L.chm_hbm = (!L.wide && L.hinge && L.N * 8 <= kBlock && L.N <= 2 * kCpkSteps) ? 1 : 0;
-  sizes[A_CHM] = (L.wide || L.chm_hbm) ? 2 * NDD : 1;
+  // chain matrices M, N in HBM: for collision problems on the segment (its chain
+  // runs from the pack, the LDS goes to hinge-row data) and for branched solves
+  // (2 sN sD^2 doubles, 78 KB for the dual arm: the LDS keeps LINV, the solve
+  // vectors and the rows' working set instead)
+  L.chm_hbm = (!L.wide && ((L.hinge && L.N * 8 <= kBlock && L.N <= 2 * kCpkSteps) || L.nbr > 1)) ? 1 : 0;
+  sizes[A_CHM] = (L.wide || L.chm_hbm) ? 2 * sNDD : 1;
   sizes[A_PB] = std::max(nc + m, nab * D);
   sizes[A_PS] = sizes[A_PR] = nc + m;
   sizes[A_HC0] = sizes[A_HC] = hc * 2 * D;
   sizes[A_HK] = sizes[A_HW] = sizes[A_HRE] = sizes[A_HDIST] = sizes[A_HCCT] = hc;
-  sizes[A_CPL] = L.hinge ? NDD : 1;
+  sizes[A_CPL] = (L.hinge || L.nbr > 1) ? sNDD : 1;
   sizes[A_CSCR] = L.coll ? (long long)kWaves * kSubCap * d.n_spheres * 3 : 1;
   sizes[A_HCOST] = L.N;
   sizes[A_HPK] = L.hinge ? hc * kHPack : 1;
@@ -614,7 +671,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     ioff += (isizes[k] + 15) / 16 * 16;
   }
   L.istride = ioff;
-  const size_t lds_d = std::max<size_t>({ (size_t)((L.wide || L.chm_hbm) ? 0 : 2 * NDD), (size_t)(30 * std::max(L.n_cart, 1)),
+  const size_t lds_d = std::max<size_t>({ (size_t)((L.wide || L.chm_hbm) ? 0 : 2 * sNDD), (size_t)(30 * std::max(L.n_cart, 1)),
                                           (size_t)(L.n_costs + L.n_cnts + 2) });
   ctx->lds_lin_bytes = lds_d * sizeof(double);
   // LDS residency plan: the per-ADMM-iteration working set, hottest first,
