@@ -208,6 +208,11 @@ struct Layout
   int nbr;
   int sD;
   int sN;
+  // the CartPose rows of every waypoint are contiguous and in order (step_rows
+  // is the identity): the generic step reads a waypoint's rows without the
+  // step_rows indirection (max_step_rows: the most rows of one waypoint)
+  int rows_contig;
+  int max_step_rows;
 };
 
 // the solve-layout index of column col (t, j): block b * N + t, row j - b sD

@@ -2575,6 +2575,76 @@ __device__ __forceinline__ double csr_row_gather(const int* rows, int p0, int p1
 }
 
 
+// csr_row_gather for contiguous rows (Layout::rows_contig): the rows [p0, p1)
+// themselves, at most 16, every load issued before the sum (in the same order)
+__device__ __forceinline__ double contig_row_gather(int p0, int p1, const double* GS, const double* MR, int D, int j,
+                                                    double b)
+{
+  double g[16], mv[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u)
+  {
+    const int r = max(min(p0 + u, p1 - 1), 0);  // clamped: every load valid (an empty range reads row 0)
+    g[u] = GS[r * D + j];
+    mv[u] = MR[r];
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u)
+    b = fma(g[u], mv[u] * ((p0 + u < p1) ? 1.0 : 0.0), b);  // masked: b unchanged
+  return b;
+}
+
+// both hinge_gather calls of column (t, j) -- pair t's rows on coefficient j,
+// then pair t - 1's on D + j -- with the first chunk of each pair loaded
+// together (a pair rarely has more than kHChunk rows); the sums and their
+// association are hinge_gather's
+__device__ __forceinline__ double hinge_gather2(const double* HC, const double* mr, int stride, int j, const int* HP,
+                                                int t, double b)
+{
+  const int D = stride / 2;
+  const int a0 = HP[t], a1 = HP[t + 1];
+  const int c0 = (t > 0) ? HP[t - 1] : a0, c1 = a0;
+  double ha[kHChunk], ma[kHChunk], hb[kHChunk], mb[kHChunk];
+  const int ae = min(a0 + kHChunk, a1), ce = min(c0 + kHChunk, c1);
+#pragma unroll
+  for (int i = 0; i < kHChunk; ++i)
+  {
+    const int h = min(a0 + i, max(ae - 1, 0));
+    ha[i] = HC[h * stride + j];
+    ma[i] = mr[h];
+    const int g = min(c0 + i, max(ce - 1, 0));
+    hb[i] = HC[g * stride + D + j];
+    mb[i] = mr[g];
+  }
+  if (a0 < a1)
+  {
+    double s0 = 0, s1 = 0;
+#pragma unroll
+    for (int i = 0; i < kHChunk; i += 2)
+    {
+      s0 = fma(ha[i], ma[i] * ((a0 + i < ae) ? 1.0 : 0.0), s0);
+      s1 = fma(ha[i + 1], ma[i + 1] * ((a0 + i + 1 < ae) ? 1.0 : 0.0), s1);
+    }
+    b += s0 + s1;
+    if (ae < a1)
+      b = hinge_gather(HC, mr, stride, j, ae, a1, b);
+  }
+  if (c0 < c1)
+  {
+    double s0 = 0, s1 = 0;
+#pragma unroll
+    for (int i = 0; i < kHChunk; i += 2)
+    {
+      s0 = fma(hb[i], mb[i] * ((c0 + i < ce) ? 1.0 : 0.0), s0);
+      s1 = fma(hb[i + 1], mb[i + 1] * ((c0 + i + 1 < ce) ? 1.0 : 0.0), s1);
+    }
+    b += s0 + s1;
+    if (ce < c1)
+      b = hinge_gather(HC, mr, stride, D + j, ce, c1, b);
+  }
+  return b;
+}
+
 // a hinge row's distance-expression value a_t.x_t + a_t+1.x_t+1 (two
 // independent partial sums, one per waypoint); x points at x_t
 template <typename XP>
@@ -2678,12 +2748,12 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     const int f = fixed_of_step[t];
     if (f >= 0)
       b += FS[f * D + j] * eta[f * D + j];
-    b = csr_row_gather(step_rows, step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
+    if (L.rows_contig && L.max_step_rows <= 16)
+      b = contig_row_gather(step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
+    else
+      b = csr_row_gather(step_rows, step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
     if (nh > 0)
-    {
-      b = hinge_gather(HC, MR + n_rows, 2 * D, j, HP[t], HP[t + 1], b);
-      b = hinge_gather(HC, MR + n_rows, 2 * D, D + j, t > 0 ? HP[t - 1] : HP[t], HP[t], b);
-    }
+      b = hinge_gather2(HC, MR + n_rows, 2 * D, j, HP, t, b);
     BX[col] = b;
   }
   BSYNC();
@@ -2826,9 +2896,10 @@ __device__ __forceinline__ double row_ax(const Ctx& c, int r, const double* x)
     const int a = r - L.n_fixed_rows;
     const int t = c.T.row_step[a];
     const double* GS = c.a(A_GS);
-    double v = 0;
-    for (int j = 0; j < D; ++j)
-      v += GS[a * D + j] * x[t * D + j];
+    // fixed-length masked product: every load in flight at once, the terms
+    // summed in the plain loop's order
+    double v = (D > kOct) ? masked_dot<THIP_MAX_DOF>(GS + a * D, 1, x + t * D, 1, 0, D)
+                          : masked_dot<kOct>(GS + a * D, 1, x + t * D, 1, 0, D);
     const int ca = L.nx + 2 * a;
     v += c.a(A_WS)[2 * a] * x[ca] + c.a(A_WS)[2 * a + 1] * x[ca + 1];
     return v;
@@ -3382,9 +3453,8 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
     }
     const int a = r - nfr;
     const int t = row_step[a];
-    double v = 0;
-    for (int j = 0; j < D; ++j)
-      v += GS[a * D + j] * XT[t * D + j];
+    double v = (D > kOct) ? masked_dot<THIP_MAX_DOF>(GS + a * D, 1, XT + t * D, 1, 0, D)
+                          : masked_dot<kOct>(GS + a * D, 1, XT + t * D, 1, 0, D);
     const int ca = nx + 2 * a;
     v += WS[2 * a] * XT[ca] + WS[2 * a + 1] * XT[ca + 1];
     return v;

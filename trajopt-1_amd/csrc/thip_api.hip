@@ -700,6 +700,11 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     int max_step_rows = 0;
     for (int t = 0; t < L.N; ++t)
       max_step_rows = std::max(max_step_rows, step_ptr[static_cast<size_t>(t) + 1] - step_ptr[static_cast<size_t>(t)]);
+    L.max_step_rows = max_step_rows;
+    L.rows_contig = 1;
+    for (int r = 0; r < L.n_abs; ++r)
+      if (step_rows[static_cast<size_t>(r)] != r)
+        L.rows_contig = 0;
     // one column slot (t, i) and one CartPose row per thread: N <= 32 and
     // n_abs <= 256; larger problems run the generic admm_step()
     // (collision problems: hinge rows are loop-owned inside the segment)
