@@ -248,6 +248,8 @@ struct Tables
   // abs rows of every source (CartPose rows, JointPos constraint rows)
   int* row_slot;   // merit slot of the row's constraint term, -1 for cost rows (n_abs)
   int* row_jpos;   // 1: JointPos EQ constraint row (row_term = JointPos term, row_comp = joint) (n_abs)
+  int* row_off;    // branched solves (Layout::nbr > 1): first dof of the row's branch, whose sD
+                   // coefficients are the row's only nonzeros (n_abs; 0 otherwise)
   // JointPos terms (hatch-clamped steps, cost or constraint slot)
   int* jpos_first; // (THIP_MAX_JPOS)
   int* jpos_last;

@@ -2741,20 +2741,33 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   }
   BSYNC();
   PROF_LAP(23);
-  for (int col = tid; col < nx; col += kBlock)
+  // the waypoint right-hand sides, kRhsU columns per thread at once (their
+  // loads overlap; each column's sums in the order of one column alone)
+  constexpr int kRhsU = 3;
+  for (int c0 = tid; c0 < nx; c0 += kRhsU * kBlock)
   {
-    const int t = col / D, j = col % D;
-    double b = BX[col] + BS[col] * eta[brow(col)];
-    const int f = fixed_of_step[t];
-    if (f >= 0)
-      b += FS[f * D + j] * eta[f * D + j];
-    if (L.rows_contig && L.max_step_rows <= 16)
-      b = contig_row_gather(step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
-    else
-      b = csr_row_gather(step_rows, step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
-    if (nh > 0)
-      b = hinge_gather2(HC, MR + n_rows, 2 * D, j, HP, t, b);
-    BX[col] = b;
+    double bv[kRhsU];
+#pragma unroll
+    for (int u = 0; u < kRhsU; ++u)
+    {
+      const int col = min(c0 + u * kBlock, nx - 1);  // clamped: every load valid
+      const int t = col / D, j = col % D;
+      double b = BX[col] + BS[col] * eta[brow(col)];
+      const int f = fixed_of_step[t];
+      if (f >= 0)
+        b += FS[f * D + j] * eta[f * D + j];
+      if (L.rows_contig && L.max_step_rows <= 16)
+        b = contig_row_gather(step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
+      else
+        b = csr_row_gather(step_rows, step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
+      if (nh > 0)
+        b = hinge_gather2(HC, MR + n_rows, 2 * D, j, HP, t, b);
+      bv[u] = b;
+    }
+#pragma unroll
+    for (int u = 0; u < kRhsU; ++u)
+      if (c0 + u * kBlock < nx)
+        BX[c0 + u * kBlock] = bv[u];
   }
   BSYNC();
   PROF_LAP(24);
@@ -2832,8 +2845,10 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       const int r = min(r0 + u * kBlock, n_abs - 1);
       const int t = row_step[r];
       const int ca = nx + 2 * r;
-      const double g = (D > kOct) ? masked_dot<THIP_MAX_DOF>(GS + r * D, 1, lds(XC) + t * D, 1, 0, D)
-                                  : masked_dot<kOct>(GS + r * D, 1, lds(XC) + t * D, 1, 0, D);
+      const int o = (nbr > 1) ? c.T.row_off[r] : 0;  // the row's branch (exact zeros elsewhere)
+      const double g = (nbr > 1)  ? masked_dot<kOct>(GS + r * D + o, 1, lds(XC) + t * D + o, 1, 0, sD)
+                       : (D > kOct) ? masked_dot<THIP_MAX_DOF>(GS + r * D, 1, lds(XC) + t * D, 1, 0, D)
+                                    : masked_dot<kOct>(GS + r * D, 1, lds(XC) + t * D, 1, 0, D);
       const double rr = rho_l(nfr + r);
       const double dn = DG[ca], dp = DG[ca + 1], wn = WS[2 * r], wp = WS[2 * r + 1];
       const double rn = BA[ca], rp = BA[ca + 1];
@@ -2898,8 +2913,15 @@ __device__ __forceinline__ double row_ax(const Ctx& c, int r, const double* x)
     const double* GS = c.a(A_GS);
     // fixed-length masked product: every load in flight at once, the terms
     // summed in the plain loop's order
-    double v = (D > kOct) ? masked_dot<THIP_MAX_DOF>(GS + a * D, 1, x + t * D, 1, 0, D)
-                          : masked_dot<kOct>(GS + a * D, 1, x + t * D, 1, 0, D);
+    double v;
+    if (L.nbr > 1)  // only the row's branch has nonzero coefficients (exact zeros elsewhere)
+    {
+      const int o = c.T.row_off[a];
+      v = masked_dot<kOct>(GS + a * D + o, 1, x + t * D + o, 1, 0, L.sD);
+    }
+    else
+      v = (D > kOct) ? masked_dot<THIP_MAX_DOF>(GS + a * D, 1, x + t * D, 1, 0, D)
+                     : masked_dot<kOct>(GS + a * D, 1, x + t * D, 1, 0, D);
     const int ca = L.nx + 2 * a;
     v += c.a(A_WS)[2 * a] * x[ca] + c.a(A_WS)[2 * a + 1] * x[ca + 1];
     return v;
@@ -3443,7 +3465,8 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
   const Layout& L = c.L;
   const int D = L.D, nx = L.nx, nfr = L.n_fixed_rows, n_rows = L.n_rows, m_base = L.m_base, nc_base = L.nc_base;
   const double *FS = c.a(A_FS), *GS = c.a(A_GS), *WS = c.a(A_WS), *BS = c.a(A_BS);
-  const int *row_step = c.T.row_step, *fixed_steps = c.d->fixed_steps;
+  const int *row_step = c.T.row_step, *fixed_steps = c.d->fixed_steps, *row_off = c.T.row_off;
+  const int nbr = L.nbr, sD = L.sD;
   // row_ax() for the fixed and CartPose rows, on the hoisted values (same expressions)
   auto row_ax_l = [&](int r) {
     if (r < nfr)
@@ -3453,8 +3476,15 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
     }
     const int a = r - nfr;
     const int t = row_step[a];
-    double v = (D > kOct) ? masked_dot<THIP_MAX_DOF>(GS + a * D, 1, XT + t * D, 1, 0, D)
-                          : masked_dot<kOct>(GS + a * D, 1, XT + t * D, 1, 0, D);
+    double v;
+    if (nbr > 1)  // the row's branch only (exact zeros elsewhere)
+    {
+      const int o = row_off[a];
+      v = masked_dot<kOct>(GS + a * D + o, 1, XT + t * D + o, 1, 0, sD);
+    }
+    else
+      v = (D > kOct) ? masked_dot<THIP_MAX_DOF>(GS + a * D, 1, XT + t * D, 1, 0, D)
+                     : masked_dot<kOct>(GS + a * D, 1, XT + t * D, 1, 0, D);
     const int ca = nx + 2 * a;
     v += WS[2 * a] * XT[ca] + WS[2 * a + 1] * XT[ca + 1];
     return v;

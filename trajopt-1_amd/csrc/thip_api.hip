@@ -565,6 +565,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   // each (the dual arm) solve as two independent narrow block chains.
   L.nbr = 1;
   L.sD = L.D;
+  std::vector<int> row_off(static_cast<size_t>(std::max(L.n_abs, 1)), 0);
   if (L.D > 8 && d.chain.is_tree && !(g_debug_path & (THIP_DEBUG_NO_BRANCH | THIP_DEBUG_FORCE_WIDE)))
   {
     std::vector<int> uf(static_cast<size_t>(L.D));
@@ -606,6 +607,23 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     {
       L.nbr = 2;
       L.sD = half;
+      // the branch of every CartPose / JointPos constraint row: its coefficients
+      // outside the branch's dofs are exact zeros
+      for (int r = 0; r < L.n_abs; ++r)
+      {
+        int dof = -1;
+        if (row_jpos[static_cast<size_t>(r)])
+          dof = row_comp[static_cast<size_t>(r)];
+        else
+        {
+          int first = -1;
+          std::vector<int> keep(uf);
+          join_path(d.cart_source_link[row_term[static_cast<size_t>(r)]], first);
+          uf = keep;
+          dof = first;
+        }
+        row_off[static_cast<size_t>(r)] = (dof >= half) ? half : 0;
+      }
     }
   }
   L.sN = L.nbr * L.N;
@@ -770,7 +788,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   const size_t o_t0 = push(term_row0, THIP_MAX_CART), o_tn = push(term_nrow, THIP_MAX_CART),
                o_ts = push(term_slot, THIP_MAX_CART);
   const size_t o_fs = push(fixed_of_step, static_cast<size_t>(L.N));
-  const size_t o_rsl = push(row_slot, na), o_rjp = push(row_jpos, na);
+  const size_t o_rsl = push(row_slot, na), o_rjp = push(row_jpos, na), o_rof = push(row_off, na);
   const size_t o_jq = push(jpos_ineq, THIP_MAX_JPOS);
   const size_t nsh = static_cast<size_t>(n_sh);
   const size_t o_shk = push(sh_kind, nsh), o_sho = push(sh_owner, nsh), o_shj = push(sh_joint, nsh),
@@ -827,6 +845,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   T.fixed_of_step = ctx->d_tables + o_fs;
   T.row_slot = ctx->d_tables + o_rsl;
   T.row_jpos = ctx->d_tables + o_rjp;
+  T.row_off = ctx->d_tables + o_rof;
   T.jpos_first = ctx->d_tables + o_jf;
   T.jpos_last = ctx->d_tables + o_jl;
   T.jpos_slot = ctx->d_tables + o_js;
