@@ -3699,6 +3699,7 @@ __device__ __forceinline__ void seg_chain_solve(const SegChain& ch, long long& l
   const int h = (wave == 1) ? 1 : 0;
   const int tdir = (wave == 0) ? -1 : 1;               // t = m + tdir * (1 + r)
   double q[kCpkSteps];
+  double nb[kCpkSteps];  // the backward blocks, loaded before the barrier (their latency hides in its wait)
   double y = 0.0;
   if (wave < 2)
   {
@@ -3745,6 +3746,10 @@ __device__ __forceinline__ void seg_chain_solve(const SegChain& ch, long long& l
     // y_{m -+ 1} (COL layout) to the middle
     if (i == 0 && k < D)
       P[kCpkYM + h * 8 + k] = y;
+    const lds_f64* NBp = P + kCpkNB + h * kCpkSteps * 64 + lane;  // + r * 64
+#pragma unroll
+    for (int r = 0; r < kCpkSteps; ++r)
+      nb[r] = NBp[r * 64];
   }
   if (pf)
     own_fwd += clock64() - tq;  // wave 0's own forward half, without the barrier
@@ -3762,12 +3767,6 @@ __device__ __forceinline__ void seg_chain_solve(const SegChain& ch, long long& l
     const double ym1 = P[kCpkYM + kc];
     const double yp1 = P[kCpkYM + 8 + kc];
     const double bm = P[kCpkBM + kc];
-    __builtin_amdgcn_sched_barrier(0);
-    const lds_f64* NBp = P + kCpkNB + h * kCpkSteps * 64 + lane;  // + r * 64
-    double nb[kCpkSteps];
-#pragma unroll
-    for (int r = 0; r < kCpkSteps; ++r)
-      nb[r] = NBp[r * 64];
     __builtin_amdgcn_sched_barrier(0);
     const double p = fma(-ch.mnb, yp1, fma(-ch.mm, ym1, ch.mli * bm));
     const double ym = octet_sum(p);           // ROW
