@@ -3681,7 +3681,9 @@ __device__ __forceinline__ int seg_b_slot(int t, int i, int m)
 // is one LDS instruction from a per-lane base with an immediate offset (the
 // pack's lane order), and the forward pass loads the (LI, M) pair of a step
 // as one 16-byte read; the next group of kSegGroup steps is loaded while the
-// current group runs.
+// current group runs, and the backward pass's blocks are loaded before the
+// barrier between the passes (their latency overlaps the wait for the other
+// half).
 constexpr int kSegGroup = 4;
 static_assert(kCpkSteps % kSegGroup == 0, "chain groups");
 typedef __attribute__((ext_vector_type(2))) double dbl2;
