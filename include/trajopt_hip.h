@@ -46,8 +46,9 @@ extern "C" {
 /* ABI version of the structs below: thip_create rejects a descriptor whose
  * abi_version differs (a caller compiled against another layout).  3: the
  * descriptor carries abi_version, thip_chain.is_tree, thip_sqp_params.max_time.
- * 4: use_time, fixed dofs, time JointVel.  5: TotalTime. */
-#define THIP_ABI_VERSION 5
+ * 4: use_time, fixed dofs, time JointVel.  5: TotalTime.  6: further collision
+ * terms (thip_coll_term), single-waypoint problems on the generic path. */
+#define THIP_ABI_VERSION 6
 
 #define THIP_MAX_DOF 16
 #define THIP_MAX_LINKS 32
@@ -60,6 +61,7 @@ extern "C" {
 #define THIP_MAX_JDT 8
 #define THIP_MAX_JVT 4
 #define THIP_MAX_TTT 2
+#define THIP_MAX_COLL_EXTRA 3
 #define THIP_MAX_CONTACTS 131072
 
 /* error codes */
@@ -167,6 +169,23 @@ typedef struct thip_osqp_settings {
   double delta;          /* 1e-6 */
   int polish_refine_iter;/* 3 */
 } thip_osqp_settings;
+
+/* One CollisionTermInfo beyond the descriptor's first (coll_* fields):
+ * CollisionTermInfo::hatch (problem_description.cpp:1735-1858) with its own
+ * evaluator, margin, coefficient and steps over the shared robot spheres and
+ * scene.  `continuous` as coll_continuous. */
+typedef struct thip_coll_term {
+  int is_cnt;
+  int first_step;
+  int last_step;   /* -1 = the last waypoint */
+  int n_fixed;
+  int fixed_steps[THIP_MAX_STEPS];
+  double margin;   /* dist_pen */
+  double coeff;    /* coeffs */
+  double buffer;   /* collision_margin_buffer */
+  double lvs;      /* longest_valid_segment_length (CONTINUOUS: +inf) */
+  int continuous;  /* 0 LVS_DISCRETE, 1 LVS_CONTINUOUS / CONTINUOUS, 2 DISCRETE */
+} thip_coll_term;
 
 /* The structure shared by every problem of a batch: chain, horizon, term
  * tables (the lowered TermInfo list), solver parameters.  Per-problem data
@@ -337,6 +356,13 @@ typedef struct thip_problem_desc {
    * batch (~800 B per row and problem), at least 2048.  A QP with more
    * contacts ends the run with OPT_FAILED and THIP_FLAG_CONTACT_OVERFLOW. */
   int coll_max_contacts;
+  /* further collision terms (a collision cost and a collision constraint in one
+   * problem, simple_collision_test.json:6-37): cost terms follow the first
+   * collision term's cost, constraint terms its constraint, each in hatch
+   * order.  The generic path evaluates them on the device (thip_eval_*);
+   * thip_create rejects n_coll_extra > 0. */
+  int n_coll_extra;
+  thip_coll_term coll_extra[THIP_MAX_COLL_EXTRA];
 
   thip_sqp_params sqp;
   thip_osqp_settings osqp;
@@ -480,6 +506,49 @@ int thip_debug_layout(thip_ctx* ctx, long long* doff, long long* ioff, long long
 #define THIP_DEBUG_NO_BRANCH 4  /* one block solve over all dofs even when the terms split the tree */
 int thip_debug_set_path(int flags);
 int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws);
+
+/* ------------------------------------------------------- Term evaluation
+ * The kinematic terms of one problem structure evaluated on the device for
+ * sco::BasicTrustRegionSQP's host loop (the generic path, which runs what the
+ * batched kernel does not lower: single-waypoint problems, several collision
+ * terms, CartPose / collision next to JointAcc / JointJerk / time terms or a
+ * user sco::Cost).  Replaces the CPU evaluation the reference's term objects
+ * do inside the loop:
+ *   thip_eval_cart_pose  <- CartPoseErrCalculator / CartPoseJacCalculator
+ *                           (trajopt/src/kinematic_terms.cpp:189-370) and the
+ *                           DynamicCartPose pair (:58-187), called through
+ *                           TrajOptCostFromErrFunc / TrajOptConstraintFromErrFunc
+ *                           (CartPoseTermInfo::hatch, problem_description.cpp:919-1005)
+ *   thip_eval_collision  <- CollisionEvaluator::CalcCollisions / GetGradient /
+ *                           CalcDistExpressions* (collision_terms.cpp:195-554,
+ *                           646-688, 817-898, 978-1161), called by
+ *                           CollisionCost / CollisionConstraint::value / convex
+ *                           (:1267-1386), one term object per unit
+ *                           (CollisionTermInfo::hatch, problem_description.cpp:1735-1858)
+ * A thip_eval holds a descriptor (any n_steps in [1, THIP_MAX_STEPS], any term
+ * set: only the chain, CartPose and collision fields are read) and the CartPose
+ * targets and scenes of `batch` problems.  Synchronous; host arrays. */
+typedef struct thip_eval thip_eval;
+int thip_eval_create(int device, const thip_problem_desc* desc, int batch, thip_eval** out);
+/* cart_targets [batch][n_cart][12], scene [batch][n_prims][16] (NULL when empty) */
+int thip_eval_upload(thip_eval* ev, const double* cart_targets, const double* scene);
+/* CartPose term `term` (descriptor order) of every problem at its waypoint's joint
+ * values q [batch][n_dof]: err [batch][6] the (banded) transform error, jac
+ * [batch][6][n_dof] its forward-difference jacobian (eps 1e-5) or NULL for the
+ * error alone.  All six components: the caller keeps those whose coefficient is
+ * nonzero (CartPoseTermInfo::hatch's indices). */
+int thip_eval_cart_pose(thip_eval* ev, int term, const double* q, double* err, double* jac);
+/* Collision term `term` (0: the coll_* term when coll_enabled, then coll_extra[])
+ * at trajectories x [batch][n_steps][n_dof]: every contact of every unit (a free
+ * waypoint of [first, last] for DISCRETE, else a step pair) with its linearised
+ * distance expression, in unit order, then ContactResultMap order.  records
+ * [batch][cap][8 + 2 n_dof + 1] = [t, link, prim, sphere, substate, distance,
+ * cc_time, n_kept, a_t[n_dof], a_t+1[n_dof], constant] as thip_collision_rows
+ * (t = the unit's waypoint; a_t+1 = 0 for DISCRETE); counts [batch] = contacts
+ * found (records beyond cap are not written). */
+int thip_eval_collision(thip_eval* ev, int term, const double* x, double* records, int cap, int* counts);
+void thip_eval_destroy(thip_eval* ev);
+const char* thip_eval_last_error(thip_eval* ev); /* NULL: the last thip_eval_create failure */
 
 /* ------------------------------------------------------------- Generic QP
  * OSQP 1.0 on an arbitrary sparse QP

@@ -9,7 +9,7 @@
  * BasicTrustRegionSQP (trajopt_sco/src/optimizers.cpp:699-991).  These C
  * wrappers expose it to ctypes / FFI callers: JSON problem text in the
  * reference's TrajOptRequest format (trajopt_common/data/config/ JSON files) on the
- * built-in PR2 "right_arm" environment.  Return 0 on success, -1 on failure
+ * built-in environment of the reference's test robots (thost_lower_json).  Return 0 on success, -1 on failure
  * with the message (the reference's std::runtime_error text) in err.
  */
 #ifndef TRAJOPT_HOST_H
@@ -21,16 +21,21 @@
 extern "C" {
 #endif
 
-/* Parse + ConstructProblem for one JSON problem; `scene` holds the
- * environment's primitives ([n_prims][16], THIP_PRIM_* records, may be NULL
- * when n_prims == 0).  Outputs (caller-sized to the maxima):
+/* Parse + ConstructProblem for one JSON problem; `scene` holds primitives added
+ * to the built-in environment's own ([n_prims][16], THIP_PRIM_* records, may be
+ * NULL when n_prims == 0).  The environment is the reference test robot of
+ * basic_info.manip: the PR2 (right_arm, left_arm, both_arms; empty scene) or
+ * spherebot ("manipulator"; its three static spheres first).  Outputs
+ * (caller-sized to the maxima):
  *   desc          the batch-shared structure (per-problem JointPos targets zeroed)
  *   init          [n_steps][n_dof]                initial trajectory
  *   cart_targets  [n_cart][12]                    CartPose target offsets in the chain root
  *   jpos_targets  [n_jpos][n_dof]                 JointPos targets
+ *   scene_out     [desc.n_prims][16]              the scene the collision terms see
  * Any output pointer may be NULL. */
 int thost_lower_json(const char* json_text, const double* scene, int n_prims, thip_problem_desc* desc,
-                     double* init, double* cart_targets, double* jpos_targets, char* err, int err_len);
+                     double* init, double* cart_targets, double* jpos_targets, double* scene_out, char* err,
+                     int err_len);
 
 /* ConstructProblem for each of `batch` JSON problems (scenes [batch][n_prims][16])
  * and one BatchTrustRegionSQP on HIP device `device`:

@@ -188,20 +188,21 @@ def fwd_kin(chain, q):
     return out
 
 
-def collision_rows(wl, b, x=None, cap=8192):
+def collision_rows(wl, b, x=None, cap=8192, term=0):
     """Linearised collision rows of problem b at trajectory x (default: the
-    initial trajectory); see oracle_collision_rows.  Returns an array
-    [n, 8 + 2 D + 1]."""
+    initial trajectory) for collision term `term` (0: the descriptor's coll_*
+    term, k: coll_extra[k - 1]); see oracle_collision_rows_term.  Returns an
+    array [n, 8 + 2 D + 1]."""
     L = lib()
-    L.oracle_collision_rows.argtypes = [C.POINTER(abi.ProblemDesc), C.POINTER(C.c_double), C.POINTER(C.c_double),
-                                        C.POINTER(C.c_double), C.c_int]
-    L.oracle_collision_rows.restype = C.c_int
+    L.oracle_collision_rows_term.argtypes = [C.POINTER(abi.ProblemDesc), C.c_int, C.POINTER(C.c_double),
+                                             C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int]
+    L.oracle_collision_rows_term.restype = C.c_int
     D = wl.n_dof
     W = 8 + 2 * D + 1
     xb = np.ascontiguousarray(wl.init[b] if x is None else x, dtype=np.float64)
     sc = np.ascontiguousarray(wl.scene[b], dtype=np.float64)
     out = np.zeros((cap, W))
-    n = L.oracle_collision_rows(C.byref(wl.desc), _dp(sc), _dp(xb), _dp(out), cap)
+    n = L.oracle_collision_rows_term(C.byref(wl.desc), term, _dp(sc), _dp(xb), _dp(out), cap)
     if n < 0:
         raise RuntimeError(L.oracle_last_error().decode())
     return out[:min(n, cap)]

@@ -703,8 +703,27 @@ private:
 };
 }  // namespace
 
-void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, const thip_problem_desc& d,
-                       const double* scene)
+thip_coll_term collisionTerm(const thip_problem_desc& d, int k)
+{
+  if (k > 0)
+    return d.coll_extra[k - 1];
+  thip_coll_term t{};
+  t.is_cnt = d.coll_is_cnt;
+  t.first_step = d.coll_first_step;
+  t.last_step = d.coll_last_step;
+  t.n_fixed = d.coll_n_fixed;
+  for (int i = 0; i < d.coll_n_fixed && i < THIP_MAX_STEPS; ++i)
+    t.fixed_steps[i] = d.coll_fixed_steps[i];
+  t.margin = d.coll_margin;
+  t.coeff = d.coll_coeff;
+  t.buffer = d.coll_buffer;
+  t.lvs = d.coll_lvs;
+  t.continuous = d.coll_continuous;
+  return t;
+}
+
+std::shared_ptr<CollisionModel> collisionModel(const thip_problem_desc& d, const thip_coll_term& t,
+                                               const double* scene)
 {
   auto cm = std::make_shared<CollisionModel>();
   cm->chain = &d.chain;
@@ -719,20 +738,28 @@ void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, cons
   cm->n_prims = d.n_prims;
   cm->scene_store.assign(scene, scene + 16 * d.n_prims);
   cm->scene = cm->scene_store.data();
-  cm->margin = d.coll_margin;
-  cm->coeff = d.coll_coeff;
-  cm->buffer = d.coll_buffer;
-  cm->lvs = d.coll_lvs;
-  cm->continuous = d.coll_continuous == 1;
-  const int first = d.coll_first_step;
-  const int last = (d.coll_last_step < 0) ? d.n_steps - 1 : d.coll_last_step;
+  cm->margin = t.margin;
+  cm->coeff = t.coeff;
+  cm->buffer = t.buffer;
+  cm->lvs = t.lvs;
+  cm->continuous = t.continuous == 1;
+  return cm;
+}
+
+void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, const thip_problem_desc& d,
+                       const double* scene, int term)
+{
+  const thip_coll_term tm = collisionTerm(d, term);
+  auto cm = collisionModel(d, tm, scene);
+  const int first = tm.first_step;
+  const int last = (tm.last_step < 0) ? d.n_steps - 1 : tm.last_step;
   auto fixed = [&](int t) {
-    for (int k = 0; k < d.coll_n_fixed; ++k)
-      if (d.coll_fixed_steps[k] == t)
+    for (int k = 0; k < tm.n_fixed; ++k)
+      if (tm.fixed_steps[k] == t)
         return true;
     return false;
   };
-  if (d.coll_continuous == 2)
+  if (tm.continuous == 2)
   {
     // DISCRETE: SINGLE_TIME_STEP terms on the free waypoints of [first, last]
     for (int i = first; i <= last; ++i)
@@ -740,7 +767,7 @@ void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, cons
       if (fixed(i))
         continue;
       CollisionSingleCalc calc(cm, rows[static_cast<std::size_t>(i)]);
-      if (d.coll_is_cnt)
+      if (tm.is_cnt)
       {
         auto c = std::make_shared<CollisionPairConstraint<CollisionSingleCalc>>(std::move(calc));
         c->setName("collision_" + std::to_string(i));
@@ -768,7 +795,7 @@ void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, cons
     else
       type = CollisionPairCalc::kStartFreeEndFixed;
     CollisionPairCalc calc(cm, rows[static_cast<std::size_t>(i)], rows[static_cast<std::size_t>(i + 1)], type);
-    if (d.coll_is_cnt)
+    if (tm.is_cnt)
     {
       auto c = std::make_shared<CollisionPairConstraint<CollisionPairCalc>>(std::move(calc));
       c->setName("collision_" + std::to_string(i));

@@ -18,6 +18,7 @@
 // Bullet; the map order is (robot link, primitive) rather than tesseract's
 // link-id hash order.
 #pragma once
+#include <memory>
 #include <vector>
 
 #include "terms.hpp"
@@ -66,6 +67,11 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
 void contactGradient(const CollisionModel& cm, const double* dofvals, const Contact& ct, bool timestep1,
                      double* grad, double& scale);
 
+// collision term k of the descriptor: 0 = the coll_* fields, k >= 1 = coll_extra[k - 1]
+thip_coll_term collisionTerm(const thip_problem_desc& d, int k);
+std::shared_ptr<CollisionModel> collisionModel(const thip_problem_desc& d, const thip_coll_term& t,
+                                               const double* scene);
+// CollisionTermInfo::hatch for collision term k: one term object per unit
 void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, const thip_problem_desc& d,
-                       const double* scene);
+                       const double* scene, int term = 0);
 }  // namespace orc

@@ -1052,6 +1052,9 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
       addTotalTimeTerm(tp, d, k);
   if (d.coll_enabled && !d.coll_is_cnt)
     addCollisionTerms(tp, rows, d, scene);
+  for (int k = 0; k < d.n_coll_extra; ++k)  // further collision terms, in hatch order
+    if (!d.coll_extra[k].is_cnt)
+      addCollisionTerms(tp, rows, d, scene, 1 + k);
   // cnt_infos: CartPose constraints, collision constraint
   for (int k = 0; k < d.n_cart; ++k)
   {
@@ -1084,6 +1087,9 @@ TrajProblem constructProblem(const thip_problem_desc& d, const double* init_traj
       addTotalTimeTerm(tp, d, k);
   if (d.coll_enabled && d.coll_is_cnt)
     addCollisionTerms(tp, rows, d, scene);
+  for (int k = 0; k < d.n_coll_extra; ++k)
+    if (d.coll_extra[k].is_cnt)
+      addCollisionTerms(tp, rows, d, scene, 1 + k);
   return tp;
 }
 

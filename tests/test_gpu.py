@@ -892,14 +892,18 @@ def test_frontdoor_single_problem_dropin(tmp_path, oracle_mod):
         xo, ro = oracle_mod.solve(lw, n_threads=1)
         assert status == ["OPT_CONVERGED", "OPT_SCO_ITERATION_LIMIT", "OPT_PENALTY_ITERATION_LIMIT"][ro[0].status]
         assert np.abs(x - xo[0]).max() <= TOL_X
-    # log_results: the reference's solver log (writeSolver, optimizers.cpp:533-547), one line per merit
-    # evaluation after the initial one (n_func_evals counts that one too, optimizers.cpp:765-766)
-    p = subprocess.run([str(exe), "--log", str(tmp_path), str(f)], capture_output=True, text=True, timeout=120)
+    # log_results observes the iterations, so the problem takes the host loop (device-evaluated
+    # CartPose terms, GpuModel QPs), which writes the reference's four CSV logs: the solver log
+    # (writeSolver, optimizers.cpp:533-547) has one line per merit evaluation after the initial
+    # one (n_func_evals counts that one too, optimizers.cpp:765-766)
+    p = subprocess.run([str(exe), "--log", str(tmp_path), str(f)], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr
     fevals = int(p.stdout.split()[7])
     log = (tmp_path / "trajopt_solver.log").read_text().splitlines()
     assert log[0] == "DESCRIPTION,oldexact,new_exact,dapprox,dexact,ratio"
     assert len(log) == 1 + (fevals - 1) and all(ln.startswith("Solver,") and len(ln.split(",")) == 6 for ln in log[1:])
+    for name in ("trajopt_vars.log", "trajopt_costs.log", "trajopt_constraints.log"):
+        assert len((tmp_path / name).read_text().splitlines()) >= fevals - 1
 
 
 def test_contact_capacity_overflow_fails_loudly():

@@ -1,0 +1,230 @@
+"""GPU tests of the drop-in boundary beyond the batched kernel: problems the
+fused kernel does not lower run sco::BasicTrustRegionSQP's host loop, with the
+CartPose and collision terms evaluated on the device (thip_eval_*,
+csrc/term_eval.hip) and every QP on the GPU (GpuModel).
+
+* the device term evaluation against the oracle: CartPose error / jacobian
+  (every evaluator form of the batched kernel's workloads) and collision rows
+  of every evaluator type, also for a second collision term;
+* the reference's own configs run unchanged through ConstructProblem ->
+  BasicTrustRegionSQP (tests/golden/json): numerical_ik1.json with
+  numerical_ik_unit.cpp's EXPECT, simple_collision_test.json with
+  simple_collision_unit.cpp's EXPECTs, each with oracle parity;
+* mixed problems (CartPose + JointAcc, collision + JointJerk, CartPose + a user
+  sco::CostFromFunc) with oracle parity;
+* a lowerable problem observed by a callback runs the host loop (callbacks at
+  every SQP iteration, optimizers.cpp:754) with the same result as the oracle.
+"""
+import ctypes as C
+import json
+
+import numpy as np
+import pytest
+
+import dropin_cases as dc
+from parity import TOL_X, check_parity
+from trajopt_amd import abi, host, problems
+from trajopt_amd.runtime import TermEvaluator
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def hip():
+    lib = abi.load_hip()
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need an AMD GPU"
+    host.load_host()
+    return lib
+
+
+# ------------------------------------------------------------------ term evaluation
+@pytest.mark.parametrize("cfg", ["A", "B", "B-tol", "B-dyn"])
+def test_eval_cart_pose_parity(oracle_mod, cfg):
+    """thip_eval_cart_pose (one wave per problem, lane p+1 the FK perturbed in dof
+    p) against the oracle's CartPoseCalc at perturbed trajectories: error to
+    1e-12, forward-difference jacobian to 1e-9 (an FD quotient over eps 1e-5),
+    for plain, toleranced and DynamicCartPose terms."""
+    wl = problems.make_workload(cfg[0], 8)
+    if cfg.endswith("tol"):
+        wl = problems.with_cart_tolerances(wl, pos=0.02, rot=0.1)
+    if cfg.endswith("dyn"):
+        wl = problems.with_dynamic_target(wl)
+    x = wl.init + 0.05 * np.random.default_rng(3).standard_normal(wl.init.shape)
+    err_o, jac_o = oracle_mod.linearize(wl, x)
+    ev = TermEvaluator(wl)
+    for k in range(wl.desc.n_cart):
+        t = wl.desc.cart_step[k]
+        err, jac = ev.cart_pose(k, x[:, t, :])
+        cf = list(wl.desc.cart_pos_coeffs[k]) + list(wl.desc.cart_rot_coeffs[k])
+        idx = [i for i in range(6) if abs(cf[i]) > 1e-5]
+        np.testing.assert_allclose(err[:, idx], err_o[:, k, : len(idx)], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(jac[:, idx], jac_o[:, k, : len(idx)], rtol=0, atol=1e-9)
+    ev.close()
+
+
+def _check_rows(rg, rc, label):
+    assert rg.shape == rc.shape, f"{label}: {len(rg)} contact rows vs {len(rc)}"
+    if len(rc) == 0:
+        return
+    np.testing.assert_array_equal(rg[:, [0, 1, 2, 3, 4, 7]], rc[:, [0, 1, 2, 3, 4, 7]], err_msg=label)
+    np.testing.assert_allclose(rg[:, 5], rc[:, 5], rtol=0, atol=1e-12, err_msg=label)
+    np.testing.assert_allclose(rg[:, 6], rc[:, 6], rtol=0, atol=1e-12, err_msg=label)
+    np.testing.assert_allclose(rg[:, 8:], rc[:, 8:], rtol=0, atol=1e-11, err_msg=label)
+
+
+@pytest.mark.parametrize("cont", [0, 1, 2])
+def test_eval_collision_rows_parity(oracle_mod, cont):
+    """thip_eval_collision (one workgroup per unit, ballot-ranked candidates in
+    ContactResultMap order) against the oracle's collision rows for LVS_DISCRETE,
+    LVS_CONTINUOUS and DISCRETE, at the initial and a perturbed trajectory, and
+    against the fused kernel's own rows (thip_collision_rows)."""
+    from trajopt_amd.runtime import BatchTrustRegionSQP
+
+    wl = problems.make_workload("C", 8)
+    wl.desc.coll_continuous = cont
+    x1 = wl.init + 0.03 * np.random.default_rng(5).standard_normal(wl.init.shape)
+    ev = TermEvaluator(wl)
+    s = BatchTrustRegionSQP(wl)
+    total = 0
+    for x in (wl.init, x1):
+        rows = ev.collision(0, x)
+        fused = s.collision_rows(x)
+        for b in range(wl.batch):
+            ref = oracle_mod.collision_rows(wl, b, x[b])
+            total += len(ref)
+            _check_rows(rows[b], ref, f"cont {cont} problem {b}")
+            _check_rows(rows[b], fused[b], f"cont {cont} problem {b} vs fused")
+    s.close()
+    ev.close()
+    assert total > 40
+
+
+def test_eval_second_collision_term(oracle_mod):
+    """A second collision term (coll_extra: another evaluator, margin and steps)
+    evaluates as its own term, matching the oracle's rows for that term."""
+    wl = problems.make_workload("C", 4)
+    d = wl.desc
+    d.n_coll_extra = 1
+    x = d.coll_extra[0]
+    x.is_cnt, x.first_step, x.last_step, x.n_fixed = 1, 2, wl.n_steps - 3, 1
+    x.fixed_steps[0] = 5
+    x.margin, x.coeff, x.buffer, x.lvs, x.continuous = 0.04, 3.0, 0.2, 0.1, 2
+    ev = TermEvaluator(wl)
+    for term in (0, 1):
+        rows = ev.collision(term, wl.init)
+        for b in range(wl.batch):
+            _check_rows(rows[b], oracle_mod.collision_rows(wl, b, wl.init[b], term=term), f"term {term} problem {b}")
+    ev.close()
+
+
+# ------------------------------------------------------------------ the reference's configs, unchanged
+def test_numerical_ik1_dropin(oracle_mod):
+    """numerical_ik1.json through ConstructProblem -> BasicTrustRegionSQP
+    (numerical_ik_unit.cpp:61-125): one waypoint, so the host loop runs it with
+    the CartPose constraint's FK and FD jacobian on the device; the final
+    l_gripper_tool_frame pose is within 1e-3 of the goal (the reference's
+    EXPECT_NEAR), and the result has oracle parity."""
+    text = dc.text("numerical_ik1.json")
+    x, res, native = host.solve_json(text)
+    assert not native
+    wl = dc.json_workload(text, host)
+    print(f"numerical_ik1: status {res.status}, pose error {dc.ik_pose_error(wl.desc, x, oracle_mod):.2e}")
+    assert res.status == 0
+    assert dc.ik_pose_error(wl.desc, x, oracle_mod) < 1e-3
+    check_parity(wl, oracle_mod, x[None], [res], label="dropin-numerical_ik1", min_strict=0.0)
+
+
+def test_simple_collision_dropin(oracle_mod):
+    """simple_collision_test.json (simple_collision_unit.cpp:62-126): spherebot,
+    one waypoint, a DISCRETE collision cost and a DISCRETE collision constraint
+    in one problem -- the initial state is in collision, the final one
+    collision-free under the 0.2 m contact margin -- and oracle parity."""
+    text = dc.text("simple_collision_test.json")
+    wl = dc.json_workload(text, host)
+    assert dc.spherebot_min_distance(wl.init[0, 0], wl.scene[0]) < 0.2  # EXPECT_TRUE(found)
+    x, res, native = host.solve_json(text)
+    assert not native
+    dmin = dc.spherebot_min_distance(x[0], wl.scene[0])
+    print(f"simple_collision: status {res.status}, x {x[0]}, min distance {dmin:.6f}")
+    assert dmin >= 0.2  # EXPECT_FALSE(found)
+    check_parity(wl, oracle_mod, x[None], [res], label="dropin-simple_collision", min_strict=0.0)
+
+
+# ------------------------------------------------------------------ mixed problems
+def test_cartpose_with_jointacc(oracle_mod):
+    text = dc.cartpose_jointacc()
+    x, res, native = host.solve_json(text)
+    assert not native and res.status in (0, 1)
+    check_parity(dc.json_workload(text, host), oracle_mod, x[None], [res], label="dropin-cart+acc", min_strict=0.0)
+
+
+@pytest.mark.parametrize("evaluator", [1, 2, 4])
+def test_collision_with_jointjerk(oracle_mod, evaluator):
+    text = dc.collision_jointjerk(evaluator)
+    scene = dc.table_scene()
+    x, res, native = host.solve_json(text, scene=scene)
+    assert not native
+    from trajopt_amd.problems import Workload
+
+    desc, init, tgt, jpt, sc = host.lower_json(text, scene=scene, with_scene=True)
+    wl = Workload("json", desc, init[None].copy(), tgt[None].copy(), sc[None].copy(), init[None].copy(),
+                  jpt[None].copy() if desc.n_jpos else None)
+    check_parity(wl, oracle_mod, x[None], [res], label=f"dropin-coll{evaluator}+jerk", min_strict=0.0)
+
+
+def test_cartpose_with_user_cost(oracle_mod):
+    """A caller's sco::CostFromFunc appended to a constructed TrajOptProb next to
+    the built-in CartPose terms (host/tests/sco_cases.cpp sco_case_user_cost):
+    the host loop with the device-evaluated CartPose terms, against the oracle
+    with the same user cost (oracle_solve_user_cost)."""
+    wl = problems.make_workload("A", 3)
+    L = C.CDLL(str(abi.LIB_DIR / "libsco_cases.so"))
+    L.sco_case_user_cost.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_double), C.POINTER(abi.Result), C.c_char_p,
+                                     C.c_int]
+    OL = oracle_mod.lib()
+    OL.oracle_solve_user_cost.argtypes = [C.POINTER(abi.ProblemDesc)] + [C.POINTER(C.c_double)] * 5 + \
+        [C.POINTER(abi.Result)]
+    dp = lambda a: None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    for b in range(wl.batch):
+        text = host.workload_to_json(wl, b)
+        x = np.zeros((wl.n_steps, wl.n_dof))
+        res = abi.Result()
+        err = C.create_string_buffer(2048)
+        assert L.sco_case_user_cost(text.encode(), 0, dp(x), C.byref(res), err, 2048) == 0, err.value.decode()
+        lw = dc.json_workload(text, host)
+        xo = np.zeros_like(x)
+        ro = abi.Result()
+        jt = None if lw.jpos_targets is None else np.ascontiguousarray(lw.jpos_targets[0])
+        assert OL.oracle_solve_user_cost(C.byref(lw.desc), dp(np.ascontiguousarray(lw.init[0])),
+                                         dp(np.ascontiguousarray(lw.targets[0])), None, dp(jt), dp(xo),
+                                         C.byref(ro)) == 0
+        print(f"user cost problem {b}: status {res.status} vs {ro.status}, |dx| {np.abs(x - xo).max():.2e}")
+        assert res.status == ro.status
+        assert np.abs(x - xo).max() <= TOL_X
+
+
+def test_callback_runs_the_host_loop(oracle_mod, tmp_path):
+    """sco::BasicTrustRegionSQP with a callback on a lowerable problem calls it at
+    every SQP iteration (optimizers.cpp:754), as the reference does: the problem
+    takes the host loop (device-evaluated CartPose terms, GpuModel QPs), writes
+    all four CSV logs with log_results, and meets the oracle's result."""
+    wl = problems.make_workload("A", 2)
+    exe = abi.LIB_DIR / "sqp_single"
+    import subprocess
+
+    for b in range(2):
+        f = tmp_path / f"p{b}.json"
+        f.write_text(host.workload_to_json(wl, b))
+        p = subprocess.run([str(exe), "--callback", str(f)], capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr
+        lines = p.stdout.strip().splitlines()
+        head = lines[0].split()
+        status, n_sqp, n_calls = head[1], int(head[3]), int(head[-1])
+        x = np.array([[float(v) for v in ln.split()] for ln in lines[1:]])
+        lw = dc.json_workload(f.read_text(), host)
+        xo, ro = oracle_mod.solve(lw, n_threads=1)
+        assert status == ["OPT_CONVERGED", "OPT_SCO_ITERATION_LIMIT", "OPT_PENALTY_ITERATION_LIMIT"][ro[0].status]
+        assert np.abs(x - xo[0]).max() <= TOL_X
+        assert n_calls == n_sqp + 1, (n_calls, n_sqp)  # one per SQP iteration, one at the end

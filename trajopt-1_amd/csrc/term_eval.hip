@@ -1,0 +1,817 @@
+// Device evaluation of the kinematic terms for the host SQP loop (the generic
+// path): CartPose error + forward-difference jacobian and the collision
+// contacts of one collision term with their linearised distance expressions,
+// for problems the fused sqp_kernel does not lower (single-waypoint problems,
+// several collision terms, CartPose / collision next to JointAcc / JointJerk /
+// time terms or a user sco::Cost).  include/trajopt_hip.h thip_eval_*.
+//
+//   cart_eval_kernel   CartPoseErrCalculator / CartPoseJacCalculator and the
+//                      DynamicCartPose pair (trajopt/src/kinematic_terms.cpp:58-370):
+//                      one wave per problem, lane 0 the unperturbed pose, lane
+//                      p + 1 the FK perturbed in dof p (the arithmetic of
+//                      sqp_kernel.hip linearize()).
+//   coll_eval_kernel   CollisionEvaluator::CalcCollisions + GetGradient +
+//                      CalcDistExpressions* for one unit (a free waypoint for
+//                      DISCRETE, SingleTimestepCollisionEvaluator
+//                      collision_terms.cpp:538-554,646-688; a step pair for
+//                      LVS_DISCRETE :817-898 and LVS_CONTINUOUS :1065-1161;
+//                      gradient :195-242; expressions :341-386, 463-536): one
+//                      256-thread workgroup per (unit, problem) walks the
+//                      (sphere, primitive, sub-state) candidates in the
+//                      flattened ContactResultMap order (robot link, primitive,
+//                      then insertion order sub-state, sphere), 256 at a time;
+//                      a ballot + cross-wave prefix gives each contact its rank,
+//                      so the list comes out ordered without a sort.  The
+//                      arithmetic is oracle/src/collision.cpp's.
+//   coll_pack_kernel   concatenates the units' records per problem.
+// fp64 throughout; integer/geometry work, no MFMA.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "collision_device.hpp"
+#include "kin_device.hpp"
+
+namespace thip
+{
+namespace ev
+{
+constexpr int kEvBlock = 256;
+constexpr int kEvWaves = kEvBlock / 64;
+
+// one collision term as the kernels read it
+struct CollTerm
+{
+  int single;      // DISCRETE: one state per unit
+  int continuous;  // LVS_CONTINUOUS: casts between consecutive sub-states
+  double margin, buffer, lvs;
+};
+
+// per-term unit table: unit u covers waypoint t0 (and t0 + 1 unless single);
+// f0 / f1: the ends that are fixed steps of the term
+struct Unit
+{
+  int t0, f0, f1;
+};
+
+// the robot spheres grouped by link, ascending (ContactResultMap key order)
+struct Spheres
+{
+  int n_groups;
+  int grp_link[THIP_MAX_SPHERES];
+  int grp_s0[THIP_MAX_SPHERES];
+  int grp_ns[THIP_MAX_SPHERES];
+  int sph_order[THIP_MAX_SPHERES];
+  double center[THIP_MAX_SPHERES][3];
+  double radius[THIP_MAX_SPHERES];
+  int link[THIP_MAX_SPHERES];
+};
+
+__shared__ thip_chain s_chain;
+
+__device__ __forceinline__ void stage_chain_ev(const thip_chain* ch)
+{
+  const int* src = reinterpret_cast<const int*>(ch);
+  int* dst = reinterpret_cast<int*>(&s_chain);
+  for (int w = threadIdx.x; w < static_cast<int>(sizeof(thip_chain) / 4); w += blockDim.x)
+    dst[w] = src[w];
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------ CartPose
+struct CartArgs
+{
+  int D;
+  int source_link, target_link, has_tol;
+  double source_offset[12];
+  double lower_tol[6], upper_tol[6];
+};
+
+__global__ __launch_bounds__(64) void cart_eval_kernel(const thip_chain* chain, CartArgs a, int batch, int n_cart,
+                                                      int term, const double* q, const double* tgt, double* err,
+                                                      double* jac)
+{
+  const int b = blockIdx.x;
+  if (b >= batch)
+    return;
+  stage_chain_ev(chain);
+  const thip_chain& ch = s_chain;
+  const int D = a.D, lane = threadIdx.x;
+  __shared__ Pose s_src, s_tinv;
+  const double* qb = q + static_cast<long long>(b) * D;
+  const double* to12 = tgt + (static_cast<long long>(b) * n_cart + term) * 12;
+  if (lane == 0)
+  {
+    Pose S, So, Ss, Tb, To, Tt, Ti;
+    chain_fk(ch, qb, a.source_link, S);
+    pose_load(So, a.source_offset);
+    pose_mul(S, So, Ss);
+    pose_load(To, to12);
+    if (a.target_link > 0)
+      chain_fk(ch, qb, a.target_link, Tb);  // DynamicCartPose: the active target link
+    else
+      pose_load(Tb, ch.base_pose);
+    pose_mul(Tb, To, Tt);
+    pose_inv(Tt, Ti);
+    double e[6];
+    transform_error(Ti, Ss, e);
+    if (a.has_tol)
+      apply_tolerances(e, a.lower_tol, a.upper_tol);
+    for (int i = 0; i < 6; ++i)
+      err[static_cast<long long>(b) * 6 + i] = e[i];
+    s_src = Ss;
+    s_tinv = Ti;
+  }
+  __syncthreads();
+  if (!jac || lane < 1 || lane > D)
+    return;
+  // forward difference in dof p (CartPoseJacCalculator, eps 1e-5)
+  const int p = lane - 1;
+  const double eps = 1e-5;
+  double qp[THIP_MAX_DOF];
+  for (int j = 0; j < D; ++j)
+    qp[j] = qb[j];
+  qp[p] = qp[p] + eps;
+  Pose S, So, Sp;
+  chain_fk(ch, qp, a.source_link, S);
+  pose_load(So, a.source_offset);
+  pose_mul(S, So, Sp);
+  const Pose Ss = s_src, Ti = s_tinv;
+  Pose pe, ppe;
+  pose_mul(Ti, Ss, pe);
+  if (a.target_link > 0)
+  {
+    Pose Tq, To, Tp, Tpi;
+    chain_fk(ch, qp, a.target_link, Tq);
+    pose_load(To, to12);
+    pose_mul(Tq, To, Tp);
+    pose_inv(Tp, Tpi);
+    pose_mul(Tpi, Sp, ppe);
+  }
+  else
+    pose_mul(Ti, Sp, ppe);
+  double diff[6];
+  if (a.has_tol)
+    transform_error_diff_tol(pe, ppe, a.lower_tol, a.upper_tol, diff);
+  else
+  {
+    double r0[3], r1[3];
+    for (int i = 0; i < 3; ++i)
+      diff[i] = ppe.t[i] - pe.t[i];
+    rot_error(pe.r, r0, true);
+    rot_error(ppe.r, r1, true);
+    for (int i = 0; i < 3; ++i)
+      diff[3 + i] = r1[i] - r0[i];
+  }
+  double* jo = jac + static_cast<long long>(b) * 6 * D;
+  for (int i = 0; i < 6; ++i)
+    jo[i * D + p] = diff[i] / eps;
+}
+
+// ------------------------------------------------------------------ collision
+constexpr int kCCNone = 0, kCCTime0 = 1, kCCTime1 = 2, kCCBetween = 3;
+
+__device__ __forceinline__ void sphere_world(const Pose& T, const double* cl, double* c)
+{
+  for (int r = 0; r < 3; ++r)
+    c[r] = T.r[r * 3 + 0] * cl[0] + T.r[r * 3 + 1] * cl[1] + T.r[r * 3 + 2] * cl[2] + T.t[r];
+}
+
+// CollisionEvaluator::GetGradient for the robot link at the waypoint's own
+// joint values (oracle/src/collision.cpp contactGradient)
+__device__ void contact_gradient(const thip_chain& ch, const double* dof, int link, const Pose& lt,
+                                 const double* p_local, const double* normal, double* grad)
+{
+  const int D = ch.n_dof;
+  double J[6 * THIP_MAX_DOF];
+  chain_jacobian(ch, dof, link, J);
+  double r[3];
+  for (int i = 0; i < 3; ++i)
+    r[i] = lt.r[i * 3 + 0] * p_local[0] + lt.r[i * 3 + 1] * p_local[1] + lt.r[i * 3 + 2] * p_local[2];
+  for (int j = 0; j < D; ++j)
+  {
+    const double wx = J[3 * D + j], wy = J[4 * D + j], wz = J[5 * D + j];
+    const double l0 = J[0 * D + j] + (wy * r[2] - wz * r[1]);
+    const double l1 = J[1 * D + j] + (wz * r[0] - wx * r[2]);
+    const double l2 = J[2 * D + j] + (wx * r[1] - wy * r[0]);
+    grad[j] = -1.0 * (normal[0] * l0 + normal[1] * l1 + normal[2] * l2);
+  }
+}
+
+// records of unit u of problem b: stage [b][u][ucap][W], counts [b][n_units]
+__global__ __launch_bounds__(kEvBlock) void coll_eval_kernel(const thip_chain* chain, const Spheres* sph, CollTerm tm,
+                                                            const Unit* units, int n_units, int batch, int N,
+                                                            const double* x, const double* scene, int n_prims,
+                                                            double* stage, int ucap, int* counts)
+{
+  const int u = blockIdx.x, b = blockIdx.y;
+  if (u >= n_units || b >= batch)
+    return;
+  stage_chain_ev(chain);
+  const thip_chain& ch = s_chain;
+  const int D = ch.n_dof, W = 8 + 2 * D + 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Unit un = units[u];
+  const double* q0 = x + (static_cast<long long>(b) * N + un.t0) * D;
+  const double* q1 = tm.single ? q0 : q0 + D;
+  const double* prims = scene + static_cast<long long>(b) * (n_prims > 0 ? n_prims : 1) * 16;
+  // sub-states (DiscreteCollisionEvaluator / CastCollisionEvaluator, collision_terms.cpp:846-852)
+  const int cnt = tm.single ? 1 : lvs_count(q0, q1, D, tm.lvs);
+  const int n_sub = tm.single ? 1 : (tm.continuous ? cnt - 1 : cnt);
+  const int last = cnt - 1;
+  const double dt = tm.single ? 0.0 : 1.0 / double(last);
+  const double threshold = tm.margin + tm.buffer;
+  const Spheres& S = *sph;
+  const int n_sph = [&] {
+    int n = 0;
+    for (int g = 0; g < S.n_groups; ++g)
+      n += S.grp_ns[g];
+    return n;
+  }();
+  const long long total = static_cast<long long>(n_sph) * n_prims * n_sub;
+  __shared__ int s_wave_cnt[kEvWaves];
+  __shared__ int s_base;
+  if (tid == 0)
+    s_base = 0;
+  __syncthreads();
+  double* out = stage + (static_cast<long long>(b) * n_units + u) * ucap * W;
+  for (long long c0 = 0; c0 < total; c0 += kEvBlock)
+  {
+    const long long cidx = c0 + tid;
+    bool hit = false;
+    int link = 0, p = 0, s = 0, i = 0, cc_type = kCCNone;
+    double dist = 0, normal[3] = { 0, 0, 0 }, p_robot[3] = { 0, 0, 0 }, cc_time = 0;
+    Pose Ta, Tb;
+    if (cidx < total)
+    {
+      // decode (group, primitive, sub-state, sphere of the group) in map order
+      long long r = cidx;
+      int g = 0;
+      for (; g < S.n_groups; ++g)
+      {
+        const long long sz = static_cast<long long>(S.grp_ns[g]) * n_prims * n_sub;
+        if (r < sz)
+          break;
+        r -= sz;
+      }
+      const int ng = S.grp_ns[g];
+      p = static_cast<int>(r / (static_cast<long long>(n_sub) * ng));
+      const int r2 = static_cast<int>(r % (static_cast<long long>(n_sub) * ng));
+      i = r2 / ng;
+      s = S.sph_order[S.grp_s0[g] + r2 % ng];
+      link = S.grp_link[g];
+      double qa[THIP_MAX_DOF];
+      for (int j = 0; j < D; ++j)
+        qa[j] = tm.single ? q0[j] : linspaced(cnt, q0[j], q1[j], i);
+      chain_fk(ch, qa, link, Ta);
+      double ca[3];
+      sphere_world(Ta, S.center[s], ca);
+      const double* prim = prims + 16 * p;
+      if (tm.continuous)
+      {
+        double qb[THIP_MAX_DOF];
+        for (int j = 0; j < D; ++j)
+          qb[j] = linspaced(cnt, q0[j], q1[j], i + 1);
+        chain_fk(ch, qb, link, Tb);
+        double cb[3], ts = 0;
+        sphere_world(Tb, S.center[s], cb);
+        swept_sphere_prim_distance(ca, cb, S.radius[s], prim, dist, normal, p_robot, ts);
+        cc_time = (double(i) + ts) * dt;
+        cc_type = (i == 0 && ts == 0.0) ? kCCTime0 : ((i + 1 == last && ts == 1.0) ? kCCTime1 : kCCBetween);
+      }
+      else
+      {
+        Tb = Ta;
+        sphere_prim_distance(ca, S.radius[s], prim, dist, normal, p_robot);
+        if (!tm.single)
+        {
+          cc_time = double(i) * dt;
+          cc_type = (i == 0) ? kCCTime0 : ((i == last) ? kCCTime1 : kCCBetween);
+        }
+      }
+      hit = (dist < threshold) && !(dist > tm.margin + tm.buffer);
+      if (hit && (un.f0 || un.f1))
+        hit = (un.f0 && cc_type != kCCNone && cc_type != kCCTime0) ||
+              (un.f1 && cc_type != kCCNone && cc_type != kCCTime1);
+    }
+    const unsigned long long m = __ballot(hit);
+    const int lrank = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0)
+      s_wave_cnt[wave] = __popcll(m);
+    __syncthreads();
+    int rank = s_base + lrank;
+    for (int w = 0; w < wave; ++w)
+      rank += s_wave_cnt[w];
+    if (hit && rank < ucap)
+    {
+      // nearest_points_local[0]: the robot point in the link frame of transform
+      double pl[3];
+      const double w3[3] = { p_robot[0] - Ta.t[0], p_robot[1] - Ta.t[1], p_robot[2] - Ta.t[2] };
+      for (int k = 0; k < 3; ++k)
+        pl[k] = Ta.r[0 * 3 + k] * w3[0] + Ta.r[1 * 3 + k] * w3[1] + Ta.r[2 * 3 + k] * w3[2];
+      double* rec = out + static_cast<long long>(rank) * W;
+      double a0[THIP_MAX_DOF], a1[THIP_MAX_DOF];
+      double cst;
+      if (tm.single)
+      {
+        // CalcDistExpressionsSingleTimeStep: 0 + g.x - g.q, then + d (scale 1, CCType_None)
+        double g[THIP_MAX_DOF], gd = 0;
+        contact_gradient(ch, q0, link, Ta, pl, normal, g);
+        for (int j = 0; j < D; ++j)
+        {
+          a0[j] = 1.0 * g[j];
+          gd += g[j] * q0[j];
+          a1[j] = 0.0;
+        }
+        cst = 0.0;
+        cst += 1.0 * -gd;
+        cst += dist;
+      }
+      else
+      {
+        cst = dist;
+        for (int j = 0; j < D; ++j)
+          a0[j] = a1[j] = 0.0;
+        if (!un.f0)
+        {
+          double g[THIP_MAX_DOF], gd = 0;
+          contact_gradient(ch, q0, link, Ta, pl, normal, g);
+          const double sc = 1 - cc_time;
+          for (int j = 0; j < D; ++j)
+          {
+            a0[j] = sc * g[j];
+            gd += g[j] * q0[j];
+          }
+          cst += sc * -gd;
+        }
+        if (!un.f1)
+        {
+          double g[THIP_MAX_DOF], gd = 0;
+          contact_gradient(ch, q1, link, Tb, pl, normal, g);
+          const double sc = cc_time;
+          for (int j = 0; j < D; ++j)
+          {
+            a1[j] = sc * g[j];
+            gd += g[j] * q1[j];
+          }
+          cst += sc * -gd;
+        }
+      }
+      int kept = 0;
+      for (int j = 0; j < D; ++j)
+      {
+        if (fabs(a0[j]) > 1e-7)
+          ++kept;
+        else
+          a0[j] = 0;
+        if (fabs(a1[j]) > 1e-7)
+          ++kept;
+        else
+          a1[j] = 0;
+      }
+      rec[0] = un.t0;
+      rec[1] = link;
+      rec[2] = p;
+      rec[3] = s;
+      rec[4] = tm.single ? 0 : i;
+      rec[5] = dist;
+      rec[6] = cc_time;
+      rec[7] = kept;
+      for (int j = 0; j < D; ++j)
+      {
+        rec[8 + j] = a0[j];
+        rec[8 + D + j] = a1[j];
+      }
+      rec[8 + 2 * D] = cst;
+    }
+    __syncthreads();
+    if (tid == 0)
+    {
+      int t = 0;
+      for (int w = 0; w < kEvWaves; ++w)
+        t += s_wave_cnt[w];
+      s_base += t;
+    }
+    __syncthreads();
+  }
+  if (tid == 0)
+    counts[b * n_units + u] = s_base;
+}
+
+// per problem: the units' records in unit order into out [b][cap][W]
+__global__ __launch_bounds__(kEvBlock) void coll_pack_kernel(const double* stage, const int* ucounts, int n_units,
+                                                            int ucap, int W, double* out, int cap, int* counts)
+{
+  const int b = blockIdx.x;
+  int off = 0;
+  for (int u = 0; u < n_units; ++u)
+  {
+    const int n = min(ucounts[b * n_units + u], ucap);
+    const double* src = stage + (static_cast<long long>(b) * n_units + u) * ucap * W;
+    for (int e = threadIdx.x; e < n * W; e += kEvBlock)
+    {
+      const int r = off + e / W;
+      if (r < cap)
+        out[(static_cast<long long>(b) * cap + r) * W + e % W] = src[e];
+    }
+    off += ucounts[b * n_units + u];
+  }
+  if (threadIdx.x == 0)
+    counts[b] = off;
+}
+}  // namespace ev
+}  // namespace thip
+
+using namespace thip::ev;
+
+struct thip_eval
+{
+  int device = 0, batch = 0;
+  thip_problem_desc desc{};
+  thip_chain* d_chain = nullptr;
+  Spheres* d_sph = nullptr;
+  double* d_tgt = nullptr;
+  double* d_scene = nullptr;
+  double* d_x = nullptr;      // q / x staging
+  double* d_err = nullptr;
+  double* d_jac = nullptr;
+  double* d_stage = nullptr;  // collision records per unit
+  double* d_out = nullptr;    // packed records
+  int* d_counts = nullptr;    // per unit, then per problem
+  Unit* d_units = nullptr;
+  size_t stage_doubles = 0, out_doubles = 0;
+  int ucap = 64;              // records per unit (grows when a unit has more)
+  // per collision term: its unit table (offset into d_units) and kernel parameters
+  std::vector<int> unit_off, unit_n;
+  std::vector<CollTerm> terms;
+  int max_units = 0;
+  hipStream_t stream = nullptr;
+  bool uploaded = false;
+  std::string err;
+};
+
+static thread_local std::string g_eval_create_err;
+
+namespace
+{
+int fail(thip_eval* ev, const std::string& m)
+{
+  ev->err = m;
+  return THIP_E_INVALID;
+}
+int hipfail(thip_eval* ev, const char* what, hipError_t e)
+{
+  ev->err = std::string(what) + ": " + hipGetErrorString(e);
+  return THIP_E_HIP;
+}
+
+// the units of a collision term: free waypoints of [first, last] (DISCRETE) or step
+// pairs (problem_description.cpp:1735-1858)
+bool term_units(int N, int first, int last, int n_fixed, const int* fixed_steps, int cont, std::vector<Unit>& out,
+                std::string& why)
+{
+  if (last < 0)
+    last = N - 1;
+  if (first < 0 || first >= N || last < first || last >= N)
+    return why = "collision: bad first/last step", false;
+  auto fixed = [&](int t) {
+    for (int k = 0; k < n_fixed; ++k)
+      if (fixed_steps[k] == t)
+        return true;
+    return false;
+  };
+  if (cont == 2)
+  {
+    for (int t = first; t <= last; ++t)
+      if (!fixed(t))
+        out.push_back({ t, 0, 0 });
+    return true;
+  }
+  for (int t = first; t < last; ++t)
+  {
+    const bool a = fixed(t), b = fixed(t + 1);
+    if (a && b)
+      return why = "Currently two adjacent fixed steps are not supported in collision term.", false;
+    out.push_back({ t, a ? 1 : 0, b ? 1 : 0 });
+  }
+  return true;
+}
+}  // namespace
+
+extern "C" {
+
+int thip_eval_create(int device, const thip_problem_desc* desc, int batch, thip_eval** out)
+{
+  if (!desc || !out || batch <= 0)
+  {
+    g_eval_create_err = "thip_eval_create: null argument or batch <= 0";
+    return THIP_E_INVALID;
+  }
+  auto reject = [](const std::string& m) {
+    g_eval_create_err = "thip_eval_create: " + m;
+    return THIP_E_INVALID;
+  };
+  if (desc->abi_version != THIP_ABI_VERSION)
+    return reject("descriptor abi_version " + std::to_string(desc->abi_version) + " != THIP_ABI_VERSION " +
+                  std::to_string(THIP_ABI_VERSION));
+  const thip_chain& ch = desc->chain;
+  const int N = desc->n_steps;
+  if (ch.n_dof <= 0 || ch.n_dof > THIP_MAX_DOF || ch.n_links < 1 || ch.n_links > THIP_MAX_LINKS)
+    return reject("chain out of range");
+  if (N < 1 || N > THIP_MAX_STEPS)
+    return reject("n_steps out of range");
+  for (int k = 1; k < ch.n_links; ++k)
+    if ((ch.joint_type[k] < 0 || ch.joint_type[k] > 3) ||
+        (ch.joint_type[k] != THIP_JOINT_FIXED && (ch.joint_dof[k] < 0 || ch.joint_dof[k] >= ch.n_dof)) ||
+        (ch.is_tree && (ch.parent[k] < 0 || ch.parent[k] >= k)))
+      return reject("bad chain joint / parent table");
+  if (desc->n_cart < 0 || desc->n_cart > THIP_MAX_CART)
+    return reject("n_cart out of range");
+  for (int k = 0; k < desc->n_cart; ++k)
+    if (desc->cart_step[k] < 0 || desc->cart_step[k] >= N || desc->cart_source_link[k] <= 0 ||
+        desc->cart_source_link[k] >= ch.n_links || desc->cart_target_link[k] < 0 ||
+        desc->cart_target_link[k] >= ch.n_links)
+      return reject("bad CartPose term");
+  if (desc->n_coll_extra < 0 || desc->n_coll_extra > THIP_MAX_COLL_EXTRA)
+    return reject("n_coll_extra out of range");
+  if ((desc->coll_enabled || desc->n_coll_extra > 0) &&
+      (desc->n_spheres < 1 || desc->n_spheres > THIP_MAX_SPHERES || desc->n_prims < 0 ||
+       desc->n_prims > THIP_MAX_PRIMS))
+    return reject("collision: spheres / primitives out of range");
+  for (int s = 0; s < (desc->coll_enabled || desc->n_coll_extra > 0 ? desc->n_spheres : 0); ++s)
+    if (desc->sphere_link[s] < 1 || desc->sphere_link[s] >= ch.n_links || !(desc->sphere_radius[s] >= 0))
+      return reject("collision: bad robot sphere");
+
+  auto* ev = new thip_eval();
+  ev->device = device;
+  ev->batch = batch;
+  ev->desc = *desc;
+  if (!ev->desc.chain.is_tree)
+    for (int k = 0; k < THIP_MAX_LINKS; ++k)
+      ev->desc.chain.parent[k] = k > 0 ? k - 1 : 0;
+  const thip_problem_desc& d = ev->desc;
+  // collision terms: 0 = coll_*, k = coll_extra[k - 1]
+  std::vector<Unit> units;
+  const int n_terms = (d.coll_enabled ? 1 : 0) + d.n_coll_extra;
+  for (int k = 0; k < n_terms; ++k)
+  {
+    const bool main = d.coll_enabled && k == 0;
+    const thip_coll_term* x = main ? nullptr : &d.coll_extra[k - (d.coll_enabled ? 1 : 0)];
+    CollTerm tm;
+    const int cont = main ? d.coll_continuous : x->continuous;
+    tm.single = cont == 2;
+    tm.continuous = cont == 1;
+    tm.margin = main ? d.coll_margin : x->margin;
+    tm.buffer = main ? d.coll_buffer : x->buffer;
+    tm.lvs = main ? d.coll_lvs : x->lvs;
+    const int nf = main ? d.coll_n_fixed : x->n_fixed;
+    if (cont < 0 || cont > 2 || nf < 0 || nf > THIP_MAX_STEPS || (!tm.single && !(tm.lvs > 0)) || !(tm.buffer >= 0))
+    {
+      delete ev;
+      return reject("collision term " + std::to_string(k) + ": bad evaluator / lvs / buffer / fixed steps");
+    }
+    std::string why;
+    ev->unit_off.push_back(static_cast<int>(units.size()));
+    if (!term_units(N, main ? d.coll_first_step : x->first_step, main ? d.coll_last_step : x->last_step, nf,
+                    main ? d.coll_fixed_steps : x->fixed_steps, cont, units, why))
+    {
+      delete ev;
+      return reject(why);
+    }
+    ev->unit_n.push_back(static_cast<int>(units.size()) - ev->unit_off.back());
+    ev->max_units = std::max(ev->max_units, ev->unit_n.back());
+    ev->terms.push_back(tm);
+  }
+  Spheres sp{};
+  if (n_terms > 0)
+  {
+    std::vector<int> order;
+    for (int s = 0; s < d.n_spheres; ++s)
+      order.push_back(s);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return d.sphere_link[a] < d.sphere_link[b]; });
+    for (size_t k = 0; k < order.size(); ++k)
+    {
+      sp.sph_order[k] = order[k];
+      const int link = d.sphere_link[order[k]];
+      if (sp.n_groups == 0 || sp.grp_link[sp.n_groups - 1] != link)
+      {
+        sp.grp_link[sp.n_groups] = link;
+        sp.grp_s0[sp.n_groups] = static_cast<int>(k);
+        sp.grp_ns[sp.n_groups] = 0;
+        sp.n_groups++;
+      }
+      sp.grp_ns[sp.n_groups - 1]++;
+    }
+    for (int s = 0; s < d.n_spheres; ++s)
+    {
+      sp.link[s] = d.sphere_link[s];
+      sp.radius[s] = d.sphere_radius[s];
+      for (int i = 0; i < 3; ++i)
+        sp.center[s][i] = d.sphere_center[s][i];
+    }
+  }
+  auto hfail = [&](const char* what, hipError_t e) {
+    g_eval_create_err = std::string("thip_eval_create: ") + what + ": " + hipGetErrorString(e);
+    thip_eval_destroy(ev);
+    return THIP_E_HIP;
+  };
+  hipError_t e;
+  if ((e = hipSetDevice(device)) != hipSuccess)
+    return hfail("hipSetDevice", e);
+  const size_t B = static_cast<size_t>(batch), D = static_cast<size_t>(d.chain.n_dof);
+  const size_t nc = static_cast<size_t>(std::max(d.n_cart, 1)), np = static_cast<size_t>(std::max(d.n_prims, 1));
+  if ((e = hipMalloc(&ev->d_chain, sizeof(thip_chain))) != hipSuccess ||
+      (e = hipMalloc(&ev->d_sph, sizeof(Spheres))) != hipSuccess ||
+      (e = hipMalloc(&ev->d_tgt, B * nc * 12 * sizeof(double))) != hipSuccess ||
+      (e = hipMalloc(&ev->d_scene, B * np * 16 * sizeof(double))) != hipSuccess ||
+      (e = hipMalloc(&ev->d_x, B * static_cast<size_t>(N) * D * sizeof(double))) != hipSuccess ||
+      (e = hipMalloc(&ev->d_err, B * 6 * sizeof(double))) != hipSuccess ||
+      (e = hipMalloc(&ev->d_jac, B * 6 * D * sizeof(double))) != hipSuccess ||
+      (e = hipMalloc(&ev->d_counts, (B * static_cast<size_t>(std::max(ev->max_units, 1)) + B) * sizeof(int))) !=
+          hipSuccess ||
+      (e = hipMalloc(&ev->d_units, std::max<size_t>(units.size(), 1) * sizeof(Unit))) != hipSuccess)
+    return hfail("hipMalloc", e);
+  if ((e = hipStreamCreateWithFlags(&ev->stream, hipStreamNonBlocking)) != hipSuccess)
+    return hfail("hipStreamCreate", e);
+  if ((e = hipMemcpyAsync(ev->d_chain, &d.chain, sizeof(thip_chain), hipMemcpyHostToDevice, ev->stream)) !=
+          hipSuccess ||
+      (e = hipMemcpyAsync(ev->d_sph, &sp, sizeof(Spheres), hipMemcpyHostToDevice, ev->stream)) != hipSuccess ||
+      (!units.empty() && (e = hipMemcpyAsync(ev->d_units, units.data(), units.size() * sizeof(Unit),
+                                             hipMemcpyHostToDevice, ev->stream)) != hipSuccess) ||
+      (e = hipMemsetAsync(ev->d_tgt, 0, B * nc * 12 * sizeof(double), ev->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(ev->d_scene, 0, B * np * 16 * sizeof(double), ev->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(ev->stream)) != hipSuccess)
+    return hfail("hipMemcpy", e);
+  *out = ev;
+  return THIP_OK;
+}
+
+int thip_eval_upload(thip_eval* ev, const double* cart_targets, const double* scene)
+{
+  if (!ev)
+    return THIP_E_INVALID;
+  const thip_problem_desc& d = ev->desc;
+  const size_t B = static_cast<size_t>(ev->batch);
+  if (d.n_cart > 0 && !cart_targets)
+    return fail(ev, "thip_eval_upload: cart_targets required when n_cart > 0");
+  if ((d.coll_enabled || d.n_coll_extra > 0) && d.n_prims > 0 && !scene)
+    return fail(ev, "thip_eval_upload: scene required with collision terms");
+  hipError_t e;
+  if ((e = hipSetDevice(ev->device)) != hipSuccess)
+    return hipfail(ev, "hipSetDevice", e);
+  if (d.n_cart > 0 &&
+      (e = hipMemcpyAsync(ev->d_tgt, cart_targets, B * static_cast<size_t>(d.n_cart) * 12 * sizeof(double),
+                          hipMemcpyHostToDevice, ev->stream)) != hipSuccess)
+    return hipfail(ev, "hipMemcpy(cart_targets)", e);
+  if (scene && d.n_prims > 0 &&
+      (e = hipMemcpyAsync(ev->d_scene, scene, B * static_cast<size_t>(d.n_prims) * 16 * sizeof(double),
+                          hipMemcpyHostToDevice, ev->stream)) != hipSuccess)
+    return hipfail(ev, "hipMemcpy(scene)", e);
+  if ((e = hipStreamSynchronize(ev->stream)) != hipSuccess)
+    return hipfail(ev, "hipStreamSynchronize", e);
+  ev->uploaded = true;
+  return THIP_OK;
+}
+
+int thip_eval_cart_pose(thip_eval* ev, int term, const double* q, double* err, double* jac)
+{
+  if (!ev)
+    return THIP_E_INVALID;
+  const thip_problem_desc& d = ev->desc;
+  if (term < 0 || term >= d.n_cart)
+    return fail(ev, "thip_eval_cart_pose: term out of range");
+  if (!q || !err)
+    return fail(ev, "thip_eval_cart_pose: null q / err");
+  if (!ev->uploaded)
+    return fail(ev, "thip_eval_cart_pose: thip_eval_upload first");
+  const int D = d.chain.n_dof;
+  CartArgs a{};
+  a.D = D;
+  a.source_link = d.cart_source_link[term];
+  a.target_link = d.cart_target_link[term];
+  a.has_tol = d.cart_has_tol[term];
+  std::memcpy(a.source_offset, d.cart_source_offset[term], sizeof(a.source_offset));
+  std::memcpy(a.lower_tol, d.cart_lower_tol[term], sizeof(a.lower_tol));
+  std::memcpy(a.upper_tol, d.cart_upper_tol[term], sizeof(a.upper_tol));
+  const size_t B = static_cast<size_t>(ev->batch);
+  hipError_t e;
+  if ((e = hipSetDevice(ev->device)) != hipSuccess)
+    return hipfail(ev, "hipSetDevice", e);
+  if ((e = hipMemcpyAsync(ev->d_x, q, B * D * sizeof(double), hipMemcpyHostToDevice, ev->stream)) != hipSuccess)
+    return hipfail(ev, "hipMemcpy(q)", e);
+  hipLaunchKernelGGL(cart_eval_kernel, dim3(ev->batch), dim3(64), 0, ev->stream, ev->d_chain, a, ev->batch, d.n_cart,
+                     term, ev->d_x, ev->d_tgt, ev->d_err, jac ? ev->d_jac : nullptr);
+  if ((e = hipGetLastError()) != hipSuccess)
+    return hipfail(ev, "cart_eval_kernel launch", e);
+  if ((e = hipMemcpyAsync(err, ev->d_err, B * 6 * sizeof(double), hipMemcpyDeviceToHost, ev->stream)) !=
+          hipSuccess ||
+      (jac && (e = hipMemcpyAsync(jac, ev->d_jac, B * 6 * D * sizeof(double), hipMemcpyDeviceToHost, ev->stream)) !=
+                  hipSuccess) ||
+      (e = hipStreamSynchronize(ev->stream)) != hipSuccess)
+    return hipfail(ev, "cart_eval_kernel", e);
+  return THIP_OK;
+}
+
+int thip_eval_collision(thip_eval* ev, int term, const double* x, double* records, int cap, int* counts)
+{
+  if (!ev)
+    return THIP_E_INVALID;
+  const thip_problem_desc& d = ev->desc;
+  if (term < 0 || term >= static_cast<int>(ev->terms.size()))
+    return fail(ev, "thip_eval_collision: term out of range");
+  if (!x || !counts || cap < 0 || (cap > 0 && !records))
+    return fail(ev, "thip_eval_collision: bad arguments");
+  if (!ev->uploaded)
+    return fail(ev, "thip_eval_collision: thip_eval_upload first");
+  const int N = d.n_steps, D = d.chain.n_dof, W = 8 + 2 * D + 1;
+  const size_t B = static_cast<size_t>(ev->batch);
+  const int nu = ev->unit_n[static_cast<size_t>(term)];
+  const Unit* units = ev->d_units + ev->unit_off[static_cast<size_t>(term)];
+  hipError_t e;
+  if ((e = hipSetDevice(ev->device)) != hipSuccess)
+    return hipfail(ev, "hipSetDevice", e);
+  if ((e = hipMemcpyAsync(ev->d_x, x, B * N * D * sizeof(double), hipMemcpyHostToDevice, ev->stream)) != hipSuccess)
+    return hipfail(ev, "hipMemcpy(x)", e);
+  if (nu == 0)
+  {
+    std::fill(counts, counts + B, 0);
+    return THIP_OK;
+  }
+  int* ucounts = ev->d_counts;
+  int* pcounts = ev->d_counts + B * static_cast<size_t>(std::max(ev->max_units, 1));
+  for (int attempt = 0; attempt < 2; ++attempt)
+  {
+    const size_t need = B * static_cast<size_t>(nu) * ev->ucap * W;
+    if (need > ev->stage_doubles)
+    {
+      hipFree(ev->d_stage);
+      ev->d_stage = nullptr;
+      if ((e = hipMalloc(&ev->d_stage, need * sizeof(double))) != hipSuccess)
+        return hipfail(ev, "hipMalloc(contact records)", e);
+      ev->stage_doubles = need;
+    }
+    hipLaunchKernelGGL(coll_eval_kernel, dim3(nu, ev->batch), dim3(kEvBlock), 0, ev->stream, ev->d_chain, ev->d_sph,
+                       ev->terms[static_cast<size_t>(term)], units, nu, ev->batch, N, ev->d_x, ev->d_scene,
+                       d.n_prims, ev->d_stage, ev->ucap, ucounts);
+    if ((e = hipGetLastError()) != hipSuccess)
+      return hipfail(ev, "coll_eval_kernel launch", e);
+    std::vector<int> uc(B * static_cast<size_t>(nu));
+    if ((e = hipMemcpyAsync(uc.data(), ucounts, uc.size() * sizeof(int), hipMemcpyDeviceToHost, ev->stream)) !=
+            hipSuccess ||
+        (e = hipStreamSynchronize(ev->stream)) != hipSuccess)
+      return hipfail(ev, "coll_eval_kernel", e);
+    const int mx = *std::max_element(uc.begin(), uc.end());
+    if (mx <= ev->ucap)
+      break;
+    ev->ucap = mx;  // a unit had more contacts than the staging holds: rerun once with room for all
+  }
+  const size_t need_out = B * static_cast<size_t>(std::max(cap, 1)) * W;
+  if (need_out > ev->out_doubles)
+  {
+    hipFree(ev->d_out);
+    ev->d_out = nullptr;
+    if ((e = hipMalloc(&ev->d_out, need_out * sizeof(double))) != hipSuccess)
+      return hipfail(ev, "hipMalloc(records)", e);
+    ev->out_doubles = need_out;
+  }
+  hipLaunchKernelGGL(coll_pack_kernel, dim3(ev->batch), dim3(kEvBlock), 0, ev->stream, ev->d_stage, ucounts, nu,
+                     ev->ucap, W, ev->d_out, cap, pcounts);
+  if ((e = hipGetLastError()) != hipSuccess)
+    return hipfail(ev, "coll_pack_kernel launch", e);
+  if ((e = hipMemcpyAsync(counts, pcounts, B * sizeof(int), hipMemcpyDeviceToHost, ev->stream)) != hipSuccess ||
+      (cap > 0 && (e = hipMemcpyAsync(records, ev->d_out, B * static_cast<size_t>(cap) * W * sizeof(double),
+                                      hipMemcpyDeviceToHost, ev->stream)) != hipSuccess) ||
+      (e = hipStreamSynchronize(ev->stream)) != hipSuccess)
+    return hipfail(ev, "coll_pack_kernel", e);
+  return THIP_OK;
+}
+
+void thip_eval_destroy(thip_eval* ev)
+{
+  if (!ev)
+    return;
+  hipSetDevice(ev->device);
+  if (ev->stream)
+    hipStreamSynchronize(ev->stream);
+  hipFree(ev->d_chain);
+  hipFree(ev->d_sph);
+  hipFree(ev->d_tgt);
+  hipFree(ev->d_scene);
+  hipFree(ev->d_x);
+  hipFree(ev->d_err);
+  hipFree(ev->d_jac);
+  hipFree(ev->d_stage);
+  hipFree(ev->d_out);
+  hipFree(ev->d_counts);
+  hipFree(ev->d_units);
+  if (ev->stream)
+    hipStreamDestroy(ev->stream);
+  delete ev;
+}
+
+const char* thip_eval_last_error(thip_eval* ev) { return ev ? ev->err.c_str() : g_eval_create_err.c_str(); }
+
+}  // extern "C"

@@ -147,7 +147,9 @@ static int validate(const thip_problem_desc* d, std::string& why)
   if (ch.n_links < 1 || ch.n_links > THIP_MAX_LINKS)
     return why = "n_links out of range", THIP_E_INVALID;
   if (d->n_steps < 2 || d->n_steps > THIP_MAX_STEPS)
-    return why = "n_steps out of range", THIP_E_INVALID;
+    return why = "n_steps must be in [2, " + std::to_string(THIP_MAX_STEPS) +
+                 "] for the batched kernel (single-waypoint problems run sco::BasicTrustRegionSQP's generic path)",
+           THIP_E_INVALID;
   for (int k = 1; k < ch.n_links; ++k)
   {
     const int ty = ch.joint_type[k];
@@ -200,6 +202,10 @@ static int validate(const thip_problem_desc* d, std::string& why)
     return why = "time-parameterised problems (use_time, JointVel terms with use_time, TotalTime) and fixed dofs are not "
                  "lowered into the batched kernel: solve such a problem with sco::BasicTrustRegionSQP (the generic "
                  "path, GpuModel)",
+           THIP_E_INVALID;
+  if (d->n_coll_extra != 0)
+    return why = "more than one collision term is not lowered into the batched kernel: solve such a problem with "
+                 "sco::BasicTrustRegionSQP (the generic path, device-evaluated terms and GpuModel)",
            THIP_E_INVALID;
   if (d->n_jpos < 0 || d->n_jpos > THIP_MAX_JPOS)
     return why = "n_jpos out of range", THIP_E_INVALID;

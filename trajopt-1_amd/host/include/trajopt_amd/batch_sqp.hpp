@@ -35,6 +35,11 @@ public:
   // Per-QP records of the next optimize() (thip_debug_trace, THIP_TRACE_W doubles each).
   void enableTrace(int capacity);
   std::vector<std::vector<double>> trace() const;  // [problem][n_records * THIP_TRACE_W]
+  // After a traced optimize(): problem b's solver log in the reference's
+  // writeSolver format (trajopt_solver.log, optimizers.cpp:533-547) at `path`.
+  // (A single problem observed through sco::BasicTrustRegionSQP -- callbacks or
+  // log_results -- runs the host loop, which writes all four logs.)
+  void writeSolverLog(int b, const std::string& path) const;
   int batch() const { return static_cast<int>(probs_.size()); }
 
 private:
@@ -79,7 +84,7 @@ public:
 };
 
 // Upper bound on the per-QP trace records of one problem under param (the
-// native path's trajopt_solver.log)
+// batched path's trajopt_solver.log: enableTrace(traceCapacity(param)))
 int traceCapacity(const sco::BasicTrustRegionSQPParameters& param);
 
 // trajopt/src/utils.cpp:13-24: the trajectory as one row-major vector

@@ -28,6 +28,7 @@
 #include <string>
 #include <vector>
 
+#include "trajopt_amd/device_terms.hpp"
 #include "trajopt_amd/json.hpp"
 #include "trajopt_amd/trajectory_costs.hpp"
 #include "trajopt_hip.h"
@@ -101,6 +102,13 @@ public:
   // trajopt_common/data/arm_around_table.urdf), zero state, the 14-sphere
   // per-arm collision model of trajopt_amd/scene.py, empty scene.
   static Ptr makePR2();
+  // spherebot (trajopt_common/data/spherebot.urdf, used by simple_collision_unit):
+  // group "manipulator", two prismatic joints, one 0.5 m robot sphere, and the
+  // URDF's three static 0.5 m spheres as the scene
+  static Ptr makeSpherebot();
+  // the reference's test robot a group name belongs to: "manipulator" ->
+  // spherebot, every other name -> the PR2 (the two share no group name)
+  static Ptr builtin(const std::string& manip);
 
 private:
   std::map<std::string, KinematicGroup::ConstPtr> groups_;
@@ -341,7 +349,9 @@ public:
   // sco::BasicTrustRegionSQP asks first: a lowerable problem runs sqp_kernel as a batch of one
   bool solveNative(const sco::BasicTrustRegionSQPParameters& param, const DblVec& x0,
                    sco::OptResults& results) override;
-  int device = 0;  // HIP device of the native path
+  int device = 0;  // HIP device of the native path and of the device-evaluated terms
+  // the evaluator of the CartPose / collision term objects (thip_eval_*)
+  const std::shared_ptr<DeviceTermEvaluator>& deviceTerms() const { return device_terms_; }
 
   friend TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci);
 
@@ -352,6 +362,7 @@ private:
   Environment::ConstPtr env_;
   VarArray traj_vars_, joint_vars_;
   std::vector<const void*> lowered_;  // the lowered Cost / Constraint objects
+  std::shared_ptr<DeviceTermEvaluator> device_terms_;
 };
 
 TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci);

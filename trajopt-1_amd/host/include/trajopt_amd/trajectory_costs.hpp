@@ -112,27 +112,4 @@ sco::MatrixOfVector::Ptr jointVelTimeJac();
 sco::VectorOfVector::Ptr totalTimeErr(double limit);
 sco::MatrixOfVector::Ptr totalTimeJac();
 
-// A term lowered into the batched kernel whose exact value / convexification
-// needs the device (CartPose FK and finite differences, collision signed
-// distances): the host loop refuses it loudly instead of computing on the CPU.
-class DeviceOnlyCost : public sco::Cost
-{
-public:
-  explicit DeviceOnlyCost(const std::string& name) : sco::Cost(name) {}
-  double value(const DblVec&) override;
-  sco::ConvexObjective::Ptr convex(const DblVec&, sco::Model*) override;
-  sco::VarVector getVars() override { return {}; }
-};
-class DeviceOnlyConstraint : public sco::Constraint
-{
-public:
-  DeviceOnlyConstraint(const std::string& name, sco::ConstraintType t) : sco::Constraint(name), type_(t) {}
-  sco::ConstraintType type() override { return type_; }
-  DblVec value(const DblVec&) override;
-  sco::ConvexConstraints::Ptr convex(const DblVec&, sco::Model*) override;
-  sco::VarVector getVars() override { return {}; }
-
-private:
-  sco::ConstraintType type_;
-};
 }  // namespace trajopt

@@ -232,6 +232,15 @@ std::vector<sco::OptResults> MultiDeviceBatchSQP::optimize()
 
 double BatchTrustRegionSQP::lastKernelMs() const { return thip_last_kernel_ms(ctx_); }
 
+void BatchTrustRegionSQP::writeSolverLog(int b, const std::string& path) const
+{
+  if (trace_cap_ <= 0)
+    throw std::runtime_error("BatchTrustRegionSQP::writeSolverLog: enableTrace() before optimize()");
+  if (b < 0 || b >= batch())
+    throw std::runtime_error("BatchTrustRegionSQP::writeSolverLog: problem out of range");
+  trajopt::writeSolverLog(path, trace()[static_cast<std::size_t>(b)]);
+}
+
 void BatchTrustRegionSQP::enableTrace(int capacity)
 {
   check(thip_debug_trace(ctx_, capacity), "thip_debug_trace");
@@ -300,11 +309,7 @@ bool TrajOptProb::solveNative(const sco::BasicTrustRegionSQPParameters& param, c
   lp.init = x0;
   copyParams(param, lp.desc.sqp);
   BatchTrustRegionSQP batch(std::vector<LoweredProblem>{ std::move(lp) }, device);
-  if (param.log_results)
-    batch.enableTrace(traceCapacity(param));
   results = batch.optimize()[0];
-  if (param.log_results)
-    writeSolverLog(param.log_dir + "/trajopt_solver.log", batch.trace()[0]);
   return true;
 }
 

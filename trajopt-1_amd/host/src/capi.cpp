@@ -25,21 +25,27 @@ trajopt::TrajOptProb::Ptr construct(const char* json_text, const double* scene, 
     throw std::runtime_error("null json text");
   if (n_prims < 0 || (n_prims > 0 && !scene))
     throw std::runtime_error("bad scene");
-  auto env = trajopt::Environment::makePR2();
+  const Json::Value root = Json::parse(json_text);
+  std::string manip;
+  if (root.isMember("basic_info") && root["basic_info"].isMember("manip"))
+    json_marshal::childFromJson(root["basic_info"], manip, "manip");
+  // the built-in environment of the group (the PR2, or spherebot for "manipulator"),
+  // then the caller's primitives after the environment's own
+  auto env = trajopt::Environment::builtin(manip);
   for (int p = 0; p < n_prims; ++p)
   {
     std::array<double, 16> rec{};
     std::copy(scene + 16 * p, scene + 16 * (p + 1), rec.begin());
     env->scene.push_back(rec);
   }
-  return trajopt::ConstructProblem(Json::parse(json_text), env);
+  return trajopt::ConstructProblem(root, env);
 }
 }  // namespace
 
 extern "C" {
 
 int thost_lower_json(const char* json_text, const double* scene, int n_prims, thip_problem_desc* desc, double* init,
-                     double* cart_targets, double* jpos_targets, char* err, int err_len)
+                     double* cart_targets, double* jpos_targets, double* scene_out, char* err, int err_len)
 {
   try
   {
@@ -55,6 +61,8 @@ int thost_lower_json(const char* json_text, const double* scene, int n_prims, th
       std::copy(prob->cart_targets.begin(), prob->cart_targets.end(), cart_targets);
     if (jpos_targets)
       std::copy(prob->jpos_targets.begin(), prob->jpos_targets.end(), jpos_targets);
+    if (scene_out)
+      std::copy(prob->scene.begin(), prob->scene.end(), scene_out);
     setErr(err, err_len, "");
     return 0;
   }

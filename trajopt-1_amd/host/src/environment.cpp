@@ -138,4 +138,61 @@ Environment::Ptr Environment::makePR2()
       env->collision_spheres.push_back({ std::string(side) + links[s], { cx[s], 0.0, 0.0 }, rad[s] });
   return env;
 }
+
+// trajopt_common/data/spherebot.urdf / spherebot.srdf: group "manipulator" =
+// base_link -> spherebot_link over two prismatic joints (x, then y; limits
+// +-20), a 0.5 m sphere on spherebot_link; the static test spheres (0.5 m) at
+// the origin (test_sphere_link), (-0.75, 0, 0) and (0, 0.75, 0) off base_link.
+Environment::Ptr Environment::makeSpherebot()
+{
+  auto env = std::make_shared<Environment>();
+  KinematicGroup g;
+  g.name = "manipulator";
+  thip_chain& c = g.chain;
+  const double eye[12] = { 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0 };
+  for (int i = 0; i < 12; ++i)
+    c.base_pose[i] = eye[i];
+  c.is_tree = 0;
+  c.joint_dof[0] = -1;
+  g.link_names = { "base_link", "spherebot_linkX", "spherebot_linkY", "spherebot_link" };
+  const int types[] = { 0, THIP_JOINT_PRISMATIC, THIP_JOINT_PRISMATIC, THIP_JOINT_FIXED };
+  const double axes[][3] = { { 0, 0, 0 }, { 1, 0, 0 }, { 0, 1, 0 }, { 0, 0, 0 } };
+  for (int k = 1; k < 4; ++k)
+  {
+    c.joint_type[k] = types[k];
+    c.parent[k] = k - 1;
+    for (int i = 0; i < 12; ++i)
+      c.joint_origin[k][i] = eye[i];
+    c.joint_dof[k] = types[k] == THIP_JOINT_FIXED ? -1 : k - 1;
+    for (int i = 0; i < 3; ++i)
+      c.joint_axis[k][i] = axes[k][i];
+  }
+  c.n_links = 4;
+  c.n_dof = 2;
+  for (int j = 0; j < 2; ++j)
+  {
+    c.lower[j] = -20.0;
+    c.upper[j] = 20.0;
+  }
+  g.joint_names = { "spherebot_x_joint", "spherebot_y_joint" };
+  env->addJointGroup(std::move(g));
+  env->collision_spheres.push_back({ "spherebot_link", { 0.0, 0.0, 0.0 }, 0.5 });
+  const double centers[][3] = { { 0.0, 0.0, 0.0 }, { -0.75, 0.0, 0.0 }, { 0.0, 0.75, 0.0 } };
+  for (const auto& ctr : centers)
+  {
+    std::array<double, 16> rec{};
+    rec[0] = THIP_PRIM_SPHERE;
+    rec[1] = ctr[0];
+    rec[2] = ctr[1];
+    rec[3] = ctr[2];
+    rec[4] = 0.5;
+    env->scene.push_back(rec);
+  }
+  return env;
+}
+
+Environment::Ptr Environment::builtin(const std::string& manip)
+{
+  return manip == "manipulator" ? makeSpherebot() : makePR2();
+}
 }  // namespace trajopt

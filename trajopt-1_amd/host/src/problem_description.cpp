@@ -927,10 +927,27 @@ void CartPoseTermInfo::hatch(TrajOptProb& prob)
     off = poseMul(poseInv(base), poseMul(kin->staticWorldPose(static_frame), static_offset));
   }
   prob.cart_targets.insert(prob.cart_targets.end(), off.begin(), off.end());
+  // the reference's TrajOptCostFromErrFunc / TrajOptConstraintFromErrFunc over the
+  // waypoint's joints with the nonzero coefficients (problem_description.cpp:924-1005),
+  // the error and its jacobian evaluated on the device (thip_eval_cart_pose)
+  std::vector<int> indices;
+  DblVec coeffs;
+  for (int i = 0; i < 6; ++i)
+  {
+    const double cf = (i < 3) ? pos_coeffs[static_cast<std::size_t>(i)] : rot_coeffs[static_cast<std::size_t>(i - 3)];
+    if (std::fabs(cf) > 1e-5)
+    {
+      indices.push_back(i);
+      coeffs.push_back(cf);
+    }
+  }
+  auto f = std::make_shared<CartPoseDeviceErr>(prob.deviceTerms(), k, indices);
+  auto dfdx = std::make_shared<CartPoseDeviceJac>(prob.deviceTerms(), k, indices);
+  const sco::VarVector vars = prob.GetVarRow(timestep, 0, prob.GetNumDOF());
   if (d.cart_is_cnt[k])
-    prob.addLoweredConstraint(std::make_shared<DeviceOnlyConstraint>(name, sco::EQ));
+    prob.addLoweredConstraint(std::make_shared<DeviceCartPoseConstraint>(f, dfdx, vars, coeffs, sco::EQ, name));
   else
-    prob.addLoweredCost(std::make_shared<DeviceOnlyCost>(name));
+    prob.addLoweredCost(std::make_shared<DeviceCartPoseCost>(f, dfdx, vars, coeffs, sco::ABS, name));
 }
 
 // ------------------------------------------------------------ Collision
@@ -1006,8 +1023,11 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
     unsupported("per link-pair collision margins / coeffs (\"pairs\") that differ from the term's");
   const auto env = prob.GetEnv();
   thip_problem_desc& d = prob.desc();
-  if (d.coll_enabled)
-    unsupported("more than one collision term");
+  // the first collision term lowers into the descriptor's coll_* fields (the batched
+  // kernel runs it), further ones into coll_extra (the generic path runs the problem)
+  const bool extra = d.coll_enabled != 0;
+  if (extra && d.n_coll_extra >= THIP_MAX_COLL_EXTRA)
+    unsupported("more than " + std::to_string(THIP_MAX_COLL_EXTRA + 1) + " collision terms");
   const int n_steps = prob.GetNumSteps();
   for (int i = first_step; evaluator_type != 1 && i < last_step; ++i)
   {
@@ -1027,20 +1047,90 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
     unsupported("a scene of more than " + std::to_string(THIP_MAX_PRIMS) + " primitives");
   if (static_cast<int>(fixed_steps.size()) > THIP_MAX_STEPS)
     throw std::runtime_error("CollisionTermInfo: too many fixed steps");
-  d.coll_enabled = 1;
-  d.coll_is_cnt = any(term_type & TermType::TT_COST) ? 0 : 1;
-  d.coll_first_step = first_step;
-  d.coll_last_step = std::min(last_step, n_steps - 1);
-  d.coll_n_fixed = static_cast<int>(fixed_steps.size());
-  for (std::size_t k = 0; k < fixed_steps.size(); ++k)
-    d.coll_fixed_steps[k] = fixed_steps[k];
-  d.coll_margin = dist_pen;
-  d.coll_coeff = coeff;
-  d.coll_buffer = collision_margin_buffer;
+  const bool is_cnt = !any(term_type & TermType::TT_COST);
+  const int last = std::min(last_step, n_steps - 1);
   // CONTINUOUS casts each step pair once (lvs = max(), problem_description.cpp:1742-1744)
   // DISCRETE: SingleTimestepCollisionEvaluator per free waypoint (:1782-1796, :1842-1856)
-  d.coll_continuous = (evaluator_type == 1) ? 2 : (evaluator_type >= 3) ? 1 : 0;
-  d.coll_lvs = (evaluator_type == 3) ? 1.7976931348623157e308 : longest_valid_segment_length;
+  const int continuous = (evaluator_type == 1) ? 2 : (evaluator_type >= 3) ? 1 : 0;
+  const double lvs = (evaluator_type == 3) ? 1.7976931348623157e308 : longest_valid_segment_length;
+  const int term = extra ? 1 + d.n_coll_extra : 0;  // thip_eval's collision term index
+  if (extra)
+  {
+    thip_coll_term& x = d.coll_extra[d.n_coll_extra++];
+    x.is_cnt = is_cnt ? 1 : 0;
+    x.first_step = first_step;
+    x.last_step = last;
+    x.n_fixed = static_cast<int>(fixed_steps.size());
+    for (std::size_t k = 0; k < fixed_steps.size(); ++k)
+      x.fixed_steps[k] = fixed_steps[k];
+    x.margin = dist_pen;
+    x.coeff = coeff;
+    x.buffer = collision_margin_buffer;
+    x.lvs = lvs;
+    x.continuous = continuous;
+  }
+  else
+  {
+    d.coll_enabled = 1;
+    d.coll_is_cnt = is_cnt ? 1 : 0;
+    d.coll_first_step = first_step;
+    d.coll_last_step = last;
+    d.coll_n_fixed = static_cast<int>(fixed_steps.size());
+    for (std::size_t k = 0; k < fixed_steps.size(); ++k)
+      d.coll_fixed_steps[k] = fixed_steps[k];
+    d.coll_margin = dist_pen;
+    d.coll_coeff = coeff;
+    d.coll_buffer = collision_margin_buffer;
+    d.coll_continuous = continuous;
+    d.coll_lvs = lvs;
+  }
+  // one CollisionCost / CollisionConstraint per unit, named <name>_<i> (:1735-1858)
+  const int n_dof = prob.GetNumDOF();
+  auto addUnit = [&](int i, bool single) {
+    DeviceCollisionUnit u;
+    u.ev = prob.deviceTerms();
+    u.term = term;
+    u.t = i;
+    u.vars0 = prob.GetVarRow(i, 0, n_dof);
+    if (!single)
+      u.vars1 = prob.GetVarRow(i + 1, 0, n_dof);
+    u.margin = dist_pen;
+    u.coeff = coeff;
+    const std::string nm = name + "_" + std::to_string(i);
+    if (is_cnt)
+    {
+      auto c = std::make_shared<DeviceCollisionConstraint>(std::move(u), nm);
+      if (extra)
+        prob.addConstraint(c);
+      else
+        prob.addLoweredConstraint(c);
+    }
+    else
+    {
+      auto c = std::make_shared<DeviceCollisionCost>(std::move(u), nm);
+      if (extra)
+        prob.addCost(c);
+      else
+        prob.addLoweredCost(c);
+    }
+  };
+  auto fixedStep = [&](int i) { return std::find(fixed_steps.begin(), fixed_steps.end(), i) != fixed_steps.end(); };
+  if (continuous == 2)
+  {
+    for (int i = first_step; i <= last; ++i)
+      if (!fixedStep(i))
+        addUnit(i, true);
+  }
+  else
+    for (int i = first_step; i < last; ++i)
+      addUnit(i, false);
+  if (extra)
+  {
+    // the robot model and the scene are the environment's, shared with the first term
+    if (d.n_spheres != static_cast<int>(spheres.size()) || d.n_prims != static_cast<int>(env->scene.size()))
+      throw std::runtime_error("CollisionTermInfo: collision terms of one problem must share the robot model and scene");
+    return;
+  }
   d.n_spheres = static_cast<int>(spheres.size());
   for (int s = 0; s < d.n_spheres; ++s)
   {
@@ -1053,10 +1143,6 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
   d.n_prims = static_cast<int>(env->scene.size());
   for (const auto& p : env->scene)
     prob.scene.insert(prob.scene.end(), p.begin(), p.end());
-  if (d.coll_is_cnt)
-    prob.addLoweredConstraint(std::make_shared<DeviceOnlyConstraint>(name, sco::INEQ));
-  else
-    prob.addLoweredCost(std::make_shared<DeviceOnlyCost>(name));
 }
 
 // ------------------------------------------------------------ ConstructProblem
@@ -1098,8 +1184,8 @@ TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci)
     throw std::runtime_error("No terms use time and basic_info is not set correctly. Try basic_info.use_time = false");
   if (!iequals(bi.convex_solver, "OSQP") && !iequals(bi.convex_solver, "AUTO_SOLVER"))
     unsupported("convex_solver " + bi.convex_solver);
-  if (n_steps < 2 || n_steps > THIP_MAX_STEPS)
-    throw std::runtime_error("n_steps must be in [2, " + std::to_string(THIP_MAX_STEPS) + "]");
+  if (n_steps < 1 || n_steps > THIP_MAX_STEPS)
+    throw std::runtime_error("n_steps must be in [1, " + std::to_string(THIP_MAX_STEPS) + "]");
 
   auto prob = std::make_shared<TrajOptProb>(n_steps, pci);
   thip_problem_desc& d = prob->desc_;
@@ -1206,7 +1292,10 @@ TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci)
 // ------------------------------------------------------------ TrajOptProb
 // problem_description.cpp:557-598: the j_i_j variables with the joint limits as bounds
 TrajOptProb::TrajOptProb(int n_steps, const ProblemConstructionInfo& pci)
-  : sco::OptProb(sco::ModelType::OSQP, modelConfig(pci)), kin_(pci.kin), env_(pci.env)
+  : sco::OptProb(sco::ModelType::OSQP, modelConfig(pci))
+  , kin_(pci.kin)
+  , env_(pci.env)
+  , device_terms_(std::make_shared<DeviceTermEvaluator>(this))
 {
   if (!kin_)
     throw std::runtime_error("TrajOptProb: pci.kin is null");
@@ -1271,8 +1360,8 @@ std::string TrajOptProb::unloweredTerms() const
 
 bool TrajOptProb::lowerable() const
 {
-  return desc_.n_jdt == 0 && desc_.n_jvt == 0 && desc_.n_ttt == 0 && !desc_.use_time && desc_.n_fixed_dofs == 0 &&
-         unloweredTerms().empty();
+  return desc_.n_steps >= 2 && desc_.n_jdt == 0 && desc_.n_jvt == 0 && desc_.n_ttt == 0 && !desc_.use_time &&
+         desc_.n_fixed_dofs == 0 && desc_.n_coll_extra == 0 && unloweredTerms().empty();
 }
 
 LoweredProblem TrajOptProb::lowered() const

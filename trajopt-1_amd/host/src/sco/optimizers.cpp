@@ -154,11 +154,15 @@ OptStatus BasicTrustRegionSQP::optimize()
     throw std::runtime_error("you forgot to initialize!");
   if (!prob_)
     throw std::runtime_error("you forgot to set the optimization problem");
+  // The batched kernel runs the whole loop on the device.  A caller that observes
+  // the iterations -- callbacks at every SQP iteration (optimizers.cpp:754), the
+  // four CSV logs (:533-647, 858-871) -- gets the reference's host loop instead, over
+  // the same terms (the kinematic ones evaluated on the device), so the observed
+  // behaviour is the reference's whichever path solves the problem.
   OptResults native;
-  if (prob_->solveNative(param_, results_.x, native))
+  if (callbacks_.empty() && !param_.log_results && prob_->solveNative(param_, results_.x, native))
   {
     results_ = native;
-    callCallbacks();
     return results_.status;
   }
   return optimizeGeneric();

@@ -261,26 +261,4 @@ sco::MatrixOfVector::Ptr totalTimeJac()
   });
 }
 
-double DeviceOnlyCost::value(const DblVec&)
-{
-  throw std::runtime_error("term '" + name_ +
-                           "' is evaluated by the batched GPU kernel only; this problem also has terms the kernel "
-                           "does not lower, so it runs sco::BasicTrustRegionSQP's host loop, which cannot evaluate it");
-}
-sco::ConvexObjective::Ptr DeviceOnlyCost::convex(const DblVec& x, sco::Model*)
-{
-  value(x);
-  return nullptr;
-}
-DblVec DeviceOnlyConstraint::value(const DblVec&)
-{
-  throw std::runtime_error("constraint '" + name_ +
-                           "' is evaluated by the batched GPU kernel only; this problem also has terms the kernel "
-                           "does not lower, so it runs sco::BasicTrustRegionSQP's host loop, which cannot evaluate it");
-}
-sco::ConvexConstraints::Ptr DeviceOnlyConstraint::convex(const DblVec& x, sco::Model*)
-{
-  value(x);
-  return nullptr;
-}
 }  // namespace trajopt

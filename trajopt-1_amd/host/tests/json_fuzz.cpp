@@ -111,11 +111,14 @@ int main(int argc, char** argv)
         // exercise the lowered form and the host objects' values
         const trajopt::LoweredProblem lp = prob->lowered();
         const sco::DblVec x(static_cast<std::size_t>(prob->getNumVars()), 0.01);
+        // (CartPose and collision terms evaluate on the device: not in this CPU-only run)
         for (const auto& c : prob->getCosts())
-          if (dynamic_cast<trajopt::DeviceOnlyCost*>(c.get()) == nullptr)
+          if (!dynamic_cast<trajopt::DeviceCartPoseCost*>(c.get()) &&
+              !dynamic_cast<trajopt::DeviceCollisionCost*>(c.get()))
             (void)c->value(x);
         for (const auto& c : prob->getConstraints())
-          if (dynamic_cast<trajopt::DeviceOnlyConstraint*>(c.get()) == nullptr)
+          if (!dynamic_cast<trajopt::DeviceCartPoseConstraint*>(c.get()) &&
+              !dynamic_cast<trajopt::DeviceCollisionConstraint*>(c.get()))
             (void)c->violation(x);
         built += lp.init.empty() ? 0 : 1;
       }

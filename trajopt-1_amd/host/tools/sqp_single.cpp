@@ -1,8 +1,10 @@
 // The reference's per-problem optimizer usage on the HIP path (planning_unit.cpp:83-124):
 //   ConstructProblem(pci) -> BasicTrustRegionSQP opt(prob); opt.initialize(...); opt.optimize()
-// usage: sqp_single [--log DIR] problem.json
-//   prints "status <s> iters <n> cost <c> fevals <f>" and the trajectory; with --log, the
-//   reference's log_results solver log in DIR/trajopt_solver.log
+// usage: sqp_single [--log DIR] [--callback] problem.json
+//   prints "status <s> iters <n> cost <c> fevals <f> callbacks <k>" and the trajectory;
+//   --log: the reference's log_results CSV logs in DIR; --callback: a callback counting
+//   its calls (optimizers.cpp:754, 978).  Either observes the iterations, so the problem
+//   runs the host loop (sco::BasicTrustRegionSQP::optimize).
 #include <cstdio>
 #include <string>
 
@@ -10,32 +12,44 @@
 
 int main(int argc, char** argv)
 {
-  std::string log_dir;
-  int a = 1;
-  if (argc == 4 && std::string(argv[1]) == "--log")
+  std::string log_dir, file;
+  bool callback = false;
+  for (int a = 1; a < argc; ++a)
   {
-    log_dir = argv[2];
-    a = 3;
+    const std::string s = argv[a];
+    if (s == "--log" && a + 1 < argc)
+      log_dir = argv[++a];
+    else if (s == "--callback")
+      callback = true;
+    else if (file.empty() && s.rfind("--", 0) != 0)
+      file = s;
+    else
+      file.clear(), a = argc;
   }
-  else if (argc != 2)
+  if (file.empty())
   {
-    std::fprintf(stderr, "usage: sqp_single [--log DIR] problem.json\n");
+    std::fprintf(stderr, "usage: sqp_single [--log DIR] [--callback] problem.json\n");
     return 2;
   }
   try
   {
-    const auto env = trajopt::Environment::makePR2();
-    trajopt::TrajOptProb::Ptr prob = trajopt::ConstructProblem(Json::parseFile(argv[a]), env);
+    const Json::Value root = Json::parseFile(file.c_str());
+    std::string manip;
+    json_marshal::childFromJson(root["basic_info"], manip, "manip");
+    trajopt::TrajOptProb::Ptr prob = trajopt::ConstructProblem(root, trajopt::Environment::builtin(manip));
     trajopt::BasicTrustRegionSQP opt(prob);
     if (!log_dir.empty())
     {
       opt.getParameters().log_results = true;
       opt.getParameters().log_dir = log_dir;
     }
+    int calls = 0;
+    if (callback)
+      opt.addCallback([&calls](sco::OptProb*, sco::OptResults&) { ++calls; });
     opt.initialize(trajopt::trajToDblVec(prob->GetInitTraj()));
     const sco::OptStatus st = opt.optimize();
-    std::printf("status %s iters %d cost %.17g fevals %d\n", sco::toString(st).c_str(), opt.results().n_sqp_iters,
-                opt.results().total_cost, opt.results().n_func_evals);
+    std::printf("status %s iters %d cost %.17g fevals %d callbacks %d\n", sco::toString(st).c_str(),
+                opt.results().n_sqp_iters, opt.results().total_cost, opt.results().n_func_evals, calls);
     const int D = prob->GetNumDOF();
     for (std::size_t i = 0; i < opt.x().size(); ++i)
       std::printf("%.17g%c", opt.x()[i], (static_cast<int>(i) % D == D - 1) ? '\n' : ' ');

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 from pathlib import Path
 
-ABI_VERSION = 5  # THIP_ABI_VERSION
+ABI_VERSION = 6  # THIP_ABI_VERSION
 MAX_DOF = 16
 MAX_LINKS = 32
 MAX_STEPS = 64
@@ -22,6 +22,7 @@ MAX_JVX = 4
 MAX_JDT = 8
 MAX_JVT = 4
 MAX_TTT = 2
+MAX_COLL_EXTRA = 3
 TRACE_W = 16  # THIP_TRACE_W
 DEBUG_NO_SEGMENT, DEBUG_FORCE_WIDE, DEBUG_NO_BRANCH = 1, 2, 4  # thip_debug_set_path flags
 
@@ -96,6 +97,22 @@ class OsqpSettings(C.Structure):
         ("polishing", C.c_int),
         ("delta", C.c_double),
         ("polish_refine_iter", C.c_int),
+    ]
+
+
+class CollTerm(C.Structure):
+    """thip_coll_term: a collision term beyond the descriptor's first."""
+    _fields_ = [
+        ("is_cnt", C.c_int),
+        ("first_step", C.c_int),
+        ("last_step", C.c_int),
+        ("n_fixed", C.c_int),
+        ("fixed_steps", C.c_int * MAX_STEPS),
+        ("margin", C.c_double),
+        ("coeff", C.c_double),
+        ("buffer", C.c_double),
+        ("lvs", C.c_double),
+        ("continuous", C.c_int),
     ]
 
 
@@ -184,6 +201,8 @@ class ProblemDesc(C.Structure):
         ("sphere_radius", C.c_double * MAX_SPHERES),
         ("n_prims", C.c_int),
         ("coll_max_contacts", C.c_int),
+        ("n_coll_extra", C.c_int),
+        ("coll_extra", CollTerm * MAX_COLL_EXTRA),
         ("sqp", SqpParams),
         ("osqp", OsqpSettings),
     ]
@@ -315,6 +334,18 @@ def _declare(lib):
     lib.thip_debug_get_profile.restype = C.c_int
     lib.thip_debug_set_path.argtypes = [C.c_int]
     lib.thip_debug_set_path.restype = C.c_int
+    lib.thip_eval_create.argtypes = [C.c_int, P(ProblemDesc), C.c_int, P(vp)]
+    lib.thip_eval_create.restype = C.c_int
+    lib.thip_eval_upload.argtypes = [vp, dp, dp]
+    lib.thip_eval_upload.restype = C.c_int
+    lib.thip_eval_cart_pose.argtypes = [vp, C.c_int, dp, dp, dp]
+    lib.thip_eval_cart_pose.restype = C.c_int
+    lib.thip_eval_collision.argtypes = [vp, C.c_int, dp, dp, C.c_int, P(C.c_int)]
+    lib.thip_eval_collision.restype = C.c_int
+    lib.thip_eval_destroy.argtypes = [vp]
+    lib.thip_eval_destroy.restype = None
+    lib.thip_eval_last_error.argtypes = [vp]
+    lib.thip_eval_last_error.restype = C.c_char_p
     lib.thip_sizeof_desc.argtypes = []
     lib.thip_sizeof_desc.restype = C.c_int
     lib.thip_sizeof_result.argtypes = []

@@ -2,7 +2,8 @@
 
 The front door parses problems in the reference's JSON format
 (ProblemConstructionInfo::fromJson, trajopt/src/problem_description.cpp:276-312)
-on the built-in PR2 "right_arm" environment and lowers them with the
+on the built-in environment of the reference's test robots (the PR2 groups, or
+spherebot's "manipulator") and lowers them with the
 TermInfo::hatch restatements; `solve_json_batch` runs them through the C++
 BatchTrustRegionSQP on the HIP path.  `workload_to_json` writes a synthetic
 workload problem in that format (used by the tests to drive the front door).
@@ -33,8 +34,8 @@ def load_host():
             raise RuntimeError(f"{HOST_LIB} is missing: run __graft_entry__.build()")
         L = C.CDLL(str(HOST_LIB))
         dp = C.POINTER(C.c_double)
-        L.thost_lower_json.argtypes = [C.c_char_p, dp, C.c_int, C.POINTER(abi.ProblemDesc), dp, dp, dp, C.c_char_p,
-                                       C.c_int]
+        L.thost_lower_json.argtypes = [C.c_char_p, dp, C.c_int, C.POINTER(abi.ProblemDesc), dp, dp, dp, dp,
+                                       C.c_char_p, C.c_int]
         L.thost_lower_json.restype = C.c_int
         L.thost_solve_json_batch.argtypes = [C.POINTER(C.c_char_p), C.c_int, dp, C.c_int, C.c_int, dp,
                                              C.POINTER(abi.Result), C.c_char_p, C.c_int]
@@ -53,8 +54,10 @@ def _dp(a):
     return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
 
 
-def lower_json(text: str, scene=None):
-    """-> (desc, init [N, D], cart_targets [n_cart, 12], jpos_targets [n_jpos, D])."""
+def lower_json(text: str, scene=None, with_scene=False):
+    """-> (desc, init [N, D], cart_targets [n_cart, 12], jpos_targets [n_jpos, D])
+    (+ the scene [n_prims, 16] the collision terms see, with_scene=True: the
+    built-in environment's primitives, then `scene`)."""
     L = load_host()
     sc = None if scene is None or len(scene) == 0 else np.ascontiguousarray(scene, dtype=np.float64)
     n_prims = 0 if sc is None else sc.shape[0]
@@ -62,14 +65,19 @@ def lower_json(text: str, scene=None):
     init = np.zeros((abi.MAX_STEPS, abi.MAX_DOF))
     tgt = np.zeros((abi.MAX_CART, 12))
     jpt = np.zeros((abi.MAX_JPOS, abi.MAX_DOF))
+    sco = np.zeros((abi.MAX_PRIMS, 16))
     err = C.create_string_buffer(4096)
-    rc = L.thost_lower_json(text.encode(), _dp(sc), n_prims, C.byref(desc), _dp(init), _dp(tgt), _dp(jpt), err, 4096)
+    rc = L.thost_lower_json(text.encode(), _dp(sc), n_prims, C.byref(desc), _dp(init), _dp(tgt), _dp(jpt), _dp(sco),
+                            err, 4096)
     if rc != 0:
         raise HostError(err.value.decode())
     N, D = desc.n_steps, desc.chain.n_dof
     init = init.reshape(-1)[: N * D].reshape(N, D)
     tgt = tgt.reshape(-1)[: desc.n_cart * 12].reshape(desc.n_cart, 12)
     jpt = jpt.reshape(-1)[: desc.n_jpos * D].reshape(desc.n_jpos, D)
+    if with_scene:
+        has_coll = desc.coll_enabled or desc.n_coll_extra > 0
+        return desc, init, tgt, jpt, sco[: desc.n_prims if has_coll else 0].copy()
     return desc, init, tgt, jpt
 
 

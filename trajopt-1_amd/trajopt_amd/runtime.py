@@ -149,3 +149,58 @@ class BatchTrustRegionSQP:
             self.close()
         except Exception:
             pass
+
+
+class TermEvaluator:
+    """thip_eval_*: the CartPose and collision terms of a workload's problems
+    evaluated on the device (what the host SQP loop calls for problems the
+    fused kernel does not lower)."""
+
+    def __init__(self, workload, device: int = 0):
+        self.lib = abi.load_hip()
+        self.wl = workload
+        self.ev = C.c_void_p()
+        rc = self.lib.thip_eval_create(device, C.byref(workload.desc), workload.batch, C.byref(self.ev))
+        if rc != 0:
+            raise HipError(f"thip_eval_create: {self.lib.thip_eval_last_error(None).decode()}")
+        self._tgt = np.ascontiguousarray(workload.targets, dtype=np.float64) if workload.targets.size else None
+        self._scene = np.ascontiguousarray(workload.scene, dtype=np.float64) if workload.scene.size else None
+        self._check(self.lib.thip_eval_upload(self.ev, None if self._tgt is None else _dp(self._tgt),
+                                              None if self._scene is None else _dp(self._scene)), "thip_eval_upload")
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise HipError(f"{what}: {self.lib.thip_eval_last_error(self.ev).decode()}")
+
+    def cart_pose(self, term, q, jac=True):
+        """q [B, D] -> err [B, 6], jac [B, 6, D] (or None)."""
+        B, D = self.wl.batch, self.wl.n_dof
+        q = np.ascontiguousarray(q, dtype=np.float64).reshape(B, D)
+        err = np.zeros((B, 6))
+        J = np.zeros((B, 6, D)) if jac else None
+        self._check(self.lib.thip_eval_cart_pose(self.ev, term, _dp(q), _dp(err), None if J is None else _dp(J)),
+                    "thip_eval_cart_pose")
+        return err, J
+
+    def collision(self, term, x, cap=4096):
+        """x [B, N, D] -> list of record arrays [n_b, 8 + 2 D + 1]."""
+        B, D = self.wl.batch, self.wl.n_dof
+        W = 8 + 2 * D + 1
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        cnt = (C.c_int * B)()
+        out = np.zeros((B, cap, W))
+        self._check(self.lib.thip_eval_collision(self.ev, term, _dp(x), _dp(out), cap, cnt), "thip_eval_collision")
+        if max(cnt) > cap:
+            return self.collision(term, x, cap=max(cnt))
+        return [out[b, : cnt[b]].copy() for b in range(B)]
+
+    def close(self):
+        if self.ev:
+            self.lib.thip_eval_destroy(self.ev)
+            self.ev = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
