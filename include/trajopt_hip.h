@@ -504,6 +504,8 @@ int thip_debug_layout(thip_ctx* ctx, long long* doff, long long* ioff, long long
 #define THIP_DEBUG_NO_SEGMENT 1
 #define THIP_DEBUG_FORCE_WIDE 2
 #define THIP_DEBUG_NO_BRANCH 4  /* one block solve over all dofs even when the terms split the tree */
+#define THIP_DEBUG_STATIC_DISPATCH 8  /* one workgroup per problem instead of persistent workgroups taking
+                                         problems from a counter (bitwise the same results) */
 int thip_debug_set_path(int flags);
 int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws);
 

@@ -51,6 +51,17 @@ int thost_solve_json_batch_multi(const char* const* json_texts, int batch, const
                                  const int* devices, int n_devices, double* x, thip_result* results, char* err,
                                  int err_len);
 
+/* A stream of n_batches batches of `batch` JSON problems each (json_texts
+ * [n_batches * batch], scenes [n_batches * batch][n_prims][16]), every batch
+ * sharded over the device entries as thost_solve_json_batch_multi does, with
+ * `inflight` batches in flight per device entry
+ * (trajopt::MultiDeviceBatchSQP::optimizeStream: the next batches fill the CUs
+ * the current batch's tail leaves idle).  x [n_batches * batch][n_steps][n_dof],
+ * results [n_batches * batch] (may be NULL), in input order. */
+int thost_solve_json_stream(const char* const* json_texts, int n_batches, int batch, const double* scenes, int n_prims,
+                            const int* devices, int n_devices, int inflight, double* x, thip_result* results, char* err,
+                            int err_len);
+
 /* ConstructProblem for one JSON problem and trajopt::BasicTrustRegionSQP
  * (sco::BasicTrustRegionSQP with the problem's opt_info) on HIP device
  * `device`, as the reference's planning code runs one problem
@@ -129,6 +140,9 @@ typedef struct tsqp_result {
 void thost_tsqp_defaults(tsqp_spec* spec);
 /* solve on HIP device `device`: x [n_nodes][n_dof] (the best variables) */
 int thost_tsqp_solve(const tsqp_spec* spec, int device, double* x, tsqp_result* result, char* err, int err_len);
+/* sizeof(tsqp_spec) / sizeof(tsqp_result) as compiled into the library (FFI layout check) */
+int thost_tsqp_sizeof_spec(void);
+int thost_tsqp_sizeof_result(void);
 
 #ifdef __cplusplus
 }

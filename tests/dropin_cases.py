@@ -73,9 +73,11 @@ def cartpose_jointacc():
 
 
 def collision_jointjerk(evaluator=2):
-    """A 10-waypoint right-arm move through a table-top scene: JointVel cost,
-    a collision cost (evaluator 1 DISCRETE / 2 LVS_DISCRETE / 4 LVS_CONTINUOUS),
-    a JointJerk cost (not lowered) and a CartPose constraint on the goal."""
+    """A 10-waypoint right-arm move over a table-top scene: JointVel cost, a
+    collision cost (evaluator 1 DISCRETE / 2 LVS_DISCRETE / 4 LVS_CONTINUOUS,
+    lvs 0.2: 250-500 contacts per QP with the JSON's 0.5 m buffer, inside the
+    generic QP solver's n + m <= THIP_QP_MAX_KKT), a JointJerk cost (not
+    lowered) and a JointPos goal constraint."""
     n = 10
     start = [-0.9, 0.2, -1.2, -1.4, 0.3, -0.6, 0.1]
     end = [0.4, 0.3, -0.8, -0.9, -0.2, -0.4, 0.5]
@@ -84,7 +86,7 @@ def collision_jointjerk(evaluator=2):
         "costs": [
             {"type": "joint_vel", "params": {"coeffs": [1] * 7, "targets": [0] * 7}},
             {"type": "collision", "name": "coll", "params": {
-                "coeffs": 20, "dist_pen": 0.025, "evaluator_type": evaluator, "longest_valid_segment_length": 0.05}},
+                "coeffs": 20, "dist_pen": 0.025, "evaluator_type": evaluator, "longest_valid_segment_length": 0.2}},
             {"type": "joint_jerk", "params": {"coeffs": [0.5] * 7, "targets": [0] * 7}},
         ],
         "constraints": [
@@ -108,3 +110,35 @@ def table_scene():
     sph[0] = 0  # SPHERE
     sph[1:5] = [0.45, -0.4, 0.8, 0.08]
     return np.stack([box, sph])
+
+
+# arm_around_table.urdf:71-94: table_link at (1.11, 0, 0.635) off base_footprint; its
+# collision mesh Table.stl is 12 triangles spanning [-0.85, 0.85] x [-0.55, 0.55] x
+# [-0.01, 0.0095] -- a box, so this primitive is the table exactly (data read from the
+# mesh, vertex bounds rounded to float32 as stored)
+def arm_around_table_scene():
+    lo = np.array([-0.85000038, -0.55000061, -0.00999997])
+    hi = np.array([0.8500005, 0.55000037, 0.00951481])
+    table = np.zeros(16)
+    table[0] = 1  # BOX
+    table[1:4] = np.array([1.11, 0.0, 0.635]) + 0.5 * (lo + hi)
+    table[4:13] = np.eye(3).reshape(9)
+    table[13:16] = 0.5 * (hi - lo)
+    return table[None, :]
+
+
+def continuous_check_found(desc, x, scene, oracle_mod):
+    """planning_unit.cpp:92-101, 143-148: checkTrajectory with a CONTINUOUS contact
+    manager, collision margin 0 over the whole trajectory -- True when some step
+    pair's cast touches the scene (distance < 0), evaluated by the oracle's
+    CastCollisionEvaluator restatement (one cast per step pair)."""
+    from trajopt_amd import abi
+    from trajopt_amd.problems import Workload
+
+    d = abi.ProblemDesc.from_buffer_copy(desc)
+    d.coll_enabled, d.coll_continuous, d.coll_lvs = 1, 1, 1.7976931348623157e308
+    d.coll_margin, d.coll_buffer = 0.0, 0.0
+    d.coll_first_step, d.coll_last_step, d.coll_n_fixed = 0, d.n_steps - 1, 0
+    x = np.asarray(x, dtype=float)
+    w = Workload("check", d, x[None], np.zeros((1, max(d.n_cart, 0), 12)), np.asarray(scene)[None], x[None], None)
+    return len(oracle_mod.collision_rows(w, 0, x)) > 0

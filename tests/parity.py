@@ -23,12 +23,17 @@ and the problem is excused iff
   (reach)   some rerun reaches the GPU's outcome: same status, same flag and
             a trajectory within 1e-5 of the GPU's; or
   (spread)  the GPU has the oracle's status and flag, the reruns' trajectories
-            spread beyond 1e-5 from the oracle's own, and the GPU's total
-            cost lies within the reruns' cost range (+-2 %).
+            spread beyond 1e-5 from the oracle's own, and the GPU's trajectory
+            lies inside that cloud: its distance to the oracle is at most the
+            cloud's own largest distance to the oracle, every coordinate lies
+            within 1e-5 of the cloud's envelope (the coordinate-wise range of
+            the oracle and its reruns), and its total cost lies within the
+            reruns' cost range (+-2 %).
 A status or flag mismatch needs (reach).  "Some QP was unpolished" is no
 longer an excuse by itself.
 
-Every check is recorded (label, batch, strict, reached, spread) and
+Every check is recorded (label, batch, strict, reached, spread, and each
+excused problem with its distance to the oracle and to the nearest rerun) and
 tests/conftest.py writes the table to gpurun_out/parity_table.json at the end
 of the session; the pooled strict fraction is bounded there too.
 """
@@ -154,7 +159,11 @@ def check_parity(wl, oracle_mod, x, res, label="", min_strict=0.85, oracle=None,
                     costs = [ro[b].total_cost] + [c for _, _, _, c in mem]
                     lo, hi = min(costs), max(costs)
                     cg = res[b].total_cost
-                    if sp > TOL_X and lo - COST_RTOL * max(1.0, abs(lo)) <= cg <= hi + COST_RTOL * max(1.0, abs(hi)):
+                    cloud_x = np.stack([xo[b]] + [xm for xm, _, _, _ in mem])
+                    env_lo, env_hi = cloud_x.min(0), cloud_x.max(0)
+                    inside = bool(np.all(x[b] >= env_lo - TOL_X) and np.all(x[b] <= env_hi + TOL_X))
+                    if (sp > TOL_X and dx[b] <= sp and inside
+                            and lo - COST_RTOL * max(1.0, abs(lo)) <= cg <= hi + COST_RTOL * max(1.0, abs(hi))):
                         spread.append(b)
                         continue
                 still.append(b)
@@ -163,7 +172,14 @@ def check_parity(wl, oracle_mod, x, res, label="", min_strict=0.85, oracle=None,
                 unexplained = pending
                 break
     strict = B - len(miss)
+    excused = []
+    for kind, lst in (("reach", reached), ("spread", spread)):
+        for b in lst:
+            near = min(np.abs(xm - x[b]).max() for xm, _, _, _ in cloud.members[b])
+            excused.append({"problem": int(b), "kind": kind, "dx_oracle": float(dx[b]), "dx_nearest_rerun": float(near),
+                            "status": int(res[b].status), "oracle_status": int(ro[b].status)})
     rec = {"label": label, "batch": B, "strict": strict, "reached": len(reached), "spread": len(spread),
+           "excused": excused,
            "status_mismatch": int(sum(res[b].status != ro[b].status for b in range(B))),
            "median_dx": float(np.median(dx)) if B else 0.0,
            "max_dx_strict": float(max([dx[b] for b in range(B) if b not in miss], default=0.0)),

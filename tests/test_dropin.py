@@ -98,3 +98,17 @@ def test_collision_term_limits():
     with pytest.raises(host.HostError) as ei:
         host.lower_json(json.dumps(doc))
     assert "collision terms" in str(ei.value)
+
+
+def test_oracle_meets_planning_unit_assertions(oracle_mod):
+    """arm_around_table.json with the table as its exact box (dropin_cases):
+    the oracle meets planning_unit.cpp's EXPECTs -- the initial trajectory in
+    collision (:101), OPT_CONVERGED (:125), the final trajectory collision-free
+    (:148) -- under this build's sphere model of the PR2 arm."""
+    text = dc.text("arm_around_table.json")
+    scene = dc.arm_around_table_scene()
+    wl = _with_scene(text, scene)
+    assert dc.continuous_check_found(wl.desc, wl.init[0], wl.scene[0], oracle_mod)
+    x, res = oracle_mod.solve(wl)
+    assert res[0].status == 0
+    assert not dc.continuous_check_found(wl.desc, x[0], wl.scene[0], oracle_mod)

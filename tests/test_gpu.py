@@ -654,7 +654,7 @@ def test_full_batch_every_problem(oracle_mod, cfg, rank):
     check_parity(wl, oracle_mod, x, res, label=label, min_strict=0.9)
 
 
-def test_dynamic_problem_assignment_matches_static(monkeypatch):
+def test_dynamic_problem_assignment_matches_static(hip):
     """Batches larger than the resident slots run persistent workgroups that take
     problems from a counter (KernelArgs::work); the results are bitwise those of
     the one-workgroup-per-problem mapping, run after run (the counter resets
@@ -664,10 +664,13 @@ def test_dynamic_problem_assignment_matches_static(monkeypatch):
     x1, r1 = s.optimize()
     x2, r2 = s.optimize()  # a second launch on the same counter
     s.close()
-    monkeypatch.setenv("THIP_STATIC_DISPATCH", "1")
-    s = BatchTrustRegionSQP(wl)
-    x0, r0 = s.optimize()
-    s.close()
+    assert hip.thip_debug_set_path(abi.DEBUG_STATIC_DISPATCH) == 0
+    try:
+        s = BatchTrustRegionSQP(wl)
+        x0, r0 = s.optimize()
+        s.close()
+    finally:
+        hip.thip_debug_set_path(0)
     np.testing.assert_array_equal(x1, x0)
     np.testing.assert_array_equal(x2, x0)
     for a, b, c in zip(r0, r1, r2):
@@ -814,27 +817,24 @@ def test_frontdoor_json_batch_parity(oracle_mod, cfg, B):
 
 def test_frontdoor_reference_planning_config(oracle_mod):
     """The reference's arm_around_table.json (tests/golden/json), unchanged
-    (LVS_CONTINUOUS collision cost, JointPos goal constraint), with a box
-    standing in for the table mesh (parity with the oracle; contact values are
-    not pinned against Bullet)."""
-    import json
-    from pathlib import Path
-
+    (LVS_CONTINUOUS collision cost, JointPos goal constraint), with the table as
+    its exact box (Table.stl is a box, tests/dropin_cases.py): parity with the
+    oracle, and planning_unit.cpp's EXPECTs -- the initial trajectory in
+    collision (:101), OPT_CONVERGED (:125), the final trajectory collision-free
+    (:148).  Contact values are not pinned against Bullet (the arm is spheres)."""
+    import dropin_cases as dc
     from trajopt_amd import host
 
-    doc = json.loads((Path(__file__).resolve().parent / "golden" / "json" / "arm_around_table.json").read_text())
-    text = json.dumps(doc)  # evaluator_type 4: LVS_CONTINUOUS, as the reference's planning_unit runs it
-    table = np.zeros(16)
-    table[0] = abi.PRIM_BOX
-    table[1:4] = [1.11, 0.0, 0.635]  # table_joint origin (world = base_footprint, like the FK poses)
-    table[4:13] = np.eye(3).reshape(9)
-    table[13:16] = [0.35, 0.6, 0.03]
-    scenes = np.stack([table[None, :]] * 4)
+    text = dc.text("arm_around_table.json")
+    scenes = np.stack([dc.arm_around_table_scene()] * 4)
     x, res = host.solve_json_batch([text] * 4, scenes)
     assert len({r.status for r in res}) == 1
     np.testing.assert_array_equal(x[0], x[3])  # identical problems, identical answers
     wl = _lowered_workload([text] * 4, scenes)
     check_parity(wl, oracle_mod, x, res, label="arm_around_table")
+    assert dc.continuous_check_found(wl.desc, wl.init[0], scenes[0], oracle_mod)  # EXPECT_TRUE(found)
+    assert res[0].status == 0  # EXPECT_TRUE(status == OPT_CONVERGED)
+    assert not dc.continuous_check_found(wl.desc, x[0], scenes[0], oracle_mod)  # EXPECT_FALSE(found)
 
 
 def test_frontdoor_multi_device_shards():
@@ -855,6 +855,24 @@ def test_frontdoor_multi_device_shards():
         [(a.status, a.n_sqp_iters, a.n_qp_solves, a.total_cost) for a in r3]
     x2, _ = host.solve_json_batch(texts[:2], devices=[0, 0, 0])  # one entry idle
     np.testing.assert_array_equal(x2, x1[:2])
+
+
+def test_frontdoor_stream_batches_in_flight():
+    """trajopt::MultiDeviceBatchSQP::optimizeStream (thost_solve_json_stream): 5
+    batches with 3 in flight on 2 device entries of the box's GPU (6 contexts,
+    each reused for a later batch after its previous one is collected) return
+    each batch bit for bit as solved alone, in order."""
+    from trajopt_amd import host
+
+    wl = problems.make_workload("B", 5 * 24)
+    texts = [host.workload_to_json(wl, b) for b in range(wl.batch)]
+    batches = [texts[24 * j:24 * (j + 1)] for j in range(5)]
+    xs, rs = host.solve_json_stream(batches, devices=[0, 0], inflight=3)
+    for j in range(5):
+        x1, r1 = host.solve_json_batch(batches[j])
+        np.testing.assert_array_equal(xs[j], x1)
+        assert [(a.status, a.n_sqp_iters, a.total_cost) for a in rs[j]] == \
+            [(a.status, a.n_sqp_iters, a.total_cost) for a in r1]
 
 
 def test_frontdoor_cli(tmp_path):

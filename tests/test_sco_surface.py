@@ -132,3 +132,22 @@ def test_time_front_door_errors(built, edit, msg):
         host.lower_json(json.dumps(doc))
     assert msg in str(ei.value)
 
+
+
+def test_gpu_model_capacity_is_an_error_not_a_qp_failure(built):
+    """GpuModel refuses a convex subproblem beyond the dense-KKT capacity
+    (n + m > THIP_QP_MAX_KKT) with the limit named, before touching the device,
+    instead of returning CVX_FAILED (which would shrink the trust box and retry
+    the same impossible QP, then write /tmp/fail.lp)."""
+    import ctypes as C
+
+    from trajopt_amd import abi
+
+    L = C.CDLL(str(abi.LIB_DIR / "libsco_cases.so"))
+    L.sco_case_run.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_int),
+                               C.POINTER(C.c_longlong), C.c_char_p, C.c_int]
+    x = np.zeros(8)
+    counts = (C.c_int * 5)()
+    err = C.create_string_buffer(2048)
+    rc = L.sco_case_run(9, 0, x.ctypes.data_as(C.POINTER(C.c_double)), 8, counts, None, err, 2048)
+    assert rc != 0 and "THIP_QP_MAX_KKT" in err.value.decode(), err.value.decode()

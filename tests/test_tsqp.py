@@ -67,3 +67,18 @@ def test_product_argument_checks():
     _expect_error(s, "hinge cost must have inequality bounds!")
     s = tsqp.make_spec(np.zeros((2, D)), [dict(kind=tsqp.JOINT_POS, first=3, lower=[0.0] * D)])
     _expect_error(s, "term nodes out of range")
+    # n_coeffs must be 0, 1 or n_dof (the C entry validates it before reading the term)
+    s = tsqp.make_spec(np.zeros((4, D)), [dict(kind=tsqp.JOINT_VEL, penalty=tsqp.SQUARED, first=0, last=3,
+                                                coeffs=[1.0, 1.0, 1.0], lower=[0.0] * D)])
+    _expect_error(s, "n_coeffs must be 0, 1 or n_dof")
+
+
+def test_qp_capacity_is_reported_before_any_solve():
+    """A QP beyond the GPU solver's dense-KKT capacity (n + m > THIP_QP_MAX_KKT)
+    is refused with the limit named, before any QP is built (not as a QP failure
+    that would shrink the trust region and retry)."""
+    D = 16
+    terms = [dict(kind=tsqp.JOINT_VEL, penalty=tsqp.CONSTRAINT, first=0, last=tsqp.MAX_NODES - 1,
+                  lower=[0.01 * k] * D) for k in range(4)]
+    s = tsqp.make_spec(np.zeros((tsqp.MAX_NODES, D)), terms)
+    _expect_error(s, "THIP_QP_MAX_KKT")

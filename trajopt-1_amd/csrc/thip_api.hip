@@ -129,7 +129,7 @@ static int g_debug_path = 0;
 
 int thip_debug_set_path(int flags)
 {
-  if (flags & ~(THIP_DEBUG_NO_SEGMENT | THIP_DEBUG_FORCE_WIDE | THIP_DEBUG_NO_BRANCH))
+  if (flags & ~(THIP_DEBUG_NO_SEGMENT | THIP_DEBUG_FORCE_WIDE | THIP_DEBUG_NO_BRANCH | THIP_DEBUG_STATIC_DISPATCH))
     return THIP_E_INVALID;
   g_debug_path = flags;
   return THIP_OK;
@@ -919,9 +919,9 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
           hipSuccess)
     return fail(std::string("hipFuncSetAttribute(dynamic LDS): ") + hipGetErrorString(e));
   // dynamic problem assignment: one persistent workgroup per resident slot
-  // (KernelArgs::work), unless THIP_STATIC_DISPATCH is set
+  // (KernelArgs::work), unless THIP_DEBUG_STATIC_DISPATCH is set (one workgroup per problem)
   ctx->grid = batch;
-  if (!std::getenv("THIP_STATIC_DISPATCH"))
+  if (!(g_debug_path & THIP_DEBUG_STATIC_DISPATCH))
   {
     int per_cu = 0, n_cu = 0;
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&sqp_kernel), kBlock,

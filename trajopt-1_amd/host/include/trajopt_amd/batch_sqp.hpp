@@ -30,6 +30,9 @@ public:
   // the context's stream and returns; collect() waits for it and downloads.
   void submit();
   std::vector<sco::OptResults> collect();
+  // submit() for another batch of the same structure and size on this context
+  // (its device workspace is reused; collect() the previous batch first)
+  void submit(std::vector<LoweredProblem> probs);
   // HIP-event duration of the last fused launch (ms).
   double lastKernelMs() const;
   // Per-QP records of the next optimize() (thip_debug_trace, THIP_TRACE_W doubles each).
@@ -63,6 +66,17 @@ public:
   std::vector<sco::OptResults> optimize();
   // problems per device entry (0 for an entry beyond the batch size)
   const std::vector<int>& shardSizes() const { return sizes_; }
+
+  // A stream of batches (each sharded over `devices` as above) with `inflight`
+  // batches in flight per device entry: one context per (device entry, slot)
+  // on its own stream, batch j in slot j % inflight, a slot's previous batch
+  // collected just before the slot is reused.  The next batch's problems take
+  // the CUs the current batch's longest problems leave idle, so
+  // a stream runs at the pipelined rate instead of lone-batch latency.  Every
+  // batch of the stream must share batch 0's structure and size.  Results are
+  // per batch, in order, bitwise those of each batch solved alone.
+  static std::vector<std::vector<sco::OptResults>> optimizeStream(
+      const std::vector<std::vector<TrajOptProb::Ptr>>& batches, const std::vector<int>& devices, int inflight);
 
 private:
   std::vector<std::unique_ptr<BatchTrustRegionSQP>> shards_;

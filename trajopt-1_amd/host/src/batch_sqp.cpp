@@ -170,6 +170,23 @@ void BatchTrustRegionSQP::submit()
   check(thip_sqp_run(ctx_), "thip_sqp_run");
 }
 
+void BatchTrustRegionSQP::submit(std::vector<LoweredProblem> probs)
+{
+  if (probs.size() != probs_.size())
+    throw std::runtime_error("BatchTrustRegionSQP::submit: a batch of " + std::to_string(probs.size()) +
+                             " problems on a context of " + std::to_string(probs_.size()));
+  const thip_problem_desc d0 = structureOf(probs_[0]);
+  for (std::size_t b = 0; b < probs.size(); ++b)
+  {
+    const thip_problem_desc db = structureOf(probs[b]);
+    if (std::memcmp(&d0, &db, sizeof(d0)) != 0)
+      throw std::runtime_error("BatchTrustRegionSQP::submit: problem " + std::to_string(b) +
+                               " does not share the context's structure");
+  }
+  probs_ = std::move(probs);
+  submit();
+}
+
 std::vector<sco::OptResults> BatchTrustRegionSQP::collect()
 {
   const thip_problem_desc& d = probs_[0].desc;
@@ -226,6 +243,77 @@ std::vector<sco::OptResults> MultiDeviceBatchSQP::optimize()
   {
     std::vector<sco::OptResults> r = s->collect();
     out.insert(out.end(), std::make_move_iterator(r.begin()), std::make_move_iterator(r.end()));
+  }
+  return out;
+}
+
+std::vector<std::vector<sco::OptResults>> MultiDeviceBatchSQP::optimizeStream(
+    const std::vector<std::vector<TrajOptProb::Ptr>>& batches, const std::vector<int>& devices, int inflight)
+{
+  if (devices.empty())
+    throw std::runtime_error("MultiDeviceBatchSQP: no devices");
+  if (inflight < 1)
+    throw std::runtime_error("MultiDeviceBatchSQP: inflight must be >= 1");
+  std::vector<std::vector<sco::OptResults>> out(batches.size());
+  if (batches.empty())
+    return out;
+  const std::size_t B = batches[0].size(), W = devices.size(), K = static_cast<std::size_t>(inflight);
+  if (B == 0)
+    throw std::runtime_error("MultiDeviceBatchSQP: empty batch");
+  // the shard bounds of every batch: contiguous, sizes differing by at most one
+  std::vector<std::size_t> lo(W + 1, 0);
+  for (std::size_t r = 0; r < W; ++r)
+    lo[r + 1] = lo[r] + B / W + (r < B % W ? 1 : 0);
+  // slots[k][r]: the context of device entry r in slot k (created with its first batch)
+  std::vector<std::vector<std::unique_ptr<BatchTrustRegionSQP>>> slots(K);
+  std::vector<long> owner(K, -1);  // the batch a slot holds, -1 = none
+  auto collectSlot = [&](std::size_t k) {
+    if (owner[k] < 0)
+      return;
+    std::vector<sco::OptResults>& res = out[static_cast<std::size_t>(owner[k])];
+    for (auto& ctx : slots[k])
+      if (ctx)
+      {
+        std::vector<sco::OptResults> r = ctx->collect();
+        res.insert(res.end(), std::make_move_iterator(r.begin()), std::make_move_iterator(r.end()));
+      }
+    owner[k] = -1;
+  };
+  for (std::size_t j = 0; j < batches.size(); ++j)
+  {
+    if (batches[j].size() != B)
+      throw std::runtime_error("MultiDeviceBatchSQP::optimizeStream: batch " + std::to_string(j) + " has " +
+                               std::to_string(batches[j].size()) + " problems, batch 0 has " + std::to_string(B));
+    const std::vector<LoweredProblem> all = lowerAll(batches[j]);
+    const std::size_t k = j % K;
+    collectSlot(k);
+    if (slots[k].empty())
+      slots[k].resize(W);
+    for (std::size_t r = 0; r < W; ++r)
+    {
+      if (lo[r + 1] == lo[r])
+        continue;
+      std::vector<LoweredProblem> part(all.begin() + static_cast<long>(lo[r]), all.begin() + static_cast<long>(lo[r + 1]));
+      if (!slots[k][r])
+      {
+        slots[k][r] = std::make_unique<BatchTrustRegionSQP>(std::move(part), devices[r]);
+        slots[k][r]->submit();
+      }
+      else
+        slots[k][r]->submit(std::move(part));
+    }
+    owner[k] = static_cast<long>(j);
+  }
+  // drain in submission order
+  for (std::size_t n = 0; n < K; ++n)
+  {
+    std::size_t best = K;
+    for (std::size_t k = 0; k < K; ++k)
+      if (owner[k] >= 0 && (best == K || owner[k] < owner[best]))
+        best = k;
+    if (best == K)
+      break;
+    collectSlot(best);
   }
   return out;
 }

@@ -117,6 +117,59 @@ int thost_solve_json_batch(const char* const* json_texts, int batch, const doubl
   return thost_solve_json_batch_multi(json_texts, batch, scenes, n_prims, &device, 1, x, results, err, err_len);
 }
 
+namespace
+{
+void toResult(const sco::OptResults& r, thip_result& o)
+{
+  std::memset(&o, 0, sizeof(o));
+  o.status = static_cast<int>(r.status);
+  o.n_sqp_iters = r.n_sqp_iters;
+  o.n_qp_solves = r.n_qp_solves;
+  o.n_func_evals = r.n_func_evals;
+  o.n_admm_iters = r.n_admm_iters;
+  o.total_cost = r.total_cost;
+  o.max_cnt_viol = r.max_cnt_viol;
+  o.flags = r.flags;
+}
+}  // namespace
+
+int thost_solve_json_stream(const char* const* json_texts, int n_batches, int batch, const double* scenes, int n_prims,
+                            const int* devices, int n_devices, int inflight, double* x, thip_result* results, char* err,
+                            int err_len)
+{
+  try
+  {
+    if (!json_texts || n_batches <= 0 || batch <= 0 || !x || !devices || n_devices <= 0)
+      throw std::runtime_error("thost_solve_json_stream: bad arguments");
+    std::vector<std::vector<trajopt::TrajOptProb::Ptr>> batches(static_cast<std::size_t>(n_batches));
+    for (int j = 0; j < n_batches; ++j)
+      for (int b = 0; b < batch; ++b)
+      {
+        const std::size_t i = static_cast<std::size_t>(j) * batch + b;
+        batches[static_cast<std::size_t>(j)].push_back(
+            construct(json_texts[i], scenes ? scenes + i * static_cast<std::size_t>(n_prims) * 16 : nullptr, n_prims));
+      }
+    const auto res = trajopt::MultiDeviceBatchSQP::optimizeStream(
+        batches, std::vector<int>(devices, devices + n_devices), inflight);
+    std::size_t i = 0;
+    for (const auto& rb : res)
+      for (const auto& r : rb)
+      {
+        std::copy(r.x.begin(), r.x.end(), x + i * r.x.size());
+        if (results)
+          toResult(r, results[i]);
+        ++i;
+      }
+    setErr(err, err_len, "");
+    return 0;
+  }
+  catch (const std::exception& e)
+  {
+    setErr(err, err_len, e.what());
+    return -1;
+  }
+}
+
 int thost_solve_json_batch_multi(const char* const* json_texts, int batch, const double* scenes, int n_prims,
                                  const int* devices, int n_devices, double* x, thip_result* results, char* err,
                                  int err_len)

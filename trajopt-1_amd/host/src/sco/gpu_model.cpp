@@ -319,8 +319,10 @@ CvxOptStatus GpuModel::optimize()
   {
     thip_qp_destroy(qp_);
     qp_ = nullptr;
-    if (n + m > THIP_QP_MAX_KKT)
-      return CVX_FAILED;
+    if (n + m > THIP_QP_MAX_KKT)  // a capacity limit, not a QP failure: no shrink-and-retry, no fail.lp
+      throw std::runtime_error("GpuModel: the convex subproblem has " + std::to_string(n) + " variables and " +
+                               std::to_string(m) + " constraints; the GPU QP solver takes n + m <= THIP_QP_MAX_KKT (" +
+                               std::to_string(THIP_QP_MAX_KKT) + ")");
     if (thip_qp_create(config_.device, n, m, P.p.data(), P.i.data(), A.p.data(), A.i.data(), 1, &qp_) != THIP_OK)
       throw std::runtime_error(std::string("GpuModel: ") + thip_qp_last_error(nullptr));
     qp_Pp_ = P.p;

@@ -100,8 +100,10 @@ bool GpuQPSolver::setupNow()
   thip_qp_destroy(qp_);
   qp_ = nullptr;
   resident_ = false;
-  if (nv_ + nc_ > THIP_QP_MAX_KKT)
-    return false;  // the dense KKT factor bounds the problem size
+  if (nv_ + nc_ > THIP_QP_MAX_KKT)  // the dense KKT factor bounds the problem size: a limit, not a QP failure
+    throw std::runtime_error("GpuQPSolver: the QP has " + std::to_string(nv_) + " variables and " +
+                             std::to_string(nc_) + " constraints; the GPU QP solver takes n + m <= THIP_QP_MAX_KKT (" +
+                             std::to_string(THIP_QP_MAX_KKT) + ")");
   if (thip_qp_create(device_, static_cast<int>(nv_), static_cast<int>(nc_), P_.p.data(), P_.i.data(), A_.p.data(),
                      A_.i.data(), 1, &qp_) != THIP_OK)
     fail("thip_qp_create");

@@ -80,6 +80,8 @@ int thost_tsqp_solve(const tsqp_spec* s, int device, double* x, tsqp_result* res
       const tsqp_term& t = s->terms[i];
       if (t.first < 0 || t.last < t.first || t.last >= s->n_nodes)
         throw std::runtime_error("thost_tsqp_solve: term nodes out of range");
+      if (t.n_coeffs != 0 && t.n_coeffs != 1 && t.n_coeffs != D)
+        throw std::runtime_error("thost_tsqp_solve: term " + std::to_string(i) + ": n_coeffs must be 0, 1 or n_dof");
       const VectorXd coeffs(t.coeffs, t.coeffs + t.n_coeffs);
       const VectorXd lower(t.lower, t.lower + D);
       std::shared_ptr<ConstraintSet> cs;
@@ -125,6 +127,12 @@ int thost_tsqp_solve(const tsqp_spec* s, int device, double* x, tsqp_result* res
       }
     }
     problem->setup();
+    // the QP keeps one size for the whole solve: check the GPU solver's capacity up front
+    if (problem->getNumQPVars() + problem->getNumQPConstraints() > THIP_QP_MAX_KKT)
+      throw std::runtime_error("thost_tsqp_solve: the QP has " + std::to_string(problem->getNumQPVars()) +
+                               " variables and " + std::to_string(problem->getNumQPConstraints()) +
+                               " constraints; the GPU QP solver takes n + m <= THIP_QP_MAX_KKT (" +
+                               std::to_string(THIP_QP_MAX_KKT) + ")");
     auto qp_solver = std::make_shared<trajopt_sqp::GpuQPSolver>(device);
     qp_solver->settings = s->osqp;
     trajopt_sqp::TrustRegionSQPSolver solver(qp_solver);
@@ -169,4 +177,6 @@ int thost_tsqp_solve(const tsqp_spec* s, int device, double* x, tsqp_result* res
   }
 }
 
+int thost_tsqp_sizeof_spec(void) { return static_cast<int>(sizeof(tsqp_spec)); }
+int thost_tsqp_sizeof_result(void) { return static_cast<int>(sizeof(tsqp_result)); }
 }  // extern "C"

@@ -7,6 +7,7 @@
 //   1, 2   solver-interface-unit.cpp:130-231 ExprMult_test2 / ExprMult_test3
 //   3, 4   small-problems-unit.cpp:49-83     QuadraticSeparable / QuadraticNonseparable
 //   5..8   small-problems-unit.cpp:111-172   TP1, TP3, TP6, TP7
+//   9      a QP beyond THIP_QP_MAX_KKT (the capacity error)
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -43,6 +44,21 @@ CaseOut qpCase(int id, int device)
 {
   CaseOut o;
   GpuModel solver(*config(device));
+  if (id == 9)
+  {
+    // beyond the dense-KKT capacity: 2049 bounded variables (n + m = 4098 > THIP_QP_MAX_KKT)
+    VarVector vars;
+    for (int i = 0; i < 2049; ++i)
+      vars.push_back(solver.addVar("v" + std::to_string(i), -1, 1));
+    solver.update();
+    QuadExpr obj;
+    for (const Var& v : vars)
+      exprInc(obj, exprSquare(AffExpr(v)));
+    solver.setObjective(obj);
+    solver.update();
+    o.status = solver.optimize();  // throws: a capacity limit, not CVX_FAILED
+    return o;
+  }
   if (id == 0)
   {
     VarVector vars;
@@ -309,9 +325,9 @@ int sco_case_run(int id, int device, double* x, int cap, int* counts, long long*
 {
   try
   {
-    if (id < 0 || id > 8)
+    if (id < 0 || id > 9)
       throw std::runtime_error("unknown case");
-    const CaseOut o = id <= 2 ? qpCase(id, device) : sqpCase(id, device);
+    const CaseOut o = (id <= 2 || id == 9) ? qpCase(id, device) : sqpCase(id, device);
     if (static_cast<int>(o.x.size()) > cap)
       throw std::runtime_error("x capacity");
     std::memcpy(x, o.x.data(), o.x.size() * sizeof(double));

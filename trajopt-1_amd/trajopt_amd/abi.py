@@ -24,7 +24,7 @@ MAX_JVT = 4
 MAX_TTT = 2
 MAX_COLL_EXTRA = 3
 TRACE_W = 16  # THIP_TRACE_W
-DEBUG_NO_SEGMENT, DEBUG_FORCE_WIDE, DEBUG_NO_BRANCH = 1, 2, 4  # thip_debug_set_path flags
+DEBUG_NO_SEGMENT, DEBUG_FORCE_WIDE, DEBUG_NO_BRANCH, DEBUG_STATIC_DISPATCH = 1, 2, 4, 8  # thip_debug_set_path flags
 
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_CONTINUOUS, JOINT_PRISMATIC = 0, 1, 2, 3
 PRIM_SPHERE, PRIM_BOX, PRIM_CAPSULE = 0, 1, 2

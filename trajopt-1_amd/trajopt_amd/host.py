@@ -43,6 +43,10 @@ def load_host():
         L.thost_solve_json_batch_multi.argtypes = [C.POINTER(C.c_char_p), C.c_int, dp, C.c_int, C.POINTER(C.c_int),
                                                    C.c_int, dp, C.POINTER(abi.Result), C.c_char_p, C.c_int]
         L.thost_solve_json_batch_multi.restype = C.c_int
+        L.thost_solve_json_stream.argtypes = [C.POINTER(C.c_char_p), C.c_int, C.c_int, dp, C.c_int,
+                                              C.POINTER(C.c_int), C.c_int, C.c_int, dp, C.POINTER(abi.Result),
+                                              C.c_char_p, C.c_int]
+        L.thost_solve_json_stream.restype = C.c_int
         L.thost_solve_json.argtypes = [C.c_char_p, dp, C.c_int, C.c_int, dp, C.POINTER(abi.Result),
                                        C.POINTER(C.c_int), C.c_char_p, C.c_int]
         L.thost_solve_json.restype = C.c_int
@@ -100,6 +104,28 @@ def solve_json_batch(texts, scenes=None, device=0, devices=None):
     if rc != 0:
         raise HostError(err.value.decode())
     return x, list(res)
+
+
+def solve_json_stream(batches, scenes=None, devices=(0,), inflight=2):
+    """A stream of batches (lists of JSON texts of one structure and size)
+    through trajopt::MultiDeviceBatchSQP::optimizeStream with `inflight` batches
+    in flight per device entry -> (x [n_batches, B, N, D], results [n_batches][B])."""
+    L = load_host()
+    J, B = len(batches), len(batches[0])
+    desc, _, _, _ = lower_json(batches[0][0], None if scenes is None else scenes[0][0])
+    N, D = desc.n_steps, desc.chain.n_dof
+    sc = None if scenes is None else np.ascontiguousarray(scenes, dtype=np.float64).reshape(J * B, -1, 16)
+    n_prims = 0 if sc is None else sc.shape[1]
+    arr = (C.c_char_p * (J * B))(*[t.encode() for bt in batches for t in bt])
+    x = np.zeros((J * B, N, D))
+    res = (abi.Result * (J * B))()
+    err = C.create_string_buffer(4096)
+    dv = (C.c_int * len(devices))(*devices)
+    rc = L.thost_solve_json_stream(arr, J, B, _dp(sc), n_prims, dv, len(devices), inflight, _dp(x), res, err, 4096)
+    if rc != 0:
+        raise HostError(err.value.decode())
+    res = list(res)
+    return x.reshape(J, B, N, D), [res[j * B:(j + 1) * B] for j in range(J)]
 
 
 def solve_json(text: str, scene=None, device=0):

@@ -59,6 +59,10 @@ def _lib():
         L.thost_tsqp_solve.argtypes = [C.POINTER(Spec), C.c_int, C.POINTER(C.c_double), C.POINTER(Result),
                                        C.c_char_p, C.c_int]
         L.thost_tsqp_solve.restype = C.c_int
+        L.thost_tsqp_sizeof_spec.restype = C.c_int
+        L.thost_tsqp_sizeof_result.restype = C.c_int
+        if L.thost_tsqp_sizeof_spec() != C.sizeof(Spec) or L.thost_tsqp_sizeof_result() != C.sizeof(Result):
+            raise RuntimeError("tsqp_spec / tsqp_result layout mismatch between Python and the host library")
         L._tsqp_ready = True
     return L
 
