@@ -588,6 +588,15 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
 int thip_qp_solve(thip_qp* qp, const double* P_values, const double* q, const double* A_values, const double* l,
                   const double* u, const thip_osqp_settings* settings, const double* warm_x, const double* warm_y,
                   const double* warm_rho, double* x, double* y, thip_qp_info* info);
+/* thip_qp_solve for the first `count` QPs of the batch (1 <= count <= batch), QP k
+ * warm started from warm_x / warm_y only when warm_mask[k] != 0 (warm_mask NULL: all
+ * of them, as thip_qp_solve), with warm_rho[k] its initial rho (NULL: settings->rho):
+ * one launch for the QPs of many problems' host SQP loops that share a pattern
+ * (sco::GpuQPBatcher).  Arrays are [count][...]. */
+int thip_qp_solve_some(thip_qp* qp, int count, const double* P_values, const double* q, const double* A_values,
+                       const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
+                       const double* warm_y, const int* warm_mask, const double* warm_rho, double* x, double* y,
+                       thip_qp_info* info);
 void thip_qp_destroy(thip_qp* qp);
 const char* thip_qp_last_error(thip_qp* qp); /* NULL: the last thip_qp_create failure */
 

@@ -44,6 +44,13 @@ int thost_lower_json(const char* json_text, const double* scene, int n_prims, th
 int thost_solve_json_batch(const char* const* json_texts, int batch, const double* scenes, int n_prims, int device,
                            double* x, thip_result* results, char* err, int err_len);
 
+/* A batch with problems the fused kernel does not lower runs each problem's host
+ * SQP loop on its own thread, every QP round of the batch in one launch per
+ * sparsity pattern (trajopt::BatchTrustRegionSQP's host-loop mode, sco::GpuQPBatcher);
+ * x then holds [batch][n_steps][n_dof (+ 1 with use_time)].  This reports the QP
+ * launches and QPs of the calling thread's last batch solve (0 for a fused-kernel batch). */
+void thost_last_batch_qp_stats(long long* launches, long long* qps);
+
 /* thost_solve_json_batch sharded over n_devices HIP devices of this process
  * (trajopt::MultiDeviceBatchSQP: contiguous shards, sizes differing by at most
  * one, all shards running concurrently; a device may be listed more than once). */

@@ -75,9 +75,8 @@ def cartpose_jointacc():
 def collision_jointjerk(evaluator=2):
     """A 10-waypoint right-arm move over a table-top scene: JointVel cost, a
     collision cost (evaluator 1 DISCRETE / 2 LVS_DISCRETE / 4 LVS_CONTINUOUS,
-    lvs 0.2: 250-500 contacts per QP with the JSON's 0.5 m buffer, inside the
-    generic QP solver's n + m <= THIP_QP_MAX_KKT), a JointJerk cost (not
-    lowered) and a JointPos goal constraint."""
+    lvs 0.2) against table_scene(), a JointJerk cost (not lowered) and a
+    JointPos goal constraint."""
     n = 10
     start = [-0.9, 0.2, -1.2, -1.4, 0.3, -0.6, 0.1]
     end = [0.4, 0.3, -0.8, -0.9, -0.2, -0.4, 0.5]
@@ -98,18 +97,14 @@ def collision_jointjerk(evaluator=2):
     return json.dumps(doc)
 
 
-# table-top scene for collision_jointjerk (THIP_PRIM_* records, world frame): a
-# table top under the arm's sweep and a sphere near its path
+# the obstacle of collision_jointjerk (THIP_PRIM_* record, world frame): a 0.1 m
+# sphere near the arm's path -- 50-90 contacts per QP with the JSON's 0.5 m buffer,
+# a size the generic path's dense-KKT QP solver runs in seconds
 def table_scene():
-    box = np.zeros(16)
-    box[0] = 1  # BOX
-    box[1:4] = [0.6, -0.25, 0.55]
-    box[4:13] = np.eye(3).reshape(-1)
-    box[13:16] = [0.3, 0.4, 0.04]
     sph = np.zeros(16)
     sph[0] = 0  # SPHERE
-    sph[1:5] = [0.45, -0.4, 0.8, 0.08]
-    return np.stack([box, sph])
+    sph[1:5] = [0.8, -0.5, 1.2, 0.1]
+    return sph[None, :]
 
 
 # arm_around_table.urdf:71-94: table_link at (1.11, 0, 0.635) off base_footprint; its

@@ -71,7 +71,7 @@ def test_mixed_problems_lower_for_the_generic_path(oracle_mod):
     d, *_ = host.lower_json(dc.cartpose_jointacc())
     assert d.n_cart == 1 and d.n_jdt == 2
     d, *_ = host.lower_json(dc.collision_jointjerk(), scene=dc.table_scene())
-    assert d.coll_enabled == 1 and d.n_jdt == 1 and d.n_prims == 2
+    assert d.coll_enabled == 1 and d.n_jdt == 1 and d.n_prims == 1
     for text in (dc.cartpose_jointacc(), dc.collision_jointjerk()):
         sc = dc.table_scene() if "collision" in text else None
         wl = dc.json_workload(text, host) if sc is None else _with_scene(text, sc)

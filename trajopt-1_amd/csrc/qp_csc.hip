@@ -104,6 +104,7 @@ struct QpArgs
   thip_osqp_settings s;
   const double *Pv, *qv, *Av, *lv, *uv;       // [batch][...]
   const double *x_ws, *y_ws, *rho_ws;         // warm start (null = cold)
+  const int* ws_mask;                         // per QP: warm start (1) or cold (0); null = all as x_ws / y_ws
   double *x_out, *y_out;                      // [batch][n], [batch][m]
   thip_qp_info* info;                         // [batch]
   double* ws;                                 // [batch][stride]
@@ -966,7 +967,7 @@ __global__ __launch_bounds__(kQB) void qp_csc_kernel(QpArgs args)
   }
   // warm start (osqp_warm_start: x / D, y / E * c, z = A x) or cold start
   double *X = q.a(W_X), *Z = q.a(W_Z), *Y = q.a(W_Y);
-  if (args.x_ws && args.y_ws)
+  if (args.x_ws && args.y_ws && (!args.ws_mask || args.ws_mask[b]))
   {
     const double *DI = q.a(W_DI), *EI = q.a(W_EI);
     const bool sc = args.s.scaling > 0;
@@ -1390,7 +1391,7 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
     return fail(std::string("hipSetDevice: ") + hipGetErrorString(e));
   if ((e = hipMalloc(&q->d_idx, idx.size() * sizeof(int))) != hipSuccess ||
       (e = hipMalloc(&q->d_ws, static_cast<size_t>(q->pat.stride) * batch * sizeof(double))) != hipSuccess ||
-      (e = hipMalloc(&q->d_in, static_cast<size_t>(q->in_doubles + 2LL * n + m + 1) * batch * sizeof(double))) !=
+      (e = hipMalloc(&q->d_in, static_cast<size_t>(q->in_doubles + 2LL * n + m + 2) * batch * sizeof(double))) !=
           hipSuccess ||
       (e = hipMalloc(&q->d_out, static_cast<size_t>(n + m) * batch * sizeof(double))) != hipSuccess ||
       (e = hipMalloc(&q->d_info, sizeof(thip_qp_info) * batch)) != hipSuccess)
@@ -1417,7 +1418,23 @@ int thip_qp_solve(thip_qp* q, const double* P_values, const double* qvec, const 
 {
   if (!q)
     return THIP_E_INVALID;
-  const int n = q->n, m = q->m, B = q->batch;
+  return thip_qp_solve_some(q, q->batch, P_values, qvec, A_values, l, u, settings, warm_x, warm_y, nullptr, warm_rho,
+                            x, y, info);
+}
+
+int thip_qp_solve_some(thip_qp* q, int count, const double* P_values, const double* qvec, const double* A_values,
+                       const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
+                       const double* warm_y, const int* warm_mask, const double* warm_rho, double* x, double* y,
+                       thip_qp_info* info)
+{
+  if (!q)
+    return THIP_E_INVALID;
+  if (count < 1 || count > q->batch)
+  {
+    q->err = "thip_qp_solve_some: count must be in [1, batch]";
+    return THIP_E_INVALID;
+  }
+  const int n = q->n, m = q->m, B = count;
   // (an empty P -- a linear objective -- or an empty A may come with NULL values)
   if ((!P_values && q->nnz_p) || !qvec || (!A_values && q->nnz_a) || (m && (!l || !u)) || !settings || !x || !info)
   {
@@ -1455,8 +1472,12 @@ int thip_qp_solve(thip_qp* q, const double* P_values, const double* qvec, const 
     return true;
   };
   const bool ws = warm_x && warm_y;
+  // the per-QP warm-start flags travel behind the rho values (the buffer holds B + batch doubles there)
+  int* dmask = reinterpret_cast<int*>(drw + q->batch);
   if (!h2d(dP, P_values, np) || !h2d(dA, A_values, na) || !h2d(dq, qvec, nn) || !h2d(dl, l, mm) || !h2d(du, u, mm) ||
-      (ws && (!h2d(dxw, warm_x, nn) || !h2d(dyw, warm_y, mm))) || (warm_rho && !h2d(drw, warm_rho, B)))
+      (ws && (!h2d(dxw, warm_x, nn) || !h2d(dyw, warm_y, mm))) || (warm_rho && !h2d(drw, warm_rho, B)) ||
+      (ws && warm_mask &&
+       (e = hipMemcpy(dmask, warm_mask, static_cast<size_t>(B) * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess))
   {
     q->err = std::string("hipMemcpy: ") + hipGetErrorString(e);
     return THIP_E_HIP;
@@ -1473,6 +1494,7 @@ int thip_qp_solve(thip_qp* q, const double* P_values, const double* qvec, const 
   a.x_ws = ws ? dxw : nullptr;
   a.y_ws = ws ? dyw : nullptr;
   a.rho_ws = warm_rho ? drw : nullptr;
+  a.ws_mask = (ws && warm_mask) ? dmask : nullptr;
   a.x_out = q->d_out;
   a.y_out = q->d_out + nn;
   a.info = q->d_info;

@@ -14,8 +14,14 @@ namespace trajopt
 class BatchTrustRegionSQP
 {
 public:
-  // Checks that every problem shares problem 0's structure (steps, chain,
-  // terms, parameters, scene size) and allocates the device workspace.
+  // Lowerable problems (every term in the descriptor): checks that every problem
+  // shares problem 0's structure (steps, chain, terms, parameters, scene size)
+  // and allocates the fused kernel's device workspace.  A batch with problems
+  // the kernel does not lower (JointAcc / JointJerk, time terms, custom terms,
+  // single waypoints, several collision terms) runs every problem's host loop
+  // (sco::BasicTrustRegionSQP) on its own host thread, the kinematic terms
+  // evaluated on the device and the QPs of all loops batched into one launch
+  // per sparsity pattern (sco::GpuQPBatcher); results are each problem's own.
   explicit BatchTrustRegionSQP(const std::vector<TrajOptProb::Ptr>& probs, int device = 0);
   explicit BatchTrustRegionSQP(std::vector<LoweredProblem> probs, int device = 0);
   ~BatchTrustRegionSQP();
@@ -43,14 +49,24 @@ public:
   // (A single problem observed through sco::BasicTrustRegionSQP -- callbacks or
   // log_results -- runs the host loop, which writes all four logs.)
   void writeSolverLog(int b, const std::string& path) const;
-  int batch() const { return static_cast<int>(probs_.size()); }
+  int batch() const { return static_cast<int>(generic_.empty() ? probs_.size() : generic_.size()); }
+  // true: the batch runs the host loops with batched QPs (see the constructor)
+  bool hostLoops() const { return !generic_.empty(); }
+  // host-loop batches: QP launches and QPs of the last optimize() (sco::GpuQPBatcher)
+  long long qpLaunches() const { return qp_launches_; }
+  long long qpSolves() const { return qp_solves_; }
 
 private:
   void init(int device);
   void check(int rc, const char* what) const;
+  std::vector<sco::OptResults> optimizeHostLoops();
   std::vector<LoweredProblem> probs_;
   struct thip_ctx* ctx_ = nullptr;
   int trace_cap_ = 0;
+  std::vector<TrajOptProb::Ptr> generic_;  // host-loop batch
+  int device_ = 0;
+  std::vector<sco::OptResults> generic_results_;
+  long long qp_launches_ = 0, qp_solves_ = 0;
 };
 
 // One batch sharded over several HIP devices of this process (SURVEY.md §8e:
@@ -64,6 +80,9 @@ class MultiDeviceBatchSQP
 public:
   MultiDeviceBatchSQP(const std::vector<TrajOptProb::Ptr>& probs, const std::vector<int>& devices);
   std::vector<sco::OptResults> optimize();
+  // host-loop shards: QP launches and QPs of the last optimize(), summed over the shards
+  long long qpLaunches() const;
+  long long qpSolves() const;
   // problems per device entry (0 for an entry beyond the batch size)
   const std::vector<int>& shardSizes() const { return sizes_; }
 
@@ -95,6 +114,8 @@ class BasicTrustRegionSQP : public sco::BasicTrustRegionSQP
 {
 public:
   explicit BasicTrustRegionSQP(const TrajOptProb::Ptr& prob, int device = 0);
+  // the reference's host loop whatever the problem (optimizers.cpp:699-991)
+  sco::OptStatus optimizeHostLoop() { return optimizeGeneric(); }
 };
 
 // Upper bound on the per-QP trace records of one problem under param (the

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "trajopt_hip.h"
+#include "trajopt_sco/gpu_qp_batcher.hpp"
 #include "trajopt_sco/solver_interface.hpp"
 
 namespace sco
@@ -55,6 +56,9 @@ public:
   // HIP device of the following solves
   void setDevice(int device);
   int device() const { return config_.device; }
+  // solve through a batcher shared with other models (one launch per pattern for
+  // the QPs of many problems' host loops); null: one launch per QP
+  void setBatcher(GpuQPBatcher::Ptr b) { batcher_ = std::move(b); }
 
   // diagnostics of the last solve
   const thip_qp_info& lastInfo() const { return info_; }
@@ -70,6 +74,9 @@ private:
   void buildObjective(Csc& P, DblVec& q) const;
   void buildConstraints(Csc& A, DblVec& l, DblVec& u) const;
   static bool bytesEqual(const Csc& a, const Csc& b);
+  void solveDirect(const Csc& P, const Csc& A, const DblVec& q, const DblVec& l, const DblVec& u,
+                   const thip_osqp_settings& s, bool ws, DblVec& x, DblVec& y);
+  CvxOptStatus finishSolve(Csc&& P, Csc&& A, const DblVec& x, const DblVec& y);
 
   GpuModelConfig config_;
   std::mutex mutex_;
@@ -90,5 +97,6 @@ private:
   std::vector<int> qp_Pp_, qp_Pi_, qp_Ap_, qp_Ai_;
   thip_qp_info info_{};
   long long admm_total_{ 0 };
+  GpuQPBatcher::Ptr batcher_;
 };
 }  // namespace sco

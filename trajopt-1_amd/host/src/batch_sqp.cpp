@@ -8,6 +8,9 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
+
+#include "trajopt_sco/gpu_qp_batcher.hpp"
 
 namespace trajopt
 {
@@ -100,10 +103,75 @@ void writeSolverLog(const std::string& path, const std::vector<double>& rec)
 }  // namespace
 
 // ------------------------------------------------------------ BatchTrustRegionSQP
-BatchTrustRegionSQP::BatchTrustRegionSQP(const std::vector<TrajOptProb::Ptr>& probs, int device)
-  : probs_(lowerAll(probs))
+namespace
 {
+bool allLowerable(const std::vector<TrajOptProb::Ptr>& probs)
+{
+  for (const auto& p : probs)
+  {
+    if (!p)
+      throw std::runtime_error("BatchTrustRegionSQP: null problem");
+    if (!p->lowerable())
+      return false;
+  }
+  return true;
+}
+}  // namespace
+
+BatchTrustRegionSQP::BatchTrustRegionSQP(const std::vector<TrajOptProb::Ptr>& probs, int device) : device_(device)
+{
+  if (probs.empty())
+    throw std::runtime_error("BatchTrustRegionSQP: empty batch");
+  if (!allLowerable(probs))
+  {
+    generic_ = probs;
+    return;
+  }
+  probs_ = lowerAll(probs);
   init(device);
+}
+
+std::vector<sco::OptResults> BatchTrustRegionSQP::optimizeHostLoops()
+{
+  const std::size_t B = generic_.size();
+  auto batcher = std::make_shared<sco::GpuQPBatcher>();
+  std::vector<sco::OptResults> out(B);
+  std::vector<std::string> errs(B);
+  // every client registered before any thread starts, so the first rounds batch all of them
+  std::vector<std::unique_ptr<sco::GpuQPBatcherClient>> clients;
+  for (std::size_t b = 0; b < B; ++b)
+    clients.push_back(std::make_unique<sco::GpuQPBatcherClient>(batcher));
+  std::vector<std::thread> threads;
+  threads.reserve(B);
+  for (std::size_t b = 0; b < B; ++b)
+    threads.emplace_back([&, b]() {
+      try
+      {
+        const TrajOptProb::Ptr& prob = generic_[b];
+        BasicTrustRegionSQP opt(prob, device_);
+        auto* gm = dynamic_cast<sco::GpuModel*>(prob->getModel().get());
+        if (!gm)
+          throw std::runtime_error("BatchTrustRegionSQP: problem " + std::to_string(b) + " has no GpuModel");
+        gm->setBatcher(batcher);
+        opt.initialize(trajToDblVec(prob->GetInitTraj()));
+        opt.optimizeHostLoop();
+        out[b] = opt.results();
+        gm->setBatcher(nullptr);
+      }
+      catch (const std::exception& e)
+      {
+        errs[b] = e.what();
+      }
+      clients[b].reset();  // leave: the others' rounds no longer wait for this problem
+    });
+  for (auto& t : threads)
+    t.join();
+  qp_launches_ = batcher->launches();
+  qp_solves_ = batcher->qps();
+  for (std::size_t b = 0; b < B; ++b)
+    if (!errs[b].empty())
+      throw std::runtime_error("BatchTrustRegionSQP: problem " + std::to_string(b) + ": " + errs[b]);
+  return out;
 }
 
 BatchTrustRegionSQP::BatchTrustRegionSQP(std::vector<LoweredProblem> probs, int device) : probs_(std::move(probs))
@@ -137,7 +205,12 @@ void BatchTrustRegionSQP::check(int rc, const char* what) const
     throw std::runtime_error(std::string(what) + ": " + thip_last_error(ctx_));
 }
 
-void BatchTrustRegionSQP::setStream(void* stream) { check(thip_set_stream(ctx_, stream), "thip_set_stream"); }
+void BatchTrustRegionSQP::setStream(void* stream)
+{
+  if (!generic_.empty())
+    return;  // (host loops: each problem's QPs run on the batcher's launches)
+  check(thip_set_stream(ctx_, stream), "thip_set_stream");
+}
 
 std::vector<sco::OptResults> BatchTrustRegionSQP::optimize()
 {
@@ -147,6 +220,11 @@ std::vector<sco::OptResults> BatchTrustRegionSQP::optimize()
 
 void BatchTrustRegionSQP::submit()
 {
+  if (!generic_.empty())
+  {
+    generic_results_ = optimizeHostLoops();  // (host loops: synchronous)
+    return;
+  }
   const thip_problem_desc& d = probs_[0].desc;
   const int B = batch(), N = d.n_steps, D = d.chain.n_dof;
   std::vector<double> init, tgt, jpt, scene;
@@ -172,6 +250,8 @@ void BatchTrustRegionSQP::submit()
 
 void BatchTrustRegionSQP::submit(std::vector<LoweredProblem> probs)
 {
+  if (!generic_.empty())
+    throw std::runtime_error("BatchTrustRegionSQP::submit: a host-loop batch takes its problems at construction");
   if (probs.size() != probs_.size())
     throw std::runtime_error("BatchTrustRegionSQP::submit: a batch of " + std::to_string(probs.size()) +
                              " problems on a context of " + std::to_string(probs_.size()));
@@ -189,6 +269,8 @@ void BatchTrustRegionSQP::submit(std::vector<LoweredProblem> probs)
 
 std::vector<sco::OptResults> BatchTrustRegionSQP::collect()
 {
+  if (!generic_.empty())
+    return std::move(generic_results_);
   const thip_problem_desc& d = probs_[0].desc;
   const int B = batch(), N = d.n_steps, D = d.chain.n_dof;
   std::vector<double> x(static_cast<std::size_t>(B) * N * D);
@@ -219,8 +301,27 @@ MultiDeviceBatchSQP::MultiDeviceBatchSQP(const std::vector<TrajOptProb::Ptr>& pr
     throw std::runtime_error("MultiDeviceBatchSQP: no devices");
   if (probs.empty())
     throw std::runtime_error("MultiDeviceBatchSQP: empty batch");
+  const std::size_t W = devices.size();
+  if (!allLowerable(probs))
+  {
+    // host-loop shards (BatchTrustRegionSQP's batched QPs), one per device entry
+    const std::size_t B = probs.size();
+    std::size_t lo = 0;
+    for (std::size_t r = 0; r < W; ++r)
+    {
+      const std::size_t n = B / W + (r < B % W ? 1 : 0);
+      sizes_.push_back(static_cast<int>(n));
+      if (n == 0)
+        continue;
+      shards_.push_back(std::make_unique<BatchTrustRegionSQP>(
+          std::vector<TrajOptProb::Ptr>(probs.begin() + static_cast<long>(lo), probs.begin() + static_cast<long>(lo + n)),
+          devices[r]));
+      lo += n;
+    }
+    return;
+  }
   const std::vector<LoweredProblem> all = lowerAll(probs);
-  const std::size_t B = all.size(), W = devices.size();
+  const std::size_t B = all.size();
   std::size_t lo = 0;
   for (std::size_t r = 0; r < W; ++r)
   {
@@ -236,6 +337,34 @@ MultiDeviceBatchSQP::MultiDeviceBatchSQP(const std::vector<TrajOptProb::Ptr>& pr
 
 std::vector<sco::OptResults> MultiDeviceBatchSQP::optimize()
 {
+  if (!shards_.empty() && shards_[0]->hostLoops())
+  {
+    // host-loop shards run concurrently, each from its own thread
+    std::vector<std::vector<sco::OptResults>> part(shards_.size());
+    std::vector<std::string> errs(shards_.size());
+    std::vector<std::thread> th;
+    for (std::size_t k = 0; k < shards_.size(); ++k)
+      th.emplace_back([&, k]() {
+        try
+        {
+          part[k] = shards_[k]->optimize();
+        }
+        catch (const std::exception& e)
+        {
+          errs[k] = e.what();
+        }
+      });
+    for (auto& t : th)
+      t.join();
+    std::vector<sco::OptResults> out;
+    for (std::size_t k = 0; k < shards_.size(); ++k)
+    {
+      if (!errs[k].empty())
+        throw std::runtime_error(errs[k]);
+      out.insert(out.end(), std::make_move_iterator(part[k].begin()), std::make_move_iterator(part[k].end()));
+    }
+    return out;
+  }
   for (auto& s : shards_)
     s->submit();
   std::vector<sco::OptResults> out;
@@ -318,7 +447,22 @@ std::vector<std::vector<sco::OptResults>> MultiDeviceBatchSQP::optimizeStream(
   return out;
 }
 
-double BatchTrustRegionSQP::lastKernelMs() const { return thip_last_kernel_ms(ctx_); }
+long long MultiDeviceBatchSQP::qpLaunches() const
+{
+  long long n = 0;
+  for (const auto& s : shards_)
+    n += s->qpLaunches();
+  return n;
+}
+long long MultiDeviceBatchSQP::qpSolves() const
+{
+  long long n = 0;
+  for (const auto& s : shards_)
+    n += s->qpSolves();
+  return n;
+}
+
+double BatchTrustRegionSQP::lastKernelMs() const { return generic_.empty() ? thip_last_kernel_ms(ctx_) : 0.0; }
 
 void BatchTrustRegionSQP::writeSolverLog(int b, const std::string& path) const
 {
@@ -331,6 +475,9 @@ void BatchTrustRegionSQP::writeSolverLog(int b, const std::string& path) const
 
 void BatchTrustRegionSQP::enableTrace(int capacity)
 {
+  if (!generic_.empty())
+    throw std::runtime_error("BatchTrustRegionSQP::enableTrace: the fused kernel's trace (a host-loop batch logs "
+                             "through sco::BasicTrustRegionSQPParameters::log_results)");
   check(thip_debug_trace(ctx_, capacity), "thip_debug_trace");
   trace_cap_ = capacity;
 }

@@ -10,6 +10,8 @@
 
 namespace
 {
+thread_local long long g_batch_qp_launches = 0, g_batch_qp_solves = 0;
+
 void setErr(char* err, int err_len, const std::string& msg)
 {
   if (!err || err_len <= 0)
@@ -111,6 +113,14 @@ int thost_solve_json(const char* json_text, const double* scene, int n_prims, in
   }
 }
 
+void thost_last_batch_qp_stats(long long* launches, long long* qps)
+{
+  if (launches)
+    *launches = g_batch_qp_launches;
+  if (qps)
+    *qps = g_batch_qp_solves;
+}
+
 int thost_solve_json_batch(const char* const* json_texts, int batch, const double* scenes, int n_prims, int device,
                            double* x, thip_result* results, char* err, int err_len)
 {
@@ -186,6 +196,8 @@ int thost_solve_json_batch_multi(const char* const* json_texts, int batch, const
                                 n_prims));
     trajopt::MultiDeviceBatchSQP opt(probs, std::vector<int>(devices, devices + n_devices));
     const auto res = opt.optimize();
+    g_batch_qp_launches = opt.qpLaunches();
+    g_batch_qp_solves = opt.qpSolves();
     for (int b = 0; b < batch; ++b)
     {
       const auto& r = res[static_cast<std::size_t>(b)];

@@ -314,15 +314,51 @@ CvxOptStatus GpuModel::optimize()
   thip_osqp_settings s = config_.settings;
   if (allow_ws)
     s.rho = prev_rho_;
+  if (n + m > THIP_QP_MAX_KKT)  // a capacity limit, not a QP failure: no shrink-and-retry, no fail.lp
+    throw std::runtime_error("GpuModel: the convex subproblem has " + std::to_string(n) + " variables and " +
+                             std::to_string(m) + " constraints; the GPU QP solver takes n + m <= THIP_QP_MAX_KKT (" +
+                             std::to_string(THIP_QP_MAX_KKT) + ")");
+  DblVec x(static_cast<std::size_t>(n)), y(static_cast<std::size_t>(std::max(m, 1)));
+  const bool ws = allow_ws && static_cast<int>(prev_x_.size()) >= n && static_cast<int>(prev_y_.size()) >= m;
+  if (batcher_)
+  {
+    GpuQPBatcher::Request r;
+    r.device = config_.device;
+    r.n = n;
+    r.m = m;
+    r.Pp = &P.p;
+    r.Pi = &P.i;
+    r.Ap = &A.p;
+    r.Ai = &A.i;
+    r.Px = &P.x;
+    r.Ax = &A.x;
+    r.q = &q;
+    r.l = &l;
+    r.u = &u;
+    r.settings = s;
+    r.warm = ws;
+    r.wx = &prev_x_;
+    r.wy = &prev_y_;
+    r.x = &x;
+    r.y = &y;
+    r.info = &info_;
+    batcher_->solve(r);
+    y.resize(static_cast<std::size_t>(std::max(m, 1)));
+  }
+  else
+    solveDirect(P, A, q, l, u, s, ws, x, y);
+  return finishSolve(std::move(P), std::move(A), x, y);
+}
+
+void GpuModel::solveDirect(const Csc& P, const Csc& A, const DblVec& q, const DblVec& l, const DblVec& u,
+                           const thip_osqp_settings& s, bool ws, DblVec& x, DblVec& y)
+{
+  const int n = P.n, m = A.m;
   // device pattern: rebuilt when it changes
   if (!qp_ || qp_Pp_ != P.p || qp_Pi_ != P.i || qp_Ap_ != A.p || qp_Ai_ != A.i)
   {
     thip_qp_destroy(qp_);
     qp_ = nullptr;
-    if (n + m > THIP_QP_MAX_KKT)  // a capacity limit, not a QP failure: no shrink-and-retry, no fail.lp
-      throw std::runtime_error("GpuModel: the convex subproblem has " + std::to_string(n) + " variables and " +
-                               std::to_string(m) + " constraints; the GPU QP solver takes n + m <= THIP_QP_MAX_KKT (" +
-                               std::to_string(THIP_QP_MAX_KKT) + ")");
     if (thip_qp_create(config_.device, n, m, P.p.data(), P.i.data(), A.p.data(), A.i.data(), 1, &qp_) != THIP_OK)
       throw std::runtime_error(std::string("GpuModel: ") + thip_qp_last_error(nullptr));
     qp_Pp_ = P.p;
@@ -330,12 +366,14 @@ CvxOptStatus GpuModel::optimize()
     qp_Ap_ = A.p;
     qp_Ai_ = A.i;
   }
-  DblVec x(static_cast<std::size_t>(n)), y(static_cast<std::size_t>(std::max(m, 1)));
-  const bool ws = allow_ws && static_cast<int>(prev_x_.size()) >= n && static_cast<int>(prev_y_.size()) >= m;
   const int rc = thip_qp_solve(qp_, P.x.data(), q.data(), A.x.data(), l.data(), u.data(), &s, ws ? prev_x_.data() : nullptr,
                                ws ? prev_y_.data() : nullptr, nullptr, x.data(), y.data(), &info_);
   if (rc != THIP_OK)
     throw std::runtime_error(std::string("GpuModel: thip_qp_solve: ") + thip_qp_last_error(qp_));
+}
+
+CvxOptStatus GpuModel::finishSolve(Csc&& P, Csc&& A, const DblVec& x, const DblVec& y)
+{
   // the next solve's warm start
   prev_P_ = std::move(P);
   prev_A_ = std::move(A);

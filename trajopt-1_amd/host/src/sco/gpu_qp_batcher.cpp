@@ -1,0 +1,163 @@
+// GpuQPBatcher (gpu_qp_batcher.hpp).
+#include "trajopt_sco/gpu_qp_batcher.hpp"
+
+#include <cstring>
+#include <stdexcept>
+
+namespace sco
+{
+namespace
+{
+void appendInts(std::string& k, const std::vector<int>& v)
+{
+  const std::size_t o = k.size();
+  k.resize(o + v.size() * sizeof(int));
+  if (!v.empty())
+    std::memcpy(&k[o], v.data(), v.size() * sizeof(int));
+}
+
+// the group a QP launches with: device, sizes, patterns and every setting but
+// rho (each QP's rho travels in warm_rho)
+std::string groupKey(const GpuQPBatcher::Request& r)
+{
+  std::string k;
+  const int head[3] = { r.device, r.n, r.m };
+  k.append(reinterpret_cast<const char*>(head), sizeof(head));
+  thip_osqp_settings s = r.settings;
+  s.rho = 0;
+  k.append(reinterpret_cast<const char*>(&s), sizeof(s));
+  for (const std::vector<int>* v : { r.Pp, r.Pi, r.Ap, r.Ai })
+  {
+    const int len = static_cast<int>(v->size());
+    k.append(reinterpret_cast<const char*>(&len), sizeof(len));
+    appendInts(k, *v);
+  }
+  return k;
+}
+}  // namespace
+
+GpuQPBatcher::~GpuQPBatcher()
+{
+  for (auto& kv : cache_)
+    thip_qp_destroy(kv.second.qp);
+}
+
+void GpuQPBatcher::enter()
+{
+  std::lock_guard<std::mutex> lk(mu_);
+  ++active_;
+}
+
+void GpuQPBatcher::leave()
+{
+  std::unique_lock<std::mutex> lk(mu_);
+  --active_;
+  // the clients still running may all be waiting now
+  if (!pending_.empty() && static_cast<int>(pending_.size()) >= active_)
+    flushLocked();
+}
+
+void GpuQPBatcher::solve(Request& r)
+{
+  std::unique_lock<std::mutex> lk(mu_);
+  r.done = false;
+  r.error.clear();
+  pending_.push_back(&r);
+  if (static_cast<int>(pending_.size()) >= active_)
+    flushLocked();  // the last client of the round launches it
+  else
+    cv_.wait(lk, [&] { return r.done; });
+  if (!r.error.empty())
+    throw std::runtime_error(r.error);
+}
+
+// Called with the lock held by the thread that completed the round: every other
+// running client is blocked in solve(), so the pending set cannot change.
+void GpuQPBatcher::flushLocked()
+{
+  std::vector<Request*> reqs;
+  reqs.swap(pending_);
+  ++round_;
+  std::map<std::string, std::vector<Request*>> groups;
+  for (Request* r : reqs)
+    groups[groupKey(*r)].push_back(r);
+  for (auto& kv : groups)
+  {
+    std::vector<Request*>& g = kv.second;
+    const Request& r0 = *g.front();
+    const int count = static_cast<int>(g.size()), n = r0.n, m = r0.m;
+    try
+    {
+      Slot& slot = cache_[kv.first];
+      if (!slot.qp || slot.capacity < count)
+      {
+        thip_qp_destroy(slot.qp);
+        slot.qp = nullptr;
+        if (thip_qp_create(r0.device, n, m, r0.Pp->data(), r0.Pi->data(), r0.Ap->data(), r0.Ai->data(), count,
+                           &slot.qp) != THIP_OK)
+          throw std::runtime_error(std::string("GpuQPBatcher: ") + thip_qp_last_error(nullptr));
+        slot.capacity = count;
+      }
+      slot.last_round = round_;
+      const std::size_t np = r0.Px->size(), na = r0.Ax->size(), nn = static_cast<std::size_t>(n),
+                        mm = static_cast<std::size_t>(m);
+      std::vector<double> P(np * count), A(na * count), q(nn * count), l(mm * count), u(mm * count),
+          wx(nn * count, 0.0), wy(mm * count, 0.0), wr(static_cast<std::size_t>(count)), x(nn * count),
+          y(std::max<std::size_t>(mm, 1) * count);
+      std::vector<int> mask(static_cast<std::size_t>(count), 0);
+      std::vector<thip_qp_info> info(static_cast<std::size_t>(count));
+      bool any_warm = false;
+      for (int k = 0; k < count; ++k)
+      {
+        const Request& r = *g[static_cast<std::size_t>(k)];
+        const std::size_t ku = static_cast<std::size_t>(k);
+        std::copy(r.Px->begin(), r.Px->end(), P.begin() + static_cast<long>(ku * np));
+        std::copy(r.Ax->begin(), r.Ax->end(), A.begin() + static_cast<long>(ku * na));
+        std::copy(r.q->begin(), r.q->end(), q.begin() + static_cast<long>(ku * nn));
+        std::copy(r.l->begin(), r.l->end(), l.begin() + static_cast<long>(ku * mm));
+        std::copy(r.u->begin(), r.u->end(), u.begin() + static_cast<long>(ku * mm));
+        wr[ku] = r.settings.rho;
+        if (r.warm)
+        {
+          any_warm = true;
+          mask[ku] = 1;
+          std::copy(r.wx->begin(), r.wx->begin() + static_cast<long>(nn), wx.begin() + static_cast<long>(ku * nn));
+          std::copy(r.wy->begin(), r.wy->begin() + static_cast<long>(mm), wy.begin() + static_cast<long>(ku * mm));
+        }
+      }
+      const int rc = thip_qp_solve_some(slot.qp, count, P.data(), q.data(), A.data(), l.data(), u.data(),
+                                        &r0.settings, any_warm ? wx.data() : nullptr, any_warm ? wy.data() : nullptr,
+                                        any_warm ? mask.data() : nullptr, wr.data(), x.data(), y.data(), info.data());
+      if (rc != THIP_OK)
+        throw std::runtime_error(std::string("GpuQPBatcher: thip_qp_solve_some: ") + thip_qp_last_error(slot.qp));
+      ++launches_;
+      qps_ += count;
+      for (int k = 0; k < count; ++k)
+      {
+        Request& r = *g[static_cast<std::size_t>(k)];
+        const std::size_t ku = static_cast<std::size_t>(k);
+        r.x->assign(x.begin() + static_cast<long>(ku * nn), x.begin() + static_cast<long>((ku + 1) * nn));
+        r.y->assign(y.begin() + static_cast<long>(ku * mm), y.begin() + static_cast<long>((ku + 1) * mm));
+        *r.info = info[ku];
+      }
+    }
+    catch (const std::exception& e)
+    {
+      for (Request* r : g)
+        r->error = e.what();
+    }
+  }
+  // patterns not used this round go (collision QPs change pattern with their contacts)
+  for (auto it = cache_.begin(); it != cache_.end();)
+    if (it->second.last_round != round_)
+    {
+      thip_qp_destroy(it->second.qp);
+      it = cache_.erase(it);
+    }
+    else
+      ++it;
+  for (Request* r : reqs)
+    r->done = true;
+  cv_.notify_all();
+}
+}  // namespace sco

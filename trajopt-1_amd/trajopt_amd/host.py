@@ -47,6 +47,8 @@ def load_host():
                                               C.POINTER(C.c_int), C.c_int, C.c_int, dp, C.POINTER(abi.Result),
                                               C.c_char_p, C.c_int]
         L.thost_solve_json_stream.restype = C.c_int
+        L.thost_last_batch_qp_stats.argtypes = [C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]
+        L.thost_last_batch_qp_stats.restype = None
         L.thost_solve_json.argtypes = [C.c_char_p, dp, C.c_int, C.c_int, dp, C.POINTER(abi.Result),
                                        C.POINTER(C.c_int), C.c_char_p, C.c_int]
         L.thost_solve_json.restype = C.c_int
@@ -91,7 +93,7 @@ def solve_json_batch(texts, scenes=None, device=0, devices=None):
     L = load_host()
     B = len(texts)
     desc, _, _, _ = lower_json(texts[0], None if scenes is None else scenes[0])
-    N, D = desc.n_steps, desc.chain.n_dof
+    N, D = desc.n_steps, desc.chain.n_dof + (1 if desc.use_time else 0)  # (+ the dt column)
     sc = None if scenes is None else np.ascontiguousarray(scenes, dtype=np.float64)
     n_prims = 0 if sc is None else sc.shape[1]
     arr = (C.c_char_p * B)(*[t.encode() for t in texts])
@@ -104,6 +106,16 @@ def solve_json_batch(texts, scenes=None, device=0, devices=None):
     if rc != 0:
         raise HostError(err.value.decode())
     return x, list(res)
+
+
+def last_batch_qp_stats():
+    """(QP launches, QPs) of this thread's last solve_json_batch: a batch of
+    problems the fused kernel does not lower runs their host loops with every
+    QP round batched into one launch per pattern."""
+    L = load_host()
+    a, b = C.c_longlong(0), C.c_longlong(0)
+    L.thost_last_batch_qp_stats(C.byref(a), C.byref(b))
+    return a.value, b.value
 
 
 def solve_json_stream(batches, scenes=None, devices=(0,), inflight=2):
