@@ -561,9 +561,11 @@ const char* thip_eval_last_error(thip_eval* ev); /* NULL: the last thip_eval_cre
  * is the sco::Model a non-lowerable OptProb (custom terms, JointAcc /
  * JointJerk terms, the reference's small-problem tests) is solved with.  A
  * thip_qp holds one sparsity pattern -- P upper-triangular CSC (n x n), A CSC
- * (m x n) -- for `batch` QPs whose values differ; one workgroup per QP, dense
- * quasi-definite LDL^T of the KKT, so n + m <= THIP_QP_MAX_KKT. */
-#define THIP_QP_MAX_KKT 4096
+ * (m x n) -- for `batch` QPs whose values differ; one workgroup per QP, sparse
+ * quasi-definite LDL^T of the KKT (minimum-degree order and elimination-tree
+ * level schedule computed once per pattern at create), n + m <= THIP_QP_MAX_KKT.
+ * Patterns must not repeat an entry. */
+#define THIP_QP_MAX_KKT 65536
 typedef struct thip_qp thip_qp;
 typedef struct thip_qp_info {
   int status;        /* OSQP 1.0 status value (1 solved, 2 solved inaccurate, 3/4 primal infeasible

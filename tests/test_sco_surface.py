@@ -135,7 +135,7 @@ def test_time_front_door_errors(built, edit, msg):
 
 
 def test_gpu_model_capacity_is_an_error_not_a_qp_failure(built):
-    """GpuModel refuses a convex subproblem beyond the dense-KKT capacity
+    """GpuModel refuses a convex subproblem beyond the KKT capacity
     (n + m > THIP_QP_MAX_KKT) with the limit named, before touching the device,
     instead of returning CVX_FAILED (which would shrink the trust box and retry
     the same impossible QP, then write /tmp/fail.lp)."""

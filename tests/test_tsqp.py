@@ -74,11 +74,13 @@ def test_product_argument_checks():
 
 
 def test_qp_capacity_is_reported_before_any_solve():
-    """A QP beyond the GPU solver's dense-KKT capacity (n + m > THIP_QP_MAX_KKT)
-    is refused with the limit named, before any QP is built (not as a QP failure
-    that would shrink the trust region and retry)."""
+    """A QP beyond the GPU solver's capacity (n + m > THIP_QP_MAX_KKT) is refused
+    with the limit named, before any QP is built (not as a QP failure that would
+    shrink the trust region and retry).  The largest spec the front door takes:
+    16 absolute-penalty velocity terms over 64 nodes of 16 joints, two slacks
+    per row (n + m = 82688)."""
     D = 16
-    terms = [dict(kind=tsqp.JOINT_VEL, penalty=tsqp.CONSTRAINT, first=0, last=tsqp.MAX_NODES - 1,
-                  lower=[0.01 * k] * D) for k in range(4)]
+    terms = [dict(kind=tsqp.JOINT_VEL, penalty=tsqp.ABSOLUTE, first=0, last=tsqp.MAX_NODES - 1,
+                  lower=[0.01 * k] * D, upper=[0.01 * k] * D) for k in range(tsqp.MAX_TERMS)]
     s = tsqp.make_spec(np.zeros((tsqp.MAX_NODES, D)), terms)
     _expect_error(s, "THIP_QP_MAX_KKT")

@@ -8,10 +8,17 @@
 //   * modified Ruiz equilibration + cost scaling (settings.scaling passes);
 //   * the rho vector (equality rows x1e3, free rows rho_min);
 //   * the quasi-definite KKT [P + sigma I, A'; A, -diag(1/rho)] factored as a
-//     dense LDL^T in the QP's HBM workspace (no pivoting: a quasi-definite
+//     sparse LDL^T in the QP's HBM workspace (no pivoting: a quasi-definite
 //     matrix factors under any symmetric order; the pivot signs give OSQP's
-//     convexity check) and solved forward / diagonal / backward with the
-//     solve vector in LDS;
+//     convexity check).  The symbolic part runs once per pattern on the host
+//     (thip_qp_create): QDLDL's role in OSQP -- a minimum-degree order (the
+//     oracle's LdlSolver::order, the AMD role), the elimination tree, the
+//     pattern of L -- plus what the GPU needs on top: the tree's levels.  The
+//     numeric factor walks the levels bottom-up, one thread per pivot then
+//     one per entry of the level's columns of L (each a merge of two rows of
+//     L); the solves walk them up (rows of L) and down (columns of L) with
+//     the permuted solve vector in LDS.  One __syncthreads per level, where
+//     the dense factor needed one per row;
 //   * ADMM with over-relaxation, termination on unscaled inf-norm residuals
 //     every check_termination iterations, primal / dual infeasibility
 //     certificates, iteration-based adaptive rho (refactorisation);
@@ -22,18 +29,22 @@
 // The structured trajectory QPs of a TrajOptProb batch do not come here: they
 // run sqp_kernel's block-tridiagonal path.  This path serves arbitrary
 // sco::Model users (custom terms, JointAcc / JointJerk terms, the reference's
-// small-problem and solver-interface tests): the dense factor bounds the KKT
-// dimension n + m at THIP_QP_MAX_KKT.
+// small-problem and solver-interface tests, collision QPs with more contacts
+// than the fused kernel's table).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
+#include <iterator>
+#include <set>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/trajopt_hip.h"
+#include "kkt_symbolic.hpp"
 
 namespace thip_qp_dev
 {
@@ -62,12 +73,14 @@ enum Arr : int
 {
   W_PX, W_AX, W_Q, W_L, W_U, W_D, W_DI, W_E, W_EI, W_TD, W_TE, W_RHO, W_RHOI, W_CT,
   W_X, W_XP, W_Z, W_ZP, W_Y, W_DX, W_DY, W_XT, W_AXV, W_PXV, W_ATY, W_RP, W_RD, W_T1, W_T2,
-  W_PXS, W_PZS, W_PYS, W_RHS, W_RES, W_FLG, W_RMAP, W_K, W_KT, W_SC, W_COUNT
+  W_PXS, W_PZS, W_PYS, W_RHS, W_RES, W_FLG, W_LX, W_DG, W_LV, W_SC, W_COUNT
 };
+// W_LX / W_DG: the factor (L values in row order, D); W_LV: the permuted solve
+// vector when it does not fit LDS.
 // W_SC: the scalars a resident workspace keeps between launches (thip_qp_setup ...
 // thip_qp_solve_resident): cost scaling c and 1/c, the current rho, setup ok, and
-// whether the ADMM KKT factor in W_K must be rebuilt (polish factors its reduced
-// KKT in the same storage; OSQP keeps a separate polish factor)
+// whether the ADMM KKT factor in W_LX must be rebuilt (polish factors its KKT in
+// the same storage; OSQP keeps a separate polish factor)
 enum : int
 {
   SC_C = 0,
@@ -94,6 +107,15 @@ struct QpPattern
   const int *Pp, *Pi, *Prp, *Prj, *Prmap;
   // A CSC and its rows (-> index into A values)
   const int *Ap, *Ai, *Arp, *Arj, *Armap;
+  // symbolic LDL^T of the permuted KKT (kkt_symbolic): perm[new] = old node
+  // (x_j = j, row r = n + r); L rows (lrp, lrj: columns ascending); L columns
+  // (lcp; lci = row, lcpos = position in the row order, lksrc = the KKT entry
+  // it starts from: 2e = P value e, 2e + 1 = A value e, -1 = fill); dpd = the
+  // P diagonal value of an x node (-1 none); nodes by etree level (lvp, lvn);
+  // the level's column entries (fip; fik = column, fic = entry)
+  const int *perm, *lrp, *lrj, *lcp, *lci, *lcpos, *lksrc, *dpd, *lvp, *lvn, *fip, *fik, *fic;
+  int nlev;
+  int lds_vec;  // the permuted solve vector lives in LDS (else W_LV)
   long long off[W_COUNT];
   long long stride;
 };
@@ -181,7 +203,7 @@ struct Qp
   const thip_osqp_settings& s;
   double* w;
   Sh& sh;
-  double* lv;  // LDS solve vector [N]
+  double* lv;  // the permuted solve vector [N] (LDS, or W_LV)
   int n, m;
   __device__ double* a(int k) const { return w + p.off[k]; }
 };
@@ -342,105 +364,147 @@ __device__ void set_rho_vec(Qp& q)
   __syncthreads();
 }
 
-// dense LDL^T of the N x N symmetric matrix K (lower triangle, row-major, in
-// place: D on the diagonal, L strictly below); KT gets L^T row-major for the
-// forward solve.  sh.npos = positive pivots, sh.fail = 1 on a zero / non-finite pivot.
-__device__ void ldl_factor(Qp& q, double* K, double* KT, int N)
+// The KKT entry an L entry starts from (kkt_symbolic's lksrc code).  In polish
+// mode the rows outside the active set are decoupled: their A entries read 0.
+__device__ __forceinline__ double kkt_entry(const Qp& q, int code, bool pol, const double* FLG)
 {
+  if (code < 0)
+    return 0.0;
+  const int e = code >> 1;
+  if (!(code & 1))
+    return q.a(W_PX)[e];
+  if (pol && FLG[q.p.Ai[e]] == 0.0)
+    return 0.0;
+  return q.a(W_AX)[e];
+}
+
+// KKT diagonal of permuted node k: ADMM [P + sigma I; -diag(1/rho)], polish
+// [P + delta I; -delta I] on the active rows and -1 on the decoupled ones
+// (their solution component is 0: OSQP's reduced KKT, without re-analysis)
+__device__ __forceinline__ double kkt_diag(const Qp& q, int k, bool pol, const double* FLG)
+{
+  const int o = q.p.perm[k];
+  if (o < q.n)
+  {
+    const int e = q.p.dpd[k];
+    const double p = (e >= 0) ? q.a(W_PX)[e] : 0.0;
+    return p + (pol ? q.s.delta : q.s.sigma);
+  }
+  const int r = o - q.n;
+  if (pol)
+    return FLG[r] != 0.0 ? -q.s.delta : -1.0;
+  return -q.a(W_RHOI)[r];
+}
+
+// numeric LDL^T of the permuted KKT over the symbolic pattern, level by level
+// of the elimination tree: first the level's pivots
+//     D_k = K_kk - sum_j L_kj^2 D_j                (row k of L is final: its
+//                                                   columns are descendants)
+// then every entry of the level's columns
+//     L_ik = (K_ik - sum_{j < k} L_ij D_j L_kj) / D_k
+// as a merge of rows i and k (both ascending).  sh.npos = positive pivots,
+// sh.fail = 1 on a zero / non-finite pivot.
+__device__ void kkt_factor(Qp& q, bool pol)
+{
+  const QpPattern& p = q.p;
+  double *LX = q.a(W_LX), *DG = q.a(W_DG);
+  const double* FLG = q.a(W_FLG);
+  double bad = 0, npos = 0;
+  for (int lev = 0; lev < p.nlev; ++lev)
+  {
+    const int n1 = p.lvp[lev + 1];
+    for (int t = p.lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
+    {
+      const int k = p.lvn[t];
+      double d = kkt_diag(q, k, pol, FLG);
+      for (int e = p.lrp[k]; e < p.lrp[k + 1]; ++e)
+      {
+        const double l = LX[e];
+        d -= (l * DG[p.lrj[e]]) * l;
+      }
+      DG[k] = d;
+      if (d == 0.0 || !isfinite(d))
+        bad = 1;
+      else if (d > 0)
+        npos += 1;
+    }
+    __syncthreads();
+    const int f1 = p.fip[lev + 1];
+    for (int t = p.fip[lev] + static_cast<int>(threadIdx.x); t < f1; t += kQB)
+    {
+      const int k = p.fik[t], c = p.fic[t], i = p.lci[c];
+      double s = kkt_entry(q, p.lksrc[c], pol, FLG);
+      int a = p.lrp[i], b = p.lrp[k];
+      const int ae = p.lrp[i + 1], be = p.lrp[k + 1];
+      while (a < ae && b < be)
+      {
+        const int ja = p.lrj[a], jb = p.lrj[b];
+        if (ja == jb)
+        {
+          s -= (LX[a] * DG[ja]) * LX[b];
+          ++a;
+          ++b;
+        }
+        else if (ja < jb)
+          ++a;
+        else
+          ++b;
+      }
+      LX[p.lcpos[c]] = s / DG[k];
+    }
+    __syncthreads();
+  }
+  bad = bmax(q.sh, bad);
+  npos = bsum(q.sh, npos);
   if (threadIdx.x == 0)
   {
-    q.sh.npos = 0;
-    q.sh.fail = 0;
-  }
-  __syncthreads();
-  for (int k = 0; k < N; ++k)
-  {
-    const double d = K[(long long)k * N + k];
-    if (d == 0.0 || !isfinite(d))
-    {
-      if (threadIdx.x == 0)
-        q.sh.fail = 1;
-      __syncthreads();
-      return;
-    }
-    if (threadIdx.x == 0 && d > 0)
-      q.sh.npos++;
-    const int T = N - k - 1;
-    const double dinv = 1.0 / d;
-    QFOR(ii, T)
-    {
-      const long long i = k + 1 + ii;
-      K[i * N + k] *= dinv;
-    }
-    __syncthreads();
-    // trailing update K[i][j] -= L[i][k] d L[j][k], k < j <= i
-    const long long TT = (long long)T * T;
-    for (long long e = threadIdx.x; e < TT; e += kQB)
-    {
-      const int ii = static_cast<int>(e / T), jj = static_cast<int>(e - (long long)ii * T);
-      if (jj <= ii)
-      {
-        const long long i = k + 1 + ii, j = k + 1 + jj;
-        K[i * N + j] -= (K[i * N + k] * d) * K[j * N + k];
-      }
-    }
-    __syncthreads();
-  }
-  // L^T rows for the forward solve
-  const long long NN = (long long)N * N;
-  for (long long e = threadIdx.x; e < NN; e += kQB)
-  {
-    const long long i = e / N, j = e - i * N;
-    if (j < i)
-      KT[j * N + i] = K[e];
+    q.sh.fail = bad != 0.0;
+    q.sh.npos = static_cast<int>(npos);
   }
   __syncthreads();
 }
 
-// in place solve K v = b with v in LDS (lv[0..N))
-__device__ void ldl_solve(Qp& q, const double* K, const double* KT, int N, double* v)
+// in place solve K v = b for v[0..N) in the QP's workspace (original order):
+// gather into the permuted vector, L forward by levels up the tree (rows of
+// L), D, L' backward by levels down the tree (columns of L), scatter back
+__device__ void kkt_solve(Qp& q, double* v)
 {
+  const QpPattern& p = q.p;
+  const double *LX = q.a(W_LX), *DG = q.a(W_DG);
+  double* w = q.lv;
+  const int N = p.N;
   __syncthreads();
-  for (int k = 0; k < N; ++k)
+  QFOR(k, N) w[k] = v[p.perm[k]];
+  __syncthreads();
+  for (int lev = 0; lev < p.nlev; ++lev)
   {
-    const double vk = v[k];
-    const double* row = KT + (long long)k * N;
-    QFOR(ii, N - k - 1)
+    const int n1 = p.lvp[lev + 1];
+    for (int t = p.lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
     {
-      const int i = k + 1 + ii;
-      v[i] -= row[i] * vk;
+      const int k = p.lvn[t];
+      double s = w[k];
+      for (int e = p.lrp[k]; e < p.lrp[k + 1]; ++e)
+        s -= LX[e] * w[p.lrj[e]];
+      w[k] = s;
     }
     __syncthreads();
   }
-  QFOR(i, N) v[i] /= K[(long long)i * N + i];
+  QFOR(k, N) w[k] /= DG[k];
   __syncthreads();
-  for (int i = N - 1; i > 0; --i)
+  for (int lev = p.nlev - 1; lev >= 0; --lev)
   {
-    const double vi = v[i];
-    const double* row = K + (long long)i * N;
-    QFOR(j, i) v[j] -= row[j] * vi;
+    const int n1 = p.lvp[lev + 1];
+    for (int t = p.lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
+    {
+      const int k = p.lvn[t];
+      double s = w[k];
+      for (int c = p.lcp[k]; c < p.lcp[k + 1]; ++c)
+        s -= LX[p.lcpos[c]] * w[p.lci[c]];
+      w[k] = s;
+    }
     __syncthreads();
   }
-}
-
-// KKT [P + sigma I, A'; A, -diag(1/rho)] (lower triangle)
-__device__ void build_kkt(Qp& q)
-{
-  const int n = q.n, m = q.m, N = n + m;
-  double *K = q.a(W_K), *PX = q.a(W_PX), *AX = q.a(W_AX), *RHOI = q.a(W_RHOI);
-  const long long NN = (long long)N * N;
-  for (long long e = threadIdx.x; e < NN; e += kQB)
-    K[e] = 0.0;
-  __syncthreads();
-  QFOR(j, n)
-  for (int e = q.p.Pp[j]; e < q.p.Pp[j + 1]; ++e)
-    K[(long long)j * N + q.p.Pi[e]] = PX[e];  // (i, j) upper -> (j, i) lower
-  QFOR(j, n)
-  for (int e = q.p.Ap[j]; e < q.p.Ap[j + 1]; ++e)
-    K[(long long)(n + q.p.Ai[e]) * N + j] = AX[e];
-  __syncthreads();
-  QFOR(j, n) K[(long long)j * N + j] += q.s.sigma;
-  QFOR(r, m) K[(long long)(n + r) * N + (n + r)] = -RHOI[r];
+  QFOR(k, N) v[p.perm[k]] = w[k];
   __syncthreads();
 }
 
@@ -632,15 +696,14 @@ __device__ bool adapt_rho(Qp& q)
     }
   }
   __syncthreads();
-  build_kkt(q);
-  ldl_factor(q, q.a(W_K), q.a(W_KT), q.n + q.m);
+  kkt_factor(q, false);
   return !q.sh.fail && q.sh.npos >= q.n;
 }
 
 __device__ void polish(Qp& q)
 {
-  const int n = q.n, m = q.m;
-  double *Z = q.a(W_Z), *Y = q.a(W_Y), *L = q.a(W_L), *U = q.a(W_U), *FLG = q.a(W_FLG), *RMAP = q.a(W_RMAP);
+  const int n = q.n, m = q.m, N = n + m;
+  double *Z = q.a(W_Z), *Y = q.a(W_Y), *L = q.a(W_L), *U = q.a(W_U), *FLG = q.a(W_FLG);
   QFOR(r, m)
   {
     double f = 0;
@@ -651,36 +714,9 @@ __device__ void polish(Qp& q)
     FLG[r] = f;
   }
   __syncthreads();
-  if (threadIdx.x == 0)
-  {
-    int k = 0;
-    for (int r = 0; r < m; ++r)
-      RMAP[r] = (FLG[r] != 0.0) ? k++ : -1;
-    q.sh.nred = k;
-  }
-  __syncthreads();
-  const int mred = q.sh.nred, N = n + mred;
-  // reduced KKT [P + delta I, Ared'; Ared, -delta I]
-  double *K = q.a(W_K), *KT = q.a(W_KT), *PX = q.a(W_PX), *AX = q.a(W_AX);
-  const long long NN = (long long)N * N;
-  for (long long e = threadIdx.x; e < NN; e += kQB)
-    K[e] = 0.0;
-  __syncthreads();
-  QFOR(j, n)
-  for (int e = q.p.Pp[j]; e < q.p.Pp[j + 1]; ++e)
-    K[(long long)j * N + q.p.Pi[e]] = PX[e];
-  QFOR(j, n)
-  for (int e = q.p.Ap[j]; e < q.p.Ap[j + 1]; ++e)
-  {
-    const int k = static_cast<int>(RMAP[q.p.Ai[e]]);
-    if (k >= 0)
-      K[(long long)(n + k) * N + j] = AX[e];
-  }
-  __syncthreads();
-  QFOR(j, n) K[(long long)j * N + j] += q.s.delta;
-  QFOR(k, mred) K[(long long)(n + k) * N + (n + k)] = -q.s.delta;
-  __syncthreads();
-  ldl_factor(q, K, KT, N);
+  // [P + delta I, Aact'; Aact, -delta I] over the full pattern, the inactive
+  // rows decoupled (kkt_diag / kkt_entry in polish mode)
+  kkt_factor(q, true);
   if (q.sh.fail || q.sh.npos < n)
   {
     if (threadIdx.x == 0)
@@ -688,56 +724,42 @@ __device__ void polish(Qp& q)
     __syncthreads();
     return;
   }
-  double *RHS = q.a(W_RHS), *RES = q.a(W_RES), *Q = q.a(W_Q), *T1 = q.a(W_T1), *T2 = q.a(W_T2);
-  double* v = q.lv;
+  double *RHS = q.a(W_RHS), *RES = q.a(W_RES), *Q = q.a(W_Q), *T1 = q.a(W_T1), *T2 = q.a(W_T2), *AX = q.a(W_AX);
+  double* SOL = q.a(W_XT);  // [x (n), y of the rows (m); 0 on the inactive rows]
+  double* SOLY = SOL + n;
   QFOR(j, n) RHS[j] = -Q[j];
-  QFOR(r, m)
-  {
-    const int k = static_cast<int>(RMAP[r]);
-    if (k >= 0)
-      RHS[n + k] = (FLG[r] < 0) ? L[r] : U[r];
-  }
+  QFOR(r, m) RHS[n + r] = (FLG[r] < 0) ? L[r] : ((FLG[r] > 0) ? U[r] : 0.0);
   __syncthreads();
-  QFOR(i, N) v[i] = RHS[i];
-  ldl_solve(q, K, KT, N, v);
-  double* SOL = q.a(W_RD) /* n */;
-  double* SOLY = q.a(W_RP) /* >= mred */;
-  QFOR(j, n) SOL[j] = v[j];
-  QFOR(k, mred) SOLY[k] = v[n + k];
-  __syncthreads();
+  QFOR(i, N) SOL[i] = RHS[i];
+  kkt_solve(q, SOL);
   for (int itr = 0; itr < q.s.polish_refine_iter; ++itr)
   {
-    // RES = RHS - [P, Ared'; Ared, 0] sol
+    // RES = RHS - [P, Aact'; Aact, 0] sol
     p_mul(q, SOL, T1);
     QFOR(j, n)
     {
       double t = 0;
       for (int e = q.p.Ap[j]; e < q.p.Ap[j + 1]; ++e)
-      {
-        const int k = static_cast<int>(RMAP[q.p.Ai[e]]);
-        if (k >= 0)
-          t += AX[e] * SOLY[k];
-      }
+        if (FLG[q.p.Ai[e]] != 0.0)
+          t += AX[e] * SOLY[q.p.Ai[e]];
       T2[j] = t;
     }
     QFOR(r, m)
     {
-      const int k = static_cast<int>(RMAP[r]);
-      if (k >= 0)
+      double res = 0;
+      if (FLG[r] != 0.0)
       {
         double t = 0;
         for (int e = q.p.Arp[r]; e < q.p.Arp[r + 1]; ++e)
           t += AX[q.p.Armap[e]] * SOL[q.p.Arj[e]];
-        RES[n + k] = RHS[n + k] - t;
+        res = RHS[n + r] - t;
       }
+      RES[n + r] = res;
     }
     __syncthreads();
     QFOR(j, n) RES[j] = (RHS[j] - T1[j]) - T2[j];
-    __syncthreads();
-    QFOR(i, N) v[i] = RES[i];
-    ldl_solve(q, K, KT, N, v);
-    QFOR(j, n) SOL[j] += v[j];
-    QFOR(k, mred) SOLY[k] += v[n + k];
+    kkt_solve(q, RES);
+    QFOR(i, N) SOL[i] += RES[i];
     __syncthreads();
   }
   double *PXS = q.a(W_PXS), *PZS = q.a(W_PZS), *PYS = q.a(W_PYS);
@@ -747,8 +769,7 @@ __device__ void polish(Qp& q)
   __syncthreads();
   QFOR(r, m)
   {
-    const int k = static_cast<int>(RMAP[r]);
-    const double py = (k >= 0) ? SOLY[k] : 0.0;
+    const double py = (FLG[r] != 0.0) ? SOLY[r] : 0.0;
     const double t = PZS[r] + py;
     PZS[r] = fmin(fmax(t, L[r]), U[r]);
     PYS[r] = t - PZS[r];
@@ -788,7 +809,6 @@ __device__ void polish(Qp& q)
 __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
 {
   Sh& sh = q.sh;
-  double* lv = q.lv;
   const int n = q.n, m = q.m;
   double *X = q.a(W_X), *XP = q.a(W_XP), *Z = q.a(W_Z), *ZP = q.a(W_ZP), *Y = q.a(W_Y), *DX = q.a(W_DX),
          *DY = q.a(W_DY), *XT = q.a(W_XT), *Q = q.a(W_Q), *L = q.a(W_L), *U = q.a(W_U), *RHO = q.a(W_RHO),
@@ -796,7 +816,6 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
   int interval = args.s.adaptive_rho_interval;
   if (args.s.adaptive_rho == 1 && interval == 0)
     interval = args.s.check_termination ? 4 * args.s.check_termination : 100;
-  const int N = n + m;
   const double alpha = args.s.alpha, sigma = args.s.sigma;
   bool can_check = false;
   bool noncvx = false;
@@ -810,10 +829,8 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
     QFOR(j, n) XT[j] = sigma * XP[j] - Q[j];
     QFOR(r, m) XT[n + r] = ZP[r] - RHOI[r] * Y[r];
     __syncthreads();
-    QFOR(i, N) lv[i] = XT[i];
-    ldl_solve(q, q.a(W_K), q.a(W_KT), N, lv);
-    QFOR(j, n) XT[j] = lv[j];
-    QFOR(r, m) XT[n + r] += RHOI[r] * lv[n + r];
+    kkt_solve(q, XT);  // (x~, nu) in place
+    QFOR(r, m) XT[n + r] = (ZP[r] - RHOI[r] * Y[r]) + RHOI[r] * XT[n + r];  // z~ = rhs + nu / rho
     __syncthreads();
     QFOR(j, n)
     {
@@ -915,7 +932,8 @@ __global__ __launch_bounds__(kQB) void qp_csc_kernel(QpArgs args)
     return;
   const QpPattern& P = args.pat;
   const int n = P.n, m = P.m;
-  Qp q{ P, args.s, args.ws + (long long)b * P.stride, sh, lv, n, m };
+  double* w = args.ws + (long long)b * P.stride;
+  Qp q{ P, args.s, w, sh, P.lds_vec ? lv : w + P.off[W_LV], n, m };
   // data (scaled in place)
   {
     double *PX = q.a(W_PX), *AX = q.a(W_AX), *Q = q.a(W_Q), *L = q.a(W_L), *U = q.a(W_U);
@@ -948,8 +966,7 @@ __global__ __launch_bounds__(kQB) void qp_csc_kernel(QpArgs args)
     __syncthreads();
   }
   set_rho_vec(q);
-  build_kkt(q);
-  ldl_factor(q, q.a(W_K), q.a(W_KT), n + m);
+  kkt_factor(q, false);
   thip_qp_info* info = args.info + b;
   if (q.sh.fail || q.sh.npos < n)
   {
@@ -1002,8 +1019,7 @@ __global__ __launch_bounds__(kQB) void qp_csc_kernel(QpArgs args)
 // HBM workspace; c, 1/c and rho in W_SC.  Only the changed vectors cross the bus.
 __device__ void resident_refactor(Qp& q)
 {
-  build_kkt(q);
-  ldl_factor(q, q.a(W_K), q.a(W_KT), q.n + q.m);
+  kkt_factor(q, false);
 }
 
 // OSQP unscale_data: P <- cinv Dinv P Dinv, q <- Dinv (cinv q), A <- Einv A Dinv, l, u <- Einv l, Einv u
@@ -1059,7 +1075,8 @@ __global__ __launch_bounds__(kQB) void qp_resident_kernel(QpArgs args, int op)
     return;
   const QpPattern& P = args.pat;
   const int n = P.n, m = P.m;
-  Qp q{ P, args.s, args.ws + (long long)b * P.stride, sh, lv, n, m };
+  double* w = args.ws + (long long)b * P.stride;
+  Qp q{ P, args.s, w, sh, P.lds_vec ? lv : w + P.off[W_LV], n, m };
   double* SC = q.a(W_SC);
   thip_qp_info* info = args.info + b;
   const bool sc = args.s.scaling > 0;
@@ -1212,7 +1229,7 @@ __global__ __launch_bounds__(kQB) void qp_resident_kernel(QpArgs args, int op)
     if (threadIdx.x == 0)
     {
       if (sh.polish != 0)
-        SC[SC_KKT_DIRTY] = 1.0;  // polish factored its reduced KKT over W_K
+        SC[SC_KKT_DIRTY] = 1.0;  // polish factored its KKT over W_LX / W_DG
       SC[SC_RHO] = sh.rho;
     }
     return;
@@ -1305,6 +1322,13 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
         return THIP_E_INVALID;
       }
   }
+  KktSymbolic S;
+  const std::string why = kkt_symbolic(n, m, P_colptr, P_rowind, A_colptr, A_rowind, S);
+  if (!why.empty())
+  {
+    g_qp_create_err = "thip_qp_create: " + why;
+    return THIP_E_INVALID;
+  }
   auto* q = new thip_qp();
   q->device = device;
   q->batch = batch;
@@ -1354,7 +1378,18 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
                oPrj = push(prj.data(), np), oPrm = push(prm.data(), np), oAp = push(A_colptr, n + 1),
                oAi = push(A_rowind, na), oArp = push(arp.data(), m + 1), oArj = push(arj.data(), na),
                oArm = push(arm.data(), na);
+  const long long nnzl = static_cast<long long>(S.lrj.size());
+  const int nlev = static_cast<int>(S.lvp.size()) - 1;
+  const size_t oPerm = push(S.perm.data(), n + m), oLrp = push(S.lrp.data(), n + m + 1),
+               oLrj = push(S.lrj.data(), static_cast<int>(nnzl)), oLcp = push(S.lcp.data(), n + m + 1),
+               oLci = push(S.lci.data(), static_cast<int>(nnzl)), oLcpos = push(S.lcpos.data(), static_cast<int>(nnzl)),
+               oLks = push(S.lksrc.data(), static_cast<int>(nnzl)), oDpd = push(S.dpd.data(), n + m),
+               oLvp = push(S.lvp.data(), nlev + 1), oLvn = push(S.lvn.data(), n + m),
+               oFip = push(S.fip.data(), nlev + 1), oFik = push(S.fik.data(), static_cast<int>(nnzl)),
+               oFic = push(S.fic.data(), static_cast<int>(nnzl));
   const long long N = n + m;
+  // the permuted solve vector in LDS up to 64 KiB
+  const bool lds_vec = N <= 8192;
   long long sizes[W_COUNT];
   sizes[W_PX] = std::max(np, 1);
   sizes[W_AX] = std::max(na, 1);
@@ -1363,9 +1398,11 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
   const long long mm = std::max(m, 1);
   sizes[W_L] = sizes[W_U] = sizes[W_E] = sizes[W_EI] = sizes[W_TE] = sizes[W_RHO] = sizes[W_RHOI] = sizes[W_CT] = mm;
   sizes[W_Z] = sizes[W_ZP] = sizes[W_Y] = sizes[W_DY] = sizes[W_AXV] = sizes[W_RP] = sizes[W_T2] = mm;
-  sizes[W_PZS] = sizes[W_PYS] = sizes[W_FLG] = sizes[W_RMAP] = mm;
+  sizes[W_PZS] = sizes[W_PYS] = sizes[W_FLG] = mm;
   sizes[W_XT] = sizes[W_RHS] = sizes[W_RES] = N;
-  sizes[W_K] = sizes[W_KT] = N * N;
+  sizes[W_LX] = std::max(nnzl, 1LL);
+  sizes[W_DG] = N;
+  sizes[W_LV] = lds_vec ? 1 : N;
   sizes[W_SC] = SC_COUNT;
   long long off = 0;
   for (int k = 0; k < W_COUNT; ++k)
@@ -1380,7 +1417,9 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
   q->pat.nnz_a = na;
   q->pat.N = static_cast<int>(N);
   q->in_doubles = (long long)np + na + n + 2LL * m;
-  q->lds = static_cast<size_t>(N) * sizeof(double);
+  q->pat.nlev = nlev;
+  q->pat.lds_vec = lds_vec ? 1 : 0;
+  q->lds = lds_vec ? static_cast<size_t>(N) * sizeof(double) : 0;
   auto fail = [&](const std::string& msg) {
     g_qp_create_err = msg;
     thip_qp_destroy(q);
@@ -1408,6 +1447,19 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
   q->pat.Arp = q->d_idx + oArp;
   q->pat.Arj = q->d_idx + oArj;
   q->pat.Armap = q->d_idx + oArm;
+  q->pat.perm = q->d_idx + oPerm;
+  q->pat.lrp = q->d_idx + oLrp;
+  q->pat.lrj = q->d_idx + oLrj;
+  q->pat.lcp = q->d_idx + oLcp;
+  q->pat.lci = q->d_idx + oLci;
+  q->pat.lcpos = q->d_idx + oLcpos;
+  q->pat.lksrc = q->d_idx + oLks;
+  q->pat.dpd = q->d_idx + oDpd;
+  q->pat.lvp = q->d_idx + oLvp;
+  q->pat.lvn = q->d_idx + oLvn;
+  q->pat.fip = q->d_idx + oFip;
+  q->pat.fik = q->d_idx + oFik;
+  q->pat.fic = q->d_idx + oFic;
   *out = q;
   return THIP_OK;
 }

@@ -100,7 +100,7 @@ bool GpuQPSolver::setupNow()
   thip_qp_destroy(qp_);
   qp_ = nullptr;
   resident_ = false;
-  if (nv_ + nc_ > THIP_QP_MAX_KKT)  // the dense KKT factor bounds the problem size: a limit, not a QP failure
+  if (nv_ + nc_ > THIP_QP_MAX_KKT)  // the KKT capacity bounds the problem size: a limit, not a QP failure
     throw std::runtime_error("GpuQPSolver: the QP has " + std::to_string(nv_) + " variables and " +
                              std::to_string(nc_) + " constraints; the GPU QP solver takes n + m <= THIP_QP_MAX_KKT (" +
                              std::to_string(THIP_QP_MAX_KKT) + ")");

@@ -46,9 +46,9 @@ CaseOut qpCase(int id, int device)
   GpuModel solver(*config(device));
   if (id == 9)
   {
-    // beyond the dense-KKT capacity: 2049 bounded variables (n + m = 4098 > THIP_QP_MAX_KKT)
+    // beyond the KKT capacity: 32769 bounded variables (n + m = 65538 > THIP_QP_MAX_KKT)
     VarVector vars;
-    for (int i = 0; i < 2049; ++i)
+    for (int i = 0; i < THIP_QP_MAX_KKT / 2 + 1; ++i)
       vars.push_back(solver.addVar("v" + std::to_string(i), -1, 1));
     solver.update();
     QuadExpr obj;
