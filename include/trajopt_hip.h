@@ -47,8 +47,9 @@ extern "C" {
  * abi_version differs (a caller compiled against another layout).  3: the
  * descriptor carries abi_version, thip_chain.is_tree, thip_sqp_params.max_time.
  * 4: use_time, fixed dofs, time JointVel.  5: TotalTime.  6: further collision
- * terms (thip_coll_term), single-waypoint problems on the generic path. */
-#define THIP_ABI_VERSION 6
+ * terms (thip_coll_term), single-waypoint problems on the generic path.  7: robot
+ * self-collision link pairs (n_self_pairs / self_pair). */
+#define THIP_ABI_VERSION 7
 
 #define THIP_MAX_DOF 16
 #define THIP_MAX_LINKS 32
@@ -62,6 +63,8 @@ extern "C" {
 #define THIP_MAX_JVT 4
 #define THIP_MAX_TTT 2
 #define THIP_MAX_COLL_EXTRA 3
+#define THIP_MAX_SELF_PAIRS 64
+#define THIP_MAX_SELF_SPHERE_PAIRS 512
 #define THIP_MAX_CONTACTS 131072
 
 /* error codes */
@@ -350,6 +353,18 @@ typedef struct thip_problem_desc {
   double sphere_center[THIP_MAX_SPHERES][3];  /* in link frame */
   double sphere_radius[THIP_MAX_SPHERES];
   int n_prims;
+  /* robot self-collision: the link pairs whose spheres are tested against each
+   * other, both links moving -- the contact manager's active-link pairs that the
+   * allowed-collision matrix leaves enabled (the SRDF's <disable_collisions>,
+   * e.g. pr2.srdf: the two arms of config E, and each arm's shoulder_pan vs its
+   * wrist links).  A pair's contacts get gradients on both links
+   * (GetGradient's two sides, collision_terms.cpp:195-242) and the scene's
+   * margin / coeff.  Key order: a unit's scene keys (link, primitive) first,
+   * then these pairs in this order; inside a key, sub-state, then the sphere of
+   * link a, then the sphere of link b.  At most THIP_MAX_SELF_SPHERE_PAIRS
+   * sphere pairs in all. */
+  int n_self_pairs;
+  int self_pair[THIP_MAX_SELF_PAIRS][2];
   /* hinge-row (contact) capacity per QP; 0 = automatic: the largest possible
    * contact count (step pairs x 64 LVS sub-states x spheres x primitives),
    * capped at THIP_MAX_CONTACTS and at what fits a 16 GB share of HBM for the

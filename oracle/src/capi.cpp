@@ -296,22 +296,9 @@ int oracle_collision_rows_term(const thip_problem_desc* d, int term, const doubl
         const double* q = x + t * D;
         for (const auto& c : calcCollisionsSingle(cm, q))
         {
-          double g[THIP_MAX_DOF], sc, gd = 0;
-          contactGradient(cm, q, c, false, g, sc);
-          double cst = 0;
-          int kept = 0;
-          double a0[THIP_MAX_DOF] = {};
-          for (int j = 0; j < D; ++j)
-          {
-            a0[j] = sc * g[j];
-            gd += g[j] * q[j];
-            if (std::fabs(a0[j]) > 1e-7)
-              ++kept;
-            else
-              a0[j] = 0;
-          }
-          cst += sc * -gd;
-          cst += c.distance;
+          double a0[THIP_MAX_DOF], a1[THIP_MAX_DOF], cst;
+          int mask;
+          contactExpression(cm, c, q, q, true, false, true, a0, a1, cst, mask);
           if (n < cap)
           {
             double* r = out + static_cast<std::size_t>(n) * W;
@@ -322,7 +309,7 @@ int oracle_collision_rows_term(const thip_problem_desc* d, int term, const doubl
             r[4] = 0;
             r[5] = c.distance;
             r[6] = 0;
-            r[7] = kept;
+            r[7] = __builtin_popcount(static_cast<unsigned>(mask));
             for (int j = 0; j < D; ++j)
             {
               r[8 + j] = a0[j];
@@ -343,44 +330,10 @@ int oracle_collision_rows_term(const thip_problem_desc* d, int term, const doubl
       const auto contacts = calcCollisions(cm, q0, q1, f0, f1);
       for (const auto& c : contacts)
       {
-        double a0[THIP_MAX_DOF] = {}, a1[THIP_MAX_DOF] = {};
-        double cst = c.distance;
-        if (!f0)
-        {
-          double g[THIP_MAX_DOF], sc;
-          contactGradient(cm, q0, c, false, g, sc);
-          double gd = 0;
-          for (int j = 0; j < D; ++j)
-          {
-            a0[j] = sc * g[j];
-            gd += g[j] * q0[j];
-          }
-          cst += sc * -gd;
-        }
-        if (!f1)
-        {
-          double g[THIP_MAX_DOF], sc;
-          contactGradient(cm, q1, c, true, g, sc);
-          double gd = 0;
-          for (int j = 0; j < D; ++j)
-          {
-            a1[j] = sc * g[j];
-            gd += g[j] * q1[j];
-          }
-          cst += sc * -gd;
-        }
-        int kept = 0;
-        for (int j = 0; j < D; ++j)
-        {
-          if (std::fabs(a0[j]) > 1e-7)
-            ++kept;
-          else
-            a0[j] = 0;
-          if (std::fabs(a1[j]) > 1e-7)
-            ++kept;
-          else
-            a1[j] = 0;
-        }
+        double a0[THIP_MAX_DOF], a1[THIP_MAX_DOF], cst;
+        int mask;
+        contactExpression(cm, c, q0, q1, !f0, !f1, false, a0, a1, cst, mask);
+        const int kept = __builtin_popcount(static_cast<unsigned>(mask));
         if (n < cap)
         {
           double* r = out + static_cast<std::size_t>(n) * W;

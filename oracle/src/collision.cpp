@@ -142,7 +142,87 @@ double segSegParam(const double p1[3], const double d1[3], const double p2[3], c
     s = std::fmin(std::fmax((b - cc) / a, 0.0), 1.0);
   return s;
 }
+
+// Both parameters of the closest points of segments p1 + s d1 and p2 + t d2
+// (Ericson 5.1.9, s as segSegParam computes it)
+void segSegParams(const double p1[3], const double d1[3], const double p2[3], const double d2[3], double& s, double& t)
+{
+  const double r[3] = { p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2] };
+  const double a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+  const double eps = 1e-24;
+  if (a <= eps && e <= eps)
+  {
+    s = t = 0.0;
+    return;
+  }
+  if (a <= eps)
+  {
+    s = 0.0;
+    t = std::fmin(std::fmax(f / e, 0.0), 1.0);
+    return;
+  }
+  const double cc = dot3(d1, r);
+  if (e <= eps)
+  {
+    t = 0.0;
+    s = std::fmin(std::fmax(-cc / a, 0.0), 1.0);
+    return;
+  }
+  const double b = dot3(d1, d2);
+  const double denom = a * e - b * b;
+  s = (denom > eps) ? std::fmin(std::fmax((b * f - cc * e) / denom, 0.0), 1.0) : 0.0;
+  t = (b * s + f) / e;
+  if (t < 0.0)
+  {
+    t = 0.0;
+    s = std::fmin(std::fmax(-cc / a, 0.0), 1.0);
+  }
+  else if (t > 1.0)
+  {
+    t = 1.0;
+    s = std::fmin(std::fmax((b - cc) / a, 0.0), 1.0);
+  }
+}
 }  // namespace
+
+// Robot sphere a vs robot sphere b (self-collision), both moving: centers
+// a0 -> a1 and b0 -> b1 over a cast (a1 = a0, b1 = b0 for one state).  The swept
+// shapes are two capsules; their distance is the closest points (sa, sb) of the
+// two center segments, each side's own time along its cast (the cast hulls are
+// independent, not synchronised).  normal from a toward b.
+void selfSphereDistance(const double a0[3], const double a1[3], double ra, const double b0[3], const double b1[3],
+                        double rb, bool cast, double& dist, double n[3], double pa[3], double pb[3], double& sa,
+                        double& sb)
+{
+  const double da[3] = { a1[0] - a0[0], a1[1] - a0[1], a1[2] - a0[2] };
+  const double db[3] = { b1[0] - b0[0], b1[1] - b0[1], b1[2] - b0[2] };
+  sa = sb = 0.0;
+  if (cast)
+    segSegParams(a0, da, b0, db, sa, sb);
+  double ca[3], cb[3];
+  for (int i = 0; i < 3; ++i)
+  {
+    ca[i] = a0[i] + sa * da[i];
+    cb[i] = b0[i] + sb * db[i];
+  }
+  const double v[3] = { cb[0] - ca[0], cb[1] - ca[1], cb[2] - ca[2] };
+  const double L = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+  if (L < 1e-12)
+  {
+    n[0] = 0;
+    n[1] = 0;
+    n[2] = 1;
+  }
+  else
+    for (int i = 0; i < 3; ++i)
+      n[i] = v[i] / L;
+  dist = L - ra - rb;
+  for (int i = 0; i < 3; ++i)
+  {
+    pa[i] = ca[i] + ra * n[i];
+    pb[i] = cb[i] - rb * n[i];
+  }
+}
 
 void sweptSpherePrimDistance(const double a[3], const double b[3], double r, const double* prim, double& dist,
                              double n[3], double p_robot[3], double p_prim[3], double& t_star)
@@ -288,6 +368,110 @@ double linspaced(int size, double low, double high, int i)
 constexpr int kCCNone = 0, kCCTime0 = 1, kCCTime1 = 2, kCCBetween = 3;
 }  // namespace
 
+namespace
+{
+void sphereWorld(const Iso3& T, const double* cl, double* c)
+{
+  for (int r = 0; r < 3; ++r)
+    c[r] = T.R[r * 3 + 0] * cl[0] + T.R[r * 3 + 1] * cl[1] + T.R[r * 3 + 2] * cl[2] + T.t[r];
+}
+
+void toLocal(const Iso3& T, const double* p, double* pl)
+{
+  const double w[3] = { p[0] - T.t[0], p[1] - T.t[1], p[2] - T.t[2] };
+  for (int r = 0; r < 3; ++r)
+    pl[r] = T.R[0 * 3 + r] * w[0] + T.R[1 * 3 + r] * w[1] + T.R[2 * 3 + r] * w[2];
+}
+
+// removeInvalidContactResults (collision_utils.cpp:73-114) at the fixed ends:
+// keep a contact when one of its active sides is not at the fixed end
+bool keepAtFixedEnds(const Contact& ct, bool vars0_fixed, bool vars1_fixed)
+{
+  if (!vars0_fixed && !vars1_fixed)
+    return true;
+  const int ta = ct.cc_type, tb = ct.self() ? ct.cc_type_b : kCCNone;
+  if (vars0_fixed && ((ta != kCCNone && ta != kCCTime0) || (tb != kCCNone && tb != kCCTime0)))
+    return true;
+  if (vars1_fixed && ((ta != kCCNone && ta != kCCTime1) || (tb != kCCNone && tb != kCCTime1)))
+    return true;
+  return false;
+}
+
+// Self contacts of sub-state i (a cast i -> i + 1 when T1 is given) appended to
+// their keys' lists.  mode 0: DISCRETE (CCType_None), 1: LVS_DISCRETE (both
+// sides at the sub-state's time i dt), 2: LVS_CONTINUOUS (each side its own
+// closest-point time, (i + s) dt).
+void addSelfContacts(const CollisionModel& cm, const std::vector<Iso3>& T, const std::vector<Iso3>* T1, int i,
+                     long last, double dt, int mode, bool vars0_fixed, bool vars1_fixed,
+                     std::vector<std::vector<Contact>>& keys)
+{
+  const double threshold = cm.margin + cm.buffer;
+  for (std::size_t j = 0; j < cm.self_a.size(); ++j)
+  {
+    const int sa = cm.self_a[j], sb = cm.self_b[j];
+    const int la = cm.sphere_link[sa], lb = cm.sphere_link[sb];
+    const Iso3 &Ta = T[static_cast<std::size_t>(la)], &Tb = T[static_cast<std::size_t>(lb)];
+    const Iso3& Ta1 = T1 ? (*T1)[static_cast<std::size_t>(la)] : Ta;
+    const Iso3& Tb1 = T1 ? (*T1)[static_cast<std::size_t>(lb)] : Tb;
+    double a0[3], a1[3], b0[3], b1[3];
+    sphereWorld(Ta, cm.sphere_center[sa], a0);
+    sphereWorld(Ta1, cm.sphere_center[sa], a1);
+    sphereWorld(Tb, cm.sphere_center[sb], b0);
+    sphereWorld(Tb1, cm.sphere_center[sb], b1);
+    Contact ct;
+    double ta = 0, tb = 0;
+    selfSphereDistance(a0, a1, cm.sphere_radius[sa], b0, b1, cm.sphere_radius[sb], mode == 2, ct.distance, ct.normal,
+                       ct.p_robot, ct.p_prim, ta, tb);
+    if (!(ct.distance < threshold) || ct.distance > cm.margin + cm.buffer)
+      continue;
+    ct.link = la;
+    ct.sphere = sa;
+    ct.prim = -1 - sb;
+    ct.link_b = lb;
+    ct.sphere_b = sb;
+    ct.substate = i;
+    ct.transform = Ta;
+    ct.cc_transform = Ta1;
+    ct.transform_b = Tb;
+    ct.cc_transform_b = Tb1;
+    toLocal(Ta, ct.p_robot, ct.p_local);
+    toLocal(Tb, ct.p_prim, ct.p_local_b);
+    if (mode == 0)
+    {
+      ct.cc_time = ct.cc_time_b = 0;
+      ct.cc_type = ct.cc_type_b = kCCNone;
+    }
+    else if (mode == 1)
+    {
+      ct.cc_time = ct.cc_time_b = double(i) * dt;
+      ct.cc_type = ct.cc_type_b = (i == 0) ? kCCTime0 : ((i == last) ? kCCTime1 : kCCBetween);
+    }
+    else
+    {
+      ct.cc_time = (double(i) + ta) * dt;
+      ct.cc_time_b = (double(i) + tb) * dt;
+      ct.cc_type = (i == 0 && ta == 0.0) ? kCCTime0 : ((i + 1 == last && ta == 1.0) ? kCCTime1 : kCCBetween);
+      ct.cc_type_b = (i == 0 && tb == 0.0) ? kCCTime0 : ((i + 1 == last && tb == 1.0) ? kCCTime1 : kCCBetween);
+    }
+    if (!keepAtFixedEnds(ct, vars0_fixed, vars1_fixed))
+      continue;
+    keys[static_cast<std::size_t>(cm.self_key[j])].push_back(ct);
+  }
+}
+
+// the flattened map: scene keys (link, primitive), then the self keys in order
+std::vector<Contact> flatten(std::map<std::pair<int, int>, std::vector<Contact>>& scene,
+                             std::vector<std::vector<Contact>>& self)
+{
+  std::vector<Contact> flat;
+  for (auto& kv : scene)
+    flat.insert(flat.end(), kv.second.begin(), kv.second.end());
+  for (auto& v : self)
+    flat.insert(flat.end(), v.begin(), v.end());
+  return flat;
+}
+}  // namespace
+
 // SingleTimestepCollisionEvaluator::CalcCollisions (collision_terms.cpp:653-688):
 // FK at one state, contactTest, then the filter drops contacts beyond
 // margin + buffer (no cc_type filtering; the results keep CCType_None).
@@ -296,6 +480,7 @@ std::vector<Contact> calcCollisionsSingle(const CollisionModel& cm, const double
   const thip_chain& ch = *cm.chain;
   const double threshold = cm.margin + cm.buffer;
   std::map<std::pair<int, int>, std::vector<Contact>> results;
+  std::vector<std::vector<Contact>> self(static_cast<std::size_t>(cm.n_self_keys));
   std::vector<Iso3> T;
   chainFwdKin(ch, q, T);
   for (int s = 0; s < cm.n_spheres; ++s)
@@ -303,9 +488,7 @@ std::vector<Contact> calcCollisionsSingle(const CollisionModel& cm, const double
     const int link = cm.sphere_link[s];
     const Iso3& Tl = T[static_cast<std::size_t>(link)];
     double c[3];
-    for (int r = 0; r < 3; ++r)
-      c[r] = Tl.R[r * 3 + 0] * cm.sphere_center[s][0] + Tl.R[r * 3 + 1] * cm.sphere_center[s][1] +
-             Tl.R[r * 3 + 2] * cm.sphere_center[s][2] + Tl.t[r];
+    sphereWorld(Tl, cm.sphere_center[s], c);
     for (int p = 0; p < cm.n_prims; ++p)
     {
       Contact ct;
@@ -318,23 +501,20 @@ std::vector<Contact> calcCollisionsSingle(const CollisionModel& cm, const double
       ct.substate = 0;
       ct.transform = Tl;
       ct.cc_transform = Tl;
-      const double w[3] = { ct.p_robot[0] - Tl.t[0], ct.p_robot[1] - Tl.t[1], ct.p_robot[2] - Tl.t[2] };
-      for (int r = 0; r < 3; ++r)
-        ct.p_local[r] = Tl.R[0 * 3 + r] * w[0] + Tl.R[1 * 3 + r] * w[1] + Tl.R[2 * 3 + r] * w[2];
+      toLocal(Tl, ct.p_robot, ct.p_local);
       ct.cc_time = 0;
       ct.cc_type = 0;  // CCType_None
       results[{ link, p }].push_back(ct);
     }
   }
-  std::vector<Contact> flat;
-  for (auto& kv : results)
-    flat.insert(flat.end(), kv.second.begin(), kv.second.end());
-  return flat;
+  addSelfContacts(cm, T, nullptr, 0, 0, 0.0, 0, false, false, self);
+  return flatten(results, self);
 }
 
 // DiscreteCollisionEvaluator::CalcCollisions (collision_terms.cpp:817-898) for
 // the step pair (q0, q1); results flattened in ContactResultMap order: link
-// pair key (robot link, primitive), then insertion (sub-state, sphere).
+// pair key (robot link, primitive), then the self keys, then insertion
+// (sub-state, sphere).
 std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, const double* q1, bool vars0_fixed,
                                     bool vars1_fixed)
 {
@@ -351,6 +531,7 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
   const double dt = 1.0 / double(last);
   const double threshold = cm.margin + cm.buffer;  // incrementCollisionMargin(buffer)
   std::map<std::pair<int, int>, std::vector<Contact>> results;
+  std::vector<std::vector<Contact>> self(static_cast<std::size_t>(cm.n_self_keys));
   std::vector<double> q(static_cast<std::size_t>(D));
   std::vector<Iso3> T;
   if (cm.continuous)
@@ -376,13 +557,8 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
         const Iso3& Ta = T[static_cast<std::size_t>(link)];
         const Iso3& Tb = T1[static_cast<std::size_t>(link)];
         double ca[3], cb[3];
-        for (int r = 0; r < 3; ++r)
-        {
-          ca[r] = Ta.R[r * 3 + 0] * cm.sphere_center[s][0] + Ta.R[r * 3 + 1] * cm.sphere_center[s][1] +
-                  Ta.R[r * 3 + 2] * cm.sphere_center[s][2] + Ta.t[r];
-          cb[r] = Tb.R[r * 3 + 0] * cm.sphere_center[s][0] + Tb.R[r * 3 + 1] * cm.sphere_center[s][1] +
-                  Tb.R[r * 3 + 2] * cm.sphere_center[s][2] + Tb.t[r];
-        }
+        sphereWorld(Ta, cm.sphere_center[s], ca);
+        sphereWorld(Tb, cm.sphere_center[s], cb);
         for (int p = 0; p < cm.n_prims; ++p)
         {
           Contact ct;
@@ -398,28 +574,19 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
           ct.transform = Ta;
           ct.cc_transform = Tb;
           // nearest_points_local[0] in the link frame at the cast's start state
-          const double w[3] = { ct.p_robot[0] - Ta.t[0], ct.p_robot[1] - Ta.t[1], ct.p_robot[2] - Ta.t[2] };
-          for (int r = 0; r < 3; ++r)
-            ct.p_local[r] = Ta.R[0 * 3 + r] * w[0] + Ta.R[1 * 3 + r] * w[1] + Ta.R[2 * 3 + r] * w[2];
+          toLocal(Ta, ct.p_robot, ct.p_local);
           ct.cc_time = (double(i) + ts) * dt;
           ct.cc_type = (i == 0 && ts == 0.0) ? kCCTime0 : ((i + 1 == last && ts == 1.0) ? kCCTime1 : kCCBetween);
           if (ct.distance > cm.margin + cm.buffer)
             continue;
-          if (vars0_fixed || vars1_fixed)
-          {
-            const bool keep = (vars0_fixed && ct.cc_type != kCCNone && ct.cc_type != kCCTime0) ||
-                              (vars1_fixed && ct.cc_type != kCCNone && ct.cc_type != kCCTime1);
-            if (!keep)
-              continue;
-          }
+          if (!keepAtFixedEnds(ct, vars0_fixed, vars1_fixed))
+            continue;
           results[{ link, p }].push_back(ct);
         }
       }
+      addSelfContacts(cm, T, &T1, static_cast<int>(i), last, dt, 2, vars0_fixed, vars1_fixed, self);
     }
-    std::vector<Contact> flat;
-    for (auto& kv : results)
-      flat.insert(flat.end(), kv.second.begin(), kv.second.end());
-    return flat;
+    return flatten(results, self);
   }
   for (long i = 0; i < cnt; ++i)
   {
@@ -431,9 +598,7 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
       const int link = cm.sphere_link[s];
       const Iso3& Tl = T[static_cast<std::size_t>(link)];
       double c[3];
-      for (int r = 0; r < 3; ++r)
-        c[r] = Tl.R[r * 3 + 0] * cm.sphere_center[s][0] + Tl.R[r * 3 + 1] * cm.sphere_center[s][1] +
-               Tl.R[r * 3 + 2] * cm.sphere_center[s][2] + Tl.t[r];
+      sphereWorld(Tl, cm.sphere_center[s], c);
       for (int p = 0; p < cm.n_prims; ++p)
       {
         Contact ct;
@@ -448,9 +613,7 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
         ct.transform = Tl;
         ct.cc_transform = Tl;
         // nearest_points_local[0]: the robot point in the link frame
-        const double w[3] = { ct.p_robot[0] - Tl.t[0], ct.p_robot[1] - Tl.t[1], ct.p_robot[2] - Tl.t[2] };
-        for (int r = 0; r < 3; ++r)
-          ct.p_local[r] = Tl.R[0 * 3 + r] * w[0] + Tl.R[1 * 3 + r] * w[1] + Tl.R[2 * 3 + r] * w[2];
+        toLocal(Tl, ct.p_robot, ct.p_local);
         // addInterpolatedCollisionResults(.., discrete = true): active link only
         ct.cc_time = double(i) * dt;
         ct.cc_type = (i == 0) ? kCCTime0 : ((i == last) ? kCCTime1 : kCCBetween);
@@ -458,21 +621,14 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
         // (collision_utils.cpp:73-114); the static primitive has CCType_None
         if (ct.distance > cm.margin + cm.buffer)
           continue;
-        if (vars0_fixed || vars1_fixed)
-        {
-          const bool keep = (vars0_fixed && ct.cc_type != kCCNone && ct.cc_type != kCCTime0) ||
-                            (vars1_fixed && ct.cc_type != kCCNone && ct.cc_type != kCCTime1);
-          if (!keep)
-            continue;
-        }
+        if (!keepAtFixedEnds(ct, vars0_fixed, vars1_fixed))
+          continue;
         results[{ link, p }].push_back(ct);
       }
     }
+    addSelfContacts(cm, T, nullptr, static_cast<int>(i), last, dt, 1, vars0_fixed, vars1_fixed, self);
   }
-  std::vector<Contact> flat;
-  for (auto& kv : results)
-    flat.insert(flat.end(), kv.second.begin(), kv.second.end());
-  return flat;
+  return flatten(results, self);
 }
 
 // CollisionEvaluator::GetGradient (collision_terms.cpp:195-242) for the robot
@@ -481,21 +637,27 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
 // discrete-continuous results cc_transform == transform), gradient
 // -normal^T J_lin, scale 1 - cc_time (timestep 0) or cc_time (timestep 1).
 void contactGradient(const CollisionModel& cm, const double* dofvals, const Contact& ct, bool timestep1,
-                     double* grad, double& scale)
+                     double* grad, double& scale, int side)
 {
   const thip_chain& ch = *cm.chain;
   const int D = ch.n_dof;
   double J[6 * THIP_MAX_DOF];
-  chainJacobian(ch, dofvals, ct.link, J);
+  const bool b = side == 1;
+  chainJacobian(ch, dofvals, b ? ct.link_b : ct.link, J);
   // scale 1 and link_transform = transform for CCType_None; otherwise scale
   // (1 - cc_time) / cc_time and link_transform = transform / cc_transform
   // (collision_terms.cpp:214-221)
-  const bool none = ct.cc_type == kCCNone;
-  const Iso3& lt = (timestep1 && !none) ? ct.cc_transform : ct.transform;
+  const int type = b ? ct.cc_type_b : ct.cc_type;
+  const double cc_time = b ? ct.cc_time_b : ct.cc_time;
+  const bool none = type == kCCNone;
+  const Iso3& lt = (timestep1 && !none) ? (b ? ct.cc_transform_b : ct.cc_transform) : (b ? ct.transform_b : ct.transform);
+  const double* pl = b ? ct.p_local_b : ct.p_local;
   double r[3];
   for (int i = 0; i < 3; ++i)
-    r[i] = lt.R[i * 3 + 0] * ct.p_local[0] + lt.R[i * 3 + 1] * ct.p_local[1] + lt.R[i * 3 + 2] * ct.p_local[2];
-  scale = none ? 1.0 : (timestep1 ? ct.cc_time : (1 - ct.cc_time));
+    r[i] = lt.R[i * 3 + 0] * pl[0] + lt.R[i * 3 + 1] * pl[1] + lt.R[i * 3 + 2] * pl[2];
+  scale = none ? 1.0 : (timestep1 ? cc_time : (1 - cc_time));
+  // gradient = (i == 0 ? -1 : 1) * normal^T J_lin (collision_terms.cpp:232)
+  const double sg = b ? 1.0 : -1.0;
   for (int j = 0; j < D; ++j)
   {
     // jacobianChangeRefPoint: J_lin += J_ang x r
@@ -503,8 +665,53 @@ void contactGradient(const CollisionModel& cm, const double* dofvals, const Cont
     const double l0 = J[0 * D + j] + (wy * r[2] - wz * r[1]);
     const double l1 = J[1 * D + j] + (wz * r[0] - wx * r[2]);
     const double l2 = J[2 * D + j] + (wx * r[1] - wy * r[0]);
-    grad[j] = -1.0 * (ct.normal[0] * l0 + ct.normal[1] * l1 + ct.normal[2] * l2);
+    grad[j] = sg * (ct.normal[0] * l0 + ct.normal[1] * l1 + ct.normal[2] * l2);
   }
+}
+
+void contactExpression(const CollisionModel& cm, const Contact& ct, const double* q0, const double* q1, bool use0,
+                       bool use1, bool single, double* a0, double* a1, double& cst, int& mask)
+{
+  const int D = cm.chain->n_dof;
+  const int nsides = ct.self() ? 2 : 1;
+  mask = 0;
+  for (int j = 0; j < D; ++j)
+    a0[j] = a1[j] = 0.0;
+  // one timestep's part (CollisionsToDistanceExpressions): per side varDot(scale g, vars)
+  // and scale * -g.q, the constant summed over the sides from 0
+  auto part = [&](const double* q, bool ts1, double* a, int bit0) {
+    double c = 0.0;
+    for (int side = 0; side < nsides; ++side)
+    {
+      double g[THIP_MAX_DOF], scale, gd = 0;
+      contactGradient(cm, q, ct, ts1, g, scale, side);
+      for (int j = 0; j < D; ++j)
+      {
+        const double av = scale * g[j];
+        gd += g[j] * q[j];
+        if (std::fabs(av) > 1e-7)  // cleanupAff
+        {
+          a[j] = (mask & (1 << (bit0 + j))) ? a[j] + av : av;
+          mask |= 1 << (bit0 + j);
+        }
+      }
+      c += scale * -gd;
+    }
+    return c;
+  };
+  if (single)
+  {
+    // CalcDistExpressionsSingleTimeStep: 0 + part(x_t), then + d
+    cst = 0.0 + part(q0, false, a0, 0);
+    cst += ct.distance;
+    return;
+  }
+  // CalcDistExpressions{BothFree, StartFree, EndFree}: d + part(x_t) + part(x_t+1)
+  cst = ct.distance;
+  if (use0)
+    cst += part(q0, false, a0, 0);
+  if (use1)
+    cst += part(q1, true, a1, D);
 }
 
 namespace
@@ -542,32 +749,24 @@ public:
     const int D = cm_->chain->n_dof;
     for (const auto& c : contacts)
     {
-      AffExpr e(c.distance);
-      auto add_part = [&](const VarVector& vars, const DblVec& dof, bool ts1) {
-        double g[THIP_MAX_DOF], scale;
-        contactGradient(*cm_, dof.data(), c, ts1, g, scale);
-        // CollisionsToDistanceExpressions: varDot(scale * g, vars) + scale * -g.dot(dofvals)
-        AffExpr part;
-        double gd = 0;
-        for (int j = 0; j < D; ++j)
+      double a0[THIP_MAX_DOF], a1[THIP_MAX_DOF], cst;
+      int mask;
+      contactExpression(*cm_, c, q0.data(), q1.data(), type_ != kStartFixedEndFree, type_ != kStartFreeEndFixed,
+                        false, a0, a1, cst, mask);
+      AffExpr e(cst);
+      for (int j = 0; j < D; ++j)
+        if (mask & (1 << j))
         {
-          part.coeffs.push_back(scale * g[j]);
-          part.vars.push_back(vars[static_cast<std::size_t>(j)]);
-          gd += g[j] * dof[static_cast<std::size_t>(j)];
+          e.coeffs.push_back(a0[j]);
+          e.vars.push_back(vars0_[static_cast<std::size_t>(j)]);
         }
-        part.constant = scale * -gd;
-        exprInc(e, part);
-      };
-      if (type_ == kBothFree)
-      {
-        add_part(vars0_, q0, false);
-        add_part(vars1_, q1, true);
-      }
-      else if (type_ == kStartFixedEndFree)
-        add_part(vars1_, q1, true);
-      else
-        add_part(vars0_, q0, false);
-      out.push_back(cleanupAff(e));
+      for (int j = 0; j < D; ++j)
+        if (mask & (1 << (D + j)))
+        {
+          e.coeffs.push_back(a1[j]);
+          e.vars.push_back(vars1_[static_cast<std::size_t>(j)]);
+        }
+      out.push_back(e);
     }
     return out;
   }
@@ -609,21 +808,17 @@ public:
     const int D = cm_->chain->n_dof;
     for (const auto& c : contacts)
     {
-      AffExpr e(0.0);
-      double g[THIP_MAX_DOF], scale;
-      contactGradient(*cm_, q.data(), c, false, g, scale);
-      AffExpr part;
-      double gd = 0;
+      double a0[THIP_MAX_DOF], a1[THIP_MAX_DOF], cst;
+      int mask;
+      contactExpression(*cm_, c, q.data(), q.data(), true, false, true, a0, a1, cst, mask);
+      AffExpr e(cst);
       for (int j = 0; j < D; ++j)
-      {
-        part.coeffs.push_back(scale * g[j]);
-        part.vars.push_back(vars0_[static_cast<std::size_t>(j)]);
-        gd += g[j] * q[static_cast<std::size_t>(j)];
-      }
-      exprInc(e, part);
-      exprInc(e, scale * -gd);
-      exprInc(e, c.distance);
-      out.push_back(cleanupAff(e));
+        if (mask & (1 << j))
+        {
+          e.coeffs.push_back(a0[j]);
+          e.vars.push_back(vars0_[static_cast<std::size_t>(j)]);
+        }
+      out.push_back(e);
     }
     return out;
   }
@@ -743,6 +938,18 @@ std::shared_ptr<CollisionModel> collisionModel(const thip_problem_desc& d, const
   cm->buffer = t.buffer;
   cm->lvs = t.lvs;
   cm->continuous = t.continuous == 1;
+  // self pairs in key order: link pairs as given, spheres of a then of b in index order
+  for (int k = 0; k < d.n_self_pairs; ++k)
+    for (int sa = 0; sa < d.n_spheres; ++sa)
+      if (d.sphere_link[sa] == d.self_pair[k][0])
+        for (int sb = 0; sb < d.n_spheres; ++sb)
+          if (d.sphere_link[sb] == d.self_pair[k][1])
+          {
+            cm->self_a.push_back(sa);
+            cm->self_b.push_back(sb);
+            cm->self_key.push_back(k);
+          }
+  cm->n_self_keys = d.n_self_pairs;
   return cm;
 }
 

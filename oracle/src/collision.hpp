@@ -37,13 +37,20 @@ struct CollisionModel
   const double* scene = nullptr;  // [n_prims][16]
   double margin = 0, coeff = 0, buffer = 0, lvs = 0;
   bool continuous = false;  // LVS_CONTINUOUS (CastCollisionEvaluator) instead of LVS_DISCRETE
+  // robot self-collision (desc.self_pair): sphere pairs (a, b) in key order --
+  // link pairs in descriptor order, then the spheres of a, then those of b
+  // (sphere index order) -- and the key of each
+  std::vector<int> self_a, self_b, self_key;
+  int n_self_keys = 0;
 };
 
 // A contact between a robot link sphere (link_ids[0], active) and a scene
-// primitive (link_ids[1], static).
+// primitive (link_ids[1], static), or -- a self contact -- another robot link
+// sphere (link_ids[1], active: prim = -1 - sphere_b).
 struct Contact
 {
   int link = 0, prim = 0, sphere = 0, substate = 0;
+  int link_b = -1, sphere_b = -1;  // self contact: the second body
   double distance = 0;
   double normal[3];    // from the robot sphere toward the primitive
   double p_robot[3];   // nearest points, world
@@ -53,6 +60,12 @@ struct Contact
   Iso3 cc_transform;   // = transform (discrete) / link pose at the cast's end state (continuous)
   double cc_time = 0;  // interpolation time of the sub-state / of the closest point along the cast
   int cc_type = 0;     // 0 None (single-timestep contactTest), 1 Time0, 2 Time1, 3 Between
+  // the second body of a self contact, as the first's fields
+  double p_local_b[3] = { 0, 0, 0 };
+  Iso3 transform_b, cc_transform_b;
+  double cc_time_b = 0;
+  int cc_type_b = 0;
+  bool self() const { return sphere_b >= 0; }
 };
 
 void spherePrimDistance(const double c[3], double r, const double* prim, double& dist, double n[3],
@@ -61,11 +74,25 @@ void spherePrimDistance(const double c[3], double r, const double* prim, double&
 // distance min_t d(a + t (b - a)) and its first minimiser t (see collision.cpp).
 void sweptSpherePrimDistance(const double a[3], const double b[3], double r, const double* prim, double& dist,
                              double n[3], double p_robot[3], double p_prim[3], double& t_star);
+// Robot sphere vs robot sphere (self-collision), see collision.cpp.
+void selfSphereDistance(const double a0[3], const double a1[3], double ra, const double b0[3], const double b1[3],
+                        double rb, bool cast, double& dist, double n[3], double pa[3], double pb[3], double& sa,
+                        double& sb);
 std::vector<Contact> calcCollisionsSingle(const CollisionModel& cm, const double* q);
 std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, const double* q1, bool vars0_fixed,
                                     bool vars1_fixed);
+// GetGradient of one side (0: link_ids[0], the robot sphere; 1: the second
+// robot link of a self contact)
 void contactGradient(const CollisionModel& cm, const double* dofvals, const Contact& ct, bool timestep1,
-                     double* grad, double& scale);
+                     double* grad, double& scale, int side = 0);
+// The linearised distance of a contact over the free ends of its unit
+// (CollisionsToDistanceExpressions + CalcDistExpressions*, collision_terms.cpp:
+// 341-386, 463-554) as dense coefficients a0 (x_t) / a1 (x_t+1) and constant:
+// cleanupAff's 1e-7 per side term, a variable's side terms summed (the QP
+// builder sums the duplicates); mask bit e*D+j = coefficient present.
+// single: DISCRETE (0 + sum g.(x - q) + d over x_t, scale 1).
+void contactExpression(const CollisionModel& cm, const Contact& ct, const double* q0, const double* q1, bool use0,
+                       bool use1, bool single, double* a0, double* a1, double& cst, int& mask);
 
 // collision term k of the descriptor: 0 = the coll_* fields, k >= 1 = coll_extra[k - 1]
 thip_coll_term collisionTerm(const thip_problem_desc& d, int k);

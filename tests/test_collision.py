@@ -68,7 +68,8 @@ def test_collision_rows_semantics(oracle_mod):
 
 def test_collision_gradient_matches_finite_differences(oracle_mod):
     """For a sub-state-0 contact of a free start step the x_t coefficients are
-    the true gradient d distance / d q_t (the sub-state is q_t itself)."""
+    the true gradient d distance / d q_t (the sub-state is q_t itself); for a
+    self contact (shoulder_pan vs a wrist link) the gradient of both links."""
     wl = _coll_wl(8)
     x, _ = oracle_mod.solve(wl, n_threads=8)
     D = wl.n_dof
@@ -84,6 +85,11 @@ def test_collision_gradient_matches_finite_differences(oracle_mod):
             def dist(q):
                 T = robots.fwd_kin(chain, q)
                 c = T[link][:3, :3] @ np.array(c_loc) + T[link][:3, 3]
+                if prim < 0:
+                    # a self contact: the second body is robot sphere -1 - prim (both move with q)
+                    lb, cb_loc, rb = scene.PR2_ARM_SPHERES[-1 - prim]
+                    cb = T[lb][:3, :3] @ np.array(cb_loc) + T[lb][:3, 3]
+                    return float(np.linalg.norm(cb - c)) - rad - rb
                 return scene.sphere_prim_distance(c, rad, wl.scene[b, prim])[0]
 
             q = x[b, t].copy()
@@ -206,3 +212,77 @@ def test_discrete_rows_match_lvs_substate_zero(oracle_mod):
             assert len(a) == len(l)
             np.testing.assert_array_equal(a[:, [1, 2, 3, 5, 7]], l[:, [1, 2, 3, 5, 7]])
             np.testing.assert_array_equal(a[:, 8:], l[:, 8:])
+
+
+def _dual_arm_crossing(wl, rng, lo_d=-0.02, hi_d=0.04, tries=20000):
+    """A both-arms configuration whose closest enabled inter-arm sphere pair is
+    within (lo_d, hi_d) (arms crossed in front of the torso)."""
+    d = wl.desc
+    chain = d.chain
+    spheres = scene.desc_spheres(d)
+    pairs = [(a, b) for a, b in ((d.self_pair[k][0], d.self_pair[k][1]) for k in range(d.n_self_pairs))]
+    lo, hi, _ = robots.chain_limits(chain)
+    lo, hi = np.maximum(lo, -3.0), np.minimum(hi, 3.0)
+    for _ in range(tries):
+        q = lo + (hi - lo) * rng.uniform(size=lo.shape)
+        C = scene.sphere_centers(chain, q, spheres=spheres)
+        best = np.inf
+        for la, lb in pairs:
+            if la > 11 or lb < 12:
+                continue  # inter-arm pairs only
+            for sa, (ka, _, ra) in enumerate(spheres):
+                for sb, (kb, _, rb) in enumerate(spheres):
+                    if ka == la and kb == lb:
+                        best = min(best, float(np.linalg.norm(C[sb] - C[sa])) - ra - rb)
+        if lo_d < best < hi_d:
+            return q
+    raise AssertionError("no crossing configuration found")
+
+
+def test_self_collision_dual_arm_rows(oracle_mod):
+    """Config E's both-arms group tests the arm link pairs pr2.srdf leaves
+    enabled against each other (collision_terms.cpp:817-898 over the manager's
+    active links): a crossed-arms trajectory yields self contacts after the
+    unit's scene contacts, keys in self_pair order, sphere a on the lower link;
+    their x_t coefficients are the distance gradient in all 14 joints (both
+    arms move the contact), and the distance is the sphere-sphere distance."""
+    wl = problems.make_workload("E", 1)
+    d = wl.desc
+    assert d.n_self_pairs == 37  # 33 inter-arm + 2 per arm (shoulder_pan vs the wrist links)
+    q = _dual_arm_crossing(wl, np.random.default_rng(5))
+    x = np.repeat(q[None, :], wl.n_steps, axis=0)
+    rows = oracle_mod.collision_rows(wl, 0, x)
+    spheres = scene.desc_spheres(d)
+    chain = d.chain
+    D = wl.n_dof
+    keys = [(d.self_pair[k][0], d.self_pair[k][1]) for k in range(d.n_self_pairs)]
+    checked = 0
+    for t in range(1, wl.n_steps - 1):
+        unit = rows[rows[:, 0] == t]
+        prims = unit[:, 2].astype(int)
+        self_rows = unit[prims < 0]
+        assert len(self_rows) > 0
+        first_self = int(np.argmax(prims < 0))
+        assert np.all(prims[first_self:] < 0)  # scene keys first
+        order = [keys.index((spheres[int(r[3])][0], spheres[-1 - int(r[2])][0])) for r in self_rows]
+        assert order == sorted(order)
+        for r in self_rows:
+            sa, sb = int(r[3]), -1 - int(r[2])
+            la, ca, ra = spheres[sa]
+            lb, cb, rb = spheres[sb]
+            assert la < lb and int(r[1]) == la
+
+            def dist(qq):
+                T = robots.fwd_kin(chain, qq)
+                pa = T[la][:3, :3] @ np.array(ca) + T[la][:3, 3]
+                pb = T[lb][:3, :3] @ np.array(cb) + T[lb][:3, 3]
+                return float(np.linalg.norm(pb - pa)) - ra - rb
+
+            assert dist(q) == pytest.approx(r[5], abs=1e-12)
+            h = 1e-6
+            g = np.array([(dist(q + h * np.eye(D)[j]) - dist(q - h * np.eye(D)[j])) / (2 * h) for j in range(D)])
+            a = r[8:8 + D]
+            np.testing.assert_allclose(a[np.abs(g) > 1e-6], g[np.abs(g) > 1e-6], rtol=1e-5, atol=1e-7)
+            assert np.any(np.abs(a[:7]) > 1e-6) and np.any(np.abs(a[7:]) > 1e-6)  # both arms
+            checked += 1
+    assert checked > 0

@@ -245,11 +245,47 @@ def test_collision_rows_parity_dual_arm(oracle_mod):
         _check_rows(rows_init[b], oracle_mod.collision_rows(wl, b, wl.init[b]), f"problem {b} (init)", cc_atol=1e-12)
 
 
+def test_collision_rows_parity_self(oracle_mod):
+    """Robot self-collision (the link pairs pr2.srdf's ACM leaves enabled): on a
+    crossed-arms trajectory of config E the fused kernel's contact rows -- the
+    scene keys, then the self keys, both links' gradients -- match the oracle,
+    for LVS_CONTINUOUS (each side its own closest-point time along its cast)
+    and LVS_DISCRETE; the device evaluator of the generic path gives the same
+    records."""
+    from test_collision import _dual_arm_crossing
+    from trajopt_amd.runtime import TermEvaluator
+    wl = problems.make_workload("E", 4, n_steps=12)
+    rng = np.random.default_rng(11)
+    q = [_dual_arm_crossing(wl, rng) for _ in range(wl.batch)]
+    # a trajectory sweeping through the crossing: casts with distinct end states
+    x = np.stack([qb[None, :] + 0.02 * np.sin(np.arange(wl.n_steps)[:, None] + np.arange(wl.n_dof)[None, :])
+                  for qb in q])
+    for cont in (1, 0):
+        wl.desc.coll_continuous = cont
+        s = BatchTrustRegionSQP(wl)
+        rows = s.collision_rows(x)
+        s.close()
+        n_self = 0
+        for b in range(wl.batch):
+            rc = oracle_mod.collision_rows(wl, b, x[b])
+            _check_rows(rows[b], rc, f"problem {b} (continuous {cont})", cc_atol=1e-12)
+            n_self += int((rc[:, 2] < 0).sum())
+        assert n_self > 0
+        ev = TermEvaluator(wl)
+        try:
+            recs = ev.collision(0, x)
+        finally:
+            ev.close()
+        for b in range(wl.batch):
+            _check_rows(recs[b], oracle_mod.collision_rows(wl, b, x[b]), f"eval problem {b} (continuous {cont})",
+                        cc_atol=1e-12)
+
+
 def test_sqp_parity_dual_arm_E(oracle_mod):
     """Config E (BASELINE.json configs[4]): 14-DoF dual arm, 50 waypoints,
-    both tool frames tracked, LVS_CONTINUOUS collision -- no term touches both
-    arms, so the block solve splits into two 7-dof branches (Layout::nbr), each
-    with its own twisted factorisation on two waves."""
+    both tool frames tracked, LVS_CONTINUOUS collision including the inter-arm
+    self-collision pairs -- they couple the arms, so the block solve runs the
+    14-dof wide path."""
     wl = problems.make_workload("E", 4)
     x, res, _ = solve_gpu(wl)
     assert all(r.flags == 0 for r in res)

@@ -241,6 +241,88 @@ __device__ inline void swept_sphere_prim_distance(const double a[3], const doubl
   t_star = t;
 }
 
+// Both parameters of the closest points of segments p1 + s d1 and p2 + t d2
+// (oracle segSegParams; s as sseg_param computes it).
+__device__ inline void sseg_params(const double p1[3], const double d1[3], const double p2[3], const double d2[3],
+                                   double& s, double& t)
+{
+  const double r[3] = { p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2] };
+  const double a = d1[0] * d1[0] + d1[1] * d1[1] + d1[2] * d1[2];
+  const double e = d2[0] * d2[0] + d2[1] * d2[1] + d2[2] * d2[2];
+  const double f = d2[0] * r[0] + d2[1] * r[1] + d2[2] * r[2];
+  const double eps = 1e-24;
+  if (a <= eps && e <= eps)
+  {
+    s = t = 0.0;
+    return;
+  }
+  if (a <= eps)
+  {
+    s = 0.0;
+    t = fmin(fmax(f / e, 0.0), 1.0);
+    return;
+  }
+  const double cc = d1[0] * r[0] + d1[1] * r[1] + d1[2] * r[2];
+  if (e <= eps)
+  {
+    t = 0.0;
+    s = fmin(fmax(-cc / a, 0.0), 1.0);
+    return;
+  }
+  const double b = d1[0] * d2[0] + d1[1] * d2[1] + d1[2] * d2[2];
+  const double denom = a * e - b * b;
+  s = (denom > eps) ? fmin(fmax((b * f - cc * e) / denom, 0.0), 1.0) : 0.0;
+  t = (b * s + f) / e;
+  if (t < 0.0)
+  {
+    t = 0.0;
+    s = fmin(fmax(-cc / a, 0.0), 1.0);
+  }
+  else if (t > 1.0)
+  {
+    t = 1.0;
+    s = fmin(fmax((b - cc) / a, 0.0), 1.0);
+  }
+}
+
+// Robot sphere a vs robot sphere b (self-collision), both moving: centers
+// a0 -> a1, b0 -> b1 over a cast (a1 = a0, b1 = b0 for one state); the two
+// capsules' distance at the closest points (sa, sb) of the center segments,
+// each side its own time; normal from a toward b (oracle selfSphereDistance).
+__device__ inline void self_sphere_distance(const double a0[3], const double a1[3], double ra, const double b0[3],
+                                            const double b1[3], double rb, bool cast, double& dist, double n[3],
+                                            double pa[3], double pb[3], double& sa, double& sb)
+{
+  const double da[3] = { a1[0] - a0[0], a1[1] - a0[1], a1[2] - a0[2] };
+  const double db[3] = { b1[0] - b0[0], b1[1] - b0[1], b1[2] - b0[2] };
+  sa = sb = 0.0;
+  if (cast)
+    sseg_params(a0, da, b0, db, sa, sb);
+  double ca[3], cb[3];
+  for (int i = 0; i < 3; ++i)
+  {
+    ca[i] = a0[i] + sa * da[i];
+    cb[i] = b0[i] + sb * db[i];
+  }
+  const double v[3] = { cb[0] - ca[0], cb[1] - ca[1], cb[2] - ca[2] };
+  const double L = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+  if (L < 1e-12)
+  {
+    n[0] = 0;
+    n[1] = 0;
+    n[2] = 1;
+  }
+  else
+    for (int i = 0; i < 3; ++i)
+      n[i] = v[i] / L;
+  dist = L - ra - rb;
+  for (int i = 0; i < 3; ++i)
+  {
+    pa[i] = ca[i] + ra * n[i];
+    pb[i] = cb[i] - rb * n[i];
+  }
+}
+
 // A lower bound of the swept distance (segment to the primitive's bounding
 // sphere): a candidate whose bound exceeds the contact distance cannot be a
 // contact, so the exact cast is skipped.

@@ -280,6 +280,12 @@ struct Tables
   int* jvx_slot;
   int* coll_slot;  // per collision unit (step pair, or waypoint for DISCRETE): term slot
                    // relative to coll_cost0, -1 for a fixed waypoint without a term (N)
+  // robot self-collision (self_pairs.hpp): sphere pairs in key order, the spheres
+  // of link a and of link b, and the first pair of each key (n_self_keys + 1)
+  int n_self_keys, n_self_sph;
+  int* self_sa;
+  int* self_sb;
+  int* self_kp;
 };
 
 struct KernelArgs

@@ -599,7 +599,8 @@ __device__ bool coll_substates_batched(Ctx& c, const double* x)
       const int cnt = c.s->subcnt[t];
       acc += cnt;
       const int nseg = cont ? cnt - 1 : cnt;
-      wacc += (c.d->n_prims * (nseg > 0 ? nseg : 0) * ns + 63) / 64 * 2;  // whole 64-bit chunks
+      // scene then self candidates, whole 64-bit chunks
+      wacc += ((c.d->n_prims * ns + c.T.n_self_sph) * (nseg > 0 ? nseg : 0) + 63) / 64 * 2;
     }
     c.s->suboff[L.coll_last] = acc;
     c.s->hboff[L.coll_last] = wacc;
@@ -636,6 +637,50 @@ __device__ bool coll_substates_batched(Ctx& c, const double* x)
   if (pf22)
     pf22[22] += clock64() - tfk0;
   return true;
+}
+
+// Self-collision candidate q of a unit (0 <= q < nseg * n_self_sph, in key
+// order: link pair, then sub-state, then sphere pair of the key): its
+// sub-state i, spheres (sa, sb), distance, and the cc types of both sides
+// (1 Time0, 2 Time1, 3 Between; oracle addSelfContacts).
+__device__ __forceinline__ void self_candidate(const Ctx& c, const CollStage& S, const double* SCR, int ns, int nseg,
+                                               int last, bool cont, int q, int& i, int& sa, int& sb, double& dist,
+                                               int& cta, int& ctb)
+{
+  int r = q, k = 0;
+  for (; k + 1 < c.T.n_self_keys; ++k)
+  {
+    const int sz = nseg * (c.T.self_kp[k + 1] - c.T.self_kp[k]);
+    if (r < sz)
+      break;
+    r -= sz;
+  }
+  const int k0 = c.T.self_kp[k], npk = c.T.self_kp[k + 1] - k0;
+  i = r / npk;
+  const int j = k0 + (r - i * npk);
+  sa = c.T.self_sa[j];
+  sb = c.T.self_sb[j];
+  const double* a0 = SCR + (i * ns + sa) * 3;
+  const double* a1 = cont ? SCR + ((i + 1) * ns + sa) * 3 : a0;
+  const double* b0 = SCR + (i * ns + sb) * 3;
+  const double* b1 = cont ? SCR + ((i + 1) * ns + sb) * 3 : b0;
+  double ca0[3], ca1[3], cb0[3], cb1[3];
+  for (int e = 0; e < 3; ++e)
+  {
+    ca0[e] = a0[e];
+    ca1[e] = a1[e];
+    cb0[e] = b0[e];
+    cb1[e] = b1[e];
+  }
+  double n[3], pa[3], pb[3], ta, tb;
+  self_sphere_distance(ca0, ca1, S.rad[sa], cb0, cb1, S.rad[sb], cont, dist, n, pa, pb, ta, tb);
+  if (cont)
+  {
+    cta = (i == 0 && ta == 0.0) ? 1 : ((i + 1 == last && ta == 1.0) ? 2 : 3);
+    ctb = (i == 0 && tb == 0.0) ? 1 : ((i + 1 == last && tb == 1.0) ? 2 : 3);
+  }
+  else
+    cta = ctb = (i == 0) ? 1 : ((i == last) ? 2 : 3);
 }
 
 template <int PASS>
@@ -796,6 +841,30 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
           }
         }
       }
+      // self-collision candidates (key order; their hit bits follow the scene's)
+      const int nself = c.T.n_self_sph * nseg, scene_total = nsi * P;
+      for (int q = c.lane; q < nself + 63; q += 64)
+      {
+        if (__builtin_amdgcn_readfirstlane(q - c.lane) >= nself)
+          break;
+        bool hit = false;
+        double dist = 0.0;
+        if (q < nself)
+        {
+          int i, sa, sb, cta, ctb;
+          self_candidate(c, S, SCR, ns, nseg, last, cont, q, i, sa, sb, dist, cta, ctb);
+          hit = dist < threshold && !(dist > margin + buffer);
+          if (hit && (f0 || f1))
+            hit = (f0 && (cta != 1 || ctb != 1)) || (f1 && (cta != 2 || ctb != 2));
+        }
+        lcount += hit ? 1.0 : 0.0;
+        lcost += hit ? fmax(margin - dist, 0.0) * coeff : 0.0;
+        if (hit && HB)
+        {
+          const int cand = scene_total + q;
+          atomicOr(HB + (cand >> 5), 1u << (cand & 31));
+        }
+      }
       const double cost = wave_sum(lcost);
       const int found = static_cast<int>(wave_sum(lcount));
       if (c.lane == 0)
@@ -808,9 +877,10 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       __builtin_amdgcn_wave_barrier();
       continue;
     }
-    int total = 0;
+    int scene_total = 0;
     for (int g = 0; g < ngr; ++g)
-      total += P * nseg * S.grp_ns[g];
+      scene_total += P * nseg * S.grp_ns[g];
+    const int total = scene_total + c.T.n_self_sph * nseg;
     int running = 0;
     double lcost = 0.0;  // per-lane partial cost, reduced once per pair
     const int base = (PASS == 1) ? coll_unit_row0(L, PCNT, out_base, t) : 0;
@@ -821,7 +891,25 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       bool hit = false;
       double dist = 0.0;
       int i = 0, s = 0, p = 0;
-      if (use_bits)
+      if (cand >= scene_total)
+      {
+        // a self-collision candidate: (sub-state, sphere a, -1 - sphere b)
+        if (cand < total)
+        {
+          int cta, ctb;
+          self_candidate(c, S, SCR, ns, nseg, last, cont, cand - scene_total, i, s, p, dist, cta, ctb);
+          p = -1 - p;
+          if (use_bits)
+            hit = (HB[cand >> 5] >> (cand & 31)) & 1u;
+          else
+          {
+            hit = dist < threshold && !(dist > margin + buffer);
+            if (hit && (f0 || f1))
+              hit = (f0 && (cta != 1 || ctb != 1)) || (f1 && (cta != 2 || ctb != 2));
+          }
+        }
+      }
+      else if (use_bits)
       {
         // the count pass's hits: 64 candidates = two words (each unit's bits
         // start on a 64-bit boundary)
@@ -1202,89 +1290,112 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
     const double* q1 = x + (t + 1) * D;
     const bool single = L.coll_single != 0;  // i = the half (waypoint t + i)
     const int cnt = single ? 1 : lvs_count(q0, q1, D, c.d->coll_lvs);
-    const int link = c.d->sphere_link[s];
     const bool cont = c.d->coll_continuous == 1;
-    double q[THIP_MAX_DOF];
+    const bool self = p < 0;  // a self contact: the second body is robot sphere -1 - p
+    const int nsides = self ? 2 : 1;
+    const int sb = self ? -1 - p : 0;
+    double q[THIP_MAX_DOF], qn[THIP_MAX_DOF];
     for (int j = 0; j < D; ++j)
+    {
       q[j] = single ? (i ? q1[j] : q0[j]) : linspaced(cnt, q0[j], q1[j], i);
-    Pose T, T1;  // link pose at sub-state i (transform) and, for a cast, at i + 1 (cc_transform)
-    chain_fk(ch, q, link, T);
-    const double* cs = c.d->sphere_center[s];
-    double ctr[3];
-    for (int r = 0; r < 3; ++r)
-      ctr[r] = T.r[r * 3 + 0] * cs[0] + T.r[r * 3 + 1] * cs[1] + T.r[r * 3 + 2] * cs[2] + T.t[r];
-    double dist, n[3], pr[3], ts = 0.0;
-    if (cont)
+      qn[j] = cont ? linspaced(cnt, q0[j], q1[j], i + 1) : q[j];
+    }
+    // side 0: the robot sphere s; side 1: the scene primitive p, or robot sphere sb.
+    // Link poses at sub-state i (transform) and, for a cast, at i + 1 (cc_transform).
+    int link[2];
+    Pose T[2], T1[2];
+    double c0[2][3], c1[2][3];
+    for (int sd = 0; sd < nsides; ++sd)
     {
-      double qn[THIP_MAX_DOF];
-      for (int j = 0; j < D; ++j)
-        qn[j] = linspaced(cnt, q0[j], q1[j], i + 1);
-      chain_fk(ch, qn, link, T1);
-      double ctr1[3];
+      const int sph = sd ? sb : s;
+      link[sd] = c.d->sphere_link[sph];
+      chain_fk(ch, q, link[sd], T[sd]);
+      if (cont)
+        chain_fk(ch, qn, link[sd], T1[sd]);
+      else
+        T1[sd] = T[sd];
+      const double* cs = c.d->sphere_center[sph];
       for (int r = 0; r < 3; ++r)
-        ctr1[r] = T1.r[r * 3 + 0] * cs[0] + T1.r[r * 3 + 1] * cs[1] + T1.r[r * 3 + 2] * cs[2] + T1.t[r];
-      swept_sphere_prim_distance(ctr, ctr1, c.d->sphere_radius[s], c.scene + 16 * p, dist, n, pr, ts);
+      {
+        c0[sd][r] = T[sd].r[r * 3 + 0] * cs[0] + T[sd].r[r * 3 + 1] * cs[1] + T[sd].r[r * 3 + 2] * cs[2] + T[sd].t[r];
+        c1[sd][r] =
+            T1[sd].r[r * 3 + 0] * cs[0] + T1[sd].r[r * 3 + 1] * cs[1] + T1[sd].r[r * 3 + 2] * cs[2] + T1[sd].t[r];
+      }
     }
+    double dist, n[3], pt[2][3], ts[2] = { 0.0, 0.0 };
+    if (self)
+      self_sphere_distance(c0[0], c1[0], c.d->sphere_radius[s], c0[1], c1[1], c.d->sphere_radius[sb], cont, dist, n,
+                           pt[0], pt[1], ts[0], ts[1]);
+    else if (cont)
+      swept_sphere_prim_distance(c0[0], c1[0], c.d->sphere_radius[s], c.scene + 16 * p, dist, n, pt[0], ts[0]);
     else
+      sphere_prim_distance(c0[0], c.d->sphere_radius[s], c.scene + 16 * p, dist, n, pt[0]);
+    // per side: nearest_points_local in the frame of the sub-state (cast start) pose and
+    // the reference-point offsets link_transform.linear() * nearest_points_local with
+    // link_transform = transform (x_t part) / cc_transform (x_t+1 part), collision_terms.cpp:217-223;
+    // cc_time: DISCRETE files the waypoint's expression on half i with scale 1 (CCType_None,
+    // GetGradient's scale 1, collision_terms.cpp:214-221), the other half absent
+    double rv0[2][3], rv1[2][3], cct[2];
+    for (int sd = 0; sd < nsides; ++sd)
     {
-      sphere_prim_distance(ctr, c.d->sphere_radius[s], c.scene + 16 * p, dist, n, pr);
-      T1 = T;
+      const double w[3] = { pt[sd][0] - T[sd].t[0], pt[sd][1] - T[sd].t[1], pt[sd][2] - T[sd].t[2] };
+      double pl[3];
+      for (int r = 0; r < 3; ++r)
+        pl[r] = T[sd].r[0 * 3 + r] * w[0] + T[sd].r[1 * 3 + r] * w[1] + T[sd].r[2 * 3 + r] * w[2];
+      for (int r = 0; r < 3; ++r)
+      {
+        rv0[sd][r] = T[sd].r[r * 3 + 0] * pl[0] + T[sd].r[r * 3 + 1] * pl[1] + T[sd].r[r * 3 + 2] * pl[2];
+        rv1[sd][r] = T1[sd].r[r * 3 + 0] * pl[0] + T1[sd].r[r * 3 + 1] * pl[1] + T1[sd].r[r * 3 + 2] * pl[2];
+      }
+      cct[sd] = single ? double(i) : (cont ? (double(i) + ts[sd]) : double(i)) * (1.0 / double(cnt - 1));
     }
-    // nearest_points_local[0] in the frame of the sub-state (cast start) pose and the
-    // reference-point offsets link_transform.linear() * nearest_points_local with
-    // link_transform = transform (x_t part) / cc_transform (x_t+1 part), collision_terms.cpp:217-223
-    const double w[3] = { pr[0] - T.t[0], pr[1] - T.t[1], pr[2] - T.t[2] };
-    double pl[3], rv0[3], rv1[3];
-    for (int r = 0; r < 3; ++r)
-      pl[r] = T.r[0 * 3 + r] * w[0] + T.r[1 * 3 + r] * w[1] + T.r[2 * 3 + r] * w[2];
-    for (int r = 0; r < 3; ++r)
-    {
-      rv0[r] = T.r[r * 3 + 0] * pl[0] + T.r[r * 3 + 1] * pl[1] + T.r[r * 3 + 2] * pl[2];
-      rv1[r] = T1.r[r * 3 + 0] * pl[0] + T1.r[r * 3 + 1] * pl[1] + T1.r[r * 3 + 2] * pl[2];
-    }
-    // DISCRETE: CCType_None, GetGradient's scale 1 (collision_terms.cpp:214-221): the
-    // waypoint's half with scale 1 - 0 (half 0) or 1 (half 1), the other half absent
-    const double cc_time =
-        single ? double(i) : (cont ? (double(i) + ts) : double(i)) * (1.0 / double(cnt - 1));
     const bool f0 = single ? (i == 1) : coll_fixed_step(c, t), f1 = single ? (i == 0) : coll_fixed_step(c, t + 1);
     double cst = dist;
     int mask = 0;
     double* a = HC0 + k * 2 * D;
+    for (int e = 0; e < 2 * D; ++e)
+      a[e] = 0.0;
     for (int e = 0; e < 2; ++e)
     {
-      const bool skip = (e == 0) ? f0 : f1;
-      const double* qe = (e == 0) ? q0 : q1;
-      if (skip)
-      {
-        for (int j = 0; j < D; ++j)
-          a[e * D + j] = 0.0;
+      if ((e == 0) ? f0 : f1)
         continue;
-      }
-      const double scale = (e == 1) ? cc_time : (1 - cc_time);
-      const double* rv = (e == 1) ? rv1 : rv0;
-      double J[6 * THIP_MAX_DOF];
-      chain_jacobian(ch, qe, link, J);
-      double gd = 0;
-      for (int j = 0; j < D; ++j)
+      const double* qe = (e == 0) ? q0 : q1;
+      // CollisionsToDistanceExpressions: per side varDot(scale g, vars) and scale * -g.q;
+      // a variable's side terms summed as the QP builder sums duplicates
+      double part = 0.0;
+      for (int sd = 0; sd < nsides; ++sd)
       {
-        const double wx = J[3 * D + j], wy = J[4 * D + j], wz = J[5 * D + j];
-        const double l0 = J[0 * D + j] + (wy * rv[2] - wz * rv[1]);
-        const double l1 = J[1 * D + j] + (wz * rv[0] - wx * rv[2]);
-        const double l2 = J[2 * D + j] + (wx * rv[1] - wy * rv[0]);
-        const double g = -1.0 * (n[0] * l0 + n[1] * l1 + n[2] * l2);
-        const double av = scale * g;
-        gd += g * qe[j];
-        // cleanupAff (expr_ops.cpp:88-99)
-        const bool keep = fabs(av) > 1e-7;
-        a[e * D + j] = keep ? av : 0.0;
-        mask |= keep ? (1 << (e * D + j)) : 0;
+        const double scale = (e == 1) ? cct[sd] : (1 - cct[sd]);
+        const double* rv = (e == 1) ? rv1[sd] : rv0[sd];
+        const double sg = sd ? 1.0 : -1.0;  // GetGradient: (i == 0 ? -1 : 1) n^T J (collision_terms.cpp:232)
+        double J[6 * THIP_MAX_DOF];
+        chain_jacobian(ch, qe, link[sd], J);
+        double gd = 0;
+        for (int j = 0; j < D; ++j)
+        {
+          const double wx = J[3 * D + j], wy = J[4 * D + j], wz = J[5 * D + j];
+          const double l0 = J[0 * D + j] + (wy * rv[2] - wz * rv[1]);
+          const double l1 = J[1 * D + j] + (wz * rv[0] - wx * rv[2]);
+          const double l2 = J[2 * D + j] + (wx * rv[1] - wy * rv[0]);
+          const double g = sg * (n[0] * l0 + n[1] * l1 + n[2] * l2);
+          const double av = scale * g;
+          gd += g * qe[j];
+          // cleanupAff (expr_ops.cpp:88-99)
+          if (fabs(av) > 1e-7)
+          {
+            const int bit = 1 << (e * D + j);
+            a[e * D + j] = (mask & bit) ? a[e * D + j] + av : av;
+            mask |= bit;
+          }
+        }
+        part += scale * -gd;
       }
-      cst += scale * -gd;
+      cst += part;
     }
     HK[k] = cst;
     HM[k] = mask;
     c.a(A_HDIST)[k] = dist;
-    c.a(A_HCCT)[k] = single ? 0.0 : cc_time;
+    c.a(A_HCCT)[k] = single ? 0.0 : cct[0];
   }
   BSYNC();
 }

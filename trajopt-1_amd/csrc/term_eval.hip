@@ -34,6 +34,7 @@
 
 #include "collision_device.hpp"
 #include "kin_device.hpp"
+#include "self_pairs.hpp"
 
 namespace thip
 {
@@ -68,6 +69,11 @@ struct Spheres
   double center[THIP_MAX_SPHERES][3];
   double radius[THIP_MAX_SPHERES];
   int link[THIP_MAX_SPHERES];
+  // self-collision sphere pairs in key order (self_pairs.hpp)
+  int n_self_keys, n_self_sph;
+  int self_sa[THIP_MAX_SELF_SPHERE_PAIRS];
+  int self_sb[THIP_MAX_SELF_SPHERE_PAIRS];
+  int self_kp[THIP_MAX_SELF_PAIRS + 1];
 };
 
 __shared__ thip_chain s_chain;
@@ -180,10 +186,11 @@ __device__ __forceinline__ void sphere_world(const Pose& T, const double* cl, do
     c[r] = T.r[r * 3 + 0] * cl[0] + T.r[r * 3 + 1] * cl[1] + T.r[r * 3 + 2] * cl[2] + T.t[r];
 }
 
-// CollisionEvaluator::GetGradient for the robot link at the waypoint's own
-// joint values (oracle/src/collision.cpp contactGradient)
+// CollisionEvaluator::GetGradient for one robot link at the waypoint's own
+// joint values (oracle/src/collision.cpp contactGradient): sg = -1 for
+// link_ids[0], +1 for the second link of a self contact
 __device__ void contact_gradient(const thip_chain& ch, const double* dof, int link, const Pose& lt,
-                                 const double* p_local, const double* normal, double* grad)
+                                 const double* p_local, const double* normal, double sg, double* grad)
 {
   const int D = ch.n_dof;
   double J[6 * THIP_MAX_DOF];
@@ -197,7 +204,7 @@ __device__ void contact_gradient(const thip_chain& ch, const double* dof, int li
     const double l0 = J[0 * D + j] + (wy * r[2] - wz * r[1]);
     const double l1 = J[1 * D + j] + (wz * r[0] - wx * r[2]);
     const double l2 = J[2 * D + j] + (wx * r[1] - wy * r[0]);
-    grad[j] = -1.0 * (normal[0] * l0 + normal[1] * l1 + normal[2] * l2);
+    grad[j] = sg * (normal[0] * l0 + normal[1] * l1 + normal[2] * l2);
   }
 }
 
@@ -231,7 +238,8 @@ __global__ __launch_bounds__(kEvBlock) void coll_eval_kernel(const thip_chain* c
       n += S.grp_ns[g];
     return n;
   }();
-  const long long total = static_cast<long long>(n_sph) * n_prims * n_sub;
+  const long long scene_total = static_cast<long long>(n_sph) * n_prims * n_sub;
+  const long long total = scene_total + static_cast<long long>(S.n_self_sph) * n_sub;
   __shared__ int s_wave_cnt[kEvWaves];
   __shared__ int s_base;
   if (tid == 0)
@@ -242,60 +250,120 @@ __global__ __launch_bounds__(kEvBlock) void coll_eval_kernel(const thip_chain* c
   {
     const long long cidx = c0 + tid;
     bool hit = false;
-    int link = 0, p = 0, s = 0, i = 0, cc_type = kCCNone;
-    double dist = 0, normal[3] = { 0, 0, 0 }, p_robot[3] = { 0, 0, 0 }, cc_time = 0;
-    Pose Ta, Tb;
+    // side 0: the robot sphere s; side 1: primitive p, or (self) robot sphere sb
+    int link[2] = { 0, 0 }, p = 0, s = 0, sb = -1, i = 0, cc_type[2] = { kCCNone, kCCNone };
+    double dist = 0, normal[3] = { 0, 0, 0 }, pt[2][3] = { { 0, 0, 0 }, { 0, 0, 0 } }, cc_time[2] = { 0, 0 };
+    Pose Ta[2], Tb[2];
     if (cidx < total)
     {
-      // decode (group, primitive, sub-state, sphere of the group) in map order
-      long long r = cidx;
-      int g = 0;
-      for (; g < S.n_groups; ++g)
-      {
-        const long long sz = static_cast<long long>(S.grp_ns[g]) * n_prims * n_sub;
-        if (r < sz)
-          break;
-        r -= sz;
-      }
-      const int ng = S.grp_ns[g];
-      p = static_cast<int>(r / (static_cast<long long>(n_sub) * ng));
-      const int r2 = static_cast<int>(r % (static_cast<long long>(n_sub) * ng));
-      i = r2 / ng;
-      s = S.sph_order[S.grp_s0[g] + r2 % ng];
-      link = S.grp_link[g];
-      double qa[THIP_MAX_DOF];
-      for (int j = 0; j < D; ++j)
-        qa[j] = tm.single ? q0[j] : linspaced(cnt, q0[j], q1[j], i);
-      chain_fk(ch, qa, link, Ta);
-      double ca[3];
-      sphere_world(Ta, S.center[s], ca);
-      const double* prim = prims + 16 * p;
-      if (tm.continuous)
-      {
-        double qb[THIP_MAX_DOF];
+      double qa[THIP_MAX_DOF], qb[THIP_MAX_DOF];
+      auto states = [&]() {
         for (int j = 0; j < D; ++j)
-          qb[j] = linspaced(cnt, q0[j], q1[j], i + 1);
-        chain_fk(ch, qb, link, Tb);
-        double cb[3], ts = 0;
-        sphere_world(Tb, S.center[s], cb);
-        swept_sphere_prim_distance(ca, cb, S.radius[s], prim, dist, normal, p_robot, ts);
-        cc_time = (double(i) + ts) * dt;
-        cc_type = (i == 0 && ts == 0.0) ? kCCTime0 : ((i + 1 == last && ts == 1.0) ? kCCTime1 : kCCBetween);
+        {
+          qa[j] = tm.single ? q0[j] : linspaced(cnt, q0[j], q1[j], i);
+          qb[j] = tm.continuous ? linspaced(cnt, q0[j], q1[j], i + 1) : qa[j];
+        }
+      };
+      if (cidx < scene_total)
+      {
+        // decode (group, primitive, sub-state, sphere of the group) in map order
+        long long r = cidx;
+        int g = 0;
+        for (; g < S.n_groups; ++g)
+        {
+          const long long sz = static_cast<long long>(S.grp_ns[g]) * n_prims * n_sub;
+          if (r < sz)
+            break;
+          r -= sz;
+        }
+        const int ng = S.grp_ns[g];
+        p = static_cast<int>(r / (static_cast<long long>(n_sub) * ng));
+        const int r2 = static_cast<int>(r % (static_cast<long long>(n_sub) * ng));
+        i = r2 / ng;
+        s = S.sph_order[S.grp_s0[g] + r2 % ng];
+        link[0] = S.grp_link[g];
+        states();
+        chain_fk(ch, qa, link[0], Ta[0]);
+        double ca[3];
+        sphere_world(Ta[0], S.center[s], ca);
+        const double* prim = prims + 16 * p;
+        if (tm.continuous)
+        {
+          chain_fk(ch, qb, link[0], Tb[0]);
+          double cb[3], ts = 0;
+          sphere_world(Tb[0], S.center[s], cb);
+          swept_sphere_prim_distance(ca, cb, S.radius[s], prim, dist, normal, pt[0], ts);
+          cc_time[0] = (double(i) + ts) * dt;
+          cc_type[0] = (i == 0 && ts == 0.0) ? kCCTime0 : ((i + 1 == last && ts == 1.0) ? kCCTime1 : kCCBetween);
+        }
+        else
+        {
+          Tb[0] = Ta[0];
+          sphere_prim_distance(ca, S.radius[s], prim, dist, normal, pt[0]);
+          if (!tm.single)
+          {
+            cc_time[0] = double(i) * dt;
+            cc_type[0] = (i == 0) ? kCCTime0 : ((i == last) ? kCCTime1 : kCCBetween);
+          }
+        }
       }
       else
       {
-        Tb = Ta;
-        sphere_prim_distance(ca, S.radius[s], prim, dist, normal, p_robot);
-        if (!tm.single)
+        // a self-collision candidate: key (link pair), sub-state, sphere pair of the key
+        int r = static_cast<int>(cidx - scene_total), k = 0;
+        for (; k + 1 < S.n_self_keys; ++k)
         {
-          cc_time = double(i) * dt;
-          cc_type = (i == 0) ? kCCTime0 : ((i == last) ? kCCTime1 : kCCBetween);
+          const int sz = n_sub * (S.self_kp[k + 1] - S.self_kp[k]);
+          if (r < sz)
+            break;
+          r -= sz;
+        }
+        const int k0 = S.self_kp[k], npk = S.self_kp[k + 1] - k0;
+        i = r / npk;
+        const int j = k0 + (r - i * npk);
+        s = S.self_sa[j];
+        sb = S.self_sb[j];
+        p = -1 - sb;
+        link[0] = S.link[s];
+        link[1] = S.link[sb];
+        states();
+        double a0[3], a1[3], b0[3], b1[3];
+        for (int sd = 0; sd < 2; ++sd)
+        {
+          chain_fk(ch, qa, link[sd], Ta[sd]);
+          if (tm.continuous)
+            chain_fk(ch, qb, link[sd], Tb[sd]);
+          else
+            Tb[sd] = Ta[sd];
+        }
+        sphere_world(Ta[0], S.center[s], a0);
+        sphere_world(Tb[0], S.center[s], a1);
+        sphere_world(Ta[1], S.center[sb], b0);
+        sphere_world(Tb[1], S.center[sb], b1);
+        double t0, t1;
+        self_sphere_distance(a0, a1, S.radius[s], b0, b1, S.radius[sb], tm.continuous != 0, dist, normal, pt[0], pt[1],
+                             t0, t1);
+        if (tm.continuous)
+        {
+          cc_time[0] = (double(i) + t0) * dt;
+          cc_time[1] = (double(i) + t1) * dt;
+          cc_type[0] = (i == 0 && t0 == 0.0) ? kCCTime0 : ((i + 1 == last && t0 == 1.0) ? kCCTime1 : kCCBetween);
+          cc_type[1] = (i == 0 && t1 == 0.0) ? kCCTime0 : ((i + 1 == last && t1 == 1.0) ? kCCTime1 : kCCBetween);
+        }
+        else if (!tm.single)
+        {
+          cc_time[0] = cc_time[1] = double(i) * dt;
+          cc_type[0] = cc_type[1] = (i == 0) ? kCCTime0 : ((i == last) ? kCCTime1 : kCCBetween);
         }
       }
       hit = (dist < threshold) && !(dist > tm.margin + tm.buffer);
+      // removeInvalidContactResults: at a fixed end keep a contact when one of its active
+      // sides is not at that end (a scene primitive's side is CCType_None)
       if (hit && (un.f0 || un.f1))
-        hit = (un.f0 && cc_type != kCCNone && cc_type != kCCTime0) ||
-              (un.f1 && cc_type != kCCNone && cc_type != kCCTime1);
+        hit = (un.f0 && ((cc_type[0] != kCCNone && cc_type[0] != kCCTime0) ||
+                         (cc_type[1] != kCCNone && cc_type[1] != kCCTime0))) ||
+              (un.f1 && ((cc_type[0] != kCCNone && cc_type[0] != kCCTime1) ||
+                         (cc_type[1] != kCCNone && cc_type[1] != kCCTime1)));
     }
     const unsigned long long m = __ballot(hit);
     const int lrank = __popcll(m & ((1ull << lane) - 1ull));
@@ -307,79 +375,69 @@ __global__ __launch_bounds__(kEvBlock) void coll_eval_kernel(const thip_chain* c
       rank += s_wave_cnt[w];
     if (hit && rank < ucap)
     {
-      // nearest_points_local[0]: the robot point in the link frame of transform
-      double pl[3];
-      const double w3[3] = { p_robot[0] - Ta.t[0], p_robot[1] - Ta.t[1], p_robot[2] - Ta.t[2] };
-      for (int k = 0; k < 3; ++k)
-        pl[k] = Ta.r[0 * 3 + k] * w3[0] + Ta.r[1 * 3 + k] * w3[1] + Ta.r[2 * 3 + k] * w3[2];
+      const int nsides = (sb >= 0) ? 2 : 1;
+      // nearest_points_local: each side's point in its link frame of transform
+      double pl[2][3];
+      for (int sd = 0; sd < nsides; ++sd)
+      {
+        const double w3[3] = { pt[sd][0] - Ta[sd].t[0], pt[sd][1] - Ta[sd].t[1], pt[sd][2] - Ta[sd].t[2] };
+        for (int k = 0; k < 3; ++k)
+          pl[sd][k] = Ta[sd].r[0 * 3 + k] * w3[0] + Ta[sd].r[1 * 3 + k] * w3[1] + Ta[sd].r[2 * 3 + k] * w3[2];
+      }
       double* rec = out + static_cast<long long>(rank) * W;
       double a0[THIP_MAX_DOF], a1[THIP_MAX_DOF];
+      for (int j = 0; j < D; ++j)
+        a0[j] = a1[j] = 0.0;
+      int mask = 0;
+      // one timestep's part: per side scale * g (cleanupAff'd, a variable's side terms
+      // summed) and scale * -g.q summed from 0 (oracle contactExpression)
+      auto part = [&](const double* qe, bool ts1, double* a, int bit0) {
+        double cpart = 0.0;
+        for (int sd = 0; sd < nsides; ++sd)
+        {
+          const bool none = cc_type[sd] == kCCNone;
+          const double sc = none ? 1.0 : (ts1 ? cc_time[sd] : 1 - cc_time[sd]);
+          const Pose& lt = (ts1 && !none) ? Tb[sd] : Ta[sd];
+          double g[THIP_MAX_DOF], gd = 0;
+          contact_gradient(ch, qe, link[sd], lt, pl[sd], normal, sd ? 1.0 : -1.0, g);
+          for (int j = 0; j < D; ++j)
+          {
+            const double av = sc * g[j];
+            gd += g[j] * qe[j];
+            if (fabs(av) > 1e-7)
+            {
+              const int bit = 1 << (bit0 + j);
+              a[j] = (mask & bit) ? a[j] + av : av;
+              mask |= bit;
+            }
+          }
+          cpart += sc * -gd;
+        }
+        return cpart;
+      };
       double cst;
       if (tm.single)
       {
-        // CalcDistExpressionsSingleTimeStep: 0 + g.x - g.q, then + d (scale 1, CCType_None)
-        double g[THIP_MAX_DOF], gd = 0;
-        contact_gradient(ch, q0, link, Ta, pl, normal, g);
-        for (int j = 0; j < D; ++j)
-        {
-          a0[j] = 1.0 * g[j];
-          gd += g[j] * q0[j];
-          a1[j] = 0.0;
-        }
-        cst = 0.0;
-        cst += 1.0 * -gd;
+        // CalcDistExpressionsSingleTimeStep: 0 + part(x_t), then + d (scale 1, CCType_None)
+        cst = 0.0 + part(q0, false, a0, 0);
         cst += dist;
       }
       else
       {
         cst = dist;
-        for (int j = 0; j < D; ++j)
-          a0[j] = a1[j] = 0.0;
         if (!un.f0)
-        {
-          double g[THIP_MAX_DOF], gd = 0;
-          contact_gradient(ch, q0, link, Ta, pl, normal, g);
-          const double sc = 1 - cc_time;
-          for (int j = 0; j < D; ++j)
-          {
-            a0[j] = sc * g[j];
-            gd += g[j] * q0[j];
-          }
-          cst += sc * -gd;
-        }
+          cst += part(q0, false, a0, 0);
         if (!un.f1)
-        {
-          double g[THIP_MAX_DOF], gd = 0;
-          contact_gradient(ch, q1, link, Tb, pl, normal, g);
-          const double sc = cc_time;
-          for (int j = 0; j < D; ++j)
-          {
-            a1[j] = sc * g[j];
-            gd += g[j] * q1[j];
-          }
-          cst += sc * -gd;
-        }
-      }
-      int kept = 0;
-      for (int j = 0; j < D; ++j)
-      {
-        if (fabs(a0[j]) > 1e-7)
-          ++kept;
-        else
-          a0[j] = 0;
-        if (fabs(a1[j]) > 1e-7)
-          ++kept;
-        else
-          a1[j] = 0;
+          cst += part(q1, true, a1, D);
       }
       rec[0] = un.t0;
-      rec[1] = link;
+      rec[1] = link[0];
       rec[2] = p;
       rec[3] = s;
       rec[4] = tm.single ? 0 : i;
       rec[5] = dist;
-      rec[6] = cc_time;
-      rec[7] = kept;
+      rec[6] = cc_time[0];
+      rec[7] = __popc(mask);
       for (int j = 0; j < D; ++j)
       {
         rec[8 + j] = a0[j];
@@ -605,6 +663,22 @@ int thip_eval_create(int device, const thip_problem_desc* desc, int batch, thip_
       }
       sp.grp_ns[sp.n_groups - 1]++;
     }
+    std::vector<int> ssa, ssb, skp;
+    const std::string why = thip::self_sphere_pairs(d, ssa, ssb, skp);
+    if (!why.empty())
+    {
+      delete ev;
+      return reject(why);
+    }
+    sp.n_self_keys = static_cast<int>(skp.size()) - 1;
+    sp.n_self_sph = static_cast<int>(ssa.size());
+    for (size_t k = 0; k < ssa.size(); ++k)
+    {
+      sp.self_sa[k] = ssa[k];
+      sp.self_sb[k] = ssb[k];
+    }
+    for (size_t k = 0; k < skp.size(); ++k)
+      sp.self_kp[k] = skp[k];
     for (int s = 0; s < d.n_spheres; ++s)
     {
       sp.link[s] = d.sphere_link[s];

@@ -16,6 +16,7 @@
 #include <functional>
 
 #include "layout.hpp"
+#include "self_pairs.hpp"
 
 namespace thip
 {
@@ -259,6 +260,13 @@ static int validate(const thip_problem_desc* d, std::string& why)
                  THIP_E_INVALID;
   if (d->coll_enabled && (d->coll_max_contacts < 0 || d->coll_max_contacts > THIP_MAX_CONTACTS))
     return why = "collision: coll_max_contacts out of range", THIP_E_INVALID;
+  if (d->coll_enabled)
+  {
+    std::vector<int> sa, sb, kp;
+    const std::string w = self_sphere_pairs(*d, sa, sb, kp);
+    if (!w.empty())
+      return why = w, THIP_E_INVALID;
+  }
   if (!(d->sqp.max_time >= 0))
     return why = "sqp.max_time must be >= 0 (DBL_MAX: no limit)", THIP_E_INVALID;
   if (!(d->sqp.trust_shrink_ratio > 0 && d->sqp.trust_shrink_ratio < 1) || !(d->sqp.min_trust_box_size > 0) ||
@@ -507,9 +515,13 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     (L.coll_cnt ? n_cnts : n_costs) += n_units;
   if (L.coll)
   {
-    // every (sphere, primitive, sub-state) candidate of every unit is at most one contact
-    const long long bound = static_cast<long long>(n_units) * (L.coll_single ? 1 : 64) * d.n_spheres *
-                            std::max(d.n_prims, 1);
+    // every (sphere, primitive, sub-state) and (self sphere pair, sub-state) candidate of
+    // every unit is at most one contact
+    std::vector<int> ssa, ssb, skp;
+    self_sphere_pairs(d, ssa, ssb, skp);
+    const long long bound = static_cast<long long>(n_units) * (L.coll_single ? 1 : 64) *
+                            (static_cast<long long>(d.n_spheres) * std::max(d.n_prims, 1) +
+                             static_cast<long long>(ssa.size()));
     // automatic: the bound, within THIP_MAX_CONTACTS and a 16 GB share of HBM for the
     // hinge-row arrays of the whole batch (~800 B per row and problem), at least 2048
     const long long by_mem = std::max<long long>(2048, (16LL << 30) / (800LL * batch));
@@ -566,8 +578,10 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   sizes[A_RE] = std::max(L.n_rows, 1);
   // branches of the block solve (Layout::nbr): the dofs split into groups no
   // term couples -- every CartPose term joins the dofs on the root paths of its
-  // source (and dynamic target) link, every collision sphere those of its link;
-  // joint-space terms touch single dofs.  Two contiguous groups of <= 8 dofs
+  // source (and dynamic target) link, every collision sphere those of its link,
+  // every self-collision link pair those of both links (config E's inter-arm
+  // pairs join the arms: it runs the 14-dof wide path); joint-space terms touch
+  // single dofs.  Two contiguous groups of <= 8 dofs
   // each (the dual arm) solve as two independent narrow block chains.
   L.nbr = 1;
   L.sD = L.D;
@@ -600,11 +614,20 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
         join_path(d.cart_target_link[c], first);
     }
     if (d.coll_enabled)
+    {
       for (int s2 = 0; s2 < d.n_spheres; ++s2)
       {
         int first = -1;
         join_path(d.sphere_link[s2], first);
       }
+      // a self-collision pair's contacts move both links: their paths join
+      for (int k = 0; k < d.n_self_pairs; ++k)
+      {
+        int first = -1;
+        join_path(d.self_pair[k][0], first);
+        join_path(d.self_pair[k][1], first);
+      }
+    }
     const int half = L.D / 2;
     bool split = (L.D % 2 == 0) && half <= 8 && root(0) != root(half);
     for (int k = 0; k < L.D && split; ++k)
@@ -828,9 +851,14 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
       if (d.coll_fixed_steps[k] >= 0 && d.coll_fixed_steps[k] < L.N)
         coll_fixed[static_cast<size_t>(d.coll_fixed_steps[k])] = 1;
   }
+  std::vector<int> self_sa, self_sb, self_kp(1, 0);
+  if (L.coll)
+    self_sphere_pairs(d, self_sa, self_sb, self_kp);
   const size_t o_gl = push(grp_link, grp_link.size()), o_g0 = push(grp_s0, grp_s0.size()),
                o_gn = push(grp_ns, grp_ns.size()), o_so = push(sph_order, sph_order.size()),
-               o_cf = push(coll_fixed, coll_fixed.size()), o_cs = push(coll_slot, coll_slot.size());
+               o_cf = push(coll_fixed, coll_fixed.size()), o_cs = push(coll_slot, coll_slot.size()),
+               o_ssa = push(self_sa, self_sa.size()), o_ssb = push(self_sb, self_sb.size()),
+               o_skp = push(self_kp, self_kp.size());
   row_w.resize(std::max<size_t>(na, 1));
   if ((e = hipMalloc(&ctx->d_tables, itab.size() * sizeof(int))) != hipSuccess ||
       (e = hipMalloc(&ctx->d_tables_f, row_w.size() * sizeof(double))) != hipSuccess ||
@@ -876,6 +904,11 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   T.sph_order = ctx->d_tables + o_so;
   T.coll_fixed = ctx->d_tables + o_cf;
   T.coll_slot = ctx->d_tables + o_cs;
+  T.n_self_keys = static_cast<int>(self_kp.size()) - 1;
+  T.n_self_sph = static_cast<int>(self_sa.size());
+  T.self_sa = ctx->d_tables + o_ssa;
+  T.self_sb = ctx->d_tables + o_ssb;
+  T.self_kp = ctx->d_tables + o_skp;
   T.row_w = ctx->d_tables_f;
   const size_t B = static_cast<size_t>(batch);
   if ((e = hipMalloc(&ctx->d_ws, B * static_cast<size_t>(L.dstride) * sizeof(double))) != hipSuccess ||

@@ -24,6 +24,7 @@
 #pragma once
 #include <array>
 #include <map>
+#include <set>
 #include <memory>
 #include <string>
 #include <vector>
@@ -96,6 +97,11 @@ public:
 
   std::vector<CollisionSphere> collision_spheres;      // robot collision model
   std::vector<std::array<double, 16>> scene;           // THIP_PRIM_* records
+  // the allowed-collision matrix (the SRDF's <disable_collisions> link pairs):
+  // robot link pairs the contact manager never tests
+  std::set<std::pair<std::string, std::string>> allowed_collisions;
+  void allowCollision(const std::string& a, const std::string& b);
+  bool isCollisionAllowed(const std::string& a, const std::string& b) const;
 
   // PR2 arms (groups "right_arm", "left_arm": torso_lift_link ->
   // *_gripper_tool_frame, and "both_arms", joint data of

@@ -136,7 +136,51 @@ Environment::Ptr Environment::makePR2()
   for (const char* side : { "l_", "r_" })
     for (int s = 0; s < 14; ++s)
       env->collision_spheres.push_back({ std::string(side) + links[s], { cx[s], 0.0, 0.0 }, rad[s] });
+  // pr2.srdf <disable_collisions> (trajopt_common/data/pr2.srdf:752-1036) between the
+  // sphere-carrying arm links; the pairs it leaves enabled are the self-collision pairs
+  // (each arm's shoulder_pan vs its wrist links, and most left-vs-right pairs)
+  static const char* const acm[][2] = {
+    { "l_elbow_flex_link", "l_forearm_roll_link" },      { "l_elbow_flex_link", "l_shoulder_lift_link" },
+    { "l_elbow_flex_link", "l_shoulder_pan_link" },      { "l_elbow_flex_link", "l_upper_arm_roll_link" },
+    { "l_elbow_flex_link", "l_wrist_flex_link" },        { "l_elbow_flex_link", "l_wrist_roll_link" },
+    { "l_elbow_flex_link", "r_shoulder_lift_link" },     { "l_elbow_flex_link", "r_shoulder_pan_link" },
+    { "l_elbow_flex_link", "r_upper_arm_roll_link" },    { "l_forearm_roll_link", "l_shoulder_lift_link" },
+    { "l_forearm_roll_link", "l_shoulder_pan_link" },    { "l_forearm_roll_link", "l_upper_arm_roll_link" },
+    { "l_forearm_roll_link", "l_wrist_flex_link" },      { "l_forearm_roll_link", "l_wrist_roll_link" },
+    { "l_forearm_roll_link", "r_shoulder_lift_link" },   { "l_forearm_roll_link", "r_shoulder_pan_link" },
+    { "l_forearm_roll_link", "r_upper_arm_roll_link" },  { "l_shoulder_lift_link", "l_shoulder_pan_link" },
+    { "l_shoulder_lift_link", "l_upper_arm_roll_link" }, { "l_shoulder_lift_link", "l_wrist_flex_link" },
+    { "l_shoulder_lift_link", "l_wrist_roll_link" },     { "l_shoulder_lift_link", "r_elbow_flex_link" },
+    { "l_shoulder_lift_link", "r_forearm_roll_link" },   { "l_shoulder_lift_link", "r_shoulder_lift_link" },
+    { "l_shoulder_lift_link", "r_upper_arm_roll_link" }, { "l_shoulder_pan_link", "l_upper_arm_roll_link" },
+    { "l_shoulder_pan_link", "r_elbow_flex_link" },      { "l_shoulder_pan_link", "r_forearm_roll_link" },
+    { "l_upper_arm_roll_link", "l_wrist_flex_link" },    { "l_upper_arm_roll_link", "l_wrist_roll_link" },
+    { "l_upper_arm_roll_link", "r_elbow_flex_link" },    { "l_upper_arm_roll_link", "r_forearm_roll_link" },
+    { "l_upper_arm_roll_link", "r_shoulder_lift_link" }, { "l_upper_arm_roll_link", "r_upper_arm_roll_link" },
+    { "l_wrist_flex_link", "l_wrist_roll_link" },        { "r_elbow_flex_link", "r_forearm_roll_link" },
+    { "r_elbow_flex_link", "r_shoulder_lift_link" },     { "r_elbow_flex_link", "r_shoulder_pan_link" },
+    { "r_elbow_flex_link", "r_upper_arm_roll_link" },    { "r_elbow_flex_link", "r_wrist_flex_link" },
+    { "r_elbow_flex_link", "r_wrist_roll_link" },        { "r_forearm_roll_link", "r_shoulder_lift_link" },
+    { "r_forearm_roll_link", "r_shoulder_pan_link" },    { "r_forearm_roll_link", "r_upper_arm_roll_link" },
+    { "r_forearm_roll_link", "r_wrist_flex_link" },      { "r_forearm_roll_link", "r_wrist_roll_link" },
+    { "r_shoulder_lift_link", "r_shoulder_pan_link" },   { "r_shoulder_lift_link", "r_upper_arm_roll_link" },
+    { "r_shoulder_lift_link", "r_wrist_flex_link" },     { "r_shoulder_lift_link", "r_wrist_roll_link" },
+    { "r_shoulder_pan_link", "r_upper_arm_roll_link" },  { "r_upper_arm_roll_link", "r_wrist_flex_link" },
+    { "r_upper_arm_roll_link", "r_wrist_roll_link" },    { "r_wrist_flex_link", "r_wrist_roll_link" },
+  };
+  for (const auto& pr : acm)
+    env->allowCollision(pr[0], pr[1]);
   return env;
+}
+
+void Environment::allowCollision(const std::string& a, const std::string& b)
+{
+  allowed_collisions.insert(a < b ? std::make_pair(a, b) : std::make_pair(b, a));
+}
+
+bool Environment::isCollisionAllowed(const std::string& a, const std::string& b) const
+{
+  return allowed_collisions.count(a < b ? std::make_pair(a, b) : std::make_pair(b, a)) != 0;
 }
 
 // trajopt_common/data/spherebot.urdf / spherebot.srdf: group "manipulator" =

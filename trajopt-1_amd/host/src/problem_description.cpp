@@ -1143,6 +1143,29 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
   d.n_prims = static_cast<int>(env->scene.size());
   for (const auto& p : env->scene)
     prob.scene.insert(prob.scene.end(), p.begin(), p.end());
+  // self-collision: every pair of the group's sphere links (ascending link index) the
+  // allowed-collision matrix does not disable -- the contact manager tests all its
+  // active links against each other (collision_terms.cpp:817-898 via contactTest)
+  std::vector<std::pair<int, std::string>> slinks;
+  for (const CollisionSphere* cs : spheres)
+  {
+    const int li = prob.GetKin()->linkIndex(cs->link);
+    if (std::find_if(slinks.begin(), slinks.end(), [&](const auto& e) { return e.first == li; }) == slinks.end())
+      slinks.push_back({ li, cs->link });
+  }
+  std::sort(slinks.begin(), slinks.end());
+  d.n_self_pairs = 0;
+  for (std::size_t a = 0; a < slinks.size(); ++a)
+    for (std::size_t b = a + 1; b < slinks.size(); ++b)
+    {
+      if (env->isCollisionAllowed(slinks[a].second, slinks[b].second))
+        continue;
+      if (d.n_self_pairs >= THIP_MAX_SELF_PAIRS)
+        unsupported("more than " + std::to_string(THIP_MAX_SELF_PAIRS) + " self-collision link pairs");
+      d.self_pair[d.n_self_pairs][0] = slinks[a].first;
+      d.self_pair[d.n_self_pairs][1] = slinks[b].first;
+      ++d.n_self_pairs;
+    }
 }
 
 // ------------------------------------------------------------ ConstructProblem

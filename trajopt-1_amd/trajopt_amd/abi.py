@@ -10,7 +10,7 @@ import ctypes as C
 import os
 from pathlib import Path
 
-ABI_VERSION = 6  # THIP_ABI_VERSION
+ABI_VERSION = 7  # THIP_ABI_VERSION
 MAX_DOF = 16
 MAX_LINKS = 32
 MAX_STEPS = 64
@@ -23,6 +23,8 @@ MAX_JDT = 8
 MAX_JVT = 4
 MAX_TTT = 2
 MAX_COLL_EXTRA = 3
+MAX_SELF_PAIRS = 64
+MAX_SELF_SPHERE_PAIRS = 512
 TRACE_W = 16  # THIP_TRACE_W
 DEBUG_NO_SEGMENT, DEBUG_FORCE_WIDE, DEBUG_NO_BRANCH, DEBUG_STATIC_DISPATCH = 1, 2, 4, 8  # thip_debug_set_path flags
 
@@ -200,6 +202,8 @@ class ProblemDesc(C.Structure):
         ("sphere_center", _D3 * MAX_SPHERES),
         ("sphere_radius", C.c_double * MAX_SPHERES),
         ("n_prims", C.c_int),
+        ("n_self_pairs", C.c_int),
+        ("self_pair", (C.c_int * 2) * MAX_SELF_PAIRS),
         ("coll_max_contacts", C.c_int),
         ("n_coll_extra", C.c_int),
         ("coll_extra", CollTerm * MAX_COLL_EXTRA),

@@ -12,7 +12,8 @@ placement is redrawn (at most 64 times, same splitmix64 stream) until every
 robot sphere at every waypoint of q_ref is farther than the contact distance
 (dist_pen + buffer = 0.075 m) from it: the reference path is collision free,
 contacts come from the interpolated initial trajectory deviating toward the
-obstacles, and only part of the problems start in collision.  The collision term is the reference's LVS_DISCRETE cost with
+obstacles, and only part of the problems start in collision.  Robot self-collision: the arm link pairs pr2.srdf's allowed-collision
+matrix leaves enabled (arm_self_pairs).  The collision term is the reference's LVS_DISCRETE cost with
 dist_pen 0.025, coeffs 20, safety_margin_buffer 0.05, lvs 0.05 and
 fixed_steps [0] (CollisionTermInfo, problem_description.cpp:1636-1733).
 Primitive record layout: include/trajopt_hip.h (THIP_PRIM_*).
@@ -49,6 +50,52 @@ PR2_ARM_SPHERES = [
 N_PRIMS = 10
 MARGIN, COEFF, BUFFER, LVS = 0.025, 20.0, 0.05, 0.05
 
+# names of the sphere-carrying links of PR2_ARM_SPHERES (without the l_ / r_ prefix)
+ARM_SPHERE_LINK_NAMES = {1: "shoulder_pan_link", 2: "shoulder_lift_link", 3: "upper_arm_roll_link",
+                         5: "elbow_flex_link", 6: "forearm_roll_link", 8: "wrist_flex_link", 9: "wrist_roll_link"}
+# pr2.srdf <disable_collisions> between those links (trajopt_common/data/pr2.srdf:752-1036): the
+# allowed-collision matrix.  The pairs it leaves enabled are tested as robot self-collision: each
+# arm's shoulder_pan vs its wrist links, and 33 of the 49 left-vs-right pairs.
+PR2_ARM_ACM = frozenset(frozenset(p) for p in [
+    ("l_elbow_flex_link", "l_forearm_roll_link"), ("l_elbow_flex_link", "l_shoulder_lift_link"),
+    ("l_elbow_flex_link", "l_shoulder_pan_link"), ("l_elbow_flex_link", "l_upper_arm_roll_link"),
+    ("l_elbow_flex_link", "l_wrist_flex_link"), ("l_elbow_flex_link", "l_wrist_roll_link"),
+    ("l_elbow_flex_link", "r_shoulder_lift_link"), ("l_elbow_flex_link", "r_shoulder_pan_link"),
+    ("l_elbow_flex_link", "r_upper_arm_roll_link"), ("l_forearm_roll_link", "l_shoulder_lift_link"),
+    ("l_forearm_roll_link", "l_shoulder_pan_link"), ("l_forearm_roll_link", "l_upper_arm_roll_link"),
+    ("l_forearm_roll_link", "l_wrist_flex_link"), ("l_forearm_roll_link", "l_wrist_roll_link"),
+    ("l_forearm_roll_link", "r_shoulder_lift_link"), ("l_forearm_roll_link", "r_shoulder_pan_link"),
+    ("l_forearm_roll_link", "r_upper_arm_roll_link"), ("l_shoulder_lift_link", "l_shoulder_pan_link"),
+    ("l_shoulder_lift_link", "l_upper_arm_roll_link"), ("l_shoulder_lift_link", "l_wrist_flex_link"),
+    ("l_shoulder_lift_link", "l_wrist_roll_link"), ("l_shoulder_lift_link", "r_elbow_flex_link"),
+    ("l_shoulder_lift_link", "r_forearm_roll_link"), ("l_shoulder_lift_link", "r_shoulder_lift_link"),
+    ("l_shoulder_lift_link", "r_upper_arm_roll_link"), ("l_shoulder_pan_link", "l_upper_arm_roll_link"),
+    ("l_shoulder_pan_link", "r_elbow_flex_link"), ("l_shoulder_pan_link", "r_forearm_roll_link"),
+    ("l_upper_arm_roll_link", "l_wrist_flex_link"), ("l_upper_arm_roll_link", "l_wrist_roll_link"),
+    ("l_upper_arm_roll_link", "r_elbow_flex_link"), ("l_upper_arm_roll_link", "r_forearm_roll_link"),
+    ("l_upper_arm_roll_link", "r_shoulder_lift_link"), ("l_upper_arm_roll_link", "r_upper_arm_roll_link"),
+    ("l_wrist_flex_link", "l_wrist_roll_link"), ("r_elbow_flex_link", "r_forearm_roll_link"),
+    ("r_elbow_flex_link", "r_shoulder_lift_link"), ("r_elbow_flex_link", "r_shoulder_pan_link"),
+    ("r_elbow_flex_link", "r_upper_arm_roll_link"), ("r_elbow_flex_link", "r_wrist_flex_link"),
+    ("r_elbow_flex_link", "r_wrist_roll_link"), ("r_forearm_roll_link", "r_shoulder_lift_link"),
+    ("r_forearm_roll_link", "r_shoulder_pan_link"), ("r_forearm_roll_link", "r_upper_arm_roll_link"),
+    ("r_forearm_roll_link", "r_wrist_flex_link"), ("r_forearm_roll_link", "r_wrist_roll_link"),
+    ("r_shoulder_lift_link", "r_shoulder_pan_link"), ("r_shoulder_lift_link", "r_upper_arm_roll_link"),
+    ("r_shoulder_lift_link", "r_wrist_flex_link"), ("r_shoulder_lift_link", "r_wrist_roll_link"),
+    ("r_shoulder_pan_link", "r_upper_arm_roll_link"), ("r_upper_arm_roll_link", "r_wrist_flex_link"),
+    ("r_upper_arm_roll_link", "r_wrist_roll_link"), ("r_wrist_flex_link", "r_wrist_roll_link"),
+])
+
+
+def arm_self_pairs(link_offsets=(0,), sides=("r_",)):
+    """Self-collision link pairs of the arms (ascending link index, the lower first): every pair of
+    sphere-carrying links the ACM does not disable -- what the host front door derives from the
+    environment for the same group (problem_description.cpp CollisionTermInfo::hatch)."""
+    links = sorted((link + off, side + name) for off, side in zip(link_offsets, sides)
+                   for link, name in ARM_SPHERE_LINK_NAMES.items())
+    return [(la, lb) for a, (la, na) in enumerate(links) for lb, nb in links[a + 1:]
+            if frozenset((na, nb)) not in PR2_ARM_ACM]
+
 
 def arm_spheres(link_offsets=(0,)):
     """PR2_ARM_SPHERES once per arm, the arm's links shifted by its offset (both_arms: the left arm at
@@ -83,6 +130,12 @@ def add_collision_model(d: abi.ProblemDesc, link_offset: int = 0, link_offsets=N
             d.sphere_center[s][i] = c[i]
         d.sphere_radius[s] = r
     d.n_prims = N_PRIMS
+    # both_arms: left arm links first (l_), then the right arm (r_); one arm: the right arm
+    pairs = (arm_self_pairs(link_offsets, ("l_", "r_")) if link_offsets is not None
+             else arm_self_pairs((link_offset,), ("r_",)))
+    d.n_self_pairs = len(pairs)
+    for k, (a, b) in enumerate(pairs):
+        d.self_pair[k][0], d.self_pair[k][1] = a, b
 
 
 def _unit(rng):
