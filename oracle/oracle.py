@@ -208,6 +208,24 @@ def collision_rows(wl, b, x=None, cap=8192, term=0):
     return out[:min(n, cap)]
 
 
+def qp_solve(P, q, A, l, u, settings):
+    """One QP (scipy CSC P upper triangular, A) through the OSQP restatement with
+    thip_osqp_settings `settings`: (status, x, y, iterations)."""
+    L = lib()
+    ip = C.POINTER(C.c_int)
+    dp = C.POINTER(C.c_double)
+    L.oracle_qp_solve.argtypes = [C.c_int, C.c_int, ip, ip, dp, dp, ip, ip, dp, dp, dp, C.c_void_p, dp, dp, ip]
+    L.oracle_qp_solve.restype = C.c_int
+    n, m = P.shape[0], A.shape[0]
+    arrs = [np.ascontiguousarray(v, dtype=np.int32) for v in (P.indptr, P.indices, A.indptr, A.indices)]
+    vals = [np.ascontiguousarray(v, dtype=np.float64) for v in (P.data, q, A.data, l, u)]
+    x, y, it = np.zeros(n), np.zeros(max(m, 1)), C.c_int(0)
+    st = L.oracle_qp_solve(n, m, arrs[0].ctypes.data_as(ip), arrs[1].ctypes.data_as(ip), _dp(vals[0]), _dp(vals[1]),
+                           arrs[2].ctypes.data_as(ip), arrs[3].ctypes.data_as(ip), _dp(vals[2]), _dp(vals[3]),
+                           _dp(vals[4]), C.cast(C.pointer(settings), C.c_void_p), _dp(x), _dp(y), C.byref(it))
+    return st, x, y[:m], it.value
+
+
 def swept_sphere_prim(a, b, r, prim):
     """(dist, normal, p_robot, t_star) of the sphere swept a -> b vs a primitive."""
     L = lib()

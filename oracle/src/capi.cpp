@@ -13,6 +13,7 @@
 #include "collision.hpp"
 #include "terms.hpp"
 #include "jitter.hpp"
+#include "osqp_restated.hpp"
 
 using namespace orc;
 
@@ -396,6 +397,62 @@ void oracle_sphere_prim(const double* c, double r, const double* prim, double* o
     out8[4 + i] = pr[i];
   }
   out8[7] = 0;
+}
+
+// One QP through the OSQP restatement (test helper: the parity gate measures the
+// GPU's generic QP kernel against it).  P upper-triangular CSC, A CSC; returns
+// the OSQP status (setup errors negated) and the ADMM iterations in *iter.
+int oracle_qp_solve(int n, int m, const int* Pp, const int* Pi, const double* Px, const double* q, const int* Ap,
+                    const int* Ai, const double* Ax, const double* l, const double* u, const thip_osqp_settings* s,
+                    double* x, double* y, int* iter)
+{
+  try
+  {
+    Csc P, A;
+    P.n = P.m = n;
+    A.n = n;
+    A.m = m;
+    P.p.assign(Pp, Pp + n + 1);
+    P.i.assign(Pi, Pi + Pp[n]);
+    P.x.assign(Px, Px + Pp[n]);
+    A.p.assign(Ap, Ap + n + 1);
+    A.i.assign(Ai, Ai + Ap[n]);
+    A.x.assign(Ax, Ax + Ap[n]);
+    OsqpSettings st;
+    st.rho = s->rho;
+    st.sigma = s->sigma;
+    st.alpha = s->alpha;
+    st.scaling = s->scaling;
+    st.adaptive_rho = s->adaptive_rho;
+    st.adaptive_rho_interval = s->adaptive_rho_interval;
+    st.adaptive_rho_tolerance = s->adaptive_rho_tolerance;
+    st.max_iter = s->max_iter;
+    st.eps_abs = s->eps_abs;
+    st.eps_rel = s->eps_rel;
+    st.eps_prim_inf = s->eps_prim_inf;
+    st.eps_dual_inf = s->eps_dual_inf;
+    st.check_termination = s->check_termination;
+    st.warm_starting = s->warm_starting;
+    st.polishing = s->polishing;
+    st.delta = s->delta;
+    st.polish_refine_iter = s->polish_refine_iter;
+    OsqpSolver solver;
+    const int e = solver.setup(P, q, A, l, u, m, n, st);
+    if (e)
+      return -e;
+    solver.solve();
+    for (int j = 0; j < n; ++j)
+      x[j] = solver.sol_x[static_cast<std::size_t>(j)];
+    for (int r = 0; r < m; ++r)
+      y[r] = solver.sol_y[static_cast<std::size_t>(r)];
+    *iter = static_cast<int>(solver.iter);
+    return solver.status_val;
+  }
+  catch (const std::exception& ex)
+  {
+    g_err = ex.what();
+    return -100;
+  }
 }
 
 int oracle_sizeof_desc() { return static_cast<int>(sizeof(thip_problem_desc)); }

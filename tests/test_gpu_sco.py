@@ -188,7 +188,10 @@ def test_joint_terms_batched_host_loops(sco_lib, oracle_mod, name):
     x, res = host.solve_json_batch(texts)
     launches, qps = host.last_batch_qp_stats()
     print(f"{name}: {qps} QPs in {launches} launches; statuses {sorted({r.status for r in res})}")
-    assert qps >= 32 and launches * 4 <= qps
+    # one launch serves every pending QP of a pattern; the time-parameterised
+    # terms' patterns follow the values (exact-zero dt coefficients drop), so
+    # their groups are smaller
+    assert qps >= 32 and launches * 2 <= qps
     for b in range(32):
         assert check(x[b]) == [], (name, b, check(x[b]))
     from trajopt_amd.problems import Workload

@@ -210,3 +210,32 @@ def test_expr_ops_against_reference_build():
     b = subprocess.run([str(orc)], capture_output=True, text=True, timeout=60, check=True).stdout
     assert a.count("\n") == 2200
     assert a == b
+
+
+def test_oracle_qp_solve_kkt():
+    """oracle.qp_solve (the OSQP restatement on one raw QP, the parity gate's
+    reference for the generic QP kernel): a small box- and row-constrained QP
+    solves to OSQP's tolerance (primal / dual residuals, complementarity)."""
+    import ctypes as C
+
+    import scipy.sparse as sp
+
+    from oracle import oracle
+    from trajopt_amd import abi
+
+    rng = np.random.default_rng(3)
+    n, m0 = 10, 6
+    M = rng.normal(size=(n, n))
+    Pd = M @ M.T + np.eye(n)
+    A = np.vstack([rng.normal(size=(m0, n)), np.eye(n)])
+    lo = np.concatenate([rng.uniform(-1, 0, m0), np.full(n, -1.0)])
+    up = np.concatenate([rng.uniform(0, 1, m0), np.full(n, 1.0)])
+    q = rng.normal(size=n)
+    s = abi.OsqpSettings()
+    s.rho, s.sigma, s.alpha, s.scaling, s.adaptive_rho, s.adaptive_rho_tolerance = 0.1, 1e-6, 1.6, 10, 1, 5.0
+    s.max_iter, s.eps_abs, s.eps_rel, s.eps_prim_inf, s.eps_dual_inf = 8192, 1e-6, 1e-6, 1e-4, 1e-4
+    s.check_termination, s.warm_starting, s.polishing, s.delta, s.polish_refine_iter = 25, 1, 1, 1e-6, 3
+    st, x, y, it = oracle.qp_solve(sp.triu(sp.csc_matrix(Pd)).tocsc(), q, sp.csc_matrix(A), lo, up, s)
+    assert st == 1 and it > 0
+    assert np.abs(np.clip(A @ x, lo, up) - A @ x).max() < 1e-5
+    assert np.abs(Pd @ x + q + A.T @ y).max() < 1e-5

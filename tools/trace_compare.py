@@ -26,6 +26,8 @@ from trajopt_amd.runtime import BatchTrustRegionSQP  # noqa: E402
 def workload(name):
     if name in ("A", "B", "C", "J"):
         return problems.make_workload(name, 32)
+    if name == "E":
+        return problems.make_workload("E", 4)
     import test_gpu
 
     return test_gpu._variant(name)

@@ -705,10 +705,15 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   isizes[I_CONT] = 3 * hc;
   isizes[I_PCNT] = L.N;
   isizes[I_HKIND] = isizes[I_HSLOT] = hc;
-  // one bit per (primitive, sub-state, sphere) candidate of every unit while the
-  // sub-states number at most kWaves * kSubCap (the batched scan), each unit's
-  // bits padded to 64
-  isizes[I_HBITS] = L.coll ? ((long long)std::max(d.n_prims, 1) * d.n_spheres * kWaves * kSubCap + 31) / 32 +
+  // one bit per (primitive, sub-state, sphere) and (self sphere pair, sub-state)
+  // candidate of every unit while the sub-states number at most kWaves * kSubCap
+  // (the batched scan), each unit's bits padded to 64
+  std::vector<int> hb_sa, hb_sb, hb_kp;
+  if (L.coll)
+    self_sphere_pairs(d, hb_sa, hb_sb, hb_kp);
+  isizes[I_HBITS] = L.coll ? (((long long)std::max(d.n_prims, 1) * d.n_spheres + (long long)hb_sa.size()) *
+                                  kWaves * kSubCap +
+                              31) / 32 +
                                  2LL * (L.N + 1)
                            : 1;
   long long ioff = 0;
