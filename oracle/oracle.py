@@ -96,6 +96,15 @@ def set_jitter(jac_abs=0.0, kkt_rel=0.0, sol_rel=0.0, seed=0, variant="exact"):
     L.oracle_set_jitter(float(jac_abs), float(kkt_rel), float(sol_rel), int(seed))
 
 
+def set_jitter_coll(coll_abs=0.0, variant="exact"):
+    """+-coll_abs on every linearised contact expression's coefficients and
+    constant in the next solves (jitter.hpp), with set_jitter's seed; 0 = off."""
+    L = lib(variant)
+    L.oracle_set_jitter_coll.argtypes = [C.c_double]
+    L.oracle_set_jitter_coll.restype = None
+    L.oracle_set_jitter_coll(float(coll_abs))
+
+
 SCO_CASES = {0: "setup_problem", 1: "ExprMult_test2", 2: "ExprMult_test3", 3: "QuadraticSeparable",
              4: "QuadraticNonseparable", 5: "TP1", 6: "TP3", 7: "TP6", 8: "TP7"}
 

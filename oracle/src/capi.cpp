@@ -108,6 +108,9 @@ void oracle_set_jitter(double jac_abs, double kkt_rel, double sol_rel, unsigned 
   g_jitter.seed = seed;
 }
 
+// The contact-expression jitter (jitter.hpp coll_abs); 0 = off.
+void oracle_set_jitter_coll(double coll_abs) { g_jitter.coll_abs = coll_abs; }
+
 // BasicTrustRegionSQP::optimize over a batch, problems spread over n_threads.
 int oracle_solve_batch(const thip_problem_desc* d, int batch, const double* init, const double* targets,
                        const double* scene, const double* jpos_targets, double* out_x, thip_result* res,

@@ -1,6 +1,8 @@
 // ORACLE — test infrastructure only (see sco_expr.hpp header).
 #include "collision.hpp"
 
+#include "jitter.hpp"
+
 #include <cmath>
 #include <map>
 #include <stdexcept>
@@ -669,6 +671,24 @@ void contactGradient(const CollisionModel& cm, const double* dofvals, const Cont
   }
 }
 
+namespace
+{
+// parity-gate rounding jitter of a contact expression (jitter.hpp coll_abs)
+void jitterContact(int D, double* a0, double* a1, double& cst, int mask)
+{
+  if (!(g_jitter.coll_abs > 0))
+    return;
+  for (int j = 0; j < D; ++j)
+  {
+    if (mask & (1 << j))
+      a0[j] += g_jitter.coll_abs * jitterU();
+    if (mask & (1 << (D + j)))
+      a1[j] += g_jitter.coll_abs * jitterU();
+  }
+  cst += g_jitter.coll_abs * jitterU();
+}
+}  // namespace
+
 void contactExpression(const CollisionModel& cm, const Contact& ct, const double* q0, const double* q1, bool use0,
                        bool use1, bool single, double* a0, double* a1, double& cst, int& mask)
 {
@@ -704,6 +724,7 @@ void contactExpression(const CollisionModel& cm, const Contact& ct, const double
     // CalcDistExpressionsSingleTimeStep: 0 + part(x_t), then + d
     cst = 0.0 + part(q0, false, a0, 0);
     cst += ct.distance;
+    jitterContact(D, a0, a1, cst, mask);
     return;
   }
   // CalcDistExpressions{BothFree, StartFree, EndFree}: d + part(x_t) + part(x_t+1)
@@ -712,6 +733,7 @@ void contactExpression(const CollisionModel& cm, const Contact& ct, const double
     cst += part(q0, false, a0, 0);
   if (use1)
     cst += part(q1, true, a1, D);
+  jitterContact(D, a0, a1, cst, mask);
 }
 
 namespace

@@ -9,7 +9,9 @@
 // rounding noise: every FD Jacobian entry gets +-jac_abs, every KKT solution
 // entry a relative +-kkt_rel, every returned QP solution a relative +-sol_rel
 // (the GPU's polished points agree with the oracle's to ~1e-9 relative: the
-// delta-regularised polish KKT is ill conditioned), uniform, splitmix64 per
+// delta-regularised polish KKT is ill conditioned), every linearised contact
+// expression (collision gradient coefficients and constant: FK and Jacobian
+// products in another contraction order) a +-coll_abs, uniform, splitmix64 per
 // problem and seed.  Off
 // (both 0) unless oracle_set_jitter() was called.
 #pragma once
@@ -22,6 +24,7 @@ struct JitterCfg
   double jac_abs = 0;
   double kkt_rel = 0;
   double sol_rel = 0;  // relative jitter of every returned QP solution entry
+  double coll_abs = 0;  // absolute jitter of every linearised contact expression's coefficients and constant
   std::uint64_t seed = 0;
 };
 inline JitterCfg g_jitter;                     // set by oracle_set_jitter before a solve

@@ -12,10 +12,13 @@ changes that leave the mathematics untouched:
     sources at -O3 with FMA contraction): the same algorithm, another rounding;
   * rounding jitter (oracle/src/jitter.hpp), re-drawing the noise that the
     GPU's different operation order puts into the quantities the algorithm
-    thresholds: +-3e-10 on every forward-difference CartPose Jacobian entry
-    (GPU and oracle agree to 1.5e-10 there, tools/mask_probe.py), a relative
-    1e-14 on every KKT solve and 1e-10 on every returned QP solution (the
-    polished points agree to ~5e-11 relative, per-QP traces);
+    thresholds: +-3e-10 on every forward-difference CartPose Jacobian entry,
+    a relative 1e-14 on every KKT solve, 1e-10 on every returned QP solution
+    and +-1e-12 on every linearised contact expression (collision gradient
+    coefficients and constant: FK and Jacobian products in the GPU's
+    contraction order); each amplitude is checked against the measured
+    GPU-vs-oracle gap of its quantity (test_gpu.py
+    test_jitter_amplitudes_match_measured_gaps);
   * the initial trajectory perturbed by 1e-13, then 1e-12 (interior
     waypoints, seeded normal noise).
 The rerun "cloud" is grown lazily, only for the problems that miss the bar,
@@ -45,13 +48,16 @@ TOL_X = 1e-5
 COST_RTOL = 0.02
 
 # (build, input perturbation amplitude, rounding jitter on, seed)
-JITTER = (3e-10, 1e-14, 1e-10)  # FD Jacobian (absolute), KKT solve, QP solution (relative)
+# FD Jacobian (absolute), KKT solve, QP solution (relative), contact expressions (absolute)
+JITTER = (3e-10, 1e-14, 1e-10, 1e-12)
 SCHEDULE = ([("fast", 0.0, False, 0)]
             + [("exact", 0.0, True, s) for s in range(1, 9)]
             + [("exact", 1e-13, False, s) for s in range(1, 5)]
             + [("fast", 0.0, True, s) for s in range(1, 5)]
             + [("exact", 1e-12, False, s) for s in range(1, 5)]
-            + [("exact", 1e-13, True, s) for s in range(9, 13)])
+            + [("exact", 1e-13, True, s) for s in range(9, 13)]
+            + [("exact", 0.0, True, s) for s in range(13, 21)]
+            + [("fast", 1e-13, True, s) for s in range(21, 25)])
 
 RECORDS: list[dict] = []
 
@@ -113,12 +119,14 @@ class Cloud:
         self.k += 1
         sub = perturbed(subset(self.wl, pending), amp, seed)
         if jit:
-            self.oracle_mod.set_jitter(*JITTER, seed=seed, variant=build)
+            self.oracle_mod.set_jitter(*JITTER[:3], seed=seed, variant=build)
+            self.oracle_mod.set_jitter_coll(JITTER[3], variant=build)
         try:
             x, res = oracle_solve(sub, self.oracle_mod, self.threads, variant=build)
         finally:
             if jit:
                 self.oracle_mod.set_jitter(0.0, 0.0, 0.0, seed=0, variant=build)
+                self.oracle_mod.set_jitter_coll(0.0, variant=build)
         progress(f"cloud run {self.k}/{len(SCHEDULE)} ({build}, input {amp:g}, jitter {jit}, seed {seed}) "
                  f"on {len(pending)} problems")
         tol = self.wl.desc.sqp.cnt_tolerance

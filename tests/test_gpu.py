@@ -183,65 +183,34 @@ def test_sqp_parity(oracle_mod, cfg, B):
     check_parity(wl, oracle_mod, x, res, label=cfg)
 
 
-def _trajectory_qps(rng, K, T=24, D=7, contacts=60):
-    """K trajectory-shaped QPs of one pattern (velocity-smoothing P over T
-    waypoints of D joints, contact rows on two waypoints plus a hinge column,
-    hinge bounds and variable bounds): CSC arrays and per-QP values."""
-    import scipy.sparse as sp
-
-    nx = T * D
-    n = nx + contacts
-    Pd = sp.lil_matrix((n, n))
-    for t in range(T):
-        for j in range(D):
-            k = t * D + j
-            Pd[k, k] = 4.0 if 0 < t < T - 1 else 2.0
-            if t > 0:
-                Pd[k - D, k] = -1.0
-    for c in range(contacts):
-        Pd[nx + c, nx + c] = 1e-3
-    A = sp.lil_matrix((2 * contacts + n, n))
-    for c in range(contacts):
-        t = int(rng.integers(0, T - 1))
-        for j in range(D):
-            A[c, t * D + j] = rng.normal()
-            A[c, (t + 1) * D + j] = rng.normal()
-        A[c, nx + c] = -1.0
-        A[contacts + c, nx + c] = 1.0
-    for k in range(n):
-        A[2 * contacts + k, k] = 1.0
-    P, A = sp.triu(Pd).tocsc(), A.tocsc()
-    P.sort_indices()
-    A.sort_indices()
-    m = A.shape[0]
-    vals = []
-    for _ in range(K):
-        Px = P.data * (1 + 0.1 * rng.random(P.nnz))
-        Ax = A.data * np.where(A.data == 1.0, 1.0, 1 + 0.2 * rng.normal(size=A.nnz))
-        q = rng.normal(size=n)
-        lo = np.concatenate([np.full(contacts, -1e30), np.zeros(contacts), np.full(n, -0.5)])
-        up = np.concatenate([rng.uniform(-0.2, 0.2, contacts), np.full(contacts, 1e30), np.full(n, 0.5)])
-        vals.append((Px, q, Ax, lo, up))
-    return P, A, n, m, vals
+def _first_qp_l1(wl, b_list, gpu_trace, oracle_mod):
+    """sum |x*| of the first QP of each listed problem: (GPU trace, oracle trace)."""
+    out = []
+    for b in b_list:
+        _, _, to = oracle_mod.solve_trace(wl, b, cap=4096)
+        out.append((gpu_trace[b][0][8], to[0][8]))
+    return np.array(out)
 
 
-def test_jitter_amplitudes_match_measured_gaps(oracle_mod, hip):
+def test_jitter_amplitudes_match_measured_gaps(oracle_mod):
     """The parity gate's rounding jitter (parity.JITTER) against the measured
-    GPU-vs-oracle gap of the same quantity:
+    GPU-vs-oracle gap of the same quantity on the fused path:
       * forward-difference CartPose Jacobian entries (thip_linearize vs the
         oracle at config C's initial trajectories, 64 problems), absolute;
-      * one KKT solve: the generic QP kernel and the oracle's OSQP after one
-        ADMM iteration from a cold start (max_iter 1, no adaptive rho, no
-        polish) -- that iterate is one scaled KKT solve -- relative to its
-        inf-norm, on trajectory-shaped QPs;
-      * QP solutions: the same QPs solved to OSQP's tolerance with polish,
-        relative.
-    Each amplitude covers the largest measured gap and lies within 30x of it:
-    the jitter re-draws the GPU's rounding without swamping it."""
-    import ctypes as C
-
+      * one KKT solve: config J (JointPos terms only, so the first QP's data
+        are exact on both sides) with one ADMM iteration per QP (max_iter 1,
+        no adaptive rho, no polish): the first QP's iterate is one scaled KKT
+        solve -- the twisted block factor against the oracle's LDL^T --
+        compared as sum |x| (trace records), relative;
+      * QP solutions: the first QP of config J solved to tolerance with
+        polish, and of config C (its data carry the Jacobian gap), relative;
+      * contact expressions (collision gradient coefficients and constant):
+        thip_collision_rows against the oracle's rows on config C, LVS_DISCRETE
+        and LVS_CONTINUOUS, at the initial and solved trajectories, absolute.
+    Each amplitude covers the largest measured gap of its quantity and lies
+    within 30x of it: the jitter re-draws the GPU's rounding without swamping
+    it."""
     from parity import JITTER
-    from test_gpu_tsqp import _qp_lib
 
     wl = problems.make_workload("C", 64)
     s = BatchTrustRegionSQP(wl)
@@ -249,47 +218,42 @@ def test_jitter_amplitudes_match_measured_gaps(oracle_mod, hip):
     s.close()
     _, Jo = oracle_mod.linearize(wl, wl.init)
     gap_jac = float(np.abs(Jg - Jo).max())
-    rng = np.random.default_rng(17)
-    K = 16
-    P, A, n, m, vals = _trajectory_qps(rng, K)
-    L = _qp_lib()
-    ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))  # noqa: E731
-    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
-    Pp, Pi, Ap, Ai = (np.ascontiguousarray(v, dtype=np.int32) for v in (P.indptr, P.indices, A.indptr, A.indices))
-    h = C.c_void_p()
-    assert L.thip_qp_create(0, n, m, ip(Pp), ip(Pi), ip(Ap), ip(Ai), K, C.byref(h)) == 0
-    gaps = {}
-    try:
-        for label, one_iter in (("kkt", True), ("sol", False)):
-            st = abi.OsqpSettings()
-            hip.thip_default_osqp_settings(C.byref(st))
-            if one_iter:
-                st.max_iter, st.check_termination, st.adaptive_rho, st.polishing = 1, 0, 0, 0
-            Pv = np.concatenate([v[0] for v in vals])
-            qv = np.concatenate([v[1] for v in vals])
-            Av = np.concatenate([v[2] for v in vals])
-            lv = np.concatenate([v[3] for v in vals])
-            uv = np.concatenate([v[4] for v in vals])
-            x, y = np.zeros(K * n), np.zeros(K * m)
-            info = (C.c_byte * (64 * K))()
-            assert L.thip_qp_solve(h, dp(Pv), dp(qv), dp(Av), dp(lv), dp(uv), C.byref(st), None, None, None, dp(x),
-                                   dp(y), info) == 0
-            worst = 0.0
-            for k in range(K):
-                Pk = P.copy()
-                Pk.data = vals[k][0]
-                Ak = A.copy()
-                Ak.data = vals[k][2]
-                _, xo, _, _ = oracle_mod.qp_solve(Pk, vals[k][1], Ak, vals[k][3], vals[k][4], st)
-                xg = x[k * n:(k + 1) * n]
-                worst = max(worst, float(np.abs(xg - xo).max() / max(np.abs(xo).max(), 1e-300)))
-            gaps[label] = worst
-    finally:
-        L.thip_qp_destroy(h)
-    print(f"measured gaps: FD jacobian {gap_jac:.2e} (jitter {JITTER[0]:.0e}), KKT solve {gaps['kkt']:.2e} "
-          f"(jitter {JITTER[1]:.0e}), QP solution {gaps['sol']:.2e} (jitter {JITTER[2]:.0e})")
-    for name, gap, amp in (("FD jacobian", gap_jac, JITTER[0]), ("KKT solve", gaps["kkt"], JITTER[1]),
-                           ("QP solution", gaps["sol"], JITTER[2])):
+    B = 16
+    rel = lambda v: float(np.max(np.abs(v[:, 0] - v[:, 1]) / np.abs(v[:, 1])))  # noqa: E731
+    wl1 = problems.make_workload("J", B)
+    wl1.desc.osqp.max_iter, wl1.desc.osqp.check_termination = 1, 0
+    wl1.desc.osqp.adaptive_rho, wl1.desc.osqp.polishing = 0, 0
+    wl1.desc.sqp.max_iter = 1
+    _, _, tr = solve_gpu(wl1, trace=64)
+    gap_kkt = rel(_first_qp_l1(wl1, range(B), tr, oracle_mod))
+    wlj = problems.make_workload("J", B)
+    _, _, tr = solve_gpu(wlj, trace=64)
+    gap_sol = rel(_first_qp_l1(wlj, range(B), tr, oracle_mod))
+    wlc = problems.make_workload("C", B)
+    _, _, tr = solve_gpu(wlc, trace=64)
+    gap_sol_c = rel(_first_qp_l1(wlc, range(B), tr, oracle_mod))
+    # contact expressions: the fused kernel's rows against the oracle's, config C (LVS_DISCRETE and
+    # LVS_CONTINUOUS) at the initial and the oracle-solved trajectories
+    gap_coll = 0.0
+    for cont in (0, 1):
+        wlr = problems.make_workload("C", 16, first_problem=200)
+        wlr.desc.coll_continuous = cont
+        xo, _ = oracle_mod.solve(wlr, n_threads=16)
+        s = BatchTrustRegionSQP(wlr)
+        for xx in (wlr.init, xo):
+            rows = s.collision_rows(xx)
+            for b in range(wlr.batch):
+                rc = oracle_mod.collision_rows(wlr, b, xx[b])
+                assert rows[b].shape == rc.shape
+                if len(rc):
+                    gap_coll = max(gap_coll, float(np.abs(rows[b][:, 8:] - rc[:, 8:]).max()))
+        s.close()
+    print(f"measured gaps: FD jacobian {gap_jac:.2e} (jitter {JITTER[0]:.0e}); one KKT solve {gap_kkt:.2e} "
+          f"(jitter {JITTER[1]:.0e}); QP solution J {gap_sol:.2e}, C {gap_sol_c:.2e} (jitter {JITTER[2]:.0e}); "
+          f"contact expressions {gap_coll:.2e} (jitter {JITTER[3]:.0e})")
+    for name, gap, amp in (("FD jacobian", gap_jac, JITTER[0]), ("KKT solve", gap_kkt, JITTER[1]),
+                           ("QP solution", max(gap_sol, gap_sol_c), JITTER[2]),
+                           ("contact expressions", gap_coll, JITTER[3])):
         assert gap <= amp <= 30 * max(gap, 1e-300), f"{name}: jitter {amp:.1e} vs measured gap {gap:.2e}"
 
 

@@ -28,6 +28,14 @@ def workload(name):
         return problems.make_workload(name, 32)
     if name == "E":
         return problems.make_workload("E", 4)
+    if name == "Ccont":
+        wl = problems.make_workload("C", 32, first_problem=200)
+        wl.desc.coll_continuous = 1
+        return wl
+    if name == "Ccnt":
+        wl = problems.make_workload("C", 32, first_problem=64)
+        wl.desc.coll_is_cnt = 1
+        return wl
     import test_gpu
 
     return test_gpu._variant(name)

@@ -1281,11 +1281,112 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
   const int* HKD = c.ia(I_HKIND);
   double *HC0 = c.a(A_HC0), *HK = c.a(A_HK);
   int* HM = c.ia(I_HMASK);
+  // scene contacts (robot sphere vs primitive)
   FOR(k, c.s->n_h)
   {
     if (HKD[k] != 0)
       continue;
     const int t = HT[k], i = CONT[3 * k + 0], s = CONT[3 * k + 1], p = CONT[3 * k + 2];
+    if (p < 0)
+      continue;  // a self contact: below
+    const double* q0 = x + t * D;
+    const double* q1 = x + (t + 1) * D;
+    const bool single = L.coll_single != 0;  // i = the half (waypoint t + i)
+    const int cnt = single ? 1 : lvs_count(q0, q1, D, c.d->coll_lvs);
+    const int link = c.d->sphere_link[s];
+    const bool cont = c.d->coll_continuous == 1;
+    double q[THIP_MAX_DOF];
+    for (int j = 0; j < D; ++j)
+      q[j] = single ? (i ? q1[j] : q0[j]) : linspaced(cnt, q0[j], q1[j], i);
+    Pose T, T1;  // link pose at sub-state i (transform) and, for a cast, at i + 1 (cc_transform)
+    chain_fk(ch, q, link, T);
+    const double* cs = c.d->sphere_center[s];
+    double ctr[3];
+    for (int r = 0; r < 3; ++r)
+      ctr[r] = T.r[r * 3 + 0] * cs[0] + T.r[r * 3 + 1] * cs[1] + T.r[r * 3 + 2] * cs[2] + T.t[r];
+    double dist, n[3], pr[3], ts = 0.0;
+    if (cont)
+    {
+      double qn[THIP_MAX_DOF];
+      for (int j = 0; j < D; ++j)
+        qn[j] = linspaced(cnt, q0[j], q1[j], i + 1);
+      chain_fk(ch, qn, link, T1);
+      double ctr1[3];
+      for (int r = 0; r < 3; ++r)
+        ctr1[r] = T1.r[r * 3 + 0] * cs[0] + T1.r[r * 3 + 1] * cs[1] + T1.r[r * 3 + 2] * cs[2] + T1.t[r];
+      swept_sphere_prim_distance(ctr, ctr1, c.d->sphere_radius[s], c.scene + 16 * p, dist, n, pr, ts);
+    }
+    else
+    {
+      sphere_prim_distance(ctr, c.d->sphere_radius[s], c.scene + 16 * p, dist, n, pr);
+      T1 = T;
+    }
+    // nearest_points_local[0] in the frame of the sub-state (cast start) pose and the
+    // reference-point offsets link_transform.linear() * nearest_points_local with
+    // link_transform = transform (x_t part) / cc_transform (x_t+1 part), collision_terms.cpp:217-223
+    const double w[3] = { pr[0] - T.t[0], pr[1] - T.t[1], pr[2] - T.t[2] };
+    double pl[3], rv0[3], rv1[3];
+    for (int r = 0; r < 3; ++r)
+      pl[r] = T.r[0 * 3 + r] * w[0] + T.r[1 * 3 + r] * w[1] + T.r[2 * 3 + r] * w[2];
+    for (int r = 0; r < 3; ++r)
+    {
+      rv0[r] = T.r[r * 3 + 0] * pl[0] + T.r[r * 3 + 1] * pl[1] + T.r[r * 3 + 2] * pl[2];
+      rv1[r] = T1.r[r * 3 + 0] * pl[0] + T1.r[r * 3 + 1] * pl[1] + T1.r[r * 3 + 2] * pl[2];
+    }
+    // DISCRETE: CCType_None, GetGradient's scale 1 (collision_terms.cpp:214-221): the
+    // waypoint's half with scale 1 - 0 (half 0) or 1 (half 1), the other half absent
+    const double cc_time =
+        single ? double(i) : (cont ? (double(i) + ts) : double(i)) * (1.0 / double(cnt - 1));
+    const bool f0 = single ? (i == 1) : coll_fixed_step(c, t), f1 = single ? (i == 0) : coll_fixed_step(c, t + 1);
+    double cst = dist;
+    int mask = 0;
+    double* a = HC0 + k * 2 * D;
+    for (int e = 0; e < 2; ++e)
+    {
+      const bool skip = (e == 0) ? f0 : f1;
+      const double* qe = (e == 0) ? q0 : q1;
+      if (skip)
+      {
+        for (int j = 0; j < D; ++j)
+          a[e * D + j] = 0.0;
+        continue;
+      }
+      const double scale = (e == 1) ? cc_time : (1 - cc_time);
+      const double* rv = (e == 1) ? rv1 : rv0;
+      double J[6 * THIP_MAX_DOF];
+      chain_jacobian(ch, qe, link, J);
+      double gd = 0;
+      for (int j = 0; j < D; ++j)
+      {
+        const double wx = J[3 * D + j], wy = J[4 * D + j], wz = J[5 * D + j];
+        const double l0 = J[0 * D + j] + (wy * rv[2] - wz * rv[1]);
+        const double l1 = J[1 * D + j] + (wz * rv[0] - wx * rv[2]);
+        const double l2 = J[2 * D + j] + (wx * rv[1] - wy * rv[0]);
+        const double g = -1.0 * (n[0] * l0 + n[1] * l1 + n[2] * l2);
+        const double av = scale * g;
+        gd += g * qe[j];
+        // cleanupAff (expr_ops.cpp:88-99)
+        const bool keep = fabs(av) > 1e-7;
+        a[e * D + j] = keep ? av : 0.0;
+        mask |= keep ? (1 << (e * D + j)) : 0;
+      }
+      cst += scale * -gd;
+    }
+    HK[k] = cst;
+    HM[k] = mask;
+    c.a(A_HDIST)[k] = dist;
+    c.a(A_HCCT)[k] = single ? 0.0 : cc_time;
+  }
+  // self contacts (robot sphere s vs robot sphere -1 - p, both links moving; GetGradient's two
+  // sides).  Kept apart from the scene loop so that loop's code -- and with it the
+  // rounding of its contraction choices -- stays as it was.
+  FOR(k, c.s->n_h)
+  {
+    if (HKD[k] != 0)
+      continue;
+    const int t = HT[k], i = CONT[3 * k + 0], s = CONT[3 * k + 1], p = CONT[3 * k + 2];
+    if (p >= 0)
+      continue;
     const double* q0 = x + t * D;
     const double* q1 = x + (t + 1) * D;
     const bool single = L.coll_single != 0;  // i = the half (waypoint t + i)
@@ -1362,7 +1463,6 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
       const double* qe = (e == 0) ? q0 : q1;
       // CollisionsToDistanceExpressions: per side varDot(scale g, vars) and scale * -g.q;
       // a variable's side terms summed as the QP builder sums duplicates
-      double part = 0.0;
       for (int sd = 0; sd < nsides; ++sd)
       {
         const double scale = (e == 1) ? cct[sd] : (1 - cct[sd]);
@@ -1388,9 +1488,8 @@ __device__ void coll_scan(Ctx& c, const double* x, double* costs, bool rows)
             mask |= bit;
           }
         }
-        part += scale * -gd;
+        cst += scale * -gd;
       }
-      cst += part;
     }
     HK[k] = cst;
     HM[k] = mask;
@@ -5577,7 +5676,6 @@ __global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
   if (!args.work && static_cast<int>(blockIdx.x) >= args.batch)
     return;
   stage_chain(args.desc);
-  const Layout& L = args.L;
   // One problem per workgroup (args.work null), or a persistent workgroup per
   // resident slot taking problems in order from the launch's counter: the
   // grid is dealt round-robin over the XCDs, so with a static mapping each

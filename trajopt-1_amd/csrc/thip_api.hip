@@ -556,7 +556,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     fixed_of_step[static_cast<size_t>(d.fixed_steps[f])] = f;
 
   // workspace layout (doubles)
-  const long long nx = L.nx, nc = L.n_cols, m = L.m, NDD = (long long)L.N * L.D * L.D;
+  const long long nx = L.nx, nc = L.n_cols, m = L.m;
   const long long nab = std::max(L.n_abs, 1), D = L.D, hc = std::max(L.h_cap, 1);
   long long sizes[A_COUNT];
   for (int k = 0; k < A_COUNT; ++k)
