@@ -13,7 +13,7 @@ changes that leave the mathematics untouched:
   * rounding jitter (oracle/src/jitter.hpp), re-drawing the noise that the
     GPU's different operation order puts into the quantities the algorithm
     thresholds: +-3e-10 on every forward-difference CartPose Jacobian entry,
-    a relative 5e-15 on every KKT solve, 1e-10 on every returned QP solution
+    a relative 5e-15 on every KKT solve, 1e-9 on every returned QP solution
     and +-1e-12 on every linearised contact expression (collision gradient
     coefficients and constant: FK and Jacobian products in the GPU's
     contraction order); each amplitude is checked against the measured
@@ -49,7 +49,7 @@ COST_RTOL = 0.02
 
 # (build, input perturbation amplitude, rounding jitter on, seed)
 # FD Jacobian (absolute), KKT solve, QP solution (relative), contact expressions (absolute)
-JITTER = (3e-10, 5e-15, 1e-10, 1e-12)
+JITTER = (3e-10, 5e-15, 1e-9, 1e-12)
 SCHEDULE = ([("fast", 0.0, False, 0)]
             + [("exact", 0.0, True, s) for s in range(1, 9)]
             + [("exact", 1e-13, False, s) for s in range(1, 5)]

@@ -180,9 +180,14 @@ def test_joint_terms_batched_host_loops(sco_lib, oracle_mod, name):
     doc = json.loads(text)
     rng = np.random.default_rng(17)
     texts = [text]
+    # perturbed starts inside the joint limits (joints 3 and 5 have upper limit 0:
+    # a fixed dof held outside its limits makes the QP infeasible)
+    chain = host.lower_json(text)[0].chain
+    lo, hi = np.array(chain.lower[:7]) + 1e-3, np.array(chain.upper[:7]) - 1e-3
     for b in range(1, 32):
         d = copy.deepcopy(doc)
-        d["init_info"] = {"type": "given_traj", "data": (0.02 * rng.standard_normal((joint_terms.STEPS, 7))).tolist()}
+        data = np.clip(0.02 * rng.standard_normal((joint_terms.STEPS, 7)), lo, hi)
+        d["init_info"] = {"type": "given_traj", "data": data.tolist()}
         if "dt" in doc["init_info"]:
             d["init_info"]["dt"] = doc["init_info"]["dt"]
         texts.append(json.dumps(d))
