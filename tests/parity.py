@@ -59,7 +59,15 @@ SCHEDULE = ([("fast", 0.0, False, 0)]
             + [("exact", 0.0, True, s) for s in range(13, 21)]
             + [("fast", 1e-13, True, s) for s in range(21, 25)]
             + [("exact", 1e-12, True, s) for s in range(25, 33)]
-            + [("fast", 1e-12, True, s) for s in range(33, 37)])
+            + [("fast", 1e-12, True, s) for s in range(33, 37)]
+            # runs 50-97: only problems the first 49 leave unexplained get here (the
+            # cloud grows lazily); a GPU outcome drawn from the same rounding
+            # distribution falls outside the envelope of n reruns in a given
+            # coordinate with probability 2/(n+2), so a chaotic problem can need more
+            # than 49 (4 of C-1024's 14 misses did in round 4)
+            + [("exact", 0.0, True, s) for s in range(37, 61)]
+            + [("fast", 0.0, True, s) for s in range(61, 73)]
+            + [("exact", 1e-13, True, s) for s in range(73, 85)])
 
 RECORDS: list[dict] = []
 
@@ -203,11 +211,19 @@ def check_parity(wl, oracle_mod, x, res, label="", min_strict=0.85, oracle=None,
         msgs.append(f"problem {b}: status {res[b].status} vs {ro[b].status}, flag {fg} vs {fo}, "
                     f"|dx| {dx[b]:.2e}, cost {res[b].total_cost:.6g} vs {ro[b].total_cost:.6g}; "
                     f"{len(mem)} oracle reruns reach {sorted({(st, fl) for _, st, fl, _ in mem})}, "
-                    f"spread {max([np.abs(xm - xo[b]).max() for xm, _, _, _ in mem], default=0):.1e}")
+                    f"spread {max([np.abs(xm - xo[b]).max() for xm, _, _, _ in mem], default=0):.1e}, "
+                    f"envelope excess {_excess(x[b], xo[b], mem):.1e}")
     assert not unexplained, f"{label}: {len(unexplained)} problems miss the bar without proof:\n" + "\n".join(msgs)
     if B >= 32:
         assert strict >= min_strict * B, f"{label}: only {strict}/{B} problems meet the bar strictly"
     return rec
+
+
+def _excess(xg, xo, mem):
+    """How far the GPU's trajectory lies outside the cloud's coordinate-wise
+    envelope (0 inside)."""
+    cx = np.stack([xo] + [xm for xm, _, _, _ in mem])
+    return float(max(0.0, (cx.min(0) - xg).max(), (xg - cx.max(0)).max()))
 
 
 def pooled(records=None):
