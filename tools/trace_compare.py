@@ -24,6 +24,9 @@ from trajopt_amd.runtime import BatchTrustRegionSQP  # noqa: E402
 
 
 def workload(name):
+    if "@" in name:  # e.g. C@613: problem 613 of config C alone (the full-batch tests' indexing)
+        cfg, first = name.split("@")
+        return problems.make_workload(cfg, 1, first_problem=int(first))
     if name in ("A", "B", "C", "J"):
         return problems.make_workload(name, 32)
     if name == "E":
