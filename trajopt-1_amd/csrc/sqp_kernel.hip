@@ -2139,6 +2139,8 @@ __device__ __noinline__ void twisted_factor_half(Ctx& c, Solver& sv, const doubl
   }
 }
 
+__device__ int build_hinge_chunks(Ctx& c);
+
 // returns false if the reduced matrix is not positive definite
 __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delta)
 {
@@ -2176,6 +2178,24 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
     c.a(A_HRE)[h] = rr * dn / (dn + rr * w * w);
   }
   BSYNC();
+  // the hinge chunk table for reduced_solve's row-parallel column sums (the
+  // QP's hinge rows are fixed from here to its last solve), and the field-major
+  // copy of the hinge coefficients its back-substitution reads (A_HCT, odd
+  // stride; the ADMM segment builds the same): one coalesced load per
+  // coefficient and wave instead of 2 D loads that each touch 64 cache lines
+  build_hinge_chunks(c);
+  if (nh > 0)
+  {
+    const int nhs = nh | 1;
+    const double* HC = c.a(A_HC);
+    double* HCT = c.a(A_HCT);
+    FOR(e, nh * 2 * D)
+    {
+      const int h = e / (2 * D), k = e - h * 2 * D;
+      HCT[k * nhs + h] = HC[e];
+    }
+    BSYNC();
+  }
   // diagonal blocks, in the solve layout (Layout::nbr): block T = b N + t holds
   // waypoint t's dofs [b sD, (b + 1) sD); the other branches' entries of the
   // waypoint block are exact zeros (no term touches two branches)
@@ -2720,44 +2740,6 @@ __device__ __forceinline__ void twisted_middle(const Ctx& c, const Solver& sv, c
                           YVp, branch);
 }
 
-// Solve K [x; aux] = r + A' eta, with r (n_cols) in A_BXW (overwritten) and
-// eta over all m rows; K = P + diag(sigK) + A' diag(rho) A as in factor().
-// The 2x2 aux block of each CartPose row is eliminated with its explicit
-// inverse, expanded so that the rho^2 and eta_r terms cancel analytically:
-// with polish rho = 1/delta the textbook Sherman-Morrison form subtracts
-// O(1/delta^2) quantities and loses ~12 digits.
-// b + sum over hinge rows h in [h0, h1) of HC[h][k] * mr[h] (a column's
-// share of the hinge rows of one step pair), summed per chunk of kHChunk rows
-// (even and odd rows apart) and the chunk sums added in order: the association of admm_segment's
-// row-parallel gather, so that both paths give identical iterates
-__device__ __forceinline__ double hinge_gather(const double* HC, const double* mr, int stride, int k, int h0, int h1,
-                                               double b)
-{
-  for (int q = h0; q < h1; q += kHChunk)
-  {
-    const int qe = min(q + kHChunk, h1);
-    // all loads of the chunk first (clamped rows), then the masked sums in
-    // the original order
-    double hc[kHChunk], mv[kHChunk];
-#pragma unroll
-    for (int i = 0; i < kHChunk; ++i)
-    {
-      const int h = min(q + i, qe - 1);
-      hc[i] = HC[h * stride + k];
-      mv[i] = mr[h];
-    }
-    double s0 = 0, s1 = 0;
-#pragma unroll
-    for (int i = 0; i < kHChunk; i += 2)
-    {
-      s0 = fma(hc[i], mv[i] * ((q + i < qe) ? 1.0 : 0.0), s0);  // masked: unchanged
-      s1 = fma(hc[i + 1], mv[i + 1] * ((q + i + 1 < qe) ? 1.0 : 0.0), s1);
-    }
-    b += s0 + s1;
-  }
-  return b;
-}
-
 // b + sum over the CSR entries p in [p0, p1) of GS[rows[p]][j] * MR[rows[p]],
 // in order; the row indices and values of four entries are loaded before
 // their products are summed (a serial chain of dependent loads otherwise)
@@ -2804,57 +2786,6 @@ __device__ __forceinline__ double contig_row_gather(int p0, int p1, const double
   return b;
 }
 
-// both hinge_gather calls of column (t, j) -- pair t's rows on coefficient j,
-// then pair t - 1's on D + j -- with the first chunk of each pair loaded
-// together (a pair rarely has more than kHChunk rows); the sums and their
-// association are hinge_gather's
-__device__ __forceinline__ double hinge_gather2(const double* HC, const double* mr, int stride, int j, const int* HP,
-                                                int t, double b)
-{
-  const int D = stride / 2;
-  const int a0 = HP[t], a1 = HP[t + 1];
-  const int c0 = (t > 0) ? HP[t - 1] : a0, c1 = a0;
-  double ha[kHChunk], ma[kHChunk], hb[kHChunk], mb[kHChunk];
-  const int ae = min(a0 + kHChunk, a1), ce = min(c0 + kHChunk, c1);
-#pragma unroll
-  for (int i = 0; i < kHChunk; ++i)
-  {
-    const int h = min(a0 + i, max(ae - 1, 0));
-    ha[i] = HC[h * stride + j];
-    ma[i] = mr[h];
-    const int g = min(c0 + i, max(ce - 1, 0));
-    hb[i] = HC[g * stride + D + j];
-    mb[i] = mr[g];
-  }
-  if (a0 < a1)
-  {
-    double s0 = 0, s1 = 0;
-#pragma unroll
-    for (int i = 0; i < kHChunk; i += 2)
-    {
-      s0 = fma(ha[i], ma[i] * ((a0 + i < ae) ? 1.0 : 0.0), s0);
-      s1 = fma(ha[i + 1], ma[i + 1] * ((a0 + i + 1 < ae) ? 1.0 : 0.0), s1);
-    }
-    b += s0 + s1;
-    if (ae < a1)
-      b = hinge_gather(HC, mr, stride, j, ae, a1, b);
-  }
-  if (c0 < c1)
-  {
-    double s0 = 0, s1 = 0;
-#pragma unroll
-    for (int i = 0; i < kHChunk; i += 2)
-    {
-      s0 = fma(hb[i], mb[i] * ((c0 + i < ce) ? 1.0 : 0.0), s0);
-      s1 = fma(hb[i + 1], mb[i + 1] * ((c0 + i + 1 < ce) ? 1.0 : 0.0), s1);
-    }
-    b += s0 + s1;
-    if (ce < c1)
-      b = hinge_gather(HC, mr, stride, D + j, ce, c1, b);
-  }
-  return b;
-}
-
 // a hinge row's distance-expression value a_t.x_t + a_t+1.x_t+1 (two
 // independent partial sums, one per waypoint); x points at x_t
 template <typename XP>
@@ -2866,6 +2797,15 @@ __device__ __forceinline__ double hinge_dot(const double* hc, XP x, int D)
   return masked_dot<kOct>(hc, 1, x, 1, 0, D) + masked_dot<kOct>(hc + D, 1, x + D, 1, 0, D);
 }
 
+// Solve K [x; aux] = r + A' eta, with r (n_cols) in A_BXW (overwritten) and
+// eta over all m rows; K = P + diag(sigK) + A' diag(rho) A as in factor().
+// The 2x2 aux block of each CartPose row is eliminated with its explicit
+// inverse, expanded so that the rho^2 and eta_r terms cancel analytically:
+// with polish rho = 1/delta the textbook Sherman-Morrison form subtracts
+// O(1/delta^2) quantities and loses ~12 digits.  The hinge rows' share of each
+// column is summed per chunk of kHChunk rows of one step pair (even and odd
+// rows apart) and the chunk sums added in order: the association of
+// admm_segment's row-parallel gather, so that both paths give identical iterates.
 __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, const double* eta, double* out)
 {
   long long* pf = (c.tid == 0) ? c.s->prof : nullptr;
@@ -2889,7 +2829,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
                *FS = c.a(A_FS);
   double *BX = c.a(A_BXW), *BA = c.a(A_BA), *MR = c.a(A_MR), *CV = c.a(A_CV), *YV = c.a(A_YV);
   const double *RHO = c.a(A_RHO), *HW = c.a(A_HW), *HC = c.a(A_HC);
-  const int *ACT = c.ia(I_ACT), *HT = c.ia(I_HT), *HP = c.ia(I_HPTR);
+  const int *ACT = c.ia(I_ACT), *HT = c.ia(I_HT);
   const int *fixed_of_step = c.T.fixed_of_step, *step_ptr = c.T.step_ptr, *step_rows = c.T.step_rows,
             *row_step = c.T.row_step;
   // rho_k() and bound_row() on the hoisted values (same expressions)
@@ -2951,6 +2891,58 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   }
   BSYNC();
   PROF_LAP(23);
+  // the hinge share of the column sums, row-parallel: chunk q's partial sum of
+  // coefficient k over its rows (build_hinge_chunks, at the factorisation),
+  // each in the association described above; the columns below add their step
+  // pairs' chunk sums in order, so b is bitwise what gathering every row of
+  // the column serially gave (one thread per column walked up to ~100 rows
+  // per pair in HBM on config E's heavy problems)
+  const int* const HCP = c.s->hcp;
+  const int pw = L.part_w;
+  double* const PART = c.a(A_HPART);
+  if (nh > 0)
+  {
+    const int* CHK = reinterpret_cast<const int*>(c.a(A_HCHK));
+    const int nchk = HCP[L.N], k = tid % pw, cstep = kBlock / pw;
+    constexpr int kChU = 4;  // chunks per thread at once: 4 x 8 coefficient loads in flight
+    if (k < 2 * D)
+      for (int q0 = tid / pw; q0 < nchk; q0 += kChU * cstep)
+      {
+        double hc[kChU][kHChunk], mv[kChU][kHChunk];
+        int h0v[kChU], h1v[kChU];
+#pragma unroll
+        for (int u = 0; u < kChU; ++u)
+        {
+          const int q = min(q0 + u * cstep, nchk - 1);  // clamped: every load valid
+          const int h0 = CHK[2 * q], h1 = CHK[2 * q + 1];
+          h0v[u] = h0;
+          h1v[u] = h1;
+#pragma unroll
+          for (int i = 0; i < kHChunk; ++i)
+          {
+            const int h = min(h0 + i, h1 - 1);
+            hc[u][i] = HC[h * 2 * D + k];
+            mv[u][i] = MR[n_rows + h];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kChU; ++u)
+        {
+          const int q = q0 + u * cstep, h0 = h0v[u], h1 = h1v[u];
+          if (q >= nchk)
+            break;
+          double s0 = 0, s1 = 0;
+#pragma unroll
+          for (int i = 0; i < kHChunk; i += 2)
+          {
+            s0 = fma(hc[u][i], mv[u][i] * ((h0 + i < h1) ? 1.0 : 0.0), s0);  // masked: unchanged
+            s1 = fma(hc[u][i + 1], mv[u][i + 1] * ((h0 + i + 1 < h1) ? 1.0 : 0.0), s1);
+          }
+          PART[q * pw + k] = s0 + s1;
+        }
+      }
+    BSYNC();
+  }
   // the waypoint right-hand sides, kRhsU columns per thread at once (their
   // loads overlap; each column's sums in the order of one column alone)
   constexpr int kRhsU = 3;
@@ -2971,7 +2963,13 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       else
         b = csr_row_gather(step_rows, step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
       if (nh > 0)
-        b = hinge_gather2(HC, MR + n_rows, 2 * D, j, HP, t, b);
+      {
+        for (int q = HCP[t]; q < HCP[t + 1]; ++q)  // pair t, coefficient j
+          b += PART[q * pw + j];
+        if (t > 0)
+          for (int q = HCP[t - 1]; q < HCP[t]; ++q)  // pair t - 1, coefficient D + j
+            b += PART[q * pw + D + j];
+      }
       bv[u] = b;
     }
 #pragma unroll
@@ -3078,15 +3076,23 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       out[nx + 2 * r + 1] = op[u];
     }
   }
+  double* const HG = c.a(A_HG);
+  const double* const HCT = c.a(A_HCT);
+  const int nhs = nh | 1;
   for (int h0 = tid; h0 < nh; h0 += kGenUHinge * kBlock)
   {
-    double ov[kGenUHinge];
+    double ov[kGenUHinge], gv[kGenUHinge];
 #pragma unroll
     for (int u = 0; u < kGenUHinge; ++u)
     {
       const int h = min(h0 + u * kBlock, nh - 1);
       const int t = HT[h];
-      const double g = hinge_dot(HC + h * 2 * D, lds(XC) + t * D, D);
+      // hinge_dot(HC + h 2D, x_t) on the field-major copy (same terms, same order)
+      const double g = (D > kOct) ? masked_dot<THIP_MAX_DOF>(HCT + h, nhs, lds(XC) + t * D, 1, 0, D) +
+                                        masked_dot<THIP_MAX_DOF>(HCT + D * nhs + h, nhs, lds(XC) + (t + 1) * D, 1, 0, D)
+                                  : masked_dot<kOct>(HCT + h, nhs, lds(XC) + t * D, 1, 0, D) +
+                                        masked_dot<kOct>(HCT + D * nhs + h, nhs, lds(XC) + (t + 1) * D, 1, 0, D);
+      gv[u] = g;
       const int col = nc_base + h;
       const double rr = rho_l(m_base + 2 * h);
       const double dn = DG[col], w = HW[h];
@@ -3099,6 +3105,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       if (h >= nh)
         break;
       out[nc_base + h] = ov[u];
+      HG[h] = gv[u];  // a.x of the x columns just solved: admm_step's hinge-row update reuses it
     }
   }
   BSYNC();
@@ -3708,14 +3715,15 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
       // hinge row m_base + 2h: a_t.x_t + a_t+1.x_t+1 + w h; m_base + 2h + 1:
       // the bound row of h.  One thread per hinge variable updates both rows
       // (a loop over the rows alternated the two kinds lane by lane)
-      const double *HC = c.a(A_HC), *HW = c.a(A_HW);
-      const int* HT = c.ia(I_HT);
+      const double *HG = c.a(A_HG), *HW = c.a(A_HW);
       const int nh = (m - m_base) >> 1;
       for (int h = tid; h < nh; h += kBlock)
       {
         const int col = nc_base + h, r0 = m_base + 2 * h;
         const double xh = XT[col];
-        const double zt2[2] = { hinge_dot(HC + h * 2 * D, XT + HT[h] * D, D) + HW[h] * xh, BS[col] * xh };
+        // a.x_tilde: reduced_solve's back-substitution computed it from the same
+        // x columns (bitwise the hinge_dot of XT)
+        const double zt2[2] = { HG[h] + HW[h] * xh, BS[col] * xh };
         double rh[2], yv[2], zv[2], lo[2], up[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u)
@@ -5129,7 +5137,7 @@ __device__ void plan_lds_dynamic(Ctx& c)
     const long long NDD = (long long)L.sN * L.sD * L.sD, nab = L.n_abs > 0 ? L.n_abs : 1;
     // the ADMM segment's working set first (chains, rhs, multipliers, the
     // hinge-row pack and coefficients), then the rest as in the host plan
-    const int order[] = { A_LINV, A_CV, A_YV, A_CPK, A_MR, A_HPART, A_HCHK, A_HCT, A_HPK, A_HC, A_BXW, A_BA, A_HW, A_HRE, A_DG, A_GS, A_WS,
+    const int order[] = { A_LINV, A_CV, A_YV, A_CPK, A_MR, A_HPART, A_HCHK, A_HCT, A_HPK, A_HG, A_HC, A_BXW, A_BA, A_HW, A_HRE, A_DG, A_GS, A_WS,
                           A_FS,   A_BS, A_XA0, A_XA1, A_Z0, A_Z1, A_Y, A_XT, A_PZ, A_RHO, A_L,  A_U,  A_Q,
                           A_DX,   A_DY, A_PD,  A_PO,  A_E,  A_DS, A_RE, A_CPL, A_PB, A_PS, A_PR };
     long long used = L.lds_scratch;
@@ -5144,7 +5152,7 @@ __device__ void plan_lds_dynamic(Ctx& c)
         case A_MR: n = L.n_rows + nh; break;
         case A_RE: n = L.n_rows; break;
         case A_HC: n = nh * 2 * D; break;
-        case A_HW: case A_HRE: n = nh; break;
+        case A_HW: case A_HRE: case A_HG: n = nh; break;
         case A_HPK: n = nh * kHPack; break;
         case A_HCT: n = (nh | 1) * 2 * D; break;
         case A_HCHK: n = nh / kHChunk + L.N + 1; break;
