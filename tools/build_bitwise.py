@@ -48,4 +48,5 @@ wl = problems.make_workload("C", 16, first_problem=200)
 wl.desc.coll_continuous = 1
 run("Ccont_generic", wl, abi.DEBUG_NO_SEGMENT)
 run("C_wide", problems.make_workload("C", 16), abi.DEBUG_FORCE_WIDE)
+run("C_seg", problems.make_workload("C", 64))
 np.savez(f"gpurun_out/bitwise_{tag}.npz", **out)

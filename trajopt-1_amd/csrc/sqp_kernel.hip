@@ -2140,6 +2140,15 @@ __device__ __noinline__ void twisted_factor_half(Ctx& c, Solver& sv, const doubl
 }
 
 __device__ int build_hinge_chunks(Ctx& c);
+__device__ __forceinline__ bool lds_resident(const Ctx& c, const double* p);
+
+// the QP's ADMM iterations run the register-resident segment (qp_solve); it
+// addresses MR, the hinge chunk table and chunk sums as LDS
+__device__ __forceinline__ bool seg_path(const Ctx& c)
+{
+  return c.L.seg_ok && lds_resident(c, c.a(A_MR)) && lds_resident(c, c.a(A_CPK)) &&
+         (c.s->n_h == 0 || (lds_resident(c, c.a(A_HCHK)) && lds_resident(c, c.a(A_HPART))));
+}
 
 // returns false if the reduced matrix is not positive definite
 __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delta)
@@ -2184,7 +2193,7 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
   // stride; the ADMM segment builds the same): one coalesced load per
   // coefficient and wave instead of 2 D loads that each touch 64 cache lines
   build_hinge_chunks(c);
-  if (nh > 0)
+  if (nh > 0 && !seg_path(c))  // (the segment builds its own copy)
   {
     const int nhs = nh | 1;
     const double* HC = c.a(A_HC);
@@ -4971,8 +4980,7 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   bool fail = false;
   const int ct = os.check_termination;
   // the segment addresses MR, the hinge chunk table and chunk sums as LDS
-  const bool seg = L.seg_ok && lds_resident(c, c.a(A_MR)) && lds_resident(c, c.a(A_CPK)) &&
-                   (c.s->n_h == 0 || (lds_resident(c, c.a(A_HCHK)) && lds_resident(c, c.a(A_HPART))));
+  const bool seg = seg_path(c);
   bool pre_ready = false;  // admm_step's ETA / BX (cleared when rho changes)
   for (it = 1; it <= os.max_iter; ++it)
   {
@@ -5152,7 +5160,8 @@ __device__ void plan_lds_dynamic(Ctx& c)
         case A_MR: n = L.n_rows + nh; break;
         case A_RE: n = L.n_rows; break;
         case A_HC: n = nh * 2 * D; break;
-        case A_HW: case A_HRE: case A_HG: n = nh; break;
+        case A_HW: case A_HRE: n = nh; break;
+        case A_HG: n = L.seg_ok ? 0 : nh; break;  // the generic step's only
         case A_HPK: n = nh * kHPack; break;
         case A_HCT: n = (nh | 1) * 2 * D; break;
         case A_HCHK: n = nh / kHChunk + L.N + 1; break;
