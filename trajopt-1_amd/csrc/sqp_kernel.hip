@@ -37,7 +37,8 @@ constexpr int kGenU = 4;
 // outstanding vector-memory operations (vmcnt), beyond which the issue stalls
 constexpr int kGenULight = 8;  // a few loads per iteration (streaming vectors, bound rows)
 constexpr int kGenUHeavy = 2;  // a CartPose row's coefficients and x (~2 D + 8 loads)
-constexpr int kGenUHinge = 1;  // a hinge row's 2 D coefficients and 2 D x values
+constexpr int kGenUHinge = 2;  // a hinge row's 2 D coefficients and 2 D x values (config E's heavy
+                                // problems: ~20 rows per thread, one HBM round trip each at 1)
 constexpr double kRhoMin = 1e-6, kRhoMax = 1e6, kRhoTol = 1e-4, kRhoEq = 1e3;
 constexpr double kMinScal = 1e-4, kMaxScal = 1e4;
 constexpr double kDivTol = 1.0 / kInf;
@@ -2806,6 +2807,25 @@ __device__ __forceinline__ double hinge_dot(const double* hc, XP x, int D)
   return masked_dot<kOct>(hc, 1, x, 1, 0, D) + masked_dot<kOct>(hc + D, 1, x + D, 1, 0, D);
 }
 
+// b + PART[q][k] for q in [q0, q1), added in order; eight loads issued before
+// their adds (one HBM round trip per chunk otherwise: ~26 per column on the
+// heavy problems, where the chunk sums do not fit in LDS).  Masked terms add
+// an exact zero.
+__device__ __forceinline__ double chunk_sum_add(const double* PART, int pw, int q0, int q1, int k, double b)
+{
+  for (int q = q0; q < q1; q += 8)
+  {
+    double p[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      p[i] = PART[min(q + i, q1 - 1) * pw + k];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      b += p[i] * ((q + i < q1) ? 1.0 : 0.0);
+  }
+  return b;
+}
+
 // Solve K [x; aux] = r + A' eta, with r (n_cols) in A_BXW (overwritten) and
 // eta over all m rows; K = P + diag(sigK) + A' diag(rho) A as in factor().
 // The 2x2 aux block of each CartPose row is eliminated with its explicit
@@ -2973,11 +2993,9 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
         b = csr_row_gather(step_rows, step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
       if (nh > 0)
       {
-        for (int q = HCP[t]; q < HCP[t + 1]; ++q)  // pair t, coefficient j
-          b += PART[q * pw + j];
+        b = chunk_sum_add(PART, pw, HCP[t], HCP[t + 1], j, b);  // pair t, coefficient j
         if (t > 0)
-          for (int q = HCP[t - 1]; q < HCP[t]; ++q)  // pair t - 1, coefficient D + j
-            b += PART[q * pw + D + j];
+          b = chunk_sum_add(PART, pw, HCP[t - 1], HCP[t], D + j, b);  // pair t - 1, coefficient D + j
       }
       bv[u] = b;
     }
