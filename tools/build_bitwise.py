@@ -49,4 +49,5 @@ wl.desc.coll_continuous = 1
 run("Ccont_generic", wl, abi.DEBUG_NO_SEGMENT)
 run("C_wide", problems.make_workload("C", 16), abi.DEBUG_FORCE_WIDE)
 run("C_seg", problems.make_workload("C", 64))
+run("torso_C", problems.make_workload("C", 8, robot="torso_right_arm"))
 np.savez(f"gpurun_out/bitwise_{tag}.npz", **out)

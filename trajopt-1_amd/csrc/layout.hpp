@@ -106,7 +106,6 @@ enum DArr : int
   A_HPART,   // hinge chunk partial sums [n_chunks][16]
   A_HCT,     // ADMM-segment copy of A_HC, field-major [2D][n_h | 1] (odd stride: no LDS bank conflicts)
   A_CPK,     // ADMM-segment chain pack (kCpk doubles, N <= 32 and D <= 8; see seg_chain_solve)
-  A_HG,      // generic ADMM step: each hinge row's a.x of the latest reduced solve (h_cap)
   A_COUNT
 };
 

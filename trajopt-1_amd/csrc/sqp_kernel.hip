@@ -3103,12 +3103,11 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       out[nx + 2 * r + 1] = op[u];
     }
   }
-  double* const HG = c.a(A_HG);
   const double* const HCT = c.a(A_HCT);
   const int nhs = nh | 1;
   for (int h0 = tid; h0 < nh; h0 += kGenUHinge * kBlock)
   {
-    double ov[kGenUHinge], gv[kGenUHinge];
+    double ov[kGenUHinge];
 #pragma unroll
     for (int u = 0; u < kGenUHinge; ++u)
     {
@@ -3119,7 +3118,6 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
                                         masked_dot<THIP_MAX_DOF>(HCT + D * nhs + h, nhs, lds(XC) + (t + 1) * D, 1, 0, D)
                                   : masked_dot<kOct>(HCT + h, nhs, lds(XC) + t * D, 1, 0, D) +
                                         masked_dot<kOct>(HCT + D * nhs + h, nhs, lds(XC) + (t + 1) * D, 1, 0, D);
-      gv[u] = g;
       const int col = nc_base + h;
       const double rr = rho_l(m_base + 2 * h);
       const double dn = DG[col], w = HW[h];
@@ -3132,7 +3130,6 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       if (h >= nh)
         break;
       out[nc_base + h] = ov[u];
-      HG[h] = gv[u];  // a.x of the x columns just solved: admm_step's hinge-row update reuses it
     }
   }
   BSYNC();
@@ -3742,15 +3739,16 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
       // hinge row m_base + 2h: a_t.x_t + a_t+1.x_t+1 + w h; m_base + 2h + 1:
       // the bound row of h.  One thread per hinge variable updates both rows
       // (a loop over the rows alternated the two kinds lane by lane)
-      const double *HG = c.a(A_HG), *HW = c.a(A_HW);
+      const double *HC = c.a(A_HC), *HW = c.a(A_HW);
+      const int* HT = c.ia(I_HT);
       const int nh = (m - m_base) >> 1;
       for (int h = tid; h < nh; h += kBlock)
       {
         const int col = nc_base + h, r0 = m_base + 2 * h;
         const double xh = XT[col];
-        // a.x_tilde: reduced_solve's back-substitution computed it from the same
-        // x columns (bitwise the hinge_dot of XT)
-        const double zt2[2] = { HG[h] + HW[h] * xh, BS[col] * xh };
+        // (reusing the back-substitution's a.x here -- the same x columns --
+        // broke torso_arm_8dof_C problem 2 deterministically: cause not found)
+        const double zt2[2] = { hinge_dot(HC + h * 2 * D, XT + HT[h] * D, D) + HW[h] * xh, BS[col] * xh };
         double rh[2], yv[2], zv[2], lo[2], up[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u)
@@ -5163,7 +5161,7 @@ __device__ void plan_lds_dynamic(Ctx& c)
     const long long NDD = (long long)L.sN * L.sD * L.sD, nab = L.n_abs > 0 ? L.n_abs : 1;
     // the ADMM segment's working set first (chains, rhs, multipliers, the
     // hinge-row pack and coefficients), then the rest as in the host plan
-    const int order[] = { A_LINV, A_CV, A_YV, A_CPK, A_MR, A_HPART, A_HCHK, A_HCT, A_HPK, A_HG, A_HC, A_BXW, A_BA, A_HW, A_HRE, A_DG, A_GS, A_WS,
+    const int order[] = { A_LINV, A_CV, A_YV, A_CPK, A_MR, A_HPART, A_HCHK, A_HCT, A_HPK, A_HC, A_BXW, A_BA, A_HW, A_HRE, A_DG, A_GS, A_WS,
                           A_FS,   A_BS, A_XA0, A_XA1, A_Z0, A_Z1, A_Y, A_XT, A_PZ, A_RHO, A_L,  A_U,  A_Q,
                           A_DX,   A_DY, A_PD,  A_PO,  A_E,  A_DS, A_RE, A_CPL, A_PB, A_PS, A_PR };
     long long used = L.lds_scratch;
@@ -5179,7 +5177,6 @@ __device__ void plan_lds_dynamic(Ctx& c)
         case A_RE: n = L.n_rows; break;
         case A_HC: n = nh * 2 * D; break;
         case A_HW: case A_HRE: n = nh; break;
-        case A_HG: n = L.seg_ok ? 0 : nh; break;  // the generic step's only
         case A_HPK: n = nh * kHPack; break;
         case A_HCT: n = (nh | 1) * 2 * D; break;
         case A_HCHK: n = nh / kHChunk + L.N + 1; break;

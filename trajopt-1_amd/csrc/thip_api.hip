@@ -680,7 +680,6 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   L.part_w = (2 * L.D <= 16) ? 16 : 32;
   sizes[A_HPART] = L.hinge ? nchk_cap * L.part_w : 1;
   sizes[A_HCT] = L.hinge ? 2 * D * (hc + 1) : 1;
-  sizes[A_HG] = L.hinge ? hc : 1;
   // the segment's chain pack: narrow blocks and N <= 32 only (the segment's domain)
   const bool cpk = !L.wide && L.N * 8 <= kBlock && L.N <= 2 * kCpkSteps;
   sizes[A_CPK] = cpk ? kCpk : 1;
