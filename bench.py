@@ -222,6 +222,13 @@ def main():
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
 
+    # stdout carries only the JSON line: anything the runtime or gloo prints
+    # there (gloo's "Rank r is connected to n peer ranks" banner at N > 1) goes
+    # to stderr, and the line is written to the saved descriptor
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
 
@@ -368,7 +375,7 @@ def main():
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_problems, args.cpu_threads)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
 
     for s in solvers:
         s.close()

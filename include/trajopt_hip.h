@@ -48,8 +48,9 @@ extern "C" {
  * descriptor carries abi_version, thip_chain.is_tree, thip_sqp_params.max_time.
  * 4: use_time, fixed dofs, time JointVel.  5: TotalTime.  6: further collision
  * terms (thip_coll_term), single-waypoint problems on the generic path.  7: robot
- * self-collision link pairs (n_self_pairs / self_pair). */
-#define THIP_ABI_VERSION 7
+ * self-collision link pairs (n_self_pairs / self_pair).  8: per link-pair collision
+ * margins and coefficients (n_coll_pairs / coll_pairs). */
+#define THIP_ABI_VERSION 8
 
 #define THIP_MAX_DOF 16
 #define THIP_MAX_LINKS 32
@@ -65,6 +66,7 @@ extern "C" {
 #define THIP_MAX_COLL_EXTRA 3
 #define THIP_MAX_SELF_PAIRS 64
 #define THIP_MAX_SELF_SPHERE_PAIRS 512
+#define THIP_MAX_COLL_PAIRS 64
 #define THIP_MAX_CONTACTS 131072
 
 /* error codes */
@@ -189,6 +191,26 @@ typedef struct thip_coll_term {
   double lvs;      /* longest_valid_segment_length (CONTINUOUS: +inf) */
   int continuous;  /* 0 LVS_DISCRETE, 1 LVS_CONTINUOUS / CONTINUOUS, 2 DISCRETE */
 } thip_coll_term;
+
+/* A per link-pair override of one collision term's margin and coefficient:
+ * CollisionTermInfo's "pairs" (problem_description.cpp:1686-1719) -- the
+ * pair's margin in the contact manager's CollisionMarginData (override type
+ * MODIFY) and its coefficient in CollisionCoeffData
+ * (trajopt_common/collision_types.h:51-184).  A pair's contacts use its margin
+ * for the contact distance (margin + buffer) and the hinge margin - d, and
+ * its coefficient for the hinge / constraint weight (collision_terms.cpp:
+ * 195-386, 646-688, 817-898, 1065-1161, 1267-1386); a coefficient with
+ * |coeff| <= 1e-6 (almostEqualRelativeAndAbs(coeff, 0)) drops the pair's
+ * contacts altogether (hasZeroCoeff).  The pair is unordered; a later entry
+ * for the same pair and term replaces an earlier one (insert_or_assign). */
+typedef struct thip_coll_pair {
+  int term;      /* 0: the coll_* term, 1 + x: coll_extra[x] */
+  int link;      /* chain link index of one side (a robot link of the group) */
+  int other;     /* >= 0: scene primitive index; < 0: -1 - chain link index (a robot link) */
+  int pad_;
+  double margin; /* the pair's dist_pen */
+  double coeff;  /* the pair's coeffs */
+} thip_coll_pair;
 
 /* The structure shared by every problem of a batch: chain, horizon, term
  * tables (the lowered TermInfo list), solver parameters.  Per-problem data
@@ -378,6 +400,10 @@ typedef struct thip_problem_desc {
    * thip_create rejects n_coll_extra > 0. */
   int n_coll_extra;
   thip_coll_term coll_extra[THIP_MAX_COLL_EXTRA];
+  /* per link-pair margins and coefficients of the collision terms (see
+   * thip_coll_pair); pairs not listed take their term's coll_margin / coll_coeff */
+  int n_coll_pairs;
+  thip_coll_pair coll_pairs[THIP_MAX_COLL_PAIRS];
 
   thip_sqp_params sqp;
   thip_osqp_settings osqp;

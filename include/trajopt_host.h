@@ -44,12 +44,16 @@ int thost_lower_json(const char* json_text, const double* scene, int n_prims, th
 int thost_solve_json_batch(const char* const* json_texts, int batch, const double* scenes, int n_prims, int device,
                            double* x, thip_result* results, char* err, int err_len);
 
-/* A batch with problems the fused kernel does not lower runs each problem's host
- * SQP loop on its own thread, every QP round of the batch in one launch per
+/* A batch with problems the fused kernel does not lower runs the problems' host
+ * SQP loops on a bounded pool of worker threads (each worker takes the next
+ * unsolved problem when its current one ends), every QP round in one launch per
  * sparsity pattern (trajopt::BatchTrustRegionSQP's host-loop mode, sco::GpuQPBatcher);
  * x then holds [batch][n_steps][n_dof (+ 1 with use_time)].  This reports the QP
  * launches and QPs of the calling thread's last batch solve (0 for a fused-kernel batch). */
 void thost_last_batch_qp_stats(long long* launches, long long* qps);
+/* Worker threads of such host-loop batches (process-wide; n <= 0 restores the
+ * default, 64; never more than the batch). */
+void thost_set_host_loop_workers(int n);
 
 /* thost_solve_json_batch sharded over n_devices HIP devices of this process
  * (trajopt::MultiDeviceBatchSQP: contiguous shards, sizes differing by at most

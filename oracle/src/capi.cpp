@@ -277,7 +277,7 @@ int oracle_collision_rows_term(const thip_problem_desc* d, int term, const doubl
     if (term < 0 || term > d->n_coll_extra || (term == 0 && !d->coll_enabled))
       throw std::runtime_error("oracle_collision_rows_term: no such collision term");
     const thip_coll_term tm = collisionTerm(*d, term);
-    const auto cmp = collisionModel(*d, tm, scene);
+    const auto cmp = collisionModel(*d, term, scene);
     const CollisionModel& cm = *cmp;
     const int first = tm.first_step;
     const int last = (tm.last_step < 0) ? N - 1 : tm.last_step;

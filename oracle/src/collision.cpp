@@ -407,11 +407,15 @@ void addSelfContacts(const CollisionModel& cm, const std::vector<Iso3>& T, const
                      long last, double dt, int mode, bool vars0_fixed, bool vars1_fixed,
                      std::vector<std::vector<Contact>>& keys)
 {
-  const double threshold = cm.margin + cm.buffer;
   for (std::size_t j = 0; j < cm.self_a.size(); ++j)
   {
     const int sa = cm.self_a[j], sb = cm.self_b[j];
     const int la = cm.sphere_link[sa], lb = cm.sphere_link[sb];
+    // the pair's contact distance (its margin + the buffer); a zero-coefficient
+    // pair's contacts are cleared by the filter
+    if (cm.hasZeroCoeff(la, lb))
+      continue;
+    const double margin = cm.marginOf(la, lb), threshold = margin + cm.buffer;
     const Iso3 &Ta = T[static_cast<std::size_t>(la)], &Tb = T[static_cast<std::size_t>(lb)];
     const Iso3& Ta1 = T1 ? (*T1)[static_cast<std::size_t>(la)] : Ta;
     const Iso3& Tb1 = T1 ? (*T1)[static_cast<std::size_t>(lb)] : Tb;
@@ -424,7 +428,7 @@ void addSelfContacts(const CollisionModel& cm, const std::vector<Iso3>& T, const
     double ta = 0, tb = 0;
     selfSphereDistance(a0, a1, cm.sphere_radius[sa], b0, b1, cm.sphere_radius[sb], mode == 2, ct.distance, ct.normal,
                        ct.p_robot, ct.p_prim, ta, tb);
-    if (!(ct.distance < threshold) || ct.distance > cm.margin + cm.buffer)
+    if (!(ct.distance < threshold) || ct.distance > margin + cm.buffer)
       continue;
     ct.link = la;
     ct.sphere = sa;
@@ -480,7 +484,6 @@ std::vector<Contact> flatten(std::map<std::pair<int, int>, std::vector<Contact>>
 std::vector<Contact> calcCollisionsSingle(const CollisionModel& cm, const double* q)
 {
   const thip_chain& ch = *cm.chain;
-  const double threshold = cm.margin + cm.buffer;
   std::map<std::pair<int, int>, std::vector<Contact>> results;
   std::vector<std::vector<Contact>> self(static_cast<std::size_t>(cm.n_self_keys));
   std::vector<Iso3> T;
@@ -493,9 +496,13 @@ std::vector<Contact> calcCollisionsSingle(const CollisionModel& cm, const double
     sphereWorld(Tl, cm.sphere_center[s], c);
     for (int p = 0; p < cm.n_prims; ++p)
     {
+      const int pk = CollisionModel::kScenePair + p;
+      if (cm.hasZeroCoeff(link, pk))
+        continue;
+      const double margin = cm.marginOf(link, pk), threshold = margin + cm.buffer;
       Contact ct;
       spherePrimDistance(c, cm.sphere_radius[s], cm.scene + 16 * p, ct.distance, ct.normal, ct.p_robot, ct.p_prim);
-      if (!(ct.distance < threshold) || ct.distance > cm.margin + cm.buffer)
+      if (!(ct.distance < threshold) || ct.distance > margin + cm.buffer)
         continue;
       ct.link = link;
       ct.prim = p;
@@ -531,7 +538,8 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
     cnt = static_cast<long>(std::ceil(dist / cm.lvs)) + 1;
   const long last = cnt - 1;
   const double dt = 1.0 / double(last);
-  const double threshold = cm.margin + cm.buffer;  // incrementCollisionMargin(buffer)
+  // per pair: contact distance margin + buffer (incrementCollisionMargin(buffer));
+  // zero-coefficient pairs are cleared by the filter
   std::map<std::pair<int, int>, std::vector<Contact>> results;
   std::vector<std::vector<Contact>> self(static_cast<std::size_t>(cm.n_self_keys));
   std::vector<double> q(static_cast<std::size_t>(D));
@@ -563,6 +571,10 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
         sphereWorld(Tb, cm.sphere_center[s], cb);
         for (int p = 0; p < cm.n_prims; ++p)
         {
+          const int pk = CollisionModel::kScenePair + p;
+          if (cm.hasZeroCoeff(link, pk))
+            continue;
+          const double margin = cm.marginOf(link, pk), threshold = margin + cm.buffer;
           Contact ct;
           double ts = 0;
           sweptSpherePrimDistance(ca, cb, cm.sphere_radius[s], cm.scene + 16 * p, ct.distance, ct.normal, ct.p_robot,
@@ -579,7 +591,7 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
           toLocal(Ta, ct.p_robot, ct.p_local);
           ct.cc_time = (double(i) + ts) * dt;
           ct.cc_type = (i == 0 && ts == 0.0) ? kCCTime0 : ((i + 1 == last && ts == 1.0) ? kCCTime1 : kCCBetween);
-          if (ct.distance > cm.margin + cm.buffer)
+          if (ct.distance > margin + cm.buffer)
             continue;
           if (!keepAtFixedEnds(ct, vars0_fixed, vars1_fixed))
             continue;
@@ -603,6 +615,10 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
       sphereWorld(Tl, cm.sphere_center[s], c);
       for (int p = 0; p < cm.n_prims; ++p)
       {
+        const int pk = CollisionModel::kScenePair + p;
+        if (cm.hasZeroCoeff(link, pk))
+          continue;
+        const double margin = cm.marginOf(link, pk), threshold = margin + cm.buffer;
         Contact ct;
         spherePrimDistance(c, cm.sphere_radius[s], cm.scene + 16 * p, ct.distance, ct.normal, ct.p_robot,
                            ct.p_prim);
@@ -621,7 +637,7 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
         ct.cc_type = (i == 0) ? kCCTime0 : ((i == last) ? kCCTime1 : kCCBetween);
         // filter: zero coeffs (none), removeInvalidContactResults
         // (collision_utils.cpp:73-114); the static primitive has CCType_None
-        if (ct.distance > cm.margin + cm.buffer)
+        if (ct.distance > margin + cm.buffer)
           continue;
         if (!keepAtFixedEnds(ct, vars0_fixed, vars1_fixed))
           continue;
@@ -763,10 +779,12 @@ public:
   }
 
   // dist = d + sum scale * g (q - q0) over the free ends, cleanupAff'd
-  AffExprVector exprs(const DblVec& x) const
+  AffExprVector exprs(const DblVec& x, std::vector<Contact>* cts = nullptr) const
   {
     AffExprVector out;
     const auto contacts = collide(x);
+    if (cts)
+      *cts = contacts;
     const DblVec q0 = getDblVec(x, vars0_), q1 = getDblVec(x, vars1_);
     const int D = cm_->chain->n_dof;
     for (const auto& c : contacts)
@@ -822,10 +840,12 @@ public:
     return calcCollisionsSingle(*cm_, q.data());
   }
 
-  AffExprVector exprs(const DblVec& x) const
+  AffExprVector exprs(const DblVec& x, std::vector<Contact>* cts = nullptr) const
   {
     AffExprVector out;
     const auto contacts = collide(x);
+    if (cts)
+      *cts = contacts;
     const DblVec q = getDblVec(x, vars0_);
     const int D = cm_->chain->n_dof;
     for (const auto& c : contacts)
@@ -868,7 +888,7 @@ public:
     const CollisionModel& cm = calc_.model();
     double out = 0;
     for (const auto& c : contacts)
-      out += std::fmax(cm.margin - c.distance, 0.0) * cm.coeff;
+      out += std::fmax(cm.marginOf(c.link, c.other()) - c.distance, 0.0) * cm.coeffOf(c.link, c.other());
     return out;
   }
 
@@ -876,8 +896,12 @@ public:
   ConvexObjective::Ptr convex(const DblVec& x, Model* model) override
   {
     auto out = std::make_shared<ConvexObjective>(model);
-    for (const AffExpr& e : calc_.exprs(x))
-      out->addHinge(exprSub(AffExpr(calc_.model().margin), e), calc_.model().coeff);
+    const CollisionModel& cm = calc_.model();
+    std::vector<Contact> cts;
+    const AffExprVector ex = calc_.exprs(x, &cts);
+    for (std::size_t i = 0; i < ex.size(); ++i)
+      out->addHinge(exprSub(AffExpr(cm.marginOf(cts[i].link, cts[i].other())), ex[i]),
+                    cm.coeffOf(cts[i].link, cts[i].other()));
     return out;
   }
 
@@ -902,7 +926,7 @@ public:
     const CollisionModel& cm = calc_.model();
     DblVec out;
     for (const auto& c : contacts)
-      out.push_back(std::fmax(cm.margin - c.distance, 0.0) * cm.coeff);
+      out.push_back(std::fmax(cm.marginOf(c.link, c.other()) - c.distance, 0.0) * cm.coeffOf(c.link, c.other()));
     return out;
   }
 
@@ -910,8 +934,12 @@ public:
   ConvexConstraints::Ptr convex(const DblVec& x, Model* model) override
   {
     auto out = std::make_shared<ConvexConstraints>(model);
-    for (const AffExpr& e : calc_.exprs(x))
-      out->addIneqCnt(exprMult(exprSub(AffExpr(calc_.model().margin), e), calc_.model().coeff));
+    const CollisionModel& cm = calc_.model();
+    std::vector<Contact> cts;
+    const AffExprVector ex = calc_.exprs(x, &cts);
+    for (std::size_t i = 0; i < ex.size(); ++i)
+      out->addIneqCnt(exprMult(exprSub(AffExpr(cm.marginOf(cts[i].link, cts[i].other())), ex[i]),
+                               cm.coeffOf(cts[i].link, cts[i].other())));
     return out;
   }
 
@@ -939,9 +967,9 @@ thip_coll_term collisionTerm(const thip_problem_desc& d, int k)
   return t;
 }
 
-std::shared_ptr<CollisionModel> collisionModel(const thip_problem_desc& d, const thip_coll_term& t,
-                                               const double* scene)
+std::shared_ptr<CollisionModel> collisionModel(const thip_problem_desc& d, int term, const double* scene)
 {
+  const thip_coll_term t = collisionTerm(d, term);
   auto cm = std::make_shared<CollisionModel>();
   cm->chain = &d.chain;
   cm->n_spheres = d.n_spheres;
@@ -972,6 +1000,23 @@ std::shared_ptr<CollisionModel> collisionModel(const thip_problem_desc& d, const
             cm->self_key.push_back(k);
           }
   cm->n_self_keys = d.n_self_pairs;
+  // "pairs" (problem_description.cpp:1707-1718): setCollisionMargin(link, p, dist_pen)
+  // and setCollisionCoeff(link, p, coeffs) per entry, in order (insert_or_assign;
+  // a zero coefficient joins zero_coeff_, a nonzero one leaves it)
+  for (int k = 0; k < d.n_coll_pairs; ++k)
+  {
+    const thip_coll_pair& e = d.coll_pairs[k];
+    if (e.term != term)
+      continue;
+    const int b = e.other >= 0 ? CollisionModel::kScenePair + e.other : -1 - e.other;
+    const auto key = CollisionModel::key(e.link, b);
+    cm->pair_margin[key] = e.margin;
+    cm->pair_coeff[key] = e.coeff;
+    if (std::fabs(e.coeff - 0.0) <= 1e-6)  // almostEqualRelativeAndAbs(coeff, 0.0)
+      cm->zero_coeff.insert(key);
+    else
+      cm->zero_coeff.erase(key);
+  }
   return cm;
 }
 
@@ -979,7 +1024,7 @@ void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, cons
                        const double* scene, int term)
 {
   const thip_coll_term tm = collisionTerm(d, term);
-  auto cm = collisionModel(d, tm, scene);
+  auto cm = collisionModel(d, term, scene);
   const int first = tm.first_step;
   const int last = (tm.last_step < 0) ? d.n_steps - 1 : tm.last_step;
   auto fixed = [&](int t) {

@@ -19,6 +19,8 @@
 // link-id hash order.
 #pragma once
 #include <memory>
+#include <map>
+#include <set>
 #include <vector>
 
 #include "terms.hpp"
@@ -42,6 +44,27 @@ struct CollisionModel
   // (sphere index order) -- and the key of each
   std::vector<int> self_a, self_b, self_key;
   int n_self_keys = 0;
+  // per link-pair data (CollisionTermInfo "pairs", problem_description.cpp:1686-1719):
+  // the contact manager's pair margins (CollisionMarginData, override MODIFY) and
+  // CollisionCoeffData's pair coefficients and zero-coefficient set
+  // (trajopt_common/src/collision_types.cpp:40-72), keyed by the unordered link
+  // pair -- a scene primitive p is the "link" kScenePair + p
+  static constexpr int kScenePair = 1 << 20;
+  std::map<std::pair<int, int>, double> pair_margin, pair_coeff;
+  std::set<std::pair<int, int>> zero_coeff;
+  static std::pair<int, int> key(int a, int b) { return a < b ? std::make_pair(a, b) : std::make_pair(b, a); }
+  // CollisionMarginData::getCollisionMargin / CollisionCoeffData::getCollisionCoeff
+  double marginOf(int a, int b) const
+  {
+    const auto it = pair_margin.find(key(a, b));
+    return it == pair_margin.end() ? margin : it->second;
+  }
+  double coeffOf(int a, int b) const
+  {
+    const auto it = pair_coeff.find(key(a, b));
+    return it == pair_coeff.end() ? coeff : it->second;
+  }
+  bool hasZeroCoeff(int a, int b) const { return zero_coeff.count(key(a, b)) != 0; }
 };
 
 // A contact between a robot link sphere (link_ids[0], active) and a scene
@@ -66,6 +89,8 @@ struct Contact
   double cc_time_b = 0;
   int cc_type_b = 0;
   bool self() const { return sphere_b >= 0; }
+  // the contact's link pair in CollisionModel's key space
+  int other() const { return self() ? link_b : CollisionModel::kScenePair + prim; }
 };
 
 void spherePrimDistance(const double c[3], double r, const double* prim, double& dist, double n[3],
@@ -96,8 +121,9 @@ void contactExpression(const CollisionModel& cm, const Contact& ct, const double
 
 // collision term k of the descriptor: 0 = the coll_* fields, k >= 1 = coll_extra[k - 1]
 thip_coll_term collisionTerm(const thip_problem_desc& d, int k);
-std::shared_ptr<CollisionModel> collisionModel(const thip_problem_desc& d, const thip_coll_term& t,
-                                               const double* scene);
+// the model of collision term `term` (0: the coll_* term, 1 + x: coll_extra[x]),
+// with that term's link-pair data (desc.coll_pairs)
+std::shared_ptr<CollisionModel> collisionModel(const thip_problem_desc& d, int term, const double* scene);
 // CollisionTermInfo::hatch for collision term k: one term object per unit
 void addCollisionTerms(TrajProblem& tp, const std::vector<VarVector>& rows, const thip_problem_desc& d,
                        const double* scene, int term = 0);

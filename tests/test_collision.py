@@ -286,3 +286,83 @@ def test_self_collision_dual_arm_rows(oracle_mod):
             assert np.any(np.abs(a[:7]) > 1e-6) and np.any(np.abs(a[7:]) > 1e-6)  # both arms
             checked += 1
     assert checked > 0
+
+
+def _row_keys(rows, desc):
+    """(link, other) of each contact row: other is the primitive, or -1 - the
+    second sphere's link for a self contact."""
+    out = []
+    for r in rows:
+        p = int(r[2])
+        out.append((int(r[1]), p if p >= 0 else -1 - desc.sphere_link[-1 - p]))
+    return out
+
+
+def test_pair_data_rows(oracle_mod):
+    """Per link-pair margins and coefficients (CollisionTermInfo "pairs",
+    problem_description.cpp:1686-1719): a pair's contacts are those within its
+    own margin + buffer (the contact manager's pair margin after
+    incrementCollisionMargin), a zero-coefficient pair has none (hasZeroCoeff),
+    and every other pair's contacts are unchanged."""
+    base = problems.make_workload("C", 8)
+    wl = problems.with_pair_data(problems.make_workload("C", 8))
+    d = wl.desc
+    over = problems.pair_overrides(d)
+    buf = d.coll_buffer
+    grown = shrunk = 0
+    for b in range(wl.batch):
+        for x in (wl.init[b], wl.init[b] + 0.05 * np.sin(np.arange(wl.n_steps))[:, None]):
+            rp = oracle_mod.collision_rows(wl, b, x)
+            r0 = oracle_mod.collision_rows(base, b, x)
+            kp, k0 = _row_keys(rp, d), _row_keys(r0, d)
+            for r, k in zip(rp, kp):
+                m, cf = over.get(k, (d.coll_margin, d.coll_coeff))
+                assert abs(cf) > 1e-6, f"zero-coefficient pair {k} kept a contact"
+                assert r[5] < m + buf
+            keep = [i for i, k in enumerate(k0) if k not in over]
+            keepp = [i for i, k in enumerate(kp) if k not in over]
+            np.testing.assert_array_equal(rp[keepp], r0[keep])
+            for k, (m, _) in over.items():
+                dp = sorted(r[5] for r, kk in zip(rp, kp) if kk == k)
+                d0 = sorted(r[5] for r, kk in zip(r0, k0) if kk == k)
+                # the pair's contacts: the base contacts within its own margin + buffer, plus
+                # (wider margin) the base candidates between the two thresholds
+                assert [v for v in d0 if v < m + buf] == [v for v in dp if v < d.coll_margin + buf]
+                grown += len(dp) > len(d0)
+                shrunk += len(dp) < len(d0)
+    assert grown > 0 and shrunk > 0
+
+
+def test_pair_data_equal_to_term_is_identity(oracle_mod):
+    """Entries carrying the term's own margin and coefficient change nothing:
+    the oracle's solve is bitwise the one without them."""
+    base = problems.make_workload("C", 6)
+    wl = problems.make_workload("C", 6)
+    d = wl.desc
+    links = sorted({d.sphere_link[s] for s in range(d.n_spheres)})
+    for p in range(3):
+        problems.add_coll_pair(d, links[-1], 5 + p, d.coll_margin, d.coll_coeff)
+    x0, r0 = oracle_mod.solve(base, n_threads=6)
+    x1, r1 = oracle_mod.solve(wl, n_threads=6)
+    np.testing.assert_array_equal(x0, x1)
+    assert [r.status for r in r0] == [r.status for r in r1]
+
+
+def test_pair_coefficients_enter_the_problem(oracle_mod):
+    """A pair's coefficient weights its contacts' hinge terms (CollisionCost::
+    convex / value, collision_terms.cpp:1267-1306): with the wrist's scene pairs
+    10x heavier the oracle's solutions move, and reverting the entries to the
+    term's coefficient restores them bitwise."""
+    wl0 = problems.make_workload("C", 4)
+    wl1 = problems.make_workload("C", 4)
+    wl2 = problems.make_workload("C", 4)
+    links = sorted({wl1.desc.sphere_link[s] for s in range(wl1.desc.n_spheres)})
+    for p in range(wl1.desc.n_prims):
+        problems.add_coll_pair(wl1.desc, links[-1], p, wl1.desc.coll_margin, 10 * wl1.desc.coll_coeff)
+        problems.add_coll_pair(wl2.desc, links[-1], p, wl2.desc.coll_margin, 10 * wl2.desc.coll_coeff)
+        problems.add_coll_pair(wl2.desc, links[-1], p, wl2.desc.coll_margin, wl2.desc.coll_coeff)
+    x0, _ = oracle_mod.solve(wl0, n_threads=4)
+    x1, _ = oracle_mod.solve(wl1, n_threads=4)
+    x2, _ = oracle_mod.solve(wl2, n_threads=4)
+    assert np.abs(x1 - x0).max() > 1e-4
+    np.testing.assert_array_equal(x2, x0)

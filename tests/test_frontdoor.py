@@ -112,9 +112,6 @@ def _coll_pairs(pairs):
         (_doc(costs=[{"type": "collision", "params": _coll_pairs([{"link": "r_forearm_link", "pair": ["table"],
                                                                     "dist_pen": 0.025}])}]),
          "missing field: coeffs"),
-        (_doc(costs=[{"type": "collision", "params": _coll_pairs([{"link": "r_forearm_link", "pair": ["table"],
-                                                                    "coeffs": 10, "dist_pen": 0.025}])}]),
-         "per link-pair collision margins / coeffs (\"pairs\") that differ from the term's is not supported"),
     ],
 )
 def test_json_errors_match_reference(text, needle):
@@ -123,17 +120,43 @@ def test_json_errors_match_reference(text, needle):
     assert needle in str(ei.value), str(ei.value)
 
 
-def test_uniform_pairs_lower_to_the_term():
-    """A "pairs" override (problem_description.cpp:1686-1719) equal to the
-    term's coeffs / dist_pen changes no pair's margin or coefficient, so the
-    problem lowers exactly as without it."""
+def test_pairs_naming_nothing_lower_to_the_term():
+    """A "pairs" entry whose names are no link of the group and no scene object
+    can be in no contact: the problem lowers exactly as without it."""
     base = _doc(costs=[{"type": "collision", "params": {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 2}}])
     same = _doc(costs=[{"type": "collision", "params": _coll_pairs(
-        [{"link": "r_forearm_link", "pair": ["table", "box"], "coeffs": 20, "dist_pen": 0.025}])}])
+        [{"link": "r_forearm_link", "pair": ["table", "box"], "coeffs": 10, "dist_pen": 0.04}])}])
     d0, i0, _, _ = host.lower_json(base)
     d1, i1, _, _ = host.lower_json(same)
     assert bytes(d0) == bytes(d1)
     np.testing.assert_array_equal(i0, i1)
+
+
+def test_pairs_lower_to_link_pair_data():
+    """CollisionTermInfo "pairs" (problem_description.cpp:1686-1719): every
+    (link, pair[i]) becomes one link-pair entry with that entry's coeffs and
+    dist_pen -- a robot link against a scene object (the caller's primitive p is
+    scene_<p>; either side may name it) or against another robot link; a later
+    entry for the same unordered pair replaces the earlier one (insert_or_assign);
+    names outside the model are dropped."""
+    prims = np.zeros((3, 16))
+    prims[:, 0] = abi.PRIM_SPHERE
+    prims[:, 1:4] = [[0.6, -0.2, 0.8], [0.5, 0.1, 0.9], [0.7, 0.0, 0.7]]
+    prims[:, 4] = 0.1
+    pairs = [{"link": "r_wrist_flex_link", "pair": ["scene_1", "r_shoulder_pan_link", "nothing"], "coeffs": 7,
+              "dist_pen": 0.04},
+             {"link": "scene_2", "pair": ["r_forearm_roll_link"], "coeffs": 0, "dist_pen": 0.1},
+             {"link": "r_shoulder_pan_link", "pair": ["r_wrist_flex_link"], "coeffs": 9, "dist_pen": 0.05}]
+    text = _doc(costs=[{"type": "collision", "params": _coll_pairs(pairs)}])
+    d, _, _, _ = host.lower_json(text, prims)
+    assert d.n_coll_pairs == 3
+    e = [d.coll_pairs[k] for k in range(3)]
+    wrist = e[0].link
+    assert (e[0].term, e[0].other, e[0].margin, e[0].coeff) == (0, 1, 0.04, 7.0)
+    assert (e[1].term, e[1].other, e[1].margin, e[1].coeff) == (0, 2, 0.1, 0.0) and e[1].link not in (0, wrist)
+    # the self pair: replaced by the last entry, (shoulder_pan, wrist_flex)
+    assert e[2].other < 0 and -1 - e[2].other == wrist and (e[2].margin, e[2].coeff) == (0.05, 9.0)
+    assert any(d.self_pair[k][0] == e[2].link and d.self_pair[k][1] == wrist for k in range(d.n_self_pairs))
 
 
 def test_init_info_types():

@@ -482,6 +482,92 @@ def test_sqp_parity_collision_constraint(oracle_mod):
     check_parity(wl, oracle_mod, x, res, label="C-cnt")
 
 
+def test_collision_rows_parity_pairs(oracle_mod):
+    """Per link-pair margins and coefficients (CollisionTermInfo "pairs",
+    problem_description.cpp:1686-1719; thip_coll_pair): the fused kernel's and
+    the device evaluator's contact rows -- each pair's own contact distance, a
+    zero-coefficient pair dropped, a self pair with its own margin -- against the
+    oracle at the initial and the solved trajectories."""
+    from trajopt_amd.runtime import TermEvaluator
+
+    wl = problems.with_pair_data(problems.make_workload("C", 16))
+    assert wl.desc.n_coll_pairs == 5
+    xo, _ = oracle_mod.solve(wl, n_threads=16)
+    s = BatchTrustRegionSQP(wl)
+    rows = {"init": s.collision_rows(wl.init), "solution": s.collision_rows(xo)}
+    s.close()
+    ev = TermEvaluator(wl)
+    try:
+        recs = {"init": ev.collision(0, wl.init), "solution": ev.collision(0, xo)}
+    finally:
+        ev.close()
+    n = 0
+    for tag, x in (("init", wl.init), ("solution", xo)):
+        for b in range(wl.batch):
+            rc = oracle_mod.collision_rows(wl, b, x[b])
+            _check_rows(rows[tag][b], rc, f"problem {b} ({tag})")
+            _check_rows(recs[tag][b], rc, f"eval problem {b} ({tag})")
+            n += len(rc)
+    assert n > 100
+
+
+def test_sqp_parity_collision_pairs(oracle_mod):
+    """SQP parity with per link-pair data on the collision cost (hinge rows with
+    their pair's margin in the bound and coefficient in the objective) and on
+    the collision constraint (the pair's coefficient scales its row,
+    exprMult(margin - dist, coeff), collision_terms.cpp:1347-1386)."""
+    wl = problems.with_pair_data(problems.make_workload("C", 32, first_problem=96))
+    x, res, _ = solve_gpu(wl)
+    assert all(r.flags == 0 for r in res)
+    check_parity(wl, oracle_mod, x, res, label="C-pairs")
+    wl = problems.with_pair_data(problems.make_workload("C", 16, first_problem=160))
+    wl.desc.coll_is_cnt = 1
+    x, res, _ = solve_gpu(wl)
+    assert all(r.flags == 0 for r in res)
+    check_parity(wl, oracle_mod, x, res, label="C-cnt-pairs")
+
+
+def test_frontdoor_json_pairs_parity(oracle_mod):
+    """JSON problems whose collision term carries "pairs" (robot link against a
+    scene object named scene_<p>, a zero coefficient, a self pair) through the
+    C++ front door onto the fused kernel, against the oracle on the lowered
+    problems; and the same problems with a second collision term (the generic
+    host loop: device-evaluated collision terms with per-record pair data)."""
+    import json as _json
+
+    from trajopt_amd import host
+
+    wl0 = problems.make_workload("C", 4)
+    texts = []
+    for b in range(4):
+        doc = _json.loads(host.workload_to_json(wl0, b))
+        for t in doc["costs"]:
+            if t["type"] == "collision":
+                t["params"]["pairs"] = [
+                    {"link": "r_wrist_roll_link", "pair": ["scene_1", "scene_2"], "coeffs": 40, "dist_pen": 0.04},
+                    {"link": "scene_0", "pair": ["r_forearm_roll_link"], "coeffs": 0, "dist_pen": 0.02},
+                    {"link": "r_shoulder_pan_link", "pair": ["r_wrist_flex_link"], "coeffs": 5, "dist_pen": 0.03}]
+        texts.append(_json.dumps(doc))
+    scenes = np.ascontiguousarray(wl0.scene[:, :3])
+    x, res = host.solve_json_batch(texts, scenes)
+    wl = _lowered_workload(texts, scenes)
+    assert wl.desc.n_coll_pairs == 4
+    check_parity(wl, oracle_mod, x, res, label="json-pairs")
+    # a second collision term (a constraint with pairs of its own): the host loop
+    texts2 = []
+    for t in texts:
+        doc = _json.loads(t)
+        doc["constraints"].append({"type": "collision", "params": {
+            "coeffs": 10, "dist_pen": 0.01, "evaluator_type": 2,
+            "pairs": [{"link": "r_wrist_roll_link", "pair": ["scene_1"], "coeffs": 3, "dist_pen": 0.0}]}})
+        texts2.append(_json.dumps(doc))
+    x2, res2 = host.solve_json_batch(texts2[:2], scenes[:2])
+    wl2 = _lowered_workload(texts2[:2], scenes[:2])
+    assert wl2.desc.n_coll_extra == 1 and wl2.desc.n_coll_pairs == 5
+    assert host.last_batch_qp_stats()[1] > 0  # the host loops ran
+    check_parity(wl2, oracle_mod, x2, res2, label="json-pairs-generic")
+
+
 def _variant(name):
     if name == "jointvel_only":
         return _jv(6)

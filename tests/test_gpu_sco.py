@@ -210,3 +210,37 @@ def test_joint_terms_batched_host_loops(sco_lib, oracle_mod, name):
     jpt = np.stack([p[3] for p in parts]) if desc.n_jpos else None
     wl = Workload("json", desc, init, np.zeros((32, 0, 12)), np.zeros((32, 0, 16)), init.copy(), jpt)
     check_parity(wl, oracle_mod, x, res, label=f"batched-{name}")
+
+
+def test_host_loop_batch_larger_than_worker_pool(sco_lib):
+    """A host-loop batch runs on a bounded pool of worker threads: 12 problems
+    on 3 workers (each takes the next problem when its current one ends) give
+    bitwise the trajectories and statuses of the same batch with one worker
+    per problem -- a QP's result does not depend on the QPs it launches with."""
+    import copy
+    import json
+
+    text, _ = joint_terms.PROBLEMS[BATCHED[0]]
+    doc = json.loads(text)
+    rng = np.random.default_rng(5)
+    chain = host.lower_json(text)[0].chain
+    lo, hi = np.array(chain.lower[:7]) + 1e-3, np.array(chain.upper[:7]) - 1e-3
+    texts = [text]
+    for _ in range(11):
+        d = copy.deepcopy(doc)
+        d["init_info"] = {"type": "given_traj",
+                          "data": np.clip(0.02 * rng.standard_normal((joint_terms.STEPS, 7)), lo, hi).tolist()}
+        if "dt" in doc["init_info"]:
+            d["init_info"]["dt"] = doc["init_info"]["dt"]
+        texts.append(json.dumps(d))
+    try:
+        host.set_host_loop_workers(3)
+        x3, r3 = host.solve_json_batch(texts)
+        _, qps3 = host.last_batch_qp_stats()
+    finally:
+        host.set_host_loop_workers(0)
+    x12, r12 = host.solve_json_batch(texts)
+    _, qps12 = host.last_batch_qp_stats()
+    assert [r.status for r in r3] == [r.status for r in r12]
+    assert np.array_equal(x3, x12)
+    assert qps3 == qps12

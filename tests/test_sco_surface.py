@@ -134,11 +134,12 @@ def test_time_front_door_errors(built, edit, msg):
 
 
 
-def test_gpu_model_capacity_is_an_error_not_a_qp_failure(built):
-    """GpuModel refuses a convex subproblem beyond the KKT capacity
-    (n + m > THIP_QP_MAX_KKT) with the limit named, before touching the device,
-    instead of returning CVX_FAILED (which would shrink the trust box and retry
-    the same impossible QP, then write /tmp/fail.lp)."""
+def test_gpu_model_capacity_is_a_failed_solve(built, capfd):
+    """GpuModel answers a convex subproblem beyond the KKT capacity
+    (n + m > THIP_QP_MAX_KKT) with CVX_FAILED before touching the device, the
+    limit named on stderr: the reference's failure handling (trust-box shrink
+    and retry, then /tmp/fail.lp and OPT_FAILED, optimizers.cpp:790-822) then
+    applies to that problem alone, and a batch's other problems go on."""
     import ctypes as C
 
     from trajopt_amd import abi
@@ -150,4 +151,6 @@ def test_gpu_model_capacity_is_an_error_not_a_qp_failure(built):
     counts = (C.c_int * 5)()
     err = C.create_string_buffer(2048)
     rc = L.sco_case_run(9, 0, x.ctypes.data_as(C.POINTER(C.c_double)), 8, counts, None, err, 2048)
-    assert rc != 0 and "THIP_QP_MAX_KKT" in err.value.decode(), err.value.decode()
+    assert rc == 0, err.value.decode()
+    assert counts[1] == 2  # sco::CVX_FAILED
+    assert "THIP_QP_MAX_KKT" in capfd.readouterr().err

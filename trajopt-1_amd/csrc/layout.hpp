@@ -286,6 +286,9 @@ struct Tables
   int* self_sa;
   int* self_sb;
   int* self_kp;
+  // per link-pair margins and coefficients of the collision term (pair_data.hpp:
+  // [n_spheres][n_prims + n_spheres][2]); null: every pair takes coll_margin / coll_coeff
+  const double* pair_mc;
 };
 
 struct KernelArgs

@@ -1278,7 +1278,7 @@ struct thip_qp
   bool resident = false;
 };
 
-static std::string g_qp_create_err;
+static thread_local std::string g_qp_create_err;
 
 extern "C" {
 

@@ -684,6 +684,29 @@ __device__ __forceinline__ void self_candidate(const Ctx& c, const CollStage& S,
     cta = ctb = (i == 0) ? 1 : ((i == last) ? 2 : 3);
 }
 
+// (margin, coeff) of the contact between robot sphere s and scene primitive p
+// (p >= 0) or robot sphere -1 - p: the per link-pair tables (pair_data.hpp,
+// CollisionMarginData / CollisionCoeffData, collision_terms.cpp:243-386) or
+// the term's own dist_pen / coeffs.  A dropped pair (zero coefficient) reads
+// margin -inf: no distance is below margin + buffer.
+__device__ __forceinline__ double2 pair_mc(const Ctx& c, int s, int p)
+{
+  if (!c.T.pair_mc)
+    return make_double2(c.d->coll_margin, c.d->coll_coeff);
+  const int P = c.d->n_prims, W = P + c.d->n_spheres;
+  const double* e = c.T.pair_mc + 2 * (s * W + (p >= 0 ? p : P + (-1 - p)));
+  return make_double2(e[0], e[1]);
+}
+
+// (margin, coeff) of collision hinge row h (its contact's sphere and primitive)
+__device__ __forceinline__ double2 row_pair_mc(const Ctx& c, int h)
+{
+  if (!c.T.pair_mc)
+    return make_double2(c.d->coll_margin, c.d->coll_coeff);
+  const int* CT = c.ia(I_CONT);
+  return pair_mc(c, CT[3 * h + 1], CT[3 * h + 2]);
+}
+
 template <int PASS>
 __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
 {
@@ -691,8 +714,9 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
   const Layout& L = c.L;
   const int D = L.D, ns = c.d->n_spheres, P = c.d->n_prims;
   const thip_chain& ch = g_chain;
-  const double margin = c.d->coll_margin, buffer = c.d->coll_buffer, coeff = c.d->coll_coeff;
-  const double threshold = margin + buffer;  // contact distance after incrementCollisionMargin(buffer)
+  // per candidate: the pair's margin and coefficient (pair_mc), contact distance
+  // margin + buffer after incrementCollisionMargin(buffer)
+  const double buffer = c.d->coll_buffer;
   // the rank pass at the point the count pass just scanned reads the hits it
   // recorded (I_HBITS) instead of recomputing every candidate's distance
   const bool use_bits = (PASS == 1) && c.s->hbits_x;
@@ -805,6 +829,8 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
           double prim[16];
           for (int e = 0; e < 16; ++e)
             prim[e] = S.scene[16 * p + e];
+          const double2 mc = pair_mc(c, s, p);
+          const double margin = mc.x, coeff = mc.y, threshold = margin + buffer;
           double dist = 0.0;
           bool hit = false;
           int cct = 3;  // CCType of the robot link: 1 Time0, 2 Time1, 3 Between
@@ -849,11 +875,15 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
         if (__builtin_amdgcn_readfirstlane(q - c.lane) >= nself)
           break;
         bool hit = false;
-        double dist = 0.0;
+        double dist = 0.0, margin = 0.0, coeff = 0.0;
         if (q < nself)
         {
           int i, sa, sb, cta, ctb;
           self_candidate(c, S, SCR, ns, nseg, last, cont, q, i, sa, sb, dist, cta, ctb);
+          const double2 mc = pair_mc(c, sa, -1 - sb);
+          margin = mc.x;
+          coeff = mc.y;
+          const double threshold = margin + buffer;
           hit = dist < threshold && !(dist > margin + buffer);
           if (hit && (f0 || f1))
             hit = (f0 && (cta != 1 || ctb != 1)) || (f1 && (cta != 2 || ctb != 2));
@@ -890,7 +920,7 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
     {
       const int cand = c0 + c.lane;
       bool hit = false;
-      double dist = 0.0;
+      double dist = 0.0, margin = 0.0, coeff = 0.0;
       int i = 0, s = 0, p = 0;
       if (cand >= scene_total)
       {
@@ -900,6 +930,10 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
           int cta, ctb;
           self_candidate(c, S, SCR, ns, nseg, last, cont, cand - scene_total, i, s, p, dist, cta, ctb);
           p = -1 - p;
+          const double2 mc = pair_mc(c, s, p);
+          margin = mc.x;
+          coeff = mc.y;
+          const double threshold = margin + buffer;
           if (use_bits)
             hit = (HB[cand >> 5] >> (cand & 31)) & 1u;
           else
@@ -953,6 +987,10 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
         double prim[16];
         for (int e = 0; e < 16; ++e)
           prim[e] = S.scene[16 * p + e];
+        const double2 mc = pair_mc(c, s, p);
+        margin = mc.x;
+        coeff = mc.y;
+        const double threshold = margin + buffer;
         const double* cp = SCR + (i * ns + s) * 3;
         const double ctr[3] = { cp[0], cp[1], cp[2] };
         double n[3], pr[3];
@@ -1724,13 +1762,10 @@ __device__ void build_and_scale(Ctx& c)
     // static rows (kind 1) are stored as the affine expression itself: addHinge(aff, 1) for
     // costs, cntsToCosts' addHinge(aff, mu) for constraints
     const int *HTq = c.ia(I_HT), *HKDq = c.ia(I_HKIND), *HSLq = c.ia(I_HSLOT);
+    FOR(e, nh * 2 * D)
     {
-      const double cf = c.d->coll_coeff;
-      FOR(e, nh * 2 * D)
-      {
-        const int h = e / (2 * D);
-        HC[e] = HKDq[h] ? HC0[e] : (L.coll_cnt ? (-HC0[e]) * cf : -HC0[e]);
-      }
+      const int h = e / (2 * D);
+      HC[e] = HKDq[h] ? HC0[e] : (L.coll_cnt ? (-HC0[e]) * row_pair_mc(c, h).y : -HC0[e]);
     }
     FOR(h, nh)
     {
@@ -1740,7 +1775,7 @@ __device__ void build_and_scale(Ctx& c)
         Q[col] = HSLq[h] >= 0 ? MU[HSLq[h]] : 1.0;
       else
         Q[col] = L.coll_cnt ? MU[L.coll_cost0 + c.T.coll_slot[HTq[h] + (L.coll_single ? c.ia(I_CONT)[3 * h] : 0)]]
-                            : c.d->coll_coeff;
+                            : row_pair_mc(c, h).y;
       DS[col] = 1.0;
       BS[col] = 1.0;
     }
@@ -4910,8 +4945,10 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
       if (c.ia(I_HKIND)[idx])
         up = -c.a(A_HK)[idx];  // affine row aff - h <= 0
       else
-        up = L.coll_cnt ? -((c.d->coll_margin - c.a(A_HK)[idx]) * c.d->coll_coeff)
-                        : -(c.d->coll_margin - c.a(A_HK)[idx]);
+      {
+        const double2 mc = row_pair_mc(c, idx);
+        up = L.coll_cnt ? -((mc.x - c.a(A_HK)[idx]) * mc.y) : -(mc.x - c.a(A_HK)[idx]);
+      }
     }
     else
     {
@@ -5538,12 +5575,13 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
               const double *HC0 = c.a(A_HC0), *HKv = c.a(A_HK);
               const int* HMv = c.ia(I_HMASK);
               const int* HKD = c.ia(I_HKIND);
-              const double cf = c.d->coll_coeff;
               for (int h = h0; h < h1; ++h)
               {
                 if (HKD[h] || other(h))
                   continue;
-                double a = (c.d->coll_margin - HKv[h]) * cf;
+                const double2 mc = row_pair_mc(c, h);
+                const double cf = mc.y;
+                double a = (mc.x - HKv[h]) * cf;
                 for (int e = 0; e < 2 * D; ++e)
                   if (HMv[h] & (1 << e))
                     a += ((-HC0[h * 2 * D + e]) * cf) * SX[(t + e / D) * D + e % D];
@@ -5556,7 +5594,7 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
               const int* HKD = c.ia(I_HKIND);
               for (int h = h0; h < h1; ++h)
                 if (!HKD[h] && !other(h))
-                  v += c.d->coll_coeff * SX[L.nc_base + h];
+                  v += row_pair_mc(c, h).y * SX[L.nc_base + h];
               mcost[L.coll_cost0 + slot] = v;
             }
           }

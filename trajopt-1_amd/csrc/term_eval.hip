@@ -34,6 +34,7 @@
 
 #include "collision_device.hpp"
 #include "kin_device.hpp"
+#include "pair_data.hpp"
 #include "self_pairs.hpp"
 
 namespace thip
@@ -49,7 +50,17 @@ struct CollTerm
   int single;      // DISCRETE: one state per unit
   int continuous;  // LVS_CONTINUOUS: casts between consecutive sub-states
   double margin, buffer, lvs;
+  // per link-pair margins (pair_data.hpp, [n_spheres][pw][2]; null: `margin` for every pair)
+  const double* pmc;
+  int pw;
 };
+
+// the contact distance margin of robot sphere s against primitive p (p >= 0)
+// or robot sphere -1 - p (CollisionMarginData, collision_terms.cpp:243-332)
+__device__ __forceinline__ double pair_margin(const CollTerm& tm, int n_prims, int s, int p)
+{
+  return tm.pmc ? tm.pmc[2 * (s * tm.pw + (p >= 0 ? p : n_prims + (-1 - p)))] : tm.margin;
+}
 
 // per-term unit table: unit u covers waypoint t0 (and t0 + 1 unless single);
 // f0 / f1: the ends that are fixed steps of the term
@@ -230,7 +241,6 @@ __global__ __launch_bounds__(kEvBlock) void coll_eval_kernel(const thip_chain* c
   const int n_sub = tm.single ? 1 : (tm.continuous ? cnt - 1 : cnt);
   const int last = cnt - 1;
   const double dt = tm.single ? 0.0 : 1.0 / double(last);
-  const double threshold = tm.margin + tm.buffer;
   const Spheres& S = *sph;
   const int n_sph = [&] {
     int n = 0;
@@ -356,7 +366,10 @@ __global__ __launch_bounds__(kEvBlock) void coll_eval_kernel(const thip_chain* c
           cc_type[0] = cc_type[1] = (i == 0) ? kCCTime0 : ((i == last) ? kCCTime1 : kCCBetween);
         }
       }
-      hit = (dist < threshold) && !(dist > tm.margin + tm.buffer);
+      // the pair's contact distance after incrementCollisionMargin(buffer)
+      const double margin = pair_margin(tm, n_prims, s, p);
+      const double threshold = margin + tm.buffer;
+      hit = (dist < threshold) && !(dist > margin + tm.buffer);
       // removeInvalidContactResults: at a fixed end keep a contact when one of its active
       // sides is not at that end (a scene primitive's side is CCType_None)
       if (hit && (un.f0 || un.f1))
@@ -505,6 +518,7 @@ struct thip_eval
   // per collision term: its unit table (offset into d_units) and kernel parameters
   std::vector<int> unit_off, unit_n;
   std::vector<CollTerm> terms;
+  std::vector<double*> d_pair;  // per term: its pair table (pair_data.hpp) or null
   int max_units = 0;
   hipStream_t stream = nullptr;
   bool uploaded = false;
@@ -599,6 +613,11 @@ int thip_eval_create(int device, const thip_problem_desc* desc, int batch, thip_
       (desc->n_spheres < 1 || desc->n_spheres > THIP_MAX_SPHERES || desc->n_prims < 0 ||
        desc->n_prims > THIP_MAX_PRIMS))
     return reject("collision: spheres / primitives out of range");
+  {
+    const std::string why = thip::validate_coll_pairs(*desc);
+    if (!why.empty())
+      return reject(why);
+  }
   for (int s = 0; s < (desc->coll_enabled || desc->n_coll_extra > 0 ? desc->n_spheres : 0); ++s)
     if (desc->sphere_link[s] < 1 || desc->sphere_link[s] >= ch.n_links || !(desc->sphere_radius[s] >= 0))
       return reject("collision: bad robot sphere");
@@ -625,6 +644,8 @@ int thip_eval_create(int device, const thip_problem_desc* desc, int batch, thip_
     tm.margin = main ? d.coll_margin : x->margin;
     tm.buffer = main ? d.coll_buffer : x->buffer;
     tm.lvs = main ? d.coll_lvs : x->lvs;
+    tm.pmc = nullptr;
+    tm.pw = d.n_prims + d.n_spheres;
     const int nf = main ? d.coll_n_fixed : x->n_fixed;
     if (cont < 0 || cont > 2 || nf < 0 || nf > THIP_MAX_STEPS || (!tm.single && !(tm.lvs > 0)) || !(tm.buffer >= 0))
     {
@@ -719,6 +740,21 @@ int thip_eval_create(int device, const thip_problem_desc* desc, int batch, thip_
       (e = hipMemsetAsync(ev->d_scene, 0, B * np * 16 * sizeof(double), ev->stream)) != hipSuccess ||
       (e = hipStreamSynchronize(ev->stream)) != hipSuccess)
     return hfail("hipMemcpy", e);
+  // per link-pair margins of each collision term (coefficients are the host's)
+  for (size_t k = 0; k < ev->terms.size(); ++k)
+  {
+    std::vector<double> tab;
+    double* dp = nullptr;
+    if (thip::coll_pair_table(d, static_cast<int>(k), tab))
+    {
+      if ((e = hipMalloc(&dp, tab.size() * sizeof(double))) != hipSuccess)
+        return hfail("hipMalloc(pair table)", e);
+      ev->d_pair.push_back(dp);
+      if ((e = hipMemcpy(dp, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+        return hfail("hipMemcpy(pair table)", e);
+      ev->terms[k].pmc = dp;
+    }
+  }
   *out = ev;
   return THIP_OK;
 }
@@ -881,6 +917,8 @@ void thip_eval_destroy(thip_eval* ev)
   hipFree(ev->d_out);
   hipFree(ev->d_counts);
   hipFree(ev->d_units);
+  for (double* dp : ev->d_pair)
+    hipFree(dp);
   if (ev->stream)
     hipStreamDestroy(ev->stream);
   delete ev;

@@ -16,6 +16,7 @@
 #include <functional>
 
 #include "layout.hpp"
+#include "pair_data.hpp"
 #include "self_pairs.hpp"
 
 namespace thip
@@ -40,6 +41,7 @@ struct thip_ctx
   thip_problem_desc* d_desc = nullptr;
   int* d_tables = nullptr;
   double* d_tables_f = nullptr;
+  double* d_pair = nullptr;  // per link-pair collision margins / coefficients (pair_data.hpp), or null
   Tables T{};
   double* d_ws = nullptr;
   int* d_iws = nullptr;
@@ -264,6 +266,11 @@ static int validate(const thip_problem_desc* d, std::string& why)
   {
     std::vector<int> sa, sb, kp;
     const std::string w = self_sphere_pairs(*d, sa, sb, kp);
+    if (!w.empty())
+      return why = w, THIP_E_INVALID;
+  }
+  {
+    const std::string w = validate_coll_pairs(*d);
     if (!w.empty())
       return why = w, THIP_E_INVALID;
   }
@@ -915,6 +922,17 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   T.self_sb = ctx->d_tables + o_ssb;
   T.self_kp = ctx->d_tables + o_skp;
   T.row_w = ctx->d_tables_f;
+  T.pair_mc = nullptr;
+  {
+    std::vector<double> ptab;
+    if (L.coll && coll_pair_table(d, 0, ptab))
+    {
+      if ((e = hipMalloc(&ctx->d_pair, ptab.size() * sizeof(double))) != hipSuccess ||
+          (e = hipMemcpy(ctx->d_pair, ptab.data(), ptab.size() * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(std::string("hipMalloc(pair table): ") + hipGetErrorString(e));
+      T.pair_mc = ctx->d_pair;
+    }
+  }
   const size_t B = static_cast<size_t>(batch);
   if ((e = hipMalloc(&ctx->d_ws, B * static_cast<size_t>(L.dstride) * sizeof(double))) != hipSuccess ||
       (e = hipMalloc(&ctx->d_iws, B * static_cast<size_t>(L.istride) * sizeof(int))) != hipSuccess ||
@@ -1363,6 +1381,7 @@ void thip_destroy(thip_ctx* ctx)
   hipFree(ctx->d_desc);
   hipFree(ctx->d_tables);
   hipFree(ctx->d_tables_f);
+  hipFree(ctx->d_pair);
   hipFree(ctx->d_ws);
   hipFree(ctx->d_iws);
   hipFree(ctx->d_res);

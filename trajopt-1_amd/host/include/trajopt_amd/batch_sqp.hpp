@@ -55,6 +55,12 @@ public:
   // host-loop batches: QP launches and QPs of the last optimize() (sco::GpuQPBatcher)
   long long qpLaunches() const { return qp_launches_; }
   long long qpSolves() const { return qp_solves_; }
+  // host-loop batches: worker threads (problems solved at once); 0 = the
+  // process default (setDefaultHostLoopWorkers, initially 64), never more
+  // than the batch
+  void setHostLoopWorkers(int n) { workers_ = n; }
+  int hostLoopWorkers() const;
+  static void setDefaultHostLoopWorkers(int n);
 
 private:
   void init(int device);
@@ -67,6 +73,7 @@ private:
   int device_ = 0;
   std::vector<sco::OptResults> generic_results_;
   long long qp_launches_ = 0, qp_solves_ = 0;
+  int workers_ = 0;
 };
 
 // One batch sharded over several HIP devices of this process (SURVEY.md §8e:

@@ -52,6 +52,10 @@ public:
     int W = 0;
     std::vector<double> rec;   // [n][W] in unit order, then ContactResultMap order
     std::vector<int> t;        // per record: the unit's (first) waypoint
+    // per record: its link pair's margin and coefficient (the term's dist_pen /
+    // coeffs unless the term's "pairs" override them: CollisionMarginData /
+    // CollisionCoeffData lookups, collision_terms.cpp:243-386)
+    std::vector<double> margin, coeff;
   };
   const Contacts& collision(int term, const DblVec& x);
 
@@ -67,6 +71,7 @@ private:
     bool valid = false;
   };
   std::vector<Cache> cache_;
+  std::vector<std::vector<double>> pair_tab_;  // per term: pair_data.hpp table, empty = the term's own
 };
 
 class CartPoseDeviceErr : public sco::VectorOfVector
@@ -120,10 +125,10 @@ struct DeviceCollisionUnit
   int term = 0;              // thip_eval collision term index
   int t = 0;                 // the unit's (first) waypoint
   sco::VarVector vars0, vars1;  // waypoint t, t + 1 (empty for DISCRETE)
-  double margin = 0, coeff = 0;
   // the unit's records at x: [first, first + n) of the term's contacts
   void records(const DblVec& x, const DeviceTermEvaluator::Contacts*& c, int& first, int& n) const;
-  sco::AffExprVector exprs(const DblVec& x) const;
+  // the distance expressions of the unit's contacts, with each contact's margin and coefficient
+  sco::AffExprVector exprs(const DblVec& x, DblVec* margins = nullptr, DblVec* coeffs = nullptr) const;
   sco::VarVector vars() const;
 };
 

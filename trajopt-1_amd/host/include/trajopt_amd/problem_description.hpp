@@ -97,6 +97,12 @@ public:
 
   std::vector<CollisionSphere> collision_spheres;      // robot collision model
   std::vector<std::array<double, 16>> scene;           // THIP_PRIM_* records
+  // the link name of each scene object (parallel to scene; a missing or empty
+  // name: "scene_<index>"), the names CollisionTermInfo "pairs" entries use
+  std::vector<std::string> scene_names;
+  void addSceneObject(const std::string& name, const std::array<double, 16>& rec);
+  std::string sceneName(std::size_t k) const;
+  int sceneIndex(const std::string& name) const;  // -1: no such scene object
   // the allowed-collision matrix (the SRDF's <disable_collisions> link pairs):
   // robot link pairs the contact manager never tests
   std::set<std::pair<std::string, std::string>> allowed_collisions;
@@ -273,7 +279,14 @@ struct CollisionTermInfo : public TermInfo
   double collision_margin_buffer = 0.5;
   double coeff = 20;             // CollisionCoeffData default
   double dist_pen = 0;           // collision margin
-  bool has_pairs = false;        // a "pairs" override differing from coeff / dist_pen
+  // "pairs" (problem_description.cpp:1686-1719): per link pair margin and
+  // coefficient overrides, in order (a later entry for a pair replaces an earlier one)
+  struct PairData
+  {
+    std::string link, other;
+    double coeff = 20, dist_pen = 0;
+  };
+  std::vector<PairData> pairs;
   CollisionTermInfo() : TermInfo(TermType::TT_COST | TermType::TT_CNT) {}
   void fromJson(ProblemConstructionInfo& pci, const Json::Value& v) override;
   void hatch(TrajOptProb& prob) override;

@@ -1,6 +1,7 @@
 #include "trajopt_amd/batch_sqp.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -131,38 +132,58 @@ BatchTrustRegionSQP::BatchTrustRegionSQP(const std::vector<TrajOptProb::Ptr>& pr
   init(device);
 }
 
+namespace
+{
+std::atomic<int> g_default_workers{ 64 };
+}
+
+void BatchTrustRegionSQP::setDefaultHostLoopWorkers(int n) { g_default_workers = n > 0 ? n : 64; }
+
+int BatchTrustRegionSQP::hostLoopWorkers() const
+{
+  const int want = workers_ > 0 ? workers_ : g_default_workers.load();
+  return std::max(1, std::min(want, batch()));
+}
+
 std::vector<sco::OptResults> BatchTrustRegionSQP::optimizeHostLoops()
 {
   const std::size_t B = generic_.size();
+  const std::size_t W = static_cast<std::size_t>(hostLoopWorkers());
   auto batcher = std::make_shared<sco::GpuQPBatcher>();
   std::vector<sco::OptResults> out(B);
   std::vector<std::string> errs(B);
-  // every client registered before any thread starts, so the first rounds batch all of them
+  // one batcher client per worker, all registered before any thread starts, so
+  // the first rounds batch every worker's QPs; a worker leaves when the batch
+  // has no unsolved problem left
   std::vector<std::unique_ptr<sco::GpuQPBatcherClient>> clients;
-  for (std::size_t b = 0; b < B; ++b)
+  for (std::size_t w = 0; w < W; ++w)
     clients.push_back(std::make_unique<sco::GpuQPBatcherClient>(batcher));
+  std::atomic<std::size_t> next{ 0 };
   std::vector<std::thread> threads;
-  threads.reserve(B);
-  for (std::size_t b = 0; b < B; ++b)
-    threads.emplace_back([&, b]() {
-      try
+  threads.reserve(W);
+  for (std::size_t w = 0; w < W; ++w)
+    threads.emplace_back([&, w]() {
+      for (std::size_t b = next++; b < B; b = next++)
       {
-        const TrajOptProb::Ptr& prob = generic_[b];
-        BasicTrustRegionSQP opt(prob, device_);
-        auto* gm = dynamic_cast<sco::GpuModel*>(prob->getModel().get());
-        if (!gm)
-          throw std::runtime_error("BatchTrustRegionSQP: problem " + std::to_string(b) + " has no GpuModel");
-        gm->setBatcher(batcher);
-        opt.initialize(trajToDblVec(prob->GetInitTraj()));
-        opt.optimizeHostLoop();
-        out[b] = opt.results();
-        gm->setBatcher(nullptr);
+        try
+        {
+          const TrajOptProb::Ptr& prob = generic_[b];
+          BasicTrustRegionSQP opt(prob, device_);
+          auto* gm = dynamic_cast<sco::GpuModel*>(prob->getModel().get());
+          if (!gm)
+            throw std::runtime_error("BatchTrustRegionSQP: problem " + std::to_string(b) + " has no GpuModel");
+          gm->setBatcher(batcher);
+          opt.initialize(trajToDblVec(prob->GetInitTraj()));
+          opt.optimizeHostLoop();
+          out[b] = opt.results();
+          gm->setBatcher(nullptr);
+        }
+        catch (const std::exception& e)
+        {
+          errs[b] = e.what();
+        }
       }
-      catch (const std::exception& e)
-      {
-        errs[b] = e.what();
-      }
-      clients[b].reset();  // leave: the others' rounds no longer wait for this problem
+      clients[w].reset();  // leave: the others' rounds no longer wait for this worker
     });
   for (auto& t : threads)
     t.join();

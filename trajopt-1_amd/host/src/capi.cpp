@@ -38,7 +38,7 @@ trajopt::TrajOptProb::Ptr construct(const char* json_text, const double* scene, 
   {
     std::array<double, 16> rec{};
     std::copy(scene + 16 * p, scene + 16 * (p + 1), rec.begin());
-    env->scene.push_back(rec);
+    env->addSceneObject("scene_" + std::to_string(p), rec);  // the caller's primitive p
   }
   return trajopt::ConstructProblem(root, env);
 }
@@ -120,6 +120,8 @@ void thost_last_batch_qp_stats(long long* launches, long long* qps)
   if (qps)
     *qps = g_batch_qp_solves;
 }
+
+void thost_set_host_loop_workers(int n) { trajopt::BatchTrustRegionSQP::setDefaultHostLoopWorkers(n); }
 
 int thost_solve_json_batch(const char* const* json_texts, int batch, const double* scenes, int n_prims, int device,
                            double* x, thip_result* results, char* err, int err_len)

@@ -4,6 +4,7 @@
 #include <cmath>
 #include <stdexcept>
 
+#include "../../csrc/pair_data.hpp"
 #include "trajopt_amd/problem_description.hpp"
 #include "trajopt_sco/expr_ops.hpp"
 
@@ -29,6 +30,9 @@ void DeviceTermEvaluator::ensure()
                        coll && d.n_prims > 0 ? prob_->scene.data() : nullptr) != THIP_OK)
     throw std::runtime_error(std::string("thip_eval_upload: ") + thip_eval_last_error(ev_));
   cache_.assign(static_cast<std::size_t>((d.coll_enabled ? 1 : 0) + d.n_coll_extra), Cache());
+  pair_tab_.assign(cache_.size(), {});
+  for (std::size_t k = 0; k < pair_tab_.size(); ++k)
+    thip::coll_pair_table(d, static_cast<int>(k), pair_tab_[k]);
 }
 
 void DeviceTermEvaluator::cartPose(int k, const DblVec& q, double* err, double* jac)
@@ -69,8 +73,28 @@ const DeviceTermEvaluator::Contacts& DeviceTermEvaluator::collision(int term, co
   c.c.W = W;
   c.c.rec.resize(static_cast<std::size_t>(count) * W);
   c.c.t.resize(static_cast<std::size_t>(count));
+  c.c.margin.resize(static_cast<std::size_t>(count));
+  c.c.coeff.resize(static_cast<std::size_t>(count));
+  const thip_problem_desc& d = prob_->desc();
+  const std::vector<double>& tab = pair_tab_[static_cast<std::size_t>(term)];
+  const double m0 = term == 0 ? d.coll_margin : d.coll_extra[term - 1].margin;
+  const double c0 = term == 0 ? d.coll_coeff : d.coll_extra[term - 1].coeff;
   for (int r = 0; r < count; ++r)
-    c.c.t[static_cast<std::size_t>(r)] = static_cast<int>(c.c.rec[static_cast<std::size_t>(r) * W]);
+  {
+    const double* rec = c.c.rec.data() + static_cast<std::size_t>(r) * W;
+    c.c.t[static_cast<std::size_t>(r)] = static_cast<int>(rec[0]);
+    // record: [t, link, prim (or -1 - sphere b), sphere, ...]
+    double m = m0, cf = c0;
+    if (!tab.empty())
+    {
+      const int P = d.n_prims, s = static_cast<int>(rec[3]), p = static_cast<int>(rec[2]);
+      const std::size_t e = (static_cast<std::size_t>(s) * (P + d.n_spheres) + (p >= 0 ? p : P + (-1 - p))) * 2;
+      m = tab[e];
+      cf = tab[e + 1];
+    }
+    c.c.margin[static_cast<std::size_t>(r)] = m;
+    c.c.coeff[static_cast<std::size_t>(r)] = cf;
+  }
   c.q = q;
   c.valid = true;
   return c.c;
@@ -120,7 +144,7 @@ sco::VarVector DeviceCollisionUnit::vars() const
 
 // CalcDistExpressions* (collision_terms.cpp:463-554): the record's kept coefficients
 // over the unit's variables, vars0 first, and its constant
-sco::AffExprVector DeviceCollisionUnit::exprs(const DblVec& x) const
+sco::AffExprVector DeviceCollisionUnit::exprs(const DblVec& x, DblVec* margins, DblVec* coeffs) const
 {
   const DeviceTermEvaluator::Contacts* c;
   int first, n;
@@ -144,6 +168,10 @@ sco::AffExprVector DeviceCollisionUnit::exprs(const DblVec& x) const
         e.vars.push_back(vars1[static_cast<std::size_t>(j)]);
       }
     out.push_back(e);
+    if (margins)
+      margins->push_back(c->margin[static_cast<std::size_t>(r)]);
+    if (coeffs)
+      coeffs->push_back(c->coeff[static_cast<std::size_t>(r)]);
   }
   return out;
 }
@@ -155,15 +183,18 @@ double DeviceCollisionCost::value(const DblVec& x)
   u_.records(x, c, first, n);
   double out = 0;
   for (int r = first; r < first + n; ++r)
-    out += std::fmax(u_.margin - c->rec[static_cast<std::size_t>(r) * c->W + 5], 0.0) * u_.coeff;
+    out += std::fmax(c->margin[static_cast<std::size_t>(r)] - c->rec[static_cast<std::size_t>(r) * c->W + 5], 0.0) *
+           c->coeff[static_cast<std::size_t>(r)];
   return out;
 }
 
 sco::ConvexObjective::Ptr DeviceCollisionCost::convex(const DblVec& x, sco::Model* model)
 {
   auto out = std::make_shared<sco::ConvexObjective>(model);
-  for (const sco::AffExpr& e : u_.exprs(x))
-    out->addHinge(sco::exprSub(sco::AffExpr(u_.margin), e), u_.coeff);
+  DblVec margin, coeff;
+  const sco::AffExprVector ex = u_.exprs(x, &margin, &coeff);
+  for (std::size_t i = 0; i < ex.size(); ++i)
+    out->addHinge(sco::exprSub(sco::AffExpr(margin[i]), ex[i]), coeff[i]);
   return out;
 }
 
@@ -174,15 +205,19 @@ DblVec DeviceCollisionConstraint::value(const DblVec& x)
   u_.records(x, c, first, n);
   DblVec out;
   for (int r = first; r < first + n; ++r)
-    out.push_back(std::fmax(u_.margin - c->rec[static_cast<std::size_t>(r) * c->W + 5], 0.0) * u_.coeff);
+    out.push_back(std::fmax(c->margin[static_cast<std::size_t>(r)] - c->rec[static_cast<std::size_t>(r) * c->W + 5],
+                            0.0) *
+                  c->coeff[static_cast<std::size_t>(r)]);
   return out;
 }
 
 sco::ConvexConstraints::Ptr DeviceCollisionConstraint::convex(const DblVec& x, sco::Model* model)
 {
   auto out = std::make_shared<sco::ConvexConstraints>(model);
-  for (const sco::AffExpr& e : u_.exprs(x))
-    out->addIneqCnt(sco::exprMult(sco::exprSub(sco::AffExpr(u_.margin), e), u_.coeff));
+  DblVec margin, coeff;
+  const sco::AffExprVector ex = u_.exprs(x, &margin, &coeff);
+  for (std::size_t i = 0; i < ex.size(); ++i)
+    out->addIneqCnt(sco::exprMult(sco::exprSub(sco::AffExpr(margin[i]), ex[i]), coeff[i]));
   return out;
 }
 }  // namespace trajopt

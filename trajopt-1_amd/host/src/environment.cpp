@@ -173,6 +173,28 @@ Environment::Ptr Environment::makePR2()
   return env;
 }
 
+void Environment::addSceneObject(const std::string& name, const std::array<double, 16>& rec)
+{
+  scene_names.resize(scene.size());
+  scene.push_back(rec);
+  scene_names.push_back(name);
+}
+
+std::string Environment::sceneName(std::size_t k) const
+{
+  if (k < scene_names.size() && !scene_names[k].empty())
+    return scene_names[k];
+  return "scene_" + std::to_string(k);
+}
+
+int Environment::sceneIndex(const std::string& name) const
+{
+  for (std::size_t k = 0; k < scene.size(); ++k)
+    if (sceneName(k) == name)
+      return static_cast<int>(k);
+  return -1;
+}
+
 void Environment::allowCollision(const std::string& a, const std::string& b)
 {
   allowed_collisions.insert(a < b ? std::make_pair(a, b) : std::make_pair(b, a));
@@ -222,15 +244,16 @@ Environment::Ptr Environment::makeSpherebot()
   env->addJointGroup(std::move(g));
   env->collision_spheres.push_back({ "spherebot_link", { 0.0, 0.0, 0.0 }, 0.5 });
   const double centers[][3] = { { 0.0, 0.0, 0.0 }, { -0.75, 0.0, 0.0 }, { 0.0, 0.75, 0.0 } };
-  for (const auto& ctr : centers)
+  const char* names[] = { "test_sphere_link", "test_sphere_link2", "test_sphere_link3" };  // spherebot.urdf:42-105
+  for (int k = 0; k < 3; ++k)
   {
     std::array<double, 16> rec{};
     rec[0] = THIP_PRIM_SPHERE;
-    rec[1] = ctr[0];
-    rec[2] = ctr[1];
-    rec[3] = ctr[2];
+    rec[1] = centers[k][0];
+    rec[2] = centers[k][1];
+    rec[3] = centers[k][2];
     rec[4] = 0.5;
-    env->scene.push_back(rec);
+    env->addSceneObject(names[k], rec);
   }
   return env;
 }

@@ -977,11 +977,9 @@ void CollisionTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value
     throw std::runtime_error("CollisionTermInfo: invalid contact_test_type");
   json_marshal::childFromJson(params, coeff, "coeffs");
   json_marshal::childFromJson(params, dist_pen, "dist_pen");
-  // problem_description.cpp:1686-1719: per link-pair overrides, validated as the reference does.
-  // An override equal to the term's own coeffs / dist_pen leaves every pair's margin and
-  // coefficient unchanged (CollisionCoeffData / CollisionMarginData defaults), so it lowers to
-  // the term-wide values; a differing one is refused in hatch().
-  has_pairs = false;
+  // problem_description.cpp:1686-1719: per link-pair margin / coefficient overrides,
+  // validated as the reference does; lowered in hatch() (coll_pairs)
+  pairs.clear();
   if (params.isMember("pairs"))
   {
     for (const Json::Value& it : params["pairs"])
@@ -999,8 +997,8 @@ void CollisionTermInfo::fromJson(ProblemConstructionInfo& pci, const Json::Value
       double pair_coeffs = 20, pair_dist_pen = 0;
       json_marshal::childFromJson(it, pair_coeffs, "coeffs");
       json_marshal::childFromJson(it, pair_dist_pen, "dist_pen");
-      if (pair_coeffs != coeff || pair_dist_pen != dist_pen)
-        has_pairs = true;
+      for (const std::string& p : pair)
+        pairs.push_back({ link, p, pair_coeffs, pair_dist_pen });
     }
   }
   const char* all_fields[] = { "type",           "first_step",        "last_step",
@@ -1019,8 +1017,6 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
                 " (DISCRETE = 1, LVS_DISCRETE = 2, CONTINUOUS = 3, LVS_CONTINUOUS = 4 are)");
   if (contact_test_type != 2)
     unsupported("collision contact_test_type " + std::to_string(contact_test_type) + " (only ALL = 2)");
-  if (has_pairs)
-    unsupported("per link-pair collision margins / coeffs (\"pairs\") that differ from the term's");
   const auto env = prob.GetEnv();
   thip_problem_desc& d = prob.desc();
   // the first collision term lowers into the descriptor's coll_* fields (the batched
@@ -1094,8 +1090,6 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
     u.vars0 = prob.GetVarRow(i, 0, n_dof);
     if (!single)
       u.vars1 = prob.GetVarRow(i + 1, 0, n_dof);
-    u.margin = dist_pen;
-    u.coeff = coeff;
     const std::string nm = name + "_" + std::to_string(i);
     if (is_cnt)
     {
@@ -1124,11 +1118,64 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
   else
     for (int i = first_step; i < last; ++i)
       addUnit(i, false);
+  // "pairs": each named link pair's margin and coefficient for this term
+  // (CollisionMarginData::setCollisionMargin / CollisionCoeffData::setCollisionCoeff,
+  // problem_description.cpp:1707-1718), as (robot link, scene object) or (robot
+  // link, robot link) entries of the descriptor; a name that is neither a link of
+  // the group nor a scene object can be in no contact, so its entries do nothing
+  auto lowerPairs = [&]() {
+    const auto kin = prob.GetKin();
+    for (const PairData& pd : pairs)
+    {
+      const int ra = kin->linkIndex(pd.link), rb = kin->linkIndex(pd.other);
+      const int sa = env->sceneIndex(pd.link), sb = env->sceneIndex(pd.other);
+      thip_coll_pair e{};
+      e.term = term;
+      if (ra > 0 && sb >= 0)
+      {
+        e.link = ra;
+        e.other = sb;
+      }
+      else if (sa >= 0 && rb > 0)
+      {
+        e.link = rb;
+        e.other = sa;
+      }
+      else if (ra > 0 && rb > 0)
+      {
+        e.link = ra;
+        e.other = -1 - rb;
+      }
+      else
+        continue;
+      e.margin = pd.dist_pen;
+      e.coeff = pd.coeff;
+      // insert_or_assign: the pair's earlier entry of this term goes
+      for (int k = 0; k < d.n_coll_pairs; ++k)
+      {
+        thip_coll_pair& o = d.coll_pairs[k];
+        const bool same = o.term == e.term &&
+                          ((o.link == e.link && o.other == e.other) ||
+                           (e.other < 0 && o.other < 0 && o.link == -1 - e.other && -1 - o.other == e.link));
+        if (same)
+        {
+          for (int j = k + 1; j < d.n_coll_pairs; ++j)
+            d.coll_pairs[j - 1] = d.coll_pairs[j];
+          --d.n_coll_pairs;
+          break;
+        }
+      }
+      if (d.n_coll_pairs >= THIP_MAX_COLL_PAIRS)
+        unsupported("more than " + std::to_string(THIP_MAX_COLL_PAIRS) + " collision link pairs with their own data");
+      d.coll_pairs[d.n_coll_pairs++] = e;
+    }
+  };
   if (extra)
   {
     // the robot model and the scene are the environment's, shared with the first term
     if (d.n_spheres != static_cast<int>(spheres.size()) || d.n_prims != static_cast<int>(env->scene.size()))
       throw std::runtime_error("CollisionTermInfo: collision terms of one problem must share the robot model and scene");
+    lowerPairs();
     return;
   }
   d.n_spheres = static_cast<int>(spheres.size());
@@ -1166,6 +1213,7 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
       d.self_pair[d.n_self_pairs][1] = slinks[b].first;
       ++d.n_self_pairs;
     }
+  lowerPairs();
 }
 
 // ------------------------------------------------------------ ConstructProblem

@@ -1,6 +1,7 @@
 // GpuModel (see gpu_model.hpp): OSQPModel's bookkeeping and QP assembly
 // (trajopt_sco/src/osqp_interface.cpp:73-640, solver_utils.cpp:12-183),
 // solved on the GPU by thip_qp_solve.
+#include <cstdio>
 #include "trajopt_sco/gpu_model.hpp"
 
 #include <algorithm>
@@ -314,10 +315,18 @@ CvxOptStatus GpuModel::optimize()
   thip_osqp_settings s = config_.settings;
   if (allow_ws)
     s.rho = prev_rho_;
-  if (n + m > THIP_QP_MAX_KKT)  // a capacity limit, not a QP failure: no shrink-and-retry, no fail.lp
-    throw std::runtime_error("GpuModel: the convex subproblem has " + std::to_string(n) + " variables and " +
-                             std::to_string(m) + " constraints; the GPU QP solver takes n + m <= THIP_QP_MAX_KKT (" +
-                             std::to_string(THIP_QP_MAX_KKT) + ")");
+  if (n + m > THIP_QP_MAX_KKT)
+  {
+    // beyond the GPU QP solver's capacity: a failed solve, so the reference's
+    // failure handling applies to this problem alone (trust-box shrink and
+    // retry, then /tmp/fail.lp and OPT_FAILED, optimizers.cpp:790-822)
+    std::fprintf(stderr,
+                 "GpuModel: the convex subproblem has %d variables and %d constraints; the GPU QP solver takes "
+                 "n + m <= THIP_QP_MAX_KKT (%d): CVX_FAILED\n",
+                 n, m, THIP_QP_MAX_KKT);
+    prev_status_ = 0;
+    return CVX_FAILED;
+  }
   DblVec x(static_cast<std::size_t>(n)), y(static_cast<std::size_t>(std::max(m, 1)));
   const bool ws = allow_ws && static_cast<int>(prev_x_.size()) >= n && static_cast<int>(prev_y_.size()) >= m;
   if (batcher_)

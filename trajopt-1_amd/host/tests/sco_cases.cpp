@@ -7,7 +7,7 @@
 //   1, 2   solver-interface-unit.cpp:130-231 ExprMult_test2 / ExprMult_test3
 //   3, 4   small-problems-unit.cpp:49-83     QuadraticSeparable / QuadraticNonseparable
 //   5..8   small-problems-unit.cpp:111-172   TP1, TP3, TP6, TP7
-//   9      a QP beyond THIP_QP_MAX_KKT (the capacity error)
+//   9      a QP beyond THIP_QP_MAX_KKT (CVX_FAILED, before touching the device)
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -56,7 +56,7 @@ CaseOut qpCase(int id, int device)
       exprInc(obj, exprSquare(AffExpr(v)));
     solver.setObjective(obj);
     solver.update();
-    o.status = solver.optimize();  // throws: a capacity limit, not CVX_FAILED
+    o.status = solver.optimize();  // CVX_FAILED: the reference's failure handling applies
     return o;
   }
   if (id == 0)

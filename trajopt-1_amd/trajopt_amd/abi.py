@@ -10,7 +10,7 @@ import ctypes as C
 import os
 from pathlib import Path
 
-ABI_VERSION = 7  # THIP_ABI_VERSION
+ABI_VERSION = 8  # THIP_ABI_VERSION
 MAX_DOF = 16
 MAX_LINKS = 32
 MAX_STEPS = 64
@@ -25,6 +25,7 @@ MAX_TTT = 2
 MAX_COLL_EXTRA = 3
 MAX_SELF_PAIRS = 64
 MAX_SELF_SPHERE_PAIRS = 512
+MAX_COLL_PAIRS = 64
 TRACE_W = 16  # THIP_TRACE_W
 DEBUG_NO_SEGMENT, DEBUG_FORCE_WIDE, DEBUG_NO_BRANCH, DEBUG_STATIC_DISPATCH = 1, 2, 4, 8  # thip_debug_set_path flags
 
@@ -118,6 +119,18 @@ class CollTerm(C.Structure):
     ]
 
 
+class CollPair(C.Structure):
+    """thip_coll_pair: one link pair's margin and coefficient in a collision term."""
+    _fields_ = [
+        ("term", C.c_int),
+        ("link", C.c_int),
+        ("other", C.c_int),
+        ("pad_", C.c_int),
+        ("margin", C.c_double),
+        ("coeff", C.c_double),
+    ]
+
+
 class ProblemDesc(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int),
@@ -207,6 +220,8 @@ class ProblemDesc(C.Structure):
         ("coll_max_contacts", C.c_int),
         ("n_coll_extra", C.c_int),
         ("coll_extra", CollTerm * MAX_COLL_EXTRA),
+        ("n_coll_pairs", C.c_int),
+        ("coll_pairs", CollPair * MAX_COLL_PAIRS),
         ("sqp", SqpParams),
         ("osqp", OsqpSettings),
     ]

@@ -49,6 +49,8 @@ def load_host():
         L.thost_solve_json_stream.restype = C.c_int
         L.thost_last_batch_qp_stats.argtypes = [C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]
         L.thost_last_batch_qp_stats.restype = None
+        L.thost_set_host_loop_workers.argtypes = [C.c_int]
+        L.thost_set_host_loop_workers.restype = None
         L.thost_solve_json.argtypes = [C.c_char_p, dp, C.c_int, C.c_int, dp, C.POINTER(abi.Result),
                                        C.POINTER(C.c_int), C.c_char_p, C.c_int]
         L.thost_solve_json.restype = C.c_int
@@ -116,6 +118,11 @@ def last_batch_qp_stats():
     a, b = C.c_longlong(0), C.c_longlong(0)
     L.thost_last_batch_qp_stats(C.byref(a), C.byref(b))
     return a.value, b.value
+
+
+def set_host_loop_workers(n):
+    """Worker threads of host-loop batches (process-wide; n <= 0: the default, 64)."""
+    load_host().thost_set_host_loop_workers(int(n))
 
 
 def solve_json_stream(batches, scenes=None, devices=(0,), inflight=2):

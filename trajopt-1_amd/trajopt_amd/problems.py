@@ -324,3 +324,49 @@ def with_dynamic_target(wl, link=3):
             rel = np.linalg.inv(T[link]) @ src
             wl.targets[b, k] = rel[:3, :].reshape(12)
     return wl
+
+
+def add_coll_pair(desc, link, other, margin, coeff, term=0):
+    """One CollisionTermInfo "pairs" entry (problem_description.cpp:1686-1719)
+    in the descriptor: robot link `link` against scene primitive `other` (>= 0)
+    or robot link `-1 - other`, with its own margin (dist_pen) and coefficient."""
+    k = desc.n_coll_pairs
+    assert k < abi.MAX_COLL_PAIRS
+    e = desc.coll_pairs[k]
+    e.term, e.link, e.other, e.margin, e.coeff = term, link, other, margin, coeff
+    desc.n_coll_pairs = k + 1
+    return desc
+
+
+def with_pair_data(wl, self_pairs=True):
+    """Config C with per link-pair data on the collision term, on the pairs
+    config C's contacts concentrate on (the wrist links against primitives 5
+    and 8, the upper arm against 9, the forearm against 7): a wider margin and
+    heavier coefficient, a zero coefficient (that pair's contacts are dropped),
+    a narrower margin, and -- when the group has self-collision pairs -- one
+    self pair with its own data."""
+    d = wl.desc
+    links = sorted({d.sphere_link[s] for s in range(d.n_spheres)})
+    add_coll_pair(d, links[-1], 5, 0.06, 35.0)           # replaced below (insert_or_assign)
+    add_coll_pair(d, links[-1], 8, 0.0, 0.0)             # dropped (hasZeroCoeff)
+    add_coll_pair(d, links[2], 9, 0.01, 4.0)             # narrower, lighter
+    add_coll_pair(d, links[4], 7, 0.04, 60.0)
+    add_coll_pair(d, links[-1], 5, 0.05, 30.0)           # the wrist against primitive 5: wider, heavier
+    if self_pairs and d.n_self_pairs > 0:
+        a, b = d.self_pair[0][0], d.self_pair[0][1]
+        add_coll_pair(d, b, -1 - a, 0.03, 12.0)          # unordered: (b, a) names the pair (a, b)
+    return wl
+
+
+def pair_overrides(desc, term=0):
+    """{(link, other): (margin, coeff)} of a term's pair entries, last entry
+    winning; `other` is a primitive index or -1 - link (both orders listed)."""
+    out = {}
+    for k in range(desc.n_coll_pairs):
+        e = desc.coll_pairs[k]
+        if e.term != term:
+            continue
+        out[(e.link, e.other)] = (e.margin, e.coeff)
+        if e.other < 0:
+            out[(-1 - e.other, -1 - e.link)] = (e.margin, e.coeff)
+    return out
