@@ -67,6 +67,10 @@ extern "C" {
 #define THIP_MAX_SELF_PAIRS 64
 #define THIP_MAX_SELF_SPHERE_PAIRS 512
 #define THIP_MAX_COLL_PAIRS 64
+/* the generic path's device evaluator (thip_eval_*) and the host loop take
+ * longer horizons and larger scenes than the fused kernel */
+#define THIP_EVAL_MAX_STEPS 4096
+#define THIP_EVAL_MAX_PRIMS 1024
 #define THIP_MAX_CONTACTS 131072
 
 /* error codes */
@@ -547,6 +551,8 @@ int thip_debug_layout(thip_ctx* ctx, long long* doff, long long* ioff, long long
 #define THIP_DEBUG_NO_BRANCH 4  /* one block solve over all dofs even when the terms split the tree */
 #define THIP_DEBUG_STATIC_DISPATCH 8  /* one workgroup per problem instead of persistent workgroups taking
                                          problems from a counter (bitwise the same results) */
+#define THIP_DEBUG_NO_GEN_BUILD 16    /* QPs outside the segment's domain run the generic step in the
+                                         256-thread build instead of the generic-step build (1024 threads) */
 int thip_debug_set_path(int flags);
 int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws);
 
@@ -568,8 +574,9 @@ int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws);
  *                           CollisionCost / CollisionConstraint::value / convex
  *                           (:1267-1386), one term object per unit
  *                           (CollisionTermInfo::hatch, problem_description.cpp:1735-1858)
- * A thip_eval holds a descriptor (any n_steps in [1, THIP_MAX_STEPS], any term
- * set: only the chain, CartPose and collision fields are read) and the CartPose
+ * A thip_eval holds a descriptor (any n_steps in [1, THIP_EVAL_MAX_STEPS], up to
+ * THIP_EVAL_MAX_PRIMS scene primitives, any term set: only the chain, CartPose and
+ * collision fields are read) and the CartPose
  * targets and scenes of `batch` problems.  Synchronous; host arrays. */
 typedef struct thip_eval thip_eval;
 int thip_eval_create(int device, const thip_problem_desc* desc, int batch, thip_eval** out);

@@ -26,7 +26,8 @@ extern "C" {
  * NULL when n_prims == 0).  The environment is the reference test robot of
  * basic_info.manip: the PR2 (right_arm, left_arm, both_arms; empty scene) or
  * spherebot ("manipulator"; its three static spheres first).  Outputs
- * (caller-sized to the maxima):
+ * (caller-sized to the maxima: THIP_EVAL_MAX_STEPS waypoints, THIP_MAX_CART,
+ * THIP_MAX_JPOS terms, THIP_EVAL_MAX_PRIMS primitives):
  *   desc          the batch-shared structure (per-problem JointPos targets zeroed)
  *   init          [n_steps][n_dof]                initial trajectory
  *   cart_targets  [n_cart][12]                    CartPose target offsets in the chain root

@@ -788,7 +788,14 @@ void addJointDiffTerm(TrajProblem& tp, const std::vector<VarVector>& rows, const
   else
   {
     if (jd.order == 1)
-      throw std::runtime_error("JointVel costs are jv / jvx terms");
+    {
+      // a JointVel cost beyond the jv term: JointVelEqCost (trajectory_costs.cpp:257-301)
+      // over the hatch-clamped steps (tolerance forms are jvx terms)
+      if (!zero)
+        throw std::runtime_error("a JointVel tolerance cost is a jvx term");
+      tp.prob->addCost(std::make_shared<JointVelEqCost>(rows, jd.coeffs, jd.targets, jd.first, jd.last));
+      return;
+    }
     if (zero)
       tp.prob->addCost(std::make_shared<JointDiffEqCost>(jd));
     else

@@ -55,3 +55,7 @@ def pytest_sessionfinish(session, exitstatus):
     strict, total = parity.pooled()
     (out / "parity_table.json").write_text(json.dumps(
         {"records": parity.RECORDS, "pooled_strict": strict, "pooled_total": total}, indent=1) + "\n")
+    # the pooled floor over every check of 8 or more problems (tests/parity.py)
+    if total and strict < parity.POOLED_MIN * total:
+        print(f"\nparity gate: pooled strict {strict}/{total} = {strict / total:.3f} < {parity.POOLED_MIN}")
+        session.exitstatus = 1

@@ -27,12 +27,12 @@ def text(name):
     return (GOLDEN / name).read_text()
 
 
-def json_workload(text_, host):
+def json_workload(text_, host, prims=None):
     """The JSON problem lowered by the host front door as a one-problem Workload
-    (scene = the built-in environment's primitives)."""
+    (scene = the built-in environment's primitives, then `prims`)."""
     from trajopt_amd.problems import Workload
 
-    desc, init, tgt, jpt, scene = host.lower_json(text_, with_scene=True)
+    desc, init, tgt, jpt, scene = host.lower_json(text_, prims, with_scene=True)
     return Workload("json", desc, init[None].copy(), tgt[None].copy(), scene[None].copy(), init[None].copy(),
                     jpt[None].copy() if desc.n_jpos else None)
 

@@ -43,7 +43,19 @@ longer an excuse by itself.
 Every check is recorded (label, batch, strict, reached, spread, and each
 excused problem with its distance to the oracle and to the nearest rerun) and
 tests/conftest.py writes the table to gpurun_out/parity_table.json at the end
-of the session; the pooled strict fraction is bounded there too.
+of the session.
+
+Floors on the strict fraction (problems that meet the bar with no excuse):
+  * a check of 32 or more problems: min_strict (default 85 %);
+  * a check of 8 to 31 problems: MIN_STRICT_SMALL (60 %);
+  * pooled over every check of 8 or more problems: POOLED_MIN (93 %), enforced
+    by tests/conftest.py at the end of the session (the run fails below it).
+
+The gate is frozen (round 5): its rules, jitter amplitudes, schedule and floors
+are those of the end of round 4 plus the floors above, and a red run is not
+answered by widening them -- the failing problem's trace is compared with the
+oracle's (tools/trace_compare.py, tools/hostloop_trace.py) and the cause fixed
+or recorded.
 """
 from __future__ import annotations
 
@@ -54,6 +66,10 @@ COST_RTOL = 0.02
 # reruns before the envelope test is calibrated by the cloud's own scatter (below
 # that, the GPU must lie within 1e-5 of the envelope)
 LOO_MIN_CLOUD = 49
+# strict-fraction floors (module docstring)
+MIN_STRICT_SMALL = 0.60
+POOLED_MIN = 0.93
+POOLED_MIN_BATCH = 8
 
 # (build, input perturbation amplitude, rounding jitter on, seed)
 # FD Jacobian (absolute), KKT solve, QP solution (relative), contact expressions (absolute)
@@ -227,6 +243,8 @@ def check_parity(wl, oracle_mod, x, res, label="", min_strict=0.85, oracle=None,
     assert not unexplained, f"{label}: {len(unexplained)} problems miss the bar without proof:\n" + "\n".join(msgs)
     if B >= 32:
         assert strict >= min_strict * B, f"{label}: only {strict}/{B} problems meet the bar strictly"
+    elif B >= POOLED_MIN_BATCH and min_strict > 0:
+        assert strict >= MIN_STRICT_SMALL * B, f"{label}: only {strict}/{B} problems meet the bar strictly"
     return rec
 
 
@@ -257,7 +275,8 @@ def _loo_excess(xo, mem):
 
 
 def pooled(records=None):
-    """Pooled (strict, total) over the recorded checks that carry a fraction bound."""
+    """Pooled (strict, total) over the recorded checks of POOLED_MIN_BATCH or
+    more problems that carry a fraction bound."""
     rs = RECORDS if records is None else records
-    rs = [r for r in rs if r["min_strict"] > 0]
+    rs = [r for r in rs if r["min_strict"] > 0 and r["batch"] >= POOLED_MIN_BATCH]
     return sum(r["strict"] for r in rs), sum(r["batch"] for r in rs)

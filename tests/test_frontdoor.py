@@ -321,3 +321,25 @@ def test_multi_device_needs_devices(built):
     rc = L.thost_solve_json_batch_multi(arr, 1, None, 0, (C.c_int * 1)(0), 0,
                                         x.ctypes.data_as(C.POINTER(C.c_double)), None, err, 512)
     assert rc == -1 and "no devices" in err.value.decode()
+
+
+def test_beyond_fused_caps_lower_for_the_generic_path():
+    """Problems beyond the fused kernel's capacities still construct, for the
+    generic path (problem_description.cpp has no such limits): a 100-waypoint
+    horizon, a second JointVel cost without tolerances (JointVelEqCost, a jdt term
+    of order 1), and a scene of 20 primitives."""
+    import json as _json
+
+    wl = problems.make_workload("A", 1, n_steps=100)
+    d, init, _, _ = host.lower_json(host.workload_to_json(wl, 0))
+    assert d.n_steps == 100 and init.shape == (100, 7)
+    doc = _json.loads(host.workload_to_json(problems.make_workload("A", 1), 0))
+    doc["costs"].append({"type": "joint_vel", "name": "jv2", "params": {
+        "coeffs": [2.0] * 7, "targets": [0.01] * 7, "first_step": 2, "last_step": 7}})
+    d, _, _, _ = host.lower_json(_json.dumps(doc))
+    assert d.jv_enabled == 1 and d.n_jdt == 1 and d.jdt_order[0] == 1 and d.jdt_is_cnt[0] == 0
+    assert (d.jdt_first_step[0], d.jdt_last_step[0]) == (2, 7)
+    wl = problems.make_workload("C", 1)
+    prims = np.concatenate([wl.scene[0]] * 2)  # 20 primitives
+    d, _, _, _ = host.lower_json(host.workload_to_json(wl, 0), prims)
+    assert d.n_prims == 20

@@ -253,3 +253,52 @@ def test_callback_runs_the_host_loop(oracle_mod, tmp_path):
         assert status == ["OPT_CONVERGED", "OPT_SCO_ITERATION_LIMIT", "OPT_PENALTY_ITERATION_LIMIT"][ro[0].status]
         assert np.abs(x - xo[0]).max() <= TOL_X
         assert n_calls == n_sqp + 1, (n_calls, n_sqp)  # one per SQP iteration, one at the end
+
+
+# ------------------------------------------------------------------ beyond the fused kernel's capacities
+def test_long_horizon_runs_the_generic_path(oracle_mod):
+    """A 100-waypoint JointVel + CartPose-constraint problem (the fused kernel
+    takes 64): ConstructProblem -> BasicTrustRegionSQP runs the host loop with
+    the CartPose term on the device, and meets the oracle."""
+    wl0 = problems.make_workload("A", 2, n_steps=100)
+    for b in range(2):
+        text = host.workload_to_json(wl0, b)
+        x, res, native = host.solve_json(text)
+        assert not native
+        check_parity(dc.json_workload(text, host), oracle_mod, x[None], [res], label="dropin-100-waypoints",
+                     min_strict=0.0)
+
+
+def test_second_jointvel_cost_runs_the_generic_path(oracle_mod):
+    """Two JointVel costs without tolerances (the reference hatches any number,
+    problem_description.cpp:1216-1391): the second is a JointVelEqCost on the
+    generic path, with oracle parity."""
+    import json as _json
+
+    wl0 = problems.make_workload("A", 2)
+    for b in range(2):
+        doc = _json.loads(host.workload_to_json(wl0, b))
+        doc["costs"].append({"type": "joint_vel", "name": "jv2", "params": {
+            "coeffs": [2.0] * 7, "targets": [0.01] * 7, "first_step": 2, "last_step": 7}})
+        text = _json.dumps(doc)
+        x, res, native = host.solve_json(text)
+        assert not native
+        check_parity(dc.json_workload(text, host), oracle_mod, x[None], [res], label="dropin-two-jointvel",
+                     min_strict=0.0)
+
+
+def test_large_scene_runs_the_generic_path(oracle_mod):
+    """A collision problem over a 24-primitive scene (the fused kernel stages 16
+    in LDS): the host loop with the device collision evaluator, oracle parity."""
+    wl0 = problems.make_workload("C", 2, n_steps=12)
+    rng = np.random.default_rng(3)
+    for b in range(2):
+        extra = wl0.scene[b].copy()
+        extra[:, 1:4] += rng.normal(0, 0.05, (len(extra), 3)) * (extra[:, :1] == 0)  # spheres moved a little
+        prims = np.ascontiguousarray(np.concatenate([wl0.scene[b], extra[:14]]))
+        text = host.workload_to_json(wl0, b)
+        x, res, native = host.solve_json(text, prims)
+        assert not native
+        wl = dc.json_workload(text, host, prims)
+        assert wl.desc.n_prims == 24
+        check_parity(wl, oracle_mod, x[None], [res], label="dropin-24-primitives", min_strict=0.0)

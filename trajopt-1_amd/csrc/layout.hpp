@@ -12,11 +12,27 @@
 
 namespace thip
 {
-constexpr int kBlock = 256;  // threads per problem workgroup
+// threads per problem workgroup.  sqp_kernel.hip is compiled twice: the main
+// build (256 threads: the register-resident ADMM segment's ownership maps and
+// launch bounds need them) and the generic-step build (THIP_GENERIC_ONLY,
+// THIP_KBLOCK = kGenBlock: no segment code, four times the waves to hide the
+// HBM latency of the generic ADMM step's row loops, for QPs the segment does
+// not take -- blocks wider than 8 dofs, more than 32 waypoints)
+#ifndef THIP_KBLOCK
+#define THIP_KBLOCK 256
+#endif
+constexpr int kBlock = THIP_KBLOCK;
 constexpr int kWaves = kBlock / 64;
+constexpr int kGenBlock = 1024;  // threads of the generic-step build
+// waves that run the contact scan's per-wave step pairs (their sub-state
+// scratch A_CSCR is sized for this many); further waves take part in the
+// batched sub-state FK only
+constexpr int kScanWaves = 4;
 // dynamic LDS a problem may use (160 KB per CU on gfx950, one workgroup per
 // CU; the rest is the kernel's static LDS)
 constexpr long long kLdsBudgetBytes = 149 * 1024;
+// ... for the generic-step build, whose static LDS is ~1.5 KB larger
+constexpr long long kLdsBudgetGenBytes = 146 * 1024;
 // ADMM-segment chain pack (A_CPK), per half h (0: top, 1: bottom) and chain
 // step r (distance from the middle block), in the lane order the octet chain
 // reads it, zero past the half's length and outside the D x D block:
@@ -97,7 +113,7 @@ enum DArr : int
   A_HW,      // scaled hinge-variable coefficient (h_cap)
   A_HRE,     // effective rho of hinge rows after eliminating the hinge variable (h_cap)
   A_CPL,     // coupling blocks K_{t+1,t} (N*D*D)
-  A_CSCR,    // contact-scan scratch: sphere centers [kWaves][kSubCap][n_spheres][3]
+  A_CSCR,    // contact-scan scratch: sphere centers [kScanWaves][kSubCap][n_spheres][3]
   A_HCOST,   // per step-pair collision cost scratch (N)
   A_HDIST,   // contact distance of each hinge row (h_cap)
   A_HCCT,    // contact cc_time of each hinge row (h_cap; diagnostics, thip_collision_rows)

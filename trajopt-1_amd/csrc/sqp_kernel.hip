@@ -23,6 +23,17 @@
 #include "kin_device.hpp"
 #include "layout.hpp"
 
+// THIP_GENERIC_ONLY: the generic-step build (layout.hpp kGenBlock threads, no
+// register-resident segment, the fused kernel alone, named sqp_kernel_gen)
+#ifndef THIP_GENERIC_ONLY
+#define THIP_GENERIC_ONLY 0
+#endif
+#if THIP_GENERIC_ONLY
+#define THIP_SQP_KERNEL sqp_kernel_gen
+#else
+#define THIP_SQP_KERNEL sqp_kernel
+#endif
+
 namespace thip
 {
 // ------------------------------------------------------------------ constants
@@ -430,7 +441,8 @@ __device__ void linearize(Ctx& c, const double* x, double* raw_jac = nullptr)
 // CalcDistExpressions* (:463-536), CollisionCost::value (:1287-1306);
 // the same arithmetic as oracle/src/collision.cpp.
 //
-// Each wave takes step pairs t = first + wave, + kWaves, ...; per pair the
+// Each of the first kScanWaves waves takes step pairs t = first + wave, +
+// kScanWaves, ...; per pair the
 // lanes compute the sphere centers of the LVS sub-states (one sub-state per
 // lane, scratch in A_CSCR), then scan the candidates (robot sphere s of link
 // group g, primitive p, sub-state i) in the flattened ContactResultMap order
@@ -564,7 +576,7 @@ __device__ __forceinline__ void sphere_centers_at(const CollStage& S, const thip
 }
 
 // The LVS sub-states of every collision unit at x, their prefix in
-// Ctl::suboff, and -- when they number at most kWaves * kSubCap -- the sphere
+// Ctl::suboff, and -- when they number at most kScanWaves * kSubCap -- the sphere
 // centers of all of them computed by the whole workgroup at once into A_CSCR
 // (unit t's sub-state i at row suboff[t] + i).  A unit of one wave has ~5
 // sub-states, so a per-unit walk keeps ~5 of its 64 lanes busy.  Returns
@@ -608,7 +620,7 @@ __device__ bool coll_substates_batched(Ctx& c, const double* x)
   }
   BSYNC();
   const int total = c.s->suboff[L.coll_last];
-  if (total > kWaves * kSubCap)
+  if (total > kScanWaves * kSubCap)
     return false;
   long long* pf22 = (c.tid == 0) ? c.s->prof : nullptr;
   const long long tfk0 = pf22 ? clock64() : 0;
@@ -728,12 +740,12 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       c.s->hbits_x = batched ? 1 : 0;
   }
   unsigned* const HBITS = reinterpret_cast<unsigned*>(c.ia(I_HBITS));
-  double* SCRW = c.a(A_CSCR) + (long long)c.wave * kSubCap * ns * 3;
+  double* SCRW = c.a(A_CSCR) + (long long)(c.wave < kScanWaves ? c.wave : 0) * kSubCap * ns * 3;
   int* PCNT = c.ia(I_PCNT);
   double* HCOST = c.a(A_HCOST);
   int* CONT = c.ia(I_CONT);
   int* HT = c.ia(I_HT);
-  for (int t = L.coll_first + c.wave; t < L.coll_last; t += kWaves)
+  for (int t = L.coll_first + c.wave; c.wave < kScanWaves && t < L.coll_last; t += kScanWaves)
   {
     const bool single = L.coll_single != 0;
     if (single && coll_fixed_step(c, t))
@@ -3841,6 +3853,7 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
     pf[31] += clock64() - tq;
 }
 
+#if !THIP_GENERIC_ONLY
 // ======================================================================
 // Register-resident ADMM segment (the hot loop)
 // ======================================================================
@@ -4769,6 +4782,8 @@ __device__ void admm_iterations(Ctx& c, Solver& sv, int n_iter, Norms* res)
   admm_segment<1, 1>(c, sv, n_iter, res);
 }
 
+#endif  // !THIP_GENERIC_ONLY
+
 __device__ double rho_estimate(Ctx& c, const Norms& nm)
 {
   double pr = nm.pr, dr = nm.dr;
@@ -5033,7 +5048,11 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
   bool fail = false;
   const int ct = os.check_termination;
   // the segment addresses MR, the hinge chunk table and chunk sums as LDS
+#if THIP_GENERIC_ONLY
+  const bool seg = false;  // (this build has no segment: its QPs run the generic step)
+#else
   const bool seg = seg_path(c);
+#endif
   bool pre_ready = false;  // admm_step's ETA / BX (cleared when rho changes)
   for (it = 1; it <= os.max_iter; ++it)
   {
@@ -5048,7 +5067,9 @@ __device__ int qp_solve(Ctx& c, Solver& sv, bool pattern_equal)
         stop = min(stop, (it + interval - 1) / interval * interval);
       // the segment computes the residuals of its last iterate when they are needed
       const bool want = (ct && stop % ct == 0) || (os.adaptive_rho && interval && stop % interval == 0);
+#if !THIP_GENERIC_ONLY
       admm_iterations(c, sv, stop - it + 1, want ? &nm : nullptr);
+#endif
       have_res = want;
       it = stop;
     }
@@ -5734,7 +5755,7 @@ done:
 __device__ __forceinline__ void solve_problem(const KernelArgs& args, int b, double* dyn, Ctl& ctl,
                                               double** ptab, CollStage& cstage);
 
-__global__ __launch_bounds__(kBlock) void sqp_kernel(KernelArgs args)
+__global__ __launch_bounds__(kBlock) void THIP_SQP_KERNEL(KernelArgs args)
 {
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ Ctl ctl;
@@ -5858,6 +5879,7 @@ __device__ __forceinline__ void solve_problem(const KernelArgs& args, int b, dou
 }
 
 // standalone convexification (thip_linearize): writes rows into err/jac layout
+#if !THIP_GENERIC_ONLY
 __global__ __launch_bounds__(kBlock) void linearize_kernel(KernelArgs args, const double* xin, double* err,
                                                            double* jac)
 {
@@ -5996,5 +6018,6 @@ __global__ __launch_bounds__(kBlock) void coll_rows_kernel(KernelArgs args, cons
     counts[b] = (ctl.flags & THIP_FLAG_CONTACT_OVERFLOW) ? -1 : ctl.n_h - c.T.n_sh;
 }
 
+#endif  // !THIP_GENERIC_ONLY
 }  // namespace thip
 

@@ -593,7 +593,7 @@ int thip_eval_create(int device, const thip_problem_desc* desc, int batch, thip_
   const int N = desc->n_steps;
   if (ch.n_dof <= 0 || ch.n_dof > THIP_MAX_DOF || ch.n_links < 1 || ch.n_links > THIP_MAX_LINKS)
     return reject("chain out of range");
-  if (N < 1 || N > THIP_MAX_STEPS)
+  if (N < 1 || N > THIP_EVAL_MAX_STEPS)
     return reject("n_steps out of range");
   for (int k = 1; k < ch.n_links; ++k)
     if ((ch.joint_type[k] < 0 || ch.joint_type[k] > 3) ||
@@ -611,7 +611,7 @@ int thip_eval_create(int device, const thip_problem_desc* desc, int batch, thip_
     return reject("n_coll_extra out of range");
   if ((desc->coll_enabled || desc->n_coll_extra > 0) &&
       (desc->n_spheres < 1 || desc->n_spheres > THIP_MAX_SPHERES || desc->n_prims < 0 ||
-       desc->n_prims > THIP_MAX_PRIMS))
+       desc->n_prims > THIP_EVAL_MAX_PRIMS))
     return reject("collision: spheres / primitives out of range");
   {
     const std::string why = thip::validate_coll_pairs(*desc);

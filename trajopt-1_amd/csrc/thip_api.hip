@@ -22,6 +22,7 @@
 namespace thip
 {
 __global__ void sqp_kernel(KernelArgs args);
+__global__ void sqp_kernel_gen(KernelArgs args);  // the generic-step build (kGenBlock threads)
 __global__ void linearize_kernel(KernelArgs args, const double* xin, double* err, double* jac);
 __global__ void fwd_kin_kernel(KernelArgs args, const double* xin, double* poses);
 __global__ void stage_inputs_kernel(KernelArgs args, const double* init, const double* tgt);
@@ -64,6 +65,8 @@ struct thip_ctx
   size_t lds_lin_bytes = 0;  // linearize_kernel: scratch only
   int* d_work = nullptr;     // sqp_kernel's problem counter (KernelArgs::work); null: static mapping
   int grid = 0;              // sqp_kernel workgroups (resident slots, or the batch)
+  bool gen = false;          // the QPs never take the segment: launch the generic-step build
+                             // (sqp_kernel_gen, kGenBlock threads) instead of sqp_kernel
   std::string err;
 };
 
@@ -679,7 +682,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   sizes[A_HC0] = sizes[A_HC] = hc * 2 * D;
   sizes[A_HK] = sizes[A_HW] = sizes[A_HRE] = sizes[A_HDIST] = sizes[A_HCCT] = hc;
   sizes[A_CPL] = (L.hinge || L.nbr > 1) ? sNDD : 1;
-  sizes[A_CSCR] = L.coll ? (long long)kWaves * kSubCap * d.n_spheres * 3 : 1;
+  sizes[A_CSCR] = L.coll ? (long long)kScanWaves * kSubCap * d.n_spheres * 3 : 1;
   sizes[A_HCOST] = L.N;
   sizes[A_HPK] = L.hinge ? hc * kHPack : 1;
   const long long nchk_cap = hc / kHChunk + L.N + 1;
@@ -713,13 +716,13 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   isizes[I_PCNT] = L.N;
   isizes[I_HKIND] = isizes[I_HSLOT] = hc;
   // one bit per (primitive, sub-state, sphere) and (self sphere pair, sub-state)
-  // candidate of every unit while the sub-states number at most kWaves * kSubCap
+  // candidate of every unit while the sub-states number at most kScanWaves * kSubCap
   // (the batched scan), each unit's bits padded to 64
   std::vector<int> hb_sa, hb_sb, hb_kp;
   if (L.coll)
     self_sphere_pairs(d, hb_sa, hb_sb, hb_kp);
   isizes[I_HBITS] = L.coll ? (((long long)std::max(d.n_prims, 1) * d.n_spheres + (long long)hb_sa.size()) *
-                                  kWaves * kSubCap +
+                                  kScanWaves * kSubCap +
                               31) / 32 +
                                  2LL * (L.N + 1)
                            : 1;
@@ -746,7 +749,17 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     L.lds_scratch = static_cast<int>(used);
     for (int k = 0; k < A_COUNT; ++k)
       L.loff[k] = -1;
-    const long long budget = kLdsBudgetBytes / static_cast<long long>(sizeof(double));
+    int max_step_rows = 0;
+    for (int t = 0; t < L.N; ++t)
+      max_step_rows = std::max(max_step_rows, step_ptr[static_cast<size_t>(t) + 1] - step_ptr[static_cast<size_t>(t)]);
+    // QPs outside the register-resident segment's domain (below) run the
+    // generic ADMM step for the whole solve: the generic-step build of the fused
+    // kernel (kGenBlock threads, no segment code) takes them; its larger static
+    // LDS (reductions over 16 waves) leaves a smaller dynamic budget
+    const bool seg_cand = max_step_rows <= kMaxStepRows && !L.wide && L.N * 8 <= kBlock && L.n_abs <= kBlock && cpk;
+    ctx->gen = (!seg_cand || (g_debug_path & THIP_DEBUG_NO_SEGMENT)) && !(g_debug_path & THIP_DEBUG_NO_GEN_BUILD);
+    const long long budget =
+        (ctx->gen ? kLdsBudgetGenBytes : kLdsBudgetBytes) / static_cast<long long>(sizeof(double));
     for (int k : order)
     {
       const long long n = (sizes[k] + 7) / 8 * 8;
@@ -756,9 +769,6 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
       used += n;
     }
     L.lds_doubles = static_cast<int>(used);
-    int max_step_rows = 0;
-    for (int t = 0; t < L.N; ++t)
-      max_step_rows = std::max(max_step_rows, step_ptr[static_cast<size_t>(t) + 1] - step_ptr[static_cast<size_t>(t)]);
     L.max_step_rows = max_step_rows;
     L.rows_contig = 1;
     for (int r = 0; r < L.n_abs; ++r)
@@ -767,11 +777,8 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     // one column slot (t, i) and one CartPose row per thread: N <= 32 and
     // n_abs <= 256; larger problems run the generic admm_step()
     // (collision problems: hinge rows are loop-owned inside the segment)
-    L.seg_ok = (max_step_rows <= kMaxStepRows && !L.wide && L.N * 8 <= kBlock && L.n_abs <= kBlock && cpk &&
-                L.loff[A_CPK] >= 0)
-                   ? 1
-                   : 0;
-    if (g_debug_path & THIP_DEBUG_NO_SEGMENT)  // diagnostic: the generic ADMM step
+    L.seg_ok = (seg_cand && L.loff[A_CPK] >= 0) ? 1 : 0;
+    if ((g_debug_path & THIP_DEBUG_NO_SEGMENT) || ctx->gen)  // diagnostic: the generic ADMM step
       L.seg_ok = 0;
     L.seg_slots = 1;
     L.tw_mid = L.N / 2;
@@ -968,8 +975,10 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     return fail(std::string("hipMemsetAsync(workspace): ") + hipGetErrorString(e));
   if ((e = hipEventCreate(&ctx->ev0)) != hipSuccess || (e = hipEventCreate(&ctx->ev1)) != hipSuccess)
     return fail(std::string("hipEventCreate: ") + hipGetErrorString(e));
-  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sqp_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               static_cast<int>(ctx->lds_bytes))) != hipSuccess ||
+  const void* fused = ctx->gen ? reinterpret_cast<const void*>(&sqp_kernel_gen) : reinterpret_cast<const void*>(&sqp_kernel);
+  const int fused_block = ctx->gen ? kGenBlock : kBlock;
+  if ((e = hipFuncSetAttribute(fused, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ctx->lds_bytes))) !=
+          hipSuccess ||
       (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&linearize_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ctx->lds_lin_bytes))) !=
           hipSuccess)
@@ -980,8 +989,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   if (!(g_debug_path & THIP_DEBUG_STATIC_DISPATCH))
   {
     int per_cu = 0, n_cu = 0;
-    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&sqp_kernel), kBlock,
-                                                          ctx->lds_bytes)) != hipSuccess ||
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fused, fused_block, ctx->lds_bytes)) != hipSuccess ||
         (e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
       return fail(std::string("occupancy query: ") + hipGetErrorString(e));
     const long long slots = static_cast<long long>(std::max(per_cu, 1)) * std::max(n_cu, 1);
@@ -1127,8 +1135,12 @@ int thip_sqp_run(thip_ctx* ctx)
   a.xout = ctx->d_x;
   a.work = ctx->d_work;
   HIPCHK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-  hipLaunchKernelGGL(sqp_kernel, dim3(ctx->d_work ? ctx->grid : ctx->batch), dim3(kBlock), ctx->lds_bytes,
-                     ctx->stream, a);
+  if (ctx->gen)
+    hipLaunchKernelGGL(sqp_kernel_gen, dim3(ctx->d_work ? ctx->grid : ctx->batch), dim3(kGenBlock), ctx->lds_bytes,
+                       ctx->stream, a);
+  else
+    hipLaunchKernelGGL(sqp_kernel, dim3(ctx->d_work ? ctx->grid : ctx->batch), dim3(kBlock), ctx->lds_bytes,
+                       ctx->stream, a);
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
   ctx->ran = true;

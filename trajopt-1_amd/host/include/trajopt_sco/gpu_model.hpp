@@ -9,6 +9,7 @@
 // QP on the GPU: thip_qp_solve, OSQP 1.0 with OSQPModelConfig's settings.
 #pragma once
 #include <memory>
+#include <array>
 #include <mutex>
 #include <vector>
 
@@ -62,6 +63,10 @@ public:
 
   // diagnostics of the last solve
   const thip_qp_info& lastInfo() const { return info_; }
+  // diagnostics: one record per solve appended to *trace (null: off) -- warm
+  // start, rho in, ADMM iterations, OSQP status, polish status, rho out, primal /
+  // dual residual, sum |x*| (the oracle's OSQPModel trace fields 0-8)
+  void setTrace(std::vector<std::array<double, 9>>* trace) { trace_ = trace; }
   long long admmItersTotal() const { return admm_total_; }
 
 private:
@@ -98,5 +103,6 @@ private:
   thip_qp_info info_{};
   long long admm_total_{ 0 };
   GpuQPBatcher::Ptr batcher_;
+  std::vector<std::array<double, 9>>* trace_{ nullptr };
 };
 }  // namespace sco

@@ -679,7 +679,12 @@ void JointVelTermInfo::hatch(TrajOptProb& prob)
     return;
   }
   if (d.jv_enabled)
-    unsupported("more than one JointVel cost without tolerances");
+  {
+    // a second JointVelEqCost: the generic path runs it (a jdt term of order 1;
+    // the fused kernel's JointVel band holds one term)
+    addJointDiffTerm(prob, 1, true, coeffs, targets, upper_tols, lower_tols, first, last, name);
+    return;
+  }
   d.jv_enabled = 1;
   d.jv_first_step = first_step;
   d.jv_last_step = last_step;
@@ -1039,8 +1044,9 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
       spheres.push_back(&cs);
   if (spheres.empty() || static_cast<int>(spheres.size()) > THIP_MAX_SPHERES)
     unsupported("a collision model with " + std::to_string(spheres.size()) + " spheres");
-  if (static_cast<int>(env->scene.size()) > THIP_MAX_PRIMS)
-    unsupported("a scene of more than " + std::to_string(THIP_MAX_PRIMS) + " primitives");
+  // (a scene beyond THIP_MAX_PRIMS runs the generic path, TrajOptProb::lowerable)
+  if (static_cast<int>(env->scene.size()) > THIP_EVAL_MAX_PRIMS)
+    unsupported("a scene of more than " + std::to_string(THIP_EVAL_MAX_PRIMS) + " primitives");
   if (static_cast<int>(fixed_steps.size()) > THIP_MAX_STEPS)
     throw std::runtime_error("CollisionTermInfo: too many fixed steps");
   const bool is_cnt = !any(term_type & TermType::TT_COST);
@@ -1255,8 +1261,10 @@ TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci)
     throw std::runtime_error("No terms use time and basic_info is not set correctly. Try basic_info.use_time = false");
   if (!iequals(bi.convex_solver, "OSQP") && !iequals(bi.convex_solver, "AUTO_SOLVER"))
     unsupported("convex_solver " + bi.convex_solver);
-  if (n_steps < 1 || n_steps > THIP_MAX_STEPS)
-    throw std::runtime_error("n_steps must be in [1, " + std::to_string(THIP_MAX_STEPS) + "]");
+  // (the fused kernel takes n_steps <= THIP_MAX_STEPS; longer problems run the
+  // generic path, whose device evaluator takes THIP_EVAL_MAX_STEPS)
+  if (n_steps < 1 || n_steps > THIP_EVAL_MAX_STEPS)
+    throw std::runtime_error("n_steps must be in [1, " + std::to_string(THIP_EVAL_MAX_STEPS) + "]");
 
   auto prob = std::make_shared<TrajOptProb>(n_steps, pci);
   thip_problem_desc& d = prob->desc_;
@@ -1431,8 +1439,11 @@ std::string TrajOptProb::unloweredTerms() const
 
 bool TrajOptProb::lowerable() const
 {
-  return desc_.n_steps >= 2 && desc_.n_jdt == 0 && desc_.n_jvt == 0 && desc_.n_ttt == 0 && !desc_.use_time &&
-         desc_.n_fixed_dofs == 0 && desc_.n_coll_extra == 0 && unloweredTerms().empty();
+  // the fused kernel's domain: at most THIP_MAX_STEPS waypoints and THIP_MAX_PRIMS
+  // scene primitives, and no term it does not lower
+  return desc_.n_steps >= 2 && desc_.n_steps <= THIP_MAX_STEPS && desc_.n_prims <= THIP_MAX_PRIMS &&
+         desc_.n_jdt == 0 && desc_.n_jvt == 0 && desc_.n_ttt == 0 && !desc_.use_time && desc_.n_fixed_dofs == 0 &&
+         desc_.n_coll_extra == 0 && unloweredTerms().empty();
 }
 
 LoweredProblem TrajOptProb::lowered() const

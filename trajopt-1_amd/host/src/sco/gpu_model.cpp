@@ -356,6 +356,14 @@ CvxOptStatus GpuModel::optimize()
   }
   else
     solveDirect(P, A, q, l, u, s, ws, x, y);
+  if (trace_)
+  {
+    double xs = 0;
+    for (double v : x)
+      xs += std::fabs(v);
+    trace_->push_back({ ws ? 1.0 : 0.0, s.rho, static_cast<double>(info_.iter), static_cast<double>(info_.status),
+                        static_cast<double>(info_.polish_status), info_.rho, info_.prim_res, info_.dual_res, xs });
+  }
   return finishSolve(std::move(P), std::move(A), x, y);
 }
 

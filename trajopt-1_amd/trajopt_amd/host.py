@@ -70,10 +70,10 @@ def lower_json(text: str, scene=None, with_scene=False):
     sc = None if scene is None or len(scene) == 0 else np.ascontiguousarray(scene, dtype=np.float64)
     n_prims = 0 if sc is None else sc.shape[0]
     desc = abi.ProblemDesc()
-    init = np.zeros((abi.MAX_STEPS, abi.MAX_DOF))
+    init = np.zeros((abi.EVAL_MAX_STEPS, abi.MAX_DOF))
     tgt = np.zeros((abi.MAX_CART, 12))
     jpt = np.zeros((abi.MAX_JPOS, abi.MAX_DOF))
-    sco = np.zeros((abi.MAX_PRIMS, 16))
+    sco = np.zeros((abi.EVAL_MAX_PRIMS, 16))
     err = C.create_string_buffer(4096)
     rc = L.thost_lower_json(text.encode(), _dp(sc), n_prims, C.byref(desc), _dp(init), _dp(tgt), _dp(jpt), _dp(sco),
                             err, 4096)
