@@ -10,6 +10,7 @@ cost against a 10-primitive scene, 1024 problems per GPU.  `value` is SQP
 (SURVEY.md §8d).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 1024]
+    python bench.py --config HB --batch 256     (host-loop workload, see main_hostloop)
 
 Batches in flight: the runtime keeps `--inflight` (default 3) batch contexts,
 each with its own HIP stream, and submits step k to context k mod inflight,
@@ -199,6 +200,140 @@ def pmc_evidence(config):
     return best
 
 
+HOSTLOOP_BASE = "B"  # bench --config HB: config B's problems + a JointAcc cost
+
+
+def hostloop_workload_name(wl, batch):
+    return (f"config HB: {wl.n_dof}-DoF PR2 arm x {wl.n_steps} waypoints, JointVel + {wl.desc.n_cart} CartPose "
+            f"ABS costs (config {HOSTLOOP_BASE}) + a JointAcc cost (joint_costs_unit), batch {batch} per GPU "
+            "(host BasicTrustRegionSQP loops, GpuModel QPs batched one launch per round)")
+
+
+def hostloop_oracle_workload(texts):
+    """The lowered JSON problems as one oracle Workload (every problem of a
+    config HB batch lowers to the same description; the targets and initial
+    trajectories differ)."""
+    from trajopt_amd import host
+    from trajopt_amd.problems import Workload
+
+    low = [host.lower_json(t) for t in texts]
+    desc = low[0][0]
+    return Workload("HB", desc, np.stack([v[1] for v in low]), np.stack([v[2] for v in low]),
+                    np.zeros((len(texts), 0, 16)), np.stack([v[1] for v in low]), None)
+
+
+def main_hostloop(args, world, rank, local_rank, json_out):
+    """bench.py --config HB: problems the fused kernel does not lower, solved by
+    the C++ host loops (one per problem, all at once) whose QP rounds go to the
+    device as one qp_csc launch per pattern (sco::GpuQPBatcher).  A step is one
+    prepared batch (thost_batch_create: parse, lower, device set-up, outside the
+    timed region) solved to convergence; each step solves fresh copies of the
+    same problems.  roofline: the QP solver's algorithmic bytes
+    (GpuQPBatcher::bytes) over the wall time inside its launches."""
+    import torch
+    import torch.distributed as dist
+
+    from trajopt_amd import host
+
+    abi.load_hip()
+    if world > 1:
+        dist.init_process_group("gloo")
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
+    wl = sharding.rank_workload(HOSTLOOP_BASE, args.batch, rank)
+    texts = [host.hostloop_workload_json(wl, b) for b in range(args.batch)]
+    batches = [host.PreparedBatch(texts, device=device) for _ in range(args.warmup + args.steps)]
+    if not batches[0].stats()["host_loops"]:
+        raise SystemExit("config HB lowered onto the fused kernel: it must run the host loops")
+    res0 = None
+    for k in range(args.warmup):
+        _, res0 = batches[k].solve()
+    barrier = (lambda: dist.barrier()) if world > 1 else (lambda: None)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = [batches[args.warmup + k].solve() for k in range(args.steps)]
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    res_last = outs[-1][1]
+    for _, r in outs[:-1] + ([(None, res0)] if res0 is not None else []):
+        if any(a.n_sqp_iters != b.n_sqp_iters or a.n_admm_iters != b.n_admm_iters for a, b in zip(r, res_last)):
+            raise SystemExit("non-deterministic SQP counters between steps")
+    st = [batches[args.warmup + k].stats() for k in range(args.steps)]
+    iters_local = sum(r.n_sqp_iters for r in res_last)
+    elapsed, iters_total = sharding.reduce_step_stats(elapsed, iters_local, world)
+    if rank == 0:
+        qp_bytes = float(np.mean([s["qp_bytes"] for s in st]))
+        qp_s = float(np.mean([s["qp_seconds"] for s in st]))
+        launches = float(np.mean([s["qp_launches"] for s in st]))
+        achieved = qp_bytes / qp_s / 1e9
+        out = {
+            "metric": "SQP iters/sec + achieved HBM GB/s, 7-DoF x 30-wpt host-loop batch (JointAcc, not lowered)",
+            "value": iters_total * args.steps / elapsed,
+            "unit": "SQP iters/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": f"synthetic (config {HOSTLOOP_BASE} seeds 20261015+b written as TrajOptRequest JSON, + JointAcc)",
+            "config": {
+                "workload": hostloop_workload_name(wl, args.batch),
+                "batch_per_gpu": args.batch,
+                "global_batch": args.batch * world,
+                "sqp_iters_per_step": iters_total,
+                "qp_solves_per_step_rank0": sum(r.n_qp_solves for r in res_last),
+                "admm_iters_per_step_rank0": sum(r.n_admm_iters for r in res_last),
+                "qp_launches_per_step": launches,
+                "parallelism": f"shard{world} (independent problems, no collective)",
+            },
+            "roofline": {
+                # the host loops' QP rounds: one launch per round of the batch (a
+                # workgroup per QP, sparse LDL^T KKT + ADMM); per launch `achieved`
+                # is the GpuQPBatcher byte model over the wall time inside
+                # thip_qp_solve_some (upload, launch, download of the round)
+                "bound": "latency",
+                "kernel": "thip::qp_csc_kernel",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "qp_launch_share_of_step": qp_s / (elapsed / args.steps),
+                "algorithmic_bytes_per_step": qp_bytes,
+                "qp_seconds_per_step": qp_s,
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu:
+            sys.path.insert(0, str(ROOT))
+            from oracle import oracle  # checker / baseline only
+
+            usable, nproc, model, _ = host_cpus()
+            threads = usable if args.cpu_threads <= 0 else args.cpu_threads
+            n = min(args.batch, args.cpu_problems if args.cpu_problems > 0 else max(128, 4 * threads))
+            owl = hostloop_oracle_workload(texts[:n])
+            t1 = time.perf_counter()
+            _, ores = oracle.solve(owl, n_threads=threads, variant="fast")
+            dt = time.perf_counter() - t1
+            it = sum(r.n_sqp_iters for r in ores)
+            out["cpu_baseline"] = {
+                "value": it / dt, "unit": "SQP iters/s", "cores": threads, "kind": "port",
+                "sample": f"first {n} problems of the same batch, {it} SQP iterations in {dt:.1f} s, one problem "
+                          f"per thread on {threads} threads",
+                "host_nproc": nproc, "host_cpu_model": model,
+            }
+        print(json.dumps(out), file=json_out, flush=True)
+    for b in batches:
+        b.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,6 +363,9 @@ def main():
     sys.stdout.flush()
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+
+    if args.config == "HB":
+        return main_hostloop(args, world, rank, local_rank, json_out)
 
     import torch
     import torch.distributed as dist

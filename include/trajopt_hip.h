@@ -551,8 +551,8 @@ int thip_debug_layout(thip_ctx* ctx, long long* doff, long long* ioff, long long
 #define THIP_DEBUG_NO_BRANCH 4  /* one block solve over all dofs even when the terms split the tree */
 #define THIP_DEBUG_STATIC_DISPATCH 8  /* one workgroup per problem instead of persistent workgroups taking
                                          problems from a counter (bitwise the same results) */
-#define THIP_DEBUG_NO_GEN_BUILD 16    /* QPs outside the segment's domain run the generic step in the
-                                         256-thread build instead of the generic-step build (1024 threads) */
+#define THIP_DEBUG_GEN_BUILD 16       /* QPs outside the segment's domain run the generic-step build
+                                         (1024 threads, no segment) instead of the 256-thread build */
 int thip_debug_set_path(int flags);
 int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws);
 
@@ -649,6 +649,9 @@ int thip_qp_solve_some(thip_qp* qp, int count, const double* P_values, const dou
                        thip_qp_info* info);
 void thip_qp_destroy(thip_qp* qp);
 const char* thip_qp_last_error(thip_qp* qp); /* NULL: the last thip_qp_create failure */
+/* Entries of the KKT factor L of the pattern (the symbolic analysis of
+ * thip_qp_create): the algorithmic-byte model of the QP solves; -1 for NULL. */
+long long thip_qp_factor_nnz(const thip_qp* qp);
 
 /* Resident workspace (update in place).  The OSQP 1.0 solver object of every QP
  * of the batch stays on the device between calls, as OsqpEigen::Solver keeps it

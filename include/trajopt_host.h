@@ -56,6 +56,25 @@ void thost_last_batch_qp_stats(long long* launches, long long* qps);
  * default, 64; never more than the batch). */
 void thost_set_host_loop_workers(int n);
 
+/* A prepared batch: ConstructProblem for each of `batch` JSON problems
+ * (scenes [batch][n_prims][16]) and the trajopt::BatchTrustRegionSQP over them
+ * on HIP device `device`, without solving -- so a caller (the bench) times the
+ * solve alone.  thost_batch_solve runs it once: x [batch][n_steps][n_dof (+1
+ * with use_time)], results [batch] (may be NULL); a host-loop batch's models
+ * keep their warm starts, so it is solved at most once (a second call fails).
+ * thost_batch_stats: host_loops (1 when the problems run the host loops with
+ * batched QPs, 0 for the fused kernel), and for host loops the QP launches, QPs,
+ * their algorithmic HBM bytes (sco::GpuQPBatcher::bytes) and the wall seconds
+ * spent in the launches.  Every problem's host loop runs at once (one worker
+ * per problem), so each QP round of the batch is one launch per pattern. */
+typedef struct thost_batch thost_batch;
+int thost_batch_create(const char* const* json_texts, int batch, const double* scenes, int n_prims, int device,
+                       thost_batch** out, char* err, int err_len);
+int thost_batch_solve(thost_batch* b, double* x, thip_result* results, char* err, int err_len);
+int thost_batch_stats(const thost_batch* b, int* host_loops, long long* qp_launches, long long* qps, double* qp_bytes,
+                      double* qp_seconds);
+void thost_batch_destroy(thost_batch* b);
+
 /* thost_solve_json_batch sharded over n_devices HIP devices of this process
  * (trajopt::MultiDeviceBatchSQP: contiguous shards, sizes differing by at most
  * one, all shards running concurrently; a device may be listed more than once). */

@@ -1,16 +1,19 @@
 """A/B of the fused kernel's two builds on a workload whose QPs never take the
 register-resident segment (config E by default): the generic-step build
 (sqp_kernel_gen, layout.hpp kGenBlock threads) against the 256-thread build
-(THIP_DEBUG_NO_GEN_BUILD).  Per build: one batch alone (HIP-event ms), SQP
+(the default; THIP_DEBUG_GEN_BUILD selects the generic-step build).  Per build: one batch alone (HIP-event ms), SQP
 iterations, statuses; then whether the two builds agree to the parity bar.
 
-    python tools/gen_ab.py [config] [batch] [n_steps]
+    python tools/gen_ab.py [config] [batch] [n_steps] [root]
+
+(root: another build tree with a trajopt-1_amd/ directory; the segment is
+switched off in both runs, so segment-capable configs run the generic step too)
 """
 import sys
 import time
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parent.parent
+ROOT = Path(sys.argv[4]).resolve() if len(sys.argv) > 4 else Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "trajopt-1_amd"))
 
 import numpy as np  # noqa: E402
@@ -20,10 +23,11 @@ from trajopt_amd.runtime import BatchTrustRegionSQP  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "E"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 64
-N = int(sys.argv[3]) if len(sys.argv) > 3 else None
+N = int(sys.argv[3]) if len(sys.argv) > 3 and int(sys.argv[3]) > 0 else None
 hip = abi.load_hip()
 out = {}
-for name, flags in (("gen", 0), ("main", abi.DEBUG_NO_GEN_BUILD)):
+print(abi.__file__, flush=True)
+for name, flags in (("gen", abi.DEBUG_GEN_BUILD | abi.DEBUG_NO_SEGMENT), ("main", abi.DEBUG_NO_SEGMENT)):
     assert hip.thip_debug_set_path(flags) == 0
     wl = problems.make_workload(cfg, B, n_steps=N) if N else problems.make_workload(cfg, B)
     s = BatchTrustRegionSQP(wl)

@@ -23,7 +23,10 @@ namespace thip
 #endif
 constexpr int kBlock = THIP_KBLOCK;
 constexpr int kWaves = kBlock / 64;
-constexpr int kGenBlock = 1024;  // threads of the generic-step build
+#ifndef THIP_GEN_BLOCK
+#define THIP_GEN_BLOCK 1024
+#endif
+constexpr int kGenBlock = THIP_GEN_BLOCK;  // threads of the generic-step build
 // waves that run the contact scan's per-wave step pairs (their sub-state
 // scratch A_CSCR is sized for this many); further waves take part in the
 // batched sub-state FK only

@@ -1265,6 +1265,7 @@ using namespace thip_qp_dev;
 struct thip_qp
 {
   int device = 0, batch = 0, n = 0, m = 0, nnz_p = 0, nnz_a = 0;
+  long long nnz_l = 0;  // entries of the KKT factor L (thip_qp_factor_nnz)
   QpPattern pat{};
   int* d_idx = nullptr;
   double* d_ws = nullptr;
@@ -1418,6 +1419,7 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
   q->pat.N = static_cast<int>(N);
   q->in_doubles = (long long)np + na + n + 2LL * m;
   q->pat.nlev = nlev;
+  q->nnz_l = nnzl;
   q->pat.lds_vec = lds_vec ? 1 : 0;
   q->lds = lds_vec ? static_cast<size_t>(N) * sizeof(double) : 0;
   auto fail = [&](const std::string& msg) {
@@ -1798,5 +1800,7 @@ void thip_qp_destroy(thip_qp* q)
 }
 
 const char* thip_qp_last_error(thip_qp* q) { return q ? q->err.c_str() : g_qp_create_err.c_str(); }
+
+long long thip_qp_factor_nnz(const thip_qp* q) { return q ? q->nnz_l : -1; }
 
 }  // extern "C"

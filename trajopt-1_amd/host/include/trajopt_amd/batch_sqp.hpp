@@ -55,6 +55,9 @@ public:
   // host-loop batches: QP launches and QPs of the last optimize() (sco::GpuQPBatcher)
   long long qpLaunches() const { return qp_launches_; }
   long long qpSolves() const { return qp_solves_; }
+  // host-loop batches: the QP solves' algorithmic HBM bytes (sco::GpuQPBatcher::bytes)
+  double qpBytes() const { return qp_bytes_; }
+  double qpLaunchSeconds() const { return qp_launch_s_; }
   // host-loop batches: worker threads (problems solved at once); 0 = the
   // process default (setDefaultHostLoopWorkers, initially 64), never more
   // than the batch
@@ -73,6 +76,7 @@ private:
   int device_ = 0;
   std::vector<sco::OptResults> generic_results_;
   long long qp_launches_ = 0, qp_solves_ = 0;
+  double qp_bytes_ = 0, qp_launch_s_ = 0;
   int workers_ = 0;
 };
 

@@ -54,6 +54,15 @@ public:
   // launches and QPs so far (diagnostics)
   long long launches() const { return launches_; }
   long long qps() const { return qps_; }
+  // algorithmic HBM bytes of the solves so far (the bench's roofline model of
+  // qp_csc.hip, per QP: each ADMM iteration streams the factor L twice -- the
+  // forward and backward solves, value and index -- plus D, A x and A'y, P x
+  // and the iterate vectors; each factorisation reads the KKT values and writes
+  // L; polish adds one factorisation and 1 + polish_refine_iter solves)
+  double bytes() const { return bytes_; }
+  long long admmIters() const { return admm_iters_; }
+  // wall seconds inside thip_qp_solve_some (the launches with their transfers)
+  double launchSeconds() const { return launch_s_; }
 
 private:
   void flushLocked();
@@ -68,7 +77,8 @@ private:
     long long last_round = 0;
   };
   std::map<std::string, Slot> cache_;
-  long long round_ = 0, launches_ = 0, qps_ = 0;
+  long long round_ = 0, launches_ = 0, qps_ = 0, admm_iters_ = 0;
+  double bytes_ = 0, launch_s_ = 0;
 };
 
 // RAII: a client of the batcher for its lifetime

@@ -189,6 +189,8 @@ std::vector<sco::OptResults> BatchTrustRegionSQP::optimizeHostLoops()
     t.join();
   qp_launches_ = batcher->launches();
   qp_solves_ = batcher->qps();
+  qp_bytes_ = batcher->bytes();
+  qp_launch_s_ = batcher->launchSeconds();
   for (std::size_t b = 0; b < B; ++b)
     if (!errs[b].empty())
       throw std::runtime_error("BatchTrustRegionSQP: problem " + std::to_string(b) + ": " + errs[b]);

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cstring>
 #include <exception>
+#include <memory>
 #include <string>
 
 #include "trajopt_amd/batch_sqp.hpp"
@@ -227,4 +228,82 @@ int thost_solve_json_batch_multi(const char* const* json_texts, int batch, const
     return -1;
   }
 }
+
+struct thost_batch
+{
+  std::unique_ptr<trajopt::BatchTrustRegionSQP> solver;
+  bool solved = false;
+};
+
+int thost_batch_create(const char* const* json_texts, int batch, const double* scenes, int n_prims, int device,
+                       thost_batch** out, char* err, int err_len)
+{
+  try
+  {
+    if (!json_texts || batch <= 0 || !out)
+      throw std::runtime_error("thost_batch_create: bad arguments");
+    std::vector<trajopt::TrajOptProb::Ptr> probs;
+    for (int b = 0; b < batch; ++b)
+      probs.push_back(construct(json_texts[b], scenes ? scenes + static_cast<std::size_t>(b) * n_prims * 16 : nullptr,
+                                n_prims));
+    auto h = std::make_unique<thost_batch>();
+    h->solver = std::make_unique<trajopt::BatchTrustRegionSQP>(probs, device);
+    h->solver->setHostLoopWorkers(batch);  // every problem's loop at once: each QP round is one launch per pattern
+    *out = h.release();
+    setErr(err, err_len, "");
+    return 0;
+  }
+  catch (const std::exception& e)
+  {
+    setErr(err, err_len, e.what());
+    return -1;
+  }
+}
+
+int thost_batch_solve(thost_batch* h, double* x, thip_result* results, char* err, int err_len)
+{
+  try
+  {
+    if (!h || !x)
+      throw std::runtime_error("thost_batch_solve: bad arguments");
+    if (h->solved && h->solver->hostLoops())
+      throw std::runtime_error("thost_batch_solve: a host-loop batch is solved once (its models keep their warm starts)");
+    const auto res = h->solver->optimize();
+    h->solved = true;
+    for (std::size_t b = 0; b < res.size(); ++b)
+    {
+      const auto& r = res[b];
+      std::copy(r.x.begin(), r.x.end(), x + b * r.x.size());
+      if (results)
+        toResult(r, results[b]);
+    }
+    setErr(err, err_len, "");
+    return 0;
+  }
+  catch (const std::exception& e)
+  {
+    setErr(err, err_len, e.what());
+    return -1;
+  }
+}
+
+int thost_batch_stats(const thost_batch* h, int* host_loops, long long* qp_launches, long long* qps, double* qp_bytes,
+                      double* qp_seconds)
+{
+  if (!h)
+    return -1;
+  if (host_loops)
+    *host_loops = h->solver->hostLoops() ? 1 : 0;
+  if (qp_launches)
+    *qp_launches = h->solver->qpLaunches();
+  if (qps)
+    *qps = h->solver->qpSolves();
+  if (qp_bytes)
+    *qp_bytes = h->solver->qpBytes();
+  if (qp_seconds)
+    *qp_seconds = h->solver->qpLaunchSeconds();
+  return 0;
+}
+
+void thost_batch_destroy(thost_batch* h) { delete h; }
 }

@@ -1,6 +1,7 @@
 // GpuQPBatcher (gpu_qp_batcher.hpp).
 #include "trajopt_sco/gpu_qp_batcher.hpp"
 
+#include <chrono>
 #include <cstring>
 #include <stdexcept>
 
@@ -125,13 +126,31 @@ void GpuQPBatcher::flushLocked()
           std::copy(r.wy->begin(), r.wy->begin() + static_cast<long>(mm), wy.begin() + static_cast<long>(ku * mm));
         }
       }
+      const auto t0 = std::chrono::steady_clock::now();
       const int rc = thip_qp_solve_some(slot.qp, count, P.data(), q.data(), A.data(), l.data(), u.data(),
                                         &r0.settings, any_warm ? wx.data() : nullptr, any_warm ? wy.data() : nullptr,
                                         any_warm ? mask.data() : nullptr, wr.data(), x.data(), y.data(), info.data());
       if (rc != THIP_OK)
         throw std::runtime_error(std::string("GpuQPBatcher: thip_qp_solve_some: ") + thip_qp_last_error(slot.qp));
+      launch_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       ++launches_;
       qps_ += count;
+      {
+        // the algorithmic-byte model (gpu_qp_batcher.hpp bytes())
+        const double nl = static_cast<double>(thip_qp_factor_nnz(slot.qp)), nP = static_cast<double>(np),
+                     nA = static_cast<double>(na), N = static_cast<double>(n + m);
+        const double per_solve = 2 * 12 * nl + 8 * N;
+        const double per_iter = per_solve + 2 * 12 * nA + 2 * 12 * nP + 8 * (6.0 * n + 8.0 * m);
+        const double per_factor = 12 * (nP + nA) + 12 * nl;
+        for (int k = 0; k < count; ++k)
+        {
+          const thip_qp_info& in = info[static_cast<std::size_t>(k)];
+          admm_iters_ += in.iter;
+          bytes_ += in.iter * per_iter + per_factor;
+          if (in.polish_status != 0)
+            bytes_ += per_factor + (1 + r0.settings.polish_refine_iter) * per_solve;
+        }
+      }
       for (int k = 0; k < count; ++k)
       {
         Request& r = *g[static_cast<std::size_t>(k)];
@@ -147,15 +166,28 @@ void GpuQPBatcher::flushLocked()
         r->error = e.what();
     }
   }
-  // patterns not used this round go (collision QPs change pattern with their contacts)
+  // patterns unused for kKeepRounds rounds go (collision QPs change pattern with
+  // their contacts, and often return to an earlier one: a kept pattern skips
+  // thip_qp_create's symbolic analysis and allocations), and at most kMaxSlots stay
+  constexpr long long kKeepRounds = 8;
+  constexpr std::size_t kMaxSlots = 256;
   for (auto it = cache_.begin(); it != cache_.end();)
-    if (it->second.last_round != round_)
+    if (it->second.last_round + kKeepRounds <= round_)
     {
       thip_qp_destroy(it->second.qp);
       it = cache_.erase(it);
     }
     else
       ++it;
+  while (cache_.size() > kMaxSlots)
+  {
+    auto oldest = cache_.begin();
+    for (auto it = cache_.begin(); it != cache_.end(); ++it)
+      if (it->second.last_round < oldest->second.last_round)
+        oldest = it;
+    thip_qp_destroy(oldest->second.qp);
+    cache_.erase(oldest);
+  }
   for (Request* r : reqs)
     r->done = true;
   cv_.notify_all();

@@ -51,6 +51,16 @@ def load_host():
         L.thost_last_batch_qp_stats.restype = None
         L.thost_set_host_loop_workers.argtypes = [C.c_int]
         L.thost_set_host_loop_workers.restype = None
+        L.thost_batch_create.argtypes = [C.POINTER(C.c_char_p), C.c_int, dp, C.c_int, C.c_int, C.POINTER(C.c_void_p),
+                                         C.c_char_p, C.c_int]
+        L.thost_batch_create.restype = C.c_int
+        L.thost_batch_solve.argtypes = [C.c_void_p, dp, C.POINTER(abi.Result), C.c_char_p, C.c_int]
+        L.thost_batch_solve.restype = C.c_int
+        L.thost_batch_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_longlong),
+                                        C.POINTER(C.c_longlong), dp, dp]
+        L.thost_batch_stats.restype = C.c_int
+        L.thost_batch_destroy.argtypes = [C.c_void_p]
+        L.thost_batch_destroy.restype = None
         L.thost_solve_json.argtypes = [C.c_char_p, dp, C.c_int, C.c_int, dp, C.POINTER(abi.Result),
                                        C.POINTER(C.c_int), C.c_char_p, C.c_int]
         L.thost_solve_json.restype = C.c_int
@@ -147,6 +157,56 @@ def solve_json_stream(batches, scenes=None, devices=(0,), inflight=2):
     return x.reshape(J, B, N, D), [res[j * B:(j + 1) * B] for j in range(J)]
 
 
+class PreparedBatch:
+    """A batch parsed, lowered and set up on its device ahead of the solve
+    (thost_batch_create): `solve()` then runs only the optimisation, which is
+    what bench.py times.  A host-loop batch solves once (its models keep their
+    warm starts)."""
+
+    def __init__(self, texts, scenes=None, device=0):
+        L = load_host()
+        self._L = L
+        self.B = len(texts)
+        desc, _, _, _ = lower_json(texts[0], None if scenes is None else scenes[0])
+        self.shape = (self.B, desc.n_steps, desc.chain.n_dof + (1 if desc.use_time else 0))
+        sc = None if scenes is None else np.ascontiguousarray(scenes, dtype=np.float64)
+        n_prims = 0 if sc is None else sc.shape[1]
+        arr = (C.c_char_p * self.B)(*[t.encode() for t in texts])
+        h = C.c_void_p()
+        err = C.create_string_buffer(4096)
+        if L.thost_batch_create(arr, self.B, _dp(sc), n_prims, device, C.byref(h), err, 4096) != 0:
+            raise HostError(err.value.decode())
+        self._h = h
+
+    def solve(self):
+        """-> (x [B, N, D], list of abi.Result)."""
+        x = np.zeros(self.shape)
+        res = (abi.Result * self.B)()
+        err = C.create_string_buffer(4096)
+        if self._L.thost_batch_solve(self._h, _dp(x), res, err, 4096) != 0:
+            raise HostError(err.value.decode())
+        return x, list(res)
+
+    def stats(self):
+        """{host_loops, qp_launches, qps, qp_bytes, qp_seconds} (thost_batch_stats)."""
+        hl, la, q = C.c_int(0), C.c_longlong(0), C.c_longlong(0)
+        by, sec = np.zeros(1), np.zeros(1)
+        self._L.thost_batch_stats(self._h, C.byref(hl), C.byref(la), C.byref(q), _dp(by), _dp(sec))
+        return {"host_loops": bool(hl.value), "qp_launches": la.value, "qps": q.value,
+                "qp_bytes": float(by[0]), "qp_seconds": float(sec[0])}
+
+    def close(self):
+        if self._h:
+            self._L.thost_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def solve_json(text: str, scene=None, device=0):
     """-> (x [N, D], abi.Result, native) through trajopt::BasicTrustRegionSQP:
     native is True when the problem ran the fused kernel as a batch of one,
@@ -234,4 +294,16 @@ def workload_to_json(wl, b: int) -> str:
         "constraints": cnts,
         "init_info": {"type": "given_traj", "data": np.asarray(wl.init[b]).tolist()},
     }
+    return json.dumps(doc)
+
+
+def hostloop_workload_json(wl, b: int, acc_coeff: float = 1.0) -> str:
+    """Problem b of `wl` with a JointAcc cost added (coefficient `acc_coeff`,
+    zero targets, every step): joint_costs_unit's term next to the synthetic
+    problem's costs.  The fused kernel does not lower JointAcc, so the problem
+    runs the host SQP loop with its QPs batched on the device (bench.py
+    --config HB)."""
+    doc = json.loads(workload_to_json(wl, b))
+    D = wl.n_dof
+    doc["costs"].append({"type": "joint_acc", "params": {"coeffs": [acc_coeff] * D, "targets": [0.0] * D}})
     return json.dumps(doc)
