@@ -200,12 +200,12 @@ def pmc_evidence(config):
     return best
 
 
-HOSTLOOP_BASE = "B"  # bench --config HB: config B's problems + a JointAcc cost
+HOSTLOOP_BASE = "B"  # bench --config HB: config B's problems + JointAcc and JointJerk costs
 
 
 def hostloop_workload_name(wl, batch):
     return (f"config HB: {wl.n_dof}-DoF PR2 arm x {wl.n_steps} waypoints, JointVel + {wl.desc.n_cart} CartPose "
-            f"ABS costs (config {HOSTLOOP_BASE}) + a JointAcc cost (joint_costs_unit), batch {batch} per GPU "
+            f"ABS costs (config {HOSTLOOP_BASE}) + JointAcc + JointJerk costs (joint_costs_unit), batch {batch} per GPU "
             "(host BasicTrustRegionSQP loops, GpuModel QPs batched one launch per round)")
 
 
@@ -269,7 +269,7 @@ def main_hostloop(args, world, rank, local_rank, json_out):
         launches = float(np.mean([s["qp_launches"] for s in st]))
         achieved = qp_bytes / qp_s / 1e9
         out = {
-            "metric": "SQP iters/sec + achieved HBM GB/s, 7-DoF x 30-wpt host-loop batch (JointAcc, not lowered)",
+            "metric": "SQP iters/sec + achieved HBM GB/s, 7-DoF x 30-wpt host-loop batch (JointAcc/Jerk, not lowered)",
             "value": iters_total * args.steps / elapsed,
             "unit": "SQP iters/s",
             "n_gpus": world,
@@ -280,7 +280,7 @@ def main_hostloop(args, world, rank, local_rank, json_out):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": f"synthetic (config {HOSTLOOP_BASE} seeds 20261015+b written as TrajOptRequest JSON, + JointAcc)",
+            "data": f"synthetic (config {HOSTLOOP_BASE} seeds 20261015+b written as TrajOptRequest JSON, + JointAcc + JointJerk)",
             "config": {
                 "workload": hostloop_workload_name(wl, args.batch),
                 "batch_per_gpu": args.batch,

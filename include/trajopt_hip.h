@@ -552,9 +552,15 @@ int thip_debug_layout(thip_ctx* ctx, long long* doff, long long* ioff, long long
 #define THIP_DEBUG_STATIC_DISPATCH 8  /* one workgroup per problem instead of persistent workgroups taking
                                          problems from a counter (bitwise the same results) */
 #define THIP_DEBUG_GEN_BUILD 16       /* QPs outside the segment's domain run the generic-step build
-                                         (1024 threads, no segment) instead of the 256-thread build */
+                                         (512 threads, no segment) instead of the 256-thread build */
 int thip_debug_set_path(int flags);
 int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws);
+/* The solve layout a context chose (diagnostic): out[0] block-solve branches
+ * (Layout::nbr), out[1] dofs per block, out[2] wide blocks, out[3] the
+ * register-resident segment possible, out[4] the generic-step build,
+ * out[5] threads per problem.  n: entries of out (<= 6 written). */
+#define THIP_LAYOUT_INFO_N 6
+int thip_debug_solve_layout(const thip_ctx* ctx, int* out, int n);
 
 /* ------------------------------------------------------- Term evaluation
  * The kinematic terms of one problem structure evaluated on the device for

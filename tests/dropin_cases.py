@@ -27,6 +27,17 @@ def text(name):
     return (GOLDEN / name).read_text()
 
 
+def json_batch_workload(texts, host):
+    """JSON problems of one structure (every problem lowers to the same
+    description; targets and initial trajectories differ) as one Workload."""
+    from trajopt_amd.problems import Workload
+
+    low = [host.lower_json(t) for t in texts]
+    init = np.stack([v[1] for v in low])
+    return Workload("json-batch", low[0][0], init, np.stack([v[2] for v in low]), np.zeros((len(texts), 0, 16)),
+                    init.copy(), None)
+
+
 def json_workload(text_, host, prims=None):
     """The JSON problem lowered by the host front door as a one-problem Workload
     (scene = the built-in environment's primitives, then `prims`)."""

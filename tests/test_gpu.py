@@ -1160,19 +1160,31 @@ def test_sqp_parity_forced_paths(oracle_mod, cfg, B, path, hip):
     assert same >= 0.85 * B, f"{cfg}: {name} path and segment agree on {same} of {B} problems"
 
 
-def test_sqp_parity_dual_arm_E_unsplit(oracle_mod, hip):
-    """Config E through the single 14-dof wide-block solve (THIP_DEBUG_NO_BRANCH:
-    block_chain_wide, twisted_middle_wide, chain matrices in HBM) against the
-    oracle and against the default two-branch solve."""
+def test_sqp_parity_dual_arm_E_branches(oracle_mod, hip):
+    """The two-branch block solve (Layout::nbr = 2: two independent 7-dof block
+    chains) on config E's scene-only variant: without the inter-arm self pairs
+    no term couples the arms, so the default layout splits them; against the
+    oracle, and against the single 14-dof wide-block solve of the same problems
+    (THIP_DEBUG_NO_BRANCH: block_chain_wide, twisted_middle_wide, chain
+    matrices in HBM -- the layout config E with its self pairs takes)."""
+    from trajopt_amd.runtime import BatchTrustRegionSQP
+
     wl = problems.make_workload("E", 8)
+    wl.desc.n_self_pairs = 0
+    s = BatchTrustRegionSQP(wl)
+    assert s.layout()["nbr"] == 2 and s.layout()["block_dofs"] == 7, s.layout()
+    s.close()
     x_br, res_br, _ = solve_gpu(wl)
     assert hip.thip_debug_set_path(abi.DEBUG_NO_BRANCH) == 0
     try:
+        s = BatchTrustRegionSQP(wl)
+        assert s.layout()["nbr"] == 1 and s.layout()["wide"] == 1, s.layout()
+        s.close()
         x, res, _ = solve_gpu(wl)
     finally:
         hip.thip_debug_set_path(0)
     xo, ro = oracle_mod.solve(wl, n_threads=16)
-    for xs, rs, name in ((x, res, "E-unsplit"), (x_br, res_br, "E-branches")):
+    for xs, rs, name in ((x_br, res_br, "E-scene-branches"), (x, res, "E-scene-unsplit")):
         assert all(r.flags == 0 for r in rs)
         check_parity(wl, oracle_mod, xs, rs, label=name, oracle=(xo, ro))
     same = sum(int(a.status == b.status and np.abs(xa - xb).max() <= TOL_X) for a, b, xa, xb in zip(res, res_br, x, x_br))

@@ -22,7 +22,7 @@ import numpy as np
 import pytest
 
 import dropin_cases as dc
-from parity import JITTER, TOL_X, check_parity
+from parity import TOL_X, check_parity
 from trajopt_amd import abi, host, problems
 from trajopt_amd.runtime import TermEvaluator
 
@@ -185,49 +185,35 @@ def test_cartpose_with_user_cost(oracle_mod):
                                      C.c_int]
     dp = lambda a: None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
 
-    def oracle_user_cost(lw, variant="exact", seed=0):
+    def oracle_user_cost(lw, variant):
+        """oracle_solve_user_cost over every problem of lw (the parity gate's solver)."""
         OL = oracle_mod.lib(variant)
         OL.oracle_solve_user_cost.argtypes = [C.POINTER(abi.ProblemDesc)] + [C.POINTER(C.c_double)] * 5 + \
             [C.POINTER(abi.Result)]
-        if seed:
-            oracle_mod.set_jitter(*JITTER[:3], seed=seed, variant=variant)
-            oracle_mod.set_jitter_coll(JITTER[3], variant=variant)
-        try:
-            xo = np.zeros((lw.n_steps, lw.n_dof))
+        xs, rs = np.zeros((lw.batch, lw.n_steps, lw.n_dof)), []
+        for k in range(lw.batch):
             ro = abi.Result()
-            jt = None if lw.jpos_targets is None else np.ascontiguousarray(lw.jpos_targets[0])
-            assert OL.oracle_solve_user_cost(C.byref(lw.desc), dp(np.ascontiguousarray(lw.init[0])),
-                                             dp(np.ascontiguousarray(lw.targets[0])), None, dp(jt), dp(xo),
+            xo = np.zeros((lw.n_steps, lw.n_dof))
+            jt = None if lw.jpos_targets is None else np.ascontiguousarray(lw.jpos_targets[k])
+            assert OL.oracle_solve_user_cost(C.byref(lw.desc), dp(np.ascontiguousarray(lw.init[k])),
+                                             dp(np.ascontiguousarray(lw.targets[k])), None, dp(jt), dp(xo),
                                              C.byref(ro)) == 0
-        finally:
-            if seed:
-                oracle_mod.set_jitter(0.0, 0.0, 0.0, seed=0, variant=variant)
-                oracle_mod.set_jitter_coll(0.0, variant=variant)
-        return xo, ro
+            xs[k] = xo
+            rs.append(ro)
+        return xs, rs
 
-    for b in range(wl.batch):
-        text = host.workload_to_json(wl, b)
+    texts = [host.workload_to_json(wl, b) for b in range(wl.batch)]
+    xg, rg = np.zeros((wl.batch, wl.n_steps, wl.n_dof)), []
+    for b, text in enumerate(texts):
         x = np.zeros((wl.n_steps, wl.n_dof))
         res = abi.Result()
         err = C.create_string_buffer(2048)
         assert L.sco_case_user_cost(text.encode(), 0, dp(x), C.byref(res), err, 2048) == 0, err.value.decode()
-        lw = dc.json_workload(text, host)
-        xo, ro = oracle_user_cost(lw)
-        dx = np.abs(x - xo).max()
-        print(f"user cost problem {b}: status {res.status} vs {ro.status}, |dx| {dx:.2e}")
-        if res.status == ro.status and dx <= TOL_X:
-            continue
-        # the parity gate's proof (tests/parity.py) on this problem: oracle reruns under
-        # rounding jitter, both builds; reach, or spread with the GPU inside the cloud
-        cloud = [oracle_user_cost(lw, variant, seed) for seed in range(1, 17)
-                 for variant in (("exact", "fast") if seed <= 8 else ("exact",))]
-        reach = any(r.status == res.status and np.abs(xm - x).max() <= TOL_X for xm, r in cloud)
-        xs = np.stack([xo] + [xm for xm, _ in cloud])
-        sp = max(np.abs(xm - xo).max() for xm, _ in cloud)
-        inside = bool(np.all(x >= xs.min(0) - TOL_X) and np.all(x <= xs.max(0) + TOL_X))
-        spread = res.status == ro.status and sp > TOL_X and dx <= sp and inside
-        print(f"  cloud of {len(cloud)}: reach {reach}, spread {sp:.2e}, GPU inside {inside}")
-        assert reach or spread, f"user cost problem {b}: |dx| {dx:.2e} without proof"
+        xg[b] = x
+        rg.append(res)
+    # the one parity gate (tests/parity.py), its reruns through the user-cost oracle
+    check_parity(dc.json_batch_workload(texts, host), oracle_mod, xg, rg, label="dropin-user-cost", min_strict=0.0,
+                 solver=oracle_user_cost)
 
 
 def test_callback_runs_the_host_loop(oracle_mod, tmp_path):
@@ -305,3 +291,28 @@ def test_large_scene_runs_the_generic_path(oracle_mod):
         wl = dc.json_workload(text, host, prims)
         assert wl.desc.n_prims == 19
         check_parity(wl, oracle_mod, x[None], [res], label="dropin-19-primitives", min_strict=0.0)
+
+
+def test_prepared_hostloop_batch(oracle_mod):
+    """bench.py --config HB's problems (config B + joint_costs_unit's JointAcc
+    and JointJerk costs, which the fused kernel does not lower) through the
+    prepared-batch C-ABI (thost_batch_create / _solve / _stats): every
+    problem's host loop at once, each QP round one launch per pattern; parity
+    with the oracle; a prepared host-loop batch solves once."""
+    from trajopt_amd import sharding
+
+    B = 16
+    wl = sharding.rank_workload("B", B, 0)
+    texts = [host.hostloop_workload_json(wl, b) for b in range(B)]
+    pb = host.PreparedBatch(texts)
+    try:
+        x, res = pb.solve()
+        st = pb.stats()
+        assert st["host_loops"]
+        assert 0 < st["qp_launches"] < st["qps"] and st["qp_bytes"] > 0 and st["qp_seconds"] > 0
+        assert st["qps"] >= B
+        with pytest.raises(host.HostError):
+            pb.solve()
+    finally:
+        pb.close()
+    check_parity(dc.json_batch_workload(texts, host), oracle_mod, x, res, label="dropin-HB")

@@ -24,7 +24,7 @@ namespace thip
 constexpr int kBlock = THIP_KBLOCK;
 constexpr int kWaves = kBlock / 64;
 #ifndef THIP_GEN_BLOCK
-#define THIP_GEN_BLOCK 1024
+#define THIP_GEN_BLOCK 512
 #endif
 constexpr int kGenBlock = THIP_GEN_BLOCK;  // threads of the generic-step build
 // waves that run the contact scan's per-wave step pairs (their sub-state

@@ -133,6 +133,17 @@ void thip_default_osqp_settings(thip_osqp_settings* s)
 // thip_debug_set_path: diagnostic solve-path overrides for contexts created afterwards
 static int g_debug_path = 0;
 
+int thip_debug_solve_layout(const thip_ctx* ctx, int* out, int n)
+{
+  if (!ctx || !out || n < 0)
+    return THIP_E_INVALID;
+  const int v[THIP_LAYOUT_INFO_N] = {ctx->L.nbr, ctx->L.sD, ctx->L.wide, ctx->L.seg_ok, ctx->gen ? 1 : 0,
+                                     ctx->gen ? kGenBlock : kBlock};
+  for (int k = 0; k < n && k < THIP_LAYOUT_INFO_N; ++k)
+    out[k] = v[k];
+  return THIP_OK;
+}
+
 int thip_debug_set_path(int flags)
 {
   if (flags & ~(THIP_DEBUG_NO_SEGMENT | THIP_DEBUG_FORCE_WIDE | THIP_DEBUG_NO_BRANCH | THIP_DEBUG_STATIC_DISPATCH |

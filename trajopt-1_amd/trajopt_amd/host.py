@@ -297,13 +297,13 @@ def workload_to_json(wl, b: int) -> str:
     return json.dumps(doc)
 
 
-def hostloop_workload_json(wl, b: int, acc_coeff: float = 1.0) -> str:
-    """Problem b of `wl` with a JointAcc cost added (coefficient `acc_coeff`,
-    zero targets, every step): joint_costs_unit's term next to the synthetic
-    problem's costs.  The fused kernel does not lower JointAcc, so the problem
-    runs the host SQP loop with its QPs batched on the device (bench.py
-    --config HB)."""
+def hostloop_workload_json(wl, b: int, acc_coeff: float = 1.0, jerk_coeff: float = 0.5) -> str:
+    """Problem b of `wl` with joint_costs_unit's JointAcc and JointJerk costs
+    added (every step, zero targets; trajopt/test/joint_costs_unit.cpp): the
+    fused kernel lowers neither, so the problem runs the host SQP loop with its
+    QPs batched on the device (bench.py --config HB)."""
     doc = json.loads(workload_to_json(wl, b))
     D = wl.n_dof
     doc["costs"].append({"type": "joint_acc", "params": {"coeffs": [acc_coeff] * D, "targets": [0.0] * D}})
+    doc["costs"].append({"type": "joint_jerk", "params": {"coeffs": [jerk_coeff] * D, "targets": [0.0] * D}})
     return json.dumps(doc)
