@@ -594,6 +594,13 @@ int thip_eval_upload(thip_eval* ev, const double* cart_targets, const double* sc
  * error alone.  All six components: the caller keeps those whose coefficient is
  * nonzero (CartPoseTermInfo::hatch's indices). */
 int thip_eval_cart_pose(thip_eval* ev, int term, const double* q, double* err, double* jac);
+/* Every CartPose term of every problem at its own waypoint of the joint
+ * trajectories x [batch][n_steps][n_dof], in one launch: err
+ * [batch][n_cart][6], jac [batch][n_cart][6][n_dof] or NULL.  Bitwise the
+ * values thip_eval_cart_pose gives term by term (the same device function);
+ * the host loop evaluates all its CartPose terms at a new x with it instead of
+ * one launch per term (sco::OptProb::prefetch). */
+int thip_eval_cart_pose_all(thip_eval* ev, const double* x, double* err, double* jac);
 /* Collision term `term` (0: the coll_* term when coll_enabled, then coll_extra[])
  * at trajectories x [batch][n_steps][n_dof]: every contact of every unit (a free
  * waypoint of [first, last] for DISCRETE, else a step pair) with its linearised
@@ -658,6 +665,10 @@ const char* thip_qp_last_error(thip_qp* qp); /* NULL: the last thip_qp_create fa
 /* Entries of the KKT factor L of the pattern (the symbolic analysis of
  * thip_qp_create): the algorithmic-byte model of the QP solves; -1 for NULL. */
 long long thip_qp_factor_nnz(const thip_qp* qp);
+/* The pattern's KKT shape: out[0] N = n + m, out[1] entries of L, out[2]
+ * elimination-tree levels (the solve's serial depth), out[3] the widest level
+ * (diagnostic; -1 for NULL). */
+int thip_qp_shape(const thip_qp* qp, long long* out);
 
 /* Resident workspace (update in place).  The OSQP 1.0 solver object of every QP
  * of the batch stays on the device between calls, as OsqpEigen::Solver keeps it

@@ -73,6 +73,9 @@ int thost_batch_create(const char* const* json_texts, int batch, const double* s
 int thost_batch_solve(thost_batch* b, double* x, thip_result* results, char* err, int err_len);
 int thost_batch_stats(const thost_batch* b, int* host_loops, long long* qp_launches, long long* qps, double* qp_bytes,
                       double* qp_seconds);
+/* Host-loop batches (diagnostic): out[0] ADMM iterations of all QPs, then the
+ * largest KKT's N, entries of L, elimination-tree levels and widest level. */
+int thost_batch_qp_shape(const thost_batch* b, long long* out);
 void thost_batch_destroy(thost_batch* b);
 
 /* thost_solve_json_batch sharded over n_devices HIP devices of this process

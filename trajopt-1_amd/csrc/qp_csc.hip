@@ -49,6 +49,7 @@
 namespace thip_qp_dev
 {
 constexpr int kQB = 256;
+constexpr long long kQpLdsBudget = 150 * 1024;  // dynamic LDS of a QP workgroup with its factor staged
 constexpr double kInf = 1e30;             // OSQP_INFTY
 constexpr double kRhoMin = 1e-6, kRhoMax = 1e6, kRhoTol = 1e-4, kRhoEq = 1e3;
 constexpr double kMinScaling = 1e-4, kMaxScaling = 1e4;
@@ -116,6 +117,11 @@ struct QpPattern
   const int *perm, *lrp, *lrj, *lcp, *lci, *lcpos, *lksrc, *dpd, *lvp, *lvn, *fip, *fik, *fic;
   int nlev;
   int lds_vec;  // the permuted solve vector lives in LDS (else W_LV)
+  // the whole factor in LDS (QP_LDS_*, staged at kernel entry): the solve
+  // vector, L and D, and the index arrays the factor and the solves walk
+  // (16-bit row / column indices)
+  int lds_pat;
+  long long lds_off[8];
   long long off[W_COUNT];
   long long stride;
 };
@@ -197,6 +203,21 @@ __device__ __forceinline__ double limit_scaling(double a)
   return a > kMaxScaling ? kMaxScaling : a;
 }
 
+// The arrays the factorisation and the solves walk: the pattern's (HBM) or
+// their LDS copies (QpPattern::lds_pat: 16-bit indices)
+template <typename IX>
+struct FacView
+{
+  const IX *lrj, *lcpos, *lci, *lvn;
+  const int *lrp, *lcp, *lvp;
+  double *LX, *DG;
+};
+// LDS layout of a staged factor (QpPattern::lds_off)
+enum : int
+{
+  QL_LX = 0, QL_DG, QL_LRJ, QL_LCPOS, QL_LCI, QL_LVN, QL_LRP, QL_LVP  // (lcp follows lrp)
+};
+
 struct Qp
 {
   const QpPattern& p;
@@ -205,8 +226,52 @@ struct Qp
   Sh& sh;
   double* lv;  // the permuted solve vector [N] (LDS, or W_LV)
   int n, m;
+  FacView<int> fg;              // HBM
+  FacView<unsigned short> fs;   // LDS (p.lds_pat)
+  bool persist;                 // keep W_LX / W_DG current (resident workspaces)
   __device__ double* a(int k) const { return w + p.off[k]; }
 };
+
+// Qp's factor views; with lds_pat, stage the index arrays and the current
+// factor (W_LX, W_DG) into the dynamic LDS after the solve vector.  All threads.
+__device__ void fac_views(Qp& q, char* lds)
+{
+  const QpPattern& p = q.p;
+  q.fg = FacView<int>{ p.lrj, p.lcpos, p.lci, p.lvn, p.lrp, p.lcp, p.lvp, q.a(W_LX), q.a(W_DG) };
+  if (!p.lds_pat)
+    return;
+  const int N = p.N, nl = static_cast<int>(p.lds_off[QL_DG] - p.lds_off[QL_LX]) / 8;  // entries of L
+  double* LX = reinterpret_cast<double*>(lds + p.lds_off[QL_LX]);
+  double* DG = reinterpret_cast<double*>(lds + p.lds_off[QL_DG]);
+  unsigned short* lrj = reinterpret_cast<unsigned short*>(lds + p.lds_off[QL_LRJ]);
+  unsigned short* lcpos = reinterpret_cast<unsigned short*>(lds + p.lds_off[QL_LCPOS]);
+  unsigned short* lci = reinterpret_cast<unsigned short*>(lds + p.lds_off[QL_LCI]);
+  unsigned short* lvn = reinterpret_cast<unsigned short*>(lds + p.lds_off[QL_LVN]);
+  int* lrp = reinterpret_cast<int*>(lds + p.lds_off[QL_LRP]);
+  int* lcp = lrp + (N + 1);
+  int* lvp = reinterpret_cast<int*>(lds + p.lds_off[QL_LVP]);
+  const double *GX = q.a(W_LX), *GD = q.a(W_DG);
+  QFOR(e, nl)
+  {
+    LX[e] = GX[e];
+    lrj[e] = static_cast<unsigned short>(p.lrj[e]);
+    lcpos[e] = static_cast<unsigned short>(p.lcpos[e]);
+    lci[e] = static_cast<unsigned short>(p.lci[e]);
+  }
+  QFOR(k, N)
+  {
+    DG[k] = GD[k];
+    lvn[k] = static_cast<unsigned short>(p.lvn[k]);
+  }
+  QFOR(k, N + 1)
+  {
+    lrp[k] = p.lrp[k];
+    lcp[k] = p.lcp[k];
+  }
+  QFOR(l, p.nlev + 1) lvp[l] = p.lvp[l];
+  q.fs = FacView<unsigned short>{ lrj, lcpos, lci, lvn, lrp, lcp, lvp, LX, DG };
+  __syncthreads();
+}
 
 // y = A x (rows), y = A' x (columns), y = P x (full symmetric from the upper triangle)
 __device__ void a_mul(const Qp& q, const double* x, double* y)
@@ -404,23 +469,36 @@ __device__ __forceinline__ double kkt_diag(const Qp& q, int k, bool pol, const d
 //     L_ik = (K_ik - sum_{j < k} L_ij D_j L_kj) / D_k
 // as a merge of rows i and k (both ascending).  sh.npos = positive pivots,
 // sh.fail = 1 on a zero / non-finite pivot.
-__device__ void kkt_factor(Qp& q, bool pol)
+template <typename IX>
+__device__ void kkt_factor_v(Qp& q, const FacView<IX>& f, bool pol)
 {
   const QpPattern& p = q.p;
-  double *LX = q.a(W_LX), *DG = q.a(W_DG);
+  double *LX = f.LX, *DG = f.DG;
   const double* FLG = q.a(W_FLG);
   double bad = 0, npos = 0;
+  // one-node levels (the chain) with the solve vector in LDS: row k of L is
+  // scattered into the (otherwise zero) vector LDS, so an entry's merge of
+  // rows i and k becomes a branch-free walk of row i's prefix (its entries
+  // before column k, lcpos order) -- (L_ij D_j) L_kj for the shared j, exact
+  // zeros for the rest: bitwise the merge's sum.  The vector is zero between levels.
+  double* dense = q.lv;
+  const bool scatter = p.lds_vec;
+  if (scatter)
+  {
+    QFOR(k, p.N) dense[k] = 0.0;
+    __syncthreads();
+  }
   for (int lev = 0; lev < p.nlev; ++lev)
   {
-    const int n1 = p.lvp[lev + 1];
-    for (int t = p.lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
+    const int n0 = f.lvp[lev], n1 = f.lvp[lev + 1];
+    for (int t = n0 + static_cast<int>(threadIdx.x); t < n1; t += kQB)
     {
-      const int k = p.lvn[t];
+      const int k = f.lvn[t];
       double d = kkt_diag(q, k, pol, FLG);
-      for (int e = p.lrp[k]; e < p.lrp[k + 1]; ++e)
+      for (int e = f.lrp[k]; e < f.lrp[k + 1]; ++e)
       {
         const double l = LX[e];
-        d -= (l * DG[p.lrj[e]]) * l;
+        d -= (l * DG[f.lrj[e]]) * l;
       }
       DG[k] = d;
       if (d == 0.0 || !isfinite(d))
@@ -428,29 +506,57 @@ __device__ void kkt_factor(Qp& q, bool pol)
       else if (d > 0)
         npos += 1;
     }
-    __syncthreads();
-    const int f1 = p.fip[lev + 1];
-    for (int t = p.fip[lev] + static_cast<int>(threadIdx.x); t < f1; t += kQB)
+    const int f0 = p.fip[lev], f1 = p.fip[lev + 1];
+    if (scatter && n1 - n0 == 1)
     {
-      const int k = p.fik[t], c = p.fic[t], i = p.lci[c];
-      double s = kkt_entry(q, p.lksrc[c], pol, FLG);
-      int a = p.lrp[i], b = p.lrp[k];
-      const int ae = p.lrp[i + 1], be = p.lrp[k + 1];
-      while (a < ae && b < be)
+      const int k = f.lvn[n0];
+      const int r0 = f.lrp[k], r1 = f.lrp[k + 1];
+      for (int e = r0 + static_cast<int>(threadIdx.x); e < r1; e += kQB)
+        dense[f.lrj[e]] = LX[e];
+      __syncthreads();
+      const double dk = DG[k];
+      for (int t = f0 + static_cast<int>(threadIdx.x); t < f1; t += kQB)
       {
-        const int ja = p.lrj[a], jb = p.lrj[b];
-        if (ja == jb)
+        const int c = p.fic[t], i = f.lci[c];
+        double s = kkt_entry(q, p.lksrc[c], pol, FLG);
+        const int ae = f.lcpos[c];  // entry (i, k)'s place in row i: the entries before it have j < k
+#pragma unroll 4
+        for (int a = f.lrp[i]; a < ae; ++a)
         {
-          s -= (LX[a] * DG[ja]) * LX[b];
-          ++a;
-          ++b;
+          const int ja = f.lrj[a];
+          s -= (LX[a] * DG[ja]) * dense[ja];
         }
-        else if (ja < jb)
-          ++a;
-        else
-          ++b;
+        LX[ae] = s / dk;
       }
-      LX[p.lcpos[c]] = s / DG[k];
+      __syncthreads();
+      for (int e = r0 + static_cast<int>(threadIdx.x); e < r1; e += kQB)
+        dense[f.lrj[e]] = 0.0;
+    }
+    else
+    {
+      __syncthreads();
+      for (int t = f0 + static_cast<int>(threadIdx.x); t < f1; t += kQB)
+      {
+        const int k = p.fik[t], c = p.fic[t], i = f.lci[c];
+        double s = kkt_entry(q, p.lksrc[c], pol, FLG);
+        int a = f.lrp[i], b = f.lrp[k];
+        const int ae = f.lrp[i + 1], be = f.lrp[k + 1];
+        while (a < ae && b < be)
+        {
+          const int ja = f.lrj[a], jb = f.lrj[b];
+          if (ja == jb)
+          {
+            s -= (LX[a] * DG[ja]) * LX[b];
+            ++a;
+            ++b;
+          }
+          else if (ja < jb)
+            ++a;
+          else
+            ++b;
+        }
+        LX[f.lcpos[c]] = s / DG[k];
+      }
     }
     __syncthreads();
   }
@@ -464,13 +570,36 @@ __device__ void kkt_factor(Qp& q, bool pol)
   __syncthreads();
 }
 
+__device__ void kkt_factor(Qp& q, bool pol)
+{
+  if (!q.p.lds_pat)
+  {
+    kkt_factor_v(q, q.fg, pol);
+    return;
+  }
+  kkt_factor_v(q, q.fs, pol);
+  if (q.persist)  // the resident workspace's copy (the next launch stages it)
+  {
+    const int nl = static_cast<int>(q.p.lds_off[QL_DG] - q.p.lds_off[QL_LX]) / 8;
+    double *GX = q.a(W_LX), *GD = q.a(W_DG);
+    QFOR(e, nl) GX[e] = q.fs.LX[e];
+    QFOR(k, q.p.N) GD[k] = q.fs.DG[k];
+    __syncthreads();
+  }
+}
+
 // in place solve K v = b for v[0..N) in the QP's workspace (original order):
 // gather into the permuted vector, L forward by levels up the tree (rows of
-// L), D, L' backward by levels down the tree (columns of L), scatter back
-__device__ void kkt_solve(Qp& q, double* v)
+// L), D, L' backward by levels down the tree (columns of L), scatter back.
+// With the factor staged in LDS (QpPattern::lds_pat) every access of a level
+// is an LDS access: a level costs a few LDS round trips and a barrier instead
+// of a chain of dependent HBM loads (level pointer -> node -> row bounds ->
+// entries), which set the pace of the HBM form.
+template <typename IX>
+__device__ void kkt_solve_v(Qp& q, const FacView<IX>& f, double* v)
 {
   const QpPattern& p = q.p;
-  const double *LX = q.a(W_LX), *DG = q.a(W_DG);
+  const double *LX = f.LX, *DG = f.DG;
   double* w = q.lv;
   const int N = p.N;
   __syncthreads();
@@ -478,13 +607,13 @@ __device__ void kkt_solve(Qp& q, double* v)
   __syncthreads();
   for (int lev = 0; lev < p.nlev; ++lev)
   {
-    const int n1 = p.lvp[lev + 1];
-    for (int t = p.lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
+    const int n1 = f.lvp[lev + 1];
+    for (int t = f.lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
     {
-      const int k = p.lvn[t];
+      const int k = f.lvn[t];
       double s = w[k];
-      for (int e = p.lrp[k]; e < p.lrp[k + 1]; ++e)
-        s -= LX[e] * w[p.lrj[e]];
+      for (int e = f.lrp[k]; e < f.lrp[k + 1]; ++e)
+        s -= LX[e] * w[f.lrj[e]];
       w[k] = s;
     }
     __syncthreads();
@@ -493,19 +622,27 @@ __device__ void kkt_solve(Qp& q, double* v)
   __syncthreads();
   for (int lev = p.nlev - 1; lev >= 0; --lev)
   {
-    const int n1 = p.lvp[lev + 1];
-    for (int t = p.lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
+    const int n1 = f.lvp[lev + 1];
+    for (int t = f.lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
     {
-      const int k = p.lvn[t];
+      const int k = f.lvn[t];
       double s = w[k];
-      for (int c = p.lcp[k]; c < p.lcp[k + 1]; ++c)
-        s -= LX[p.lcpos[c]] * w[p.lci[c]];
+      for (int c = f.lcp[k]; c < f.lcp[k + 1]; ++c)
+        s -= LX[f.lcpos[c]] * w[f.lci[c]];
       w[k] = s;
     }
     __syncthreads();
   }
   QFOR(k, N) v[p.perm[k]] = w[k];
   __syncthreads();
+}
+
+__device__ void kkt_solve(Qp& q, double* v)
+{
+  if (q.p.lds_pat)
+    kkt_solve_v(q, q.fs, v);
+  else
+    kkt_solve_v(q, q.fg, v);
 }
 
 __device__ double prim_res(Qp& q, const double* x, const double* z)
@@ -933,7 +1070,8 @@ __global__ __launch_bounds__(kQB) void qp_csc_kernel(QpArgs args)
   const QpPattern& P = args.pat;
   const int n = P.n, m = P.m;
   double* w = args.ws + (long long)b * P.stride;
-  Qp q{ P, args.s, w, sh, P.lds_vec ? lv : w + P.off[W_LV], n, m };
+  Qp q{ P, args.s, w, sh, P.lds_vec ? lv : w + P.off[W_LV], n, m, {}, {}, false };
+  fac_views(q, reinterpret_cast<char*>(lv));
   // data (scaled in place)
   {
     double *PX = q.a(W_PX), *AX = q.a(W_AX), *Q = q.a(W_Q), *L = q.a(W_L), *U = q.a(W_U);
@@ -1076,7 +1214,8 @@ __global__ __launch_bounds__(kQB) void qp_resident_kernel(QpArgs args, int op)
   const QpPattern& P = args.pat;
   const int n = P.n, m = P.m;
   double* w = args.ws + (long long)b * P.stride;
-  Qp q{ P, args.s, w, sh, P.lds_vec ? lv : w + P.off[W_LV], n, m };
+  Qp q{ P, args.s, w, sh, P.lds_vec ? lv : w + P.off[W_LV], n, m, {}, {}, true };
+  fac_views(q, reinterpret_cast<char*>(lv));
   double* SC = q.a(W_SC);
   thip_qp_info* info = args.info + b;
   const bool sc = args.s.scaling > 0;
@@ -1266,6 +1405,7 @@ struct thip_qp
 {
   int device = 0, batch = 0, n = 0, m = 0, nnz_p = 0, nnz_a = 0;
   long long nnz_l = 0;  // entries of the KKT factor L (thip_qp_factor_nnz)
+  int max_level = 0;    // nodes of the widest elimination-tree level (thip_qp_shape)
   QpPattern pat{};
   int* d_idx = nullptr;
   double* d_ws = nullptr;
@@ -1419,9 +1559,40 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
   q->pat.N = static_cast<int>(N);
   q->in_doubles = (long long)np + na + n + 2LL * m;
   q->pat.nlev = nlev;
+  for (int lv = 0; lv < nlev; ++lv)
+    q->max_level = std::max(q->max_level, S.lvp[static_cast<size_t>(lv) + 1] - S.lvp[static_cast<size_t>(lv)]);
   q->nnz_l = nnzl;
   q->pat.lds_vec = lds_vec ? 1 : 0;
   q->lds = lds_vec ? static_cast<size_t>(N) * sizeof(double) : 0;
+  // the whole factor in LDS when it fits next to the solve vector (16-bit
+  // indices: N and the entries of L below 65536)
+  {
+    const long long nl = std::max(nnzl, 1LL);
+    long long o = N * 8;  // the solve vector first
+    long long offs[8];
+    auto take = [&](int k, long long bytes) {
+      offs[k] = o;
+      o += (bytes + 15) / 16 * 16;
+    };
+    take(QL_LX, nl * 8);
+    take(QL_DG, N * 8);
+    take(QL_LRJ, nl * 2);
+    take(QL_LCPOS, nl * 2);
+    take(QL_LCI, nl * 2);
+    take(QL_LVN, N * 2);
+    take(QL_LRP, 2 * (N + 1) * 4);
+    take(QL_LVP, (nlev + 1) * 4);
+    const bool fits = lds_vec && N < 65536 && nnzl < 65536 && o <= kQpLdsBudget;
+    q->pat.lds_pat = fits ? 1 : 0;
+    if (fits)
+    {
+      // lds_off[QL_DG] - lds_off[QL_LX] = 8 x entries of L exactly (fac_views)
+      offs[QL_DG] = offs[QL_LX] + nl * 8;
+      for (int k = 0; k < 8; ++k)
+        q->pat.lds_off[k] = offs[k];
+      q->lds = static_cast<size_t>(o);
+    }
+  }
   auto fail = [&](const std::string& msg) {
     g_qp_create_err = msg;
     thip_qp_destroy(q);
@@ -1554,6 +1725,9 @@ int thip_qp_solve_some(thip_qp* q, int count, const double* P_values, const doub
   a.info = q->d_info;
   a.ws = q->d_ws;
   a.batch = B;
+  if (q->lds > 65536)
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&qp_csc_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        static_cast<int>(q->lds));
   hipLaunchKernelGGL(qp_csc_kernel, dim3(B), dim3(kQB), q->lds, nullptr, a);
   if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess)
   {
@@ -1637,6 +1811,9 @@ static int qp_resident(thip_qp* q, int op, const double* P_values, const double*
   a.info = q->d_info;
   a.ws = q->d_ws;
   a.batch = B;
+  if (q->lds > 65536)
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&qp_resident_kernel),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(q->lds));
   hipLaunchKernelGGL(qp_resident_kernel, dim3(B), dim3(kQB), q->lds, nullptr, a, op);
   if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess)
   {
@@ -1802,5 +1979,16 @@ void thip_qp_destroy(thip_qp* q)
 const char* thip_qp_last_error(thip_qp* q) { return q ? q->err.c_str() : g_qp_create_err.c_str(); }
 
 long long thip_qp_factor_nnz(const thip_qp* q) { return q ? q->nnz_l : -1; }
+
+int thip_qp_shape(const thip_qp* q, long long* out)
+{
+  if (!q || !out)
+    return THIP_E_INVALID;
+  out[0] = q->pat.N;
+  out[1] = q->nnz_l;
+  out[2] = q->pat.nlev;
+  out[3] = q->max_level;
+  return THIP_OK;
+}
 
 }  // extern "C"

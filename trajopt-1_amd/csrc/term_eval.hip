@@ -107,19 +107,28 @@ struct CartArgs
   double lower_tol[6], upper_tol[6];
 };
 
-__global__ __launch_bounds__(64) void cart_eval_kernel(const thip_chain* chain, CartArgs a, int batch, int n_cart,
-                                                      int term, const double* q, const double* tgt, double* err,
-                                                      double* jac)
+static CartArgs cart_args(const thip_problem_desc& d, int term)
 {
-  const int b = blockIdx.x;
-  if (b >= batch)
-    return;
-  stage_chain_ev(chain);
-  const thip_chain& ch = s_chain;
+  CartArgs a{};
+  a.D = d.chain.n_dof;
+  a.source_link = d.cart_source_link[term];
+  a.target_link = d.cart_target_link[term];
+  a.has_tol = d.cart_has_tol[term];
+  std::memcpy(a.source_offset, d.cart_source_offset[term], sizeof(a.source_offset));
+  std::memcpy(a.lower_tol, d.cart_lower_tol[term], sizeof(a.lower_tol));
+  std::memcpy(a.upper_tol, d.cart_upper_tol[term], sizeof(a.upper_tol));
+  return a;
+}
+
+// One CartPose term at one problem's joint values qb: err[6] and (jac non-null)
+// jac[6][D].  One 64-lane wavefront: lane 0 the error, lane p + 1 the FK
+// perturbed in dof p.  Shared by the one-term and the all-terms kernels, so
+// both give the same bits.
+__device__ void cart_eval_one(const thip_chain& ch, const CartArgs& a, const double* qb, const double* to12,
+                              double* err, double* jac)
+{
   const int D = a.D, lane = threadIdx.x;
   __shared__ Pose s_src, s_tinv;
-  const double* qb = q + static_cast<long long>(b) * D;
-  const double* to12 = tgt + (static_cast<long long>(b) * n_cart + term) * 12;
   if (lane == 0)
   {
     Pose S, So, Ss, Tb, To, Tt, Ti;
@@ -138,7 +147,7 @@ __global__ __launch_bounds__(64) void cart_eval_kernel(const thip_chain* chain, 
     if (a.has_tol)
       apply_tolerances(e, a.lower_tol, a.upper_tol);
     for (int i = 0; i < 6; ++i)
-      err[static_cast<long long>(b) * 6 + i] = e[i];
+      err[i] = e[i];
     s_src = Ss;
     s_tinv = Ti;
   }
@@ -183,9 +192,40 @@ __global__ __launch_bounds__(64) void cart_eval_kernel(const thip_chain* chain, 
     for (int i = 0; i < 3; ++i)
       diff[3 + i] = r1[i] - r0[i];
   }
-  double* jo = jac + static_cast<long long>(b) * 6 * D;
   for (int i = 0; i < 6; ++i)
-    jo[i * D + p] = diff[i] / eps;
+    jac[i * D + p] = diff[i] / eps;
+}
+
+__global__ __launch_bounds__(64) void cart_eval_kernel(const thip_chain* chain, CartArgs a, int batch, int n_cart,
+                                                      int term, const double* q, const double* tgt, double* err,
+                                                      double* jac)
+{
+  const int b = blockIdx.x;
+  if (b >= batch)
+    return;
+  stage_chain_ev(chain);
+  const long long D = a.D;
+  cart_eval_one(s_chain, a, q + b * D, tgt + (static_cast<long long>(b) * n_cart + term) * 12, err + b * 6LL,
+                jac ? jac + b * 6 * D : nullptr);
+}
+
+// every CartPose term of every problem at its own waypoint of the joint
+// trajectories x [batch][N][D]: one workgroup per (problem, term),
+// err [batch][n_cart][6], jac [batch][n_cart][6][D] (or null)
+__global__ __launch_bounds__(64) void cart_eval_all_kernel(const thip_chain* chain, const CartArgs* args,
+                                                          const int* steps, int batch, int n_cart, int N,
+                                                          const double* x, const double* tgt, double* err,
+                                                          double* jac)
+{
+  const int item = blockIdx.x;
+  if (item >= batch * n_cart)
+    return;
+  stage_chain_ev(chain);
+  const int b = item / n_cart, k = item % n_cart;
+  const CartArgs a = args[k];
+  const long long D = a.D;
+  cart_eval_one(s_chain, a, x + (static_cast<long long>(b) * N + steps[k]) * D, tgt + static_cast<long long>(item) * 12,
+                err + item * 6LL, jac ? jac + item * 6 * D : nullptr);
 }
 
 // ------------------------------------------------------------------ collision
@@ -509,6 +549,10 @@ struct thip_eval
   double* d_x = nullptr;      // q / x staging
   double* d_err = nullptr;
   double* d_jac = nullptr;
+  CartArgs* d_cargs = nullptr;  // per CartPose term (cart_eval_all_kernel)
+  int* d_csteps = nullptr;      // per CartPose term: its waypoint
+  double* d_err_all = nullptr;  // [batch][n_cart][6]
+  double* d_jac_all = nullptr;  // [batch][n_cart][6][D]
   double* d_stage = nullptr;  // collision records per unit
   double* d_out = nullptr;    // packed records
   int* d_counts = nullptr;    // per unit, then per problem
@@ -740,6 +784,28 @@ int thip_eval_create(int device, const thip_problem_desc* desc, int batch, thip_
       (e = hipMemsetAsync(ev->d_scene, 0, B * np * 16 * sizeof(double), ev->stream)) != hipSuccess ||
       (e = hipStreamSynchronize(ev->stream)) != hipSuccess)
     return hfail("hipMemcpy", e);
+  // every CartPose term's arguments and waypoint (cart_eval_all_kernel)
+  if (d.n_cart > 0)
+  {
+    std::vector<CartArgs> cargs(static_cast<size_t>(d.n_cart));
+    std::vector<int> steps(static_cast<size_t>(d.n_cart));
+    for (int k = 0; k < d.n_cart; ++k)
+    {
+      cargs[static_cast<size_t>(k)] = cart_args(d, k);
+      steps[static_cast<size_t>(k)] = d.cart_step[k];
+      if (d.cart_step[k] < 0 || d.cart_step[k] >= N)
+        return reject("CartPose term waypoint out of range");
+    }
+    if ((e = hipMalloc(&ev->d_cargs, cargs.size() * sizeof(CartArgs))) != hipSuccess ||
+        (e = hipMalloc(&ev->d_csteps, steps.size() * sizeof(int))) != hipSuccess ||
+        (e = hipMalloc(&ev->d_err_all, B * nc * 6 * sizeof(double))) != hipSuccess ||
+        (e = hipMalloc(&ev->d_jac_all, B * nc * 6 * D * sizeof(double))) != hipSuccess)
+      return hfail("hipMalloc(CartPose terms)", e);
+    if ((e = hipMemcpy(ev->d_cargs, cargs.data(), cargs.size() * sizeof(CartArgs), hipMemcpyHostToDevice)) !=
+            hipSuccess ||
+        (e = hipMemcpy(ev->d_csteps, steps.data(), steps.size() * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)
+      return hfail("hipMemcpy(CartPose terms)", e);
+  }
   // per link-pair margins of each collision term (coefficients are the host's)
   for (size_t k = 0; k < ev->terms.size(); ++k)
   {
@@ -798,14 +864,7 @@ int thip_eval_cart_pose(thip_eval* ev, int term, const double* q, double* err, d
   if (!ev->uploaded)
     return fail(ev, "thip_eval_cart_pose: thip_eval_upload first");
   const int D = d.chain.n_dof;
-  CartArgs a{};
-  a.D = D;
-  a.source_link = d.cart_source_link[term];
-  a.target_link = d.cart_target_link[term];
-  a.has_tol = d.cart_has_tol[term];
-  std::memcpy(a.source_offset, d.cart_source_offset[term], sizeof(a.source_offset));
-  std::memcpy(a.lower_tol, d.cart_lower_tol[term], sizeof(a.lower_tol));
-  std::memcpy(a.upper_tol, d.cart_upper_tol[term], sizeof(a.upper_tol));
+  const CartArgs a = cart_args(d, term);
   const size_t B = static_cast<size_t>(ev->batch);
   hipError_t e;
   if ((e = hipSetDevice(ev->device)) != hipSuccess)
@@ -822,6 +881,38 @@ int thip_eval_cart_pose(thip_eval* ev, int term, const double* q, double* err, d
                   hipSuccess) ||
       (e = hipStreamSynchronize(ev->stream)) != hipSuccess)
     return hipfail(ev, "cart_eval_kernel", e);
+  return THIP_OK;
+}
+
+int thip_eval_cart_pose_all(thip_eval* ev, const double* x, double* err, double* jac)
+{
+  if (!ev)
+    return THIP_E_INVALID;
+  const thip_problem_desc& d = ev->desc;
+  if (!x || !err)
+    return fail(ev, "thip_eval_cart_pose_all: null x / err");
+  if (!ev->uploaded)
+    return fail(ev, "thip_eval_cart_pose_all: thip_eval_upload first");
+  if (d.n_cart == 0)
+    return THIP_OK;
+  const int N = d.n_steps, D = d.chain.n_dof;
+  const size_t B = static_cast<size_t>(ev->batch), nc = static_cast<size_t>(d.n_cart);
+  hipError_t e;
+  if ((e = hipSetDevice(ev->device)) != hipSuccess)
+    return hipfail(ev, "hipSetDevice", e);
+  if ((e = hipMemcpyAsync(ev->d_x, x, B * N * D * sizeof(double), hipMemcpyHostToDevice, ev->stream)) != hipSuccess)
+    return hipfail(ev, "hipMemcpy(x)", e);
+  hipLaunchKernelGGL(cart_eval_all_kernel, dim3(static_cast<unsigned>(B * nc)), dim3(64), 0, ev->stream, ev->d_chain,
+                     ev->d_cargs, ev->d_csteps, ev->batch, d.n_cart, N, ev->d_x, ev->d_tgt, ev->d_err_all,
+                     jac ? ev->d_jac_all : nullptr);
+  if ((e = hipGetLastError()) != hipSuccess)
+    return hipfail(ev, "cart_eval_all_kernel launch", e);
+  if ((e = hipMemcpyAsync(err, ev->d_err_all, B * nc * 6 * sizeof(double), hipMemcpyDeviceToHost, ev->stream)) !=
+          hipSuccess ||
+      (jac && (e = hipMemcpyAsync(jac, ev->d_jac_all, B * nc * 6 * D * sizeof(double), hipMemcpyDeviceToHost,
+                                  ev->stream)) != hipSuccess) ||
+      (e = hipStreamSynchronize(ev->stream)) != hipSuccess)
+    return hipfail(ev, "cart_eval_all_kernel", e);
   return THIP_OK;
 }
 
@@ -913,6 +1004,10 @@ void thip_eval_destroy(thip_eval* ev)
   hipFree(ev->d_x);
   hipFree(ev->d_err);
   hipFree(ev->d_jac);
+  hipFree(ev->d_cargs);
+  hipFree(ev->d_csteps);
+  hipFree(ev->d_err_all);
+  hipFree(ev->d_jac_all);
   hipFree(ev->d_stage);
   hipFree(ev->d_out);
   hipFree(ev->d_counts);

@@ -58,6 +58,8 @@ public:
   // host-loop batches: the QP solves' algorithmic HBM bytes (sco::GpuQPBatcher::bytes)
   double qpBytes() const { return qp_bytes_; }
   double qpLaunchSeconds() const { return qp_launch_s_; }
+  long long qpAdmmIters() const { return qp_admm_; }
+  const long long* qpMaxShape() const { return qp_shape_; }
   // host-loop batches: worker threads (problems solved at once); 0 = the
   // process default (setDefaultHostLoopWorkers, initially 64), never more
   // than the batch
@@ -77,6 +79,7 @@ private:
   std::vector<sco::OptResults> generic_results_;
   long long qp_launches_ = 0, qp_solves_ = 0;
   double qp_bytes_ = 0, qp_launch_s_ = 0;
+  long long qp_admm_ = 0, qp_shape_[4] = { 0, 0, 0, 0 };
   int workers_ = 0;
 };
 

@@ -44,6 +44,10 @@ public:
   // CartPose term k (descriptor order) at its waypoint's joint values q:
   // err[6], jac[6][n_dof] (row-major; may be null)
   void cartPose(int k, const DblVec& q, double* err, double* jac);
+  // every CartPose term at its waypoint of the full variable vector x in one
+  // launch (thip_eval_cart_pose_all); cartPose(k, q) then answers from it while
+  // q is bitwise term k's waypoint of that x
+  void prefetchCart(const DblVec& x);
 
   // the contact records of one collision term (0 = the descriptor's coll_*,
   // then coll_extra[]) at the full variable vector x; W = 8 + 2 n_dof + 1
@@ -71,6 +75,14 @@ private:
     bool valid = false;
   };
   std::vector<Cache> cache_;
+  struct CartCache
+  {
+    DblVec q;                 // the joint trajectory [n_steps][n_dof] of the prefetch
+    std::vector<double> err;  // [n_cart][6]
+    std::vector<double> jac;  // [n_cart][6][n_dof]
+    bool valid = false;
+  } cart_;
+  DblVec jointTrajectory(const DblVec& x) const;
   std::vector<std::vector<double>> pair_tab_;  // per term: pair_data.hpp table, empty = the term's own
 };
 

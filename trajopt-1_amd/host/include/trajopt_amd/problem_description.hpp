@@ -371,6 +371,7 @@ public:
   int device = 0;  // HIP device of the native path and of the device-evaluated terms
   // the evaluator of the CartPose / collision term objects (thip_eval_*)
   const std::shared_ptr<DeviceTermEvaluator>& deviceTerms() const { return device_terms_; }
+  void prefetch(const DblVec& x) override;
 
   friend TrajOptProb::Ptr ConstructProblem(const ProblemConstructionInfo& pci);
 

@@ -63,6 +63,8 @@ public:
   long long admmIters() const { return admm_iters_; }
   // wall seconds inside thip_qp_solve_some (the launches with their transfers)
   double launchSeconds() const { return launch_s_; }
+  // the largest KKT seen: N, entries of L, elimination-tree levels, widest level
+  const long long* maxShape() const { return shape_; }
 
 private:
   void flushLocked();
@@ -79,6 +81,7 @@ private:
   std::map<std::string, Slot> cache_;
   long long round_ = 0, launches_ = 0, qps_ = 0, admm_iters_ = 0;
   double bytes_ = 0, launch_s_ = 0;
+  long long shape_[4] = { 0, 0, 0, 0 };
 };
 
 // RAII: a client of the batcher for its lifetime

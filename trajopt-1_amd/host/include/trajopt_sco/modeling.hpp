@@ -169,6 +169,11 @@ public:
   // true; BasicTrustRegionSQP::optimize otherwise runs the reference's loop
   // over getCosts() / getConstraints() with the GpuModel.
   virtual bool solveNative(const BasicTrustRegionSQPParameters& param, const DblVec& x0, OptResults& results);
+  // MI355X build: called by BasicTrustRegionSQP before it evaluates or
+  // convexifies the costs and constraints at x, so that a problem whose terms
+  // run on the device can evaluate them all in one launch (TrajOptProb: every
+  // CartPose term at once) instead of one launch per term.  No effect on values.
+  virtual void prefetch(const DblVec& /*x*/) {}
 
 protected:
   Model::Ptr model_;

@@ -191,6 +191,8 @@ std::vector<sco::OptResults> BatchTrustRegionSQP::optimizeHostLoops()
   qp_solves_ = batcher->qps();
   qp_bytes_ = batcher->bytes();
   qp_launch_s_ = batcher->launchSeconds();
+  qp_admm_ = batcher->admmIters();
+  std::copy(batcher->maxShape(), batcher->maxShape() + 4, qp_shape_);
   for (std::size_t b = 0; b < B; ++b)
     if (!errs[b].empty())
       throw std::runtime_error("BatchTrustRegionSQP: problem " + std::to_string(b) + ": " + errs[b]);
@@ -537,6 +539,12 @@ int traceCapacity(const sco::BasicTrustRegionSQPParameters& param)
   const double bound = (param.max_merit_coeff_increases + 1.0) * param.max_iter * tries;
   // (a non-finite bound -- absurd parameters -- takes the fixed cap)
   return static_cast<int>(std::isfinite(bound) ? std::min(std::max(bound, 64.0), 1.0e6) : 1.0e6);
+}
+
+void TrajOptProb::prefetch(const DblVec& x)
+{
+  if (device_terms_)
+    device_terms_->prefetchCart(x);
 }
 
 bool TrajOptProb::solveNative(const sco::BasicTrustRegionSQPParameters& param, const DblVec& x0,

@@ -305,5 +305,14 @@ int thost_batch_stats(const thost_batch* h, int* host_loops, long long* qp_launc
   return 0;
 }
 
+int thost_batch_qp_shape(const thost_batch* h, long long* out)
+{
+  if (!h || !h->solver || !out)
+    return -1;
+  out[0] = h->solver->qpAdmmIters();
+  std::copy(h->solver->qpMaxShape(), h->solver->qpMaxShape() + 4, out + 1);
+  return 0;
+}
+
 void thost_batch_destroy(thost_batch* h) { delete h; }
 }

@@ -1,6 +1,7 @@
 // Device-evaluated kinematic terms (device_terms.hpp) over thip_eval_*.
 #include "trajopt_amd/device_terms.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 
@@ -35,11 +36,55 @@ void DeviceTermEvaluator::ensure()
     thip::coll_pair_table(d, static_cast<int>(k), pair_tab_[k]);
 }
 
+DblVec DeviceTermEvaluator::jointTrajectory(const DblVec& x) const
+{
+  // the joint trajectory [n_steps][n_dof] (x also holds dt columns with use_time)
+  auto* prob = const_cast<TrajOptProb*>(prob_);
+  const VarArray& jv = prob->GetJointVars();
+  DblVec q(jv.data.size());
+  for (std::size_t i = 0; i < q.size(); ++i)
+    q[i] = x[static_cast<std::size_t>(jv.data[i].var_rep->index)];
+  return q;
+}
+
+void DeviceTermEvaluator::prefetchCart(const DblVec& x)
+{
+  const thip_problem_desc& d = prob_->desc();
+  if (d.n_cart == 0)
+    return;
+  ensure();
+  DblVec q = jointTrajectory(x);
+  if (cart_.valid && cart_.q == q)
+    return;
+  const std::size_t D = static_cast<std::size_t>(prob_->GetNumDOF()), nc = static_cast<std::size_t>(d.n_cart);
+  cart_.valid = false;
+  cart_.err.resize(nc * 6);
+  cart_.jac.resize(nc * 6 * D);
+  if (thip_eval_cart_pose_all(ev_, q.data(), cart_.err.data(), cart_.jac.data()) != THIP_OK)
+    throw std::runtime_error(std::string("thip_eval_cart_pose_all: ") + thip_eval_last_error(ev_));
+  cart_.q = std::move(q);
+  cart_.valid = true;
+}
+
 void DeviceTermEvaluator::cartPose(int k, const DblVec& q, double* err, double* jac)
 {
   ensure();
   if (static_cast<int>(q.size()) != prob_->GetNumDOF())
     throw std::runtime_error("CartPose evaluation: expected " + std::to_string(prob_->GetNumDOF()) + " joint values");
+  if (cart_.valid && k >= 0 && k < prob_->desc().n_cart)
+  {
+    // the prefetched values when q is this term's waypoint of the prefetched x
+    const std::size_t D = q.size(), t = static_cast<std::size_t>(prob_->desc().cart_step[k]);
+    if (std::equal(q.begin(), q.end(), cart_.q.begin() + static_cast<long>(t * D)))
+    {
+      const std::size_t ku = static_cast<std::size_t>(k);
+      std::copy(cart_.err.begin() + static_cast<long>(ku * 6), cart_.err.begin() + static_cast<long>(ku * 6 + 6), err);
+      if (jac)
+        std::copy(cart_.jac.begin() + static_cast<long>(ku * 6 * D),
+                  cart_.jac.begin() + static_cast<long>((ku + 1) * 6 * D), jac);
+      return;
+    }
+  }
   if (thip_eval_cart_pose(ev_, k, q.data(), err, jac) != THIP_OK)
     throw std::runtime_error(std::string("thip_eval_cart_pose: ") + thip_eval_last_error(ev_));
 }
@@ -49,12 +94,7 @@ const DeviceTermEvaluator::Contacts& DeviceTermEvaluator::collision(int term, co
   ensure();
   if (term < 0 || term >= static_cast<int>(cache_.size()))
     throw std::runtime_error("collision evaluation: term out of range");
-  // the joint trajectory [n_steps][n_dof] (x also holds dt columns with use_time)
-  auto* prob = const_cast<TrajOptProb*>(prob_);
-  const VarArray& jv = prob->GetJointVars();
-  DblVec q(jv.data.size());
-  for (std::size_t i = 0; i < q.size(); ++i)
-    q[i] = x[static_cast<std::size_t>(jv.data[i].var_rep->index)];
+  const DblVec q = jointTrajectory(x);
   Cache& c = cache_[static_cast<std::size_t>(term)];
   if (c.valid && c.q == q)
     return c.c;

@@ -1,6 +1,7 @@
 // GpuQPBatcher (gpu_qp_batcher.hpp).
 #include "trajopt_sco/gpu_qp_batcher.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -125,6 +126,11 @@ void GpuQPBatcher::flushLocked()
           std::copy(r.wx->begin(), r.wx->begin() + static_cast<long>(nn), wx.begin() + static_cast<long>(ku * nn));
           std::copy(r.wy->begin(), r.wy->begin() + static_cast<long>(mm), wy.begin() + static_cast<long>(ku * mm));
         }
+      }
+      {
+        long long sh[4];
+        if (thip_qp_shape(slot.qp, sh) == THIP_OK && sh[0] > shape_[0])
+          std::copy(sh, sh + 4, shape_);
       }
       const auto t0 = std::chrono::steady_clock::now();
       const int rc = thip_qp_solve_some(slot.qp, count, P.data(), q.data(), A.data(), l.data(), u.data(),

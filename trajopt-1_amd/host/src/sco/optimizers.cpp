@@ -83,6 +83,7 @@ void BasicTrustRegionSQP::setTrustBoxConstraints(const DblVec& x)
 
 DblVec BasicTrustRegionSQP::evaluateCosts(const std::vector<Cost::Ptr>& costs, const DblVec& x) const
 {
+  prob_->prefetch(x);
   DblVec out(costs.size());
   for (std::size_t i = 0; i < costs.size(); ++i)
     out[i] = costs[i]->value(x);
@@ -90,6 +91,7 @@ DblVec BasicTrustRegionSQP::evaluateCosts(const std::vector<Cost::Ptr>& costs, c
 }
 DblVec BasicTrustRegionSQP::evaluateConstraintViols(const std::vector<Constraint::Ptr>& cnts, const DblVec& x) const
 {
+  prob_->prefetch(x);
   DblVec out(cnts.size());
   for (std::size_t i = 0; i < cnts.size(); ++i)
     out[i] = cnts[i]->violation(x);
@@ -98,6 +100,7 @@ DblVec BasicTrustRegionSQP::evaluateConstraintViols(const std::vector<Constraint
 std::vector<ConvexObjective::Ptr> BasicTrustRegionSQP::convexifyCosts(const std::vector<Cost::Ptr>& costs,
                                                                       const DblVec& x, Model* model) const
 {
+  prob_->prefetch(x);
   std::vector<ConvexObjective::Ptr> out(costs.size());
   for (std::size_t i = 0; i < costs.size(); ++i)
     out[i] = costs[i]->convex(x, model);
@@ -106,6 +109,7 @@ std::vector<ConvexObjective::Ptr> BasicTrustRegionSQP::convexifyCosts(const std:
 std::vector<ConvexConstraints::Ptr> BasicTrustRegionSQP::convexifyConstraints(const std::vector<Constraint::Ptr>& cnts,
                                                                               const DblVec& x, Model* model) const
 {
+  prob_->prefetch(x);
   std::vector<ConvexConstraints::Ptr> out(cnts.size());
   for (std::size_t i = 0; i < cnts.size(); ++i)
     out[i] = cnts[i]->convex(x, model);

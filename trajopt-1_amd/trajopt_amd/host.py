@@ -59,6 +59,8 @@ def load_host():
         L.thost_batch_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_longlong),
                                         C.POINTER(C.c_longlong), dp, dp]
         L.thost_batch_stats.restype = C.c_int
+        L.thost_batch_qp_shape.argtypes = [C.c_void_p, C.POINTER(C.c_longlong)]
+        L.thost_batch_qp_shape.restype = C.c_int
         L.thost_batch_destroy.argtypes = [C.c_void_p]
         L.thost_batch_destroy.restype = None
         L.thost_solve_json.argtypes = [C.c_char_p, dp, C.c_int, C.c_int, dp, C.POINTER(abi.Result),
@@ -194,6 +196,12 @@ class PreparedBatch:
         self._L.thost_batch_stats(self._h, C.byref(hl), C.byref(la), C.byref(q), _dp(by), _dp(sec))
         return {"host_loops": bool(hl.value), "qp_launches": la.value, "qps": q.value,
                 "qp_bytes": float(by[0]), "qp_seconds": float(sec[0])}
+
+    def qp_shape(self):
+        """{admm_iters, N, nnz_L, levels, widest_level} (thost_batch_qp_shape)."""
+        out = (C.c_longlong * 5)()
+        self._L.thost_batch_qp_shape(self._h, out)
+        return dict(zip(("admm_iters", "N", "nnz_L", "levels", "widest_level"), list(out)))
 
     def close(self):
         if self._h:
