@@ -665,10 +665,15 @@ const char* thip_qp_last_error(thip_qp* qp); /* NULL: the last thip_qp_create fa
 /* Entries of the KKT factor L of the pattern (the symbolic analysis of
  * thip_qp_create): the algorithmic-byte model of the QP solves; -1 for NULL. */
 long long thip_qp_factor_nnz(const thip_qp* qp);
-/* The pattern's KKT shape: out[0] N = n + m, out[1] entries of L, out[2]
- * elimination-tree levels (the solve's serial depth), out[3] the widest level
- * (diagnostic; -1 for NULL). */
+/* The pattern's KKT shape (diagnostic): out[0] N = n + m, out[1] entries of L,
+ * out[2] elimination-tree levels (the solve's serial depth), out[3] the widest
+ * level, out[4] 1 when the factor is staged in LDS, out[5] dynamic LDS bytes. */
 int thip_qp_shape(const thip_qp* qp, long long* out);
+/* Cycle counters of the first QP of every qp_csc_kernel launch on the current
+ * device (diagnostic): out[8] = iterate copies + rhs, KKT solves, updates,
+ * checks (residuals, termination, rho updates), ADMM iterations, polish; reset
+ * zeroes them after the read. */
+int thip_qp_debug_profile(long long* out, int reset);
 
 /* Resident workspace (update in place).  The OSQP 1.0 solver object of every QP
  * of the batch stays on the device between calls, as OsqpEigen::Solver keeps it

@@ -74,7 +74,7 @@ int thost_batch_solve(thost_batch* b, double* x, thip_result* results, char* err
 int thost_batch_stats(const thost_batch* b, int* host_loops, long long* qp_launches, long long* qps, double* qp_bytes,
                       double* qp_seconds);
 /* Host-loop batches (diagnostic): out[0] ADMM iterations of all QPs, then the
- * largest KKT's N, entries of L, elimination-tree levels and widest level. */
+ * largest KKT's thip_qp_shape (6 entries). */
 int thost_batch_qp_shape(const thost_batch* b, long long* out);
 void thost_batch_destroy(thost_batch* b);
 

@@ -278,12 +278,12 @@ def test_large_scene_runs_the_generic_path(oracle_mod):
     in LDS): the host loop with the device collision evaluator, oracle parity.
     Three primitives of config C's scene near the arm and 16 small spheres far
     from it (JSON problems carry the reference's 0.5 m buffer: a QP per contact)."""
-    wl0 = problems.make_workload("C", 2, n_steps=12)
+    wl0 = problems.make_workload("C", 1, n_steps=12)
     far = np.zeros((16, 16))
     far[:, 0] = abi.PRIM_SPHERE
     far[:, 1:4] = np.array([3.0, 3.0, 3.0]) + 0.3 * np.arange(16)[:, None]
     far[:, 4] = 0.05
-    for b in range(2):
+    for b in range(wl0.batch):
         prims = np.ascontiguousarray(np.concatenate([wl0.scene[b][:3], far]))
         text = host.workload_to_json(wl0, b)
         x, res, native = host.solve_json(text, prims)
@@ -301,7 +301,7 @@ def test_prepared_hostloop_batch(oracle_mod):
     with the oracle; a prepared host-loop batch solves once."""
     from trajopt_amd import sharding
 
-    B = 16
+    B = 4
     wl = sharding.rank_workload("B", B, 0)
     texts = [host.hostloop_workload_json(wl, b) for b in range(B)]
     pb = host.PreparedBatch(texts)

@@ -204,19 +204,34 @@ __device__ __forceinline__ double limit_scaling(double a)
 }
 
 // The arrays the factorisation and the solves walk: the pattern's (HBM) or
-// their LDS copies (QpPattern::lds_pat: 16-bit indices)
-template <typename IX>
-struct FacView
+// their LDS copies (QpPattern::lds_pat: 16-bit indices).  The LDS view's
+// pointers are address-space-3 typed, so its accesses are ds_* instructions: a
+// generic pointer would make each a FLAT access, which pays the vector-memory
+// latency even when it lands in LDS (the level loops are chains of dependent
+// loads, so that latency is their whole cost).
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(3))) int lds_i32;
+typedef __attribute__((address_space(3))) unsigned short lds_u16;
+template <typename IX, typename IN, typename DB>
+struct FacViewT
 {
   const IX *lrj, *lcpos, *lci, *lvn;
-  const int *lrp, *lcp, *lvp;
-  double *LX, *DG;
+  const IN *lrp, *lcp, *lvp;
+  DB *LX, *DG;
 };
+using FacViewG = FacViewT<int, int, double>;
+using FacViewL = FacViewT<lds_u16, lds_i32, lds_f64>;
 // LDS layout of a staged factor (QpPattern::lds_off)
 enum : int
 {
   QL_LX = 0, QL_DG, QL_LRJ, QL_LCPOS, QL_LCI, QL_LVN, QL_LRP, QL_LVP  // (lcp follows lrp)
 };
+
+// phase cycles of workgroup 0's ADMM loop (diagnostic, thip_qp_debug_profile):
+// [0] iterate copies + rhs, [1] KKT solves, [2] z / y / x updates, [3] residuals,
+// termination and rho updates (incl. refactorisations), [4] iterations, [5] polish
+__device__ long long g_qp_prof[8];
+
 
 struct Qp
 {
@@ -226,8 +241,8 @@ struct Qp
   Sh& sh;
   double* lv;  // the permuted solve vector [N] (LDS, or W_LV)
   int n, m;
-  FacView<int> fg;              // HBM
-  FacView<unsigned short> fs;   // LDS (p.lds_pat)
+  FacViewG fg;  // HBM
+  FacViewL fs;  // LDS (p.lds_pat)
   bool persist;                 // keep W_LX / W_DG current (resident workspaces)
   __device__ double* a(int k) const { return w + p.off[k]; }
 };
@@ -237,7 +252,7 @@ struct Qp
 __device__ void fac_views(Qp& q, char* lds)
 {
   const QpPattern& p = q.p;
-  q.fg = FacView<int>{ p.lrj, p.lcpos, p.lci, p.lvn, p.lrp, p.lcp, p.lvp, q.a(W_LX), q.a(W_DG) };
+  q.fg = FacViewG{ p.lrj, p.lcpos, p.lci, p.lvn, p.lrp, p.lcp, p.lvp, q.a(W_LX), q.a(W_DG) };
   if (!p.lds_pat)
     return;
   const int N = p.N, nl = static_cast<int>(p.lds_off[QL_DG] - p.lds_off[QL_LX]) / 8;  // entries of L
@@ -269,7 +284,8 @@ __device__ void fac_views(Qp& q, char* lds)
     lcp[k] = p.lcp[k];
   }
   QFOR(l, p.nlev + 1) lvp[l] = p.lvp[l];
-  q.fs = FacView<unsigned short>{ lrj, lcpos, lci, lvn, lrp, lcp, lvp, LX, DG };
+  q.fs = FacViewL{ (const lds_u16*)lrj, (const lds_u16*)lcpos, (const lds_u16*)lci, (const lds_u16*)lvn,
+                   (const lds_i32*)lrp, (const lds_i32*)lcp, (const lds_i32*)lvp, (lds_f64*)LX, (lds_f64*)DG };
   __syncthreads();
 }
 
@@ -469,11 +485,72 @@ __device__ __forceinline__ double kkt_diag(const Qp& q, int k, bool pol, const d
 //     L_ik = (K_ik - sum_{j < k} L_ij D_j L_kj) / D_k
 // as a merge of rows i and k (both ascending).  sh.npos = positive pivots,
 // sh.fail = 1 on a zero / non-finite pivot.
-template <typename IX>
-__device__ void kkt_factor_v(Qp& q, const FacView<IX>& f, bool pol)
+// s - sum over e in [e0, e1) of LX[e] w[j[e]], in order (the same expression
+// as the plain loop, so the same contraction and rounding), eight entries'
+// loads issued before their products: one memory round trip per eight
+// entries instead of one per entry (a long row near the tree's root is a
+// serial chain otherwise)
+template <typename PL, typename PJ, typename PW>
+__device__ __forceinline__ double row_sub(double s, PL LX, PJ j, PW w, int e0, int e1)
+{
+  int e = e0;
+  for (; e + 8 <= e1; e += 8)
+  {
+    double a[8], b[8];
+    int jj[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+    {
+      a[u] = LX[e + u];
+      jj[u] = j[e + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      b[u] = w[jj[u]];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      s -= a[u] * b[u];
+  }
+  for (; e < e1; ++e)
+    s -= LX[e] * w[j[e]];
+  return s;
+}
+// the same over column entries c in [c0, c1): LX[pos[c]] w[i[c]]
+template <typename PL, typename PJ, typename PW>
+__device__ __forceinline__ double col_sub(double s, PL LX, PJ pos, PJ i, PW w, int c0, int c1)
+{
+  int c = c0;
+  for (; c + 8 <= c1; c += 8)
+  {
+    double a[8], b[8];
+    int pp[8], ii[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+    {
+      pp[u] = pos[c + u];
+      ii[u] = i[c + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+    {
+      a[u] = LX[pp[u]];
+      b[u] = w[ii[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      s -= a[u] * b[u];
+  }
+  for (; c < c1; ++c)
+    s -= LX[pos[c]] * w[i[c]];
+  return s;
+}
+
+template <typename V, typename PW>
+__device__ void kkt_factor_v(Qp& q, const V f, PW dense, bool pol)
 {
   const QpPattern& p = q.p;
-  double *LX = f.LX, *DG = f.DG;
+  auto LX = f.LX;
+  auto DG = f.DG;
   const double* FLG = q.a(W_FLG);
   double bad = 0, npos = 0;
   // one-node levels (the chain) with the solve vector in LDS: row k of L is
@@ -481,7 +558,6 @@ __device__ void kkt_factor_v(Qp& q, const FacView<IX>& f, bool pol)
   // rows i and k becomes a branch-free walk of row i's prefix (its entries
   // before column k, lcpos order) -- (L_ij D_j) L_kj for the shared j, exact
   // zeros for the rest: bitwise the merge's sum.  The vector is zero between levels.
-  double* dense = q.lv;
   const bool scatter = p.lds_vec;
   if (scatter)
   {
@@ -520,8 +596,28 @@ __device__ void kkt_factor_v(Qp& q, const FacView<IX>& f, bool pol)
         const int c = p.fic[t], i = f.lci[c];
         double s = kkt_entry(q, p.lksrc[c], pol, FLG);
         const int ae = f.lcpos[c];  // entry (i, k)'s place in row i: the entries before it have j < k
-#pragma unroll 4
-        for (int a = f.lrp[i]; a < ae; ++a)
+        int a = f.lrp[i];
+        for (; a + 4 <= ae; a += 4)
+        {
+          double la[4], da[4], xa[4];
+          int ja[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+          {
+            la[u] = LX[a + u];
+            ja[u] = f.lrj[a + u];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+          {
+            da[u] = DG[ja[u]];
+            xa[u] = dense[ja[u]];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            s -= (la[u] * da[u]) * xa[u];
+        }
+        for (; a < ae; ++a)
         {
           const int ja = f.lrj[a];
           s -= (LX[a] * DG[ja]) * dense[ja];
@@ -574,10 +670,10 @@ __device__ void kkt_factor(Qp& q, bool pol)
 {
   if (!q.p.lds_pat)
   {
-    kkt_factor_v(q, q.fg, pol);
+    kkt_factor_v(q, q.fg, q.lv, pol);
     return;
   }
-  kkt_factor_v(q, q.fs, pol);
+  kkt_factor_v(q, q.fs, (lds_f64*)q.lv, pol);
   if (q.persist)  // the resident workspace's copy (the next launch stages it)
   {
     const int nl = static_cast<int>(q.p.lds_off[QL_DG] - q.p.lds_off[QL_LX]) / 8;
@@ -595,54 +691,64 @@ __device__ void kkt_factor(Qp& q, bool pol)
 // is an LDS access: a level costs a few LDS round trips and a barrier instead
 // of a chain of dependent HBM loads (level pointer -> node -> row bounds ->
 // entries), which set the pace of the HBM form.
-template <typename IX>
-__device__ void kkt_solve_v(Qp& q, const FacView<IX>& f, double* v)
+// (the view by value and every pointer in a local: a Qp or view reached through
+// a reference lives in scratch, and the stores to w would force a reload of
+// each of its pointers from there at every level)
+// (the view by value and every pointer in a local: a Qp or view reached through
+// a reference lives in scratch)
+template <typename V, typename PW>
+__device__ void kkt_solve_v(Qp& q, const V f, PW w, double* v)
 {
   const QpPattern& p = q.p;
-  const double *LX = f.LX, *DG = f.DG;
-  double* w = q.lv;
-  const int N = p.N;
+  auto LX = f.LX;
+  auto DG = f.DG;
+  const int N = p.N, nlev = p.nlev;
+  const int* perm = p.perm;
   __syncthreads();
-  QFOR(k, N) w[k] = v[p.perm[k]];
+  QFOR(k, N) w[k] = v[perm[k]];
   __syncthreads();
-  for (int lev = 0; lev < p.nlev; ++lev)
+  const bool prof = blockIdx.x == 0 && threadIdx.x == 0;
+  long long t0 = prof ? clock64() : 0;
+  for (int lev = 0; lev < nlev; ++lev)
   {
     const int n1 = f.lvp[lev + 1];
     for (int t = f.lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
     {
       const int k = f.lvn[t];
-      double s = w[k];
-      for (int e = f.lrp[k]; e < f.lrp[k + 1]; ++e)
-        s -= LX[e] * w[f.lrj[e]];
-      w[k] = s;
+      w[k] = row_sub(static_cast<double>(w[k]), LX, f.lrj, w, f.lrp[k], f.lrp[k + 1]);
     }
     __syncthreads();
   }
+  if (prof)
+    g_qp_prof[6] += clock64() - t0;
   QFOR(k, N) w[k] /= DG[k];
   __syncthreads();
-  for (int lev = p.nlev - 1; lev >= 0; --lev)
+  if (prof)
+    t0 = clock64();
+  for (int lev = nlev - 1; lev >= 0; --lev)
   {
     const int n1 = f.lvp[lev + 1];
     for (int t = f.lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
     {
       const int k = f.lvn[t];
-      double s = w[k];
-      for (int c = f.lcp[k]; c < f.lcp[k + 1]; ++c)
-        s -= LX[f.lcpos[c]] * w[f.lci[c]];
-      w[k] = s;
+      w[k] = col_sub(static_cast<double>(w[k]), LX, f.lcpos, f.lci, w, f.lcp[k], f.lcp[k + 1]);
     }
     __syncthreads();
   }
-  QFOR(k, N) v[p.perm[k]] = w[k];
+  if (prof)
+    g_qp_prof[7] += clock64() - t0;
+  QFOR(k, N) v[perm[k]] = w[k];
   __syncthreads();
 }
 
 __device__ void kkt_solve(Qp& q, double* v)
 {
   if (q.p.lds_pat)
-    kkt_solve_v(q, q.fs, v);
+    kkt_solve_v(q, q.fs, (lds_f64*)q.lv, v);
+  else if (q.p.lds_vec)
+    kkt_solve_v(q, q.fg, (lds_f64*)q.lv, v);
   else
-    kkt_solve_v(q, q.fg, v);
+    kkt_solve_v(q, q.fg, q.lv, v);
 }
 
 __device__ double prim_res(Qp& q, const double* x, const double* z)
@@ -957,6 +1063,8 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
   bool can_check = false;
   bool noncvx = false;
   int it;
+  const bool prof = blockIdx.x == 0 && threadIdx.x == 0;
+  long long t0 = prof ? clock64() : 0, t1;
   for (it = 1; it <= args.s.max_iter; ++it)
   {
     // (x_prev, z_prev) <- (x, z): OSQP swaps the buffers; x and z are overwritten below
@@ -966,7 +1074,19 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
     QFOR(j, n) XT[j] = sigma * XP[j] - Q[j];
     QFOR(r, m) XT[n + r] = ZP[r] - RHOI[r] * Y[r];
     __syncthreads();
+    if (prof)
+    {
+      t1 = clock64();
+      g_qp_prof[0] += t1 - t0;
+      t0 = t1;
+    }
     kkt_solve(q, XT);  // (x~, nu) in place
+    if (prof)
+    {
+      t1 = clock64();
+      g_qp_prof[1] += t1 - t0;
+      t0 = t1;
+    }
     QFOR(r, m) XT[n + r] = (ZP[r] - RHOI[r] * Y[r]) + RHOI[r] * XT[n + r];  // z~ = rhs + nu / rho
     __syncthreads();
     QFOR(j, n)
@@ -984,6 +1104,12 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
       Y[r] += DY[r];
     }
     __syncthreads();
+    if (prof)
+    {
+      t1 = clock64();
+      g_qp_prof[2] += t1 - t0;
+      t0 = t1;
+    }
     can_check = args.s.check_termination && (it % args.s.check_termination == 0);
     const bool adapt_now = args.s.adaptive_rho && interval && (it % interval == 0);
     bool done = false;
@@ -1005,6 +1131,13 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
         noncvx = true;
         break;
       }
+    }
+    if (prof)
+    {
+      t1 = clock64();
+      g_qp_prof[3] += t1 - t0;
+      g_qp_prof[4] += 1;
+      t0 = t1;
     }
     if (done)
       break;
@@ -1039,6 +1172,8 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
     }
     if (args.s.polishing && sh.status == SOLVED)
       polish(q);
+    if (prof)
+      g_qp_prof[5] += clock64() - t0;
   }
   // store_solution (unscaled), NaN on infeasibility
   const int st = sh.status;
@@ -1980,6 +2115,19 @@ const char* thip_qp_last_error(thip_qp* q) { return q ? q->err.c_str() : g_qp_cr
 
 long long thip_qp_factor_nnz(const thip_qp* q) { return q ? q->nnz_l : -1; }
 
+int thip_qp_debug_profile(long long* out, int reset)
+{
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qp_prof), sizeof(long long) * 8) != hipSuccess)
+    return THIP_E_HIP;
+  if (reset)
+  {
+    const long long z[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_qp_prof), z, sizeof(z)) != hipSuccess)
+      return THIP_E_HIP;
+  }
+  return THIP_OK;
+}
+
 int thip_qp_shape(const thip_qp* q, long long* out)
 {
   if (!q || !out)
@@ -1988,6 +2136,8 @@ int thip_qp_shape(const thip_qp* q, long long* out)
   out[1] = q->nnz_l;
   out[2] = q->pat.nlev;
   out[3] = q->max_level;
+  out[4] = q->pat.lds_pat;
+  out[5] = static_cast<long long>(q->lds);
   return THIP_OK;
 }
 

@@ -79,7 +79,7 @@ private:
   std::vector<sco::OptResults> generic_results_;
   long long qp_launches_ = 0, qp_solves_ = 0;
   double qp_bytes_ = 0, qp_launch_s_ = 0;
-  long long qp_admm_ = 0, qp_shape_[4] = { 0, 0, 0, 0 };
+  long long qp_admm_ = 0, qp_shape_[6] = { 0, 0, 0, 0, 0, 0 };
   int workers_ = 0;
 };
 

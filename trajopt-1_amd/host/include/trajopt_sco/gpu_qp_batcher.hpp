@@ -81,7 +81,7 @@ private:
   std::map<std::string, Slot> cache_;
   long long round_ = 0, launches_ = 0, qps_ = 0, admm_iters_ = 0;
   double bytes_ = 0, launch_s_ = 0;
-  long long shape_[4] = { 0, 0, 0, 0 };
+  long long shape_[6] = { 0, 0, 0, 0, 0, 0 };
 };
 
 // RAII: a client of the batcher for its lifetime

@@ -192,7 +192,7 @@ std::vector<sco::OptResults> BatchTrustRegionSQP::optimizeHostLoops()
   qp_bytes_ = batcher->bytes();
   qp_launch_s_ = batcher->launchSeconds();
   qp_admm_ = batcher->admmIters();
-  std::copy(batcher->maxShape(), batcher->maxShape() + 4, qp_shape_);
+  std::copy(batcher->maxShape(), batcher->maxShape() + 6, qp_shape_);
   for (std::size_t b = 0; b < B; ++b)
     if (!errs[b].empty())
       throw std::runtime_error("BatchTrustRegionSQP: problem " + std::to_string(b) + ": " + errs[b]);

@@ -310,7 +310,7 @@ int thost_batch_qp_shape(const thost_batch* h, long long* out)
   if (!h || !h->solver || !out)
     return -1;
   out[0] = h->solver->qpAdmmIters();
-  std::copy(h->solver->qpMaxShape(), h->solver->qpMaxShape() + 4, out + 1);
+  std::copy(h->solver->qpMaxShape(), h->solver->qpMaxShape() + 6, out + 1);
   return 0;
 }
 

@@ -128,9 +128,9 @@ void GpuQPBatcher::flushLocked()
         }
       }
       {
-        long long sh[4];
+        long long sh[6];
         if (thip_qp_shape(slot.qp, sh) == THIP_OK && sh[0] > shape_[0])
-          std::copy(sh, sh + 4, shape_);
+          std::copy(sh, sh + 6, shape_);
       }
       const auto t0 = std::chrono::steady_clock::now();
       const int rc = thip_qp_solve_some(slot.qp, count, P.data(), q.data(), A.data(), l.data(), u.data(),

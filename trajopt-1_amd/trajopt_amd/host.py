@@ -199,9 +199,9 @@ class PreparedBatch:
 
     def qp_shape(self):
         """{admm_iters, N, nnz_L, levels, widest_level} (thost_batch_qp_shape)."""
-        out = (C.c_longlong * 5)()
+        out = (C.c_longlong * 7)()
         self._L.thost_batch_qp_shape(self._h, out)
-        return dict(zip(("admm_iters", "N", "nnz_L", "levels", "widest_level"), list(out)))
+        return dict(zip(("admm_iters", "N", "nnz_L", "levels", "widest_level", "lds_factor", "lds_bytes"), list(out)))
 
     def close(self):
         if self._h:
