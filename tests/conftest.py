@@ -59,3 +59,13 @@ def pytest_sessionfinish(session, exitstatus):
     if total and strict < parity.POOLED_MIN * total:
         print(f"\nparity gate: pooled strict {strict}/{total} = {strict / total:.3f} < {parity.POOLED_MIN}")
         session.exitstatus = 1
+
+
+def pytest_runtest_logreport(report):
+    """Each GPU test's wall time as it finishes (THIP_TEST_TIMES=1: the suite's
+    time budget is checked from a log that a time limit may cut short)."""
+    import os
+
+    if report.when == "call" and os.environ.get("THIP_TEST_TIMES"):
+        sys.__stderr__.write(f"[time] {report.nodeid} {report.duration:.1f} s {report.outcome}\n")
+        sys.__stderr__.flush()

@@ -491,7 +491,8 @@ def test_collision_rows_parity_pairs(oracle_mod):
     from trajopt_amd.runtime import TermEvaluator
 
     wl = problems.with_pair_data(problems.make_workload("C", 16))
-    assert wl.desc.n_coll_pairs == 5
+    # five scene pair entries (one replaced), plus a self pair when the arm has self-collision pairs
+    assert wl.desc.n_coll_pairs == 5 + (1 if wl.desc.n_self_pairs > 0 else 0)
     xo, _ = oracle_mod.solve(wl, n_threads=16)
     s = BatchTrustRegionSQP(wl)
     rows = {"init": s.collision_rows(wl.init), "solution": s.collision_rows(xo)}
@@ -554,15 +555,23 @@ def test_frontdoor_json_pairs_parity(oracle_mod):
     assert wl.desc.n_coll_pairs == 4
     check_parity(wl, oracle_mod, x, res, label="json-pairs")
     # a second collision term (a constraint with pairs of its own): the host loop
-    texts2 = []
-    for t in texts:
-        doc = _json.loads(t)
-        doc["constraints"].append({"type": "collision", "params": {
-            "coeffs": 10, "dist_pen": 0.01, "evaluator_type": 2,
-            "pairs": [{"link": "r_wrist_roll_link", "pair": ["scene_1"], "coeffs": 3, "dist_pen": 0.0}]}})
-        texts2.append(_json.dumps(doc))
-    x2, res2 = host.solve_json_batch(texts2[:2], scenes[:2])
-    wl2 = _lowered_workload(texts2[:2], scenes[:2])
+    # (one problem on a 10-waypoint horizon: the generic path's sparse-LDL QPs on
+    # a 30-waypoint collision problem take minutes)
+    wls = problems.make_workload("C", 1, n_steps=10)
+    doc = _json.loads(host.workload_to_json(wls, 0))
+    for t in doc["costs"]:
+        if t["type"] == "collision":
+            t["params"]["pairs"] = [
+                {"link": "r_wrist_roll_link", "pair": ["scene_1", "scene_2"], "coeffs": 40, "dist_pen": 0.04},
+                {"link": "scene_0", "pair": ["r_forearm_roll_link"], "coeffs": 0, "dist_pen": 0.02},
+                {"link": "r_shoulder_pan_link", "pair": ["r_wrist_flex_link"], "coeffs": 5, "dist_pen": 0.03}]
+    doc["constraints"].append({"type": "collision", "params": {
+        "coeffs": 10, "dist_pen": 0.01, "evaluator_type": 2,
+        "pairs": [{"link": "r_wrist_roll_link", "pair": ["scene_1"], "coeffs": 3, "dist_pen": 0.0}]}})
+    texts2 = [_json.dumps(doc)]
+    scenes2 = np.ascontiguousarray(wls.scene[:, :3])
+    x2, res2 = host.solve_json_batch(texts2, scenes2)
+    wl2 = _lowered_workload(texts2, scenes2)
     assert wl2.desc.n_coll_extra == 1 and wl2.desc.n_coll_pairs == 5
     assert host.last_batch_qp_stats()[1] > 0  # the host loops ran
     check_parity(wl2, oracle_mod, x2, res2, label="json-pairs-generic")
