@@ -474,7 +474,7 @@ def test_sqp_parity_collision_constraint(oracle_mod):
     """CollisionConstraint (LVS-discrete, collision_terms.cpp:1308-1386) as a
     constraint: ineq rows coeff*(margin - dist) inflated by the per-step-pair
     merit coefficients, violations counted in the penalty loop."""
-    wl = problems.make_workload("C", 32, first_problem=64)
+    wl = problems.make_workload("C", 16, first_problem=64)
     wl.desc.coll_is_cnt = 1
     x, res, _ = solve_gpu(wl)
     assert all(r.flags == 0 for r in res)
@@ -898,7 +898,7 @@ def test_dynamic_problem_assignment_matches_static(hip):
 def test_full_batch_E_512(oracle_mod):
     """Config E at one GPU's share of configs[4] (4096 problems over 8 GPUs):
     512 problems of the 14-DoF dual arm, 50 waypoints, LVS_CONTINUOUS.
-    Properties on every problem, the strict gate on 32 problems spread over the
+    Properties on every problem, the strict gate on 16 problems spread over the
     batch."""
     wl = problems.make_workload("E", 512)
     s = BatchTrustRegionSQP(wl)
@@ -906,9 +906,9 @@ def test_full_batch_E_512(oracle_mod):
     s.close()
     from parity import subset
 
-    idx = np.arange(0, 512, 16)
+    idx = np.arange(0, 512, 32)
     sub = subset(wl, idx)
-    check_parity(sub, oracle_mod, x[idx], [res[i] for i in idx], label="E-512-sample32", min_strict=0.9)
+    check_parity(sub, oracle_mod, x[idx], [res[i] for i in idx], label="E-512-sample16", min_strict=0.9)
 
 
 def test_devices_stream_interop():
