@@ -660,6 +660,16 @@ int thip_qp_solve_some(thip_qp* qp, int count, const double* P_values, const dou
                        const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
                        const double* warm_y, const int* warm_mask, const double* warm_rho, double* x, double* y,
                        thip_qp_info* info);
+/* thip_qp_solve_some in two halves: thip_qp_submit copies the inputs and
+ * launches on the QP object's own stream and returns; thip_qp_collect waits for
+ * that launch and returns x, y, info.  Submissions to different QP objects
+ * (patterns) run concurrently on the device -- sco::GpuQPBatcher submits every
+ * pattern of a round before it collects any.  The host arrays of a submission
+ * must stay valid until it is collected; one submission per object at a time. */
+int thip_qp_submit(thip_qp* qp, int count, const double* P_values, const double* q, const double* A_values,
+                   const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
+                   const double* warm_y, const int* warm_mask, const double* warm_rho);
+int thip_qp_collect(thip_qp* qp, double* x, double* y, thip_qp_info* info);
 void thip_qp_destroy(thip_qp* qp);
 const char* thip_qp_last_error(thip_qp* qp); /* NULL: the last thip_qp_create failure */
 /* Entries of the KKT factor L of the pattern (the symbolic analysis of

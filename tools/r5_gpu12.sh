@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 (while sleep 45; do date >> gpurun_out/tick.log; done) &
 TICK=$!
 trap 'kill $TICK' EXIT
-timeout -k 10 200 python -u tools/hb_probe.py 1 8 > gpurun_out/r5_hb_probe6.log 2>&1
+timeout -k 10 200 python -u tools/hb_probe.py 8 > gpurun_out/r5_hb_probe6.log 2>&1
 rc=$?
 cat gpurun_out/r5_hb_probe6.log
 [ $rc = 0 ] || exit $rc

@@ -1541,6 +1541,9 @@ struct thip_qp
   int device = 0, batch = 0, n = 0, m = 0, nnz_p = 0, nnz_a = 0;
   long long nnz_l = 0;  // entries of the KKT factor L (thip_qp_factor_nnz)
   int max_level = 0;    // nodes of the widest elimination-tree level (thip_qp_shape)
+  hipStream_t stream = nullptr;  // thip_qp_submit / thip_qp_collect
+  int pending = 0;               // QPs submitted and not yet collected
+  std::vector<int> bad;          // per submitted QP: l > u somewhere (osqp_setup's validate_data)
   QpPattern pat{};
   int* d_idx = nullptr;
   double* d_ws = nullptr;
@@ -1745,6 +1748,8 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
     return fail(std::string("hipMalloc: ") + hipGetErrorString(e));
   if ((e = hipMemcpy(q->d_idx, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)
     return fail(std::string("hipMemcpy: ") + hipGetErrorString(e));
+  if ((e = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking)) != hipSuccess)
+    return fail(std::string("hipStreamCreate: ") + hipGetErrorString(e));
   q->pat.Pp = q->d_idx + oPp;
   q->pat.Pi = q->d_idx + oPi;
   q->pat.Prp = q->d_idx + oPrp;
@@ -1782,13 +1787,17 @@ int thip_qp_solve(thip_qp* q, const double* P_values, const double* qvec, const 
                             x, y, info);
 }
 
-int thip_qp_solve_some(thip_qp* q, int count, const double* P_values, const double* qvec, const double* A_values,
-                       const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
-                       const double* warm_y, const int* warm_mask, const double* warm_rho, double* x, double* y,
-                       thip_qp_info* info)
+int thip_qp_submit(thip_qp* q, int count, const double* P_values, const double* qvec, const double* A_values,
+                   const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
+                   const double* warm_y, const int* warm_mask, const double* warm_rho)
 {
   if (!q)
     return THIP_E_INVALID;
+  if (q->pending)
+  {
+    q->err = "thip_qp_submit: the previous submission is not collected";
+    return THIP_E_INVALID;
+  }
   if (count < 1 || count > q->batch)
   {
     q->err = "thip_qp_solve_some: count must be in [1, batch]";
@@ -1796,7 +1805,7 @@ int thip_qp_solve_some(thip_qp* q, int count, const double* P_values, const doub
   }
   const int n = q->n, m = q->m, B = count;
   // (an empty P -- a linear objective -- or an empty A may come with NULL values)
-  if ((!P_values && q->nnz_p) || !qvec || (!A_values && q->nnz_a) || (m && (!l || !u)) || !settings || !x || !info)
+  if ((!P_values && q->nnz_p) || !qvec || (!A_values && q->nnz_a) || (m && (!l || !u)) || !settings)
   {
     q->err = "thip_qp_solve: null argument";
     return THIP_E_INVALID;
@@ -1809,11 +1818,11 @@ int thip_qp_solve_some(thip_qp* q, int count, const double* P_values, const doub
     return THIP_E_INVALID;
   }
   // osqp_setup's validate_data: l <= u (a failing problem is reported, not solved)
-  std::vector<int> bad(static_cast<size_t>(B), 0);
+  q->bad.assign(static_cast<size_t>(B), 0);
   for (int b = 0; b < B; ++b)
     for (int r = 0; r < m; ++r)
       if (!(l[(long long)b * m + r] <= u[(long long)b * m + r]))
-        bad[static_cast<size_t>(b)] = 1;
+        q->bad[static_cast<size_t>(b)] = 1;
   hipError_t e;
   if ((e = hipSetDevice(q->device)) != hipSuccess)
   {
@@ -1826,8 +1835,9 @@ int thip_qp_solve_some(thip_qp* q, int count, const double* P_values, const doub
   double* d = q->d_in;
   double *dP = d, *dA = dP + np, *dq = dA + na, *dl = dq + nn, *du = dl + mm, *dxw = du + mm, *dyw = dxw + nn,
          *drw = dyw + mm;
+  // (on the QP object's own stream: the submissions of several patterns overlap)
   auto h2d = [&](double* dst, const double* src, size_t cnt) {
-    if (cnt && (e = hipMemcpy(dst, src, cnt * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+    if (cnt && (e = hipMemcpyAsync(dst, src, cnt * sizeof(double), hipMemcpyHostToDevice, q->stream)) != hipSuccess)
       return false;
     return true;
   };
@@ -1837,7 +1847,8 @@ int thip_qp_solve_some(thip_qp* q, int count, const double* P_values, const doub
   if (!h2d(dP, P_values, np) || !h2d(dA, A_values, na) || !h2d(dq, qvec, nn) || !h2d(dl, l, mm) || !h2d(du, u, mm) ||
       (ws && (!h2d(dxw, warm_x, nn) || !h2d(dyw, warm_y, mm))) || (warm_rho && !h2d(drw, warm_rho, B)) ||
       (ws && warm_mask &&
-       (e = hipMemcpy(dmask, warm_mask, static_cast<size_t>(B) * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess))
+       (e = hipMemcpyAsync(dmask, warm_mask, static_cast<size_t>(B) * sizeof(int), hipMemcpyHostToDevice,
+                           q->stream)) != hipSuccess))
   {
     q->err = std::string("hipMemcpy: ") + hipGetErrorString(e);
     return THIP_E_HIP;
@@ -1863,8 +1874,35 @@ int thip_qp_solve_some(thip_qp* q, int count, const double* P_values, const doub
   if (q->lds > 65536)
     hipFuncSetAttribute(reinterpret_cast<const void*>(&qp_csc_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                         static_cast<int>(q->lds));
-  hipLaunchKernelGGL(qp_csc_kernel, dim3(B), dim3(kQB), q->lds, nullptr, a);
-  if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess)
+  hipLaunchKernelGGL(qp_csc_kernel, dim3(B), dim3(kQB), q->lds, q->stream, a);
+  if ((e = hipGetLastError()) != hipSuccess)
+  {
+    q->err = std::string("qp_csc_kernel: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  q->pending = B;
+  return THIP_OK;
+}
+
+int thip_qp_collect(thip_qp* q, double* x, double* y, thip_qp_info* info)
+{
+  if (!q)
+    return THIP_E_INVALID;
+  if (!q->pending)
+  {
+    q->err = "thip_qp_collect: nothing submitted";
+    return THIP_E_INVALID;
+  }
+  if (!x || !info)
+  {
+    q->err = "thip_qp_collect: null argument";
+    return THIP_E_INVALID;
+  }
+  const int B = q->pending, n = q->n, m = q->m;
+  q->pending = 0;
+  const size_t nn = static_cast<size_t>(n) * B, mm = static_cast<size_t>(m) * B;
+  hipError_t e;
+  if ((e = hipSetDevice(q->device)) != hipSuccess || (e = hipStreamSynchronize(q->stream)) != hipSuccess)
   {
     q->err = std::string("qp_csc_kernel: ") + hipGetErrorString(e);
     return THIP_E_HIP;
@@ -1880,13 +1918,30 @@ int thip_qp_solve_some(thip_qp* q, int count, const double* P_values, const doub
   for (int b = 0; b < B; ++b)
   {
     info[b] = hinfo[static_cast<size_t>(b)];
-    if (bad[static_cast<size_t>(b)])
+    if (q->bad[static_cast<size_t>(b)])
     {
       info[b].status = -1;
       info[b].setup_error = 1;  // OSQP_DATA_VALIDATION_ERROR
     }
   }
   return THIP_OK;
+}
+
+int thip_qp_solve_some(thip_qp* q, int count, const double* P_values, const double* qvec, const double* A_values,
+                       const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
+                       const double* warm_y, const int* warm_mask, const double* warm_rho, double* x, double* y,
+                       thip_qp_info* info)
+{
+  if (!q)
+    return THIP_E_INVALID;
+  if (!x || !info)
+  {
+    q->err = "thip_qp_solve: null argument";
+    return THIP_E_INVALID;
+  }
+  const int rc =
+      thip_qp_submit(q, count, P_values, qvec, A_values, l, u, settings, warm_x, warm_y, warm_mask, warm_rho);
+  return rc != THIP_OK ? rc : thip_qp_collect(q, x, y, info);
 }
 
 // ---- resident workspace (update in place) --------------------------------
@@ -2103,6 +2158,12 @@ void thip_qp_destroy(thip_qp* q)
 {
   if (!q)
     return;
+  hipSetDevice(q->device);
+  if (q->stream)
+  {
+    hipStreamSynchronize(q->stream);
+    hipStreamDestroy(q->stream);
+  }
   hipFree(q->d_idx);
   hipFree(q->d_ws);
   hipFree(q->d_in);

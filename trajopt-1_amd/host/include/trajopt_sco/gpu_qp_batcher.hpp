@@ -61,7 +61,8 @@ public:
   // L; polish adds one factorisation and 1 + polish_refine_iter solves)
   double bytes() const { return bytes_; }
   long long admmIters() const { return admm_iters_; }
-  // wall seconds inside thip_qp_solve_some (the launches with their transfers)
+  // wall seconds of the rounds on the device: first submission to last collection
+  // (the launches of a round run concurrently, each pattern on its own stream)
   double launchSeconds() const { return launch_s_; }
   // the largest KKT seen: N, entries of L, elimination-tree levels, widest level
   const long long* maxShape() const { return shape_; }

@@ -83,11 +83,32 @@ void GpuQPBatcher::flushLocked()
   std::map<std::string, std::vector<Request*>> groups;
   for (Request* r : reqs)
     groups[groupKey(*r)].push_back(r);
+  // every pattern's launch is submitted (each on its QP object's own stream)
+  // before any is collected, so the round's launches run concurrently on the
+  // device: the round takes its slowest pattern, not the sum of them
+  struct Launch
+  {
+    std::vector<Request*>* g = nullptr;
+    Slot* slot = nullptr;
+    int n = 0, m = 0;
+    std::vector<double> P, A, q, l, u, wx, wy, wr, x, y;
+    std::vector<int> mask;
+    std::vector<thip_qp_info> info;
+    bool submitted = false;
+  };
+  std::vector<Launch> launches;
+  launches.reserve(groups.size());
+  const auto t0 = std::chrono::steady_clock::now();
   for (auto& kv : groups)
   {
     std::vector<Request*>& g = kv.second;
     const Request& r0 = *g.front();
     const int count = static_cast<int>(g.size()), n = r0.n, m = r0.m;
+    launches.emplace_back();
+    Launch& L = launches.back();
+    L.g = &g;
+    L.n = n;
+    L.m = m;
     try
     {
       Slot& slot = cache_[kv.first];
@@ -101,30 +122,38 @@ void GpuQPBatcher::flushLocked()
         slot.capacity = count;
       }
       slot.last_round = round_;
+      L.slot = &slot;
       const std::size_t np = r0.Px->size(), na = r0.Ax->size(), nn = static_cast<std::size_t>(n),
                         mm = static_cast<std::size_t>(m);
-      std::vector<double> P(np * count), A(na * count), q(nn * count), l(mm * count), u(mm * count),
-          wx(nn * count, 0.0), wy(mm * count, 0.0), wr(static_cast<std::size_t>(count)), x(nn * count),
-          y(std::max<std::size_t>(mm, 1) * count);
-      std::vector<int> mask(static_cast<std::size_t>(count), 0);
-      std::vector<thip_qp_info> info(static_cast<std::size_t>(count));
+      L.P.resize(np * count);
+      L.A.resize(na * count);
+      L.q.resize(nn * count);
+      L.l.resize(mm * count);
+      L.u.resize(mm * count);
+      L.wx.assign(nn * count, 0.0);
+      L.wy.assign(mm * count, 0.0);
+      L.wr.resize(static_cast<std::size_t>(count));
+      L.x.resize(nn * count);
+      L.y.resize(std::max<std::size_t>(mm, 1) * count);
+      L.mask.assign(static_cast<std::size_t>(count), 0);
+      L.info.resize(static_cast<std::size_t>(count));
       bool any_warm = false;
       for (int k = 0; k < count; ++k)
       {
         const Request& r = *g[static_cast<std::size_t>(k)];
         const std::size_t ku = static_cast<std::size_t>(k);
-        std::copy(r.Px->begin(), r.Px->end(), P.begin() + static_cast<long>(ku * np));
-        std::copy(r.Ax->begin(), r.Ax->end(), A.begin() + static_cast<long>(ku * na));
-        std::copy(r.q->begin(), r.q->end(), q.begin() + static_cast<long>(ku * nn));
-        std::copy(r.l->begin(), r.l->end(), l.begin() + static_cast<long>(ku * mm));
-        std::copy(r.u->begin(), r.u->end(), u.begin() + static_cast<long>(ku * mm));
-        wr[ku] = r.settings.rho;
+        std::copy(r.Px->begin(), r.Px->end(), L.P.begin() + static_cast<long>(ku * np));
+        std::copy(r.Ax->begin(), r.Ax->end(), L.A.begin() + static_cast<long>(ku * na));
+        std::copy(r.q->begin(), r.q->end(), L.q.begin() + static_cast<long>(ku * nn));
+        std::copy(r.l->begin(), r.l->end(), L.l.begin() + static_cast<long>(ku * mm));
+        std::copy(r.u->begin(), r.u->end(), L.u.begin() + static_cast<long>(ku * mm));
+        L.wr[ku] = r.settings.rho;
         if (r.warm)
         {
           any_warm = true;
-          mask[ku] = 1;
-          std::copy(r.wx->begin(), r.wx->begin() + static_cast<long>(nn), wx.begin() + static_cast<long>(ku * nn));
-          std::copy(r.wy->begin(), r.wy->begin() + static_cast<long>(mm), wy.begin() + static_cast<long>(ku * mm));
+          L.mask[ku] = 1;
+          std::copy(r.wx->begin(), r.wx->begin() + static_cast<long>(nn), L.wx.begin() + static_cast<long>(ku * nn));
+          std::copy(r.wy->begin(), r.wy->begin() + static_cast<long>(mm), L.wy.begin() + static_cast<long>(ku * mm));
         }
       }
       {
@@ -132,25 +161,44 @@ void GpuQPBatcher::flushLocked()
         if (thip_qp_shape(slot.qp, sh) == THIP_OK && sh[0] > shape_[0])
           std::copy(sh, sh + 6, shape_);
       }
-      const auto t0 = std::chrono::steady_clock::now();
-      const int rc = thip_qp_solve_some(slot.qp, count, P.data(), q.data(), A.data(), l.data(), u.data(),
-                                        &r0.settings, any_warm ? wx.data() : nullptr, any_warm ? wy.data() : nullptr,
-                                        any_warm ? mask.data() : nullptr, wr.data(), x.data(), y.data(), info.data());
-      if (rc != THIP_OK)
-        throw std::runtime_error(std::string("GpuQPBatcher: thip_qp_solve_some: ") + thip_qp_last_error(slot.qp));
-      launch_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (thip_qp_submit(slot.qp, count, L.P.data(), L.q.data(), L.A.data(), L.l.data(), L.u.data(), &r0.settings,
+                         any_warm ? L.wx.data() : nullptr, any_warm ? L.wy.data() : nullptr,
+                         any_warm ? L.mask.data() : nullptr, L.wr.data()) != THIP_OK)
+        throw std::runtime_error(std::string("GpuQPBatcher: thip_qp_submit: ") + thip_qp_last_error(slot.qp));
+      L.submitted = true;
+    }
+    catch (const std::exception& e)
+    {
+      for (Request* r : g)
+        r->error = e.what();
+    }
+  }
+  for (Launch& L : launches)
+  {
+    if (!L.submitted)
+      continue;
+    std::vector<Request*>& g = *L.g;
+    const Request& r0 = *g.front();
+    const int count = static_cast<int>(g.size()), n = L.n, m = L.m;
+    try
+    {
+      if (thip_qp_collect(L.slot->qp, L.x.data(), L.y.data(), L.info.data()) != THIP_OK)
+        throw std::runtime_error(std::string("GpuQPBatcher: thip_qp_solve_some: ") +
+                                 thip_qp_last_error(L.slot->qp));
       ++launches_;
       qps_ += count;
+      const std::size_t np = r0.Px->size(), na = r0.Ax->size(), nn = static_cast<std::size_t>(n),
+                        mm = static_cast<std::size_t>(m);
       {
         // the algorithmic-byte model (gpu_qp_batcher.hpp bytes())
-        const double nl = static_cast<double>(thip_qp_factor_nnz(slot.qp)), nP = static_cast<double>(np),
+        const double nl = static_cast<double>(thip_qp_factor_nnz(L.slot->qp)), nP = static_cast<double>(np),
                      nA = static_cast<double>(na), N = static_cast<double>(n + m);
         const double per_solve = 2 * 12 * nl + 8 * N;
         const double per_iter = per_solve + 2 * 12 * nA + 2 * 12 * nP + 8 * (6.0 * n + 8.0 * m);
         const double per_factor = 12 * (nP + nA) + 12 * nl;
         for (int k = 0; k < count; ++k)
         {
-          const thip_qp_info& in = info[static_cast<std::size_t>(k)];
+          const thip_qp_info& in = L.info[static_cast<std::size_t>(k)];
           admm_iters_ += in.iter;
           bytes_ += in.iter * per_iter + per_factor;
           if (in.polish_status != 0)
@@ -161,9 +209,9 @@ void GpuQPBatcher::flushLocked()
       {
         Request& r = *g[static_cast<std::size_t>(k)];
         const std::size_t ku = static_cast<std::size_t>(k);
-        r.x->assign(x.begin() + static_cast<long>(ku * nn), x.begin() + static_cast<long>((ku + 1) * nn));
-        r.y->assign(y.begin() + static_cast<long>(ku * mm), y.begin() + static_cast<long>((ku + 1) * mm));
-        *r.info = info[ku];
+        r.x->assign(L.x.begin() + static_cast<long>(ku * nn), L.x.begin() + static_cast<long>((ku + 1) * nn));
+        r.y->assign(L.y.begin() + static_cast<long>(ku * mm), L.y.begin() + static_cast<long>((ku + 1) * mm));
+        *r.info = L.info[ku];
       }
     }
     catch (const std::exception& e)
@@ -172,6 +220,7 @@ void GpuQPBatcher::flushLocked()
         r->error = e.what();
     }
   }
+  launch_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   // patterns unused for kKeepRounds rounds go (collision QPs change pattern with
   // their contacts, and often return to an earlier one: a kept pattern skips
   // thip_qp_create's symbolic analysis and allocations), and at most kMaxSlots stay
