@@ -857,10 +857,10 @@ def test_full_batch_every_problem(oracle_mod, cfg, rank):
     """1024 problems per GPU, every problem against the oracle under the strict
     gate: config B, the bench workload (config C), and rank 7's shard of config D
     (configs[3]: 8192 problems over 8 GPUs, seeds 7168-8191, the per-GPU
-    workload of the last rank; its first 512 here)."""
+    workload of the last rank; its first 256 here)."""
     # (rank 7: the first half of its shard -- the suite's time budget; the
     # driver's bench runs the full 1024 of rank 0's shard)
-    B = 1024 if rank == 0 else 512
+    B = 1024 if rank == 0 else 256
     wl = sharding.rank_workload(cfg, B, rank)
     s = BatchTrustRegionSQP(wl)
     x, res = _full_size_properties(wl, s)
@@ -895,20 +895,20 @@ def test_dynamic_problem_assignment_matches_static(hip):
 
 
 @pytest.mark.timeout(1500)
-def test_full_batch_E_512(oracle_mod):
-    """Config E at one GPU's share of configs[4] (4096 problems over 8 GPUs):
-    512 problems of the 14-DoF dual arm, 50 waypoints, LVS_CONTINUOUS.
-    Properties on every problem, the strict gate on 16 problems spread over the
-    batch."""
-    wl = problems.make_workload("E", 512)
+def test_full_batch_E(oracle_mod):
+    """Config E at half of one GPU's share of configs[4] (4096 problems over 8
+    GPUs; the suite's time budget): 256 problems of the 14-DoF dual arm, 50
+    waypoints, LVS_CONTINUOUS. Properties on every problem, the strict gate on 16
+    problems spread over the batch."""
+    wl = problems.make_workload("E", 256)
     s = BatchTrustRegionSQP(wl)
     x, res = _full_size_properties(wl, s)
     s.close()
     from parity import subset
 
-    idx = np.arange(0, 512, 32)
+    idx = np.arange(0, 256, 16)
     sub = subset(wl, idx)
-    check_parity(sub, oracle_mod, x[idx], [res[i] for i in idx], label="E-512-sample16", min_strict=0.9)
+    check_parity(sub, oracle_mod, x[idx], [res[i] for i in idx], label="E-256-sample16", min_strict=0.9)
 
 
 def test_devices_stream_interop():
