@@ -670,6 +670,16 @@ int thip_qp_submit(thip_qp* qp, int count, const double* P_values, const double*
                    const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
                    const double* warm_y, const int* warm_mask, const double* warm_rho);
 int thip_qp_collect(thip_qp* qp, double* x, double* y, thip_qp_info* info);
+/* thip_qp_submit without the launch (inputs copied, arguments kept), then one
+ * launch for the staged QPs of several objects (patterns) of one device:
+ * thip_qp_launch_staged(qps, n) runs them as one grid on qps[0]'s stream (each
+ * workgroup finds its pattern), so a round of many patterns is one launch;
+ * thip_qp_collect then returns each object's results.  A destroyed qps[0] must
+ * be collected first (its stream runs the group). */
+int thip_qp_stage(thip_qp* qp, int count, const double* P_values, const double* q, const double* A_values,
+                  const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
+                  const double* warm_y, const int* warm_mask, const double* warm_rho);
+int thip_qp_launch_staged(thip_qp* const* qps, int n);
 void thip_qp_destroy(thip_qp* qp);
 const char* thip_qp_last_error(thip_qp* qp); /* NULL: the last thip_qp_create failure */
 /* Entries of the KKT factor L of the pattern (the symbolic analysis of

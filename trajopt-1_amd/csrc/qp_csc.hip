@@ -1195,13 +1195,10 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
   }
 }
 
-__global__ __launch_bounds__(kQB) void qp_csc_kernel(QpArgs args)
+// one QP of a launch: setup (scaling, rho vector, factor), warm start, ADMM,
+// polish, solution out
+__device__ __forceinline__ void qp_csc_body(const QpArgs& args, const int b, double* lv, Sh& sh)
 {
-  extern __shared__ double lv[];
-  __shared__ Sh sh;
-  const int b = blockIdx.x;
-  if (b >= args.batch)
-    return;
   const QpPattern& P = args.pat;
   const int n = P.n, m = P.m;
   double* w = args.ws + (long long)b * P.stride;
@@ -1274,6 +1271,32 @@ __global__ __launch_bounds__(kQB) void qp_csc_kernel(QpArgs args)
   __syncthreads();
   admm_solve(q, args, b, info);
 }
+
+__global__ __launch_bounds__(kQB) void qp_csc_kernel(QpArgs args)
+{
+  extern __shared__ double lv[];
+  __shared__ Sh sh;
+  if (static_cast<int>(blockIdx.x) >= args.batch)
+    return;
+  qp_csc_body(args, static_cast<int>(blockIdx.x), lv, sh);
+}
+
+// the QPs of several patterns in one launch (thip_qp_launch_staged): workgroup
+// blockIdx.x belongs to pattern g with first[g] <= blockIdx.x < first[g + 1]
+__global__ __launch_bounds__(kQB) void qp_csc_group_kernel(const QpArgs* list, const int* first, int nlist)
+{
+  extern __shared__ double lv[];
+  __shared__ Sh sh;
+  int g = 0;
+  for (int k = 1; k < nlist; ++k)
+    if (static_cast<int>(blockIdx.x) >= first[k])
+      g = k;
+  const int b = static_cast<int>(blockIdx.x) - first[g];
+  if (b >= list[g].batch)
+    return;
+  qp_csc_body(list[g], b, lv, sh);
+}
+
 
 // ---------------------------------------------------------------------------
 // Resident workspace (update in place): the OSQP 1.0 solver object kept on the
@@ -1543,6 +1566,15 @@ struct thip_qp
   int max_level = 0;    // nodes of the widest elimination-tree level (thip_qp_shape)
   hipStream_t stream = nullptr;  // thip_qp_submit / thip_qp_collect
   int pending = 0;               // QPs submitted and not yet collected
+  bool staged = false;           // thip_qp_stage: inputs on the device, launch deferred
+  QpArgs staged_args{};
+  hipStream_t done_stream = nullptr;  // the stream the pending launch runs on
+  // thip_qp_launch_staged, when this object leads a group: the argument list
+  QpArgs* d_list = nullptr;
+  int* d_first = nullptr;
+  int list_cap = 0;
+  std::vector<QpArgs> h_list;
+  std::vector<int> h_first;
   std::vector<int> bad;          // per submitted QP: l > u somewhere (osqp_setup's validate_data)
   QpPattern pat{};
   int* d_idx = nullptr;
@@ -1787,13 +1819,13 @@ int thip_qp_solve(thip_qp* q, const double* P_values, const double* qvec, const 
                             x, y, info);
 }
 
-int thip_qp_submit(thip_qp* q, int count, const double* P_values, const double* qvec, const double* A_values,
-                   const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
-                   const double* warm_y, const int* warm_mask, const double* warm_rho)
+static int qp_stage(thip_qp* q, int count, const double* P_values, const double* qvec, const double* A_values,
+                    const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
+                    const double* warm_y, const int* warm_mask, const double* warm_rho, bool launch)
 {
   if (!q)
     return THIP_E_INVALID;
-  if (q->pending)
+  if (q->pending || q->staged)
   {
     q->err = "thip_qp_submit: the previous submission is not collected";
     return THIP_E_INVALID;
@@ -1874,6 +1906,14 @@ int thip_qp_submit(thip_qp* q, int count, const double* P_values, const double* 
   if (q->lds > 65536)
     hipFuncSetAttribute(reinterpret_cast<const void*>(&qp_csc_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                         static_cast<int>(q->lds));
+  q->done_stream = q->stream;
+  if (!launch)
+  {
+    q->staged_args = a;
+    q->staged = true;
+    q->pending = B;
+    return THIP_OK;
+  }
   hipLaunchKernelGGL(qp_csc_kernel, dim3(B), dim3(kQB), q->lds, q->stream, a);
   if ((e = hipGetLastError()) != hipSuccess)
   {
@@ -1884,13 +1924,104 @@ int thip_qp_submit(thip_qp* q, int count, const double* P_values, const double* 
   return THIP_OK;
 }
 
+int thip_qp_submit(thip_qp* q, int count, const double* P_values, const double* qvec, const double* A_values,
+                   const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
+                   const double* warm_y, const int* warm_mask, const double* warm_rho)
+{
+  return qp_stage(q, count, P_values, qvec, A_values, l, u, settings, warm_x, warm_y, warm_mask, warm_rho, true);
+}
+
+int thip_qp_stage(thip_qp* q, int count, const double* P_values, const double* qvec, const double* A_values,
+                  const double* l, const double* u, const thip_osqp_settings* settings, const double* warm_x,
+                  const double* warm_y, const int* warm_mask, const double* warm_rho)
+{
+  return qp_stage(q, count, P_values, qvec, A_values, l, u, settings, warm_x, warm_y, warm_mask, warm_rho, false);
+}
+
+int thip_qp_launch_staged(thip_qp* const* qps, int n)
+{
+  if (!qps || n < 1 || !qps[0])
+    return THIP_E_INVALID;
+  thip_qp* lead = qps[0];
+  for (int k = 0; k < n; ++k)
+    if (!qps[k] || !qps[k]->staged || qps[k]->device != lead->device)
+    {
+      lead->err = "thip_qp_launch_staged: every object staged, on one device";
+      return THIP_E_INVALID;
+    }
+  hipError_t e;
+  if ((e = hipSetDevice(lead->device)) != hipSuccess)
+  {
+    lead->err = std::string("hipSetDevice: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  // the staged inputs were copied on each object's stream
+  for (int k = 0; k < n; ++k)
+    if ((e = hipStreamSynchronize(qps[k]->stream)) != hipSuccess)
+    {
+      lead->err = std::string("hipStreamSynchronize: ") + hipGetErrorString(e);
+      return THIP_E_HIP;
+    }
+  lead->h_list.resize(static_cast<size_t>(n));
+  lead->h_first.resize(static_cast<size_t>(n) + 1);
+  size_t lds = 0;
+  int total = 0;
+  for (int k = 0; k < n; ++k)
+  {
+    lead->h_list[static_cast<size_t>(k)] = qps[k]->staged_args;
+    lead->h_first[static_cast<size_t>(k)] = total;
+    total += qps[k]->staged_args.batch;
+    lds = std::max(lds, qps[k]->lds);
+  }
+  lead->h_first[static_cast<size_t>(n)] = total;
+  if (lead->list_cap < n)
+  {
+    hipFree(lead->d_list);
+    hipFree(lead->d_first);
+    lead->d_list = nullptr;
+    lead->d_first = nullptr;
+    if ((e = hipMalloc(&lead->d_list, sizeof(QpArgs) * n)) != hipSuccess ||
+        (e = hipMalloc(&lead->d_first, sizeof(int) * (n + 1))) != hipSuccess)
+    {
+      lead->list_cap = 0;
+      lead->err = std::string("hipMalloc: ") + hipGetErrorString(e);
+      return THIP_E_HIP;
+    }
+    lead->list_cap = n;
+  }
+  if ((e = hipMemcpyAsync(lead->d_list, lead->h_list.data(), sizeof(QpArgs) * n, hipMemcpyHostToDevice,
+                          lead->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(lead->d_first, lead->h_first.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice,
+                          lead->stream)) != hipSuccess)
+  {
+    lead->err = std::string("hipMemcpy: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  if (lds > 65536)
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&qp_csc_group_kernel),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+  hipLaunchKernelGGL(qp_csc_group_kernel, dim3(total), dim3(kQB), lds, lead->stream, lead->d_list, lead->d_first, n);
+  if ((e = hipGetLastError()) != hipSuccess)
+  {
+    lead->err = std::string("qp_csc_group_kernel: ") + hipGetErrorString(e);
+    return THIP_E_HIP;
+  }
+  for (int k = 0; k < n; ++k)
+  {
+    qps[k]->staged = false;
+    qps[k]->done_stream = lead->stream;
+  }
+  return THIP_OK;
+}
+
 int thip_qp_collect(thip_qp* q, double* x, double* y, thip_qp_info* info)
 {
   if (!q)
     return THIP_E_INVALID;
-  if (!q->pending)
+  if (!q->pending || q->staged)
   {
-    q->err = "thip_qp_collect: nothing submitted";
+    q->err = q->staged ? "thip_qp_collect: staged and not launched (thip_qp_launch_staged)"
+                       : "thip_qp_collect: nothing submitted";
     return THIP_E_INVALID;
   }
   if (!x || !info)
@@ -1902,7 +2033,8 @@ int thip_qp_collect(thip_qp* q, double* x, double* y, thip_qp_info* info)
   q->pending = 0;
   const size_t nn = static_cast<size_t>(n) * B, mm = static_cast<size_t>(m) * B;
   hipError_t e;
-  if ((e = hipSetDevice(q->device)) != hipSuccess || (e = hipStreamSynchronize(q->stream)) != hipSuccess)
+  if ((e = hipSetDevice(q->device)) != hipSuccess ||
+      (e = hipStreamSynchronize(q->done_stream ? q->done_stream : q->stream)) != hipSuccess)
   {
     q->err = std::string("qp_csc_kernel: ") + hipGetErrorString(e);
     return THIP_E_HIP;
@@ -2164,6 +2296,8 @@ void thip_qp_destroy(thip_qp* q)
     hipStreamSynchronize(q->stream);
     hipStreamDestroy(q->stream);
   }
+  hipFree(q->d_list);
+  hipFree(q->d_first);
   hipFree(q->d_idx);
   hipFree(q->d_ws);
   hipFree(q->d_in);

@@ -83,9 +83,10 @@ void GpuQPBatcher::flushLocked()
   std::map<std::string, std::vector<Request*>> groups;
   for (Request* r : reqs)
     groups[groupKey(*r)].push_back(r);
-  // every pattern's launch is submitted (each on its QP object's own stream)
-  // before any is collected, so the round's launches run concurrently on the
-  // device: the round takes its slowest pattern, not the sum of them
+  // every pattern's QPs are staged (inputs copied on each QP object's own
+  // stream), then the round is one launch per device (thip_qp_launch_staged:
+  // the workgroups of all patterns in one grid), then collected: the round
+  // takes its slowest QP, not the sum of its patterns' launches
   struct Launch
   {
     std::vector<Request*>* g = nullptr;
@@ -95,6 +96,7 @@ void GpuQPBatcher::flushLocked()
     std::vector<int> mask;
     std::vector<thip_qp_info> info;
     bool submitted = false;
+    int device = 0;
   };
   std::vector<Launch> launches;
   launches.reserve(groups.size());
@@ -161,16 +163,40 @@ void GpuQPBatcher::flushLocked()
         if (thip_qp_shape(slot.qp, sh) == THIP_OK && sh[0] > shape_[0])
           std::copy(sh, sh + 6, shape_);
       }
-      if (thip_qp_submit(slot.qp, count, L.P.data(), L.q.data(), L.A.data(), L.l.data(), L.u.data(), &r0.settings,
-                         any_warm ? L.wx.data() : nullptr, any_warm ? L.wy.data() : nullptr,
-                         any_warm ? L.mask.data() : nullptr, L.wr.data()) != THIP_OK)
-        throw std::runtime_error(std::string("GpuQPBatcher: thip_qp_submit: ") + thip_qp_last_error(slot.qp));
+      if (thip_qp_stage(slot.qp, count, L.P.data(), L.q.data(), L.A.data(), L.l.data(), L.u.data(), &r0.settings,
+                        any_warm ? L.wx.data() : nullptr, any_warm ? L.wy.data() : nullptr,
+                        any_warm ? L.mask.data() : nullptr, L.wr.data()) != THIP_OK)
+        throw std::runtime_error(std::string("GpuQPBatcher: thip_qp_stage: ") + thip_qp_last_error(slot.qp));
       L.submitted = true;
+      L.device = r0.device;
     }
     catch (const std::exception& e)
     {
       for (Request* r : g)
         r->error = e.what();
+    }
+  }
+  // one launch per device for every pattern staged this round
+  {
+    std::map<int, std::vector<Launch*>> by_dev;
+    for (Launch& L : launches)
+      if (L.submitted)
+        by_dev[L.device].push_back(&L);
+    for (auto& kv : by_dev)
+    {
+      std::vector<thip_qp*> qps;
+      for (Launch* L : kv.second)
+        qps.push_back(L->slot->qp);
+      if (thip_qp_launch_staged(qps.data(), static_cast<int>(qps.size())) != THIP_OK)
+      {
+        const std::string msg = std::string("GpuQPBatcher: thip_qp_launch_staged: ") + thip_qp_last_error(qps[0]);
+        for (Launch* L : kv.second)
+        {
+          L->submitted = false;
+          for (Request* r : *L->g)
+            r->error = msg;
+        }
+      }
     }
   }
   for (Launch& L : launches)
