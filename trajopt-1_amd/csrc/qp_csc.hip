@@ -702,6 +702,13 @@ __device__ void kkt_solve_v(Qp& q, const V f, PW w, double* v)
   const QpPattern& p = q.p;
   auto LX = f.LX;
   auto DG = f.DG;
+  const auto lvp = f.lvp;
+  const auto lvn = f.lvn;
+  const auto lrp = f.lrp;
+  const auto lrj = f.lrj;
+  const auto lcp = f.lcp;
+  const auto lcpos = f.lcpos;
+  const auto lci = f.lci;
   const int N = p.N, nlev = p.nlev;
   const int* perm = p.perm;
   __syncthreads();
@@ -711,11 +718,11 @@ __device__ void kkt_solve_v(Qp& q, const V f, PW w, double* v)
   long long t0 = prof ? clock64() : 0;
   for (int lev = 0; lev < nlev; ++lev)
   {
-    const int n1 = f.lvp[lev + 1];
-    for (int t = f.lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
+    const int n1 = lvp[lev + 1];
+    for (int t = lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
     {
-      const int k = f.lvn[t];
-      w[k] = row_sub(static_cast<double>(w[k]), LX, f.lrj, w, f.lrp[k], f.lrp[k + 1]);
+      const int k = lvn[t];
+      w[k] = row_sub(static_cast<double>(w[k]), LX, lrj, w, lrp[k], lrp[k + 1]);
     }
     __syncthreads();
   }
@@ -727,11 +734,11 @@ __device__ void kkt_solve_v(Qp& q, const V f, PW w, double* v)
     t0 = clock64();
   for (int lev = nlev - 1; lev >= 0; --lev)
   {
-    const int n1 = f.lvp[lev + 1];
-    for (int t = f.lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
+    const int n1 = lvp[lev + 1];
+    for (int t = lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
     {
-      const int k = f.lvn[t];
-      w[k] = col_sub(static_cast<double>(w[k]), LX, f.lcpos, f.lci, w, f.lcp[k], f.lcp[k + 1]);
+      const int k = lvn[t];
+      w[k] = col_sub(static_cast<double>(w[k]), LX, lcpos, lci, w, lcp[k], lcp[k + 1]);
     }
     __syncthreads();
   }
