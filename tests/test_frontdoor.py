@@ -343,3 +343,33 @@ def test_beyond_fused_caps_lower_for_the_generic_path():
     prims = np.concatenate([wl.scene[0]] * 2)  # 20 primitives
     d, _, _, _ = host.lower_json(host.workload_to_json(wl, 0), prims)
     assert d.n_prims == 20
+
+
+def test_hostloop_workload_lowers_jointacc_and_jointjerk(built):
+    """bench.py --config HB's problems: config B's terms plus joint_costs_unit's
+    JointAcc and JointJerk costs, which lower as jdt terms of order 2 and 3 (the
+    generic path; the fused kernel refuses them), on every step."""
+    from trajopt_amd import sharding
+
+    wl = sharding.rank_workload("B", 2, 0)
+    d, init, tgt, _ = host.lower_json(host.hostloop_workload_json(wl, 1))
+    assert d.n_cart == wl.desc.n_cart and d.jv_enabled == 1
+    assert d.n_jdt == 2 and sorted(d.jdt_order[k] for k in range(2)) == [2, 3]
+    assert all(d.jdt_is_cnt[k] == 0 for k in range(2))
+    np.testing.assert_allclose(init, wl.init[1], rtol=0, atol=1e-12)
+
+
+def test_prepared_batch_needs_a_gpu_or_fails_loudly(built):
+    """A prepared host-loop batch constructs its problems on the host, and its
+    solve fails with an error without a GPU (no CPU fallback)."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: tests/test_gpu_dropin.py::test_prepared_hostloop_batch covers it")
+    wl = problems.make_workload("B", 1)
+    pb = host.PreparedBatch([host.hostloop_workload_json(wl, 0)])
+    try:
+        with pytest.raises(host.HostError):
+            pb.solve()
+    finally:
+        pb.close()
