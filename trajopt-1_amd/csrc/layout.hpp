@@ -15,9 +15,10 @@ namespace thip
 // threads per problem workgroup.  sqp_kernel.hip is compiled twice: the main
 // build (256 threads: the register-resident ADMM segment's ownership maps and
 // launch bounds need them) and the generic-step build (THIP_GENERIC_ONLY,
-// THIP_KBLOCK = kGenBlock: no segment code, four times the waves to hide the
-// HBM latency of the generic ADMM step's row loops, for QPs the segment does
-// not take -- blocks wider than 8 dofs, more than 32 waypoints)
+// THIP_KBLOCK = kGenBlock: no segment code, twice the waves, meant to hide the
+// HBM latency of the generic ADMM step's row loops for QPs the segment does not
+// take -- blocks wider than 8 dofs, more than 32 waypoints; opt-in through
+// THIP_DEBUG_GEN_BUILD: measured no faster on config E)
 #ifndef THIP_KBLOCK
 #define THIP_KBLOCK 256
 #endif
