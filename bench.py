@@ -292,12 +292,15 @@ def main_hostloop(args, world, rank, local_rank, json_out):
                 "parallelism": f"shard{world} (independent problems, no collective)",
             },
             "roofline": {
-                # the host loops' QP rounds: one launch per round of the batch (a
-                # workgroup per QP, sparse LDL^T KKT + ADMM); per launch `achieved`
-                # is the GpuQPBatcher byte model over the wall time inside
-                # thip_qp_solve_some (upload, launch, download of the round)
+                # the host loops' QP rounds: one qp_csc_group_kernel launch per
+                # round of the batch (a workgroup per QP, sparse LDL^T KKT + ADMM);
+                # `achieved` is ALGORITHMIC bytes (the GpuQPBatcher model, which
+                # leaves out the factor of a pattern staged in LDS) over the wall
+                # time inside the rounds (staging, H2D, launch, D2H) -- not
+                # measured HBM traffic
                 "bound": "latency",
-                "kernel": "thip::qp_csc_kernel",
+                "kernel": "thip::qp_csc_group_kernel",
+                "achieved_kind": "algorithmic bytes / round wall time",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -1,12 +1,13 @@
 """Per-phase cycle breakdown of sqp_kernel (thip_debug_profile), diagnostic.
 
     python tools/phase_profile.py B 1024
+    PP_ROOT=r6nc python tools/phase_profile.py C 1024   (another build tree)
 """
 import os
 import sys
 import time
 
-sys.path.insert(0, "trajopt-1_amd")
+sys.path.insert(0, os.path.join(os.environ.get("PP_ROOT", "."), "trajopt-1_amd"))
 import numpy as np
 
 from trajopt_amd import problems

@@ -56,8 +56,12 @@ inline bool coll_pair_table(const thip_problem_desc& d, int term, std::vector<do
     any |= d.coll_pairs[k].term == term;
   if (!any)
     return false;
-  const double m0 = term == 0 ? d.coll_margin : d.coll_extra[term - 1].margin;
-  const double c0 = term == 0 ? d.coll_coeff : d.coll_extra[term - 1].coeff;
+  // term k is the main term only when it is enabled (k == 0 && coll_enabled);
+  // the extra terms follow it (term_eval.hip, validate_coll_pairs)
+  const bool main_term = d.coll_enabled && term == 0;
+  const int extra = term - (d.coll_enabled ? 1 : 0);
+  const double m0 = main_term ? d.coll_margin : d.coll_extra[extra].margin;
+  const double c0 = main_term ? d.coll_coeff : d.coll_extra[extra].coeff;
   const int ns = d.n_spheres, P = d.n_prims, W = P + ns;
   tab.assign(static_cast<std::size_t>(ns) * W * 2, 0.0);
   for (int s = 0; s < ns; ++s)

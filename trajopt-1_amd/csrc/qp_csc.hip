@@ -229,8 +229,17 @@ enum : int
 
 // phase cycles of workgroup 0's ADMM loop (diagnostic, thip_qp_debug_profile):
 // [0] iterate copies + rhs, [1] KKT solves, [2] z / y / x updates, [3] residuals,
-// termination and rho updates (incl. refactorisations), [4] iterations, [5] polish
-__device__ long long g_qp_prof[8];
+// termination and rho updates (incl. refactorisations), [4] iterations, [5] polish.
+// Compiled in only with -DTHIP_QP_PROF=1 (csrc/Makefile EXTRA): the shipped
+// kernels carry no clock reads or counter traffic on the solve's critical path.
+#ifndef THIP_QP_PROF
+#define THIP_QP_PROF 0
+#endif
+__device__ unsigned long long g_qp_prof[8];
+__device__ __forceinline__ void qp_prof_add(int k, long long v)
+{
+  atomicAdd(&g_qp_prof[k], static_cast<unsigned long long>(v));  // concurrent launches on other streams
+}
 
 
 struct Qp
@@ -714,7 +723,7 @@ __device__ void kkt_solve_v(Qp& q, const V f, PW w, double* v)
   __syncthreads();
   QFOR(k, N) w[k] = v[perm[k]];
   __syncthreads();
-  const bool prof = blockIdx.x == 0 && threadIdx.x == 0;
+  const bool prof = THIP_QP_PROF && blockIdx.x == 0 && threadIdx.x == 0;
   long long t0 = prof ? clock64() : 0;
   for (int lev = 0; lev < nlev; ++lev)
   {
@@ -727,7 +736,7 @@ __device__ void kkt_solve_v(Qp& q, const V f, PW w, double* v)
     __syncthreads();
   }
   if (prof)
-    g_qp_prof[6] += clock64() - t0;
+    qp_prof_add(6, clock64() - t0);
   QFOR(k, N) w[k] /= DG[k];
   __syncthreads();
   if (prof)
@@ -743,7 +752,7 @@ __device__ void kkt_solve_v(Qp& q, const V f, PW w, double* v)
     __syncthreads();
   }
   if (prof)
-    g_qp_prof[7] += clock64() - t0;
+    qp_prof_add(7, clock64() - t0);
   QFOR(k, N) v[perm[k]] = w[k];
   __syncthreads();
 }
@@ -1070,7 +1079,7 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
   bool can_check = false;
   bool noncvx = false;
   int it;
-  const bool prof = blockIdx.x == 0 && threadIdx.x == 0;
+  const bool prof = THIP_QP_PROF && blockIdx.x == 0 && threadIdx.x == 0;
   long long t0 = prof ? clock64() : 0, t1;
   for (it = 1; it <= args.s.max_iter; ++it)
   {
@@ -1084,14 +1093,14 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
     if (prof)
     {
       t1 = clock64();
-      g_qp_prof[0] += t1 - t0;
+      qp_prof_add(0, t1 - t0);
       t0 = t1;
     }
     kkt_solve(q, XT);  // (x~, nu) in place
     if (prof)
     {
       t1 = clock64();
-      g_qp_prof[1] += t1 - t0;
+      qp_prof_add(1, t1 - t0);
       t0 = t1;
     }
     QFOR(r, m) XT[n + r] = (ZP[r] - RHOI[r] * Y[r]) + RHOI[r] * XT[n + r];  // z~ = rhs + nu / rho
@@ -1114,7 +1123,7 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
     if (prof)
     {
       t1 = clock64();
-      g_qp_prof[2] += t1 - t0;
+      qp_prof_add(2, t1 - t0);
       t0 = t1;
     }
     can_check = args.s.check_termination && (it % args.s.check_termination == 0);
@@ -1142,8 +1151,8 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
     if (prof)
     {
       t1 = clock64();
-      g_qp_prof[3] += t1 - t0;
-      g_qp_prof[4] += 1;
+      qp_prof_add(3, t1 - t0);
+      qp_prof_add(4, 1);
       t0 = t1;
     }
     if (done)
@@ -1180,7 +1189,7 @@ __device__ void admm_solve(Qp& q, const QpArgs& args, int b, thip_qp_info* info)
     if (args.s.polishing && sh.status == SOLVED)
       polish(q);
     if (prof)
-      g_qp_prof[5] += clock64() - t0;
+      qp_prof_add(5, clock64() - t0);
   }
   // store_solution (unscaled), NaN on infeasibility
   const int st = sh.status;
@@ -1950,24 +1959,32 @@ int thip_qp_launch_staged(thip_qp* const* qps, int n)
   if (!qps || n < 1 || !qps[0])
     return THIP_E_INVALID;
   thip_qp* lead = qps[0];
+  // any failure: the staged submissions are dropped (staged and pending
+  // cleared), so the objects take new submissions instead of refusing every
+  // later one as "not collected"
+  auto fail = [&](int code, std::string msg) {
+    for (int k = 0; k < n; ++k)
+      if (qps[k] && qps[k]->staged)
+      {
+        qps[k]->staged = false;
+        qps[k]->pending = 0;
+      }
+    lead->err = std::move(msg);
+    return code;
+  };
   for (int k = 0; k < n; ++k)
     if (!qps[k] || !qps[k]->staged || qps[k]->device != lead->device)
-    {
-      lead->err = "thip_qp_launch_staged: every object staged, on one device";
-      return THIP_E_INVALID;
-    }
+      return fail(THIP_E_INVALID, "thip_qp_launch_staged: every object staged, on one device");
   hipError_t e;
   if ((e = hipSetDevice(lead->device)) != hipSuccess)
   {
-    lead->err = std::string("hipSetDevice: ") + hipGetErrorString(e);
-    return THIP_E_HIP;
+    return fail(THIP_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
   }
   // the staged inputs were copied on each object's stream
   for (int k = 0; k < n; ++k)
     if ((e = hipStreamSynchronize(qps[k]->stream)) != hipSuccess)
     {
-      lead->err = std::string("hipStreamSynchronize: ") + hipGetErrorString(e);
-      return THIP_E_HIP;
+      return fail(THIP_E_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
     }
   lead->h_list.resize(static_cast<size_t>(n));
   lead->h_first.resize(static_cast<size_t>(n) + 1);
@@ -1991,8 +2008,7 @@ int thip_qp_launch_staged(thip_qp* const* qps, int n)
         (e = hipMalloc(&lead->d_first, sizeof(int) * (n + 1))) != hipSuccess)
     {
       lead->list_cap = 0;
-      lead->err = std::string("hipMalloc: ") + hipGetErrorString(e);
-      return THIP_E_HIP;
+      return fail(THIP_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
     }
     lead->list_cap = n;
   }
@@ -2001,8 +2017,7 @@ int thip_qp_launch_staged(thip_qp* const* qps, int n)
       (e = hipMemcpyAsync(lead->d_first, lead->h_first.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice,
                           lead->stream)) != hipSuccess)
   {
-    lead->err = std::string("hipMemcpy: ") + hipGetErrorString(e);
-    return THIP_E_HIP;
+    return fail(THIP_E_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
   }
   if (lds > 65536)
     hipFuncSetAttribute(reinterpret_cast<const void*>(&qp_csc_group_kernel),
@@ -2010,8 +2025,7 @@ int thip_qp_launch_staged(thip_qp* const* qps, int n)
   hipLaunchKernelGGL(qp_csc_group_kernel, dim3(total), dim3(kQB), lds, lead->stream, lead->d_list, lead->d_first, n);
   if ((e = hipGetLastError()) != hipSuccess)
   {
-    lead->err = std::string("qp_csc_group_kernel: ") + hipGetErrorString(e);
-    return THIP_E_HIP;
+    return fail(THIP_E_HIP, std::string("qp_csc_group_kernel: ") + hipGetErrorString(e));
   }
   for (int k = 0; k < n; ++k)
   {
@@ -2103,6 +2117,13 @@ static int qp_resident(thip_qp* q, int op, const double* P_values, const double*
                        double* y, thip_qp_info* info)
 {
   const int n = q->n, m = q->m, B = q->batch;
+  // the resident calls use d_in / d_ws synchronously on the null stream: an
+  // uncollected submission (its own stream) would race them
+  if (q->pending || q->staged)
+  {
+    q->err = "thip_qp resident call: a submission is not collected (thip_qp_collect first)";
+    return THIP_E_INVALID;
+  }
   hipError_t e;
   if ((e = hipSetDevice(q->device)) != hipSuccess)
   {
@@ -2298,6 +2319,11 @@ void thip_qp_destroy(thip_qp* q)
   if (!q)
     return;
   hipSetDevice(q->device);
+  // an uncollected group launch runs on another object's stream (done_stream,
+  // which may already be destroyed) and may still read this object's buffers:
+  // wait for the whole device then
+  if (q->pending)
+    hipDeviceSynchronize();
   if (q->stream)
   {
     hipStreamSynchronize(q->stream);

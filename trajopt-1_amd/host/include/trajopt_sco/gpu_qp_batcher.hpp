@@ -58,7 +58,9 @@ public:
   // qp_csc.hip, per QP: each ADMM iteration streams the factor L twice -- the
   // forward and backward solves, value and index -- plus D, A x and A'y, P x
   // and the iterate vectors; each factorisation reads the KKT values and writes
-  // L; polish adds one factorisation and 1 + polish_refine_iter solves)
+  // L; polish adds one factorisation and 1 + polish_refine_iter solves).  A
+  // pattern staged in LDS (thip_qp_shape out[4]) keeps L out of HBM: its
+  // factor and solve terms count only the vectors
   double bytes() const { return bytes_; }
   long long admmIters() const { return admm_iters_; }
   // wall seconds of the rounds on the device: first submission to last collection

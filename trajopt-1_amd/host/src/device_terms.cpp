@@ -117,8 +117,11 @@ const DeviceTermEvaluator::Contacts& DeviceTermEvaluator::collision(int term, co
   c.c.coeff.resize(static_cast<std::size_t>(count));
   const thip_problem_desc& d = prob_->desc();
   const std::vector<double>& tab = pair_tab_[static_cast<std::size_t>(term)];
-  const double m0 = term == 0 ? d.coll_margin : d.coll_extra[term - 1].margin;
-  const double c0 = term == 0 ? d.coll_coeff : d.coll_extra[term - 1].coeff;
+  // the main term only when enabled (pair_data.hpp coll_pair_table)
+  const bool main_term = d.coll_enabled && term == 0;
+  const int extra = term - (d.coll_enabled ? 1 : 0);
+  const double m0 = main_term ? d.coll_margin : d.coll_extra[extra].margin;
+  const double c0 = main_term ? d.coll_coeff : d.coll_extra[extra].coeff;
   for (int r = 0; r < count; ++r)
   {
     const double* rec = c.c.rec.data() + static_cast<std::size_t>(r) * W;

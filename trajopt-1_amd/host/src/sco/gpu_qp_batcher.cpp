@@ -217,8 +217,13 @@ void GpuQPBatcher::flushLocked()
                         mm = static_cast<std::size_t>(m);
       {
         // the algorithmic-byte model (gpu_qp_batcher.hpp bytes())
-        const double nl = static_cast<double>(thip_qp_factor_nnz(L.slot->qp)), nP = static_cast<double>(np),
-                     nA = static_cast<double>(na), N = static_cast<double>(n + m);
+        // a pattern staged in LDS (thip_qp_shape out[4]: factor, D and the
+        // 16-bit indices LDS-resident for the whole launch) never streams L
+        // from HBM, so its factor and solve terms count only the vectors
+        long long sh[6] = { 0, 0, 0, 0, 0, 0 };
+        const bool lds_pat = thip_qp_shape(L.slot->qp, sh) == THIP_OK && sh[4] != 0;
+        const double nl = lds_pat ? 0.0 : static_cast<double>(thip_qp_factor_nnz(L.slot->qp)),
+                     nP = static_cast<double>(np), nA = static_cast<double>(na), N = static_cast<double>(n + m);
         const double per_solve = 2 * 12 * nl + 8 * N;
         const double per_iter = per_solve + 2 * 12 * nA + 2 * 12 * nP + 8 * (6.0 * n + 8.0 * m);
         const double per_factor = 12 * (nP + nA) + 12 * nl;
