@@ -11,6 +11,8 @@ cost against a 10-primitive scene, 1024 problems per GPU.  `value` is SQP
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 1024]
     python bench.py --config HB --batch 256     (host-loop workload, see main_hostloop)
+    python bench.py --config HA                 (config B + JointAcc cost: the fused kernel's
+                                                 waypoint-pair solve)
 
 Batches in flight: the runtime keeps `--inflight` (default 3) batch contexts,
 each with its own HIP stream, and submits step k to context k mod inflight,
@@ -55,6 +57,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 
 def workload_name(wl, config, batch):
     terms = f"JointVel + {wl.desc.n_cart} CartPose ABS costs"
+    if wl.desc.n_jdt:
+        terms += " + JointAcc cost (joint_costs_unit; waypoint-pair solve)"
     if wl.desc.coll_enabled:
         ev = {0: "LVS-discrete", 1: "LVS-continuous", 2: "discrete"}[wl.desc.coll_continuous]
         terms += f" + {ev} collision cost ({wl.desc.n_prims}-primitive scene)"
@@ -75,6 +79,12 @@ def algorithmic_bytes(wl, results):
     nnz_a = R * (D + 2) + D * wl.desc.n_fixed + n
     nnz_p = nx + (N - 1) * D
     nnz_l = N * D * (D + 1) // 2 + (N - 1) * D * D  # block-tridiagonal Cholesky factor
+    if wl.desc.n_jdt:
+        # JointAccEqCost: P couples t and t + 2; the factor is block-tridiagonal over
+        # waypoint pairs (N / 2 blocks of 2 D)
+        nnz_p += (N - 2) * D
+        G, sD = N // 2, 2 * D
+        nnz_l = G * sD * (sD + 1) // 2 + (G - 1) * sD * sD
     fixed = 2 * 8 * nx + 8 * R * (1 + D) + 96 * wl.desc.n_cart + 2 * 8 * (n + 2 * m + R * (D + 2))
     per_admm = 2 * 12 * nnz_a + 24 * nnz_p + 8 * (3 * n + 7 * m)
     refine = wl.desc.osqp.polish_refine_iter

@@ -301,15 +301,17 @@ typedef struct thip_problem_desc {
   double jvx_upper_tols[THIP_MAX_JVX][THIP_MAX_DOF];
   double jvx_lower_tols[THIP_MAX_JVX][THIP_MAX_DOF];
 
-  /* Joint-derivative terms the fused sqp_kernel does not lower (the generic
-   * path runs them: sco::BasicTrustRegionSQP on the host with the GpuModel):
-   * order 1 JointVelEqConstraint (trajectory_costs.cpp:376-424), order 2
-   * JointAcc{Eq,Ineq}{Cost,Constraint} (:502-753), order 3 JointJerk (:756-1016),
-   * zero tolerances -> Eq forms.  Steps after the hatch clamping
-   * (problem_description.cpp:1412-1533, 1534-1640).  Costs follow every other
-   * cost term but collision, constraints every other constraint but collision.
-   * thip_create rejects a descriptor with n_jdt > 0; it is the lowered record
-   * the oracle reads. */
+  /* Joint-derivative terms: order 1 JointVelEqConstraint (trajectory_costs.cpp:
+   * 376-424), order 2 JointAcc{Eq,Ineq}{Cost,Constraint} (:502-753), order 3
+   * JointJerk (:756-1016), zero tolerances -> Eq forms.  Steps after the hatch
+   * clamping (problem_description.cpp:1412-1533, 1534-1640).  Costs follow every
+   * other cost term but collision, constraints every other constraint but
+   * collision.  The fused sqp_kernel lowers JointAccEqCost (order 2, cost, zero
+   * tolerances) when thip_jdt_fused() holds: the reduced KKT matrix is then
+   * block-tridiagonal over waypoint PAIRS (2 D-wide blocks).  Every other form is
+   * refused by thip_create and runs the generic path (sco::BasicTrustRegionSQP
+   * on the host with the GpuModel); this table is also the record the oracle
+   * reads. */
   int n_jdt;
   int jdt_order[THIP_MAX_JDT];
   int jdt_is_cnt[THIP_MAX_JDT];
@@ -412,6 +414,13 @@ typedef struct thip_problem_desc {
   thip_sqp_params sqp;
   thip_osqp_settings osqp;
 } thip_problem_desc;
+
+/* 1 when the descriptor's jdt terms can run in the fused sqp_kernel: every one a
+ * JointAccEqCost (order 2, cost, all tolerances zero as JointAccTermInfo::hatch
+ * tests them, |tol| < 1e-5), the waypoints pairing into 2 D-wide solve blocks
+ * (n_steps even, 2 n_dof <= THIP_MAX_DOF), no time parameterisation.  0 when a
+ * jdt term needs the generic path; also 1 without jdt terms. */
+int thip_jdt_fused(const thip_problem_desc* d);
 
 /* Per-problem results (sco::OptResults + counters the build adds). */
 typedef struct thip_result {
@@ -558,8 +567,10 @@ int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws);
 /* The solve layout a context chose (diagnostic): out[0] block-solve branches
  * (Layout::nbr), out[1] dofs per block, out[2] wide blocks, out[3] the
  * register-resident segment possible, out[4] the generic-step build,
- * out[5] threads per problem.  n: entries of out (<= 6 written). */
-#define THIP_LAYOUT_INFO_N 6
+ * out[5] threads per problem, out[6] waypoints per solve block (Layout::grp:
+ * 2 with JointAccEqCost terms), out[7] solve blocks per branch.  n: entries of
+ * out (<= 8 written). */
+#define THIP_LAYOUT_INFO_N 8
 int thip_debug_solve_layout(const thip_ctx* ctx, int* out, int n);
 
 /* ------------------------------------------------------- Term evaluation

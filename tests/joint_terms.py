@@ -220,9 +220,22 @@ PROBLEMS = {
 LOWERABLE = {"equality_jointPos", "inequality_jointPos", "inequality_jointVel"}
 
 
+def jdt_fused(desc):
+    """thip_jdt_fused (trajopt_hip.h): every jdt term a JointAccEqCost on an even
+    number of waypoints with 2 n_dof <= 16 (waypoint-pair blocks)."""
+    D = desc.chain.n_dof
+    if desc.n_jdt == 0:
+        return True
+    if desc.n_steps % 2 or 2 * D > 16 or desc.use_time:
+        return False
+    return all(desc.jdt_order[k] == 2 and not desc.jdt_is_cnt[k] and
+               all(abs(desc.jdt_upper_tols[k][j]) < 1e-5 and abs(desc.jdt_lower_tols[k][j]) < 1e-5 for j in range(D))
+               for k in range(desc.n_jdt))
+
+
 def lowerable(desc):
     """TrajOptProb::lowerable(): no term or variable the kernel does not lower."""
-    return desc.n_jdt == 0 and desc.n_jvt == 0 and desc.n_ttt == 0 and not desc.use_time and desc.n_fixed_dofs == 0
+    return jdt_fused(desc) and desc.n_jvt == 0 and desc.n_ttt == 0 and not desc.use_time and desc.n_fixed_dofs == 0
 
 
 def workload(text, host):

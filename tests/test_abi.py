@@ -129,3 +129,26 @@ def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(abi, "_hip", None)
     with pytest.raises(RuntimeError, match="missing"):
         abi.load_hip()
+
+
+def test_jdt_fused_domain(lib):
+    """thip_jdt_fused (trajopt_hip.h): the fused kernel takes JointAccEqCost terms on an
+    even number of waypoints with 2 n_dof <= 16; every other joint-derivative form (a
+    constraint, tolerances, JointJerk, an odd horizon) is the generic path's."""
+    def fused(wl):
+        return lib.thip_jdt_fused(C.byref(wl.desc))
+
+    assert fused(problems.make_workload("B", 1)) == 1  # no jdt terms
+    assert fused(problems.with_joint_acc(problems.make_workload("B", 1))) == 1
+    assert fused(problems.make_workload("HA", 1)) == 1
+    assert fused(problems.with_joint_acc(problems.make_workload("B", 1, n_steps=29))) == 0
+    wl = problems.with_joint_acc(problems.make_workload("B", 1))
+    wl.desc.jdt_is_cnt[0] = 1
+    assert fused(wl) == 0
+    wl = problems.with_joint_acc(problems.make_workload("B", 1))
+    wl.desc.jdt_upper_tols[0][3] = 0.1
+    assert fused(wl) == 0
+    wl = problems.with_joint_acc(problems.make_workload("B", 1))
+    wl.desc.jdt_order[0] = 3
+    assert fused(wl) == 0
+    assert fused(problems.with_joint_acc(problems.make_workload("E", 1))) == 0  # 2 x 14 dofs > 16

@@ -1203,6 +1203,75 @@ def test_sqp_parity_dual_arm_E_branches(oracle_mod, hip):
     assert same >= 7, f"unsplit and two-branch solves agree on {same} of 8 problems"
 
 
+# ------------------------------------------------------------ JointAccEqCost in the fused kernel
+# (trajectory_costs.cpp:502-546, JointAccTermInfo::hatch problem_description.cpp:1412-1533):
+# P couples waypoints t and t + 2, so the reduced KKT matrix is block-tridiagonal
+# over waypoint PAIRS (Layout::grp = 2, 2 D-wide blocks on the wide block path)
+def test_joint_acc_runs_the_pair_layout():
+    wl = problems.with_joint_acc(problems.make_workload("B", 2))
+    s = BatchTrustRegionSQP(wl)
+    lay = s.layout()
+    s.close()
+    assert lay["grp"] == 2 and lay["block_dofs"] == 14 and lay["wide"] == 1 and lay["blocks"] == 15, lay
+    assert lay["seg_ok"] == 0 and lay["nbr"] == 1, lay
+
+
+def test_joint_acc_odd_horizon_is_refused():
+    """An odd number of waypoints does not pair: thip_create names the generic path."""
+    wl = problems.with_joint_acc(problems.make_workload("B", 2, n_steps=29))
+    with pytest.raises(HipError) as ei:
+        BatchTrustRegionSQP(wl)
+    assert "generic path" in str(ei.value)
+
+
+def _joint_acc_variant(name):
+    if name == "B-acc":
+        return problems.with_joint_acc(problems.make_workload("B", 32, first_problem=100))
+    if name == "C-acc":
+        return problems.with_joint_acc(problems.make_workload("C", 16, first_problem=100))
+    if name == "A-acc":
+        # 10 waypoints, the CartPose constraint on the last one, acceleration cost on steps 2..7
+        return problems.with_joint_acc(problems.make_workload("A", 32, first_problem=100), coeff=2.0, target=0.01,
+                                       first_step=2, last_step=7)
+    if name == "J-acc-8dof":
+        return problems.with_joint_acc(problems.make_workload("J", 16, robot="torso_right_arm", goal_offset=0.05),
+                                       coeff=0.5)
+    if name == "B-acc-two-terms":
+        wl = problems.with_joint_acc(problems.make_workload("B", 16, first_problem=140), coeff=1.0)
+        return problems.with_joint_acc(wl, coeff=3.0, target=-0.002, first_step=10, last_step=20)
+    raise KeyError(name)
+
+
+@pytest.mark.parametrize("name", ["B-acc", "C-acc", "A-acc", "J-acc-8dof", "B-acc-two-terms"])
+def test_sqp_parity_joint_acc(oracle_mod, name):
+    wl = _joint_acc_variant(name)
+    x, res, _ = solve_gpu(wl)
+    assert all(r.flags == 0 for r in res)
+    check_parity(wl, oracle_mod, x, res, label=name)
+
+
+def test_joint_acc_reference_unit_cost(oracle_mod):
+    """joint_costs_unit.cpp:677-766 (equality_jointAcc), its cost part: JointAcc
+    coefficient 10 targeting 0.1 on every step of a 10-waypoint stationary start
+    (the PR2 right arm at rest); EXPECT_NEAR(accel, 0.1, 0.01) on every step, and
+    parity with the oracle (the unit's zero-acceleration constraint on step 0 is an
+    abs row over three waypoints: the generic path runs that form)."""
+    wl = problems.make_workload("J", 4)
+    d = wl.desc
+    d.n_jpos = 0
+    d.n_fixed = 0
+    d.jv_enabled = 0
+    for j in range(wl.n_dof):  # a stationary start in the middle of each joint's range
+        lo, hi = d.chain.lower[j], d.chain.upper[j]
+        wl.init[:, :, j] = 0.5 * (lo + hi) if hi - lo < 10 else 0.0
+    problems.with_joint_acc(wl, coeff=10.0, target=0.1)
+    x, res, _ = solve_gpu(wl)
+    for b in range(wl.batch):
+        acc = x[b, :-2] - 2 * x[b, 1:-1] + x[b, 2:]
+        assert np.abs(acc - 0.1).max() < 0.01, np.abs(acc - 0.1).max()
+    check_parity(wl, oracle_mod, x, res, label="jointacc-unit-cost", min_strict=0.0)
+
+
 def test_zz_pooled_strict_fraction():
     """Pooled over every parity check of the session that carries a fraction
     bound: at least 93 % of all problems meet the bar strictly (the rest carry

@@ -48,6 +48,8 @@ def make(name, B, problems=problems):
         wl.desc.coll_is_cnt = 1
     elif var == "tol":
         problems.with_cart_tolerances(wl, rot=0.2, axes=(3,))
+    elif var == "acc":
+        problems.with_joint_acc(wl)
     return wl
 
 

@@ -41,7 +41,10 @@ def workload(name):
         return wl
     import test_gpu
 
-    return test_gpu._variant(name)
+    try:
+        return test_gpu._variant(name)
+    except KeyError:
+        return test_gpu._joint_acc_variant(name)  # B-acc, C-acc, ... (JointAccEqCost)
 
 
 def fmt(r):

@@ -28,6 +28,10 @@ constexpr int kWaves = kBlock / 64;
 #define THIP_GEN_BLOCK 512
 #endif
 constexpr int kGenBlock = THIP_GEN_BLOCK;  // threads of the generic-step build
+// 1,024 threads faults on collision problems (HSA aperture violation, config C;
+// configs J and B run clean and bitwise at 1,024: DESIGN.md section 4), and 512
+// was measured no faster than 256 -- the build refuses anything above 512
+static_assert(kGenBlock == 256 || kGenBlock == 512, "the generic-step build runs 256 or 512 threads");
 // waves that run the contact scan's per-wave step pairs (their sub-state
 // scratch A_CSCR is sized for this many); further waves take part in the
 // batched sub-state FK only
@@ -126,6 +130,7 @@ enum DArr : int
   A_HPART,   // hinge chunk partial sums [n_chunks][16]
   A_HCT,     // ADMM-segment copy of A_HC, field-major [2D][n_h | 1] (odd stride: no LDS bank conflicts)
   A_CPK,     // ADMM-segment chain pack (kCpk doubles, N <= 32 and D <= 8; see seg_chain_solve)
+  A_PO2,     // scaled P (t,j)-(t+2,j) coupling of JointAccEqCost terms (nx; Layout::grp == 2)
   A_COUNT
 };
 
@@ -187,6 +192,10 @@ struct Layout
   int n_jvx;      // further JointVel tolerance terms (static hinge owners n_jpos + 1 + x)
   int jv_first, jv_last;
   int jv_ineq;    // JointVelIneqCost (tolerances) instead of the quadratic JointVelEqCost
+  // JointAccEqCost terms (desc jdt_*, thip_jdt_fused): their cost slots; P gains
+  // the (t, t+2) coupling A_PO2 and the solve pairs waypoints (grp = 2)
+  int n_jacc;
+  int jacc_slot[THIP_MAX_JDT];
   int hinge;      // the QP has hinge rows (collision contacts and/or static hinge rows)
   long long dstride;  // doubles per problem
   long long istride;  // ints per problem
@@ -228,6 +237,13 @@ struct Layout
   int nbr;
   int sD;
   int sN;
+  // Waypoint pairs (JointAccEqCost: P couples t and t + 2, so the reduced KKT
+  // matrix is block-tridiagonal over pairs, not over waypoints): grp = 2 makes
+  // solve block T waypoints 2T and 2T + 1 (sD = 2 D, sN = N / 2; the solve
+  // layout is the column order itself).  grp = 1 otherwise.  sNb: solve blocks
+  // per branch (N / grp), the length of each twisted factorisation.
+  int grp;
+  int sNb;
   // the CartPose rows of every waypoint are contiguous and in order (step_rows
   // is the identity): the generic step reads a waypoint's rows without the
   // step_rows indirection (max_step_rows: the most rows of one waypoint)

@@ -1580,6 +1580,24 @@ __device__ void jpos_values(Ctx& c, const double* x, double* costs, double* viol
   }
 }
 
+// JointAccEqCost::value (trajectory_costs.cpp:533-542) of jdt term k at x:
+// sum over (i, j) of c_j (diffAxis0(diffAxis0(traj))_{i,j} - targ_j)^2, the
+// repeated difference (x_i+2 - x_i+1) - (x_i+1 - x_i) as diffAxis0 forms it.
+// Also its model value (the quadratic is exact).  All threads; block sum.
+__device__ double jacc_value(Ctx& c, const double* x, int k)
+{
+  const int D = c.L.D, f = c.d->jdt_first_step[k], n = (c.d->jdt_last_step[k] - 2 - f + 1) * D;
+  double v = 0;
+  FOR(e, n)
+  {
+    const int i = f + e / D, j = e % D;
+    const double x0 = x[i * D + j], x1 = x[(i + 1) * D + j], x2 = x[(i + 2) * D + j];
+    const double dd = ((x2 - x1) - (x1 - x0)) - c.d->jdt_targets[k][j];
+    v += (dd * dd) * c.d->jdt_coeffs[k][j];
+  }
+  return block_sum(c, v);
+}
+
 // ======================================================================
 // Exact cost values / constraint violations at x (Cost::value,
 // Constraint::violation).  costs[n_costs], viols[n_cnts]
@@ -1605,6 +1623,12 @@ __device__ void evaluate(Ctx& c, const double* x, double* costs, double* viols)
   jv = block_sum(c, jv);
   if (c.tid == 0 && c.d->jv_enabled && !L.jv_ineq)
     costs[0] = jv;
+  for (int k = 0; k < L.n_jacc; ++k)
+  {
+    const double v = jacc_value(c, x, k);
+    if (c.tid == 0)
+      costs[L.jacc_slot[k]] = v;
+  }
   const double* tgt = c.a(A_TGT);
   FOR(k, L.n_cart)
   {
@@ -1699,10 +1723,37 @@ __device__ void build_and_scale(Ctx& c)
   double *GS = c.a(A_GS), *WS = c.a(A_WS), *FS = c.a(A_FS), *E = c.a(A_E);
   const double *G = c.a(A_G), *MU = c.a(A_MU);
   // ---- unscaled data
+  double* PO2 = (L.grp > 1) ? c.a(A_PO2) : nullptr;
   FOR(col, nx)
   {
     const int t = col / D, j = col % D;
-    double pd = 0, po = 0, q = 0;
+    double pd = 0, po = 0, po2 = 0, q = 0;
+    // JointAccEqCost (trajectory_costs.cpp:502-531): coeff * exprSquare(x_i - 2 x_i+1
+    // + x_i+2 - targ) per (i, j), i = first .. last - 2: squares a_p^2 c on the
+    // diagonal (P_tt = 2 sum), cross terms (2 a_p a_r) c on (t, t+1) and (t, t+2),
+    // linear (2 (-targ) a_p) c (expr_ops.cpp exprSquare; zero coefficients skipped)
+    double jsq = 0, jq = 0;
+    for (int k = 0; k < L.n_jacc; ++k)
+    {
+      const double ck = c.d->jdt_coeffs[k][j], tk = c.d->jdt_targets[k][j];
+      const int f = c.d->jdt_first_step[k], l = c.d->jdt_last_step[k] - 2;
+      constexpr double st[3] = { 1.0, -2.0, 1.0 };
+      for (int p = 0; p < 3; ++p)
+        if (t - p >= f && t - p <= l)
+        {
+          jsq += (st[p] * st[p]) * ck;
+          const double v = (2 * (-tk) * st[p]) * ck;
+          if (v != 0.)
+            jq += v;
+        }
+      if (t >= f && t <= l)
+      {
+        po += (2 * st[0] * st[1]) * ck;  // term i = t: positions 0, 1
+        po2 += (2 * st[0] * st[2]) * ck;
+      }
+      if (t - 1 >= f && t - 1 <= l)
+        po += (2 * st[1] * st[2]) * ck;  // term i = t - 1: positions 1, 2
+    }
     if (c.d->jv_enabled && !L.jv_ineq)
     {
       const double cj = c.d->jv_coeffs[j], tg = c.d->jv_targets[j];
@@ -1713,8 +1764,9 @@ __device__ void build_and_scale(Ctx& c)
         dsum += cj;
       if (here)
         dsum += cj;
+      dsum += jsq;
       pd = dsum + dsum;
-      po = here ? cj * -2.0 : 0.0;
+      po = (here ? cj * -2.0 : 0.0) + po;
       // q: term t-1 contributes (2*(-tg)*1)*c, term t (2*(-tg)*(-1))*c; zero coefficients skipped
       double qa = 0;
       if (prev)
@@ -1729,7 +1781,12 @@ __device__ void build_and_scale(Ctx& c)
         if (v != 0.)
           qa += v;
       }
-      q = qa;
+      q = qa + jq;
+    }
+    else
+    {
+      pd = jsq + jsq;
+      q = jq;
     }
     // JointPosEqCost: exprSquare(x - targ) * c -> P diagonal 2c, q -2 targ c (trajectory_costs.cpp:40-51)
     for (int k = 0; k < L.n_jpos; ++k)
@@ -1743,6 +1800,8 @@ __device__ void build_and_scale(Ctx& c)
       }
     PD[col] = pd;
     PO[col] = po;
+    if (PO2)
+      PO2[col] = po2;
     Q[col] = q;
     DS[col] = 1.0;
     BS[col] = 1.0;
@@ -1812,6 +1871,13 @@ __device__ void build_and_scale(Ctx& c)
           v = fmax(v, fabs(PO[col]));
         if (t > 0)
           v = fmax(v, fabs(PO[col - D]));
+        if (PO2)
+        {
+          if (t < L.N - 2)
+            v = fmax(v, fabs(PO2[col]));
+          if (t > 1)
+            v = fmax(v, fabs(PO2[col - 2 * D]));
+        }
         const int f = c.T.fixed_of_step[t];
         if (f >= 0)
           v = fmax(v, fabs(FS[f * D + j]));
@@ -1875,6 +1941,8 @@ __device__ void build_and_scale(Ctx& c)
         PD[col] = (PD[col] * Dt[col]) * Dt[col];
         if (t < L.N - 1)
           PO[col] = (PO[col] * Dt[col]) * Dt[col + D];
+        if (PO2 && t < L.N - 2)
+          PO2[col] = (PO2[col] * Dt[col]) * Dt[col + 2 * D];
       }
       BS[col] = (BS[col] * Et[bound_row(L, col)]) * Dt[col];
       Q[col] *= Dt[col];
@@ -1921,6 +1989,13 @@ __device__ void build_and_scale(Ctx& c)
           v = fmax(v, fabs(PO[col]));
         if (t > 0)
           v = fmax(v, fabs(PO[col - D]));
+        if (PO2)
+        {
+          if (t < L.N - 2)
+            v = fmax(v, fabs(PO2[col]));
+          if (t > 1)
+            v = fmax(v, fabs(PO2[col - 2 * D]));
+        }
         colsum += v;
       }
       qn = fmax(qn, fabs(Q[col]));
@@ -1939,6 +2014,8 @@ __device__ void build_and_scale(Ctx& c)
       {
         PD[col] *= ct;
         PO[col] *= ct;
+        if (PO2)
+          PO2[col] *= ct;
       }
       Q[col] *= ct;
     }
@@ -2081,9 +2158,10 @@ __device__ __noinline__ void twisted_factor_half(Ctx& c, Solver& sv, const doubl
   const Layout& L = c.L;
   // the solve layout's blocks (Layout::nbr): wave 2b runs branch b's top half,
   // wave 2b + 1 its bottom half
-  const int D = L.sD, N = L.N, DD = D * D, m = L.tw_mid, half = c.wave & 1, base = (c.wave >> 1) * N;
+  // (N: the solve blocks of a branch, Layout::sNb)
+  const int D = L.sD, N = L.sNb, DD = D * D, m = L.tw_mid, half = c.wave & 1, base = (c.wave >> 1) * N;
   const int len = (half == 0) ? m : (N - 1 - m);
-  const bool use_cpl = L.hinge || L.nbr > 1;
+  const bool use_cpl = L.hinge || L.nbr > 1 || L.grp > 1;
   lds_f64* S = lds(Sp);
   lds_f64* Ls = lds(Lsp);
   for (int k = 0; k < len; ++k)
@@ -2253,14 +2331,12 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
     }
     BSYNC();
   }
-  // diagonal blocks, in the solve layout (Layout::nbr): block T = b N + t holds
-  // waypoint t's dofs [b sD, (b + 1) sD); the other branches' entries of the
-  // waypoint block are exact zeros (no term touches two branches)
-  const int sD = L.sD, sDD = sD * sD;
-  FOR(e, L.sN * sDD)
-  {
-    const int T = e / sDD, bi = T / N, t = T - bi * N;
-    const int i = bi * sD + (e / sD) % sD, j = bi * sD + e % sD;  // dofs of the waypoint block
+  // waypoint t's diagonal block entry (i, j): P, sigma + bound rows, the fixed
+  // rows, its CartPose rows and the hinge rows of pairs t and t - 1 (the row
+  // sums in chunks of 8 rows, all loads of a chunk first; masked terms add
+  // fma(w, 0, v) = v: a loop of dependent loads otherwise)
+  const int nh_ = nh;
+  auto wblock = [&](int t, int i, int j) {
     double v = 0;
     if (i == j)
     {
@@ -2272,8 +2348,6 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
         v += rho_k(c, fr, polish, delta) * (FS[fr] * FS[fr]);
       }
     }
-    // the row sums in chunks of 8 rows, all loads of a chunk first (masked
-    // terms add fma(w, 0, v) = v): a loop of dependent loads otherwise
     {
       const int p0 = c.T.step_ptr[t], p1 = c.T.step_ptr[t + 1];
       for (int p = p0; p < p1; p += 8)
@@ -2294,7 +2368,7 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
           v += w[u] * a[u];
       }
     }
-    if (nh > 0)
+    if (nh_ > 0)
     {
       const double *HC = c.a(A_HC), *HRE = c.a(A_HRE);
       const int* HP = c.ia(I_HPTR);
@@ -2302,27 +2376,72 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
       if (t > 0)
         v = hinge_outer_sum(HC, HRE, 2 * D, D + i, D + j, HP[t - 1], HP[t], v);
     }
-    KB[e] = v;
-  }
-  if (L.hinge || L.nbr > 1)
+    return v;
+  };
+  // the coupling K_{t+1,t}[i][j] = diag(PO_t) + sum_h rho_eff a_t+1 a_t^T over
+  // the hinge rows of pair t (t < N - 1)
+  auto wcoup = [&](int t, int i, int j) {
+    double v = (i == j) ? PO[t * D + i] : 0.0;
+    if (nh_ > 0)
+      v = hinge_outer_sum(c.a(A_HC), c.a(A_HRE), 2 * D, D + i, j, c.ia(I_HPTR)[t], c.ia(I_HPTR)[t + 1], v);
+    return v;
+  };
+  const int sD = L.sD, sDD = sD * sD, sNb = L.sNb;
+  if (L.grp == 1)
   {
-    // dense couplings K_{t+1,t} = diag(PO_t) + sum_h rho_eff a_t+1 a_t^T, per
-    // solve block (T, T + 1) of one branch (block N - 1 of a branch couples to
-    // nothing; its entry is unused)
-    double* CPL = c.a(A_CPL);
-    const double *HC = c.a(A_HC), *HRE = c.a(A_HRE);
-    const int* HP = c.ia(I_HPTR);
-    FOR(e, (L.sN - 1) * sDD)
+    // diagonal blocks, in the solve layout (Layout::nbr): block T = b N + t holds
+    // waypoint t's dofs [b sD, (b + 1) sD); the other branches' entries of the
+    // waypoint block are exact zeros (no term touches two branches)
+    FOR(e, L.sN * sDD)
     {
       const int T = e / sDD, bi = T / N, t = T - bi * N;
-      const int il = (e / sD) % sD, jl = e % sD, i = bi * sD + il, j = bi * sD + jl;
-      double v = 0.0;
-      if (t < N - 1)
+      const int i = bi * sD + (e / sD) % sD, j = bi * sD + e % sD;  // dofs of the waypoint block
+      KB[e] = wblock(t, i, j);
+    }
+    if (L.hinge || L.nbr > 1)
+    {
+      // dense couplings K_{t+1,t}, per solve block (T, T + 1) of one branch
+      // (block N - 1 of a branch couples to nothing; its entry is unused)
+      double* CPL = c.a(A_CPL);
+      FOR(e, (L.sN - 1) * sDD)
       {
-        v = (i == j) ? PO[t * D + i] : 0.0;
-        if (nh > 0)
-          v = hinge_outer_sum(HC, HRE, 2 * D, D + i, j, HP[t], HP[t + 1], v);
+        const int T = e / sDD, bi = T / N, t = T - bi * N;
+        const int il = (e / sD) % sD, jl = e % sD, i = bi * sD + il, j = bi * sD + jl;
+        CPL[e] = (t < N - 1) ? wcoup(t, i, j) : 0.0;
       }
+    }
+  }
+  else
+  {
+    // waypoint pairs (Layout::grp = 2, JointAccEqCost): solve block T holds
+    // waypoints 2T (rows / columns [0, D)) and 2T + 1 ([D, 2D)); P couples
+    // t and t + 2 (A_PO2, diagonal), so the couplings between blocks T and
+    // T + 1 are K_{2T+2,2T} = diag(PO2_2T), K_{2T+2,2T+1} (the waypoint
+    // coupling of pair 2T + 1), K_{2T+3,2T+1} = diag(PO2_2T+1), K_{2T+3,2T} = 0
+    const double* PO2 = c.a(A_PO2);
+    FOR(e, L.sN * sDD)
+    {
+      const int T = e / sDD, il = (e / sD) % sD, jl = e % sD;
+      const int wi = il / D, wj = jl / D, i = il - wi * D, j = jl - wj * D;
+      double v;
+      if (wi == wj)
+        v = wblock(2 * T + wi, i, j);
+      else if (wi == 1)
+        v = wcoup(2 * T, i, j);  // K_{2T+1,2T}
+      else
+        v = wcoup(2 * T, j, i);  // K_{2T,2T+1} = K_{2T+1,2T}^T
+      KB[e] = v;
+    }
+    double* CPL = c.a(A_CPL);
+    FOR(e, (L.sN - 1) * sDD)
+    {
+      const int T = e / sDD, il = (e / sD) % sD, jl = e % sD;
+      const int wi = il / D, wj = jl / D, i = il - wi * D, j = jl - wj * D;
+      double v = 0.0;
+      if (wi == 0 && wj == 1)
+        v = wcoup(2 * T + 1, i, j);  // K_{2T+2,2T+1}
+      else if (wi == wj && i == j)
+        v = PO2[(2 * T + wi) * D + i];  // K_{2T+2,2T}, K_{2T+3,2T+1}
       CPL[e] = v;
     }
   }
@@ -2366,8 +2485,8 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
   if ((c.wave & 1) == 0 && c.wave < 2 * L.nbr)
   {
     // the middle block of branch b: both halves' Schur complements
-    const int bi = c.wave >> 1, mb = bi * N + m;
-    const bool top = m > 0, bot = (N - 1 - m) > 0;
+    const int bi = c.wave >> 1, mb = bi * sNb + m;
+    const bool top = m > 0, bot = (sNb - 1 - m) > 0;
     double* S = Sblk(c.wave);
     const double *Lt = Lsub(c.wave), *Lb = Lsub(c.wave + 1);
     for (int e = c.lane; e < sDD; e += 64)
@@ -2663,7 +2782,7 @@ __device__ __forceinline__ void twisted_forward(const Ctx& c, const Solver& sv, 
   // solve layout (Layout::nbr): branch b's blocks b N .. b N + N - 1, its top
   // half on wave 2b, its bottom half on wave 2b + 1
   const Layout& L = c.L;
-  const int N = L.N, m = L.tw_mid, half = c.wave & 1, base = (c.wave >> 1) * N;
+  const int N = L.sNb, m = L.tw_mid, half = c.wave & 1, base = (c.wave >> 1) * N;  // (N: blocks per branch)
   if (c.wave >= 2 * L.nbr)
     return;
   if (half == 0)
@@ -2678,7 +2797,7 @@ __device__ __forceinline__ void twisted_forward(const Ctx& c, const Solver& sv, 
 __device__ __forceinline__ void twisted_backward(const Ctx& c, const Solver& sv, double* CV)
 {
   const Layout& L = c.L;
-  const int N = L.N, m = L.tw_mid, half = c.wave & 1, base = (c.wave >> 1) * N;
+  const int N = L.sNb, m = L.tw_mid, half = c.wave & 1, base = (c.wave >> 1) * N;  // (N: blocks per branch)
   if (c.wave >= 2 * L.nbr)
     return;
   if (half == 0)
@@ -2718,7 +2837,8 @@ __device__ __forceinline__ double twisted_dvalue(const Ctx& c, const double* LIp
 __device__ __noinline__ void twisted_middle_wide(const Ctx& c, const Solver& sv, const double* LIp, double* CVp,
                                                 double* YVp)
 {
-  const int D = c.L.D, DD = D * D, m = c.L.tw_mid, N = c.L.N, i = c.lane;
+  // solve blocks (Layout::grp: a waypoint pair), one branch
+  const int D = c.L.sD, DD = D * D, m = c.L.tw_mid, N = c.L.sNb, i = c.lane;
   const lds_f64* LI = lds(LIp);
   const gbl_f64* M = gbl(sv.M);  // HBM (Layout::wide)
   const gbl_f64* Mb = gbl(sv.Nb);
@@ -2760,7 +2880,7 @@ template <typename MP>
 __device__ __forceinline__ void twisted_middle_narrow(const Ctx& c, MP M, MP Mb, const double* LIp, double* CVp,
                                                       const double* YVp, int branch)
 {
-  const int D = c.L.sD, DD = D * D, N = c.L.N, mloc = c.L.tw_mid, m = branch * N + mloc;
+  const int D = c.L.sD, DD = D * D, N = c.L.sNb, mloc = c.L.tw_mid, m = branch * N + mloc;
   const int i = c.lane >> 3, k = c.lane & 7;
   const bool act = (i < D) && (k < D);
   const lds_f64* LI = lds(LIp);
@@ -3055,11 +3175,13 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   PROF_LAP(24);
   // c = LI b per solve block (Layout::nbr): solve index v is row i of block T,
   // branch bi's part of waypoint t
-  const int sD = L.sD, sDD = sD * sD, N = L.N, nbr = L.nbr;
+  const int sD = L.sD, sDD = sD * sD, N = L.sNb, nbr = L.nbr;
   for (int v = tid; v < nx; v += kBlock)
   {
     const int T = v / sD, i = v - T * sD, bi = T / N, t = T - bi * N;
-    const double* bt = BX + t * D + bi * sD;
+    // the block's first column: waypoint t's branch bi part, or (waypoint
+    // pairs, Layout::grp) columns T sD onwards
+    const double* bt = (L.grp > 1) ? BX + T * sD : BX + t * D + bi * sD;
     const double cv = wide ? masked_dot<THIP_MAX_DOF>(lds(LI) + T * sDD + i * sD, 1, bt, 1, 0, i + 1)
                            : masked_dot<kOct>(lds(LI) + T * sDD + i * sD, 1, bt, 1, 0, i + 1);
     lds(CV)[v] = cv;
@@ -3311,6 +3433,14 @@ __device__ __forceinline__ double col_px(const Ctx& c, int col, const double* x)
     v += PO[col] * x[col + D];
   if (t > 0)
     v += PO[col - D] * x[col - D];
+  if (L.grp > 1)  // JointAccEqCost's (t, t+2) coupling
+  {
+    const double* PO2 = c.a(A_PO2);
+    if (t < L.N - 2)
+      v += PO2[col] * x[col + 2 * D];
+    if (t > 1)
+      v += PO2[col - 2 * D] * x[col - 2 * D];
+  }
   return v;
 }
 __device__ __forceinline__ double col_aty(const Ctx& c, int col, const double* y, bool chunked = false)
@@ -5221,7 +5351,7 @@ __device__ void plan_lds_dynamic(Ctx& c)
     // hinge-row pack and coefficients), then the rest as in the host plan
     const int order[] = { A_LINV, A_CV, A_YV, A_CPK, A_MR, A_HPART, A_HCHK, A_HCT, A_HPK, A_HC, A_BXW, A_BA, A_HW, A_HRE, A_DG, A_GS, A_WS,
                           A_FS,   A_BS, A_XA0, A_XA1, A_Z0, A_Z1, A_Y, A_XT, A_PZ, A_RHO, A_L,  A_U,  A_Q,
-                          A_DX,   A_DY, A_PD,  A_PO,  A_E,  A_DS, A_RE, A_CPL, A_PB, A_PS, A_PR };
+                          A_DX,   A_DY, A_PD,  A_PO,  A_PO2, A_E,  A_DS, A_RE, A_CPL, A_PB, A_PS, A_PR };
     long long used = L.lds_scratch;
     for (int k : order)
     {
@@ -5231,6 +5361,7 @@ __device__ void plan_lds_dynamic(Ctx& c)
         case A_LINV: case A_CPL: n = NDD; break;
         case A_CPK: n = (L.loff[A_CPK] >= 0) ? kCpk : 0; break;  // the host plan's offset
         case A_CV: case A_YV: case A_PD: case A_PO: n = nx; break;
+        case A_PO2: n = (L.grp > 1) ? nx : 0; break;
         case A_MR: n = L.n_rows + nh; break;
         case A_RE: n = L.n_rows; break;
         case A_HC: n = nh * 2 * D; break;
@@ -5519,6 +5650,12 @@ __device__ void sqp_optimize(Ctx& c, Solver& sv)
         double* mviol = c.big + L.n_costs;     // [n_cnts]
         if (c.tid == 0 && c.d->jv_enabled && !L.jv_ineq)
           mcost[0] = jvm;
+        for (int k = 0; k < L.n_jacc; ++k)  // JointAccEqCost: quadratic, model = exact
+        {
+          const double v = jacc_value(c, XN, k);
+          if (c.tid == 0)
+            mcost[L.jacc_slot[k]] = v;
+        }
         const double *G = c.a(A_G), *GC = c.a(A_GC);
         // JointPos: costs are quadratic (model = exact value), constraint
         // rows are abs rows like CartPose constraint rows (below)

@@ -138,7 +138,7 @@ int thip_debug_solve_layout(const thip_ctx* ctx, int* out, int n)
   if (!ctx || !out || n < 0)
     return THIP_E_INVALID;
   const int v[THIP_LAYOUT_INFO_N] = {ctx->L.nbr, ctx->L.sD, ctx->L.wide, ctx->L.seg_ok, ctx->gen ? 1 : 0,
-                                     ctx->gen ? kGenBlock : kBlock};
+                                     ctx->gen ? kGenBlock : kBlock, ctx->L.grp, ctx->L.sNb};
   for (int k = 0; k < n && k < THIP_LAYOUT_INFO_N; ++k)
     out[k] = v[k];
   return THIP_OK;
@@ -151,6 +151,26 @@ int thip_debug_set_path(int flags)
     return THIP_E_INVALID;
   g_debug_path = flags;
   return THIP_OK;
+}
+
+extern "C" int thip_jdt_fused(const thip_problem_desc* d)
+{
+  int k, j;
+  if (d->n_jdt == 0)
+    return 1;
+  if (d->n_jdt < 0 || d->n_jdt > THIP_MAX_JDT || d->n_steps % 2 != 0 || 2 * d->chain.n_dof > THIP_MAX_DOF ||
+      d->use_time)
+    return 0;
+  for (k = 0; k < d->n_jdt; ++k)
+  {
+    if (d->jdt_order[k] != 2 || d->jdt_is_cnt[k])
+      return 0;
+    for (j = 0; j < d->chain.n_dof; ++j)
+      if (d->jdt_upper_tols[k][j] >= 1e-5 || d->jdt_upper_tols[k][j] <= -1e-5 || d->jdt_lower_tols[k][j] >= 1e-5 ||
+          d->jdt_lower_tols[k][j] <= -1e-5)
+        return 0;
+  }
+  return 1;
 }
 
 static int validate(const thip_problem_desc* d, std::string& why)
@@ -212,8 +232,9 @@ static int validate(const thip_problem_desc* d, std::string& why)
                    "a term with zero tolerances goes in jv_*",
              THIP_E_INVALID;
   }
-  if (d->n_jdt != 0)
-    return why = "JointAcc / JointJerk terms and JointVel equality constraints are not lowered into the batched "
+  if (!thip_jdt_fused(d))
+    return why = "JointAcc / JointJerk terms other than JointAccEqCost on an even number of waypoints with "
+                 "2 n_dof <= THIP_MAX_DOF, and JointVel equality constraints, are not lowered into the batched "
                  "kernel: solve such a problem with sco::BasicTrustRegionSQP (the generic path, GpuModel)",
            THIP_E_INVALID;
   if (d->use_time != 0 || d->n_jvt != 0 || d->n_ttt != 0 || d->n_fixed_dofs != 0)
@@ -416,6 +437,11 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   for (int x = 0; x < d.n_jvx; ++x)
     if (!d.jvx_is_cnt[x])
       jvx_slot[static_cast<size_t>(x)] = n_costs++;
+  // JointAccEqCost terms (thip_jdt_fused): cost slots after the JointVel
+  // tolerance costs (the oracle's / ConstructProblem's cost order)
+  L.n_jacc = d.n_jdt;
+  for (int k = 0; k < THIP_MAX_JDT; ++k)
+    L.jacc_slot[k] = (k < d.n_jdt) ? n_costs++ : -1;
   for (int k = 0; k < d.n_jpos; ++k)
   {
     if (!d.jpos_is_cnt[k])
@@ -590,6 +616,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   sizes[A_COST] = sizes[A_NCOST] = std::max(L.n_costs, 1);
   sizes[A_VIOL] = sizes[A_NVIOL] = sizes[A_MU] = std::max(L.n_cnts, 1);
   sizes[A_PD] = sizes[A_PO] = sizes[A_CV] = sizes[A_YV] = nx;
+  sizes[A_PO2] = (d.n_jdt > 0) ? nx : 1;
   sizes[A_Q] = sizes[A_DS] = sizes[A_BS] = sizes[A_XA0] = sizes[A_XA1] = sizes[A_XT] = sizes[A_DX] = nc;
   sizes[A_BA] = sizes[A_PX] = sizes[A_ATY] = sizes[A_DRV] = sizes[A_DG] = sizes[A_SOLX] = sizes[A_BXW] = nc;
   sizes[A_WS] = nab * 2;
@@ -678,6 +705,17 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     }
   }
   L.sN = L.nbr * L.N;
+  // JointAccEqCost couples waypoints t and t + 2: solve over waypoint pairs
+  // (Layout::grp; thip_jdt_fused guarantees N even and 2 D <= THIP_MAX_DOF, and
+  // D <= 8 never takes the branch split above)
+  L.grp = (d.n_jdt > 0) ? 2 : 1;
+  if (L.grp == 2)
+  {
+    L.nbr = 1;
+    L.sD = 2 * L.D;
+    L.sN = L.N / 2;
+  }
+  L.sNb = L.sN / L.nbr;
   const long long sNDD = (long long)L.sN * L.sD * L.sD;
   sizes[A_LINV] = sizes[A_KB] = sNDD;
   L.wide = (L.sD > 8) ? 1 : 0;
@@ -693,7 +731,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   sizes[A_PS] = sizes[A_PR] = nc + m;
   sizes[A_HC0] = sizes[A_HC] = hc * 2 * D;
   sizes[A_HK] = sizes[A_HW] = sizes[A_HRE] = sizes[A_HDIST] = sizes[A_HCCT] = hc;
-  sizes[A_CPL] = (L.hinge || L.nbr > 1) ? sNDD : 1;
+  sizes[A_CPL] = (L.hinge || L.nbr > 1 || L.grp > 1) ? sNDD : 1;  // dense couplings (factor())
   sizes[A_CSCR] = L.coll ? (long long)kScanWaves * kSubCap * d.n_spheres * 3 : 1;
   sizes[A_HCOST] = L.N;
   sizes[A_HPK] = L.hinge ? hc * kHPack : 1;
@@ -752,12 +790,12 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
   // until the budget of one workgroup per CU is used; the rest stays in HBM.
   {
     const int order[] = { A_LINV, A_CV,  A_YV, A_CPK, A_BXW, A_BA, A_MR, A_DG, A_GS, A_WS, A_FS, A_BS, A_XA0, A_XA1,
-                          A_Z0,   A_Z1,  A_Y,  A_XT,  A_PZ, A_RHO, A_L, A_U,  A_Q,  A_DX, A_DY, A_PD,  A_PO,
+                          A_Z0,   A_Z1,  A_Y,  A_XT,  A_PZ, A_RHO, A_L, A_U,  A_Q,  A_DX, A_DY, A_PD,  A_PO,  A_PO2,
                           A_E,    A_DS,  A_RE, A_PB,  A_PS, A_PR };
     long long used = static_cast<long long>(lds_d);
     used = (used + 7) / 8 * 8;
-    L.fac_off = static_cast<int>(used);  // factor()'s 4 D x D blocks
-    used += (4LL * L.D * L.D + 7) / 8 * 8;
+    L.fac_off = static_cast<int>(used);  // factor()'s 4 D x D blocks (4 nbr sD x sD; pairs: 4 of 2D x 2D)
+    used += (4LL * std::max<long long>((long long)L.D * L.D, (long long)L.nbr * L.sD * L.sD) + 7) / 8 * 8;
     L.lds_scratch = static_cast<int>(used);
     for (int k = 0; k < A_COUNT; ++k)
       L.loff[k] = -1;
@@ -793,7 +831,7 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     if ((g_debug_path & THIP_DEBUG_NO_SEGMENT) || ctx->gen)  // diagnostic: the generic ADMM step
       L.seg_ok = 0;
     L.seg_slots = 1;
-    L.tw_mid = L.N / 2;
+    L.tw_mid = L.sNb / 2;
     if (L.loff[A_LINV] < 0 || L.loff[A_CV] < 0 || L.loff[A_YV] < 0)
     {
       g_create_err = "thip_create: problem too large, the block-solve factor does not fit in LDS";

@@ -235,7 +235,8 @@ void addJointDiffObjects(trajopt::TrajOptProb& prob, const trajopt::JointDiffSpe
 }
 
 // a JointVel equality constraint / JointAcc / JointJerk term: the descriptor's jdt
-// table (the oracle's input; the batched kernel refuses it) and the host object
+// table (the oracle's input; the batched kernel takes JointAccEqCost only,
+// thip_jdt_fused) and the host object
 void addJointDiffTerm(trajopt::TrajOptProb& prob, int order, bool is_cost, const trajopt::DblVec& coeffs,
                       const trajopt::DblVec& targets, const trajopt::DblVec& upper, const trajopt::DblVec& lower,
                       int first, int last, const std::string& name)
@@ -259,8 +260,12 @@ void addJointDiffTerm(trajopt::TrajOptProb& prob, int order, bool is_cost, const
     d.jdt_upper_tols[k][j] = upper[j];
     d.jdt_lower_tols[k][j] = lower[j];
   }
-  addJointDiffObjects(prob, diffSpec(prob, order, coeffs, targets, upper, lower, first, last), is_cost,
-                      allZero(upper) && allZero(lower), name, false);
+  // JointAccEqCost runs in the fused kernel (waypoint-pair blocks) when the whole
+  // problem qualifies (TrajOptProb::lowerable, thip_jdt_fused); every other form
+  // only on the generic path
+  const bool zero_tols = allZero(upper) && allZero(lower);
+  addJointDiffObjects(prob, diffSpec(prob, order, coeffs, targets, upper, lower, first, last), is_cost, zero_tols,
+                      name, order == 2 && is_cost && zero_tols);
 }
 
 sco::ModelConfig::ConstPtr modelConfig(const trajopt::ProblemConstructionInfo& pci)
@@ -1442,7 +1447,7 @@ bool TrajOptProb::lowerable() const
   // the fused kernel's domain: at most THIP_MAX_STEPS waypoints and THIP_MAX_PRIMS
   // scene primitives, and no term it does not lower
   return desc_.n_steps >= 2 && desc_.n_steps <= THIP_MAX_STEPS && desc_.n_prims <= THIP_MAX_PRIMS &&
-         desc_.n_jdt == 0 && desc_.n_jvt == 0 && desc_.n_ttt == 0 && !desc_.use_time && desc_.n_fixed_dofs == 0 &&
+         thip_jdt_fused(&desc_) && desc_.n_jvt == 0 && desc_.n_ttt == 0 && !desc_.use_time && desc_.n_fixed_dofs == 0 &&
          desc_.n_coll_extra == 0 && unloweredTerms().empty();
 }
 

@@ -355,6 +355,8 @@ def _declare(lib):
     lib.thip_debug_get_profile.restype = C.c_int
     lib.thip_debug_set_path.argtypes = [C.c_int]
     lib.thip_debug_set_path.restype = C.c_int
+    lib.thip_jdt_fused.argtypes = [C.POINTER(ProblemDesc)]
+    lib.thip_jdt_fused.restype = C.c_int
     lib.thip_debug_solve_layout.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
     lib.thip_debug_solve_layout.restype = C.c_int
     lib.thip_eval_create.argtypes = [C.c_int, P(ProblemDesc), C.c_int, P(vp)]

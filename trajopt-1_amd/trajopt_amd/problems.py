@@ -147,6 +147,11 @@ def make_workload(config: str, batch: int, first_problem: int = 0, n_steps: int 
     """Synthetic workload of SURVEY.md §8d config A/B/C (or J: JointPos terms).  robot picks the chain
     (robots.ROBOTS); the default is the reference's PR2 right_arm group."""
     config = config.upper()
+    if config == "HA":
+        # config B plus joint_costs_unit's JointAcc cost on every step (coefficient 1,
+        # zero targets): the fused kernel's waypoint-pair solve (bench.py --config HA)
+        return with_joint_acc(make_workload("B", batch, first_problem=first_problem, n_steps=n_steps,
+                                            goal_offset=goal_offset, robot=robot))
     if config == "A":
         N = n_steps or 10
     elif config in ("B", "C"):
@@ -305,6 +310,39 @@ def with_cart_tolerances(wl, pos=0.02, rot=0.1, axes=range(6)):
             b = (pos if i < 3 else rot) if i in axes else 0.0
             d.cart_lower_tol[k][i] = -b
             d.cart_upper_tol[k][i] = b
+    return wl
+
+
+def with_joint_acc(wl, coeff=1.0, target=0.0, first_step=0, last_step=-1):
+    """Add a JointAccEqCost to every problem of wl (JointAccTermInfo, coefficient and
+    target per joint, zero tolerances: joint_costs_unit.cpp's acceleration cost), with
+    JointAccTermInfo::hatch's step clamping (problem_description.cpp:1412-1440).  On an
+    even number of waypoints with 2 n_dof <= 16 the fused kernel lowers it (waypoint
+    pairs, thip_jdt_fused); otherwise only the generic path runs it."""
+    d = wl.desc
+    N, D = d.n_steps, d.chain.n_dof
+    f, l = first_step, last_step
+    if l <= -1:
+        l = N - 1
+    if N - 3 <= f:
+        f = N - 3
+    if N - 1 <= l:
+        l = N - 1
+    if l == f:
+        l += 2
+    if l < f:
+        f, l = l, f
+    k = d.n_jdt
+    d.jdt_order[k] = 2
+    d.jdt_is_cnt[k] = 0
+    d.jdt_first_step[k] = f
+    d.jdt_last_step[k] = l
+    for j in range(D):
+        d.jdt_coeffs[k][j] = coeff
+        d.jdt_targets[k][j] = target
+        d.jdt_upper_tols[k][j] = 0.0
+        d.jdt_lower_tols[k][j] = 0.0
+    d.n_jdt = k + 1
     return wl
 
 

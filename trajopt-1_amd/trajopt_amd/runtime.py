@@ -132,10 +132,11 @@ class BatchTrustRegionSQP:
 
     def layout(self):
         """The solve layout this context chose (thip_debug_solve_layout): branches, dofs
-        per block, wide, segment possible, generic-step build, threads."""
-        out = (C.c_int * 6)()
-        self._check(self.lib.thip_debug_solve_layout(self.ctx, out, 6), "thip_debug_solve_layout")
-        return dict(zip(("nbr", "block_dofs", "wide", "seg_ok", "gen", "threads"), list(out)))
+        per block, wide, segment possible, generic-step build, threads, waypoints per solve
+        block (2 with JointAccEqCost terms), solve blocks per branch."""
+        out = (C.c_int * 8)()
+        self._check(self.lib.thip_debug_solve_layout(self.ctx, out, 8), "thip_debug_solve_layout")
+        return dict(zip(("nbr", "block_dofs", "wide", "seg_ok", "gen", "threads", "grp", "blocks"), list(out)))
 
     def enable_profile(self, on=True):
         self._check(self.lib.thip_debug_profile(self.ctx, 1 if on else 0), "thip_debug_profile")
