@@ -49,8 +49,9 @@ extern "C" {
  * 4: use_time, fixed dofs, time JointVel.  5: TotalTime.  6: further collision
  * terms (thip_coll_term), single-waypoint problems on the generic path.  7: robot
  * self-collision link pairs (n_self_pairs / self_pair).  8: per link-pair collision
- * margins and coefficients (n_coll_pairs / coll_pairs). */
-#define THIP_ABI_VERSION 8
+ * margins and coefficients (n_coll_pairs / coll_pairs).  9: the collision terms'
+ * contact test type (coll_contact_test, thip_coll_term.contact_test). */
+#define THIP_ABI_VERSION 9
 
 #define THIP_MAX_DOF 16
 #define THIP_MAX_LINKS 32
@@ -72,6 +73,23 @@ extern "C" {
 #define THIP_EVAL_MAX_STEPS 4096
 #define THIP_EVAL_MAX_PRIMS 1024
 #define THIP_MAX_CONTACTS 131072
+
+/* contact test type of a collision term (CollisionTermInfo::contact_test_type,
+ * problem_description.cpp:1669-1673, tesseract ContactTestType {FIRST = 0,
+ * CLOSEST = 1, ALL = 2}), encoded so that a zero-initialised descriptor means
+ * ALL, the reference's default.  Per contactTest call (one LVS sub-state, one
+ * cast, or the DISCRETE state), before the evaluator's filter (zero-coefficient
+ * pairs, removeInvalidContactResults): ALL keeps every contact within each
+ * pair's contact distance; CLOSEST keeps one per link-pair key, the smallest
+ * distance (the first in sphere order on ties); FIRST keeps the first contact
+ * of the whole test in ContactResultMap order (keys (link, primitive), then the
+ * self link pairs; inside a key, sphere order).  The primitive model replaces
+ * Bullet's broad phase, so FIRST's choice is parity unpinned against tesseract,
+ * as every contact value is.  Only ALL runs in the fused kernel; FIRST and
+ * CLOSEST run on the generic path (device evaluator thip_eval_collision). */
+#define THIP_CONTACT_ALL 0
+#define THIP_CONTACT_FIRST 1
+#define THIP_CONTACT_CLOSEST 2
 
 /* error codes */
 #define THIP_OK 0
@@ -194,6 +212,7 @@ typedef struct thip_coll_term {
   double buffer;   /* collision_margin_buffer */
   double lvs;      /* longest_valid_segment_length (CONTINUOUS: +inf) */
   int continuous;  /* 0 LVS_DISCRETE, 1 LVS_CONTINUOUS / CONTINUOUS, 2 DISCRETE */
+  int contact_test; /* THIP_CONTACT_ALL / FIRST / CLOSEST */
 } thip_coll_term;
 
 /* A per link-pair override of one collision term's margin and coefficient:
@@ -376,6 +395,7 @@ typedef struct thip_problem_desc {
                               collision_terms.cpp:978-1161): each robot sphere is swept between
                               consecutive sub-states (a capsule) and tested against the scene;
                               CONTINUOUS is LVS_CONTINUOUS with coll_lvs = +inf (one cast per pair) */
+  int coll_contact_test;   /* THIP_CONTACT_ALL (0) / FIRST / CLOSEST; the fused kernel takes ALL */
   int n_spheres;
   int sphere_link[THIP_MAX_SPHERES];
   double sphere_center[THIP_MAX_SPHERES][3];  /* in link frame */

@@ -428,7 +428,7 @@ void addSelfContacts(const CollisionModel& cm, const std::vector<Iso3>& T, const
     double ta = 0, tb = 0;
     selfSphereDistance(a0, a1, cm.sphere_radius[sa], b0, b1, cm.sphere_radius[sb], mode == 2, ct.distance, ct.normal,
                        ct.p_robot, ct.p_prim, ta, tb);
-    if (!(ct.distance < threshold) || ct.distance > margin + cm.buffer)
+    if (!(ct.distance < threshold))  // contactTest: within the pair's contact distance
       continue;
     ct.link = la;
     ct.sphere = sa;
@@ -459,9 +459,91 @@ void addSelfContacts(const CollisionModel& cm, const std::vector<Iso3>& T, const
       ct.cc_type = (i == 0 && ta == 0.0) ? kCCTime0 : ((i + 1 == last && ta == 1.0) ? kCCTime1 : kCCBetween);
       ct.cc_type_b = (i == 0 && tb == 0.0) ? kCCTime0 : ((i + 1 == last && tb == 1.0) ? kCCTime1 : kCCBetween);
     }
-    if (!keepAtFixedEnds(ct, vars0_fixed, vars1_fixed))
-      continue;
+    (void)vars0_fixed;
+    (void)vars1_fixed;  // (the evaluator's filter runs after the test: applyContactTest)
     keys[static_cast<std::size_t>(cm.self_key[j])].push_back(ct);
+  }
+}
+
+// One contactTest call's contacts (the candidates within their pair's contact
+// distance, per key in ContactResultMap order), reduced as the request's test
+// type returns them (trajopt_hip.h THIP_CONTACT_*: ALL every one, CLOSEST the
+// smallest distance per key -- the first on ties --, FIRST the first of the whole
+// call), then the evaluator's filter (removeInvalidContactResults,
+// collision_utils.cpp:73-114: beyond margin + buffer, at a fixed end) and
+// appended to the run's key lists (addInterpolatedCollisionResults,
+// collision_terms.cpp:880-897).
+void applyContactTest(const CollisionModel& cm, std::map<std::pair<int, int>, std::vector<Contact>>& call_scene,
+                      std::vector<std::vector<Contact>>& call_self, bool vars0_fixed, bool vars1_fixed,
+                      std::map<std::pair<int, int>, std::vector<Contact>>& results,
+                      std::vector<std::vector<Contact>>& self)
+{
+  auto filter = [&](const Contact& ct) {
+    return !(ct.distance > cm.marginOf(ct.link, ct.other()) + cm.buffer) && keepAtFixedEnds(ct, vars0_fixed, vars1_fixed);
+  };
+  auto closest = [](const std::vector<Contact>& v) {
+    std::size_t best = 0;
+    for (std::size_t k = 1; k < v.size(); ++k)
+      if (v[k].distance < v[best].distance)
+        best = k;
+    return best;
+  };
+  if (cm.contact_test == THIP_CONTACT_FIRST)
+  {
+    const Contact* first = nullptr;
+    std::pair<int, int> key;
+    int skey = -1;
+    for (auto& kv : call_scene)
+      if (!kv.second.empty())
+      {
+        first = &kv.second.front();
+        key = kv.first;
+        break;
+      }
+    for (std::size_t k = 0; !first && k < call_self.size(); ++k)
+      if (!call_self[k].empty())
+      {
+        first = &call_self[k].front();
+        skey = static_cast<int>(k);
+      }
+    if (first && filter(*first))
+    {
+      if (skey < 0)
+        results[key].push_back(*first);
+      else
+        self[static_cast<std::size_t>(skey)].push_back(*first);
+    }
+    return;
+  }
+  for (auto& kv : call_scene)
+  {
+    if (kv.second.empty())
+      continue;
+    if (cm.contact_test == THIP_CONTACT_CLOSEST)
+    {
+      const Contact& ct = kv.second[closest(kv.second)];
+      if (filter(ct))
+        results[kv.first].push_back(ct);
+    }
+    else
+      for (const Contact& ct : kv.second)
+        if (filter(ct))
+          results[kv.first].push_back(ct);
+  }
+  for (std::size_t k = 0; k < call_self.size(); ++k)
+  {
+    if (call_self[k].empty())
+      continue;
+    if (cm.contact_test == THIP_CONTACT_CLOSEST)
+    {
+      const Contact& ct = call_self[k][closest(call_self[k])];
+      if (filter(ct))
+        self[k].push_back(ct);
+    }
+    else
+      for (const Contact& ct : call_self[k])
+        if (filter(ct))
+          self[k].push_back(ct);
   }
 }
 
@@ -484,8 +566,8 @@ std::vector<Contact> flatten(std::map<std::pair<int, int>, std::vector<Contact>>
 std::vector<Contact> calcCollisionsSingle(const CollisionModel& cm, const double* q)
 {
   const thip_chain& ch = *cm.chain;
-  std::map<std::pair<int, int>, std::vector<Contact>> results;
-  std::vector<std::vector<Contact>> self(static_cast<std::size_t>(cm.n_self_keys));
+  std::map<std::pair<int, int>, std::vector<Contact>> results, call;
+  std::vector<std::vector<Contact>> self(static_cast<std::size_t>(cm.n_self_keys)), call_self(self.size());
   std::vector<Iso3> T;
   chainFwdKin(ch, q, T);
   for (int s = 0; s < cm.n_spheres; ++s)
@@ -502,7 +584,7 @@ std::vector<Contact> calcCollisionsSingle(const CollisionModel& cm, const double
       const double margin = cm.marginOf(link, pk), threshold = margin + cm.buffer;
       Contact ct;
       spherePrimDistance(c, cm.sphere_radius[s], cm.scene + 16 * p, ct.distance, ct.normal, ct.p_robot, ct.p_prim);
-      if (!(ct.distance < threshold) || ct.distance > margin + cm.buffer)
+      if (!(ct.distance < threshold))
         continue;
       ct.link = link;
       ct.prim = p;
@@ -513,10 +595,11 @@ std::vector<Contact> calcCollisionsSingle(const CollisionModel& cm, const double
       toLocal(Tl, ct.p_robot, ct.p_local);
       ct.cc_time = 0;
       ct.cc_type = 0;  // CCType_None
-      results[{ link, p }].push_back(ct);
+      call[{ link, p }].push_back(ct);
     }
   }
-  addSelfContacts(cm, T, nullptr, 0, 0, 0.0, 0, false, false, self);
+  addSelfContacts(cm, T, nullptr, 0, 0, 0.0, 0, false, false, call_self);
+  applyContactTest(cm, call, call_self, false, false, results, self);
   return flatten(results, self);
 }
 
@@ -554,6 +637,8 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
     std::vector<double> qn(static_cast<std::size_t>(D));
     for (long i = 0; i + 1 < cnt; ++i)
     {
+      std::map<std::pair<int, int>, std::vector<Contact>> call;
+      std::vector<std::vector<Contact>> call_self(self.size());
       for (int j = 0; j < D; ++j)
       {
         q[static_cast<std::size_t>(j)] = linspaced(static_cast<int>(cnt), q0[j], q1[j], static_cast<int>(i));
@@ -591,19 +676,18 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
           toLocal(Ta, ct.p_robot, ct.p_local);
           ct.cc_time = (double(i) + ts) * dt;
           ct.cc_type = (i == 0 && ts == 0.0) ? kCCTime0 : ((i + 1 == last && ts == 1.0) ? kCCTime1 : kCCBetween);
-          if (ct.distance > margin + cm.buffer)
-            continue;
-          if (!keepAtFixedEnds(ct, vars0_fixed, vars1_fixed))
-            continue;
-          results[{ link, p }].push_back(ct);
+          call[{ link, p }].push_back(ct);
         }
       }
-      addSelfContacts(cm, T, &T1, static_cast<int>(i), last, dt, 2, vars0_fixed, vars1_fixed, self);
+      addSelfContacts(cm, T, &T1, static_cast<int>(i), last, dt, 2, vars0_fixed, vars1_fixed, call_self);
+      applyContactTest(cm, call, call_self, vars0_fixed, vars1_fixed, results, self);
     }
     return flatten(results, self);
   }
   for (long i = 0; i < cnt; ++i)
   {
+    std::map<std::pair<int, int>, std::vector<Contact>> call;
+    std::vector<std::vector<Contact>> call_self(self.size());
     for (int j = 0; j < D; ++j)
       q[static_cast<std::size_t>(j)] = linspaced(static_cast<int>(cnt), q0[j], q1[j], static_cast<int>(i));
     chainFwdKin(ch, q.data(), T);
@@ -635,16 +719,12 @@ std::vector<Contact> calcCollisions(const CollisionModel& cm, const double* q0, 
         // addInterpolatedCollisionResults(.., discrete = true): active link only
         ct.cc_time = double(i) * dt;
         ct.cc_type = (i == 0) ? kCCTime0 : ((i == last) ? kCCTime1 : kCCBetween);
-        // filter: zero coeffs (none), removeInvalidContactResults
-        // (collision_utils.cpp:73-114); the static primitive has CCType_None
-        if (ct.distance > margin + cm.buffer)
-          continue;
-        if (!keepAtFixedEnds(ct, vars0_fixed, vars1_fixed))
-          continue;
-        results[{ link, p }].push_back(ct);
+        // (filter after the test: applyContactTest; the static primitive has CCType_None)
+        call[{ link, p }].push_back(ct);
       }
     }
-    addSelfContacts(cm, T, nullptr, static_cast<int>(i), last, dt, 1, vars0_fixed, vars1_fixed, self);
+    addSelfContacts(cm, T, nullptr, static_cast<int>(i), last, dt, 1, vars0_fixed, vars1_fixed, call_self);
+    applyContactTest(cm, call, call_self, vars0_fixed, vars1_fixed, results, self);
   }
   return flatten(results, self);
 }
@@ -964,6 +1044,7 @@ thip_coll_term collisionTerm(const thip_problem_desc& d, int k)
   t.buffer = d.coll_buffer;
   t.lvs = d.coll_lvs;
   t.continuous = d.coll_continuous;
+  t.contact_test = d.coll_contact_test;
   return t;
 }
 
@@ -988,6 +1069,7 @@ std::shared_ptr<CollisionModel> collisionModel(const thip_problem_desc& d, int t
   cm->buffer = t.buffer;
   cm->lvs = t.lvs;
   cm->continuous = t.continuous == 1;
+  cm->contact_test = t.contact_test;
   // self pairs in key order: link pairs as given, spheres of a then of b in index order
   for (int k = 0; k < d.n_self_pairs; ++k)
     for (int sa = 0; sa < d.n_spheres; ++sa)

@@ -39,6 +39,7 @@ struct CollisionModel
   const double* scene = nullptr;  // [n_prims][16]
   double margin = 0, coeff = 0, buffer = 0, lvs = 0;
   bool continuous = false;  // LVS_CONTINUOUS (CastCollisionEvaluator) instead of LVS_DISCRETE
+  int contact_test = THIP_CONTACT_ALL;  // the request's test type (trajopt_hip.h THIP_CONTACT_*)
   // robot self-collision (desc.self_pair): sphere pairs (a, b) in key order --
   // link pairs in descriptor order, then the spheres of a, then those of b
   // (sphere index order) -- and the key of each

@@ -366,3 +366,48 @@ def test_pair_coefficients_enter_the_problem(oracle_mod):
     x2, _ = oracle_mod.solve(wl2, n_threads=4)
     assert np.abs(x1 - x0).max() > 1e-4
     np.testing.assert_array_equal(x2, x0)
+
+
+def _groups(rows, key):
+    out = {}
+    for r in rows:
+        out.setdefault(key(r), []).append(r)
+    return out
+
+
+@pytest.mark.parametrize("cont", [0, 1, 2])
+def test_contact_test_types_oracle(oracle_mod, cont):
+    """CollisionTermInfo contact_test_type (problem_description.cpp:1669-1673;
+    trajopt_hip.h THIP_CONTACT_*), per contactTest call: CLOSEST keeps, per
+    (link, primitive) key and sub-state, the smallest distance of ALL's contacts
+    of that key (the filter runs after the test, so a key whose closest contact
+    is filtered out keeps nothing); FIRST keeps at most one contact per
+    sub-state, ALL's first one in ContactResultMap order."""
+    from trajopt_amd import abi
+
+    wl = problems.make_workload("C", 6)
+    wl.desc.coll_continuous = cont
+    x = wl.init + 0.02 * np.random.default_rng(11).standard_normal(wl.init.shape)
+    n_all = n_cl = n_fi = 0
+    for b in range(wl.batch):
+        wl.desc.coll_contact_test = abi.CONTACT_ALL
+        rows_all = oracle_mod.collision_rows(wl, b, x[b])
+        wl.desc.coll_contact_test = abi.CONTACT_CLOSEST
+        rows_cl = oracle_mod.collision_rows(wl, b, x[b])
+        wl.desc.coll_contact_test = abi.CONTACT_FIRST
+        rows_fi = oracle_mod.collision_rows(wl, b, x[b])
+        n_all, n_cl, n_fi = n_all + len(rows_all), n_cl + len(rows_cl), n_fi + len(rows_fi)
+        # unit t (DISCRETE: the waypoint t + half), key (link, primitive), sub-state
+        gk = lambda r: (int(r[0]), int(r[1]), int(r[2]), int(r[4]))  # noqa: E731
+        g_all = _groups(rows_all, gk)
+        g_cl = _groups(rows_cl, gk)
+        for k, v in g_cl.items():
+            assert len(v) == 1, (b, k)
+            assert v[0][5] == min(r[5] for r in g_all[k]), (b, k)
+            assert any(np.array_equal(v[0], r) for r in g_all[k])
+        gs = lambda r: (int(r[0]), int(r[4]))  # noqa: E731
+        a_sub = _groups(rows_all, gs)
+        for k, v in _groups(rows_fi, gs).items():
+            assert len(v) == 1, (b, k)
+            assert np.array_equal(v[0], a_sub[k][0]), (b, k)
+    assert n_all >= n_cl >= n_fi > 0 and n_all > n_fi, (n_all, n_cl, n_fi)

@@ -373,3 +373,15 @@ def test_prepared_batch_needs_a_gpu_or_fails_loudly(built):
             pb.solve()
     finally:
         pb.close()
+
+
+@pytest.mark.parametrize("json_type,ctest", [(None, 0), (2, 0), (0, 1), (1, 2)])
+def test_contact_test_type_lowering(json_type, ctest):
+    """CollisionTermInfo "contact_test_type" (problem_description.cpp:1669-1673,
+    tesseract FIRST = 0, CLOSEST = 1, ALL = 2, default ALL) lowers to the
+    descriptor's THIP_CONTACT_* code (ALL = 0, FIRST = 1, CLOSEST = 2)."""
+    params = {"coeffs": 20, "dist_pen": 0.025, "evaluator_type": 2}
+    if json_type is not None:
+        params["contact_test_type"] = json_type
+    d, _, _, _ = host.lower_json(_doc(costs=[{"type": "collision", "params": params}]))
+    assert d.coll_enabled == 1 and d.coll_contact_test == ctest

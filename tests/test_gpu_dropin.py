@@ -316,3 +316,62 @@ def test_prepared_hostloop_batch(oracle_mod):
     finally:
         pb.close()
     check_parity(dc.json_batch_workload(texts, host), oracle_mod, x, res, label="dropin-HB")
+
+
+# ------------------------------------------------------------------ contact test types
+@pytest.mark.parametrize("cont", [0, 1, 2])
+@pytest.mark.parametrize("ctest", [abi.CONTACT_FIRST, abi.CONTACT_CLOSEST])
+def test_eval_collision_rows_contact_test(oracle_mod, cont, ctest):
+    """contact_test_type FIRST / CLOSEST (problem_description.cpp:1669-1673,
+    trajopt_hip.h THIP_CONTACT_*): thip_eval_collision's rows against the
+    oracle's, for every evaluator, at the initial and a perturbed trajectory."""
+    wl = problems.make_workload("C", 8)
+    wl.desc.coll_continuous = cont
+    wl.desc.coll_contact_test = ctest
+    x1 = wl.init + 0.03 * np.random.default_rng(7).standard_normal(wl.init.shape)
+    ev = TermEvaluator(wl)
+    total = 0
+    for x in (wl.init, x1):
+        rows = ev.collision(0, x)
+        for b in range(wl.batch):
+            ref = oracle_mod.collision_rows(wl, b, x[b])
+            total += len(ref)
+            _check_rows(rows[b], ref, f"cont {cont} test {ctest} problem {b}")
+    ev.close()
+    assert total > 20
+
+
+def test_contact_test_refused_by_the_fused_kernel():
+    """The fused kernel runs ALL only: a FIRST / CLOSEST descriptor names the generic path."""
+    from trajopt_amd.runtime import BatchTrustRegionSQP, HipError
+
+    wl = problems.make_workload("C", 2)
+    wl.desc.coll_contact_test = abi.CONTACT_CLOSEST
+    with pytest.raises(HipError) as ei:
+        BatchTrustRegionSQP(wl)
+    assert "generic path" in str(ei.value)
+
+
+@pytest.mark.parametrize("json_type,ctest", [(0, abi.CONTACT_FIRST), (1, abi.CONTACT_CLOSEST)])
+def test_contact_test_dropin(oracle_mod, json_type, ctest):
+    """Config C problems as TrajOptRequest JSON with "contact_test_type" 0 (FIRST)
+    or 1 (CLOSEST): ConstructProblem lowers the type, the problem runs the host
+    loop (device-evaluated collision terms, GPU QPs), and the result has oracle
+    parity (three of the ten primitives: the JSON problems carry the reference's
+    0.5 m safety buffer)."""
+    wl0 = problems.make_workload("C", 4, first_problem=40)
+    texts = []
+    for b in range(wl0.batch):
+        doc = json.loads(host.workload_to_json(wl0, b))
+        for c in doc["costs"]:
+            if c["type"] == "collision":
+                c["params"]["contact_test_type"] = json_type
+        texts.append(json.dumps(doc))
+    scenes = np.ascontiguousarray(wl0.scene[:, :3])
+    x, res = host.solve_json_batch(texts, scenes)
+    parts = [host.lower_json(t, scenes[b]) for b, t in enumerate(texts)]
+    desc = parts[0][0]
+    assert desc.coll_contact_test == ctest
+    wl = problems.Workload("json", desc, np.stack([p[1] for p in parts]), np.stack([p[2] for p in parts]), scenes,
+                           np.stack([p[1] for p in parts]), None)
+    check_parity(wl, oracle_mod, x, res, label=f"json-contact-test-{json_type}", min_strict=0.0)

@@ -53,6 +53,7 @@ struct CollTerm
   // per link-pair margins (pair_data.hpp, [n_spheres][pw][2]; null: `margin` for every pair)
   const double* pmc;
   int pw;
+  int contact_test;  // THIP_CONTACT_ALL / FIRST / CLOSEST (trajopt_hip.h)
 };
 
 // the contact distance margin of robot sphere s against primitive p (p >= 0)
@@ -296,15 +297,37 @@ __global__ __launch_bounds__(kEvBlock) void coll_eval_kernel(const thip_chain* c
     s_base = 0;
   __syncthreads();
   double* out = stage + (static_cast<long long>(b) * n_units + u) * ucap * W;
-  for (long long c0 = 0; c0 < total; c0 += kEvBlock)
+  // one candidate (cidx in the flattened ContactResultMap order): its distance and
+  // fields; `pre` = contactTest's hit (within the pair's contact distance)
+  struct Cand
   {
-    const long long cidx = c0 + tid;
-    bool hit = false;
-    // side 0: the robot sphere s; side 1: primitive p, or (self) robot sphere sb
-    int link[2] = { 0, 0 }, p = 0, s = 0, sb = -1, i = 0, cc_type[2] = { kCCNone, kCCNone };
-    double dist = 0, normal[3] = { 0, 0, 0 }, pt[2][3] = { { 0, 0, 0 }, { 0, 0, 0 } }, cc_time[2] = { 0, 0 };
+    bool pre;
+    int link[2], p, s, sb, i, cc_type[2];
+    double dist, normal[3], pt[2][3], cc_time[2];
     Pose Ta[2], Tb[2];
-    if (cidx < total)
+  };
+  auto eval_cand = [&](long long cidx, Cand& cd) {
+    cd.link[0] = cd.link[1] = 0;
+    cd.p = cd.s = 0;
+    cd.sb = -1;
+    cd.i = 0;
+    cd.cc_type[0] = cd.cc_type[1] = kCCNone;
+    cd.cc_time[0] = cd.cc_time[1] = 0.0;
+    for (int k = 0; k < 3; ++k)
+      cd.normal[k] = cd.pt[0][k] = cd.pt[1][k] = 0.0;
+    cd.dist = 0.0;
+    int* const link = cd.link;
+    int& p = cd.p;
+    int& s = cd.s;
+    int& sb = cd.sb;
+    int& i = cd.i;
+    int* const cc_type = cd.cc_type;
+    double& dist = cd.dist;
+    double* const normal = cd.normal;
+    double(&pt)[2][3] = cd.pt;
+    double* const cc_time = cd.cc_time;
+    Pose* const Ta = cd.Ta;
+    Pose* const Tb = cd.Tb;
     {
       double qa[THIP_MAX_DOF], qb[THIP_MAX_DOF];
       auto states = [&]() {
@@ -406,18 +429,174 @@ __global__ __launch_bounds__(kEvBlock) void coll_eval_kernel(const thip_chain* c
           cc_type[0] = cc_type[1] = (i == 0) ? kCCTime0 : ((i == last) ? kCCTime1 : kCCBetween);
         }
       }
-      // the pair's contact distance after incrementCollisionMargin(buffer)
-      const double margin = pair_margin(tm, n_prims, s, p);
-      const double threshold = margin + tm.buffer;
-      hit = (dist < threshold) && !(dist > margin + tm.buffer);
-      // removeInvalidContactResults: at a fixed end keep a contact when one of its active
-      // sides is not at that end (a scene primitive's side is CCType_None)
-      if (hit && (un.f0 || un.f1))
-        hit = (un.f0 && ((cc_type[0] != kCCNone && cc_type[0] != kCCTime0) ||
-                         (cc_type[1] != kCCNone && cc_type[1] != kCCTime0))) ||
-              (un.f1 && ((cc_type[0] != kCCNone && cc_type[0] != kCCTime1) ||
-                         (cc_type[1] != kCCNone && cc_type[1] != kCCTime1)));
     }
+    // the pair's contact distance after incrementCollisionMargin(buffer) (a
+    // zero-coefficient pair reads margin -inf: it never enters the test)
+    const double margin = pair_margin(tm, n_prims, s, p);
+    cd.pre = dist < margin + tm.buffer;
+  };
+  // the evaluator's filter on a tested contact: removeInvalidContactResults
+  // (distance beyond the contact distance; at a fixed end keep a contact when one
+  // of its active sides is not at that end -- a scene primitive's side is CCType_None)
+  auto keep = [&](const Cand& cd) {
+    const double margin = pair_margin(tm, n_prims, cd.s, cd.p);
+    bool h = cd.pre && !(cd.dist > margin + tm.buffer);
+    if (h && (un.f0 || un.f1))
+      h = (un.f0 && ((cd.cc_type[0] != kCCNone && cd.cc_type[0] != kCCTime0) ||
+                     (cd.cc_type[1] != kCCNone && cd.cc_type[1] != kCCTime0))) ||
+          (un.f1 && ((cd.cc_type[0] != kCCNone && cd.cc_type[0] != kCCTime1) ||
+                     (cd.cc_type[1] != kCCNone && cd.cc_type[1] != kCCTime1)));
+    return h;
+  };
+  // the contact test type (trajopt_hip.h THIP_CONTACT_*): ALL, one item per
+  // candidate; CLOSEST, one item per (key, sub-state) group -- its candidates are
+  // contiguous in map order -- keeping the smallest distance (the first on ties);
+  // FIRST, one item per sub-state, its first candidate in map order within the
+  // contact distance.  The filter runs on what the test returned.
+  const int ctest = tm.contact_test;
+  long long n_scene_grp = 0;  // CLOSEST: scene groups (link group, primitive, sub-state)
+  for (int g = 0; g < S.n_groups; ++g)
+    n_scene_grp += static_cast<long long>(n_prims) * n_sub;
+  const long long n_items = (ctest == THIP_CONTACT_ALL) ? total
+                            : (ctest == THIP_CONTACT_CLOSEST) ? n_scene_grp + static_cast<long long>(S.n_self_keys) * n_sub
+                                                              : n_sub;
+  // first candidate of scene group g's block (its candidates: primitive-major,
+  // then sub-state, then the group's spheres)
+  auto grp_base = [&](int g) {
+    long long off = 0;
+    for (int h = 0; h < g; ++h)
+      off += static_cast<long long>(S.grp_ns[h]) * n_prims * n_sub;
+    return off;
+  };
+  auto self_base = [&](int k) {
+    long long off = scene_total;
+    for (int h = 0; h < k; ++h)
+      off += static_cast<long long>(n_sub) * (S.self_kp[h + 1] - S.self_kp[h]);
+    return off;
+  };
+  // FIRST returns one contact per contactTest call (sub-state), but the run's
+  // map flattens key-major: pass 1 stores each sub-state's chosen candidate (its
+  // index in map order, -1 for none) in a scratch at the tail of this unit's
+  // records, pass 2 writes each record at its chosen index's rank.  A unit whose
+  // records and scratch do not fit asks for that room (counts > ucap: the host
+  // reruns once with it).
+  const bool first_t = ctest == THIP_CONTACT_FIRST;
+  double* const fscr = out + static_cast<long long>(ucap) * W - n_sub;
+  if (first_t)
+  {
+    const long long need = static_cast<long long>(n_sub) + (n_sub + W - 1) / W;
+    if (need > ucap)
+    {
+      if (tid == 0)
+        counts[b * n_units + u] = static_cast<int>(need);
+      return;
+    }
+    for (int ii = tid; ii < n_sub; ii += kEvBlock)
+    {
+      Cand cd;
+      long long chosen = -1;
+      bool found = false;
+      for (int g = 0; g < S.n_groups && !found; ++g)
+      {
+        const int ng = S.grp_ns[g];
+        for (int pp = 0; pp < n_prims && !found; ++pp)
+          for (int e = 0; e < ng && !found; ++e)
+          {
+            chosen = grp_base(g) + (static_cast<long long>(pp) * n_sub + ii) * ng + e;
+            eval_cand(chosen, cd);
+            found = cd.pre;
+          }
+      }
+      for (int k = 0; k < S.n_self_keys && !found; ++k)
+      {
+        const int npk = S.self_kp[k + 1] - S.self_kp[k];
+        for (int e = 0; e < npk && !found; ++e)
+        {
+          chosen = self_base(k) + static_cast<long long>(ii) * npk + e;
+          eval_cand(chosen, cd);
+          found = cd.pre;
+        }
+      }
+      fscr[ii] = (found && keep(cd)) ? static_cast<double>(chosen) : -1.0;
+    }
+    __syncthreads();
+  }
+  for (long long c0 = 0; c0 < n_items; c0 += kEvBlock)
+  {
+    const long long item = c0 + tid;
+    Cand cd;
+    cd.pre = false;
+    bool hit = false;
+    int fpos = 0;
+    if (item < n_items)
+    {
+      if (ctest == THIP_CONTACT_ALL)
+      {
+        eval_cand(item, cd);
+        hit = keep(cd);
+      }
+      else if (ctest == THIP_CONTACT_CLOSEST)
+      {
+        long long c_first = 0;
+        int c_n = 0;
+        if (item < n_scene_grp)
+        {
+          long long r = item;
+          int g = 0;
+          for (; g < S.n_groups; ++g)
+          {
+            const long long sz = static_cast<long long>(n_prims) * n_sub;
+            if (r < sz)
+              break;
+            r -= sz;
+          }
+          const int ng = S.grp_ns[g];
+          // (primitive, sub-state) = r / n_sub, r % n_sub: candidates r * ng .. + ng
+          c_first = grp_base(g) + r * ng;
+          c_n = ng;
+        }
+        else
+        {
+          const long long r = item - n_scene_grp;
+          const int k = static_cast<int>(r / n_sub), ii = static_cast<int>(r % n_sub);
+          const int npk = S.self_kp[k + 1] - S.self_kp[k];
+          c_first = self_base(k) + static_cast<long long>(ii) * npk;
+          c_n = npk;
+        }
+        Cand c2;
+        for (int e = 0; e < c_n; ++e)
+        {
+          eval_cand(c_first + e, c2);
+          if (c2.pre && (!cd.pre || c2.dist < cd.dist))
+            cd = c2;
+        }
+        hit = keep(cd);
+      }
+      else  // FIRST: sub-state item, its pass-1 choice placed at its rank in map order
+      {
+        const double c = fscr[item];
+        hit = c >= 0.0;
+        if (hit)
+        {
+          eval_cand(static_cast<long long>(c), cd);
+          for (int i2 = 0; i2 < n_sub; ++i2)
+          {
+            const double c2 = fscr[i2];
+            fpos += (c2 >= 0.0 && c2 < c) ? 1 : 0;
+          }
+        }
+      }
+    }
+    // the contact's fields for the record below
+    int* const link = cd.link;
+    const int p = cd.p, s = cd.s, sb = cd.sb, i = cd.i;
+    const int* const cc_type = cd.cc_type;
+    const double dist = cd.dist;
+    const double* const normal = cd.normal;
+    const double(&pt)[2][3] = cd.pt;
+    const double* const cc_time = cd.cc_time;
+    const Pose* const Ta = cd.Ta;
+    const Pose* const Tb = cd.Tb;
     const unsigned long long m = __ballot(hit);
     const int lrank = __popcll(m & ((1ull << lane) - 1ull));
     if (lane == 0)
@@ -426,6 +605,8 @@ __global__ __launch_bounds__(kEvBlock) void coll_eval_kernel(const thip_chain* c
     int rank = s_base + lrank;
     for (int w = 0; w < wave; ++w)
       rank += s_wave_cnt[w];
+    if (first_t)
+      rank = fpos;
     if (hit && rank < ucap)
     {
       const int nsides = (sb >= 0) ? 2 : 1;
@@ -690,6 +871,7 @@ int thip_eval_create(int device, const thip_problem_desc* desc, int batch, thip_
     tm.lvs = main ? d.coll_lvs : x->lvs;
     tm.pmc = nullptr;
     tm.pw = d.n_prims + d.n_spheres;
+    tm.contact_test = main ? d.coll_contact_test : x->contact_test;
     const int nf = main ? d.coll_n_fixed : x->n_fixed;
     if (cont < 0 || cont > 2 || nf < 0 || nf > THIP_MAX_STEPS || (!tm.single && !(tm.lvs > 0)) || !(tm.buffer >= 0))
     {

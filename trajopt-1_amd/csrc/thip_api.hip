@@ -242,6 +242,10 @@ static int validate(const thip_problem_desc* d, std::string& why)
                  "lowered into the batched kernel: solve such a problem with sco::BasicTrustRegionSQP (the generic "
                  "path, GpuModel)",
            THIP_E_INVALID;
+  if (d->coll_enabled && d->coll_contact_test != THIP_CONTACT_ALL)
+    return why = "collision contact_test_type FIRST / CLOSEST is not lowered into the batched kernel: solve such a "
+                 "problem with sco::BasicTrustRegionSQP (the generic path, device-evaluated terms and GpuModel)",
+           THIP_E_INVALID;
   if (d->n_coll_extra != 0)
     return why = "more than one collision term is not lowered into the batched kernel: solve such a problem with "
                  "sco::BasicTrustRegionSQP (the generic path, device-evaluated terms and GpuModel)",

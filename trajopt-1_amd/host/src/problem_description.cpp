@@ -1025,8 +1025,6 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
   if (evaluator_type < 1 || evaluator_type > 4)
     unsupported("collision evaluator_type " + std::to_string(evaluator_type) +
                 " (DISCRETE = 1, LVS_DISCRETE = 2, CONTINUOUS = 3, LVS_CONTINUOUS = 4 are)");
-  if (contact_test_type != 2)
-    unsupported("collision contact_test_type " + std::to_string(contact_test_type) + " (only ALL = 2)");
   const auto env = prob.GetEnv();
   thip_problem_desc& d = prob.desc();
   // the first collision term lowers into the descriptor's coll_* fields (the batched
@@ -1061,6 +1059,9 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
   const int continuous = (evaluator_type == 1) ? 2 : (evaluator_type >= 3) ? 1 : 0;
   const double lvs = (evaluator_type == 3) ? 1.7976931348623157e308 : longest_valid_segment_length;
   const int term = extra ? 1 + d.n_coll_extra : 0;  // thip_eval's collision term index
+  // tesseract ContactTestType {FIRST = 0, CLOSEST = 1, ALL = 2} -> THIP_CONTACT_* (ALL = 0)
+  const int ctest = contact_test_type == 0 ? THIP_CONTACT_FIRST
+                                           : (contact_test_type == 1 ? THIP_CONTACT_CLOSEST : THIP_CONTACT_ALL);
   if (extra)
   {
     thip_coll_term& x = d.coll_extra[d.n_coll_extra++];
@@ -1075,6 +1076,7 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
     x.buffer = collision_margin_buffer;
     x.lvs = lvs;
     x.continuous = continuous;
+    x.contact_test = ctest;
   }
   else
   {
@@ -1089,6 +1091,7 @@ void CollisionTermInfo::hatch(TrajOptProb& prob)
     d.coll_coeff = coeff;
     d.coll_buffer = collision_margin_buffer;
     d.coll_continuous = continuous;
+    d.coll_contact_test = ctest;
     d.coll_lvs = lvs;
   }
   // one CollisionCost / CollisionConstraint per unit, named <name>_<i> (:1735-1858)
@@ -1448,7 +1451,8 @@ bool TrajOptProb::lowerable() const
   // scene primitives, and no term it does not lower
   return desc_.n_steps >= 2 && desc_.n_steps <= THIP_MAX_STEPS && desc_.n_prims <= THIP_MAX_PRIMS &&
          thip_jdt_fused(&desc_) && desc_.n_jvt == 0 && desc_.n_ttt == 0 && !desc_.use_time && desc_.n_fixed_dofs == 0 &&
-         desc_.n_coll_extra == 0 && unloweredTerms().empty();
+         desc_.n_coll_extra == 0 && (!desc_.coll_enabled || desc_.coll_contact_test == THIP_CONTACT_ALL) &&
+         unloweredTerms().empty();
 }
 
 LoweredProblem TrajOptProb::lowered() const

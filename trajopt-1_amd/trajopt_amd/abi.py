@@ -10,7 +10,8 @@ import ctypes as C
 import os
 from pathlib import Path
 
-ABI_VERSION = 8  # THIP_ABI_VERSION
+ABI_VERSION = 9  # THIP_ABI_VERSION
+CONTACT_ALL, CONTACT_FIRST, CONTACT_CLOSEST = 0, 1, 2  # THIP_CONTACT_* (collision contact_test_type)
 MAX_DOF = 16
 MAX_LINKS = 32
 MAX_STEPS = 64
@@ -118,6 +119,7 @@ class CollTerm(C.Structure):
         ("buffer", C.c_double),
         ("lvs", C.c_double),
         ("continuous", C.c_int),
+        ("contact_test", C.c_int),
     ]
 
 
@@ -212,6 +214,7 @@ class ProblemDesc(C.Structure):
         ("coll_buffer", C.c_double),
         ("coll_lvs", C.c_double),
         ("coll_continuous", C.c_int),
+        ("coll_contact_test", C.c_int),
         ("n_spheres", C.c_int),
         ("sphere_link", C.c_int * MAX_SPHERES),
         ("sphere_center", _D3 * MAX_SPHERES),
