@@ -308,7 +308,8 @@ def main_hostloop(args, world, rank, local_rank, json_out):
                 # leaves out the factor of a pattern staged in LDS) over the wall
                 # time inside the rounds (staging, H2D, launch, D2H) -- not
                 # measured HBM traffic
-                "bound": "latency",
+                "bound": "hbm",
+                "limiter": "latency",
                 "kernel": "thip::qp_csc_group_kernel",
                 "achieved_kind": "algorithmic bytes / round wall time",
                 "achieved": achieved,
@@ -506,7 +507,8 @@ def main():
                 # `frac` are the SURVEY.md 8d streaming-byte model against HBM peak, as
                 # the metric asks; the working set is LDS/register resident, so the
                 # measured HBM traffic (`traffic`, `measured_gbs`) is far below it.
-                "bound": "latency",
+                "bound": "hbm",
+                "limiter": "latency",
                 "kernel": "thip::sqp_kernel",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
