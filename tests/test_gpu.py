@@ -949,7 +949,7 @@ def test_bench_json_line():
     assert line["value"] > 0 and line["n_gpus"] == 1 and line["dtype"] == "f64"
     assert line["config"]["batches_in_flight"] == 3 and line["config"]["batch_latency_ms"] > 0
     rf = line["roofline"]
-    assert rf["bound"] == "latency" and rf["peak"] == 8000.0 and 0 < rf["frac"] == pytest.approx(rf["achieved"] / 8000.0)
+    assert rf["bound"] == "hbm" and rf["limiter"] == "latency" and rf["peak"] == 8000.0 and 0 < rf["frac"] == pytest.approx(rf["achieved"] / 8000.0)
     cb = line["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
     assert cb["host_nproc"] >= 1 and cb["single_problem_latency_s"] > 0
