@@ -580,8 +580,10 @@ int thip_debug_layout(thip_ctx* ctx, long long* doff, long long* ioff, long long
 #define THIP_DEBUG_NO_BRANCH 4  /* one block solve over all dofs even when the terms split the tree */
 #define THIP_DEBUG_STATIC_DISPATCH 8  /* one workgroup per problem instead of persistent workgroups taking
                                          problems from a counter (bitwise the same results) */
-#define THIP_DEBUG_GEN_BUILD 16       /* QPs outside the segment's domain run the generic-step build
-                                         (512 threads, no segment) instead of the 256-thread build */
+#define THIP_DEBUG_GEN_BUILD 16       /* with THIP_DEBUG_NO_SEGMENT: every QP runs the generic-step build
+                                         (its own compilation, no segment code) */
+#define THIP_DEBUG_MAIN_BUILD 32      /* QPs outside the segment's domain run the main build's generic step
+                                         instead of the generic-step build (the default since round 6) */
 int thip_debug_set_path(int flags);
 int thip_debug_workspace(thip_ctx* ctx, double* dws, int* iws);
 /* The solve layout a context chose (diagnostic): out[0] block-solve branches

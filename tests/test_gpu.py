@@ -1220,6 +1220,34 @@ def test_joint_acc_runs_the_pair_layout():
     s.close()
     assert lay["grp"] == 2 and lay["block_dofs"] == 14 and lay["wide"] == 1 and lay["blocks"] == 15, lay
     assert lay["seg_ok"] == 0 and lay["nbr"] == 1, lay
+    # QPs outside the segment's domain run the generic-step build (round 6)
+    assert lay["gen"] == 1 and lay["threads"] == 256, lay
+
+
+@pytest.mark.parametrize("cfg,B", [("HA", 16), ("E", 4), ("C50", 8)])
+def test_generic_step_build_matches_main_build(cfg, B):
+    """The generic-step build (sqp_kernel_gen: its own compilation without the
+    register-resident segment, adaptive unroll in its row / column loops) runs
+    the QPs the segment does not take; its results are bitwise those of the
+    main build's generic step (THIP_DEBUG_MAIN_BUILD), so the parity checks of
+    either cover both."""
+    def solve(flags):
+        wl = problems.make_workload("C", B, n_steps=50) if cfg == "C50" else problems.make_workload(cfg, B)
+        hip = abi.load_hip()
+        assert hip.thip_debug_set_path(flags) == 0
+        try:
+            s = BatchTrustRegionSQP(wl)
+            lay = s.layout()
+            x, res = s.optimize()
+            s.close()
+        finally:
+            hip.thip_debug_set_path(0)
+        return lay, x, [(r.status, r.n_sqp_iters, r.n_admm_iters) for r in res]
+
+    lg, xg, rg = solve(0)
+    lm, xm, rm = solve(abi.DEBUG_MAIN_BUILD)
+    assert lg["gen"] == 1 and lm["gen"] == 0, (lg, lm)
+    assert rg == rm and np.array_equal(xg, xm)
 
 
 def test_joint_acc_odd_horizon_is_refused():

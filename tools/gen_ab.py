@@ -1,8 +1,9 @@
 """A/B of the fused kernel's two builds on a workload whose QPs never take the
 register-resident segment (config E by default): the generic-step build
-(sqp_kernel_gen, layout.hpp kGenBlock threads) against the 256-thread build
-(the default; THIP_DEBUG_GEN_BUILD selects the generic-step build).  Per build: one batch alone (HIP-event ms), SQP
-iterations, statuses; then whether the two builds agree to the parity bar.
+(sqp_kernel_gen, layout.hpp kGenBlock threads; the default for such QPs since
+round 6) against the main build's generic step (THIP_DEBUG_MAIN_BUILD).  Per
+build: one batch alone (HIP-event ms), SQP iterations, statuses; then whether
+the two builds agree to the parity bar.
 
     python tools/gen_ab.py [config] [batch] [n_steps] [root]
 
@@ -27,7 +28,8 @@ N = int(sys.argv[3]) if len(sys.argv) > 3 and int(sys.argv[3]) > 0 else None
 hip = abi.load_hip()
 out = {}
 print(abi.__file__, flush=True)
-for name, flags in (("gen", abi.DEBUG_GEN_BUILD | abi.DEBUG_NO_SEGMENT), ("main", abi.DEBUG_NO_SEGMENT)):
+for name, flags in (("gen", abi.DEBUG_GEN_BUILD | abi.DEBUG_NO_SEGMENT),
+                    ("main", abi.DEBUG_NO_SEGMENT | abi.DEBUG_MAIN_BUILD)):
     assert hip.thip_debug_set_path(flags) == 0
     wl = problems.make_workload(cfg, B, n_steps=N) if N else problems.make_workload(cfg, B)
     s = BatchTrustRegionSQP(wl)

@@ -15,17 +15,19 @@ namespace thip
 // threads per problem workgroup.  sqp_kernel.hip is compiled twice: the main
 // build (256 threads: the register-resident ADMM segment's ownership maps and
 // launch bounds need them) and the generic-step build (THIP_GENERIC_ONLY,
-// THIP_KBLOCK = kGenBlock: no segment code, twice the waves, meant to hide the
-// HBM latency of the generic ADMM step's row loops for QPs the segment does not
-// take -- blocks wider than 8 dofs, more than 32 waypoints; opt-in through
-// THIP_DEBUG_GEN_BUILD: measured no faster on config E)
+// THIP_KBLOCK = kGenBlock, default 256: no segment code, so 17 VGPR spills
+// instead of the main build's ~210, and its generic loops adapt their unroll to
+// the loop length).  QPs the segment does not take -- blocks wider than 8 dofs
+// (config E, JointAcc's waypoint pairs), more than 32 waypoints -- run it
+// (round 6; THIP_DEBUG_MAIN_BUILD restores the main build's generic step).
+// 512 threads was measured no faster on config E.
 #ifndef THIP_KBLOCK
 #define THIP_KBLOCK 256
 #endif
 constexpr int kBlock = THIP_KBLOCK;
 constexpr int kWaves = kBlock / 64;
 #ifndef THIP_GEN_BLOCK
-#define THIP_GEN_BLOCK 512
+#define THIP_GEN_BLOCK 256
 #endif
 constexpr int kGenBlock = THIP_GEN_BLOCK;  // threads of the generic-step build
 // 1,024 threads faults on collision problems (HSA aperture violation, config C;
@@ -39,8 +41,9 @@ constexpr int kScanWaves = 4;
 // dynamic LDS a problem may use (160 KB per CU on gfx950, one workgroup per
 // CU; the rest is the kernel's static LDS)
 constexpr long long kLdsBudgetBytes = 149 * 1024;
-// ... for the generic-step build, whose static LDS is ~1.5 KB larger
-constexpr long long kLdsBudgetGenBytes = 146 * 1024;
+// ... for the generic-step build: the same static LDS at 256 threads, ~1.5 KB
+// more at 512 (reductions over 8 waves)
+constexpr long long kLdsBudgetGenBytes = (kGenBlock == 256) ? kLdsBudgetBytes : 146 * 1024;
 // ADMM-segment chain pack (A_CPK), per half h (0: top, 1: bottom) and chain
 // step r (distance from the middle block), in the lane order the octet chain
 // reads it, zero past the half's length and outside the D x D block:

@@ -50,6 +50,39 @@ constexpr int kGenULight = 8;  // a few loads per iteration (streaming vectors, 
 constexpr int kGenUHeavy = 2;  // a CartPose row's coefficients and x (~2 D + 8 loads)
 constexpr int kGenUHinge = 2;  // a hinge row's 2 D coefficients and 2 D x values (config E's heavy
                                 // problems: ~20 rows per thread, one HBM round trip each at 1)
+// Calls f(integral_constant<U'>) with U' the smallest power of two <= U whose
+// U' kBlock items cover n (a uniform choice).  A loop over fewer items than
+// U kBlock would otherwise issue the clamped loads of U - U' duplicate
+// iterations per thread; on the FLAT path those cost issue slots even when
+// they hit LDS (config HA: 181 CartPose rows and 210 columns on 256 threads).
+// Each item's arithmetic is the same at any U'.  Only the generic-step build
+// adapts: in the main build U' = U, and its code is instruction for
+// instruction that of the plain loops (the register-resident segment's results
+// were seen to depend on how the rest of that kernel compiles).
+template <int U, typename F>
+__device__ __forceinline__ void unroll_for(int n, F&& f)
+{
+#if THIP_GENERIC_ONLY
+  if constexpr (U > 1)
+  {
+    if (n <= (U / 2) * kBlock)
+    {
+      unroll_for<U / 2>(n, f);
+      return;
+    }
+  }
+#endif
+  f(std::integral_constant<int, U>());
+}
+// A loop over n items unrolled U per thread: adaptive (unroll_for) in the
+// generic-step build, the plain loop with U = UMAX in the main build
+#if THIP_GENERIC_ONLY
+#define GEN_UNROLL_BEGIN(UMAX, N) unroll_for<(UMAX)>((N), [&](auto uc_) { constexpr int U = decltype(uc_)::value;
+#define GEN_UNROLL_END });
+#else
+#define GEN_UNROLL_BEGIN(UMAX, N) { constexpr int U = (UMAX);
+#define GEN_UNROLL_END }
+#endif
 constexpr double kRhoMin = 1e-6, kRhoMax = 1e6, kRhoTol = 1e-4, kRhoEq = 1e3;
 constexpr double kMinScal = 1e-4, kMaxScal = 1e4;
 constexpr double kDivTol = 1.0 / kInf;
@@ -2945,20 +2978,21 @@ __device__ __forceinline__ double csr_row_gather(const int* rows, int p0, int p1
 
 
 // csr_row_gather for contiguous rows (Layout::rows_contig): the rows [p0, p1)
-// themselves, at most 16, every load issued before the sum (in the same order)
+// themselves, at most R, every load issued before the sum (in the same order)
+template <int R>
 __device__ __forceinline__ double contig_row_gather(int p0, int p1, const double* GS, const double* MR, int D, int j,
                                                     double b)
 {
-  double g[16], mv[16];
+  double g[R], mv[R];
 #pragma unroll
-  for (int u = 0; u < 16; ++u)
+  for (int u = 0; u < R; ++u)
   {
     const int r = max(min(p0 + u, p1 - 1), 0);  // clamped: every load valid (an empty range reads row 0)
     g[u] = GS[r * D + j];
     mv[u] = MR[r];
   }
 #pragma unroll
-  for (int u = 0; u < 16; ++u)
+  for (int u = 0; u < R; ++u)
     b = fma(g[u], mv[u] * ((p0 + u < p1) ? 1.0 : 0.0), b);  // masked: b unchanged
   return b;
 }
@@ -3032,11 +3066,12 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   auto rho_l = [&](int r) { return !polish ? RHO[r] : (ACT[r] != 0 ? 1.0 / delta : 0.0); };
   auto brow = [&](int col) { return col < nc_base ? n_rows + col : m_base + 2 * (col - nc_base) + 1; };
   // kGenU rows per thread at once, every load before any store (see admm_step)
-  for (int r0 = tid; r0 < n_abs; r0 += kGenU * kBlock)
+  GEN_UNROLL_BEGIN(kGenU, n_abs)
+  for (int r0 = tid; r0 < n_abs; r0 += U * kBlock)
   {
-    double mr[kGenU], rnv[kGenU], rpv[kGenU];
+    double mr[U], rnv[U], rpv[U];
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int r = min(r0 + u * kBlock, n_abs - 1);
       const int ca = nx + 2 * r;
@@ -3050,7 +3085,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       rpv[u] = rp;
     }
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int r = r0 + u * kBlock;
       if (r >= n_abs)
@@ -3060,12 +3095,14 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       BA[nx + 2 * r + 1] = rpv[u];
     }
   }
+  GEN_UNROLL_END
   const int nh = c.s->n_h;
-  for (int h0 = tid; h0 < nh; h0 += kGenU * kBlock)
+  GEN_UNROLL_BEGIN(kGenU, nh)
+  for (int h0 = tid; h0 < nh; h0 += U * kBlock)
   {
-    double mr[kGenU], rnv[kGenU];
+    double mr[U], rnv[U];
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int h = min(h0 + u * kBlock, nh - 1);
       const int col = nc_base + h;
@@ -3076,7 +3113,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       rnv[u] = rn;
     }
 #pragma unroll
-    for (int u = 0; u < kGenU; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int h = h0 + u * kBlock;
       if (h >= nh)
@@ -3085,6 +3122,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       BA[nc_base + h] = rnv[u];
     }
   }
+  GEN_UNROLL_END
   BSYNC();
   PROF_LAP(23);
   // the hinge share of the column sums, row-parallel: chunk q's partial sum of
@@ -3142,11 +3180,16 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
   // the waypoint right-hand sides, kRhsU columns per thread at once (their
   // loads overlap; each column's sums in the order of one column alone)
   constexpr int kRhsU = 3;
-  for (int c0 = tid; c0 < nx; c0 += kRhsU * kBlock)
+#if THIP_GENERIC_ONLY
+  // (the main build keeps the 16-row gather, see unroll_for)
+  const bool rows8 = L.max_step_rows <= 8, rows16 = L.rows_contig && L.max_step_rows <= 16;
+#endif
+  GEN_UNROLL_BEGIN(kRhsU, nx)
+  for (int c0 = tid; c0 < nx; c0 += U * kBlock)
   {
-    double bv[kRhsU];
+    double bv[U];
 #pragma unroll
-    for (int u = 0; u < kRhsU; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int col = min(c0 + u * kBlock, nx - 1);  // clamped: every load valid
       const int t = col / D, j = col % D;
@@ -3154,9 +3197,17 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       const int f = fixed_of_step[t];
       if (f >= 0)
         b += FS[f * D + j] * eta[f * D + j];
-      if (L.rows_contig && L.max_step_rows <= 16)
-        b = contig_row_gather(step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
+#if THIP_GENERIC_ONLY
+      if (rows16 && rows8)
+        b = contig_row_gather<8>(step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
+      else if (rows16)
+        b = contig_row_gather<16>(step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
       else
+#else
+      if (L.rows_contig && L.max_step_rows <= 16)
+        b = contig_row_gather<16>(step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
+      else
+#endif
         b = csr_row_gather(step_rows, step_ptr[t], step_ptr[t + 1], GS, MR, D, j, b);
       if (nh > 0)
       {
@@ -3167,10 +3218,11 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       bv[u] = b;
     }
 #pragma unroll
-    for (int u = 0; u < kRhsU; ++u)
+    for (int u = 0; u < U; ++u)
       if (c0 + u * kBlock < nx)
         BX[c0 + u * kBlock] = bv[u];
   }
+  GEN_UNROLL_END
   BSYNC();
   PROF_LAP(24);
   // c = LI b per solve block (Layout::nbr): solve index v is row i of block T,
@@ -3240,11 +3292,12 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     for (int col = tid; col < nx; col += kBlock)
       out[col] = CV[col];
   // aux back-substitution
-  for (int r0 = tid; r0 < n_abs; r0 += kGenUHeavy * kBlock)
+  GEN_UNROLL_BEGIN(kGenUHeavy, n_abs)
+  for (int r0 = tid; r0 < n_abs; r0 += U * kBlock)
   {
-    double on[kGenUHeavy], op[kGenUHeavy];
+    double on[U], op[U];
 #pragma unroll
-    for (int u = 0; u < kGenUHeavy; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int r = min(r0 + u * kBlock, n_abs - 1);
       const int t = row_step[r];
@@ -3263,7 +3316,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       op[u] = (dn * rp - rr * wn * cross + wp * dn * h) / det;
     }
 #pragma unroll
-    for (int u = 0; u < kGenUHeavy; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int r = r0 + u * kBlock;
       if (r >= n_abs)
@@ -3272,13 +3325,15 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       out[nx + 2 * r + 1] = op[u];
     }
   }
+  GEN_UNROLL_END
   const double* const HCT = c.a(A_HCT);
   const int nhs = nh | 1;
-  for (int h0 = tid; h0 < nh; h0 += kGenUHinge * kBlock)
+  GEN_UNROLL_BEGIN(kGenUHinge, nh)
+  for (int h0 = tid; h0 < nh; h0 += U * kBlock)
   {
-    double ov[kGenUHinge];
+    double ov[U];
 #pragma unroll
-    for (int u = 0; u < kGenUHinge; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int h = min(h0 + u * kBlock, nh - 1);
       const int t = HT[h];
@@ -3293,7 +3348,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       ov[u] = (BA[col] + w * (eta[m_base + 2 * h] - rr * g)) / (dn + rr * w * w);
     }
 #pragma unroll
-    for (int u = 0; u < kGenUHinge; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int h = h0 + u * kBlock;
       if (h >= nh)
@@ -3301,6 +3356,7 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
       out[nc_base + h] = ov[u];
     }
   }
+  GEN_UNROLL_END
   BSYNC();
   PROF_LAP(11);
 #undef PROF_LAP
@@ -3806,34 +3862,38 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
   // loads above this one's stores and each iteration paid a full memory
   // round trip (config E: 14-DoF x 50 waypoints, ~4,300 rows)
   const int m = c.m(), nc = c.nc();
-  for (int r0 = tid; r0 < (pre_ready ? 0 : m); r0 += kGenULight * kBlock)
+  GEN_UNROLL_BEGIN(kGenULight, m)
+  for (int r0 = tid; r0 < (pre_ready ? 0 : m); r0 += U * kBlock)
   {
-    double e[kGenULight];
+    double e[U];
 #pragma unroll
-    for (int u = 0; u < kGenULight; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int r = min(r0 + u * kBlock, m - 1);
       e[u] = RH[r] * zp[r] - Y[r];
     }
 #pragma unroll
-    for (int u = 0; u < kGenULight; ++u)
+    for (int u = 0; u < U; ++u)
       if (r0 + u * kBlock < m)
         ETA[r0 + u * kBlock] = e[u];
   }
-  for (int c0 = tid; c0 < (pre_ready ? 0 : nc); c0 += kGenULight * kBlock)
+  GEN_UNROLL_END
+  GEN_UNROLL_BEGIN(kGenULight, nc)
+  for (int c0 = tid; c0 < (pre_ready ? 0 : nc); c0 += U * kBlock)
   {
-    double e[kGenULight];
+    double e[U];
 #pragma unroll
-    for (int u = 0; u < kGenULight; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int col = min(c0 + u * kBlock, nc - 1);
       e[u] = sig * xp[col] - Q[col];
     }
 #pragma unroll
-    for (int u = 0; u < kGenULight; ++u)
+    for (int u = 0; u < U; ++u)
       if (c0 + u * kBlock < nc)
         BX[c0 + u * kBlock] = e[u];
   }
+  GEN_UNROLL_END
   BSYNC();
   if (pf)
     pf[30] += clock64() - tq;
@@ -3907,10 +3967,12 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
     v += WS[2 * a] * XT[ca] + WS[2 * a + 1] * XT[ca + 1];
     return v;
   };
-  update_rows(0, n_rows, row_ax_l, std::integral_constant<int, kGenUHeavy>());
+  GEN_UNROLL_BEGIN(kGenUHeavy, n_rows) update_rows(0, n_rows, row_ax_l, std::integral_constant<int, U>()); GEN_UNROLL_END
   {
+    GEN_UNROLL_BEGIN(kGenULight, m_base - n_rows)
     update_rows(n_rows, m_base, [&](int r) { return BS[r - n_rows] * XT[r - n_rows]; },
-                std::integral_constant<int, kGenULight>());
+                std::integral_constant<int, U>());
+    GEN_UNROLL_END
     if (m > m_base)
     {
       // hinge row m_base + 2h: a_t.x_t + a_t+1.x_t+1 + w h; m_base + 2h + 1:
@@ -3955,11 +4017,12 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
       }
     }
   }
-  for (int c0 = tid; c0 < nc; c0 += kGenULight * kBlock)
+  GEN_UNROLL_BEGIN(kGenULight, nc)
+  for (int c0 = tid; c0 < nc; c0 += U * kBlock)
   {
-    double xt[kGenULight], xo[kGenULight], qv[kGenULight];
+    double xt[U], xo[U], qv[U];
 #pragma unroll
-    for (int u = 0; u < kGenULight; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int col = min(c0 + u * kBlock, nc - 1);
       xt[u] = XT[col];
@@ -3967,7 +4030,7 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
       qv[u] = Q[col];
     }
 #pragma unroll
-    for (int u = 0; u < kGenULight; ++u)
+    for (int u = 0; u < U; ++u)
     {
       const int col = c0 + u * kBlock;
       if (col >= nc)
@@ -3978,6 +4041,7 @@ __device__ void admm_step(Ctx& c, Solver& sv, bool pre_ready)
       BX[col] = sig * xv - qv[u];  // the next step's sigma xp - q (same expression)
     }
   }
+  GEN_UNROLL_END
   BSYNC();
   if (pf)
     pf[31] += clock64() - tq;

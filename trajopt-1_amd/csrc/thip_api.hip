@@ -147,7 +147,7 @@ int thip_debug_solve_layout(const thip_ctx* ctx, int* out, int n)
 int thip_debug_set_path(int flags)
 {
   if (flags & ~(THIP_DEBUG_NO_SEGMENT | THIP_DEBUG_FORCE_WIDE | THIP_DEBUG_NO_BRANCH | THIP_DEBUG_STATIC_DISPATCH |
-                THIP_DEBUG_GEN_BUILD))
+                THIP_DEBUG_GEN_BUILD | THIP_DEBUG_MAIN_BUILD))
     return THIP_E_INVALID;
   g_debug_path = flags;
   return THIP_OK;
@@ -811,7 +811,8 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     // kernel (kGenBlock threads, no segment code) takes them; its larger static
     // LDS (reductions over 16 waves) leaves a smaller dynamic budget
     const bool seg_cand = max_step_rows <= kMaxStepRows && !L.wide && L.N * 8 <= kBlock && L.n_abs <= kBlock && cpk;
-    ctx->gen = (!seg_cand || (g_debug_path & THIP_DEBUG_NO_SEGMENT)) && (g_debug_path & THIP_DEBUG_GEN_BUILD);
+    ctx->gen = (!seg_cand && !(g_debug_path & THIP_DEBUG_MAIN_BUILD)) ||
+               ((g_debug_path & THIP_DEBUG_NO_SEGMENT) && (g_debug_path & THIP_DEBUG_GEN_BUILD));
     const long long budget =
         (ctx->gen ? kLdsBudgetGenBytes : kLdsBudgetBytes) / static_cast<long long>(sizeof(double));
     for (int k : order)

@@ -31,6 +31,7 @@ EVAL_MAX_STEPS = 4096  # THIP_EVAL_MAX_STEPS: the generic path's horizon
 EVAL_MAX_PRIMS = 1024  # THIP_EVAL_MAX_PRIMS
 TRACE_W = 16  # THIP_TRACE_W
 DEBUG_NO_SEGMENT, DEBUG_FORCE_WIDE, DEBUG_NO_BRANCH, DEBUG_STATIC_DISPATCH, DEBUG_GEN_BUILD = 1, 2, 4, 8, 16  # thip_debug_set_path flags
+DEBUG_MAIN_BUILD = 32
 
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_CONTINUOUS, JOINT_PRISMATIC = 0, 1, 2, 3
 PRIM_SPHERE, PRIM_BOX, PRIM_CAPSULE = 0, 1, 2
