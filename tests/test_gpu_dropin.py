@@ -359,7 +359,7 @@ def test_contact_test_dropin(oracle_mod, json_type, ctest):
     loop (device-evaluated collision terms, GPU QPs), and the result has oracle
     parity (three of the ten primitives: the JSON problems carry the reference's
     0.5 m safety buffer)."""
-    wl0 = problems.make_workload("C", 4, first_problem=40)
+    wl0 = problems.make_workload("C", 2, first_problem=40)
     texts = []
     for b in range(wl0.batch):
         doc = json.loads(host.workload_to_json(wl0, b))
