@@ -85,8 +85,10 @@ extern "C" {
  * of the whole test in ContactResultMap order (keys (link, primitive), then the
  * self link pairs; inside a key, sphere order).  The primitive model replaces
  * Bullet's broad phase, so FIRST's choice is parity unpinned against tesseract,
- * as every contact value is.  Only ALL runs in the fused kernel; FIRST and
- * CLOSEST run on the generic path (device evaluator thip_eval_collision). */
+ * as every contact value is.  The fused kernel runs FIRST and CLOSEST in its
+ * generic-step build (sqp_kernel_gen: thip_create selects it for such a
+ * descriptor, and thip_collision_rows runs that build's scan); the device
+ * evaluator (thip_eval_collision) runs all three. */
 #define THIP_CONTACT_ALL 0
 #define THIP_CONTACT_FIRST 1
 #define THIP_CONTACT_CLOSEST 2

@@ -341,24 +341,59 @@ def test_eval_collision_rows_contact_test(oracle_mod, cont, ctest):
     assert total > 20
 
 
-def test_contact_test_refused_by_the_fused_kernel():
-    """The fused kernel runs ALL only: a FIRST / CLOSEST descriptor names the generic path."""
-    from trajopt_amd.runtime import BatchTrustRegionSQP, HipError
+@pytest.mark.parametrize("ctest", [abi.CONTACT_FIRST, abi.CONTACT_CLOSEST])
+@pytest.mark.parametrize("cont", [0, 1, 2])
+def test_contact_test_fused_rows(oracle_mod, cont, ctest):
+    """The fused kernel's contact scan with contact_test_type FIRST / CLOSEST (the
+    generic-step build, sqp_kernel_gen: thip_collision_rows runs its scan) against
+    the oracle's rows and the device evaluator's, for every evaluator."""
+    from trajopt_amd.runtime import BatchTrustRegionSQP
 
-    wl = problems.make_workload("C", 2)
-    wl.desc.coll_contact_test = abi.CONTACT_CLOSEST
-    with pytest.raises(HipError) as ei:
-        BatchTrustRegionSQP(wl)
-    assert "generic path" in str(ei.value)
+    wl = problems.make_workload("C", 8)
+    wl.desc.coll_continuous = cont
+    wl.desc.coll_contact_test = ctest
+    x1 = wl.init + 0.03 * np.random.default_rng(7).standard_normal(wl.init.shape)
+    s = BatchTrustRegionSQP(wl)
+    assert s.layout()["gen"] == 1
+    ev = TermEvaluator(wl)
+    total = 0
+    for x in (wl.init, x1):
+        fused = s.collision_rows(x)
+        rows = ev.collision(0, x)
+        for b in range(wl.batch):
+            ref = oracle_mod.collision_rows(wl, b, x[b])
+            total += len(ref)
+            _check_rows(fused[b], ref, f"cont {cont} test {ctest} problem {b} (fused)")
+            _check_rows(fused[b], rows[b], f"cont {cont} test {ctest} problem {b} (fused vs evaluator)")
+    s.close()
+    ev.close()
+    assert total > 20
+
+
+@pytest.mark.parametrize("cfg", ["C-first", "C-closest", "C-cont-closest", "C-cont-first"])
+def test_sqp_parity_contact_test(oracle_mod, cfg):
+    """BasicTrustRegionSQP with contact_test_type FIRST / CLOSEST in the fused
+    kernel (generic-step build) against the oracle, LVS_DISCRETE and
+    LVS_CONTINUOUS."""
+    from trajopt_amd.runtime import BatchTrustRegionSQP
+
+    wl = problems.make_workload("C", 32)
+    wl.desc.coll_continuous = 1 if "cont" in cfg else 0
+    wl.desc.coll_contact_test = abi.CONTACT_FIRST if cfg.endswith("first") else abi.CONTACT_CLOSEST
+    s = BatchTrustRegionSQP(wl)
+    x, res = s.optimize()
+    s.close()
+    check_parity(wl, oracle_mod, x, res, label=f"{cfg}-32", min_strict=0.6)
 
 
 @pytest.mark.parametrize("json_type,ctest", [(0, abi.CONTACT_FIRST), (1, abi.CONTACT_CLOSEST)])
 def test_contact_test_dropin(oracle_mod, json_type, ctest):
     """Config C problems as TrajOptRequest JSON with "contact_test_type" 0 (FIRST)
-    or 1 (CLOSEST): ConstructProblem lowers the type, the problem runs the host
-    loop (device-evaluated collision terms, GPU QPs), and the result has oracle
-    parity (three of the ten primitives: the JSON problems carry the reference's
-    0.5 m safety buffer)."""
+    or 1 (CLOSEST): ConstructProblem lowers the type, the batch runs the fused
+    kernel (its generic-step build selects among each call's contacts), and the
+    result has oracle parity (three of the ten primitives: the JSON problems
+    carry the reference's 0.5 m safety buffer).  The host loop with the device
+    evaluator is checked row by row above."""
     wl0 = problems.make_workload("C", 2, first_problem=40)
     texts = []
     for b in range(wl0.batch):

@@ -41,9 +41,9 @@ constexpr int kScanWaves = 4;
 // dynamic LDS a problem may use (160 KB per CU on gfx950, one workgroup per
 // CU; the rest is the kernel's static LDS)
 constexpr long long kLdsBudgetBytes = 149 * 1024;
-// ... for the generic-step build: the same static LDS at 256 threads, ~1.5 KB
-// more at 512 (reductions over 8 waves)
-constexpr long long kLdsBudgetGenBytes = (kGenBlock == 256) ? kLdsBudgetBytes : 146 * 1024;
+// ... for the generic-step build: ~0.5 KB more static LDS at 256 threads (the
+// contact scan's FIRST bits), ~2 KB more at 512 (reductions over 8 waves)
+constexpr long long kLdsBudgetGenBytes = (kGenBlock == 256) ? 148 * 1024 : 146 * 1024;
 // ADMM-segment chain pack (A_CPK), per half h (0: top, 1: bottom) and chain
 // step r (distance from the middle block), in the lane order the octet chain
 // reads it, zero past the half's length and outside the D x D block:

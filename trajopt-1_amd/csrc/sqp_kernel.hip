@@ -150,6 +150,12 @@ struct Ctl
 // descriptor in HBM they were FLAT loads with L2 latency at every joint of
 // every walk (sub-state FK of the contact scans, the CartPose jacobians).
 __shared__ thip_chain g_chain;
+#if THIP_GENERIC_ONLY
+// contact_test_type FIRST in the fused scan (coll_scan_pairs): per scan wave,
+// one bit per sub-state of the unit being scanned -- a contactTest call whose
+// first contact has been met in ContactResultMap order
+__shared__ unsigned g_first_done[kScanWaves][kSubCap / 32];
+#endif
 
 __device__ __forceinline__ void stage_chain(const thip_problem_desc* d)
 {
@@ -770,7 +776,12 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
   {
     BSYNC();  // every wave past its reads of the previous flag
     if (c.tid == 0)
+#if THIP_GENERIC_ONLY
+      // (FIRST / CLOSEST select among a call's contacts: the rank pass recomputes them)
+      c.s->hbits_x = (batched && c.d->coll_contact_test == THIP_CONTACT_ALL) ? 1 : 0;
+#else
       c.s->hbits_x = batched ? 1 : 0;
+#endif
   }
   unsigned* const HBITS = reinterpret_cast<unsigned*>(c.ia(I_HBITS));
   double* SCRW = c.a(A_CSCR) + (long long)(c.wave < kScanWaves ? c.wave : 0) * kSubCap * ns * 3;
@@ -843,7 +854,11 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
       if (pf22)
         pf22[22] += clock64() - tfk0;
     }
+#if THIP_GENERIC_ONLY
+    if (PASS == 0 && c.d->coll_contact_test == THIP_CONTACT_ALL)
+#else
     if (PASS == 0)
+#endif
     {
       // counts and cost only: lane = (sub-state, sphere), looping over the
       // primitives, so every distance call of the wave is for one primitive
@@ -961,12 +976,32 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
     double lcost = 0.0;  // per-lane partial cost, reduced once per pair
     const int base = (PASS == 1) ? coll_unit_row0(L, PCNT, out_base, t) : 0;
     const int pair = coll_pair_of(L, t);
+#if THIP_GENERIC_ONLY
+    // contact_test_type (trajopt_hip.h THIP_CONTACT_*; oracle applyContactTest):
+    // the test selects among each contactTest call's contacts (one call per
+    // sub-state) before the evaluator's filter -- CLOSEST the first smallest
+    // distance of each (key, sub-state) group, FIRST the call's first contact in
+    // ContactResultMap order; the fixed-end rule then applies to the selected one
+    const int ctest = c.d->coll_contact_test;
+    unsigned* const done = g_first_done[c.wave];
+    if (ctest == THIP_CONTACT_FIRST)
+    {
+      for (int w = c.lane; w < (nseg + 31) / 32; w += 64)
+        done[w] = 0u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+#endif
     for (int c0 = 0; c0 < total; c0 += 64)
     {
       const int cand = c0 + c.lane;
       bool hit = false;
       double dist = 0.0, margin = 0.0, coeff = 0.0;
       int i = 0, s = 0, p = 0;
+#if THIP_GENERIC_ONLY
+      bool pre = false, fixed_ok = true;  // a contact of the call; the fixed-end rule keeps it
+#endif
       if (cand >= scene_total)
       {
         // a self-collision candidate: (sub-state, sphere a, -1 - sphere b)
@@ -987,6 +1022,40 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
             if (hit && (f0 || f1))
               hit = (f0 && (cta != 1 || ctb != 1)) || (f1 && (cta != 2 || ctb != 2));
           }
+#if THIP_GENERIC_ONLY
+          if (ctest != THIP_CONTACT_ALL)
+          {
+            pre = dist < threshold;
+            fixed_ok = !(f0 || f1) || (f0 && (cta != 1 || ctb != 1)) || (f1 && (cta != 2 || ctb != 2));
+            if (ctest == THIP_CONTACT_CLOSEST && pre)
+            {
+              // the key of this self candidate and its pair j (self_candidate's decode)
+              const int q = cand - scene_total;
+              int r = q, k = 0;
+              for (; k + 1 < c.T.n_self_keys; ++k)
+              {
+                const int sz = nseg * (c.T.self_kp[k + 1] - c.T.self_kp[k]);
+                if (r < sz)
+                  break;
+                r -= sz;
+              }
+              const int npk = c.T.self_kp[k + 1] - c.T.self_kp[k];
+              const int j = r - (r / npk) * npk;
+              for (int j2 = 0; j2 < npk; ++j2)
+              {
+                if (j2 == j)
+                  continue;
+                int i2, sa2, sb2, ca2, cb2;
+                double d2;
+                self_candidate(c, S, SCR, ns, nseg, last, cont, q - j + j2, i2, sa2, sb2, d2, ca2, cb2);
+                const double th2 = pair_mc(c, sa2, -1 - sb2).x + buffer;
+                if (d2 < th2 && (d2 < dist || (d2 == dist && j2 < j)))
+                  pre = false;  // a closer (or an earlier as close) contact of the key
+              }
+            }
+            hit = pre && fixed_ok;
+          }
+#endif
         }
       }
       else if (use_bits)
@@ -1064,7 +1133,67 @@ __device__ void coll_scan_pairs(Ctx& c, const double* x, int* out_base)
         // robot link: Time0 / Time1 / Between)
         if (hit && (f0 || f1))
           hit = (f0 && cct != 1) || (f1 && cct != 2);
+#if THIP_GENERIC_ONLY
+        if (ctest != THIP_CONTACT_ALL)
+        {
+          pre = dist < threshold;
+          fixed_ok = !(f0 || f1) || (f0 && cct != 1) || (f1 && cct != 2);
+          if (ctest == THIP_CONTACT_CLOSEST && pre)
+          {
+            // the other spheres of this key (link group g, primitive p) at sub-state i
+            const int e = r2 % gn;
+            for (int e2 = 0; e2 < gn; ++e2)
+            {
+              if (e2 == e)
+                continue;
+              const int s2 = S.sph_order[S.grp_s0[g] + e2];
+              const double th2 = pair_mc(c, s2, p).x + buffer;
+              const double* cp2 = SCR + (i * ns + s2) * 3;
+              const double ctr2[3] = { cp2[0], cp2[1], cp2[2] };
+              double d2, n2[3], pr2[3];
+              if (cont)
+              {
+                const double* cq2 = SCR + ((i + 1) * ns + s2) * 3;
+                const double ctr21[3] = { cq2[0], cq2[1], cq2[2] };
+                d2 = th2;
+                if (swept_lower_bound(ctr2, ctr21, S.rad[s2], prim) < th2)
+                {
+                  double ts2;
+                  swept_sphere_prim_distance(ctr2, ctr21, S.rad[s2], prim, d2, n2, pr2, ts2);
+                }
+              }
+              else
+                sphere_prim_distance(ctr2, S.rad[s2], prim, d2, n2, pr2);
+              if (d2 < th2 && (d2 < dist || (d2 == dist && e2 < e)))
+                pre = false;  // a closer (or an earlier as close) contact of the key
+            }
+          }
+          hit = pre && fixed_ok;
+        }
+#endif
       }
+#if THIP_GENERIC_ONLY
+      if (ctest == THIP_CONTACT_FIRST)
+      {
+        // the call's first contact: no earlier lane of this chunk and no earlier
+        // chunk of the unit had a contact at sub-state i
+        const int iv = pre ? i : -1;
+        bool earlier = false;
+        for (int l = 0; l < 64; ++l)
+        {
+          const int il = __shfl(iv, l);
+          earlier = earlier || (l < c.lane && iv >= 0 && il == iv);
+        }
+        const bool was = pre && ((done[i >> 5] >> (i & 31)) & 1u);
+        hit = pre && !earlier && !was && fixed_ok;
+        __builtin_amdgcn_wave_barrier();
+        if (pre)
+          atomicOr(done + (i >> 5), 1u << (i & 31));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      }
+#endif
       const unsigned long long mask = __ballot(hit);
       if (PASS == 0)
         lcost += hit ? fmax(margin - dist, 0.0) * coeff : 0.0;
@@ -6153,10 +6282,20 @@ __global__ __launch_bounds__(kBlock) void fwd_kin_kernel(KernelArgs args, const 
   }
 }
 
+
+#endif  // !THIP_GENERIC_ONLY
+
+// (in both builds: the generic-step build's, coll_rows_kernel_gen, scans with
+// its contact_test_type selection)
+#if THIP_GENERIC_ONLY
+#define THIP_COLL_ROWS_KERNEL coll_rows_kernel_gen
+#else
+#define THIP_COLL_ROWS_KERNEL coll_rows_kernel
+#endif
 // Linearised collision rows at a given trajectory (parity/debug entry
 // thip_collision_rows): records [t, link, prim, sphere, substate, distance,
 // cc_time, n_kept, a_t[D], a_t+1[D], constant] in the hinge-row order.
-__global__ __launch_bounds__(kBlock) void coll_rows_kernel(KernelArgs args, const double* xin, double* out, int cap,
+__global__ __launch_bounds__(kBlock) void THIP_COLL_ROWS_KERNEL(KernelArgs args, const double* xin, double* out, int cap,
                                                           int* counts)
 {
   __shared__ Ctl ctl;
@@ -6218,7 +6357,5 @@ __global__ __launch_bounds__(kBlock) void coll_rows_kernel(KernelArgs args, cons
   if (threadIdx.x == 0)
     counts[b] = (ctl.flags & THIP_FLAG_CONTACT_OVERFLOW) ? -1 : ctl.n_h - c.T.n_sh;
 }
-
-#endif  // !THIP_GENERIC_ONLY
 }  // namespace thip
 

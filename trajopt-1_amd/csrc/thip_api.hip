@@ -28,6 +28,7 @@ __global__ void fwd_kin_kernel(KernelArgs args, const double* xin, double* poses
 __global__ void stage_inputs_kernel(KernelArgs args, const double* init, const double* tgt);
 __global__ void gather_x_kernel(KernelArgs args, double* xout);
 __global__ void coll_rows_kernel(KernelArgs args, const double* xin, double* out, int cap, int* counts);
+__global__ void coll_rows_kernel_gen(KernelArgs args, const double* xin, double* out, int cap, int* counts);
 }  // namespace thip
 
 using namespace thip;
@@ -242,10 +243,9 @@ static int validate(const thip_problem_desc* d, std::string& why)
                  "lowered into the batched kernel: solve such a problem with sco::BasicTrustRegionSQP (the generic "
                  "path, GpuModel)",
            THIP_E_INVALID;
-  if (d->coll_enabled && d->coll_contact_test != THIP_CONTACT_ALL)
-    return why = "collision contact_test_type FIRST / CLOSEST is not lowered into the batched kernel: solve such a "
-                 "problem with sco::BasicTrustRegionSQP (the generic path, device-evaluated terms and GpuModel)",
-           THIP_E_INVALID;
+  if (d->coll_enabled && d->coll_contact_test != THIP_CONTACT_ALL && d->coll_contact_test != THIP_CONTACT_FIRST &&
+      d->coll_contact_test != THIP_CONTACT_CLOSEST)
+    return why = "coll_contact_test is not a THIP_CONTACT_* value", THIP_E_INVALID;
   if (d->n_coll_extra != 0)
     return why = "more than one collision term is not lowered into the batched kernel: solve such a problem with "
                  "sco::BasicTrustRegionSQP (the generic path, device-evaluated terms and GpuModel)",
@@ -811,7 +811,9 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     // kernel (kGenBlock threads, no segment code) takes them; its larger static
     // LDS (reductions over 16 waves) leaves a smaller dynamic budget
     const bool seg_cand = max_step_rows <= kMaxStepRows && !L.wide && L.N * 8 <= kBlock && L.n_abs <= kBlock && cpk;
-    ctx->gen = (!seg_cand && !(g_debug_path & THIP_DEBUG_MAIN_BUILD)) ||
+    // (contact_test_type FIRST / CLOSEST: only the generic-step build's contact scan selects among a call's contacts)
+    const bool ctest = d.coll_enabled && d.coll_contact_test != THIP_CONTACT_ALL;
+    ctx->gen = ctest || (!seg_cand && !(g_debug_path & THIP_DEBUG_MAIN_BUILD)) ||
                ((g_debug_path & THIP_DEBUG_NO_SEGMENT) && (g_debug_path & THIP_DEBUG_GEN_BUILD));
     const long long budget =
         (ctx->gen ? kLdsBudgetGenBytes : kLdsBudgetBytes) / static_cast<long long>(sizeof(double));
@@ -1381,7 +1383,11 @@ int thip_collision_rows(thip_ctx* ctx, const double* x, double* records, int cap
   hipMemcpyAsync(dx, x, B * L.nx * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
   hipMemsetAsync(dout, 0, B * static_cast<size_t>(cap) * W * sizeof(double), ctx->stream);
   KernelArgs a = make_args(ctx);
-  hipLaunchKernelGGL(coll_rows_kernel, dim3(ctx->batch), dim3(kBlock), 0, ctx->stream, a, dx, dout, cap, dcnt);
+  // the contact scan of the build the context's SQP runs
+  if (ctx->gen)
+    hipLaunchKernelGGL(coll_rows_kernel_gen, dim3(ctx->batch), dim3(kGenBlock), 0, ctx->stream, a, dx, dout, cap, dcnt);
+  else
+    hipLaunchKernelGGL(coll_rows_kernel, dim3(ctx->batch), dim3(kBlock), 0, ctx->stream, a, dx, dout, cap, dcnt);
   e = hipGetLastError();
   if (e == hipSuccess)
     e = hipMemcpyAsync(records, dout, B * static_cast<size_t>(cap) * W * sizeof(double), hipMemcpyDeviceToHost,

@@ -1451,8 +1451,7 @@ bool TrajOptProb::lowerable() const
   // scene primitives, and no term it does not lower
   return desc_.n_steps >= 2 && desc_.n_steps <= THIP_MAX_STEPS && desc_.n_prims <= THIP_MAX_PRIMS &&
          thip_jdt_fused(&desc_) && desc_.n_jvt == 0 && desc_.n_ttt == 0 && !desc_.use_time && desc_.n_fixed_dofs == 0 &&
-         desc_.n_coll_extra == 0 && (!desc_.coll_enabled || desc_.coll_contact_test == THIP_CONTACT_ALL) &&
-         unloweredTerms().empty();
+         desc_.n_coll_extra == 0 && unloweredTerms().empty();
 }
 
 LoweredProblem TrajOptProb::lowered() const
