@@ -377,13 +377,13 @@ def test_sqp_parity_contact_test(oracle_mod, cfg):
     LVS_CONTINUOUS."""
     from trajopt_amd.runtime import BatchTrustRegionSQP
 
-    wl = problems.make_workload("C", 32)
+    wl = problems.make_workload("C", 16)
     wl.desc.coll_continuous = 1 if "cont" in cfg else 0
     wl.desc.coll_contact_test = abi.CONTACT_FIRST if cfg.endswith("first") else abi.CONTACT_CLOSEST
     s = BatchTrustRegionSQP(wl)
     x, res = s.optimize()
     s.close()
-    check_parity(wl, oracle_mod, x, res, label=f"{cfg}-32", min_strict=0.6)
+    check_parity(wl, oracle_mod, x, res, label=f"{cfg}-16", min_strict=0.6)
 
 
 @pytest.mark.parametrize("json_type,ctest", [(0, abi.CONTACT_FIRST), (1, abi.CONTACT_CLOSEST)])
