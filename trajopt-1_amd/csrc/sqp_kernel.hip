@@ -2679,6 +2679,15 @@ __device__ bool factor(Ctx& c, Solver& sv, double sigK, bool polish, double delt
         sv.M[mb * sDD + e] = vt;
       if (bot)
         sv.Nb[mb * sDD + e] = vb;
+#if THIP_GENERIC_ONLY
+      // the wide middle's couplings also in the scratch (blocks 0, 1: consumed
+      // above) for twisted_middle_wide's reads, the rest of the factorisation
+      if (L.wide)
+      {
+        Sblk(0)[e] = vt;
+        Sblk(1)[e] = vb;
+      }
+#endif
     }
   }
   BSYNC();
@@ -3002,8 +3011,15 @@ __device__ __noinline__ void twisted_middle_wide(const Ctx& c, const Solver& sv,
   // solve blocks (Layout::grp: a waypoint pair), one branch
   const int D = c.L.sD, DD = D * D, m = c.L.tw_mid, N = c.L.sNb, i = c.lane;
   const lds_f64* LI = lds(LIp);
+#if THIP_GENERIC_ONLY
+  // M_m and M'_m as factor() left them in its LDS scratch (the HBM copies'
+  // values: one LDS round trip instead of one HBM round trip per solve)
+  const lds_f64* Mm = lds(static_cast<const double*>(c.big + c.L.fac_off));
+  const lds_f64* Mbm = Mm + DD;
+#else
   const gbl_f64* M = gbl(sv.M);  // HBM (Layout::wide)
   const gbl_f64* Mb = gbl(sv.Nb);
+#endif
   lds_f64* CV = lds(CVp);
   lds_f64* YV = lds(YVp);
   if (i < D)
@@ -3015,9 +3031,15 @@ __device__ __noinline__ void twisted_middle_wide(const Ctx& c, const Solver& sv,
     for (int k = 0; k < THIP_MAX_DOF; ++k)
     {
       const int kk = min(k, D - 1);
+#if THIP_GENERIC_ONLY
+      mt[k] = Mm[i * D + kk];
+      yt[k] = YV[max(m - 1, 0) * D + kk];
+      mb[k] = Mbm[i * D + kk];
+#else
       mt[k] = M[m * DD + i * D + kk];
       yt[k] = YV[max(m - 1, 0) * D + kk];
       mb[k] = Mb[m * DD + i * D + kk];
+#endif
       yb[k] = YV[min(m + 1, N - 1) * D + kk];
     }
     double s = 0.0;
