@@ -53,7 +53,7 @@ print("slowest problems (per-ADMM cycles by phase):")
 nh_avg = np.array([r.n_hinge_admm for r in res], dtype=np.float64) / np.maximum(admm, 1)
 for b in np.argsort(-pf[:, 14])[:4]:
     parts = "  ".join(f"{BatchTrustRegionSQP.PROFILE_SLOTS[k]}={pf[b, k] / max(admm[b], 1):.0f}"
-                      for k in (0, 1, 3, 5, 6, 8, 9, 10, 11, 15, 16, 17, 18, 34, 19, 20, 21, 22, 23, 24, 25, 26, 30, 31, 32, 33))
+                      for k in (0, 1, 3, 5, 6, 8, 9, 10, 11, 15, 16, 17, 18, 34, 19, 20, 21, 22, 23, 24, 25, 35, 36, 26, 30, 31, 32, 33))
     print(f"  problem {b}: {pf[b, 14] / 100:.0f} us, admm {admm[b]:.0f}, qp {qps[b]:.0f}, sqp {sqp[b]:.0f}, "
           f"mean hinge rows {nh_avg[b]:.0f}, contact rows {res[b].n_contact_rows}\n    {parts}")
 print(f"mean hinge rows per ADMM iteration (all): {nh_avg.mean():.1f}, max {nh_avg.max():.0f}")

@@ -28,6 +28,10 @@
 #ifndef THIP_GENERIC_ONLY
 #define THIP_GENERIC_ONLY 0
 #endif
+// generic-step build: the d-value / middle-block phase on hoisted layout values
+#ifndef THIP_GEN_DV_HOIST
+#define THIP_GEN_DV_HOIST 1
+#endif
 #if THIP_GENERIC_ONLY
 #define THIP_SQP_KERNEL sqp_kernel_gen
 #else
@@ -3060,6 +3064,72 @@ __device__ __noinline__ void twisted_middle_wide(const Ctx& c, const Solver& sv,
   wave_sync();
 }
 
+#if THIP_GENERIC_ONLY && THIP_GEN_DV_HOIST
+// twisted_dvalue on layout values the caller holds (the same sum)
+__device__ __forceinline__ double twisted_dvalue_l(const double* LIp, const double* YVp, int t, int i, int D, bool wide)
+{
+  const int DD = D * D;
+  const lds_f64* LI = lds(LIp);
+  const lds_f64* YV = lds(YVp);
+  if (wide)
+    return masked_dot<THIP_MAX_DOF>(LI + t * DD + i, D, YV + t * D, 1, i, D);
+  double v0 = 0, v1 = 0;
+#pragma unroll
+  for (int k = 0; k < kOct; ++k)
+  {
+    const int kk = (k < D) ? k : D - 1;
+    const double a = LI[t * DD + kk * D + i] * (YV[t * D + kk] * (((k >= i) && (k < D)) ? 1.0 : 0.0));
+    if (k & 1)
+      v1 += a;
+    else
+      v0 += a;
+  }
+  return v0 + v1;
+}
+
+// twisted_middle_wide on layout values the caller holds: M_m, M'_m from
+// factor()'s LDS scratch (Mm), middle block m of N, D dofs (the same sums)
+__device__ __forceinline__ void twisted_middle_wide_l(const lds_f64* Mm, const double* LIp, double* CVp, double* YVp,
+                                                     int D, int m, int N, int i)
+{
+  const int DD = D * D;
+  const lds_f64* LI = lds(LIp);
+  const lds_f64* Mbm = Mm + DD;
+  lds_f64* CV = lds(CVp);
+  lds_f64* YV = lds(YVp);
+  if (i < D)
+  {
+    const bool top = m > 0, bot = N - 1 - m > 0;
+    double mt[THIP_MAX_DOF], yt[THIP_MAX_DOF], mb[THIP_MAX_DOF], yb[THIP_MAX_DOF];
+#pragma unroll
+    for (int k = 0; k < THIP_MAX_DOF; ++k)
+    {
+      const int kk = min(k, D - 1);
+      mt[k] = Mm[i * D + kk];
+      yt[k] = YV[max(m - 1, 0) * D + kk];
+      mb[k] = Mbm[i * D + kk];
+      yb[k] = YV[min(m + 1, N - 1) * D + kk];
+    }
+    // branch-free: a masked term is fma(0, y, s) = s (the coupling itself is
+    // selected away: an absent half's scratch block is not initialised), the
+    // same sum in the same order as the guarded adds, which compiled to one
+    // branch and one LDS wait per term
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < THIP_MAX_DOF; ++k)
+    {
+      s = fma((top && k < D) ? mt[k] : 0.0, yt[k], s);
+      s = fma((bot && k < D) ? mb[k] : 0.0, yb[k], s);
+    }
+    YV[m * D + i] = CV[m * D + i] - s;
+  }
+  wave_sync();
+  if (i < D)
+    CV[m * D + i] = masked_dot<THIP_MAX_DOF>(LI + m * DD + i, D, YV + m * D, 1, i, D);
+  wave_sync();
+}
+#endif
+
 template <typename MP>
 __device__ __forceinline__ void twisted_middle_narrow(const Ctx& c, MP M, MP Mb, const double* LIp, double* CVp,
                                                       const double* YVp, int branch)
@@ -3402,15 +3472,43 @@ __device__ void reduced_solve(Ctx& c, Solver& sv, bool polish, double delta, con
     const int m = L.tw_mid;
     double dv[kCols];
     auto off_middle = [&](int cu) { return cu < nx && (cu / sD) % N != m; };
+#if THIP_GENERIC_ONLY && THIP_GEN_DV_HOIST
+    // the same sums on the hoisted layout values (twisted_dvalue / twisted_middle
+    // re-read them from the Ctx, which lives in private memory: dependent FLAT
+    // round trips ahead of every block's loads)
+#pragma unroll
+    for (int u = 0; u < kCols; ++u)
+    {
+      const int cu = tid + kBlock * u;
+      dv[u] = off_middle(cu) ? twisted_dvalue_l(LI, YV, cu / sD, cu % sD, sD, wide) : 0.0;
+    }
+    PROF_LAP(35);
+    if (c.wave >= kWaves - nbr)  // the last nbr waves: one middle block each
+    {
+      if (wide)
+        twisted_middle_wide_l(lds(static_cast<const double*>(c.big + L.fac_off)), LI, CV, YV, sD, m, N, c.lane);
+      else
+        twisted_middle(c, sv, LI, CV, YV, c.wave - (kWaves - nbr));
+    }
+    BSYNC();
+    PROF_LAP(36);
+#else
 #pragma unroll
     for (int u = 0; u < kCols; ++u)
     {
       const int cu = tid + kBlock * u;
       dv[u] = off_middle(cu) ? twisted_dvalue(c, LI, YV, cu / sD, cu % sD) : 0.0;
     }
+#if THIP_GENERIC_ONLY
+    PROF_LAP(35);
+#endif
     if (c.wave >= kWaves - nbr)  // the last nbr waves: one middle block each
       twisted_middle(c, sv, LI, CV, YV, c.wave - (kWaves - nbr));
     BSYNC();
+#if THIP_GENERIC_ONLY
+    PROF_LAP(36);
+#endif
+#endif
 #pragma unroll
     for (int u = 0; u < kCols; ++u)
     {

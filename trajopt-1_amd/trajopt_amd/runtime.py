@@ -127,7 +127,7 @@ class BatchTrustRegionSQP:
                      "seg_hinge_gather", "seg_hinge_E", "coll_count_pass", "coll_rank_pass", "coll_rows", "coll_fk_substates",
                      "gen_rhs_mr", "gen_rhs_cols", "gen_rhs_linv", "gen_dvalue_middle",
                      "n_primal_inf_full", "n_dual_inf_full", "n_factor", "gen_pre", "gen_updates",
-                     "factor_blocks", "factor_twisted", "bwd_wave0_own", "unused35", "unused36", "unused37", "unused38",
+                     "factor_blocks", "factor_twisted", "bwd_wave0_own", "gen_dvalue", "gen_middle_wait", "unused37", "unused38",
                      "unused39"]
 
     def layout(self):
