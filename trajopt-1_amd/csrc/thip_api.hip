@@ -796,13 +796,6 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
     const int order[] = { A_LINV, A_CV,  A_YV, A_CPK, A_BXW, A_BA, A_MR, A_DG, A_GS, A_WS, A_FS, A_BS, A_XA0, A_XA1,
                           A_Z0,   A_Z1,  A_Y,  A_XT,  A_PZ, A_RHO, A_L, A_U,  A_Q,  A_DX, A_DY, A_PD,  A_PO,  A_PO2,
                           A_E,    A_DS,  A_RE, A_PB,  A_PS, A_PR };
-    long long used = static_cast<long long>(lds_d);
-    used = (used + 7) / 8 * 8;
-    L.fac_off = static_cast<int>(used);  // factor()'s 4 D x D blocks (4 nbr sD x sD; pairs: 4 of 2D x 2D)
-    used += (4LL * std::max<long long>((long long)L.D * L.D, (long long)L.nbr * L.sD * L.sD) + 7) / 8 * 8;
-    L.lds_scratch = static_cast<int>(used);
-    for (int k = 0; k < A_COUNT; ++k)
-      L.loff[k] = -1;
     int max_step_rows = 0;
     for (int t = 0; t < L.N; ++t)
       max_step_rows = std::max(max_step_rows, step_ptr[static_cast<size_t>(t) + 1] - step_ptr[static_cast<size_t>(t)]);
@@ -817,6 +810,13 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
                ((g_debug_path & THIP_DEBUG_NO_SEGMENT) && (g_debug_path & THIP_DEBUG_GEN_BUILD));
     const long long budget =
         (ctx->gen ? kLdsBudgetGenBytes : kLdsBudgetBytes) / static_cast<long long>(sizeof(double));
+    long long used = static_cast<long long>(lds_d);
+    used = (used + 7) / 8 * 8;
+    L.fac_off = static_cast<int>(used);  // factor()'s 4 D x D blocks (4 nbr sD x sD; pairs: 4 of 2D x 2D)
+    used += (4LL * std::max<long long>((long long)L.D * L.D, (long long)L.nbr * L.sD * L.sD) + 7) / 8 * 8;
+    L.lds_scratch = static_cast<int>(used);
+    for (int k = 0; k < A_COUNT; ++k)
+      L.loff[k] = -1;
     for (int k : order)
     {
       const long long n = (sizes[k] + 7) / 8 * 8;
@@ -858,6 +858,17 @@ int thip_create(int device, const thip_problem_desc* desc, int batch, thip_ctx**
       L.lds_doubles = static_cast<int>(budget);
     }
     L.lds_budget = static_cast<int>(ctx->lds_bytes / sizeof(double));
+    if (std::getenv("THIP_DEBUG_PLAN"))  // diagnostic: the residency plan (doubles), on stderr
+    {
+      std::fprintf(stderr, "thip plan: gen %d wide %d hinge %d N %d D %d sN %d sD %d nx %d m %d nc %d budget %lld "
+                           "fac_off %d lds_scratch %d lds_doubles %d; HBM:",
+                   ctx->gen ? 1 : 0, L.wide, L.hinge, L.N, L.D, L.sN, L.sD, L.nx, L.m, L.n_cols, budget, L.fac_off,
+                   L.lds_scratch, L.lds_doubles);
+      for (int k : order)
+        if (L.loff[k] < 0)
+          std::fprintf(stderr, " %d(%lld)", k, sizes[k]);
+      std::fprintf(stderr, "\n");
+    }
   }
 
   auto fail = [&](const std::string& msg) {
