@@ -14,6 +14,14 @@
 struct KktSymbolic
 {
   std::vector<int> perm, lrp, lrj, lcp, lci, lcpos, lksrc, dpd, lvp, lvn, fip, fik, fic;
+  // the forward solve as passes of row segments: entry e of row k is ready
+  // once every column up to it is final, i.e. after level pm(e) - 1, with pm
+  // the prefix maximum of level(j) + 1 along the row; a row's entries of equal
+  // pm form one segment (k, fwa, fwb) of pass pm, and pass p runs after pass
+  // p - 1 (empty passes dropped): each row is still summed in its order, but
+  // the entries of a row near the root are taken as soon as they are ready
+  // instead of all at its own level
+  std::vector<int> fwp, fwk, fwa, fwb;
 };
 
 // Returns "" or the reason the pattern is refused.
@@ -168,6 +176,41 @@ inline std::string kkt_symbolic(int n, int m, const int* Pp, const int* Pi, cons
     std::vector<int> nx(S.lvp.begin(), S.lvp.end() - 1);
     for (int k = 0; k < N; ++k)
       S.lvn[nx[level[k]]++] = k;
+  }
+  {
+    std::vector<std::vector<int>> seg(static_cast<size_t>(nlev) + 1);  // per pass: (k, a, b) triples
+    for (int k = 0; k < N; ++k)
+    {
+      int pm = 0, a = S.lrp[k];
+      for (int e = S.lrp[k]; e < S.lrp[k + 1]; ++e)
+      {
+        const int r = std::max(pm, level[S.lrj[e]] + 1);
+        if (r != pm && e > a)
+        {
+          seg[pm].insert(seg[pm].end(), { k, a, e });
+          a = e;
+        }
+        pm = r;
+      }
+      if (S.lrp[k + 1] > a)
+        seg[pm].insert(seg[pm].end(), { k, a, S.lrp[k + 1] });
+    }
+    S.fwp.assign(1, 0);
+    S.fwk.clear();
+    S.fwa.clear();
+    S.fwb.clear();
+    for (const auto& v : seg)
+    {
+      if (v.empty())
+        continue;
+      for (size_t i = 0; i < v.size(); i += 3)
+      {
+        S.fwk.push_back(v[i]);
+        S.fwa.push_back(v[i + 1]);
+        S.fwb.push_back(v[i + 2]);
+      }
+      S.fwp.push_back(static_cast<int>(S.fwk.size()));
+    }
   }
   S.fip.assign(static_cast<size_t>(nlev) + 1, 0);
   S.fik.clear();

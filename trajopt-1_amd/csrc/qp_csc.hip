@@ -36,6 +36,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <iterator>
 #include <set>
@@ -116,12 +117,15 @@ struct QpPattern
   // the level's column entries (fip; fik = column, fic = entry)
   const int *perm, *lrp, *lrj, *lcp, *lci, *lcpos, *lksrc, *dpd, *lvp, *lvn, *fip, *fik, *fic;
   int nlev;
+  // the forward solve's passes of row segments (kkt_symbolic: fwp, fwk, fwa, fwb)
+  const int *fwp, *fwk, *fwa, *fwb;
+  int npass;
   int lds_vec;  // the permuted solve vector lives in LDS (else W_LV)
   // the whole factor in LDS (QP_LDS_*, staged at kernel entry): the solve
   // vector, L and D, and the index arrays the factor and the solves walk
   // (16-bit row / column indices)
   int lds_pat;
-  long long lds_off[8];
+  long long lds_off[12];
   long long off[W_COUNT];
   long long stride;
 };
@@ -218,13 +222,16 @@ struct FacViewT
   const IX *lrj, *lcpos, *lci, *lvn;
   const IN *lrp, *lcp, *lvp;
   DB *LX, *DG;
+  const IX *fwk, *fwa, *fwb;
+  const IN* fwp;
 };
 using FacViewG = FacViewT<int, int, double>;
 using FacViewL = FacViewT<lds_u16, lds_i32, lds_f64>;
 // LDS layout of a staged factor (QpPattern::lds_off)
 enum : int
 {
-  QL_LX = 0, QL_DG, QL_LRJ, QL_LCPOS, QL_LCI, QL_LVN, QL_LRP, QL_LVP  // (lcp follows lrp)
+  QL_LX = 0, QL_DG, QL_LRJ, QL_LCPOS, QL_LCI, QL_LVN, QL_LRP, QL_LVP,  // (lcp follows lrp)
+  QL_FWK, QL_FWA, QL_FWB, QL_FWP, QL_COUNT
 };
 
 // phase cycles of workgroup 0's ADMM loop (diagnostic, thip_qp_debug_profile):
@@ -261,7 +268,7 @@ struct Qp
 __device__ void fac_views(Qp& q, char* lds)
 {
   const QpPattern& p = q.p;
-  q.fg = FacViewG{ p.lrj, p.lcpos, p.lci, p.lvn, p.lrp, p.lcp, p.lvp, q.a(W_LX), q.a(W_DG) };
+  q.fg = FacViewG{ p.lrj, p.lcpos, p.lci, p.lvn, p.lrp, p.lcp, p.lvp, q.a(W_LX), q.a(W_DG), p.fwk, p.fwa, p.fwb, p.fwp };
   if (!p.lds_pat)
     return;
   const int N = p.N, nl = static_cast<int>(p.lds_off[QL_DG] - p.lds_off[QL_LX]) / 8;  // entries of L
@@ -274,6 +281,10 @@ __device__ void fac_views(Qp& q, char* lds)
   int* lrp = reinterpret_cast<int*>(lds + p.lds_off[QL_LRP]);
   int* lcp = lrp + (N + 1);
   int* lvp = reinterpret_cast<int*>(lds + p.lds_off[QL_LVP]);
+  unsigned short* fwk = reinterpret_cast<unsigned short*>(lds + p.lds_off[QL_FWK]);
+  unsigned short* fwa = reinterpret_cast<unsigned short*>(lds + p.lds_off[QL_FWA]);
+  unsigned short* fwb = reinterpret_cast<unsigned short*>(lds + p.lds_off[QL_FWB]);
+  int* fwp = reinterpret_cast<int*>(lds + p.lds_off[QL_FWP]);
   const double *GX = q.a(W_LX), *GD = q.a(W_DG);
   QFOR(e, nl)
   {
@@ -293,8 +304,17 @@ __device__ void fac_views(Qp& q, char* lds)
     lcp[k] = p.lcp[k];
   }
   QFOR(l, p.nlev + 1) lvp[l] = p.lvp[l];
+  const int nseg = p.fwp[p.npass];
+  QFOR(t, nseg)
+  {
+    fwk[t] = static_cast<unsigned short>(p.fwk[t]);
+    fwa[t] = static_cast<unsigned short>(p.fwa[t]);
+    fwb[t] = static_cast<unsigned short>(p.fwb[t]);
+  }
+  QFOR(l, p.npass + 1) fwp[l] = p.fwp[l];
   q.fs = FacViewL{ (const lds_u16*)lrj, (const lds_u16*)lcpos, (const lds_u16*)lci, (const lds_u16*)lvn,
-                   (const lds_i32*)lrp, (const lds_i32*)lcp, (const lds_i32*)lvp, (lds_f64*)LX, (lds_f64*)DG };
+                   (const lds_i32*)lrp, (const lds_i32*)lcp, (const lds_i32*)lvp, (lds_f64*)LX, (lds_f64*)DG,
+                   (const lds_u16*)fwk, (const lds_u16*)fwa, (const lds_u16*)fwb, (const lds_i32*)fwp };
   __syncthreads();
 }
 
@@ -713,7 +733,6 @@ __device__ void kkt_solve_v(Qp& q, const V f, PW w, double* v)
   auto DG = f.DG;
   const auto lvp = f.lvp;
   const auto lvn = f.lvn;
-  const auto lrp = f.lrp;
   const auto lrj = f.lrj;
   const auto lcp = f.lcp;
   const auto lcpos = f.lcpos;
@@ -725,16 +744,35 @@ __device__ void kkt_solve_v(Qp& q, const V f, PW w, double* v)
   __syncthreads();
   const bool prof = THIP_QP_PROF && blockIdx.x == 0 && threadIdx.x == 0;
   long long t0 = prof ? clock64() : 0;
-  for (int lev = 0; lev < nlev; ++lev)
+  // forward: the passes of row segments (kkt_symbolic), each row still
+  // summed in its order -- its segments run in increasing passes -- and a
+  // segment's columns final by the end of the pass before it
+  const auto fwp = f.fwp;
+  const auto fwk = f.fwk;
+  const auto fwa = f.fwa;
+  const auto fwb = f.fwb;
+  for (int ps = 0; ps < p.npass; ++ps)
   {
-    const int n1 = lvp[lev + 1];
-    for (int t = lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
+    const int t1 = fwp[ps + 1];
+    for (int t = fwp[ps] + static_cast<int>(threadIdx.x); t < t1; t += kQB)
     {
-      const int k = lvn[t];
-      w[k] = row_sub(static_cast<double>(w[k]), LX, lrj, w, lrp[k], lrp[k + 1]);
+      const int k = fwk[t];
+      w[k] = row_sub(static_cast<double>(w[k]), LX, lrj, w, static_cast<int>(fwa[t]), static_cast<int>(fwb[t]));
     }
     __syncthreads();
   }
+  // (npass = 0: the level-by-level forward solve, THIP_QP_LEVEL_SOLVE -- the same sums)
+  if (p.npass == 0)
+    for (int lev = 0; lev < nlev; ++lev)
+    {
+      const int n1 = lvp[lev + 1];
+      for (int t = lvp[lev] + static_cast<int>(threadIdx.x); t < n1; t += kQB)
+      {
+        const int k = lvn[t];
+        w[k] = row_sub(static_cast<double>(w[k]), LX, lrj, w, f.lrp[k], f.lrp[k + 1]);
+      }
+      __syncthreads();
+    }
   if (prof)
     qp_prof_add(6, clock64() - t0);
   QFOR(k, N) w[k] /= DG[k];
@@ -1714,6 +1752,9 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
                oLvp = push(S.lvp.data(), nlev + 1), oLvn = push(S.lvn.data(), n + m),
                oFip = push(S.fip.data(), nlev + 1), oFik = push(S.fik.data(), static_cast<int>(nnzl)),
                oFic = push(S.fic.data(), static_cast<int>(nnzl));
+  const int npass = static_cast<int>(S.fwp.size()) - 1, nseg = S.fwp.back();
+  const size_t oFwp = push(S.fwp.data(), npass + 1), oFwk = push(S.fwk.data(), nseg),
+               oFwa = push(S.fwa.data(), nseg), oFwb = push(S.fwb.data(), nseg);
   const long long N = n + m;
   // the permuted solve vector in LDS up to 64 KiB
   const bool lds_vec = N <= 8192;
@@ -1745,6 +1786,9 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
   q->pat.N = static_cast<int>(N);
   q->in_doubles = (long long)np + na + n + 2LL * m;
   q->pat.nlev = nlev;
+  // diagnostic: THIP_QP_LEVEL_SOLVE=1 runs the forward solve level by level,
+  // one thread per node (the A/B baseline; the same sums)
+  q->pat.npass = std::getenv("THIP_QP_LEVEL_SOLVE") ? 0 : npass;
   for (int lv = 0; lv < nlev; ++lv)
     q->max_level = std::max(q->max_level, S.lvp[static_cast<size_t>(lv) + 1] - S.lvp[static_cast<size_t>(lv)]);
   q->nnz_l = nnzl;
@@ -1755,7 +1799,7 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
   {
     const long long nl = std::max(nnzl, 1LL);
     long long o = N * 8;  // the solve vector first
-    long long offs[8];
+    long long offs[QL_COUNT];
     auto take = [&](int k, long long bytes) {
       offs[k] = o;
       o += (bytes + 15) / 16 * 16;
@@ -1768,13 +1812,17 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
     take(QL_LVN, N * 2);
     take(QL_LRP, 2 * (N + 1) * 4);
     take(QL_LVP, (nlev + 1) * 4);
+    take(QL_FWK, (long long)nseg * 2);
+    take(QL_FWA, (long long)nseg * 2);
+    take(QL_FWB, (long long)nseg * 2);
+    take(QL_FWP, (long long)(npass + 1) * 4);
     const bool fits = lds_vec && N < 65536 && nnzl < 65536 && o <= kQpLdsBudget;
     q->pat.lds_pat = fits ? 1 : 0;
     if (fits)
     {
       // lds_off[QL_DG] - lds_off[QL_LX] = 8 x entries of L exactly (fac_views)
       offs[QL_DG] = offs[QL_LX] + nl * 8;
-      for (int k = 0; k < 8; ++k)
+      for (int k = 0; k < QL_COUNT; ++k)
         q->pat.lds_off[k] = offs[k];
       q->lds = static_cast<size_t>(o);
     }
@@ -1821,6 +1869,10 @@ int thip_qp_create(int device, int n, int m, const int* P_colptr, const int* P_r
   q->pat.fip = q->d_idx + oFip;
   q->pat.fik = q->d_idx + oFik;
   q->pat.fic = q->d_idx + oFic;
+  q->pat.fwp = q->d_idx + oFwp;
+  q->pat.fwk = q->d_idx + oFwk;
+  q->pat.fwa = q->d_idx + oFwa;
+  q->pat.fwb = q->d_idx + oFwb;
   *out = q;
   return THIP_OK;
 }

@@ -8,6 +8,7 @@
 // Exit status 0 = every case passed.
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <random>
 
 #include "../../csrc/kkt_symbolic.hpp"
@@ -142,6 +143,54 @@ bool check(const char* name, const Qp& q, bool pol, std::mt19937& rng)
         b[q.n + r] = 0;
   for (int k = 0; k < N; ++k)
     w[k] = b[S.perm[k]];
+  // the forward solve as the device runs it: passes of row segments
+  // (S.fwp..fwb), the segments of a pass shuffled; every column a segment
+  // reads must be final (all of its row's segments done) before the pass, and
+  // each row's segments must tile its entries in order -- then the result is
+  // bitwise the level-by-level forward solve below
+  std::vector<double> wp = w;
+  {
+    std::vector<int> left(static_cast<size_t>(N)), next(static_cast<size_t>(N));
+    for (int k = 0; k < N; ++k)
+    {
+      left[k] = S.lrp[k + 1] - S.lrp[k];
+      next[k] = S.lrp[k];
+    }
+    bool sched_ok = true;
+    const int npass = static_cast<int>(S.fwp.size()) - 1;
+    for (int ps = 0; ps < npass; ++ps)
+    {
+      std::vector<int> items;
+      for (int t = S.fwp[ps]; t < S.fwp[ps + 1]; ++t)
+        items.push_back(t);
+      std::shuffle(items.begin(), items.end(), rng);
+      std::vector<int> done_before = left;  // finality as of the pass's start
+      for (int t : items)
+      {
+        const int k = S.fwk[t];
+        if (S.fwa[t] != next[k] || S.fwb[t] <= S.fwa[t])
+          sched_ok = false;
+        double s = wp[k];
+        for (int e = S.fwa[t]; e < S.fwb[t]; ++e)
+        {
+          if (done_before[S.lrj[e]] != 0)
+            sched_ok = false;
+          s -= LX[e] * wp[S.lrj[e]];
+        }
+        wp[k] = s;
+        next[k] = S.fwb[t];
+        left[k] -= S.fwb[t] - S.fwa[t];
+      }
+    }
+    for (int k = 0; k < N; ++k)
+      if (left[k] != 0)
+        sched_ok = false;
+    if (!sched_ok)
+    {
+      std::printf("FAIL %s: forward pass schedule\n", name);
+      return false;
+    }
+  }
   for (int lev = 0; lev < nlev; ++lev)
     for (int t = S.lvp[lev + 1] - 1; t >= S.lvp[lev]; --t)
     {
@@ -151,6 +200,11 @@ bool check(const char* name, const Qp& q, bool pol, std::mt19937& rng)
         s -= LX[e] * w[S.lrj[e]];
       w[k] = s;
     }
+  if (std::memcmp(wp.data(), w.data(), sizeof(double) * static_cast<size_t>(N)) != 0)
+  {
+    std::printf("FAIL %s: forward pass schedule not bitwise the level schedule\n", name);
+    return false;
+  }
   for (int k = 0; k < N; ++k)
     w[k] /= DG[k];
   for (int lev = nlev - 1; lev >= 0; --lev)
@@ -181,7 +235,8 @@ bool check(const char* name, const Qp& q, bool pol, std::mt19937& rng)
   res /= scale;
   // (delta = 1e-6 pivots: growth without pivoting, which polish refines away)
   const bool ok = std::isfinite(res) && res <= (pol ? 1e-9 : 1e-12);
-  std::printf("%s %s: N %d nnzL %zu levels %d residual %.3e\n", ok ? "ok" : "FAIL", name, N, S.lrj.size(), nlev, res);
+  std::printf("%s %s: N %d nnzL %zu levels %d forward passes %zu (%zu segments) residual %.3e\n", ok ? "ok" : "FAIL",
+              name, N, S.lrj.size(), nlev, S.fwp.size() - 1, S.fwk.size(), res);
   return ok;
 }
 
